@@ -1,0 +1,218 @@
+"""Benchmark: training images/sec of the NewBP-NAFNet hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], the 1-GPU headline config): NAFNet width 32, enc [2,2,4,8], middle 12,
+dec [2,2,2,2] (29.16 M params), rgb/B2 crosstalk PSF, 16 x 3 x 256 x 256 synthetic sRGB per GPU,
+HybridLoss terms L1 + SSIM + Phys_srgb, global-norm clip 0.01 + AdamW.  One "step" = forward + loss + backward
+(+ bucketed RCCL all-reduce when N > 1) + clip + AdamW, all HIP kernels.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...)
+
+Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel class measured live with HIP events on the launch
+stream during the timed steps; `nafblock_roofline` is the north-star figure (NAFBlock fwd+bwd algorithmic bytes,
+SURVEY §8d: 5*B*C*H*W*4 bytes per block per step, vs 8 TB/s); `cpu_baseline` is the CPU oracle (oracle/, kind
+"port") on a bounded sample, timed on this box's host cores; `psnr_vs_cpu_ref_db` compares the GPU output with
+the CPU oracle's on the same weights and input.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training images/sec at 256×256 bs=16 (1/2/4/8 GPU) + PSNR vs CPU ref"
+CFG = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+BATCH, IMG = 16, 256
+W_L1, W_SSIM, W_PHYS = 1.0, 0.05, 0.1
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
+HBM_PEAK_GBPS = 8000.0
+
+
+def nafblock_bytes(net, B, H, W):
+    tot = 0
+    h, w = H, W
+    for i, n in enumerate(net.enc_blk_nums):
+        tot += n * B * net.enc_chans[i] * h * w
+        h, w = h // 2, w // 2
+    tot += net.middle_blk_num * B * net.mid_chan * h * w
+    for i, n in enumerate(net.dec_blk_nums):
+        h, w = h * 2, w * 2
+        tot += n * B * net.dec_chans[i] * h * w
+    return 5 * tot * 4
+
+
+def cpu_baseline(state_dict, B=2, steps=2):
+    """Time the oracle's training step (oracle/train_step.py, torch CPU fp32) on a bounded sample."""
+    from oracle.train_step import OracleTrainer
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+    torch.set_num_threads(threads)
+    P = {k: v.detach().cpu() for k, v in state_dict.items()}
+    ora = OracleTrainer(P, dict(enc_blk_nums=CFG["enc_blk_nums"], middle_blk_num=CFG["middle_blk_num"],
+                                dec_blk_nums=CFG["dec_blk_nums"]), w_l1=W_L1, w_ssim=W_SSIM, w_phys=W_PHYS)
+    g = torch.Generator().manual_seed(123)
+    lq = torch.rand(B, 3, IMG, IMG, generator=g)
+    gt = torch.rand(B, 3, IMG, IMG, generator=g)
+    r = torch.ones(B, 1, 1, 1)
+    ora.step(lq, gt, lq.clamp(0, 1), r)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ora.step(lq, gt, lq.clamp(0, 1), r)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(B / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
+            "sample": f"oracle train step (torch CPU fp32), cfg2 model, bs={B} {IMG}x{IMG}, {steps} timed steps "
+                      f"after 1 warm-up, {dt:.2f} s/step"}
+
+
+def psnr_vs_cpu(net, dev):
+    from oracle.nafnet import nafnet as oracle_nafnet
+    g = torch.Generator().manual_seed(321)
+    x = torch.rand(1, 3, IMG, IMG, generator=g)
+    with torch.no_grad():
+        y = net(x.to(dev)).cpu()
+        P = {k: v.cpu() for k, v in net.state_dict().items()}
+        yr = oracle_nafnet(P, x, CFG["enc_blk_nums"], CFG["middle_blk_num"], CFG["dec_blk_nums"])
+    mse = ((y.double() - yr.double()) ** 2).mean().item()
+    psnr = float("inf") if mse <= 1e-30 else 10 * torch.log10(torch.tensor(1.0 / mse)).item()
+    return psnr, (y - yr).abs().max().item()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from lowlight_image_enhancement_amd import _lib
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+
+    torch.manual_seed(0)
+    net = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **CFG)
+    init_sd = {k: v.clone() for k, v in net.state_dict().items()}
+    net = net.to(dev)
+    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", w_l1=W_L1, w_ssim=W_SSIM, w_phys=W_PHYS)
+    g = torch.Generator(device=dev).manual_seed(0 + rank)
+    lq = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
+    gt = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
+    ratio = torch.ones(BATCH, 1, 1, 1, device=dev)
+    short = (lq * ratio).clamp(0, 1)
+
+    for _ in range(args.warmup):
+        tr.step(lq, gt, short, ratio)
+    logs_warm = tr.logs()
+
+    # live per-kernel timing (HIP events on the launch stream) for the timed steps
+    prof = {"gemm_f32": [], "wgrad_f32": []}
+
+    def mk(name, fl):
+        def cb(a, e0, e1):
+            prof[name].append((fl(a), e0, e1))
+        return cb
+
+    _lib.PROFILE["gemm_f32"] = mk("gemm_f32", lambda a: 2.0 * a[11] * a[12] * a[13])
+    _lib.PROFILE["wgrad_f32"] = mk("wgrad_f32", lambda a: 2.0 * a[8] * a[9] * a[10])
+    blk_events = []
+    orig_fwd, orig_bwd = net._block_fwd, net._block_bwd
+
+    def timed(fn):
+        def w(*a, **k):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*a, **k)
+            e1.record()
+            blk_events.append((e0, e1))
+            return r
+        return w
+
+    net._block_fwd, net._block_bwd = timed(orig_fwd), timed(orig_bwd)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step(lq, gt, short, ratio)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.PROFILE.clear()
+    net._block_fwd, net._block_bwd = orig_fwd, orig_bwd
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    logs = tr.logs()
+
+    classes = {}
+    for name, recs in prof.items():
+        ms = sum(e0.elapsed_time(e1) for _, e0, e1 in recs)
+        fl = sum(f for f, _, _ in recs)
+        classes[name] = (ms, fl, len(recs))
+    dom = max(classes, key=lambda k: classes[k][0])
+    ms, fl, nl = classes[dom]
+    achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    blk_ms = sum(e0.elapsed_time(e1) for e0, e1 in blk_events) / args.steps
+    blk_bytes = nafblock_bytes(net, BATCH, IMG, IMG)
+    blk_gbps = blk_bytes / (blk_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        step_ms = elapsed / args.steps * 1e3
+        res = {
+            "metric": METRIC,
+            "value": round(BATCH * world * args.steps / elapsed, 3),
+            "unit": "img/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U[0,1) sRGB, expo_ratio 1, torch default init, seed 0+rank)",
+            "config": {"workload": "cfg2: NAFNet w32 enc[2,2,4,8] mid12 dec[2,2,2,2] (29.16M), rgb/B2 PSF, "
+                                   "bs16/GPU 256x256, L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW",
+                       "global_batch": BATCH * world, "image": IMG, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "launches_per_step": nl // args.steps,
+                         "ms_per_step": round(ms / args.steps, 3),
+                         "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in classes.items()}},
+            "nafblock_roofline": {"bytes_per_step": blk_bytes, "ms_per_step": round(blk_ms, 3),
+                                  "achieved_GBps": round(blk_gbps, 1), "peak_GBps": HBM_PEAK_GBPS,
+                                  "frac": round(blk_gbps / HBM_PEAK_GBPS, 4)},
+            "losses": logs,
+        }
+        if world == 1:
+            psnr, maxabs = psnr_vs_cpu(net, dev)
+            res["psnr_vs_cpu_ref_db"] = round(psnr, 2) if psnr != float("inf") else "inf"
+            res["max_abs_vs_cpu_ref"] = maxabs
+            if not args.no_cpu_baseline:
+                res["cpu_baseline"] = cpu_baseline(init_sd)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

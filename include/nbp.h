@@ -1,0 +1,188 @@
+/*
+ * nbp.h — C-ABI of the MI355X (gfx950) NewBP-NAFNet hot-path library  (liblowlight_nbp.so).
+ *
+ * The reference (RUA1027/Lowlight_Image_Enhancement) is pure Python; its "operator boundary" is the set of
+ * torch ops its hot-path modules call.  Each entry point below replaces the reference op named in its comment
+ * (file:line relative to the reference root).  The Python host layer (lowlight_image_enhancement_amd/) binds
+ * these with ctypes and keeps the reference's module/function names.
+ *
+ * Conventions
+ *  - All tensors are caller-owned device pointers (fp32 unless stated).  The library never allocates
+ *    persistent device memory: scratch is a caller-provided workspace sized by the *_workspace_* queries.
+ *  - Every call is asynchronous on the caller's stream (hipStream_t passed as nbp_stream_t) and stateless.
+ *  - Return 0 on success or a negative NBP_ERR_* code; nbp_last_error_string() describes the last failure
+ *    (thread-local).
+ *  - Activations inside the network are NHWC ([B][H][W][C], M = B*H*W rows of C channels); images at the
+ *    network boundary and the loss terms are NCHW, the reference's public layout.
+ *  - Scalars produced on the device (losses, norms) are written to device memory; gradients of scalar losses
+ *    read the upstream gradient from device memory (`up`), so nothing forces a host sync.
+ */
+#ifndef NBP_H_
+#define NBP_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NBP_VERSION 1
+typedef void* nbp_stream_t; /* hipStream_t */
+
+enum { NBP_OK = 0, NBP_ERR_ARG = -1, NBP_ERR_LAUNCH = -2, NBP_ERR_INTERNAL = -3 };
+
+const char* nbp_last_error_string(void);
+int nbp_version(void);
+
+/* ------------------------------------------------------------------ physics branch (NewBP) */
+/* CrosstalkPSF.__init__ normalisation k / clamp_min(k.sum(1), 1e-12) (NewBP_model/newbp_layer.py:102-106),
+ * host-side, bit-exact with torch's CPU fp32 row sum (8 interleaved accumulators). */
+int nbp_psf_normalize_host(const float* k, int n_kernels, int len, float* out);
+/* depthwise KxK conv on NCHW, pad_mode 0 zeros / 1 replicate / 2 reflect; k [C][KH*KW] or shared [1][KH*KW]:
+ * CrosstalkPSF.forward F.conv2d(x, K, padding=1, groups=3) (newbp_layer.py:109-126); pre_clamp applies
+ * clamp(0,1) to the input first. */
+int nbp_dwconv_nchw_fwd(const float* x, const float* k, int k_shared, float* y, int N, int C, int H, int W, int KH,
+                        int KW, int pad_mode, int pre_clamp, nbp_stream_t s);
+/* adjoint of the zero-padded depthwise conv = conv_transpose2d(g, K, padding=1, groups=3)
+ * (core_tests/test_physics_loss_grad.py:65-86). */
+int nbp_dwconv_nchw_bwd_zero(const float* gy, const float* k, int k_shared, float* gx, int N, int C, int H, int W,
+                             int KH, int KW, nbp_stream_t s);
+/* Fused physics L1: loss = mean |PSF_pad(clamp?(bhat)) - clamp?(clamp?(a) * ratio)|
+ *   pad_mode 0 + normalised K + clamp_align : PhysicalConsistencyLossSRGB (NewBP_model/losses.py:206-220) with
+ *     align_exposure_srgb (:195-203);
+ *   pad_mode 1 (replicate) + raw K           : PhysicsConsistencyLoss (losses.py:158-192).
+ * ratio: [N*C] per (sample, channel) (ratio_full = 0) or a full [N,C,H,W] map.  sign_map (optional, [N,C,H,W])
+ * keeps sign(residual) for the backward.  ws: nbp_phys_l1_workspace_doubles() doubles. */
+size_t nbp_phys_l1_workspace_doubles(int N, int C, int H, int W);
+int nbp_phys_l1_fwd(const float* bhat, const float* a, const float* ratio, int ratio_full, const float* k, int k_shared,
+                    int N, int C, int H, int W, int KH, int KW, int pad_mode, int clamp_bhat, int clamp_a_in,
+                    int clamp_align, double* ws, float* loss, float* sign_map, nbp_stream_t s);
+/* d loss / d bhat = up[0]/numel * PSF^T(sign) (* 1[0 <= bhat <= 1] when clamp_bhat). */
+int nbp_phys_l1_bwd(const float* sign_map, const float* bhat, const float* k, int k_shared, const float* up, int N,
+                    int C, int H, int W, int KH, int KW, int pad_mode, int clamp_bhat, float* gx, nbp_stream_t s);
+/* _phys_cons_core (metrics/phys_consistency.py:193-255) for phys_cons_raw (:260) / phys_cons_srgb (:323):
+ * full [Co][Ci][KH][KW] PSF (already prepared), pad 0/1/2, ratio_mode 0 [N] / 1 [N,1,H,W] / 2 [N,Co,H,W],
+ * crop 'valid' (crop_valid=1) or 'same', clamp01 of the synthesised observation (sRGB), L1 or Charbonnier
+ * sqrt(d^2 + eps^2).  out[0..N-1] per-sample means, out[N] batch mean, out[N+1] batch sum;
+ * amap (optional) = |y - obs| over the compared region, [N][Co][Ho][Wo]. */
+size_t nbp_phys_cons_workspace_doubles(int N, int H, int W);
+int nbp_phys_cons(const float* pred, const float* obs, const float* psf, const float* ratio, int ratio_mode, int N,
+                  int Ci, int Co, int H, int W, int KH, int KW, int pad_mode, int crop_valid, int clamp01_out,
+                  int charbonnier, float eps, float* amap, double* ws, float* out, nbp_stream_t s);
+/* align_exposure_srgb (NewBP_model/losses.py:195-203): clamp(a * ratio, 0, 1), ratio [N*C] or full [N,C,H,W]. */
+int nbp_align_exposure(const float* a, const float* ratio, int ratio_full, float* out, int N, int C, long HW,
+                       nbp_stream_t s);
+/* torch.isfinite(x).all() (phys_consistency.py:58-61, losses.py:298-306): *flag_dev = 1 if any non-finite. */
+int nbp_all_finite(const float* x, long n, int* flag_dev, nbp_stream_t s);
+
+/* ------------------------------------------------------------------ NAFNet (NHWC) */
+/* 1x1 conv / channel contraction on MFMA (fp32 in, fp32 accumulate):  C = A(M,K) . B + epilogue
+ *   NAFBlock conv1/conv3/conv4/conv5 (NAFNet_arch.py:31-48), down conv 2x2/s2 (:106-108) through a_mode 1
+ *   (space-to-depth gather), up conv 1x1 + PixelShuffle(2) + skip add (:117-122,148-149) through c_mode 1
+ *   (depth-to-space scatter + residual), and the dgrad of all of them.
+ *   a_mode: 0 plain A[m*lda+k], 1 S2D gather of a 2x map (K = 4*cs), 2 per-image column scale (SCA, :67)
+ *   b_nk  : 1 B stored [N][K] (conv weight [out][in]); 0 B stored [K][N]
+ *   c_mode: 0 plain C[m*ldc+n], 1 D2S scatter into a 2x map (N = 4*cs)
+ *   epilogue: v = acc + bias[n]; pre (opt) = v; C = R ? R + rscale[n] * v : v   (layer-scale residual :72,80) */
+int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const float* B,
+                 long ldb, int b_nk, float* C, long ldc, int c_mode, int M, int N, int K, int gh, int gw, int cs,
+                 const float* bias, const float* R, const float* rscale, float* pre, nbp_stream_t s);
+/* weight gradient dW[n][k] = sum_m G(m,n) X(m,k) (+ db[n] = sum_m G(m,n)): split over M, fixed-order slab reduce. */
+size_t nbp_wgrad_workspace_floats(int M, int N, int K);
+int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx, int x_mode, const float* x_scale,
+                  int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
+                  float* ws, size_t ws_floats, nbp_stream_t s);
+/* out[i] = sum_{s<S} slab[s*L + i] (fixed order). */
+int nbp_reduce_slab(const float* slab, int S, long L, float* out, nbp_stream_t s);
+
+/* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC:
+ * writes yhat (normalised, optional), nout = w*yhat + b and den = sqrt(var + eps) per pixel. */
+int nbp_ln_nhwc_grid(long M, int C);
+int nbp_ln_fwd_nhwc(const float* x, const float* w, const float* b, float* yhat, float* nout, float* den, long M, int C,
+                    float eps, nbp_stream_t s);
+/* closed-form backward (:277-289) + residual gradient dres; per-block partials of dw/db in slab_w/slab_b
+ * ([nbp_ln_nhwc_grid][C] each, fold with nbp_reduce_slab). */
+int nbp_ln_bwd_nhwc(const float* dn, const float* yhat, const float* den, const float* w, const float* dres, float* dx,
+                    float* slab_w, float* slab_b, long M, int C, nbp_stream_t s);
+/* NCHW variants for the standalone LayerNorm2d module. */
+int nbp_ln_fwd_nchw(const float* x, const float* w, const float* b, float* y, float* yhat, float* den, int N, int C,
+                    long HW, float eps, nbp_stream_t s);
+int nbp_ln_bwd_nchw_workspace_floats(int N, int C, long HW);
+int nbp_ln_bwd_nchw(const float* dy, const float* yhat, const float* den, const float* w, float* dx, float* dw,
+                    float* db, float* ws, int N, int C, long HW, nbp_stream_t s);
+
+/* NAFBlock spatial branch: conv2 depthwise 3x3 + bias on 2C channels (NAFNet_arch.py:32-33) -> SimpleGate
+ * (:22-25) -> AdaptiveAvgPool2d(1) partial sums (:38) in pool_slab [B][chunks][C]. */
+int nbp_dw_chunks(int B, int H, int W, int C, int which);
+int nbp_dw_sg_pool_fwd(const float* t1, const float* wdw, const float* bdw, float* t2, float* g, float* pool_slab, int B,
+                       int H, int W, int C, nbp_stream_t s);
+/* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
+int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
+                int HW, int C, nbp_stream_t s);
+/* per-image channel sums slab[b][chunk][c] = sum_p x*y (y may be NULL). */
+int nbp_img_chan_dot(const float* x, const float* y, float* slab, int B, int H, int W, int C, nbp_stream_t s);
+/* SCA backward: da, ds = W^T da, dW = da^T mean, db = sum_b da. */
+int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float* mean, float* da, float* ds, float* dwsca,
+                float* dbsca, int B, int C, nbp_stream_t s);
+/* dg = dh*a + ds/HW, then SimpleGate backward into dt2 [M][2C]. */
+int nbp_sca_sg_bwd(const float* dh, const float* a, const float* ds, const float* t2, float* dt2, long M, int C, int HW,
+                   nbp_stream_t s);
+/* depthwise 3x3 backward: dt1, dW [2C][9], db [2C]. */
+size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C);
+int nbp_dw_bwd(const float* dt2, const float* t1, const float* wdw, float* dt1, float* dwdw, float* dbdw, float* ws,
+               int B, int H, int W, int C, nbp_stream_t s);
+
+/* SimpleGate on the FFN half (NAFNet_arch.py:75): g = t[:C]*t[C:], and its backward. */
+int nbp_sg_fwd(const float* t, float* g, long M, int C, nbp_stream_t s);
+int nbp_sg_bwd(const float* dg, const float* t, float* dt, long M, int C, nbp_stream_t s);
+/* layer-scale residual gradients (NAFNet_arch.py:72,80): ds = d*scale, slab partials of sum d*t (dbeta/dgamma). */
+int nbp_scale_dot_grid(long M, int C);
+int nbp_scale_dot(const float* d, const float* t, const float* scale, float* ds, float* slab, long M, int C,
+                  nbp_stream_t s);
+int nbp_nchw_to_nhwc(const float* x, float* y, int N, int C, long HW, nbp_stream_t s);
+int nbp_nhwc_to_nchw(const float* x, float* y, int N, int C, long HW, nbp_stream_t s);
+int nbp_add(const float* a, const float* b, float* y, long n, nbp_stream_t s);
+
+/* intro conv 3x3 (NAFNet_arch.py:88-89,136) on the check_image_size zero-padded grid (:157-162): NCHW image ->
+ * NHWC features [B][Hp][Wp][Cf]; backward gives dW, db and (optional) d image. */
+int nbp_intro_fwd(const float* img, const float* w, const float* bias, float* out, int B, int Cimg, int H0, int W0,
+                  int Hp, int Wp, int Cf, nbp_stream_t s);
+size_t nbp_intro_bwd_workspace_floats(int B, int Cimg, int Hp, int Wp, int Cf);
+int nbp_intro_bwd(const float* img, const float* dout, const float* w, float* dw, float* db, float* dimg, float* ws,
+                  int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s);
+/* ending conv 3x3 + global residual + crop (NAFNet_arch.py:90-91,152-155): NHWC features -> NCHW image. */
+int nbp_ending_fwd(const float* feat, const float* w, const float* bias, const float* img, float* out, int B, int Cimg,
+                   int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s);
+size_t nbp_ending_bwd_workspace_floats(int B, int Cimg, int H0, int W0, int Cf);
+int nbp_ending_bwd(const float* dy, const float* feat, const float* w, float* dfeat, float* dw, float* db, float* ws,
+                   int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s);
+
+/* ------------------------------------------------------------------ HybridLoss terms (NCHW) */
+/* mode 0: nn.L1Loss (NewBP_model/losses.py:249,332); mode 1: Charbonnier sqrt(d^2+eps)
+ * (NAFNet_base/basicsr/models/losses/losses.py:29-31).  clamp_a/clamp_b apply clamp(0,1) to the inputs. */
+size_t nbp_pix_workspace_doubles(long n);
+int nbp_pix_loss_fwd(const float* a, const float* b, long n, int mode, float eps, int clamp_a, int clamp_b, double* ws,
+                     float* loss, nbp_stream_t s);
+int nbp_pix_loss_bwd(const float* a, const float* b, long n, int mode, float eps, int clamp_a, int clamp_b,
+                     const float* up, float* ga, nbp_stream_t s);
+/* SSIMLoss (losses.py:146-155 -> kornia 0.6.12 ssim_loss, window 11, sigma 1.5, reflect pad). */
+size_t nbp_ssim_workspace_floats(long n);
+int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W, int window, float max_val,
+                      int clamp_in, int want_grad, float* ws, float* loss, nbp_stream_t s);
+int nbp_ssim_loss_bwd(const float* x, const float* y, int N, int C, int H, int W, int clamp_in, const float* up,
+                      float* ws, float* gx, nbp_stream_t s);
+
+/* ------------------------------------------------------------------ optimizer (image_restoration_model.py:313-320) */
+/* clip_grad_norm_(params, max_norm): state[0] = ||grad*grad_scale||, state[1] = clip coef * grad_scale. */
+size_t nbp_clip_workspace_doubles(long n);
+int nbp_grad_clip_coef(const float* grad, long n, float grad_scale, float max_norm, double* ws, float* state,
+                       nbp_stream_t s);
+/* torch.optim.AdamW step over the flat buffer with gradient * state[1]. */
+int nbp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
+                   float lr, float beta1, float beta2, float eps, float weight_decay, int step, nbp_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NBP_H_ */

@@ -1,0 +1,350 @@
+"""NewBP_model.losses on MI355X (reference: NewBP_model/losses.py).
+
+Same class/function names, constructor arguments, term order and return values as the reference; every term's
+forward and backward runs as HIP kernels (include/nbp.h): L1 / Charbonnier (nbp_pix_loss_*), SSIM
+(nbp_ssim_loss_*), the physics-consistency L1 with the crosstalk PSF (nbp_phys_l1_*), exposure alignment
+(nbp_align_exposure).  Scalars stay on the device; the upstream gradient is read from device memory.
+
+Not yet on the MI355X path (raise NotImplementedError when used, never a silent CPU/torch fallback):
+the VGG19 perceptual term, LPIPS and ΔE00 (SURVEY §8a rows 19-22, cfg3 — scheduled next).
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Dict, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .._lib import call, query
+from .newbp_layer import CrosstalkPSF
+
+
+def _resolve_device(device: Union[str, torch.device]) -> torch.device:
+    """losses.py:20-29."""
+    if isinstance(device, torch.device):
+        return device
+    if isinstance(device, str):
+        if device == "auto":
+            return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        return torch.device(device)
+    raise TypeError(f"Unsupported device spec: {device!r}")
+
+
+# ---------------------------------------------------------------- autograd wrappers over the C-ABI
+class _PixLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, mode, eps, clamp_a, clamp_b):
+        _lib.require_cuda(a, b)
+        if a.shape != b.shape:
+            raise ValueError(f"shape mismatch {tuple(a.shape)} vs {tuple(b.shape)}")
+        a, b = a.contiguous(), b.contiguous()
+        n = a.numel()
+        ws = torch.empty(query("pix_workspace_doubles", n), dtype=torch.float64, device=a.device)
+        loss = torch.empty((), device=a.device)
+        call("pix_loss_fwd", a, b, n, mode, eps, clamp_a, clamp_b, ws, loss)
+        ctx.save_for_backward(a, b)
+        ctx.args = (mode, eps, clamp_a, clamp_b)
+        return loss
+
+    @staticmethod
+    def backward(ctx, up):
+        a, b = ctx.saved_tensors
+        mode, eps, ca, cb = ctx.args
+        up = up.contiguous()
+        ga = gb = None
+        if ctx.needs_input_grad[0]:
+            ga = torch.empty_like(a)
+            call("pix_loss_bwd", a, b, a.numel(), mode, eps, ca, cb, up, ga)
+        if ctx.needs_input_grad[1]:
+            gb = torch.empty_like(b)
+            call("pix_loss_bwd", b, a, b.numel(), mode, eps, cb, ca, up, gb)
+        return ga, gb, None, None, None, None
+
+
+def l1_loss(a, b, clamp01=False):
+    return _PixLossFn.apply(a, b, 0, 0.0, bool(clamp01), bool(clamp01))
+
+
+def charbonnier_loss(a, b, eps=1e-12):
+    """NAFNet_base/basicsr/models/losses/losses.py:29-31 (mean reduction)."""
+    return _PixLossFn.apply(a, b, 1, float(eps), False, False)
+
+
+class _SSIMLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, window, max_val, clamp_in):
+        _lib.require_cuda(x, y)
+        if x.shape != y.shape or x.dim() != 4:
+            raise ValueError("SSIMLoss expects two [N,C,H,W] tensors of the same shape")
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("SSIM gradient w.r.t. the target is not implemented on the MI355X path")
+        x, y = x.contiguous(), y.contiguous()
+        N, C, H, W = x.shape
+        ws = torch.empty(query("ssim_workspace_floats", x.numel()), device=x.device)
+        loss = torch.empty((), device=x.device)
+        want = ctx.needs_input_grad[0]
+        call("ssim_loss_fwd", x, y, N, C, H, W, window, float(max_val), clamp_in, int(want), ws, loss)
+        ctx.save_for_backward(x, y, ws)
+        ctx.clamp_in = clamp_in
+        return loss
+
+    @staticmethod
+    def backward(ctx, up):
+        x, y, ws = ctx.saved_tensors
+        N, C, H, W = x.shape
+        gx = torch.empty_like(x)
+        call("ssim_loss_bwd", x, y, N, C, H, W, ctx.clamp_in, up.contiguous(), ws, gx)
+        return gx, None, None, None, None
+
+
+def _ratio_array(ratio, ref: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """Broadcast the exposure ratio against ref [N,C,H,W] following losses.py:195-203 (float -> tensor,
+    0-d -> [1], 1-d -> [B,1,1,1]); returns ([N*C] per-plane array, 0) or (full [N,C,H,W] map, 1)."""
+    N, C, H, W = ref.shape
+    if not torch.is_tensor(ratio):
+        return torch.full((N * C,), float(ratio), device=ref.device, dtype=torch.float32), 0
+    r = ratio.to(device=ref.device, dtype=torch.float32)
+    if r.dim() == 0:
+        r = r.view(1)
+    if r.dim() == 1:
+        r = r.view(-1, 1, 1, 1)
+    try:
+        shape = torch.broadcast_shapes(r.shape, ref.shape)
+    except RuntimeError:
+        shape = None
+    if shape is None or tuple(shape) != tuple(ref.shape):
+        raise ValueError(f"exposure ratio of shape {tuple(ratio.shape)} does not broadcast to {tuple(ref.shape)}")
+    if r.dim() == 4 and r.shape[2] == 1 and r.shape[3] == 1:
+        return r.expand(N, C, 1, 1).contiguous().view(-1), 0
+    return r.expand(N, C, H, W).contiguous(), 1
+
+
+class _PhysL1Fn(torch.autograd.Function):
+    """mean |PSF(clamp?(bhat)) - clamp?(clamp?(a)*ratio)| ; pad 0 = zero (sRGB loss), 1 = replicate (raw loss)."""
+
+    @staticmethod
+    def forward(ctx, bhat, a, ratio_arr, ratio_full, k, k_shared, pad_mode, clamp_bhat, clamp_a_in, clamp_align):
+        _lib.require_cuda(bhat, a, k)
+        if bhat.shape != a.shape:
+            raise ValueError(f"shape mismatch {tuple(bhat.shape)} vs {tuple(a.shape)}")
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("physics loss gradient w.r.t. the short exposure is not implemented")
+        bhat, a = bhat.contiguous(), a.contiguous()
+        N, C, H, W = bhat.shape
+        kk = k.detach().contiguous()
+        ws = torch.empty(query("phys_l1_workspace_doubles", N, C, H, W), dtype=torch.float64, device=bhat.device)
+        loss = torch.empty((), device=bhat.device)
+        sign = torch.empty_like(bhat) if ctx.needs_input_grad[0] else None
+        call("phys_l1_fwd", bhat, a, ratio_arr, ratio_full, kk, k_shared, N, C, H, W, kk.shape[-2], kk.shape[-1],
+             pad_mode, clamp_bhat, clamp_a_in, clamp_align, ws, loss, sign)
+        ctx.save_for_backward(sign, bhat, kk)
+        ctx.args = (k_shared, pad_mode, clamp_bhat)
+        return loss
+
+    @staticmethod
+    def backward(ctx, up):
+        sign, bhat, kk = ctx.saved_tensors
+        k_shared, pad_mode, clamp_bhat = ctx.args
+        N, C, H, W = bhat.shape
+        g = torch.empty_like(bhat)
+        call("phys_l1_bwd", sign, bhat, kk, k_shared, up.contiguous(), N, C, H, W, kk.shape[-2], kk.shape[-1],
+             pad_mode, clamp_bhat, g)
+        return g, None, None, None, None, None, None, None, None, None
+
+
+# ---------------------------------------------------------------- public classes (reference names)
+class PerceptualLoss(nn.Module):
+    """losses.py:32-69 — VGG19 features[:36] perceptual MSE.  The VGG19 conv stack is not on the MI355X path
+    yet; constructing is allowed, calling raises."""
+
+    def __init__(self, device: Union[str, torch.device] = "cuda", use_mse: bool = True, reduction: str = "mean"):
+        super().__init__()
+        self.use_mse = use_mse
+        self.reduction = reduction
+
+    def forward(self, generated_img, target_img):
+        raise NotImplementedError("PerceptualLoss (VGG19) is not implemented on the MI355X path yet; "
+                                  "set w_perc=0 / lambda_perceptual=0")
+
+
+class HybridLoss(nn.Module):
+    """losses.py:72-89: total = l1 * L1 + lp * Perc; returns (total, l1, perc)."""
+
+    def __init__(self, lambda_l1=1.0, lambda_perceptual=0.1, device="cuda"):
+        super().__init__()
+        self.device = _resolve_device(device)
+        self.lambda_l1 = lambda_l1
+        self.lambda_perceptual = lambda_perceptual
+        self.perceptual_loss = PerceptualLoss(device=self.device)
+
+    def forward(self, generated_img, target_img):
+        l1_val = l1_loss(generated_img, target_img)
+        if self.lambda_perceptual:
+            perceptual_val = self.perceptual_loss(generated_img, target_img)
+        else:
+            perceptual_val = torch.zeros((), device=generated_img.device)
+        total = self.lambda_l1 * l1_val + self.lambda_perceptual * perceptual_val
+        return total, l1_val, perceptual_val
+
+
+class DeltaE00Loss(nn.Module):
+    """losses.py:92-143 — ΔE00 on sRGB via kornia rgb_to_lab.  Scheduled (cfg3); raises when called."""
+
+    def __init__(self, eps: float = 1e-6):
+        super().__init__()
+        self.eps = eps
+
+    def forward(self, gen_srgb01, tgt_srgb01):
+        raise NotImplementedError("DeltaE00Loss is not implemented on the MI355X path yet")
+
+
+class SSIMLoss(nn.Module):
+    """losses.py:146-155: kornia SSIMLoss(window_size=11, max_val=1) on clamp(0,1) inputs, mean reduction."""
+
+    def __init__(self, window_size: int = 11, max_val: float = 1.0, reduction: str = "mean"):
+        super().__init__()
+        if window_size != 11 or reduction != "mean":
+            raise NotImplementedError("SSIMLoss on MI355X implements window_size=11, reduction='mean'")
+        self.window_size = window_size
+        self.max_val = max_val
+
+    def forward(self, gen_srgb01, tgt_srgb01):
+        return _SSIMLossFn.apply(gen_srgb01, tgt_srgb01, self.window_size, self.max_val, 1)
+
+
+class PhysicsConsistencyLoss(nn.Module):
+    """losses.py:158-192: |K * ReplicationPad(Bhat_raw) - clamp(A_raw * ratio)|_1 with the UN-normalised K
+    (depthwise: K is [C,1,kh,kw] or the shared [1,1,kh,kw])."""
+
+    def __init__(self, K_kernel: torch.Tensor, device: str = "cuda", clamp_align: bool = True):
+        super().__init__()
+        if K_kernel is None:
+            raise ValueError("K_kernel must be provided for PhysicsConsistencyLoss")
+        self.register_buffer("K", K_kernel.to(device))
+        self.K: torch.Tensor
+        self.clamp_align = clamp_align
+
+    def forward(self, Bhat_raw, A_raw, expo_ratio):
+        if expo_ratio.dim() == 1:
+            expo_ratio = expo_ratio.view(-1, 1, 1, 1)
+        C = Bhat_raw.shape[1]
+        k = self.K
+        if k.shape[1] != 1 or k.shape[0] not in (1, C):
+            raise NotImplementedError("PhysicsConsistencyLoss on MI355X implements the depthwise kernel forms "
+                                      "[C,1,kh,kw] and [1,1,kh,kw]")
+        r, full = _ratio_array(expo_ratio, A_raw)
+        return _PhysL1Fn.apply(Bhat_raw, A_raw, r, full, k.to(Bhat_raw.dtype), int(k.shape[0] == 1 and C > 1), 1,
+                               0, 0, int(self.clamp_align))
+
+
+def align_exposure_srgb(a_srgb: torch.Tensor, ratio) -> torch.Tensor:
+    """losses.py:195-203: clamp(a * ratio, 0, 1)."""
+    _lib.require_cuda(a_srgb)
+    a = a_srgb.contiguous()
+    N, C, H, W = a.shape
+    r, full = _ratio_array(ratio, a)
+    out = torch.empty_like(a)
+    call("align_exposure", a, r, full, out, N, C, H * W)
+    return out
+
+
+class PhysicalConsistencyLossSRGB(nn.Module):
+    """losses.py:206-220: L1(PSF(bhat_srgb), align(a_srgb; ratio)) — one fused kernel, adjoint backward."""
+
+    def __init__(self, psf_module: nn.Module):
+        super().__init__()
+        self.psf = psf_module
+
+    def forward(self, bhat_srgb, a_srgb, ratio, _clamp_bhat: bool = False, _clamp_a: bool = False):
+        if bhat_srgb.shape[1] != 3:
+            raise AssertionError("CrosstalkPSF expects sRGB inputs (3 channels).")
+        k = self.psf.kernel
+        mono = getattr(self.psf, "mode", "rgb") == "mono"
+        r, full = _ratio_array(ratio, a_srgb)
+        return _PhysL1Fn.apply(bhat_srgb, a_srgb, r, full, k.to(bhat_srgb.dtype), int(mono), 0, int(_clamp_bhat),
+                               int(_clamp_a), 1)
+
+
+class HybridLossPlus(nn.Module):
+    """losses.py:223-372: weighted sum of L1_raw, Perc, LPIPS, DeltaE, SSIM, Phys in that order; returns
+    (L_total, logs).  `check_finite=True` keeps the reference's per-term host-side finiteness check
+    (losses.py:298-306, a host sync per term); the fused trainer turns it off and checks once per log step."""
+
+    def __init__(self, device: str = "cuda", w_l1_raw: float = 1.0, w_perc: float = 0.02, w_lpips: float = 0.0,
+                 w_deltaE: float = 0.02, w_ssim: float = 0.05, w_phys: float = 0.10, use_deltaE: bool = True,
+                 use_ssim: bool = True, use_lpips: bool = False, use_phys: bool = True, use_uncertainty: bool = False,
+                 physics_kernel: Optional[torch.Tensor] = None, physics_psf_module: Optional[nn.Module] = None):
+        super().__init__()
+        device = _resolve_device(device)
+        self.register_buffer("_zero", torch.tensor(0.0), persistent=False)
+        self.perc = PerceptualLoss(device=device)
+        self.deltaE = DeltaE00Loss() if use_deltaE else None
+        self.ssim = SSIMLoss() if use_ssim else None
+        self.lpips = None
+        if use_lpips:
+            warnings.warn("Disabling LPIPS term: LPIPS is not implemented on the MI355X path yet", RuntimeWarning)
+        self.phys = PhysicsConsistencyLoss(physics_kernel, device=device) if use_phys and physics_kernel is not None else None
+        self.phys_srgb = PhysicalConsistencyLossSRGB(physics_psf_module.to(device)) if (
+            use_phys and physics_psf_module is not None) else None
+        self.use_uncertainty = use_uncertainty
+        if use_uncertainty:
+            self.log_sigma = nn.ParameterDict({k: nn.Parameter(torch.zeros(())) for k in
+                                               ("l1", "perc", "lpips", "de", "ssim", "phys")})
+        else:
+            self.w = dict(l1=w_l1_raw, perc=w_perc, lpips=w_lpips, de=w_deltaE, ssim=w_ssim, phys=w_phys)
+        self.check_finite = True
+
+    def _ensure_finite(self, name: str, value: torch.Tensor):
+        if not self.check_finite:
+            return
+        if not torch.isfinite(value).all():
+            raise RuntimeError(f"HybridLossPlus detected non-finite values in term '{name}'.")
+
+    def _weighted(self, name, val):
+        if val is None:
+            z = self._zero.clone()
+            return z, z.detach()
+        if self.use_uncertainty:
+            s = self.log_sigma[name]
+            return val * torch.exp(-2 * s) + s, val.detach()
+        return self.w[name] * val, val.detach()
+
+    def _active(self, name):
+        return self.use_uncertainty or self.w[name] != 0
+
+    def forward(self, *, Bhat_raw, B_raw, A_raw, expo_ratio, Bhat_srgb01, B_srgb01, A_srgb01=None):
+        logs: Dict[str, torch.Tensor] = {}
+        L_total = 0.0
+        L_l1 = l1_loss(Bhat_raw, B_raw)
+        self._ensure_finite("L1_raw", L_l1)
+        Lw, logs["L1_raw"] = self._weighted("l1", L_l1)
+        L_total = L_total + Lw
+        if self._active("perc"):  # the reference always evaluates VGG; a zero weight is skipped here
+            L_p = self.perc(Bhat_srgb01, B_srgb01)
+            self._ensure_finite("Perc", L_p)
+            Lw, logs["Perc"] = self._weighted("perc", L_p)
+            L_total = L_total + Lw
+        if self.deltaE is not None and self._active("de"):
+            L_de = self.deltaE(Bhat_srgb01, B_srgb01)
+            self._ensure_finite("DeltaE", L_de)
+            Lw, logs["DeltaE"] = self._weighted("de", L_de)
+            L_total = L_total + Lw
+        if self.ssim is not None:
+            L_ss = self.ssim(Bhat_srgb01, B_srgb01)
+            self._ensure_finite("SSIM", L_ss)
+            Lw, logs["SSIM"] = self._weighted("ssim", L_ss)
+            L_total = L_total + Lw
+        if self.phys is not None:
+            L_ph = self.phys(Bhat_raw, A_raw, expo_ratio)
+            self._ensure_finite("Phys_raw", L_ph)
+            Lw, logs["Phys"] = self._weighted("phys", L_ph)
+            L_total = L_total + Lw
+        elif self.phys_srgb is not None and A_srgb01 is not None:
+            L_phs = self.phys_srgb(Bhat_srgb01, A_srgb01, expo_ratio)
+            self._ensure_finite("Phys_srgb", L_phs)
+            Lw, logs["Phys"] = self._weighted("phys", L_phs)
+            L_total = L_total + Lw
+        logs["Total"] = L_total.detach()
+        return L_total, logs

@@ -1,0 +1,26 @@
+"""MI355X-native (gfx950) NewBP-NAFNet hot path: NAFNet fwd/bwd (Scenario B), the crosstalk-PSF physics branch
+and the HybridLoss terms as hand-written HIP kernels behind a C-ABI (include/nbp.h), exposed through the
+reference's Python API (RUA1027/Lowlight_Image_Enhancement: NewBP_model.*, metrics.phys_consistency).
+
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net, create_crosstalk_psf
+    from lowlight_image_enhancement_amd.NewBP_model.losses import HybridLossPlus
+    from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_srgb
+
+`install_aliases()` registers the reference's top-level module names (NewBP_model, metrics.phys_consistency)
+so unmodified train/eval scripts import this implementation.
+"""
+import sys
+
+__version__ = "0.1.0"
+
+
+def install_aliases():
+    from . import NewBP_model, metrics
+    from .NewBP_model import losses, newbp_layer, newbp_net_arch
+    from .metrics import phys_consistency
+    sys.modules.setdefault("NewBP_model", NewBP_model)
+    sys.modules.setdefault("NewBP_model.newbp_layer", newbp_layer)
+    sys.modules.setdefault("NewBP_model.newbp_net_arch", newbp_net_arch)
+    sys.modules.setdefault("NewBP_model.losses", losses)
+    sys.modules.setdefault("metrics", metrics)
+    sys.modules.setdefault("metrics.phys_consistency", phys_consistency)

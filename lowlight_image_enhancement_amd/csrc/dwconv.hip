@@ -1,0 +1,350 @@
+// NAFBlock spatial branch on NHWC activations (NAFNet_arch.py:32-41,64-67):
+//   conv2 = depthwise 3x3 (zero pad 1, bias) on 2C channels  ->  SimpleGate (x[:C] * x[C:])
+//   -> SCA: AdaptiveAvgPool2d(1) -> 1x1 conv C->C (+bias) -> broadcast multiply.
+// The pool is a per-image global reduction: the forward writes per-(image, chunk) partial sums in a slab that the
+// SCA kernel folds in a fixed order (bitwise reproducible, no atomics).
+#include "nbp_common.h"
+
+using namespace nbp;
+
+namespace {
+
+struct Geo {
+  int B, H, W, C;  // C = gate width; the depthwise conv runs on 2C channels
+  int chunks;      // pixel chunks per image
+  int chunk_px;    // pixels per chunk
+};
+
+// thread layout: quad q (4 channels) = tid % Q, pixel lane = tid / Q, PPI = blockDim / Q pixels per step
+__global__ void dw_sg_pool_fwd(const float* __restrict__ t1, const float* __restrict__ wdw, const float* __restrict__ bdw,
+                               float* __restrict__ t2, float* __restrict__ g, float* __restrict__ pool_slab, Geo geo) {
+  extern __shared__ float red[];  // [blockDim][4]
+  const int C = geo.C, C2 = 2 * C, Q = C / 4;
+  const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int HW = geo.H * geo.W;
+  float wa[4][9], wb[4][9];
+  float4 ba = ld4(bdw + q * 4), bb = ld4(bdw + C + q * 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      wa[j][t] = wdw[(q * 4 + j) * 9 + t];
+      wb[j][t] = wdw[(C + q * 4 + j) * 9 + t];
+    }
+  float4 pacc = f4(0.f);
+  const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
+  const float* base = t1 + (long)b * HW * C2;
+  if (pl < PPI) {
+    for (int p = p0 + pl; p < p1; p += PPI) {
+      const int h = p / geo.W, w = p - h * geo.W;
+      float4 aa = ba, ab = bb;
+#pragma unroll
+      for (int dh = -1; dh <= 1; ++dh) {
+        const int hh = h + dh;
+        if (hh < 0 || hh >= geo.H) continue;
+#pragma unroll
+        for (int dw = -1; dw <= 1; ++dw) {
+          const int ww = w + dw;
+          if (ww < 0 || ww >= geo.W) continue;
+          const int t = (dh + 1) * 3 + (dw + 1);
+          const float* src = base + ((long)hh * geo.W + ww) * C2 + q * 4;
+          const float4 va = ld4(src), vb = ld4(src + C);
+          aa.x = fmaf(wa[0][t], va.x, aa.x); aa.y = fmaf(wa[1][t], va.y, aa.y);
+          aa.z = fmaf(wa[2][t], va.z, aa.z); aa.w = fmaf(wa[3][t], va.w, aa.w);
+          ab.x = fmaf(wb[0][t], vb.x, ab.x); ab.y = fmaf(wb[1][t], vb.y, ab.y);
+          ab.z = fmaf(wb[2][t], vb.z, ab.z); ab.w = fmaf(wb[3][t], vb.w, ab.w);
+        }
+      }
+      const long m = (long)b * HW + p;
+      st4(t2 + m * C2 + q * 4, aa);
+      st4(t2 + m * C2 + C + q * 4, ab);
+      const float4 gv = aa * ab;
+      st4(g + m * C + q * 4, gv);
+      pacc += gv;
+    }
+  }
+  st4(red + tid * 4, pacc);
+  __syncthreads();
+  if (pl == 0) {
+    float4 s = f4(0.f);
+    for (int k = 0; k < PPI; ++k) s += ld4(red + (k * Q + q) * 4);
+    st4(pool_slab + ((long)b * geo.chunks + chunk) * C + q * 4, s);
+  }
+}
+
+// SCA: mean[b][i] = sum_chunks slab / HW ; a[b][o] = bsca[o] + sum_i W[o][i] mean[i]  (one wave per output o)
+__global__ void sca_fwd(const float* __restrict__ pool_slab, int chunks, const float* __restrict__ wsca,
+                        const float* __restrict__ bsca, float* __restrict__ mean_out, float* __restrict__ a_out, int C,
+                        float inv_hw) {
+  extern __shared__ float mean[];
+  const int b = blockIdx.y;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < chunks; ++k) s += pool_slab[((long)b * chunks + k) * C + i];
+    mean[i] = s * inv_hw;
+    if (blockIdx.x == 0) mean_out[(long)b * C + i] = s * inv_hw;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int o0 = blockIdx.x * 64;
+  for (int o = o0 + wv; o < min(C, o0 + 64); o += nw) {
+    float acc = 0.f;
+    for (int i = lane; i < C; i += 64) acc = fmaf(wsca[(long)o * C + i], mean[i], acc);
+    acc = wave_sum(acc);
+    if (lane == 0) a_out[(long)b * C + o] = acc + bsca[o];
+  }
+}
+
+// per-image channel reduction: slab[b][chunk][c] = sum_{p in chunk} x[p][c] * (y ? y[p][c] : 1)
+__global__ void img_chan_dot(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ slab,
+                             Geo geo) {
+  extern __shared__ float red[];
+  const int C = geo.C, Q = C / 4;
+  const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int HW = geo.H * geo.W;
+  const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
+  float4 acc = f4(0.f);
+  if (pl < PPI) {
+    for (int p = p0 + pl; p < p1; p += PPI) {
+      const long o = ((long)b * HW + p) * C + q * 4;
+      float4 v = ld4(x + o);
+      if (y) v = v * ld4(y + o);
+      acc += v;
+    }
+  }
+  st4(red + tid * 4, acc);
+  __syncthreads();
+  if (pl == 0) {
+    float4 s = f4(0.f);
+    for (int k = 0; k < PPI; ++k) s += ld4(red + (k * Q + q) * 4);
+    st4(slab + ((long)b * geo.chunks + chunk) * C + q * 4, s);
+  }
+}
+
+// SCA backward, per image: da[b][o] = sum_chunks slab ; ds[b][i] = sum_o W[o][i] da[b][o]
+__global__ void sca_bwd_a(const float* __restrict__ da_slab, int chunks, const float* __restrict__ wsca,
+                          float* __restrict__ da_out, float* __restrict__ ds_out, int C) {
+  extern __shared__ float da[];
+  const int b = blockIdx.y;
+  for (int o = threadIdx.x; o < C; o += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < chunks; ++k) s += da_slab[((long)b * chunks + k) * C + o];
+    da[o] = s;
+    if (blockIdx.x == 0) da_out[(long)b * C + o] = s;
+  }
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < C) {
+    float acc = 0.f;
+    for (int o = 0; o < C; ++o) acc = fmaf(wsca[(long)o * C + i], da[o], acc);
+    ds_out[(long)b * C + i] = acc;
+  }
+}
+
+// dW[o][i] = sum_b da[b][o] * mean[b][i] ; db[o] = sum_b da[b][o]
+__global__ void sca_bwd_b(const float* __restrict__ da, const float* __restrict__ mean, int B, int C,
+                          float* __restrict__ dw, float* __restrict__ db) {
+  const long total = (long)C * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int o = e / C, i = e % C;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc = fmaf(da[(long)b * C + o], mean[(long)b * C + i], acc);
+    dw[e] = acc;
+    if (i == 0) {
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) s += da[(long)b * C + o];
+      db[o] = s;
+    }
+  }
+}
+
+// dg = dh * a[b] + ds[b] / HW ; SimpleGate backward: dt2[:C] = dg * t2[C:], dt2[C:] = dg * t2[:C]
+__global__ void sca_sg_bwd(const float* __restrict__ dh, const float* __restrict__ a, const float* __restrict__ ds,
+                           const float* __restrict__ t2, float* __restrict__ dt2, long M, int C, int HW, float inv_hw) {
+  const int Q = C / 4;
+  const long total = M * Q;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long m = e / Q;
+    const int q = e % Q;
+    const int b = m / HW;
+    const float4 dg = fma4(ld4(dh + m * C + q * 4), ld4(a + (long)b * C + q * 4), ld4(ds + (long)b * C + q * 4) * f4(inv_hw));
+    const float4 ta = ld4(t2 + m * 2 * C + q * 4), tb = ld4(t2 + m * 2 * C + C + q * 4);
+    st4(dt2 + m * 2 * C + q * 4, dg * tb);
+    st4(dt2 + m * 2 * C + C + q * 4, dg * ta);
+  }
+}
+
+// depthwise 3x3 backward on C2 channels: dt1 = sum_t w[t] dt2(p - off_t) ; partial dW[c][t] = sum dt2(p) t1(p+off_t),
+// partial db[c] = sum dt2(p).  slab: [B*chunks][C2][10]
+__global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ t1, const float* __restrict__ wdw,
+                       float* __restrict__ dt1, float* __restrict__ slab, Geo geo) {
+  extern __shared__ float red[];  // [blockDim][4]
+  const int C2 = 2 * geo.C, Q = C2 / 4;
+  const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
+  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int HW = geo.H * geo.W;
+  float wk[4][9];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wk[j][t] = wdw[(q * 4 + j) * 9 + t];
+  float4 aw[9], ab = f4(0.f);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) aw[t] = f4(0.f);
+  const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
+  const float* gb = dt2 + (long)b * HW * C2 + q * 4;
+  const float* xb = t1 + (long)b * HW * C2 + q * 4;
+  if (pl < PPI) {
+    for (int p = p0 + pl; p < p1; p += PPI) {
+      const int h = p / geo.W, w = p - h * geo.W;
+      const float4 gc = ld4(gb + (long)p * C2);
+      ab += gc;
+      float4 acc = f4(0.f);
+#pragma unroll
+      for (int dh = -1; dh <= 1; ++dh) {
+#pragma unroll
+        for (int dw = -1; dw <= 1; ++dw) {
+          const int t = (dh + 1) * 3 + (dw + 1);
+          // forward: t2(q) += w[t] t1(q + off)  ->  dt1(p) += w[t] dt2(p - off) ; dW[t] += dt2(p) t1(p + off)
+          const int hs = h - dh, ws = w - dw;
+          if (hs >= 0 && hs < geo.H && ws >= 0 && ws < geo.W) {
+            const float4 gv = ld4(gb + ((long)hs * geo.W + ws) * C2);
+            acc.x = fmaf(wk[0][t], gv.x, acc.x); acc.y = fmaf(wk[1][t], gv.y, acc.y);
+            acc.z = fmaf(wk[2][t], gv.z, acc.z); acc.w = fmaf(wk[3][t], gv.w, acc.w);
+          }
+          const int hp = h + dh, wp = w + dw;
+          if (hp >= 0 && hp < geo.H && wp >= 0 && wp < geo.W) {
+            aw[t] = fma4(gc, ld4(xb + ((long)hp * geo.W + wp) * C2), aw[t]);
+          }
+        }
+      }
+      st4(dt1 + ((long)b * HW + p) * C2 + q * 4, acc);
+    }
+  }
+  // block reduction over pixel lanes sharing quad q, one tap at a time through a [blockDim][4] buffer
+  float* dst = slab + ((long)b * geo.chunks + chunk) * C2 * 10;
+#pragma unroll
+  for (int t = 0; t < 10; ++t) {
+    st4(red + tid * 4, t < 9 ? aw[t] : ab);
+    __syncthreads();
+    if (pl == 0) {
+      float4 sum = f4(0.f);
+      for (int k = 0; k < PPI; ++k) sum += ld4(red + (k * Q + q) * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[(long)(q * 4 + j) * 10 + t] = get(sum, j);
+    }
+    __syncthreads();
+  }
+}
+
+// fold the [S][C2][10] slab into dW [C2][9] and db [C2]
+__global__ void dw_bwd_reduce(const float* __restrict__ slab, int S_, int C2, float* __restrict__ dw, float* __restrict__ db) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= C2 * 10) return;
+  float s = 0.f;
+  for (int k = 0; k < S_; ++k) s += slab[(long)k * C2 * 10 + e];
+  const int c = e / 10, t = e % 10;
+  if (t < 9) dw[c * 9 + t] = s;
+  else db[c] = s;
+}
+
+int block_for_quads(int Q) {
+  if (Q >= 256) return Q;  // one pixel per step, one thread per quad (Q <= 1024)
+  return 256;
+}
+
+Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
+  Geo g{B, H, W, C, 1, H * W};
+  const int HW = H * W;
+  const int ppi = block / Q;
+  long want = cap_blocks / B;
+  if (want < 1) want = 1;
+  long maxc = (HW + ppi - 1) / ppi;  // at least one step per chunk
+  if (want > maxc) want = maxc;
+  int px = (int)((HW + want - 1) / want);
+  px = ((px + ppi - 1) / ppi) * ppi;
+  g.chunk_px = px;
+  g.chunks = (HW + px - 1) / px;
+  return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+// geometry helper for callers sizing the slabs: returns chunks per image for the forward pool / img_chan_dot
+int nbp_dw_chunks(int B, int H, int W, int C, int which) {
+  // which 0: forward/pool (quads = C/4), 1: dw backward (quads = 2C/4)
+  const int Q = which == 0 ? C / 4 : C / 2;
+  const int blk = block_for_quads(Q);
+  long cap = which == 0 ? 2048 : (4L << 20) / (2L * C * 10) ;
+  if (cap > 2048) cap = 2048;
+  return make_geo(B, H, W, C, Q, blk, cap).chunks;
+}
+
+int nbp_dw_sg_pool_fwd(const float* t1, const float* wdw, const float* bdw, float* t2, float* g, float* pool_slab, int B,
+                       int H, int W, int C, nbp_stream_t s) {
+  NBP_REQUIRE(t1 && wdw && bdw && t2 && g && pool_slab && B > 0 && H > 0 && W > 0, "nbp_dw_sg_pool_fwd: bad args");
+  NBP_REQUIRE(C % 4 == 0 && C / 4 <= 1024, "nbp_dw_sg_pool_fwd: C");
+  const int Q = C / 4, blk = block_for_quads(Q);
+  Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
+  dim3 grid(geo.chunks, B);
+  dw_sg_pool_fwd<<<grid, blk, blk * 4 * sizeof(float), S(s)>>>(t1, wdw, bdw, t2, g, pool_slab, geo);
+  return check_launch("dw_sg_pool_fwd");
+}
+
+int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
+                int HW, int C, nbp_stream_t s) {
+  NBP_REQUIRE(pool_slab && wsca && bsca && mean && a && B > 0 && C > 0 && chunks > 0, "nbp_sca_fwd: bad args");
+  dim3 grid(cdiv(C, 64), B);
+  sca_fwd<<<grid, 256, C * sizeof(float), S(s)>>>(pool_slab, chunks, wsca, bsca, mean, a, C, 1.f / (float)HW);
+  return check_launch("sca_fwd");
+}
+
+int nbp_img_chan_dot(const float* x, const float* y, float* slab, int B, int H, int W, int C, nbp_stream_t s) {
+  NBP_REQUIRE(x && slab && B > 0 && C % 4 == 0 && C / 4 <= 1024, "nbp_img_chan_dot: bad args");
+  const int Q = C / 4, blk = block_for_quads(Q);
+  Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
+  img_chan_dot<<<dim3(geo.chunks, B), blk, blk * 4 * sizeof(float), S(s)>>>(x, y, slab, geo);
+  return check_launch("img_chan_dot");
+}
+
+int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float* mean, float* da, float* ds, float* dwsca,
+                float* dbsca, int B, int C, nbp_stream_t s) {
+  NBP_REQUIRE(da_slab && wsca && mean && da && ds && dwsca && dbsca && B > 0 && C > 0, "nbp_sca_bwd: bad args");
+  sca_bwd_a<<<dim3(cdiv(C, 256), B), 256, C * sizeof(float), S(s)>>>(da_slab, chunks, wsca, da, ds, C);
+  const long tot = (long)C * C;
+  sca_bwd_b<<<cdiv(tot, 256) > 2048 ? 2048 : cdiv(tot, 256), 256, 0, S(s)>>>(da, mean, B, C, dwsca, dbsca);
+  return check_launch("sca_bwd");
+}
+
+int nbp_sca_sg_bwd(const float* dh, const float* a, const float* ds, const float* t2, float* dt2, long M, int C, int HW,
+                   nbp_stream_t s) {
+  NBP_REQUIRE(dh && a && ds && t2 && dt2 && M > 0 && C % 4 == 0 && HW > 0, "nbp_sca_sg_bwd: bad args");
+  const long tot = M * (C / 4);
+  sca_sg_bwd<<<cdiv(tot, 256) > 4096 ? 4096 : cdiv(tot, 256), 256, 0, S(s)>>>(dh, a, ds, t2, dt2, M, C, HW,
+                                                                             1.f / (float)HW);
+  return check_launch("sca_sg_bwd");
+}
+
+size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
+  return (size_t)B * nbp_dw_chunks(B, H, W, C, 1) * 2 * C * 10;
+}
+
+int nbp_dw_bwd(const float* dt2, const float* t1, const float* wdw, float* dt1, float* dwdw, float* dbdw, float* ws,
+               int B, int H, int W, int C, nbp_stream_t s) {
+  NBP_REQUIRE(dt2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && C % 2 == 0, "nbp_dw_bwd: bad args");
+  const int Q = C / 2;  // quads over 2C channels
+  NBP_REQUIRE(Q <= 1024, "nbp_dw_bwd: too many channels");
+  const int blk = block_for_quads(Q);
+  long cap = (4L << 20) / (2L * C * 10);
+  if (cap > 2048) cap = 2048;
+  Geo geo = make_geo(B, H, W, C, Q, blk, cap);
+  dw_bwd<<<dim3(geo.chunks, B), blk, (size_t)blk * 4 * sizeof(float), S(s)>>>(dt2, t1, wdw, dt1, ws, geo);
+  dw_bwd_reduce<<<cdiv(2 * C * 10, 256), 256, 0, S(s)>>>(ws, B * geo.chunks, 2 * C, dwdw, dbdw);
+  return check_launch("dw_bwd");
+}
+
+}  // extern "C"

@@ -1,0 +1,375 @@
+// fp32 MFMA GEMMs for every channel contraction of NAFNet on NHWC activations:
+//   the NAFBlock 1x1 convs conv1/conv3/conv4/conv5 (NAFNet_arch.py:31-48), the 2x2/s2 down conv (:106-108,
+//   as a GEMM over a space-to-depth gather), the 1x1 up conv + PixelShuffle(2) (:117-122, as a GEMM whose
+//   epilogue scatters depth-to-space and adds the skip, :148-149), and their dgrad / wgrad.
+// v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation (one rounding per fma).
+#include "nbp_common.h"
+
+using namespace nbp;
+
+namespace {
+
+enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2 };
+enum { CM_PLAIN = 0, CM_D2S = 1 };
+
+struct GemmP {
+  const float* A;
+  long lda;
+  const float* a_scale;
+  int rows_per_img;
+  const float* B;
+  long ldb;
+  float* C;
+  long ldc;
+  int M, N, K;
+  int gh, gw, cs;  // S2D/D2S geometry: low-res grid gh x gw, cs channels per sub-position of the 2x map
+  const float* bias;
+  const float* R;
+  const float* rscale;
+  float* pre;
+};
+
+// offset of element (m, kq*4 .. +3) of a space-to-depth view of a 2x-resolution NHWC map
+__device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
+  const int per = gh * gw;
+  const int b = m / per, rem = m - b * per;
+  const int i = rem / gw, j = rem - i * gw;
+  const int q = k / cs, c = k - q * cs;
+  const int kh = q >> 1, kw = q & 1;
+  return ((long)(b * 2 * gh + 2 * i + kh) * (2 * gw) + 2 * j + kw) * cs + c;
+}
+
+template <int BM, int BN, bool B_NK, int AMODE, int CMODE>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
+  constexpr int BK = 32, LS = BK + 1;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int A_IT = BM / 32, B_IT = BN / 32;  // float4 loads per thread per K-tile
+  __shared__ float As[BM * LS];
+  __shared__ float Bs[BN * LS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int M = p.M, N = p.N, K = p.K;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 ra[A_IT], rb[B_IT];
+
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx >> 3, kq = idx & 7;
+      const int m = m0 + r, k = k0 + kq * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < M && k < K) {
+        if (AMODE == AM_S2D) v = ld4(p.A + s2d_off(m, k, p.gh, p.gw, p.cs));
+        else v = ld4(p.A + (long)m * p.lda + k);
+        if (AMODE == AM_SCALE) v = v * ld4(p.a_scale + (long)(m / p.rows_per_img) * K + k);
+      }
+      ra[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int idx = tid + it * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (B_NK) {
+        const int r = idx >> 3, kq = idx & 7;
+        const int n = n0 + r, k = k0 + kq * 4;
+        if (n < N && k < K) v = ld4(p.B + (long)n * p.ldb + k);
+      } else {
+        const int kr = idx / (BN / 4), nq = idx % (BN / 4);
+        const int k = k0 + kr, n = n0 + nq * 4;
+        if (k < K && n < N) v = ld4(p.B + (long)k * p.ldb + n);
+      }
+      rb[it] = v;
+    }
+  };
+  auto store_tiles = [&]() {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx >> 3, kq = idx & 7;
+      float* d = As + r * LS + kq * 4;
+      d[0] = ra[it].x; d[1] = ra[it].y; d[2] = ra[it].z; d[3] = ra[it].w;
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int idx = tid + it * 256;
+      if (B_NK) {
+        const int r = idx >> 3, kq = idx & 7;
+        float* d = Bs + r * LS + kq * 4;
+        d[0] = rb[it].x; d[1] = rb[it].y; d[2] = rb[it].z; d[3] = rb[it].w;
+      } else {
+        const int kr = idx / (BN / 4), nq = idx % (BN / 4);
+        float* d = Bs + (nq * 4) * LS + kr;
+        d[0] = rb[it].x; d[LS] = rb[it].y; d[2 * LS] = rb[it].z; d[3 * LS] = rb[it].w;
+      }
+    }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  load_tiles(0);
+  store_tiles();
+  __syncthreads();
+  const int arow = wm * (BM / 2) + (lane & 31);
+  const int brow = wn * (BN / 2) + (lane & 31);
+  const int kh = lane >> 5;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) load_tiles((t + 1) * BK);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[(arow + i * 32) * LS + kk + kh];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[(brow + j * 32) * LS + kk + kh];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (t + 1 < nk) {
+      store_tiles();
+      __syncthreads();
+    }
+  }
+
+  // epilogue: C/D map of 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float bcol = p.bias ? p.bias[col] : 0.f;
+      const float scol = p.rscale ? p.rscale[col] : 1.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        long off;
+        if (CMODE == CM_D2S) off = s2d_off(row, col, p.gh, p.gw, p.cs);
+        else off = (long)row * p.ldc + col;
+        float v = acc[i][j][r] + bcol;
+        if (p.pre) p.pre[off] = v;
+        if (p.R) v = p.R[off] + scol * v;
+        p.C[off] = v;
+      }
+    }
+}
+
+// ---------------------------------------------------------------- weight gradient: dW[n][k] = sum_m G(m,n) X(m,k)
+struct WgradP {
+  const float* G;
+  long ldg;
+  const float* X;
+  long ldx;
+  const float* x_scale;
+  int rows_per_img;
+  int M, N, K;
+  int gh, gw, cs_g, cs_x;
+  float* slab;    // [S][N][K]
+  float* slab_b;  // [S][N] (column sums of G) or null
+  int chunk;
+};
+
+template <int GMODE, int XMODE>
+__global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
+  constexpr int RM = 32, TNW = 64, TKW = 64, LS = 68;
+  __shared__ float Gs[RM * LS];
+  __shared__ float Xs[RM * LS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * TNW, k0 = blockIdx.y * TKW, s = blockIdx.z;
+  const int mb = s * p.chunk;
+  const int me = min(p.M, mb + p.chunk);
+  const bool do_b = p.slab_b && blockIdx.y == 0;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bsum = 0.f;
+  float4 rg[2], rx[2];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx >> 4, q = idx & 15;
+      const int m = m0 + r;
+      float4 g = make_float4(0.f, 0.f, 0.f, 0.f), x = g;
+      const int n = n0 + q * 4, k = k0 + q * 4;
+      if (m < me) {
+        if (n < p.N) {
+          if (GMODE == AM_S2D) g = ld4(p.G + s2d_off(m, n, p.gh, p.gw, p.cs_g));
+          else g = ld4(p.G + (long)m * p.ldg + n);
+        }
+        if (k < p.K) {
+          if (XMODE == AM_S2D) x = ld4(p.X + s2d_off(m, k, p.gh, p.gw, p.cs_x));
+          else x = ld4(p.X + (long)m * p.ldx + k);
+          if (XMODE == AM_SCALE) x = x * ld4(p.x_scale + (long)(m / p.rows_per_img) * p.K + k);
+        }
+      }
+      rg[it] = g;
+      rx[it] = x;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx >> 4, q = idx & 15;
+      st4(Gs + r * LS + q * 4, rg[it]);
+      st4(Xs + r * LS + q * 4, rx[it]);
+    }
+  };
+  const int kh = lane >> 5;
+  if (mb < me) {
+    load(mb);
+    store();
+    __syncthreads();
+    for (int m0 = mb; m0 < me; m0 += RM) {
+      const bool more = m0 + RM < me;
+      if (more) load(m0 + RM);
+#pragma unroll
+      for (int kk = 0; kk < RM; kk += 2) {
+        const float a = Gs[(kk + kh) * LS + wn * 32 + (lane & 31)];
+        const float b = Xs[(kk + kh) * LS + wk * 32 + (lane & 31)];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      }
+      if (do_b && tid < TNW) {
+#pragma unroll 8
+        for (int r = 0; r < RM; ++r) bsum += Gs[r * LS + tid];
+      }
+      __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int k = k0 + wk * 32 + (lane & 31);
+    if (n < p.N && k < p.K) p.slab[((long)s * p.N + n) * p.K + k] = acc[r];
+  }
+  if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
+}
+
+// out[i] = sum_{s < S} slab[s * L + i]  (fixed order: bitwise reproducible)
+__global__ void reduce_slab_kernel(const float* __restrict__ slab, int S, long L, float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < L; i += (long)gridDim.x * blockDim.x) {
+    float a = 0.f;
+    for (int s = 0; s < S; ++s) a += slab[(long)s * L + i];
+    out[i] = a;
+  }
+}
+
+template <int BM, int BN, bool B_NK, int AMODE, int CMODE>
+void launch_gemm(const GemmP& p, hipStream_t st) {
+  dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
+  gemm_f32_kernel<BM, BN, B_NK, AMODE, CMODE><<<grid, 256, 0, st>>>(p);
+}
+
+template <bool B_NK, int AMODE, int CMODE>
+void dispatch_tiles(const GemmP& p, hipStream_t st) {
+  const bool bn128 = p.N >= 128;
+  const long tiles128 = (long)cdiv(p.M, 128) * cdiv(p.N, bn128 ? 128 : 64);
+  const bool bm128 = tiles128 >= 1024;
+  if (bm128 && bn128) launch_gemm<128, 128, B_NK, AMODE, CMODE>(p, st);
+  else if (bm128) launch_gemm<128, 64, B_NK, AMODE, CMODE>(p, st);
+  else if (bn128) launch_gemm<64, 128, B_NK, AMODE, CMODE>(p, st);
+  else launch_gemm<64, 64, B_NK, AMODE, CMODE>(p, st);
+}
+
+int wgrad_splits(int M, int N, int K) {
+  const long tiles = (long)cdiv(N, 64) * cdiv(K, 64);
+  long s = (2048 + tiles - 1) / tiles;
+  const long maxs = cdiv(M, 256);  // keep >= 256 rows per split
+  if (s > maxs) s = maxs;
+  if (s < 1) s = 1;
+  if (s > 1024) s = 1024;
+  return (int)s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const float* B,
+                 long ldb, int b_nk, float* C, long ldc, int c_mode, int M, int N, int K, int gh, int gw, int cs,
+                 const float* bias, const float* R, const float* rscale, float* pre, nbp_stream_t s) {
+  NBP_REQUIRE(A && B && C && M > 0 && N > 0 && K > 0, "nbp_gemm_f32: null pointer or empty shape");
+  NBP_REQUIRE(K % 4 == 0 && N % 4 == 0, "nbp_gemm_f32: K and N must be multiples of 4 (K=%d N=%d)", K, N);
+  NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && c_mode >= 0 && c_mode <= 1, "nbp_gemm_f32: mode");
+  NBP_REQUIRE(a_mode != AM_SCALE || (a_scale && rows_per_img > 0), "nbp_gemm_f32: a_scale");
+  NBP_REQUIRE((a_mode != AM_S2D && c_mode != CM_D2S) || (gh > 0 && gw > 0 && cs > 0 && cs % 4 == 0),
+              "nbp_gemm_f32: s2d geometry");
+  NBP_REQUIRE(a_mode != AM_S2D || K == 4 * cs, "nbp_gemm_f32: S2D needs K == 4*cs");
+  NBP_REQUIRE(c_mode != CM_D2S || N == 4 * cs, "nbp_gemm_f32: D2S needs N == 4*cs");
+  NBP_REQUIRE(a_mode == AM_S2D || lda % 4 == 0, "nbp_gemm_f32: lda alignment");
+  GemmP p{A, lda, a_scale, rows_per_img, B, ldb, C, ldc, M, N, K, gh, gw, cs, bias, R, rscale, pre};
+  hipStream_t st = S(s);
+  if (b_nk) {
+    if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch_tiles<true, AM_PLAIN, CM_PLAIN>(p, st);
+    else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch_tiles<true, AM_SCALE, CM_PLAIN>(p, st);
+    else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch_tiles<true, AM_S2D, CM_PLAIN>(p, st);
+    else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch_tiles<true, AM_PLAIN, CM_D2S>(p, st);
+    else { set_error("nbp_gemm_f32: unsupported NK mode combination"); return NBP_ERR_ARG; }
+  } else {
+    if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch_tiles<false, AM_PLAIN, CM_PLAIN>(p, st);
+    else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch_tiles<false, AM_PLAIN, CM_D2S>(p, st);
+    else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch_tiles<false, AM_S2D, CM_PLAIN>(p, st);
+    else { set_error("nbp_gemm_f32: unsupported KN mode combination"); return NBP_ERR_ARG; }
+  }
+  return check_launch("gemm_f32");
+}
+
+size_t nbp_wgrad_workspace_floats(int M, int N, int K) {
+  const int S_ = wgrad_splits(M, N, K);
+  return (size_t)S_ * N * K + (size_t)S_ * N;
+}
+
+int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx, int x_mode, const float* x_scale,
+                  int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
+                  float* ws, size_t ws_floats, nbp_stream_t s) {
+  NBP_REQUIRE(G && X && dW && ws && M > 0 && N > 0 && K > 0, "nbp_wgrad_f32: null pointer or empty shape");
+  NBP_REQUIRE(N % 4 == 0 && K % 4 == 0, "nbp_wgrad_f32: N, K multiples of 4");
+  NBP_REQUIRE((g_mode == AM_PLAIN || g_mode == AM_S2D) && x_mode >= 0 && x_mode <= 2, "nbp_wgrad_f32: mode");
+  NBP_REQUIRE(g_mode != AM_S2D || (N == 4 * cs_g && gh > 0 && gw > 0), "nbp_wgrad_f32: G s2d geometry");
+  NBP_REQUIRE(x_mode != AM_S2D || (K == 4 * cs_x && gh > 0 && gw > 0), "nbp_wgrad_f32: X s2d geometry");
+  NBP_REQUIRE(x_mode != AM_SCALE || (x_scale && rows_per_img > 0), "nbp_wgrad_f32: x_scale");
+  const int S_ = wgrad_splits(M, N, K);
+  NBP_REQUIRE(ws_floats >= (size_t)S_ * N * K + (size_t)S_ * N, "nbp_wgrad_f32: workspace too small");
+  int chunk = cdiv(M, S_);
+  chunk = cdiv(chunk, 32) * 32;
+  float* slab = ws;
+  float* slab_b = db ? ws + (size_t)S_ * N * K : nullptr;
+  WgradP p{G, ldg, X, ldx, x_scale, rows_per_img, M, N, K, gh, gw, cs_g, cs_x, slab, slab_b, chunk};
+  dim3 grid(cdiv(N, 64), cdiv(K, 64), S_);
+  hipStream_t st = S(s);
+  if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
+  else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_f32_kernel<AM_PLAIN, AM_SCALE><<<grid, 256, 0, st>>>(p);
+  else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_f32_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
+  else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);
+  else { set_error("nbp_wgrad_f32: unsupported mode combination"); return NBP_ERR_ARG; }
+  const long L = (long)N * K;
+  reduce_slab_kernel<<<cdiv(L, 256) > 2048 ? 2048 : cdiv(L, 256), 256, 0, st>>>(slab, S_, L, dW);
+  if (db) reduce_slab_kernel<<<cdiv(N, 256), 256, 0, st>>>(slab_b, S_, N, db);
+  return check_launch("wgrad_f32");
+}
+
+int nbp_reduce_slab(const float* slab, int S_, long L, float* out, nbp_stream_t s) {
+  NBP_REQUIRE(slab && out && S_ > 0 && L > 0, "nbp_reduce_slab: bad args");
+  reduce_slab_kernel<<<cdiv(L, 256) > 2048 ? 2048 : cdiv(L, 256), 256, 0, S(s)>>>(slab, S_, L, out);
+  return check_launch("reduce_slab");
+}
+
+}  // extern "C"

@@ -1,0 +1,499 @@
+"""NAFNet (Scenario B) on MI355X: one flat fp32 parameter buffer + an executor over the HIP C-ABI.
+
+Reference: NAFNet_base/basicsr/models/archs/NAFNet_arch.py:22-162 (NAFNet, NAFBlock, SimpleGate) and
+arch_util.py:264-300 (LayerNorm2d).  Same constructor signature, same state_dict keys and tensor shapes
+(checkpoints interchange with the reference); different internals:
+
+* activations are NHWC between the intro and ending convs (channels contiguous for the 1x1 GEMMs, the
+  per-pixel LayerNorm and the depthwise conv);
+* all parameters live in ONE flat fp32 buffer (`self.flat`, the module's only nn.Parameter), laid out in
+  reverse backward order so that gradient buckets for the data-parallel all-reduce are contiguous slices that
+  complete in order; the optimizer, the global-norm clip and the all-reduce all run over that buffer;
+* two weights are stored in the layout their kernels read: downs.i.weight as [2C][kh][kw][C] (the GEMM's K
+  order over a space-to-depth gather) and ups.i.0.weight with its output rows grouped by PixelShuffle
+  sub-position (r1, r2, c').  state_dict()/load_state_dict() convert to and from the reference layout.
+
+The forward/backward executor launches the kernels of include/nbp.h on the current stream and keeps the
+tensors the backward needs in a tape.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import call, query
+
+AM_PLAIN, AM_S2D, AM_SCALE = 0, 1, 2
+CM_PLAIN, CM_D2S = 0, 1
+LN_EPS = 1e-6
+
+
+@dataclass
+class PEntry:
+    key: str
+    ref_shape: Tuple[int, ...]
+    offset: int
+    numel: int
+    kind: str = "plain"  # plain | down | up
+
+
+@dataclass
+class Stage:
+    name: str
+    lo: int  # flat offsets [lo, hi) of the parameters whose gradients this stage completes
+    hi: int
+
+
+def _block_keys(pre: str, c: int):
+    return [(pre + "beta", (1, c, 1, 1)), (pre + "gamma", (1, c, 1, 1)),
+            (pre + "conv1.weight", (2 * c, c, 1, 1)), (pre + "conv1.bias", (2 * c,)),
+            (pre + "conv2.weight", (2 * c, 1, 3, 3)), (pre + "conv2.bias", (2 * c,)),
+            (pre + "conv3.weight", (c, c, 1, 1)), (pre + "conv3.bias", (c,)),
+            (pre + "sca.1.weight", (c, c, 1, 1)), (pre + "sca.1.bias", (c,)),
+            (pre + "conv4.weight", (2 * c, c, 1, 1)), (pre + "conv4.bias", (2 * c,)),
+            (pre + "conv5.weight", (c, c, 1, 1)), (pre + "conv5.bias", (c,)),
+            (pre + "norm1.weight", (c,)), (pre + "norm1.bias", (c,)),
+            (pre + "norm2.weight", (c,)), (pre + "norm2.bias", (c,))]
+
+
+def _ceil_to(v, m):
+    return (v + 3) // 4 * 4 if m == 4 else v
+
+
+class NAFNet(nn.Module):
+    """NAFNet(img_channel=3, width=16, middle_blk_num=1, enc_blk_nums=[], dec_blk_nums=[]) (NAFNet_arch.py:85)."""
+
+    def __init__(self, img_channel=3, width=16, middle_blk_num=1, enc_blk_nums=[], dec_blk_nums=[]):  # noqa: B006
+        super().__init__()
+        if width % 8 or width & (width - 1):
+            raise ValueError("the MI355X NAFNet needs a power-of-two width >= 8 (channel-quad vector kernels)")
+        if len(dec_blk_nums) != len(enc_blk_nums):
+            raise ValueError("enc_blk_nums and dec_blk_nums must have the same length (U-Net skips)")
+        if img_channel > 4:
+            raise ValueError("img_channel <= 4")
+        self.img_channel = img_channel
+        self.width = width
+        self.enc_blk_nums = list(enc_blk_nums)
+        self.middle_blk_num = int(middle_blk_num)
+        self.dec_blk_nums = list(dec_blk_nums)
+        self.padder_size = 2 ** len(self.enc_blk_nums)
+        self._build_layout()
+        self.flat = nn.Parameter(torch.zeros(self.numel, dtype=torch.float32))
+        self._init_reference_like()
+        self.grad_ready_hook: Optional[Callable[[Stage], None]] = None
+
+    # ------------------------------------------------------------------ layout
+    def _build_layout(self):
+        w = self.width
+        # reference registration order (for state_dict key order)
+        ref: List[Tuple[str, Tuple[int, ...]]] = [("intro.weight", (w, self.img_channel, 3, 3)), ("intro.bias", (w,)),
+                                                  ("ending.weight", (self.img_channel, w, 3, 3)),
+                                                  ("ending.bias", (self.img_channel,))]
+        chan = w
+        enc_keys, downs = [], []
+        self.enc_chans = []
+        for i, n in enumerate(self.enc_blk_nums):
+            self.enc_chans.append(chan)
+            for j in range(n):
+                enc_keys += _block_keys(f"encoders.{i}.{j}.", chan)
+            downs += [(f"downs.{i}.weight", (2 * chan, chan, 2, 2)), (f"downs.{i}.bias", (2 * chan,))]
+            chan *= 2
+        self.mid_chan = chan
+        mid_keys = []
+        for j in range(self.middle_blk_num):
+            mid_keys += _block_keys(f"middle_blks.{j}.", chan)
+        dec_keys, ups = [], []
+        self.dec_chans = []
+        for i, n in enumerate(self.dec_blk_nums):
+            ups += [(f"ups.{i}.0.weight", (2 * chan, chan, 1, 1))]
+            chan //= 2
+            self.dec_chans.append(chan)
+            for j in range(n):
+                dec_keys += _block_keys(f"decoders.{i}.{j}.", chan)
+        self.ref_order = [k for k, _ in ref + enc_keys + dec_keys + mid_keys + ups + downs]
+        shapes = dict(ref + enc_keys + dec_keys + mid_keys + ups + downs)
+
+        # flat layout in reverse backward order: ending, decoders (last first), ups, middle, enc/downs, intro
+        # ending.bias (img_channel floats, not a multiple of 4) goes last so no alignment padding is needed and
+        # the flat buffer holds exactly the reference's parameter count
+        groups: List[Tuple[str, List[str]]] = [("ending", ["ending.weight"])]
+        for i in reversed(range(len(self.dec_blk_nums))):
+            for j in reversed(range(self.dec_blk_nums[i])):
+                groups.append((f"decoders.{i}.{j}", [k for k, _ in _block_keys(f"decoders.{i}.{j}.", 1)]))
+            groups.append((f"ups.{i}", [f"ups.{i}.0.weight"]))
+        for j in reversed(range(self.middle_blk_num)):
+            groups.append((f"middle_blks.{j}", [k for k, _ in _block_keys(f"middle_blks.{j}.", 1)]))
+        for i in reversed(range(len(self.enc_blk_nums))):
+            groups.append((f"downs.{i}", [f"downs.{i}.weight", f"downs.{i}.bias"]))
+            for j in reversed(range(self.enc_blk_nums[i])):
+                groups.append((f"encoders.{i}.{j}", [k for k, _ in _block_keys(f"encoders.{i}.{j}.", 1)]))
+        groups.append(("intro", ["intro.weight", "intro.bias", "ending.bias"]))
+        self.entries: Dict[str, PEntry] = OrderedDict()
+        self.stages: Dict[str, Stage] = OrderedDict()
+        off = 0
+        for gname, keys in groups:
+            lo = off
+            for k in keys:
+                shp = shapes[k]
+                n = 1
+                for s in shp:
+                    n *= s
+                kind = "down" if k.startswith("downs.") and k.endswith("weight") else (
+                    "up" if k.startswith("ups.") else "plain")
+                self.entries[k] = PEntry(k, shp, off, n, kind)
+                off += n if k == "ending.bias" else _ceil_to(n, 4)  # 16-byte aligned slices for float4 access
+            self.stages[gname] = Stage(gname, lo, off)
+        self.numel = off
+
+    # reference layout <-> internal layout
+    def _to_internal(self, e: PEntry, t: torch.Tensor) -> torch.Tensor:
+        if e.kind == "down":  # [2C, C, 2, 2] -> [2C, 2, 2, C]
+            return t.permute(0, 2, 3, 1).reshape(-1)
+        if e.kind == "up":  # row n_ref = c'*4 + r1*2 + r2 -> n_int = (r1*2 + r2)*(C/2) + c'
+            n2, c = t.shape[0], t.shape[1]
+            return t.reshape(n2 // 4, 4, c).permute(1, 0, 2).reshape(-1)
+        return t.reshape(-1)
+
+    def _to_reference(self, e: PEntry, flat_slice: torch.Tensor) -> torch.Tensor:
+        if e.kind == "down":
+            o, c = e.ref_shape[0], e.ref_shape[1]
+            return flat_slice.view(o, 2, 2, c).permute(0, 3, 1, 2).contiguous()
+        if e.kind == "up":
+            n2, c = e.ref_shape[0], e.ref_shape[1]
+            return flat_slice.view(4, n2 // 4, c).permute(1, 0, 2).reshape(n2, c, 1, 1).contiguous()
+        return flat_slice.view(e.ref_shape)
+
+    def _slice(self, buf: torch.Tensor, key: str) -> torch.Tensor:
+        e = self.entries[key]
+        return buf[e.offset:e.offset + e.numel]
+
+    def p(self, key: str) -> torch.Tensor:
+        return self._slice(self.flat.data, key)
+
+    @torch.no_grad()
+    def _init_reference_like(self):
+        """torch default init of the reference modules (Conv2d kaiming-uniform(a=sqrt(5)) weights and bias
+        U(+-1/sqrt(fan_in)); LayerNorm2d ones/zeros; beta = gamma = 0, NAFNet_arch.py:56-57)."""
+        for k, e in self.entries.items():
+            leaf = k.rsplit(".", 1)[-1]
+            if leaf in ("beta", "gamma"):
+                v = torch.zeros(e.ref_shape)
+            elif ".norm" in k:
+                v = torch.ones(e.ref_shape) if leaf == "weight" else torch.zeros(e.ref_shape)
+            elif leaf == "weight":
+                fan_in = e.ref_shape[1] * e.ref_shape[2] * e.ref_shape[3]
+                bound = 1.0 / fan_in ** 0.5
+                v = torch.empty(e.ref_shape).uniform_(-bound, bound)
+            else:  # bias: fan_in of the owning conv
+                wk = k[:-4] + "weight"
+                ws = self.entries[wk].ref_shape
+                bound = 1.0 / (ws[1] * ws[2] * ws[3]) ** 0.5
+                v = torch.empty(e.ref_shape).uniform_(-bound, bound)
+            self.flat.data[e.offset:e.offset + e.numel] = self._to_internal(e, v)
+
+    # ------------------------------------------------------------------ state dict in reference form
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        flat = self.flat if keep_vars else self.flat.detach()
+        for k in self.ref_order:
+            e = self.entries[k]
+            destination[prefix + k] = self._to_reference(e, flat[e.offset:e.offset + e.numel])
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        seen = set()
+        with torch.no_grad():
+            for k in self.ref_order:
+                e = self.entries[k]
+                full = prefix + k
+                if full not in state_dict:
+                    missing_keys.append(full)
+                    continue
+                v = state_dict[full]
+                if tuple(v.shape) != e.ref_shape:
+                    error_msgs.append(f"size mismatch for {full}: copying {tuple(v.shape)}, expected {e.ref_shape}")
+                    continue
+                self.flat.data[e.offset:e.offset + e.numel] = self._to_internal(e, v.to(self.flat.device,
+                                                                                        torch.float32))
+                seen.add(full)
+        if strict:
+            for k in state_dict:
+                if k.startswith(prefix) and k not in seen and k[len(prefix):] not in self.entries:
+                    unexpected_keys.append(k)
+
+    # ------------------------------------------------------------------ forward
+    def check_image_size_hw(self, h: int, w: int) -> Tuple[int, int]:
+        ps = self.padder_size
+        return h + (ps - h % ps) % ps, w + (ps - w % ps) % ps
+
+    def forward(self, inp: torch.Tensor) -> torch.Tensor:
+        _lib.require_cuda(inp)
+        if inp.dim() != 4 or inp.shape[1] != self.img_channel:
+            raise ValueError(f"expected [B,{self.img_channel},H,W], got {tuple(inp.shape)}")
+        inp = inp.contiguous()
+        if torch.is_grad_enabled() and (self.flat.requires_grad or inp.requires_grad):
+            return _NAFNetFn.apply(inp, self.flat, self)
+        out, _ = self.exec_forward(inp, save=False)
+        return out
+
+    # The executor.  Every op appends a record to the tape when save=True.
+    def exec_forward(self, x: torch.Tensor, save: bool, flat: Optional[torch.Tensor] = None):
+        P = self.flat.data if flat is None else flat
+        B, Ci, H0, W0 = x.shape
+        Hp, Wp = self.check_image_size_hw(H0, W0)
+        tape: List[tuple] = []
+        w = self.width
+        feat = torch.empty(B, Hp, Wp, w, device=x.device)
+        call("intro_fwd", x, self._slice(P, "intro.weight"), self._slice(P, "intro.bias"), feat, B, Ci, H0, W0, Hp,
+             Wp, w)
+        if save:
+            tape.append(("intro", x, (B, Ci, H0, W0, Hp, Wp, w)))
+        h, wd = Hp, Wp
+        skips = []
+        for i, n in enumerate(self.enc_blk_nums):
+            c = self.enc_chans[i]
+            for j in range(n):
+                feat = self._block_fwd(P, f"encoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None)
+            skips.append(feat)
+            feat = self._down_fwd(P, i, feat, B, h, wd, c, tape if save else None)
+            h, wd = h // 2, wd // 2
+        for j in range(self.middle_blk_num):
+            feat = self._block_fwd(P, f"middle_blks.{j}.", feat, B, h, wd, self.mid_chan, tape if save else None)
+        for i, n in enumerate(self.dec_blk_nums):
+            chan = self.dec_chans[i] * 2
+            feat = self._up_fwd(P, i, feat, skips[::-1][i], B, h, wd, chan, tape if save else None)
+            h, wd = h * 2, wd * 2
+            c = self.dec_chans[i]
+            for j in range(n):
+                feat = self._block_fwd(P, f"decoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None)
+        out = torch.empty(B, Ci, H0, W0, device=x.device)
+        call("ending_fwd", feat, self._slice(P, "ending.weight"), self._slice(P, "ending.bias"), x, out, B, Ci, H0,
+             W0, Hp, Wp, w)
+        if save:
+            tape.append(("ending", feat, (B, Ci, H0, W0, Hp, Wp, w)))
+        return out, tape
+
+    def _block_fwd(self, P, pre, x, B, h, w, c, tape):
+        M = B * h * w
+        dev = x.device
+        E = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        yh1, n1, den1 = E(M, c), E(M, c), E(M)
+        call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), yh1, n1,
+             den1, M, c, LN_EPS)
+        t1 = E(M, 2 * c)
+        call("gemm_f32", n1, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv1.weight"), c, 1, t1, 2 * c, CM_PLAIN,
+             M, 2 * c, c, 0, 0, 0, self._slice(P, pre + "conv1.bias"), None, None, None)
+        chunks = query("dw_chunks", B, h, w, c, 0)
+        t2, g, pool = E(M, 2 * c), E(M, c), E(B * chunks * c)
+        call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2, g,
+             pool, B, h, w, c)
+        mean, a = E(B, c), E(B, c)
+        call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
+             a, B, h * w, c)
+        y, t3 = E(M, c), E(M, c)
+        call("gemm_f32", g, c, AM_SCALE, a, h * w, self._slice(P, pre + "conv3.weight"), c, 1, y, c, CM_PLAIN, M, c,
+             c, 0, 0, 0, self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"), t3)
+        yh2, n2, den2 = E(M, c), E(M, c), E(M)
+        call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), yh2, n2,
+             den2, M, c, LN_EPS)
+        t4 = E(M, 2 * c)
+        call("gemm_f32", n2, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv4.weight"), c, 1, t4, 2 * c, CM_PLAIN,
+             M, 2 * c, c, 0, 0, 0, self._slice(P, pre + "conv4.bias"), None, None, None)
+        g2 = E(M, c)
+        call("sg_fwd", t4, g2, M, c)
+        out, t5 = E(M, c), E(M, c)
+        call("gemm_f32", g2, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv5.weight"), c, 1, out, c, CM_PLAIN, M,
+             c, c, 0, 0, 0, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"), t5)
+        if tape is not None:
+            tape.append(("block", pre, (B, h, w, c), dict(x=x, yh1=yh1, n1=n1, den1=den1, t1=t1, t2=t2, g=g, mean=mean,
+                                                           a=a, t3=t3, yh2=yh2, n2=n2, den2=den2, t4=t4, g2=g2, t5=t5)))
+        return out.view(B, h, w, c)
+
+    def _down_fwd(self, P, i, x, B, h, w, c, tape):
+        ho, wo = h // 2, w // 2
+        M = B * ho * wo
+        out = torch.empty(B, ho, wo, 2 * c, device=x.device)
+        call("gemm_f32", x, 0, AM_S2D, None, 1, self._slice(P, f"downs.{i}.weight"), 4 * c, 1, out, 2 * c, CM_PLAIN,
+             M, 2 * c, 4 * c, ho, wo, c, self._slice(P, f"downs.{i}.bias"), None, None, None)
+        if tape is not None:
+            tape.append(("down", i, (B, h, w, c), x))
+        return out
+
+    def _up_fwd(self, P, i, x, skip, B, h, w, chan, tape):
+        M = B * h * w
+        out = torch.empty(B, 2 * h, 2 * w, chan // 2, device=x.device)
+        call("gemm_f32", x, chan, AM_PLAIN, None, 1, self._slice(P, f"ups.{i}.0.weight"), chan, 1, out, 0, CM_D2S, M,
+             2 * chan, chan, h, w, chan // 2, None, skip, None, None)
+        if tape is not None:
+            tape.append(("up", i, (B, h, w, chan), x))
+        return out
+
+    # ------------------------------------------------------------------ backward
+    def exec_backward(self, tape, dout: torch.Tensor, dflat: torch.Tensor, need_dx: bool,
+                      flat: Optional[torch.Tensor] = None, hook: Optional[Callable[[Stage], None]] = None):
+        """Walk the tape in reverse.  Writes every parameter gradient (exactly once) into dflat, calls
+        hook(stage) as each stage's gradient slice is complete, returns d(input) or None."""
+        P = self.flat.data if flat is None else flat
+        dfeat = None
+        dskips: List[torch.Tensor] = []
+        dx_img = None
+        for rec in reversed(tape):
+            kind = rec[0]
+            if kind == "ending":
+                feat, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
+                dfeat = torch.empty(B, Hp, Wp, w, device=dout.device)
+                ws = torch.empty(query("ending_bwd_workspace_floats", B, Ci, H0, W0, w), device=dout.device)
+                call("ending_bwd", dout, feat, self._slice(P, "ending.weight"), dfeat,
+                     self._slice(dflat, "ending.weight"), self._slice(dflat, "ending.bias"), ws, B, Ci, H0, W0, Hp,
+                     Wp, w)
+                self._stage_done("ending", hook)
+            elif kind == "block":
+                pre, geo, S = rec[1], rec[2], rec[3]
+                dfeat = self._block_bwd(P, dflat, pre, geo, S, dfeat)
+                self._stage_done(pre[:-1], hook)
+            elif kind == "up":
+                i, (B, h, w, chan), x = rec[1], rec[2], rec[3]
+                dskips.append(dfeat)  # d(skip) = d(up output): the skip add is an identity branch
+                M = B * h * w
+                dx = torch.empty(B, h, w, chan, device=dout.device)
+                call("gemm_f32", dfeat, 0, AM_S2D, None, 1, self._slice(P, f"ups.{i}.0.weight"), chan, 0, dx, chan,
+                     CM_PLAIN, M, chan, 2 * chan, h, w, chan // 2, None, None, None, None)
+                self._wgrad(dfeat, 0, AM_S2D, x, chan, AM_PLAIN, None, 1, M, 2 * chan, chan, h, w, chan // 2, 0,
+                            self._slice(dflat, f"ups.{i}.0.weight"), None)
+                self._stage_done(f"ups.{i}", hook)
+                dfeat = dx
+            elif kind == "down":
+                i, (B, h, w, c), x = rec[1], rec[2], rec[3]
+                ho, wo = h // 2, w // 2
+                M = B * ho * wo
+                dskip = dskips.pop()
+                dx = torch.empty(B, h, w, c, device=dout.device)
+                # d enc = D2S(dout . Wd) + d skip
+                call("gemm_f32", dfeat, 2 * c, AM_PLAIN, None, 1, self._slice(P, f"downs.{i}.weight"), 4 * c, 0, dx, 0,
+                     CM_D2S, M, 4 * c, 2 * c, ho, wo, c, None, dskip, None, None)
+                self._wgrad(dfeat, 2 * c, AM_PLAIN, x, 0, AM_S2D, None, 1, M, 2 * c, 4 * c, ho, wo, 0, c,
+                            self._slice(dflat, f"downs.{i}.weight"), self._slice(dflat, f"downs.{i}.bias"))
+                self._stage_done(f"downs.{i}", hook)
+                dfeat = dx
+            elif kind == "intro":
+                x, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
+                ws = torch.empty(query("intro_bwd_workspace_floats", B, Ci, Hp, Wp, w), device=dout.device)
+                if need_dx:
+                    dx_img = torch.empty(B, Ci, H0, W0, device=dout.device)
+                call("intro_bwd", x, dfeat, self._slice(P, "intro.weight"), self._slice(dflat, "intro.weight"),
+                     self._slice(dflat, "intro.bias"), dx_img, ws, B, Ci, H0, W0, Hp, Wp, w)
+                self._stage_done("intro", hook)
+        if need_dx:
+            # global residual x + inp (NAFNet_arch.py:153): d inp += d out
+            call("add", dx_img, dout, dx_img, dx_img.numel())
+        return dx_img
+
+    def _stage_done(self, name, hook):
+        if hook is not None:
+            hook(self.stages[name])
+
+    def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db):
+        n_ws = query("wgrad_workspace_floats", M, N, K)
+        ws = torch.empty(n_ws, device=G.device)
+        call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws, n_ws)
+
+    def _reduce(self, slab, S, L, out):
+        call("reduce_slab", slab, S, L, out)
+
+    def _block_bwd(self, P, dflat, pre, geo, S, dout):
+        B, h, w, c = geo
+        M = B * h * w
+        HW = h * w
+        dev = dout.device
+        E = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        dout = dout.reshape(M, c)
+        # out = y + gamma * t5
+        gs = query("scale_dot_grid", M, c)
+        slab = E(gs * c)
+        dt5 = E(M, c)
+        call("scale_dot", dout, S["t5"], self._slice(P, pre + "gamma"), dt5, slab, M, c)
+        self._reduce(slab, gs, c, self._slice(dflat, pre + "gamma"))
+        # conv5
+        dg2 = E(M, c)
+        call("gemm_f32", dt5, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv5.weight"), c, 0, dg2, c, CM_PLAIN, M,
+             c, c, 0, 0, 0, None, None, None, None)
+        self._wgrad(dt5, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0,
+                    self._slice(dflat, pre + "conv5.weight"), self._slice(dflat, pre + "conv5.bias"))
+        # SimpleGate (FFN)
+        dt4 = E(M, 2 * c)
+        call("sg_bwd", dg2, S["t4"], dt4, M, c)
+        # conv4
+        dn2 = E(M, c)
+        call("gemm_f32", dt4, 2 * c, AM_PLAIN, None, 1, self._slice(P, pre + "conv4.weight"), c, 0, dn2, c, CM_PLAIN,
+             M, c, 2 * c, 0, 0, 0, None, None, None, None)
+        self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
+                    self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
+        # norm2 + residual
+        lg = query("ln_nhwc_grid", M, c)
+        sw, sb = E(lg * c), E(lg * c)
+        dy = E(M, c)
+        call("ln_bwd_nhwc", dn2, S["yh2"], S["den2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb, M, c)
+        self._reduce(sw, lg, c, self._slice(dflat, pre + "norm2.weight"))
+        self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
+        # y = x + beta * t3
+        dt3 = E(M, c)
+        call("scale_dot", dy, S["t3"], self._slice(P, pre + "beta"), dt3, slab, M, c)
+        self._reduce(slab, gs, c, self._slice(dflat, pre + "beta"))
+        # conv3 (input h = g * a)
+        dh = E(M, c)
+        call("gemm_f32", dt3, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv3.weight"), c, 0, dh, c, CM_PLAIN, M,
+             c, c, 0, 0, 0, None, None, None, None)
+        self._wgrad(dt3, c, AM_PLAIN, S["g"], c, AM_SCALE, S["a"], HW, M, c, c, 0, 0, 0, 0,
+                    self._slice(dflat, pre + "conv3.weight"), self._slice(dflat, pre + "conv3.bias"))
+        # SCA
+        chunks = query("dw_chunks", B, h, w, c, 0)
+        da_slab = E(B * chunks * c)
+        call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c)
+        da, ds = E(B, c), E(B, c)
+        call("sca_bwd", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], da, ds,
+             self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
+        dt2 = E(M, 2 * c)
+        call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW)
+        # depthwise conv2
+        dt1 = E(M, 2 * c)
+        ws = E(query("dw_bwd_workspace_floats", B, h, w, c))
+        call("dw_bwd", dt2, S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
+             self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c)
+        # conv1
+        dn1 = E(M, c)
+        call("gemm_f32", dt1, 2 * c, AM_PLAIN, None, 1, self._slice(P, pre + "conv1.weight"), c, 0, dn1, c, CM_PLAIN,
+             M, c, 2 * c, 0, 0, 0, None, None, None, None)
+        self._wgrad(dt1, 2 * c, AM_PLAIN, S["n1"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
+                    self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
+        # norm1 + residual
+        dx = E(M, c)
+        call("ln_bwd_nhwc", dn1, S["yh1"], S["den1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb, M, c)
+        self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
+        self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))
+        return dx.view(B, h, w, c)
+
+
+class _NAFNetFn(torch.autograd.Function):
+    """The whole network as one autograd node: forward and backward run the HIP executor."""
+
+    @staticmethod
+    def forward(ctx, inp, flat, net: NAFNet):
+        out, tape = net.exec_forward(inp, save=True, flat=flat.detach())
+        ctx.tape = tape
+        ctx.net = net
+        ctx.flat = flat.detach()
+        ctx.need_dx = ctx.needs_input_grad[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        net: NAFNet = ctx.net
+        dflat = torch.zeros_like(ctx.flat)
+        dx = net.exec_backward(ctx.tape, dout.contiguous(), dflat, ctx.need_dx, flat=ctx.flat,
+                               hook=net.grad_ready_hook)
+        ctx.tape = None
+        return dx, dflat, None

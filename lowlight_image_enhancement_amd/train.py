@@ -1,0 +1,164 @@
+"""Fused training step on MI355X — the hot path of ImageRestorationModel.optimize_parameters
+(NAFNet_base/basicsr/models/image_restoration_model.py:247-322, fp32 branch :316-320) with the HybridLossPlus term
+wiring of the configs (NewBP_model/losses.py:318-372, configs/colab/sid_newbp_rgb.yml:78-96):
+
+    out = net(lq) ; L = w_l1*L1(out, gt) + w_ssim*SSIM(out01, gt01) + w_phys*Phys_srgb(out01, short01, ratio)
+    backward ; [all-reduce grads / world] ; clip_grad_norm_(0.01) ; AdamW(lr, (0.9, 0.999), wd 0.01)
+
+Everything runs as HIP kernels on the current stream: the executor of nafnet.py, the loss kernels (clamp(0,1) of
+the caller, :298-300, is fused into them), the global-norm clip and AdamW over the flat parameter buffer.  No host
+synchronisation inside a step: loss values stay on the device until `logs()` is read.
+
+Data parallel (one process per GPU, torch.distributed 'nccl' = RCCL): the backward executor reports each stage
+whose gradient slice is complete; stages are packed into ~bucket_mb buckets that are all-reduced asynchronously
+(SUM) while the backward continues, the 1/world average is folded into the clip kernel.  The initial parameters are
+broadcast from rank 0 (the DDP construction broadcast, base_model.py:72-78).
+
+Deliberate differences, all numerically neutral: the `0.0 * sum(p.sum())` term (:306) is omitted (its value and
+gradient are exactly zero for finite parameters); the per-term `_ensure_finite` host syncs (losses.py:298-306)
+become one device-side finiteness flag checked when logs are read; the loss dict is reduced with an all-reduce
+instead of reduce-to-rank-0 (:351).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import call, query
+from .NewBP_model.losses import _ratio_array
+from .NewBP_model.newbp_layer import build_psf_kernels, normalize_kernels
+from .nafnet import NAFNet, Stage
+
+
+class TrueCosineAnnealingLR:
+    """lr(t) = eta_min + (base - eta_min) * (1 + cos(pi * t / T_max)) / 2 (configs .../sid_newbp_rgb.yml:74-77)."""
+
+    def __init__(self, base_lr: float, T_max: int, eta_min: float = 0.0):
+        self.base, self.T, self.eta_min = base_lr, T_max, eta_min
+
+    def __call__(self, t: int) -> float:
+        return self.eta_min + (self.base - self.eta_min) * (1 + math.cos(math.pi * t / self.T)) / 2
+
+
+class NBPTrainer:
+    def __init__(self, net: NAFNet, psf_mode: str = "rgb", psf_spec: str = "B2", w_l1: float = 1.0,
+                 w_ssim: float = 0.0, w_phys: float = 0.1, lr: float = 5e-4, betas=(0.9, 0.999),
+                 weight_decay: float = 0.01, eps: float = 1e-8, max_norm: Optional[float] = 0.01,
+                 scheduler: Optional[TrueCosineAnnealingLR] = None, process_group=None, bucket_mb: float = 25.0):
+        self.net = net
+        dev = net.flat.device
+        self.dev = dev
+        self.kernel = normalize_kernels(build_psf_kernels(psf_mode, psf_spec)).to(dev)
+        self.k_shared = int(psf_mode == "mono")
+        self.w = (float(w_l1), float(w_ssim), float(w_phys))
+        self.up = torch.tensor(self.w, dtype=torch.float32, device=dev)  # upstream gradients of the loss terms
+        self.lr, self.betas, self.wd, self.eps = lr, betas, weight_decay, eps
+        self.max_norm = max_norm if max_norm is not None else 0.0
+        self.scheduler = scheduler
+        n = net.numel
+        self.grad = torch.zeros(n, device=dev)
+        self.exp_avg = torch.zeros(n, device=dev)
+        self.exp_avg_sq = torch.zeros(n, device=dev)
+        self.clip_ws = torch.empty(query("clip_workspace_doubles", n), dtype=torch.float64, device=dev)
+        self.clip_state = torch.zeros(2, device=dev)
+        self.loss_buf = torch.zeros(4, device=dev)  # L1, SSIM, Phys, Total
+        self.finite_flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.t = 0
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.bucket_elems = int(bucket_mb * 1024 * 1024 / 4)
+        self._handles: List = []
+        self._pending_lo: Optional[int] = None
+        self._pending_hi = 0
+        if self.world > 1:
+            dist.broadcast(net.flat.data, src=0, group=process_group)
+
+    # ------------------------------------------------------------------ bucketed all-reduce during backward
+    def _on_stage(self, st: Stage):
+        if self._pending_lo is None:
+            self._pending_lo = st.lo
+        self._pending_hi = st.hi
+        if self._pending_hi - self._pending_lo >= self.bucket_elems:
+            self._flush()
+
+    def _flush(self):
+        if self._pending_lo is None or self._pending_hi <= self._pending_lo:
+            return
+        h = dist.all_reduce(self.grad[self._pending_lo:self._pending_hi], op=dist.ReduceOp.SUM, group=self.pg,
+                            async_op=True)
+        self._handles.append(h)
+        self._pending_lo = None
+
+    # ------------------------------------------------------------------ the step
+    def loss_and_grad(self, lq, gt, short=None, expo_ratio=None):
+        """Forward + loss head + backward into self.grad (no optimizer update)."""
+        net = self.net
+        _lib.require_cuda(lq, gt)
+        lq, gt = lq.contiguous(), gt.contiguous()
+        B, C, H, W = lq.shape
+        out, tape = net.exec_forward(lq, save=True)
+        n = out.numel()
+        wl1, wss, wph = self.w
+        d_out = torch.empty_like(out)
+        tmp = torch.empty_like(out)
+        pix_ws = torch.empty(query("pix_workspace_doubles", n), dtype=torch.float64, device=lq.device)
+        call("pix_loss_fwd", out, gt, n, 0, 0.0, 0, 0, pix_ws, self.loss_buf[0:1])
+        call("pix_loss_bwd", out, gt, n, 0, 0.0, 0, 0, self.up[0:1], d_out)
+        if wss != 0.0:
+            ss_ws = torch.empty(query("ssim_workspace_floats", n), device=lq.device)
+            call("ssim_loss_fwd", out, gt, B, C, H, W, 11, 1.0, 1, 1, ss_ws, self.loss_buf[1:2])
+            call("ssim_loss_bwd", out, gt, B, C, H, W, 1, self.up[1:2], ss_ws, tmp)
+            call("add", d_out, tmp, d_out, n)
+        if wph != 0.0 and short is not None:
+            if expo_ratio is None:  # ones [B,1,1,1] when the batch has no ratio (image_restoration_model.py:281-287)
+                expo_ratio = torch.ones(B, 1, 1, 1, device=lq.device)
+            r, full = _ratio_array(expo_ratio, short)
+            ph_ws = torch.empty(query("phys_l1_workspace_doubles", B, C, H, W), dtype=torch.float64, device=lq.device)
+            sign = torch.empty_like(out)
+            call("phys_l1_fwd", out, short.contiguous(), r, full, self.kernel, self.k_shared, B, C, H, W, 3, 3, 0, 1, 1,
+                 1, ph_ws, self.loss_buf[2:3], sign)
+            call("phys_l1_bwd", sign, out, self.kernel, self.k_shared, self.up[2:3], B, C, H, W, 3, 3, 0, 1, tmp)
+            call("add", d_out, tmp, d_out, n)
+        hook = self._on_stage if self.world > 1 else None
+        net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
+        if self.world > 1:
+            self._flush()
+            for h in self._handles:
+                h.wait()
+            self._handles.clear()
+        return out
+
+    def step(self, lq, gt, short=None, expo_ratio=None):
+        out = self.loss_and_grad(lq, gt, short, expo_ratio)
+        self.t += 1
+        lr = self.scheduler(self.t - 1) if self.scheduler is not None else self.lr
+        call("grad_clip_coef", self.grad, self.grad.numel(), 1.0 / self.world, float(self.max_norm), self.clip_ws,
+             self.clip_state)
+        call("adamw_step", self.net.flat.data, self.grad, self.exp_avg, self.exp_avg_sq, self.grad.numel(),
+             self.clip_state, float(lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
+             self.t)
+        return out
+
+    def logs(self, reduce: bool = True) -> Dict[str, float]:
+        """Loss dict of the last step (host sync), averaged over ranks like reduce_loss_dict (base_model.py:335-360)."""
+        wl1, wss, wph = self.w
+        buf = self.loss_buf.clone()
+        buf[3] = wl1 * buf[0] + wss * buf[1] + wph * buf[2]
+        if reduce and self.world > 1:
+            dist.all_reduce(buf, group=self.pg)
+            buf /= self.world
+        vals = buf.cpu()
+        if not torch.isfinite(vals).all():
+            raise RuntimeError(f"HybridLossPlus detected non-finite values: {vals.tolist()}")
+        out = {"L1_raw": float(vals[0])}
+        if wss:
+            out["SSIM"] = float(vals[1])
+        if wph:
+            out["Phys"] = float(vals[2])
+        out["Total"] = float(vals[3])
+        out["grad_norm"] = float(self.clip_state[0].cpu())
+        return out

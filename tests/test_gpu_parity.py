@@ -1,0 +1,248 @@
+"""GPU parity: the HIP path (through the C-ABI) against fixtures produced by the reference and against the oracle.
+
+Tolerances (BASELINE.json north_star): PSF normalisation bit-exact; fp32 restored image within 1e-4 max-abs;
+loss scalars within 1e-5 relative; gradients within the stated atol/rtol.
+"""
+import json
+import os
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+
+pytestmark = pytest.mark.gpu
+T = torch.from_numpy
+
+
+def close(a, b, atol=1e-6, rtol=1e-5):
+    a = a.detach().cpu().numpy() if torch.is_tensor(a) else np.asarray(a)
+    np.testing.assert_allclose(a, np.asarray(b), atol=atol, rtol=rtol)
+
+
+def C(x, dev):
+    return T(np.ascontiguousarray(x)).to(dev)
+
+
+# ---------------------------------------------------------------- physics branch
+def test_psf_module_bits_and_conv(dev):
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_crosstalk_psf
+    g = golden("psf.npz")
+    for mode, spec in (("mono", "P2"), ("rgb", "B2")):
+        psf = create_crosstalk_psf(mode, spec)
+        assert np.array_equal(psf.kernel.numpy().view(np.uint32), g[f"{mode}_{spec}_kernel"].view(np.uint32))
+        psf = psf.to(dev)
+        x = C(g["x"], dev).requires_grad_(True)
+        y = psf(x)
+        y.backward(C(g["gy"], dev))
+        close(y, g[f"y_{mode}"], atol=1e-6)
+        close(x.grad, g[f"dx_{mode}"], atol=1e-6)
+
+
+def test_phys_srgb_loss_all_ratio_forms(dev):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PhysicalConsistencyLossSRGB, align_exposure_srgb
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_crosstalk_psf
+    g = golden("phys_srgb.npz")
+    ratios = {"float1": 1.0, "float07": 0.7, "t0d": torch.tensor(1.3, device=dev),
+              "t1d": torch.tensor([0.6, 1.0, 1.7], device=dev),
+              "t4d": torch.tensor([0.9, 1.2, 2.5], device=dev).view(3, 1, 1, 1)}
+    for mode, spec in (("mono", "P2"), ("rgb", "B2")):
+        crit = PhysicalConsistencyLossSRGB(create_crosstalk_psf(mode, spec).to(dev))
+        for rk, r in ratios.items():
+            b = C(g["bhat"], dev).requires_grad_(True)
+            loss = crit(b, C(g["a"], dev), r)
+            loss.backward()
+            ref = float(g[f"{mode}_{rk}_loss"])
+            assert abs(loss.item() - ref) <= 1e-5 * abs(ref)
+            close(b.grad, g[f"{mode}_{rk}_grad"], atol=1e-9, rtol=1e-5)
+            close(align_exposure_srgb(C(g["a"], dev), r), g[f"{mode}_{rk}_align"], atol=0, rtol=0)
+
+
+def test_phys_raw_loss(dev):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PhysicsConsistencyLoss
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_layer import build_psf_kernels
+    g = golden("phys_srgb.npz")
+    for name, (mode, spec) in (("mono", ("mono", "P2")), ("rgb", ("rgb", "B2"))):
+        for c in (True, False):
+            crit = PhysicsConsistencyLoss(build_psf_kernels(mode, spec), device=dev, clamp_align=c)
+            b = C(g["bhat"], dev).requires_grad_(True)
+            loss = crit(b, C(g["araw"], dev), C(g["raw_ratio"], dev))
+            loss.backward()
+            ref = float(g[f"raw_{name}_c{int(c)}_loss"])
+            assert abs(loss.item() - ref) <= 1e-5 * abs(ref)
+            close(b.grad, g[f"raw_{name}_c{int(c)}_grad"], atol=1e-9, rtol=1e-5)
+
+
+def test_phys_cons_variant_matrix(dev):
+    from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_raw, phys_cons_srgb
+    g = golden("phys_cons.npz")
+    cases = json.load(open(os.path.join(GOLDEN, "phys_cons_cases.json")))
+    for name in cases:
+        fn, padding, crop, robust, rk, psfk, nn_ = name.split("|")
+        r = g[f"ratio_{rk}"]
+        r = float(r) if r.ndim == 0 else C(r, dev)
+        f = phys_cons_raw if fn == "raw" else phys_cons_srgb
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            m, amap = f(C(g["pred"], dev), C(g["obs"], dev), T(g[psfk]), r, padding=padding, crop=crop,
+                        robust=robust, enforce_nonnegative=bool(int(nn_)), return_map=True, reduction="none",
+                        eps=1e-3 if robust == "charbonnier" else 1e-12)
+        close(m, g["v:" + name], atol=2e-6, rtol=1e-5)
+        close(amap, g["m:" + name], atol=2e-6, rtol=1e-5)
+    for red in ("mean", "sum"):
+        close(phys_cons_srgb(C(g["pred"], dev), C(g["obs"], dev), T(g["psf3"]), 1.4, clamp01=False, reduction=red),
+              g[f"srgb_noclamp_{red}"], atol=2e-6)
+        close(phys_cons_raw(C(g["pred"], dev), C(g["obs"], dev), T(g["psf3"]), 0.9, normalize_psf=False,
+                            reduction=red), g[f"raw_nonorm_{red}"], atol=2e-6)
+
+
+def test_phys_cons_validation_errors(dev):
+    from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_raw
+    x = torch.rand(1, 3, 24, 24, device=dev)
+    with pytest.raises(ValueError):
+        phys_cons_raw(x, x, torch.ones(3, 3, 4, 4), expo_ratio=1.0)
+    with pytest.raises(ValueError):
+        phys_cons_raw(x, x, torch.ones(2, 3, 3, 3), expo_ratio=1.0)
+    with pytest.warns(RuntimeWarning):
+        v = phys_cons_raw(x, x, torch.zeros(3, 3, 3, 3), expo_ratio=1.0)
+    assert np.isfinite(v.item())
+    bad = x.clone()
+    bad[0, 0, 0, 0] = float("nan")
+    with pytest.raises(ValueError):
+        phys_cons_raw(bad, x, torch.ones(3, 3, 3, 3), expo_ratio=1.0)
+
+
+# ---------------------------------------------------------------- loss terms vs the oracle (torch fp32 on the GPU)
+def test_l1_charbonnier_ssim_against_oracle(dev):
+    from lowlight_image_enhancement_amd.NewBP_model import losses as HL
+    from oracle import losses as OL
+    gen = torch.Generator(device=dev).manual_seed(5)
+    a = (torch.rand(2, 3, 37, 29, device=dev, generator=gen) * 1.2 - 0.1)
+    b = torch.rand(2, 3, 37, 29, device=dev, generator=gen)
+    for mine_fn, ref_fn in ((HL.l1_loss, OL.l1), (HL.charbonnier_loss, OL.charbonnier),
+                            (HL.SSIMLoss(), OL.ssim_loss)):
+        x1 = a.clone().requires_grad_(True)
+        x2 = a.clone().requires_grad_(True)
+        l1 = mine_fn(x1, b)
+        l2 = ref_fn(x2, b)
+        l1.backward()
+        l2.backward()
+        assert abs(l1.item() - l2.item()) <= 1e-5 * abs(l2.item()) + 1e-7
+        close(x1.grad, x2.grad.cpu().numpy(), atol=1e-7, rtol=1e-3)
+
+
+# ---------------------------------------------------------------- GEMM / building blocks vs torch fp32
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 32), (4096, 1024, 512), (300, 36, 68), (130, 8, 8)])
+def test_gemm_nt_nn_against_torch(dev, M, N, K):
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=dev, generator=gen)
+    W = torch.randn(N, K, device=dev, generator=gen)
+    bias = torch.randn(N, device=dev, generator=gen)
+    R = torch.randn(M, N, device=dev, generator=gen)
+    sc = torch.randn(N, device=dev, generator=gen)
+    out = torch.empty(M, N, device=dev)
+    pre = torch.empty(M, N, device=dev)
+    call("gemm_f32", A, K, 0, None, 1, W, K, 1, out, N, 0, M, N, K, 0, 0, 0, bias, R, sc, pre)
+    ref_pre = A.double() @ W.double().t() + bias.double()
+    close(pre, ref_pre.cpu().numpy(), atol=1e-4, rtol=1e-5)
+    close(out, (R.double() + sc.double() * ref_pre).cpu().numpy(), atol=1e-4, rtol=1e-5)
+    # NN (dgrad) form: C[M,K] = A2[M,N] . W[N,K]
+    A2 = torch.randn(M, N, device=dev, generator=gen)
+    out2 = torch.empty(M, K, device=dev)
+    call("gemm_f32", A2, N, 0, None, 1, W, K, 0, out2, K, 0, M, K, N, 0, 0, 0, None, None, None, None)
+    close(out2, (A2.double() @ W.double()).cpu().numpy(), atol=1e-4, rtol=1e-5)
+    # wgrad: dW[N][K] = G^T X, db = colsum G
+    from lowlight_image_enhancement_amd._lib import query
+    G = torch.randn(M, N, device=dev, generator=gen)
+    dW = torch.empty(N, K, device=dev)
+    db = torch.empty(N, device=dev)
+    n_ws = query("wgrad_workspace_floats", M, N, K)
+    ws = torch.empty(n_ws, device=dev)
+    call("wgrad_f32", G, N, 0, A, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws)
+    close(dW, (G.double().t() @ A.double()).cpu().numpy(), atol=2e-4, rtol=1e-5)
+    close(db, G.double().sum(0).cpu().numpy(), atol=1e-4, rtol=1e-5)
+
+
+# ---------------------------------------------------------------- the network
+def _load_net(name, cfg, dev):
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    g = golden(name)
+    keys = [str(k) for k in g["keys"]]
+    net = create_newbp_net(in_channels=3, **cfg)
+    if "p:" + keys[0] in g.files:
+        net.load_state_dict({k: T(g["p:" + k]) for k in keys})
+    else:
+        from param_recipe import recipe_state
+        net.load_state_dict(recipe_state([(k, tuple(v.shape)) for k, v in net.state_dict().items()], int(g["seed"])))
+    return g, keys, net.to(dev)
+
+
+@pytest.mark.parametrize("name,width,cfg,mode", [
+    ("nafnet_cfg0.npz", 8, dict(enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]), ("rgb", "B2")),
+    ("nafnet_cfg0_pad.npz", 8, dict(enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]), ("mono", "P2")),
+    ("nafnet_cfg1.npz", 16, dict(enc_blk_nums=[1, 1, 1, 1], middle_blk_num=1, dec_blk_nums=[1, 1, 1, 1]),
+     ("mono", "P2")),
+])
+def test_nafnet_forward_backward_golden(dev, name, width, cfg, mode):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PhysicalConsistencyLossSRGB, l1_loss
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_crosstalk_psf
+    g, keys, net = _load_net(name, dict(width=width, **cfg), dev)
+    lq, gt, r = C(g["lq"], dev), C(g["gt"], dev), C(g["ratio"], dev)
+    out = net(lq)
+    close(out, g["out"], atol=1e-4, rtol=0)
+    L1 = l1_loss(out, gt)
+    phys = PhysicalConsistencyLossSRGB(create_crosstalk_psf(*mode).to(dev))
+    Lp = phys(out.clamp(0, 1), (lq * r).clamp(0, 1), r)
+    (L1 + 0.1 * Lp).backward()
+    assert abs(L1.item() - float(g["L1"])) <= 1e-5 * abs(float(g["L1"]))
+    assert abs(Lp.item() - float(g["Phys"])) <= 1e-5 * abs(float(g["Phys"]))
+    grads = {}
+    for k, e in net.entries.items():
+        grads[k] = net._to_reference(e, net.flat.grad[e.offset:e.offset + e.numel]).cpu()
+    for k in keys:
+        if "g:" + k in g.files:
+            ref = g["g:" + k]
+            scale = max(np.abs(ref).max(), 1e-8)
+            assert np.abs(grads[k].numpy() - ref).max() <= 1e-3 * scale + 1e-7, k
+        else:
+            ref = float(g["gsum:" + k])
+            assert abs(float(grads[k].double().sum()) - ref) <= 1e-3 * (abs(ref) + float(g["gnorm:" + k])) + 1e-7, k
+
+
+def test_train_steps_golden(dev):
+    """Two fused optimize_parameters steps (L1 + 0.1 Phys_srgb, clip 0.01, AdamW) against the reference."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    g = golden("train_steps_cfg0.npz")
+    net = create_newbp_net(in_channels=3, width=8, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1])
+    keys = list(net.state_dict().keys())
+    net.load_state_dict({k: T(g["init:" + k]) for k in keys})
+    net = net.to(dev)
+    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", w_l1=1.0, w_ssim=0.0, w_phys=0.1)
+    for s in range(2):
+        lq, gt = C(g[f"s{s}:lq"], dev), C(g[f"s{s}:gt"], dev)
+        r = torch.ones(2, 1, 1, 1, device=dev)
+        tr.step(lq, gt, (lq * r).clamp(0, 1), r)
+        logs = tr.logs()
+        for k, gk in (("L1_raw", "L1"), ("Phys", "Phys"), ("Total", "total")):
+            ref = float(g[f"s{s}:{gk}"])
+            assert abs(logs[k] - ref) <= 1e-5 * abs(ref), (s, k, logs[k], ref)
+        assert abs(logs["grad_norm"] - float(g[f"s{s}:gradnorm"])) <= 1e-4 * float(g[f"s{s}:gradnorm"])
+        sd = net.state_dict()
+        worst = max((sd[k].cpu() - T(g[f"s{s}:p:{k}"])).abs().max().item() for k in keys)
+        # AdamW moves each weight by ~lr per step; 1e-4 of that is the fp32 reorder budget
+        assert worst < 5e-6, (s, worst)
+
+
+def test_nan_fill_every_grad_written(dev):
+    """The backward executor must write every parameter gradient exactly (no stale/uninitialised slots)."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    net = create_newbp_net(in_channels=3, width=8, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]).to(dev)
+    x = torch.rand(1, 3, 32, 32, device=dev)
+    out, tape = net.exec_forward(x, save=True)
+    dflat = torch.full((net.numel,), float("nan"), device=dev)
+    net.exec_backward(tape, torch.ones_like(out), dflat, need_dx=False)
+    assert torch.isfinite(dflat).all()
