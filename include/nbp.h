@@ -92,8 +92,9 @@ size_t nbp_wgrad_workspace_floats(int M, int N, int K);
 int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx, int x_mode, const float* x_scale,
                   int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
                   float* ws, size_t ws_floats, nbp_stream_t s);
-/* out[i] = sum_{s<S} slab[s*L + i] (fixed order). */
+/* out[i] = sum_{s<S} slab[s*L + i] (fixed order); batched: out[b][i] = scale * sum_s slab[b][s][i]. */
 int nbp_reduce_slab(const float* slab, int S, long L, float* out, nbp_stream_t s);
+int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
 /* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC:
  * writes yhat (normalised, optional), nout = w*yhat + b and den = sqrt(var + eps) per pixel. */

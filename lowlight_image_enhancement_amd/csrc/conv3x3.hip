@@ -9,7 +9,7 @@ using namespace nbp;
 
 namespace {
 
-constexpr int kMaxCin = 4;
+constexpr int kMaxCin = 4;  // img_channel <= 4 (kernels are instantiated for 1..4)
 
 struct Img {
   int B, Cimg, H0, W0;  // image (unpadded)
@@ -18,83 +18,84 @@ struct Img {
 };
 
 // ------------------------------------------------------------------ intro forward
-__global__ void intro_fwd(const float* __restrict__ img, const float* __restrict__ w, const float* __restrict__ bias,
+template <int CI>
+__global__ __launch_bounds__(256) void intro_fwd(const float* __restrict__ img, const float* __restrict__ w, const float* __restrict__ bias,
                           float* __restrict__ out, Img g) {
-  extern __shared__ float wl[];  // [Cf][Cimg*9]
-  const int K = g.Cimg * 9;
+  extern __shared__ float wl[];  // [Cf][CI*9]
+  constexpr int K = CI * 9;
   for (int i = threadIdx.x; i < g.Cf * K; i += blockDim.x) wl[i] = w[i];
   __syncthreads();
   const long total = (long)g.B * g.Hp * g.Wp;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < total; p += (long)gridDim.x * blockDim.x) {
     const int x = p % g.Wp, y = (p / g.Wp) % g.Hp, b = p / ((long)g.Wp * g.Hp);
-    float in[kMaxCin * 9];
+    float in[K];
 #pragma unroll
-    for (int c = 0; c < kMaxCin; ++c) {
-      if (c >= g.Cimg) break;
+    for (int c = 0; c < CI; ++c)
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
         in[c * 9 + t] = (yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
-                            ? img[(((long)b * g.Cimg + c) * g.H0 + yy) * g.W0 + xx] : 0.f;
+                            ? img[(((long)b * CI + c) * g.H0 + yy) * g.W0 + xx] : 0.f;
       }
-    }
     float* op = out + p * g.Cf;
     for (int o = 0; o < g.Cf; o += 4) {
       float r[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float a = bias[o + j];
+        float acc = bias[o + j];
         const float* wr = wl + (o + j) * K;
-        for (int k = 0; k < K; ++k) a = fmaf(wr[k], in[k], a);
-        r[j] = a;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fmaf(wr[k], in[k], acc);
+        r[j] = acc;
       }
       st4(op + o, make_float4(r[0], r[1], r[2], r[3]));
     }
   }
 }
 
-// intro weight gradient: slab[blk][Cf][Cimg*9 + 1] (last column = bias)
-__global__ void intro_bwd_w(const float* __restrict__ img, const float* __restrict__ dout, float* __restrict__ slab,
-                            Img g, long px_per_blk) {
+// intro weight gradient: slab_w[blk][Cf][CI*9], slab_b[blk][Cf]
+template <int CI>
+__global__ __launch_bounds__(256) void intro_bwd_w(const float* __restrict__ img, const float* __restrict__ dout, float* __restrict__ slab_w,
+                            float* __restrict__ slab_b, Img g, long px_per_blk) {
   extern __shared__ float red[];  // [blockDim][4]
+  constexpr int K = CI * 9;
   const int Q = g.Cf / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
-  const int K = g.Cimg * 9;
-  float4 acc[kMaxCin * 9 + 1];
+  float4 acc[K + 1];
 #pragma unroll
-  for (int k = 0; k < kMaxCin * 9 + 1; ++k) acc[k] = f4(0.f);
+  for (int k = 0; k <= K; ++k) acc[k] = f4(0.f);
   const long total = (long)g.B * g.Hp * g.Wp;
   const long p0 = blockIdx.x * px_per_blk, p1 = min(total, p0 + px_per_blk);
   if (pl < PPI) {
     for (long p = p0 + pl; p < p1; p += PPI) {
       const int x = p % g.Wp, y = (p / g.Wp) % g.Hp, b = p / ((long)g.Wp * g.Hp);
       const float4 d = ld4(dout + p * g.Cf + q * 4);
-      acc[kMaxCin * 9] += d;
+      acc[K] += d;
 #pragma unroll
-      for (int c = 0; c < kMaxCin; ++c) {
-        if (c >= g.Cimg) break;
+      for (int c = 0; c < CI; ++c)
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
           const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
           const float v = (yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
-                              ? img[(((long)b * g.Cimg + c) * g.H0 + yy) * g.W0 + xx] : 0.f;
+                              ? img[(((long)b * CI + c) * g.H0 + yy) * g.W0 + xx] : 0.f;
           acc[c * 9 + t] = fma4(d, f4(v), acc[c * 9 + t]);
         }
-      }
     }
   }
-  float* dst = slab + (long)blockIdx.x * g.Cf * (K + 1);
+  float* dw = slab_w + (long)blockIdx.x * g.Cf * K;
+  float* db = slab_b + (long)blockIdx.x * g.Cf;
 #pragma unroll
-  for (int kk = 0; kk < kMaxCin * 9 + 1; ++kk) {
-    if (kk >= K && kk != kMaxCin * 9) continue;  // uniform across the block
-    const int col = kk == kMaxCin * 9 ? K : kk;
+  for (int kk = 0; kk <= K; ++kk) {
     st4(red + tid * 4, acc[kk]);
     __syncthreads();
     if (pl == 0) {
-      float4 s = f4(0.f);
-      for (int i = 0; i < PPI; ++i) s += ld4(red + (i * Q + q) * 4);
+      float4 s4 = f4(0.f);
+      for (int i = 0; i < PPI; ++i) s4 += ld4(red + (i * Q + q) * 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dst[(long)(q * 4 + j) * (K + 1) + col] = get(s, j);
+      for (int j = 0; j < 4; ++j) {
+        if (kk < K) dw[(long)(q * 4 + j) * K + kk] = get(s4, j);
+        else db[q * 4 + j] = get(s4, j);
+      }
     }
     __syncthreads();
   }
@@ -179,16 +180,17 @@ __global__ void ending_bwd_x(const float* __restrict__ dy, const float* __restri
   }
 }
 
-// ending weight gradient: slab[blk][Cimg][Cf][9] then Cimg bias entries
-__global__ void ending_bwd_w(const float* __restrict__ dy, const float* __restrict__ feat, float* __restrict__ slab, Img g,
-                             long px_per_blk) {
+// ending weight gradient: slab_w[blk][CI][Cf][9], slab_b[blk][CI]
+template <int CI>
+__global__ __launch_bounds__(256) void ending_bwd_w(const float* __restrict__ dy, const float* __restrict__ feat, float* __restrict__ slab_w,
+                             float* __restrict__ slab_b, Img g, long px_per_blk) {
   extern __shared__ float red[];  // [blockDim][4]
   const int Q = g.Cf / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
-  float4 acc[kMaxCin][9];
-  float bacc[kMaxCin];
+  float4 acc[CI][9];
+  float bacc[CI];
 #pragma unroll
-  for (int o = 0; o < kMaxCin; ++o) {
+  for (int o = 0; o < CI; ++o) {
     bacc[o] = 0.f;
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[o][t] = f4(0.f);
@@ -198,10 +200,10 @@ __global__ void ending_bwd_w(const float* __restrict__ dy, const float* __restri
   if (pl < PPI) {
     for (long p = p0 + pl; p < p1; p += PPI) {
       const int x = p % g.W0, y = (p / g.W0) % g.H0, b = p / ((long)g.W0 * g.H0);
-      float d[kMaxCin];
+      float d[CI];
 #pragma unroll
-      for (int o = 0; o < kMaxCin; ++o) {
-        d[o] = o < g.Cimg ? dy[(((long)b * g.Cimg + o) * g.H0 + y) * g.W0 + x] : 0.f;
+      for (int o = 0; o < CI; ++o) {
+        d[o] = dy[(((long)b * CI + o) * g.H0 + y) * g.W0 + x];
         bacc[o] += d[o];
       }
 #pragma unroll
@@ -210,64 +212,47 @@ __global__ void ending_bwd_w(const float* __restrict__ dy, const float* __restri
         if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) continue;
         const float4 v = ld4(feat + (((long)b * g.Hp + yy) * g.Wp + xx) * g.Cf + q * 4);
 #pragma unroll
-        for (int o = 0; o < kMaxCin; ++o) acc[o][t] = fma4(v, f4(d[o]), acc[o][t]);
+        for (int o = 0; o < CI; ++o) acc[o][t] = fma4(v, f4(d[o]), acc[o][t]);
       }
     }
   }
-  const long L = (long)g.Cimg * g.Cf * 9 + g.Cimg;
-  float* dst = slab + (long)blockIdx.x * L;
+  float* dw = slab_w + (long)blockIdx.x * CI * g.Cf * 9;
 #pragma unroll
-  for (int o = 0; o < kMaxCin; ++o) {
-    if (o >= g.Cimg) break;
+  for (int o = 0; o < CI; ++o) {
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       st4(red + tid * 4, acc[o][t]);
       __syncthreads();
       if (pl == 0) {
-        float4 s = f4(0.f);
-        for (int i = 0; i < PPI; ++i) s += ld4(red + (i * Q + q) * 4);
+        float4 s4 = f4(0.f);
+        for (int i = 0; i < PPI; ++i) s4 += ld4(red + (i * Q + q) * 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) dst[((long)o * g.Cf + q * 4 + j) * 9 + t] = get(s, j);
+        for (int j = 0; j < 4; ++j) dw[((long)o * g.Cf + q * 4 + j) * 9 + t] = get(s4, j);
       }
       __syncthreads();
     }
   }
-  // bias: every thread holds the same sums for its pixel subset; reduce over pixel lanes (q == 0 lanes only)
+  // bias: lanes with q == 0 hold the pixel-lane sums of every output channel
 #pragma unroll
-  for (int o = 0; o < kMaxCin; ++o) {
-    if (o >= g.Cimg) break;
+  for (int o = 0; o < CI; ++o) {
     red[tid] = (q == 0 && pl < PPI) ? bacc[o] : 0.f;
     __syncthreads();
     if (tid == 0) {
-      float s = 0.f;
-      for (int i = 0; i < PPI; ++i) s += red[i * Q];
-      dst[(long)g.Cimg * g.Cf * 9 + o] = s;
+      float s1 = 0.f;
+      for (int i = 0; i < PPI; ++i) s1 += red[i * Q];
+      slab_b[(long)blockIdx.x * CI + o] = s1;
     }
     __syncthreads();
   }
 }
 
-__global__ void fold_slab_2(const float* __restrict__ slab, int S_, int rows, int cols, float* __restrict__ w,
-                            float* __restrict__ b, int wcols) {
-  // slab rows of (cols) floats: the first wcols go to w[row][..], column wcols goes to b[row]  (intro layout)
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= rows * cols) return;
-  float s = 0.f;
-  for (int k = 0; k < S_; ++k) s += slab[(long)k * rows * cols + e];
-  const int r = e / cols, c = e % cols;
-  if (c < wcols) w[(long)r * wcols + c] = s;
-  else b[r] = s;
-}
-
-__global__ void fold_slab_flat(const float* __restrict__ slab, int S_, long L, long nw, float* __restrict__ w,
-                               float* __restrict__ b) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < L; e += (long)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < S_; ++k) s += slab[(long)k * L + e];
-    if (e < nw) w[e] = s;
-    else b[e - nw] = s;
+#define NBP_DISPATCH_CI(ci, ...)                        \
+  switch (ci) {                                          \
+    case 1: { constexpr int CI = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int CI = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int CI = 3; __VA_ARGS__; } break; \
+    default: { constexpr int CI = 4; __VA_ARGS__; } break; \
   }
-}
 
 int blocks_for(long total, long want_px) {
   long g = (total + want_px - 1) / want_px;
@@ -286,7 +271,8 @@ int nbp_intro_fwd(const float* img, const float* w, const float* bias, float* ou
   Img g{B, Cimg, H0, W0, Hp, Wp, Cf};
   const long total = (long)B * Hp * Wp;
   long grid = (total + 255) / 256;
-  intro_fwd<<<(int)(grid > 4096 ? 4096 : grid), 256, Cf * Cimg * 9 * sizeof(float), S(s)>>>(img, w, bias, out, g);
+  NBP_DISPATCH_CI(Cimg, intro_fwd<CI><<<(int)(grid > 4096 ? 4096 : grid), 256, Cf * Cimg * 9 * sizeof(float), S(s)>>>(
+                            img, w, bias, out, g));
   return check_launch("intro_fwd");
 }
 
@@ -302,9 +288,15 @@ int nbp_intro_bwd(const float* img, const float* dout, const float* w, float* dw
   const long total = (long)B * Hp * Wp;
   const int nb = blocks_for(total, 1024);
   const long ppb = (total + nb - 1) / nb;
-  intro_bwd_w<<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(img, dout, ws, g, ppb);
-  const int cols = Cimg * 9 + 1;
-  fold_slab_2<<<cdiv(Cf * cols, 256), 256, 0, S(s)>>>(ws, nb, Cf, cols, dw, db, Cimg * 9);
+  float* slab_w = ws;
+  float* slab_b = ws + (long)nb * Cf * Cimg * 9;
+  NBP_DISPATCH_CI(Cimg, intro_bwd_w<CI><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(img, dout, slab_w, slab_b, g, ppb));
+  int rc = check_launch("intro_bwd_w");
+  if (rc) return rc;
+  rc = nbp_reduce_slab(slab_w, nb, (long)Cf * Cimg * 9, dw, s);
+  if (rc) return rc;
+  rc = nbp_reduce_slab(slab_b, nb, Cf, db, s);
+  if (rc) return rc;
   if (dimg) {
     const long ti = (long)B * Cimg * H0 * W0;
     long gr = (ti + 255) / 256;
@@ -338,10 +330,14 @@ int nbp_ending_bwd(const float* dy, const float* feat, const float* w, float* df
   const long total = (long)B * H0 * W0;
   const int nb = blocks_for(total, 1024);
   const long ppb = (total + nb - 1) / nb;
-  ending_bwd_w<<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(dy, feat, ws, g, ppb);
-  const long L = (long)Cimg * Cf * 9 + Cimg;
-  fold_slab_flat<<<cdiv(L, 256), 256, 0, S(s)>>>(ws, nb, L, (long)Cimg * Cf * 9, dw, db);
-  return check_launch("ending_bwd");
+  float* slab_w = ws;
+  float* slab_b = ws + (long)nb * Cimg * Cf * 9;
+  NBP_DISPATCH_CI(Cimg, ending_bwd_w<CI><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(dy, feat, slab_w, slab_b, g, ppb));
+  int rc = check_launch("ending_bwd_w");
+  if (rc) return rc;
+  rc = nbp_reduce_slab(slab_w, nb, (long)Cimg * Cf * 9, dw, s);
+  if (rc) return rc;
+  return nbp_reduce_slab(slab_b, nb, Cimg, db, s);
 }
 
 }  // extern "C"

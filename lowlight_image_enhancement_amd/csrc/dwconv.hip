@@ -73,24 +73,16 @@ __global__ void dw_sg_pool_fwd(const float* __restrict__ t1, const float* __rest
   }
 }
 
-// SCA: mean[b][i] = sum_chunks slab / HW ; a[b][o] = bsca[o] + sum_i W[o][i] mean[i]  (one wave per output o)
-__global__ void sca_fwd(const float* __restrict__ pool_slab, int chunks, const float* __restrict__ wsca,
-                        const float* __restrict__ bsca, float* __restrict__ mean_out, float* __restrict__ a_out, int C,
-                        float inv_hw) {
-  extern __shared__ float mean[];
+// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i]  (one wave per output o)
+__global__ void sca_gemv(const float* __restrict__ mean, const float* __restrict__ wsca, const float* __restrict__ bsca,
+                         float* __restrict__ a_out, int C) {
   const int b = blockIdx.y;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < chunks; ++k) s += pool_slab[((long)b * chunks + k) * C + i];
-    mean[i] = s * inv_hw;
-    if (blockIdx.x == 0) mean_out[(long)b * C + i] = s * inv_hw;
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int o0 = blockIdx.x * 64;
+  const float* mb = mean + (long)b * C;
   for (int o = o0 + wv; o < min(C, o0 + 64); o += nw) {
     float acc = 0.f;
-    for (int i = lane; i < C; i += 64) acc = fmaf(wsca[(long)o * C + i], mean[i], acc);
+    for (int i = lane; i < C; i += 64) acc = fmaf(wsca[(long)o * C + i], mb[i], acc);
     acc = wave_sum(acc);
     if (lane == 0) a_out[(long)b * C + o] = acc + bsca[o];
   }
@@ -123,22 +115,17 @@ __global__ void img_chan_dot(const float* __restrict__ x, const float* __restric
   }
 }
 
-// SCA backward, per image: da[b][o] = sum_chunks slab ; ds[b][i] = sum_o W[o][i] da[b][o]
-__global__ void sca_bwd_a(const float* __restrict__ da_slab, int chunks, const float* __restrict__ wsca,
-                          float* __restrict__ da_out, float* __restrict__ ds_out, int C) {
-  extern __shared__ float da[];
+// SCA backward, per image: ds[b][i] = sum_o W[o][i] da[b][o]  (da already reduced over chunks)
+__global__ void sca_bwd_ds(const float* __restrict__ da, const float* __restrict__ wsca, float* __restrict__ ds_out,
+                           int C) {
+  extern __shared__ float dab[];
   const int b = blockIdx.y;
-  for (int o = threadIdx.x; o < C; o += blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < chunks; ++k) s += da_slab[((long)b * chunks + k) * C + o];
-    da[o] = s;
-    if (blockIdx.x == 0) da_out[(long)b * C + o] = s;
-  }
+  for (int o = threadIdx.x; o < C; o += blockDim.x) dab[o] = da[(long)b * C + o];
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < C) {
     float acc = 0.f;
-    for (int o = 0; o < C; ++o) acc = fmaf(wsca[(long)o * C + i], da[o], acc);
+    for (int o = 0; o < C; ++o) acc = fmaf(wsca[(long)o * C + i], dab[o], acc);
     ds_out[(long)b * C + i] = acc;
   }
 }
@@ -179,7 +166,7 @@ __global__ void sca_sg_bwd(const float* __restrict__ dh, const float* __restrict
 // depthwise 3x3 backward on C2 channels: dt1 = sum_t w[t] dt2(p - off_t) ; partial dW[c][t] = sum dt2(p) t1(p+off_t),
 // partial db[c] = sum dt2(p).  slab: [B*chunks][C2][10]
 __global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ t1, const float* __restrict__ wdw,
-                       float* __restrict__ dt1, float* __restrict__ slab, Geo geo) {
+                       float* __restrict__ dt1, float* __restrict__ slab_w, float* __restrict__ slab_b, Geo geo) {
   extern __shared__ float red[];  // [blockDim][4]
   const int C2 = 2 * geo.C, Q = C2 / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
@@ -224,7 +211,9 @@ __global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ 
     }
   }
   // block reduction over pixel lanes sharing quad q, one tap at a time through a [blockDim][4] buffer
-  float* dst = slab + ((long)b * geo.chunks + chunk) * C2 * 10;
+  const long row = (long)b * geo.chunks + chunk;
+  float* dw_dst = slab_w + row * C2 * 9;
+  float* db_dst = slab_b + row * C2;
 #pragma unroll
   for (int t = 0; t < 10; ++t) {
     st4(red + tid * 4, t < 9 ? aw[t] : ab);
@@ -233,21 +222,13 @@ __global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ 
       float4 sum = f4(0.f);
       for (int k = 0; k < PPI; ++k) sum += ld4(red + (k * Q + q) * 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dst[(long)(q * 4 + j) * 10 + t] = get(sum, j);
+      for (int j = 0; j < 4; ++j) {
+        if (t < 9) dw_dst[(long)(q * 4 + j) * 9 + t] = get(sum, j);
+        else db_dst[q * 4 + j] = get(sum, j);
+      }
     }
     __syncthreads();
   }
-}
-
-// fold the [S][C2][10] slab into dW [C2][9] and db [C2]
-__global__ void dw_bwd_reduce(const float* __restrict__ slab, int S_, int C2, float* __restrict__ dw, float* __restrict__ db) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= C2 * 10) return;
-  float s = 0.f;
-  for (int k = 0; k < S_; ++k) s += slab[(long)k * C2 * 10 + e];
-  const int c = e / 10, t = e % 10;
-  if (t < 9) dw[c * 9 + t] = s;
-  else db[c] = s;
 }
 
 int block_for_quads(int Q) {
@@ -298,8 +279,9 @@ int nbp_dw_sg_pool_fwd(const float* t1, const float* wdw, const float* bdw, floa
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s) {
   NBP_REQUIRE(pool_slab && wsca && bsca && mean && a && B > 0 && C > 0 && chunks > 0, "nbp_sca_fwd: bad args");
-  dim3 grid(cdiv(C, 64), B);
-  sca_fwd<<<grid, 256, C * sizeof(float), S(s)>>>(pool_slab, chunks, wsca, bsca, mean, a, C, 1.f / (float)HW);
+  int rc = nbp_reduce_slab_batched(pool_slab, B, chunks, C, 1.f / (float)HW, mean, s);
+  if (rc) return rc;
+  sca_gemv<<<dim3(cdiv(C, 64), B), 256, 0, S(s)>>>(mean, wsca, bsca, a, C);
   return check_launch("sca_fwd");
 }
 
@@ -314,7 +296,9 @@ int nbp_img_chan_dot(const float* x, const float* y, float* slab, int B, int H, 
 int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float* mean, float* da, float* ds, float* dwsca,
                 float* dbsca, int B, int C, nbp_stream_t s) {
   NBP_REQUIRE(da_slab && wsca && mean && da && ds && dwsca && dbsca && B > 0 && C > 0, "nbp_sca_bwd: bad args");
-  sca_bwd_a<<<dim3(cdiv(C, 256), B), 256, C * sizeof(float), S(s)>>>(da_slab, chunks, wsca, da, ds, C);
+  int rc = nbp_reduce_slab_batched(da_slab, B, chunks, C, 1.f, da, s);
+  if (rc) return rc;
+  sca_bwd_ds<<<dim3(cdiv(C, 256), B), 256, C * sizeof(float), S(s)>>>(da, wsca, ds, C);
   const long tot = (long)C * C;
   sca_bwd_b<<<cdiv(tot, 256) > 2048 ? 2048 : cdiv(tot, 256), 256, 0, S(s)>>>(da, mean, B, C, dwsca, dbsca);
   return check_launch("sca_bwd");
@@ -342,9 +326,15 @@ int nbp_dw_bwd(const float* dt2, const float* t1, const float* wdw, float* dt1, 
   long cap = (4L << 20) / (2L * C * 10);
   if (cap > 2048) cap = 2048;
   Geo geo = make_geo(B, H, W, C, Q, blk, cap);
-  dw_bwd<<<dim3(geo.chunks, B), blk, (size_t)blk * 4 * sizeof(float), S(s)>>>(dt2, t1, wdw, dt1, ws, geo);
-  dw_bwd_reduce<<<cdiv(2 * C * 10, 256), 256, 0, S(s)>>>(ws, B * geo.chunks, 2 * C, dwdw, dbdw);
-  return check_launch("dw_bwd");
+  const long nrow = (long)B * geo.chunks;
+  float* slab_w = ws;
+  float* slab_b = ws + nrow * 2 * C * 9;
+  dw_bwd<<<dim3(geo.chunks, B), blk, (size_t)blk * 4 * sizeof(float), S(s)>>>(dt2, t1, wdw, dt1, slab_w, slab_b, geo);
+  int rc = check_launch("dw_bwd");
+  if (rc) return rc;
+  rc = nbp_reduce_slab(slab_w, (int)nrow, 2L * C * 9, dwdw, s);
+  if (rc) return rc;
+  return nbp_reduce_slab(slab_b, (int)nrow, 2L * C, dbdw, s);
 }
 
 }  // extern "C"

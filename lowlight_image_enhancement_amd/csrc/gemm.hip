@@ -263,12 +263,42 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
 
-// out[i] = sum_{s < S} slab[s * L + i]  (fixed order: bitwise reproducible)
-__global__ void reduce_slab_kernel(const float* __restrict__ slab, int S, long L, float* __restrict__ out) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < L; i += (long)gridDim.x * blockDim.x) {
-    float a = 0.f;
-    for (int s = 0; s < S; ++s) a += slab[(long)s * L + i];
-    out[i] = a;
+// out[b][i] = scale * sum_{s < S} slab[b][s][i].  TY row-lanes per column, each summing a fixed strided subset of
+// rows with 4 independent accumulators, then a fixed-order combine: bitwise reproducible, latency-tolerant.
+template <int TY>
+__global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, int S, long L, float scale,
+                                                          float* __restrict__ out) {
+  constexpr int TX = 256 / TY;
+  __shared__ float red[TY][TX + 1];
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const long col = (long)blockIdx.x * TX + tx;
+  const float* base = slab + (long)blockIdx.y * S * L;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < L) {
+    int s = ty;
+    for (; s + 3 * TY < S; s += 4 * TY) {
+      a0 += base[(long)s * L + col];
+      a1 += base[(long)(s + TY) * L + col];
+      a2 += base[(long)(s + 2 * TY) * L + col];
+      a3 += base[(long)(s + 3 * TY) * L + col];
+    }
+    for (; s < S; s += TY) a0 += base[(long)s * L + col];
+  }
+  red[ty][tx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (ty == 0 && col < L) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < TY; ++k) t += red[k][tx];
+    out[(long)blockIdx.y * L + col] = t * scale;
+  }
+}
+
+void launch_reduce(const float* slab, int batch, int S, long L, float scale, float* out, hipStream_t st) {
+  if (L < 4096 && S >= 64) {
+    reduce_slab_kernel<16><<<dim3(cdiv(L, 16), batch), 256, 0, st>>>(slab, S, L, scale, out);
+  } else {
+    reduce_slab_kernel<4><<<dim3(cdiv(L, 64), batch), 256, 0, st>>>(slab, S, L, scale, out);
   }
 }
 
@@ -360,16 +390,21 @@ int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx
   else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_f32_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
   else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);
   else { set_error("nbp_wgrad_f32: unsupported mode combination"); return NBP_ERR_ARG; }
-  const long L = (long)N * K;
-  reduce_slab_kernel<<<cdiv(L, 256) > 2048 ? 2048 : cdiv(L, 256), 256, 0, st>>>(slab, S_, L, dW);
-  if (db) reduce_slab_kernel<<<cdiv(N, 256), 256, 0, st>>>(slab_b, S_, N, db);
+  launch_reduce(slab, 1, S_, (long)N * K, 1.f, dW, st);
+  if (db) launch_reduce(slab_b, 1, S_, N, 1.f, db, st);
   return check_launch("wgrad_f32");
 }
 
 int nbp_reduce_slab(const float* slab, int S_, long L, float* out, nbp_stream_t s) {
   NBP_REQUIRE(slab && out && S_ > 0 && L > 0, "nbp_reduce_slab: bad args");
-  reduce_slab_kernel<<<cdiv(L, 256) > 2048 ? 2048 : cdiv(L, 256), 256, 0, S(s)>>>(slab, S_, L, out);
+  launch_reduce(slab, 1, S_, L, 1.f, out, S(s));
   return check_launch("reduce_slab");
+}
+
+int nbp_reduce_slab_batched(const float* slab, int batch, int S_, long L, float scale, float* out, nbp_stream_t s) {
+  NBP_REQUIRE(slab && out && batch > 0 && batch <= 65535 && S_ > 0 && L > 0, "nbp_reduce_slab_batched: bad args");
+  launch_reduce(slab, batch, S_, L, scale, out, S(s));
+  return check_launch("reduce_slab_batched");
 }
 
 }  // extern "C"

@@ -36,12 +36,12 @@ def _filter2d_reflect(x, k1d):
     C = x.shape[1]
     p = ks // 2
     xp = F.pad(x, (p, p, p, p), mode="reflect")
-    return F.conv2d(xp, k2.expand(C, 1, ks, ks).to(x.dtype), groups=C)
+    return F.conv2d(xp, k2.expand(C, 1, ks, ks).to(x.dtype).to(x.device), groups=C)
 
 
 def ssim_map(img1, img2, window_size=11, max_val=1.0, eps=1e-12):
     """kornia.metrics.ssim (0.6.12): C1=(0.01L)^2, C2=(0.03L)^2, num/(den+eps)."""
-    k = gaussian1d(window_size, 1.5)
+    k = gaussian1d(window_size, 1.5).to(img1.device)
     C1 = (0.01 * max_val) ** 2
     C2 = (0.03 * max_val) ** 2
     mu1 = _filter2d_reflect(img1, k)
