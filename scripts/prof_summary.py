@@ -1,0 +1,12 @@
+"""Summarise a rocprofv3 kernel_stats.csv per training step: python scripts/prof_summary.py <csv> <steps>."""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+print(f"total {tot / 1e6 / steps:.2f} ms/step over {len(rows)} kernels")
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:int(sys.argv[3]) if len(sys.argv) > 3 else 30]:
+    name = r["Name"].replace("(anonymous namespace)::", "")
+    print(f"{float(r['TotalDurationNs']) / 1e6 / steps:8.2f} ms {float(r['Percentage']):6.2f}% "
+          f"calls/step={int(r['Calls']) / steps:6.1f} avg={float(r['AverageNs']) / 1e3:8.1f}us  {name[:110]}")
