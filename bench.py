@@ -33,6 +33,7 @@ CFG = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=
 BATCH, IMG = 16, 256
 W_L1, W_SSIM, W_PHYS = 1.0, 0.05, 0.1
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak
 HBM_PEAK_GBPS = 8000.0
 
 
@@ -90,6 +91,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="bf16: bf16 MFMA operands + fp32 accumulation (the reference's AMP training); "
+                         "fp32: fp32 everywhere (parity mode)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -108,6 +112,7 @@ def main():
     net = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **CFG)
     init_sd = {k: v.clone() for k, v in net.state_dict().items()}
     net = net.to(dev)
+    net.precision = args.precision
     tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", w_l1=W_L1, w_ssim=W_SSIM, w_phys=W_PHYS)
     g = torch.Generator(device=dev).manual_seed(0 + rank)
     lq = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
@@ -120,14 +125,17 @@ def main():
     logs_warm = tr.logs()
 
     # live per-kernel timing (HIP events on the launch stream) for the timed steps
-    prof = {"gemm_f32": [], "wgrad_f32": []}
-
     def mk(name, fl):
         def cb(a, e0, e1):
             prof[name].append((fl(a), e0, e1))
         return cb
 
-    _lib.PROFILE["gemm_f32"] = mk("gemm_f32", lambda a: 2.0 * a[11] * a[12] * a[13])
+    gemm_name = "gemm_f32" if args.precision == "fp32" else "gemm_bf16"
+    prof = {gemm_name: [], "wgrad_f32": []}
+    if args.precision == "fp32":
+        _lib.PROFILE["gemm_f32"] = mk("gemm_f32", lambda a: 2.0 * a[11] * a[12] * a[13])
+    else:
+        _lib.PROFILE["gemm_bf16"] = mk("gemm_bf16", lambda a: 2.0 * a[12] * a[13] * a[14])
     _lib.PROFILE["wgrad_f32"] = mk("wgrad_f32", lambda a: 2.0 * a[8] * a[9] * a[10])
     blk_events = []
     orig_fwd, orig_bwd = net._block_fwd, net._block_bwd
@@ -188,13 +196,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.precision if args.precision == "bf16" else "f32",
             "data": "synthetic (U[0,1) sRGB, expo_ratio 1, torch default init, seed 0+rank)",
             "config": {"workload": "cfg2: NAFNet w32 enc[2,2,4,8] mid12 dec[2,2,2,2] (29.16M), rgb/B2 PSF, "
                                    "bs16/GPU 256x256, L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW",
                        "global_batch": BATCH * world, "image": IMG, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
+                         "peak": BF16_PEAK_TFLOPS if dom == "gemm_bf16" else FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s",
+                         "frac": round(achieved / (BF16_PEAK_TFLOPS if dom == "gemm_bf16" else FP32_PEAK_TFLOPS), 4),
+                         "traffic": None,
                          "launches_per_step": nl // args.steps,
                          "ms_per_step": round(ms / args.steps, 3),
                          "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in classes.items()}},

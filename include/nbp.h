@@ -87,6 +87,15 @@ int nbp_all_finite(const float* x, long n, int* flag_dev, nbp_stream_t s);
 int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const float* B,
                  long ldb, int b_nk, float* C, long ldc, int c_mode, int M, int N, int K, int gh, int gw, int cs,
                  const float* bias, const float* R, const float* rscale, float* pre, nbp_stream_t s);
+/* bf16-operand MFMA variant (perf mode; AMP-equivalent operands, fp32 accumulate): C = A . Bw^T, Bw bf16 [N][ldb];
+ * a_dtype / c_dtype: 0 fp32, 1 bf16 storage of A and of C/R/pre.  Same a_mode/c_mode/epilogue as nbp_gemm_f32;
+ * dgrads pass the transposed weight copy.  K, ldb multiples of 8; S2D/D2S need cs % 8 == 0. */
+int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, int a_dtype,
+                  const void* Bw, long ldb, void* C, long ldc, int c_mode, int c_dtype, int M, int N, int K, int gh,
+                  int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s);
+/* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols} (int64, device) out_t[offset..] =
+ * bf16(flat matrix)^T. */
+int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);
 /* weight gradient dW[n][k] = sum_m G(m,n) X(m,k) (+ db[n] = sum_m G(m,n)): split over M, fixed-order slab reduce. */
 size_t nbp_wgrad_workspace_floats(int M, int N, int K);
 int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx, int x_mode, const float* x_scale,

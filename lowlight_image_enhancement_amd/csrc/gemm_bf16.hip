@@ -1,0 +1,296 @@
+// bf16-operand MFMA GEMM (perf mode): C = A(M,K) . W(N,K)^T with fp32 accumulation, v_mfma_f32_32x32x16_bf16.
+// The reference trains under AMP (image_restoration_model.py:255, GradScaler :104-106): its convs take half-precision
+// operands; here the operands are bf16 (no loss scaling needed: 8-bit exponent), accumulation and epilogue fp32.
+// A may be stored fp32 (converted in the tile loader) or bf16; C/R/pre fp32 or bf16.  Same A/C modes as gemm.hip
+// (space-to-depth gather for the down conv / up-conv dgrad, per-image column scale for SCA, depth-to-space scatter
+// + residual for the up conv).  Weights come from a per-step bf16 copy of the flat parameter buffer; dgrads use
+// the transposed copy so every launch is NT.
+#include <hip/hip_bf16.h>
+
+#include "nbp_common.h"
+
+using namespace nbp;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2 };
+enum { CM_PLAIN = 0, CM_D2S = 1 };
+
+struct GemmPB {
+  const void* A;
+  long lda;
+  const float* a_scale;
+  int rows_per_img;
+  const __bf16* B;
+  long ldb;
+  void* C;
+  long ldc;
+  int M, N, K;
+  int gh, gw, cs;
+  const float* bias;
+  const void* R;
+  const float* rscale;
+  void* pre;
+};
+
+__device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
+  const int per = gh * gw;
+  const int b = m / per, rem = m - b * per;
+  const int i = rem / gw, j = rem - i * gw;
+  const int q = k / cs, c = k - q * cs;
+  const int kh = q >> 1, kw = q & 1;
+  return ((long)(b * 2 * gh + 2 * i + kh) * (2 * gw) + 2 * j + kw) * cs + c;
+}
+
+template <typename T>
+__device__ __forceinline__ float ldf(const void* p, long off) {
+  if constexpr (sizeof(T) == 4) return reinterpret_cast<const float*>(p)[off];
+  else return (float)reinterpret_cast<const __bf16*>(p)[off];
+}
+template <typename T>
+__device__ __forceinline__ void stf(void* p, long off, float v) {
+  if constexpr (sizeof(T) == 4) reinterpret_cast<float*>(p)[off] = v;
+  else reinterpret_cast<__bf16*>(p)[off] = (__bf16)v;
+}
+
+// 8 consecutive elements of A at element offset `off`, optionally scaled, as bf16x8
+template <typename TA, int AMODE>
+__device__ __forceinline__ bf16x8 load8(const void* A, long off, const float* scale) {
+  bf16x8 r;
+  if constexpr (sizeof(TA) == 4) {
+    const float4 a = ld4(reinterpret_cast<const float*>(A) + off);
+    const float4 b = ld4(reinterpret_cast<const float*>(A) + off + 4);
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (AMODE == AM_SCALE) {
+      const float4 s0 = ld4(scale), s1 = ld4(scale + 4);
+      v[0] *= s0.x; v[1] *= s0.y; v[2] *= s0.z; v[3] *= s0.w;
+      v[4] *= s1.x; v[5] *= s1.y; v[6] *= s1.z; v[7] *= s1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+  } else {
+    r = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(A) + off);
+    if (AMODE == AM_SCALE) {
+      const float4 s0 = ld4(scale), s1 = ld4(scale + 4);
+      const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (__bf16)((float)r[j] * s[j]);
+    }
+  }
+  return r;
+}
+
+template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
+  constexpr int BK = 32, LS = 40;  // 80-byte LDS rows: conflict-free 16-byte fragment reads
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int A_IT = BM / 64, B_IT = BN / 64;  // 8-element chunks per thread per K-tile
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * LS];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * LS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int M = p.M, N = p.N, K = p.K;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  bf16x8 ra[A_IT], rb[B_IT];
+  auto load_tiles = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx >> 2, kc = idx & 3;
+      const int m = m0 + r, k = k0 + kc * 8;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      if (m < M && k < K) {
+        long off;
+        if (AMODE == AM_S2D) off = s2d_off(m, k, p.gh, p.gw, p.cs);
+        else off = (long)m * p.lda + k;
+        const float* sc = AMODE == AM_SCALE ? p.a_scale + (long)(m / p.rows_per_img) * K + k : nullptr;
+        v = load8<TA, AMODE>(p.A, off, sc);
+      }
+      ra[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx >> 2, kc = idx & 3;
+      const int n = n0 + r, k = k0 + kc * 8;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      if (n < N && k < K) v = *reinterpret_cast<const bf16x8*>(p.B + (long)n * p.ldb + k);
+      rb[it] = v;
+    }
+  };
+  auto store_tiles = [&]() {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int idx = tid + it * 256;
+      *reinterpret_cast<bf16x8*>(As + (idx >> 2) * LS + (idx & 3) * 8) = ra[it];
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int idx = tid + it * 256;
+      *reinterpret_cast<bf16x8*>(Bs + (idx >> 2) * LS + (idx & 3) * 8) = rb[it];
+    }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  load_tiles(0);
+  store_tiles();
+  __syncthreads();
+  const int arow = wm * (BM / 2) + (lane & 31);
+  const int brow = wn * (BN / 2) + (lane & 31);
+  const int kh = (lane >> 5) * 8;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk) load_tiles((t + 1) * BK);
+#pragma unroll
+    for (int s = 0; s < BK; s += 16) {
+      bf16x8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (arow + i * 32) * LS + s + kh);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (brow + j * 32) * LS + s + kh);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (t + 1 < nk) {
+      store_tiles();
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
+      if (col >= N) continue;
+      const float bcol = p.bias ? p.bias[col] : 0.f;
+      const float scol = p.rscale ? p.rscale[col] : 1.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row >= M) continue;
+        long off;
+        if (CMODE == CM_D2S) off = s2d_off(row, col, p.gh, p.gw, p.cs);
+        else off = (long)row * p.ldc + col;
+        float v = acc[i][j][r] + bcol;
+        if (p.pre) stf<TC>(p.pre, off, v);
+        if (p.R) v = ldf<TC>(p.R, off) + scol * v;
+        stf<TC>(p.C, off, v);
+      }
+    }
+}
+
+// fp32 flat parameters -> bf16 copy (all), plus transposed bf16 copies of the listed [rows][cols] matrices
+__global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, __bf16* __restrict__ dst) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = (__bf16)src[i];
+}
+
+// desc: [ndesc][3] int64 {offset, rows, cols}; block (x: tile index, y: matrix)
+__global__ void transpose_bf16_kernel(const float* __restrict__ src, const long* __restrict__ desc,
+                                      __bf16* __restrict__ dst_t) {
+  __shared__ float tile[32][33];
+  const long off = desc[blockIdx.y * 3], R = desc[blockIdx.y * 3 + 1], Cc = desc[blockIdx.y * 3 + 2];
+  const long tiles_c = (Cc + 31) / 32, ntiles = ((R + 31) / 32) * tiles_c;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const long r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
+    for (int rr = ty; rr < 32; rr += 8) {
+      const long r = r0 + rr, c = c0 + tx;
+      tile[rr][tx] = (r < R && c < Cc) ? src[off + r * Cc + c] : 0.f;
+    }
+    __syncthreads();
+    for (int cc = ty; cc < 32; cc += 8) {
+      const long c = c0 + cc, r = r0 + tx;
+      if (r < R && c < Cc) dst_t[off + c * R + r] = (__bf16)tile[tx][cc];
+    }
+    __syncthreads();
+  }
+}
+
+template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC>
+void launch(const GemmPB& p, hipStream_t st) {
+  dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
+  gemm_bf16_kernel<BM, BN, AMODE, CMODE, TA, TC><<<grid, 256, 0, st>>>(p);
+}
+
+template <int AMODE, int CMODE, typename TA, typename TC>
+void dispatch(const GemmPB& p, hipStream_t st) {
+  const bool bn128 = p.N >= 128;
+  const long tiles128 = (long)cdiv(p.M, 128) * cdiv(p.N, bn128 ? 128 : 64);
+  const bool bm128 = tiles128 >= 1024;
+  if (bm128 && bn128) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
+  else if (bm128) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
+  else if (bn128) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
+  else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
+}
+
+template <typename TA, typename TC>
+int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {
+  if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch<AM_PLAIN, CM_PLAIN, TA, TC>(p, st);
+  else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch<AM_SCALE, CM_PLAIN, TA, TC>(p, st);
+  else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch<AM_S2D, CM_PLAIN, TA, TC>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch<AM_PLAIN, CM_D2S, TA, TC>(p, st);
+  else {
+    set_error("nbp_gemm_bf16: unsupported mode combination");
+    return NBP_ERR_ARG;
+  }
+  return NBP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, int a_dtype,
+                  const void* Bw, long ldb, void* C, long ldc, int c_mode, int c_dtype, int M, int N, int K, int gh,
+                  int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s) {
+  NBP_REQUIRE(A && Bw && C && M > 0 && N > 0 && K > 0, "nbp_gemm_bf16: null pointer or empty shape");
+  NBP_REQUIRE(K % 8 == 0 && N % 4 == 0 && ldb % 8 == 0, "nbp_gemm_bf16: K, ldb multiples of 8, N of 4 (K=%d N=%d)", K, N);
+  NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && c_mode >= 0 && c_mode <= 1, "nbp_gemm_bf16: mode");
+  NBP_REQUIRE((a_dtype == 0 || a_dtype == 1) && (c_dtype == 0 || c_dtype == 1), "nbp_gemm_bf16: dtype");
+  NBP_REQUIRE(a_mode != AM_SCALE || (a_scale && rows_per_img > 0), "nbp_gemm_bf16: a_scale");
+  NBP_REQUIRE((a_mode != AM_S2D && c_mode != CM_D2S) || (gh > 0 && gw > 0 && cs > 0 && cs % 8 == 0),
+              "nbp_gemm_bf16: s2d geometry (cs multiple of 8)");
+  NBP_REQUIRE(a_mode != AM_S2D || K == 4 * cs, "nbp_gemm_bf16: S2D needs K == 4*cs");
+  NBP_REQUIRE(c_mode != CM_D2S || N == 4 * cs, "nbp_gemm_bf16: D2S needs N == 4*cs");
+  NBP_REQUIRE(a_mode == AM_S2D || lda % 8 == 0, "nbp_gemm_bf16: lda alignment");
+  GemmPB p{A, lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb, C, ldc, M, N, K, gh, gw, cs,
+           bias, R, rscale, pre};
+  hipStream_t st = S(s);
+  int rc;
+  if (a_dtype == 0 && c_dtype == 0) rc = dispatch_modes<float, float>(p, a_mode, c_mode, st);
+  else if (a_dtype == 1 && c_dtype == 1) rc = dispatch_modes<__bf16, __bf16>(p, a_mode, c_mode, st);
+  else if (a_dtype == 0 && c_dtype == 1) rc = dispatch_modes<float, __bf16>(p, a_mode, c_mode, st);
+  else rc = dispatch_modes<__bf16, float>(p, a_mode, c_mode, st);
+  if (rc) return rc;
+  return check_launch("gemm_bf16");
+}
+
+int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s) {
+  NBP_REQUIRE(flat && out && n > 0 && (ndesc == 0 || (desc && out_t)) && ndesc <= 65535, "nbp_weights_bf16: bad args");
+  long g = (n + 255) / 256;
+  cvt_bf16_kernel<<<(int)(g > 4096 ? 4096 : g), 256, 0, S(s)>>>(flat, n, reinterpret_cast<__bf16*>(out));
+  if (ndesc > 0)
+    transpose_bf16_kernel<<<dim3(256, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<__bf16*>(out_t));
+  return check_launch("weights_bf16");
+}
+
+}  // extern "C"

@@ -86,6 +86,13 @@ class NAFNet(nn.Module):
         self.flat = nn.Parameter(torch.zeros(self.numel, dtype=torch.float32))
         self._init_reference_like()
         self.grad_ready_hook: Optional[Callable[[Stage], None]] = None
+        # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
+        # (the reference's AMP training, image_restoration_model.py:255), fp32 storage and statistics.
+        self.precision = "fp32"
+        self._tdesc_cpu = torch.tensor([[e.offset, e.ref_shape[0], e.numel // e.ref_shape[0]]
+                                        for k, e in self.entries.items() if self._is_gemm_weight(k)],
+                                       dtype=torch.int64).reshape(-1, 3)
+        self._tdesc = None
 
     # ------------------------------------------------------------------ layout
     def _build_layout(self):
@@ -149,6 +156,33 @@ class NAFNet(nn.Module):
                 off += n if k == "ending.bias" else _ceil_to(n, 4)  # 16-byte aligned slices for float4 access
             self.stages[gname] = Stage(gname, lo, off)
         self.numel = off
+
+    @staticmethod
+    def _is_gemm_weight(k: str) -> bool:
+        return k.endswith(("conv1.weight", "conv3.weight", "conv4.weight", "conv5.weight")) or (
+            k.startswith(("downs.", "ups.")) and k.endswith("weight"))
+
+    def _prep_weights(self, P: torch.Tensor):
+        """bf16 copy of the flat parameters + transposed copies of the GEMM weights (for the dgrads)."""
+        if self._tdesc is None or self._tdesc.device != P.device:
+            self._tdesc = self._tdesc_cpu.to(P.device)
+        wb = torch.empty(self.numel, dtype=torch.bfloat16, device=P.device)
+        wt = torch.empty(self.numel, dtype=torch.bfloat16, device=P.device)
+        call("weights_bf16", P, self.numel, wb, self._tdesc, self._tdesc.shape[0], wt)
+        return wb, wt
+
+    def _mm(self, W, A, lda, amode, ascale, rows, wkey, C, ldc, cmode, M, N, K, gh=0, gw=0, cs=0, bias=None,
+            R=None, rscale=None, pre=None, dgrad=False):
+        """One GEMM launch.  W = (fp32 flat,) or (fp32 flat, bf16 copy, bf16 transposed copy).
+        forward: C[M,N] = A[M,K] . W[N,K]^T ; dgrad: C[M,N] = A[M,K] . W[K,N] (W stored [out=K][in=N])."""
+        if len(W) == 1:
+            Wf = self._slice(W[0], wkey)
+            call("gemm_f32", A, lda, amode, ascale, rows, Wf, N if dgrad else K, 0 if dgrad else 1, C, ldc, cmode,
+                 M, N, K, gh, gw, cs, bias, R, rscale, pre)
+        else:
+            Wb = self._slice(W[2] if dgrad else W[1], wkey)
+            call("gemm_bf16", A, lda, amode, ascale, rows, 0, Wb, K, C, ldc, cmode, 0, M, N, K, gh, gw, cs, bias,
+                 R, rscale, pre)
 
     # reference layout <-> internal layout
     def _to_internal(self, e: PEntry, t: torch.Tensor) -> torch.Tensor:
@@ -246,6 +280,8 @@ class NAFNet(nn.Module):
         B, Ci, H0, W0 = x.shape
         Hp, Wp = self.check_image_size_hw(H0, W0)
         tape: List[tuple] = []
+        Wt = (P,) if self.precision == "fp32" else (P,) + self._prep_weights(P)
+        self._W = Wt
         w = self.width
         feat = torch.empty(B, Hp, Wp, w, device=x.device)
         call("intro_fwd", x, self._slice(P, "intro.weight"), self._slice(P, "intro.bias"), feat, B, Ci, H0, W0, Hp,
@@ -275,6 +311,8 @@ class NAFNet(nn.Module):
              W0, Hp, Wp, w)
         if save:
             tape.append(("ending", feat, (B, Ci, H0, W0, Hp, Wp, w)))
+            tape.append(("weights", Wt))
+        self._W = None
         return out, tape
 
     def _block_fwd(self, P, pre, x, B, h, w, c, tape):
@@ -285,8 +323,8 @@ class NAFNet(nn.Module):
         call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), yh1, n1,
              den1, M, c, LN_EPS)
         t1 = E(M, 2 * c)
-        call("gemm_f32", n1, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv1.weight"), c, 1, t1, 2 * c, CM_PLAIN,
-             M, 2 * c, c, 0, 0, 0, self._slice(P, pre + "conv1.bias"), None, None, None)
+        self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
+                 bias=self._slice(P, pre + "conv1.bias"))
         chunks = query("dw_chunks", B, h, w, c, 0)
         t2, g, pool = E(M, 2 * c), E(M, c), E(B * chunks * c)
         call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2, g,
@@ -295,19 +333,19 @@ class NAFNet(nn.Module):
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
              a, B, h * w, c)
         y, t3 = E(M, c), E(M, c)
-        call("gemm_f32", g, c, AM_SCALE, a, h * w, self._slice(P, pre + "conv3.weight"), c, 1, y, c, CM_PLAIN, M, c,
-             c, 0, 0, 0, self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"), t3)
+        self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
+                 bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"), pre=t3)
         yh2, n2, den2 = E(M, c), E(M, c), E(M)
         call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), yh2, n2,
              den2, M, c, LN_EPS)
         t4 = E(M, 2 * c)
-        call("gemm_f32", n2, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv4.weight"), c, 1, t4, 2 * c, CM_PLAIN,
-             M, 2 * c, c, 0, 0, 0, self._slice(P, pre + "conv4.bias"), None, None, None)
+        self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c, c,
+                 bias=self._slice(P, pre + "conv4.bias"))
         g2 = E(M, c)
         call("sg_fwd", t4, g2, M, c)
         out, t5 = E(M, c), E(M, c)
-        call("gemm_f32", g2, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv5.weight"), c, 1, out, c, CM_PLAIN, M,
-             c, c, 0, 0, 0, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"), t5)
+        self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
+                 bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"), pre=t5)
         if tape is not None:
             tape.append(("block", pre, (B, h, w, c), dict(x=x, yh1=yh1, n1=n1, den1=den1, t1=t1, t2=t2, g=g, mean=mean,
                                                            a=a, t3=t3, yh2=yh2, n2=n2, den2=den2, t4=t4, g2=g2, t5=t5)))
@@ -317,8 +355,8 @@ class NAFNet(nn.Module):
         ho, wo = h // 2, w // 2
         M = B * ho * wo
         out = torch.empty(B, ho, wo, 2 * c, device=x.device)
-        call("gemm_f32", x, 0, AM_S2D, None, 1, self._slice(P, f"downs.{i}.weight"), 4 * c, 1, out, 2 * c, CM_PLAIN,
-             M, 2 * c, 4 * c, ho, wo, c, self._slice(P, f"downs.{i}.bias"), None, None, None)
+        self._mm(self._W, x, 0, AM_S2D, None, 1, f"downs.{i}.weight", out, 2 * c, CM_PLAIN, M, 2 * c, 4 * c, ho, wo,
+                 c, bias=self._slice(P, f"downs.{i}.bias"))
         if tape is not None:
             tape.append(("down", i, (B, h, w, c), x))
         return out
@@ -326,8 +364,8 @@ class NAFNet(nn.Module):
     def _up_fwd(self, P, i, x, skip, B, h, w, chan, tape):
         M = B * h * w
         out = torch.empty(B, 2 * h, 2 * w, chan // 2, device=x.device)
-        call("gemm_f32", x, chan, AM_PLAIN, None, 1, self._slice(P, f"ups.{i}.0.weight"), chan, 1, out, 0, CM_D2S, M,
-             2 * chan, chan, h, w, chan // 2, None, skip, None, None)
+        self._mm(self._W, x, chan, AM_PLAIN, None, 1, f"ups.{i}.0.weight", out, 0, CM_D2S, M, 2 * chan, chan, h, w,
+                 chan // 2, R=skip)
         if tape is not None:
             tape.append(("up", i, (B, h, w, chan), x))
         return out
@@ -338,11 +376,17 @@ class NAFNet(nn.Module):
         """Walk the tape in reverse.  Writes every parameter gradient (exactly once) into dflat, calls
         hook(stage) as each stage's gradient slice is complete, returns d(input) or None."""
         P = self.flat.data if flat is None else flat
+        Wt = (P,)
+        for rec in tape:
+            if rec[0] == "weights":
+                Wt = rec[1]
         dfeat = None
         dskips: List[torch.Tensor] = []
         dx_img = None
         for rec in reversed(tape):
             kind = rec[0]
+            if kind == "weights":
+                continue
             if kind == "ending":
                 feat, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
                 dfeat = torch.empty(B, Hp, Wp, w, device=dout.device)
@@ -353,15 +397,15 @@ class NAFNet(nn.Module):
                 self._stage_done("ending", hook)
             elif kind == "block":
                 pre, geo, S = rec[1], rec[2], rec[3]
-                dfeat = self._block_bwd(P, dflat, pre, geo, S, dfeat)
+                dfeat = self._block_bwd(P, Wt, dflat, pre, geo, S, dfeat)
                 self._stage_done(pre[:-1], hook)
             elif kind == "up":
                 i, (B, h, w, chan), x = rec[1], rec[2], rec[3]
                 dskips.append(dfeat)  # d(skip) = d(up output): the skip add is an identity branch
                 M = B * h * w
                 dx = torch.empty(B, h, w, chan, device=dout.device)
-                call("gemm_f32", dfeat, 0, AM_S2D, None, 1, self._slice(P, f"ups.{i}.0.weight"), chan, 0, dx, chan,
-                     CM_PLAIN, M, chan, 2 * chan, h, w, chan // 2, None, None, None, None)
+                self._mm(Wt, dfeat, 0, AM_S2D, None, 1, f"ups.{i}.0.weight", dx, chan, CM_PLAIN, M, chan, 2 * chan,
+                         h, w, chan // 2, dgrad=True)
                 self._wgrad(dfeat, 0, AM_S2D, x, chan, AM_PLAIN, None, 1, M, 2 * chan, chan, h, w, chan // 2, 0,
                             self._slice(dflat, f"ups.{i}.0.weight"), None)
                 self._stage_done(f"ups.{i}", hook)
@@ -373,8 +417,8 @@ class NAFNet(nn.Module):
                 dskip = dskips.pop()
                 dx = torch.empty(B, h, w, c, device=dout.device)
                 # d enc = D2S(dout . Wd) + d skip
-                call("gemm_f32", dfeat, 2 * c, AM_PLAIN, None, 1, self._slice(P, f"downs.{i}.weight"), 4 * c, 0, dx, 0,
-                     CM_D2S, M, 4 * c, 2 * c, ho, wo, c, None, dskip, None, None)
+                self._mm(Wt, dfeat, 2 * c, AM_PLAIN, None, 1, f"downs.{i}.weight", dx, 0, CM_D2S, M, 4 * c, 2 * c,
+                         ho, wo, c, R=dskip, dgrad=True)
                 self._wgrad(dfeat, 2 * c, AM_PLAIN, x, 0, AM_S2D, None, 1, M, 2 * c, 4 * c, ho, wo, 0, c,
                             self._slice(dflat, f"downs.{i}.weight"), self._slice(dflat, f"downs.{i}.bias"))
                 self._stage_done(f"downs.{i}", hook)
@@ -404,7 +448,7 @@ class NAFNet(nn.Module):
     def _reduce(self, slab, S, L, out):
         call("reduce_slab", slab, S, L, out)
 
-    def _block_bwd(self, P, dflat, pre, geo, S, dout):
+    def _block_bwd(self, P, Wt, dflat, pre, geo, S, dout):
         B, h, w, c = geo
         M = B * h * w
         HW = h * w
@@ -419,8 +463,7 @@ class NAFNet(nn.Module):
         self._reduce(slab, gs, c, self._slice(dflat, pre + "gamma"))
         # conv5
         dg2 = E(M, c)
-        call("gemm_f32", dt5, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv5.weight"), c, 0, dg2, c, CM_PLAIN, M,
-             c, c, 0, 0, 0, None, None, None, None)
+        self._mm(Wt, dt5, c, AM_PLAIN, None, 1, pre + "conv5.weight", dg2, c, CM_PLAIN, M, c, c, dgrad=True)
         self._wgrad(dt5, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv5.weight"), self._slice(dflat, pre + "conv5.bias"))
         # SimpleGate (FFN)
@@ -428,8 +471,7 @@ class NAFNet(nn.Module):
         call("sg_bwd", dg2, S["t4"], dt4, M, c)
         # conv4
         dn2 = E(M, c)
-        call("gemm_f32", dt4, 2 * c, AM_PLAIN, None, 1, self._slice(P, pre + "conv4.weight"), c, 0, dn2, c, CM_PLAIN,
-             M, c, 2 * c, 0, 0, 0, None, None, None, None)
+        self._mm(Wt, dt4, 2 * c, AM_PLAIN, None, 1, pre + "conv4.weight", dn2, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
         # norm2 + residual
@@ -445,8 +487,7 @@ class NAFNet(nn.Module):
         self._reduce(slab, gs, c, self._slice(dflat, pre + "beta"))
         # conv3 (input h = g * a)
         dh = E(M, c)
-        call("gemm_f32", dt3, c, AM_PLAIN, None, 1, self._slice(P, pre + "conv3.weight"), c, 0, dh, c, CM_PLAIN, M,
-             c, c, 0, 0, 0, None, None, None, None)
+        self._mm(Wt, dt3, c, AM_PLAIN, None, 1, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c, dgrad=True)
         self._wgrad(dt3, c, AM_PLAIN, S["g"], c, AM_SCALE, S["a"], HW, M, c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv3.weight"), self._slice(dflat, pre + "conv3.bias"))
         # SCA
@@ -465,8 +506,7 @@ class NAFNet(nn.Module):
              self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c)
         # conv1
         dn1 = E(M, c)
-        call("gemm_f32", dt1, 2 * c, AM_PLAIN, None, 1, self._slice(P, pre + "conv1.weight"), c, 0, dn1, c, CM_PLAIN,
-             M, c, 2 * c, 0, 0, 0, None, None, None, None)
+        self._mm(Wt, dt1, 2 * c, AM_PLAIN, None, 1, pre + "conv1.weight", dn1, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
         self._wgrad(dt1, 2 * c, AM_PLAIN, S["n1"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
         # norm1 + residual

@@ -246,3 +246,47 @@ def test_nan_fill_every_grad_written(dev):
     dflat = torch.full((net.numel,), float("nan"), device=dev)
     net.exec_backward(tape, torch.ones_like(out), dflat, need_dx=False)
     assert torch.isfinite(dflat).all()
+
+
+# ---------------------------------------------------------------- bf16 perf mode
+@pytest.mark.parametrize("M,N,K,amode", [(1000, 64, 32, 0), (4096, 1024, 512, 0), (300, 40, 72, 0), (2048, 64, 64, 2)])
+def test_gemm_bf16_against_torch(dev, M, N, K, amode):
+    """bf16 operands, fp32 accumulate: equals float64 math on the bf16-rounded operands up to fp32 summation."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M + N + K + amode)
+    A = torch.randn(M, K, device=dev, generator=gen)
+    W = torch.randn(N, K, device=dev, generator=gen)
+    bias = torch.randn(N, device=dev, generator=gen)
+    R = torch.randn(M, N, device=dev, generator=gen)
+    sc = torch.randn(N, device=dev, generator=gen)
+    rows = 64
+    ascale = torch.rand(M // rows + 1, K, device=dev, generator=gen) if amode == 2 else None
+    Wb = W.to(torch.bfloat16)
+    out = torch.empty(M, N, device=dev)
+    call("gemm_bf16", A, K, amode, ascale, rows, 0, Wb, K, out, N, 0, 0, M, N, K, 0, 0, 0, bias, R, sc, None)
+    Aeff = A if ascale is None else A * ascale.repeat_interleave(rows, 0)[:M]
+    ref = (Aeff.to(torch.bfloat16).double() @ Wb.double().t() + bias.double()) * sc.double() + R.double()
+    close(out, ref.cpu().numpy(), atol=2e-4 * K ** 0.5, rtol=1e-4)
+    # bf16 in / bf16 out
+    Ab = A.to(torch.bfloat16)
+    outb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    call("gemm_bf16", Ab, K, 0, None, 1, 1, Wb, K, outb, N, 0, 1, M, N, K, 0, 0, 0, None, None, None, None)
+    refb = Ab.double() @ Wb.double().t()
+    close(outb.float(), refb.cpu().numpy(), atol=1e-2 * K ** 0.5, rtol=1e-2)
+
+
+def test_nafnet_bf16_mode_close_to_reference(dev):
+    """Perf mode (bf16 MFMA operands, fp32 accumulate and storage) vs the fp32 reference fixtures: AMP-level
+    agreement (the reference's own GPU path trains under autocast fp16)."""
+    from lowlight_image_enhancement_amd.NewBP_model.losses import l1_loss
+    g, keys, net = _load_net("nafnet_cfg1.npz", dict(width=16, enc_blk_nums=[1, 1, 1, 1], middle_blk_num=1,
+                                                      dec_blk_nums=[1, 1, 1, 1]), dev)
+    net.precision = "bf16"
+    lq, gt = C(g["lq"], dev), C(g["gt"], dev)
+    out = net(lq)
+    err = (out.detach().cpu() - T(g["out"])).abs().max().item()
+    assert err < 3e-2, err
+    L1 = l1_loss(out, gt)
+    L1.backward()
+    assert abs(L1.item() - float(g["L1"])) <= 5e-3 * float(g["L1"])
+    assert torch.isfinite(net.flat.grad).all()
