@@ -16,6 +16,8 @@
  *    network boundary and the loss terms are NCHW, the reference's public layout.
  *  - Scalars produced on the device (losses, norms) are written to device memory; gradients of scalar losses
  *    read the upstream gradient from device memory (`up`), so nothing forces a host sync.
+ *  - `dtype` selects the storage of NHWC activations/activation-gradients: 0 fp32, 1 bf16 (perf mode).  Math,
+ *    statistics, parameters and parameter gradients are fp32 in both.
  */
 #ifndef NBP_H_
 #define NBP_H_
@@ -98,9 +100,9 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);
 /* weight gradient dW[n][k] = sum_m G(m,n) X(m,k) (+ db[n] = sum_m G(m,n)): split over M, fixed-order slab reduce. */
 size_t nbp_wgrad_workspace_floats(int M, int N, int K);
-int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx, int x_mode, const float* x_scale,
+int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, int x_mode, const float* x_scale,
                   int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
-                  float* ws, size_t ws_floats, nbp_stream_t s);
+                  float* ws, size_t ws_floats, int dtype, nbp_stream_t s);
 /* out[i] = sum_{s<S} slab[s*L + i] (fixed order); batched: out[b][i] = scale * sum_s slab[b][s][i]. */
 int nbp_reduce_slab(const float* slab, int S, long L, float* out, nbp_stream_t s);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
@@ -108,12 +110,12 @@ int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float s
 /* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC:
  * writes yhat (normalised, optional), nout = w*yhat + b and den = sqrt(var + eps) per pixel. */
 int nbp_ln_nhwc_grid(long M, int C);
-int nbp_ln_fwd_nhwc(const float* x, const float* w, const float* b, float* yhat, float* nout, float* den, long M, int C,
-                    float eps, nbp_stream_t s);
+int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* yhat, void* nout, float* den, long M, int C,
+                    float eps, int dtype, nbp_stream_t s);
 /* closed-form backward (:277-289) + residual gradient dres; per-block partials of dw/db in slab_w/slab_b
  * ([nbp_ln_nhwc_grid][C] each, fold with nbp_reduce_slab). */
-int nbp_ln_bwd_nhwc(const float* dn, const float* yhat, const float* den, const float* w, const float* dres, float* dx,
-                    float* slab_w, float* slab_b, long M, int C, nbp_stream_t s);
+int nbp_ln_bwd_nhwc(const void* dn, const void* yhat, const float* den, const float* w, const void* dres, void* dx,
+                    float* slab_w, float* slab_b, long M, int C, int dtype, nbp_stream_t s);
 /* NCHW variants for the standalone LayerNorm2d module. */
 int nbp_ln_fwd_nchw(const float* x, const float* w, const float* b, float* y, float* yhat, float* den, int N, int C,
                     long HW, float eps, nbp_stream_t s);
@@ -124,48 +126,48 @@ int nbp_ln_bwd_nchw(const float* dy, const float* yhat, const float* den, const 
 /* NAFBlock spatial branch: conv2 depthwise 3x3 + bias on 2C channels (NAFNet_arch.py:32-33) -> SimpleGate
  * (:22-25) -> AdaptiveAvgPool2d(1) partial sums (:38) in pool_slab [B][chunks][C]. */
 int nbp_dw_chunks(int B, int H, int W, int C, int which);
-int nbp_dw_sg_pool_fwd(const float* t1, const float* wdw, const float* bdw, float* t2, float* g, float* pool_slab, int B,
-                       int H, int W, int C, nbp_stream_t s);
+int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
+                       int H, int W, int C, int dtype, nbp_stream_t s);
 /* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s);
 /* per-image channel sums slab[b][chunk][c] = sum_p x*y (y may be NULL). */
-int nbp_img_chan_dot(const float* x, const float* y, float* slab, int B, int H, int W, int C, nbp_stream_t s);
+int nbp_img_chan_dot(const void* x, const void* y, float* slab, int B, int H, int W, int C, int dtype, nbp_stream_t s);
 /* SCA backward: da, ds = W^T da, dW = da^T mean, db = sum_b da. */
 int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float* mean, float* da, float* ds, float* dwsca,
                 float* dbsca, int B, int C, nbp_stream_t s);
 /* dg = dh*a + ds/HW, then SimpleGate backward into dt2 [M][2C]. */
-int nbp_sca_sg_bwd(const float* dh, const float* a, const float* ds, const float* t2, float* dt2, long M, int C, int HW,
-                   nbp_stream_t s);
+int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* t2, void* dt2, long M, int C, int HW,
+                   int dtype, nbp_stream_t s);
 /* depthwise 3x3 backward: dt1, dW [2C][9], db [2C]. */
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C);
-int nbp_dw_bwd(const float* dt2, const float* t1, const float* wdw, float* dt1, float* dwdw, float* dbdw, float* ws,
-               int B, int H, int W, int C, nbp_stream_t s);
+int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws,
+               int B, int H, int W, int C, int dtype, nbp_stream_t s);
 
 /* SimpleGate on the FFN half (NAFNet_arch.py:75): g = t[:C]*t[C:], and its backward. */
-int nbp_sg_fwd(const float* t, float* g, long M, int C, nbp_stream_t s);
-int nbp_sg_bwd(const float* dg, const float* t, float* dt, long M, int C, nbp_stream_t s);
+int nbp_sg_fwd(const void* t, void* g, long M, int C, int dtype, nbp_stream_t s);
+int nbp_sg_bwd(const void* dg, const void* t, void* dt, long M, int C, int dtype, nbp_stream_t s);
 /* layer-scale residual gradients (NAFNet_arch.py:72,80): ds = d*scale, slab partials of sum d*t (dbeta/dgamma). */
 int nbp_scale_dot_grid(long M, int C);
-int nbp_scale_dot(const float* d, const float* t, const float* scale, float* ds, float* slab, long M, int C,
+int nbp_scale_dot(const void* d, const void* t, const float* scale, void* ds, float* slab, long M, int C, int dtype,
                   nbp_stream_t s);
 int nbp_nchw_to_nhwc(const float* x, float* y, int N, int C, long HW, nbp_stream_t s);
 int nbp_nhwc_to_nchw(const float* x, float* y, int N, int C, long HW, nbp_stream_t s);
-int nbp_add(const float* a, const float* b, float* y, long n, nbp_stream_t s);
+int nbp_add(const void* a, const void* b, void* y, long n, int dtype, nbp_stream_t s);
 
 /* intro conv 3x3 (NAFNet_arch.py:88-89,136) on the check_image_size zero-padded grid (:157-162): NCHW image ->
  * NHWC features [B][Hp][Wp][Cf]; backward gives dW, db and (optional) d image. */
-int nbp_intro_fwd(const float* img, const float* w, const float* bias, float* out, int B, int Cimg, int H0, int W0,
-                  int Hp, int Wp, int Cf, nbp_stream_t s);
+int nbp_intro_fwd(const float* img, const float* w, const float* bias, void* out, int B, int Cimg, int H0, int W0,
+                  int Hp, int Wp, int Cf, int dtype, nbp_stream_t s);
 size_t nbp_intro_bwd_workspace_floats(int B, int Cimg, int Hp, int Wp, int Cf);
-int nbp_intro_bwd(const float* img, const float* dout, const float* w, float* dw, float* db, float* dimg, float* ws,
-                  int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s);
+int nbp_intro_bwd(const float* img, const void* dout, const float* w, float* dw, float* db, float* dimg, float* ws,
+                  int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, int dtype, nbp_stream_t s);
 /* ending conv 3x3 + global residual + crop (NAFNet_arch.py:90-91,152-155): NHWC features -> NCHW image. */
-int nbp_ending_fwd(const float* feat, const float* w, const float* bias, const float* img, float* out, int B, int Cimg,
-                   int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s);
+int nbp_ending_fwd(const void* feat, const float* w, const float* bias, const float* img, float* out, int B, int Cimg,
+                   int H0, int W0, int Hp, int Wp, int Cf, int dtype, nbp_stream_t s);
 size_t nbp_ending_bwd_workspace_floats(int B, int Cimg, int H0, int W0, int Cf);
-int nbp_ending_bwd(const float* dy, const float* feat, const float* w, float* dfeat, float* dw, float* db, float* ws,
-                   int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s);
+int nbp_ending_bwd(const float* dy, const void* feat, const float* w, void* dfeat, float* dw, float* db, float* ws,
+                   int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, int dtype, nbp_stream_t s);
 
 /* ------------------------------------------------------------------ HybridLoss terms (NCHW) */
 /* mode 0: nn.L1Loss (NewBP_model/losses.py:249,332); mode 1: Charbonnier sqrt(d^2+eps)

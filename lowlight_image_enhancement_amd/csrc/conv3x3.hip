@@ -18,9 +18,9 @@ struct Img {
 };
 
 // ------------------------------------------------------------------ intro forward
-template <int CI>
-__global__ __launch_bounds__(256) void intro_fwd(const float* __restrict__ img, const float* __restrict__ w, const float* __restrict__ bias,
-                          float* __restrict__ out, Img g) {
+template <int CI, typename T>
+__global__ __launch_bounds__(256) void intro_fwd(const float* __restrict__ img, const float* __restrict__ w,
+                                                 const float* __restrict__ bias, T* __restrict__ out, Img g) {
   extern __shared__ float wl[];  // [Cf][CI*9]
   constexpr int K = CI * 9;
   for (int i = threadIdx.x; i < g.Cf * K; i += blockDim.x) wl[i] = w[i];
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void intro_fwd(const float* __restrict__ img, 
         in[c * 9 + t] = (yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
                             ? img[(((long)b * CI + c) * g.H0 + yy) * g.W0 + xx] : 0.f;
       }
-    float* op = out + p * g.Cf;
+    T* op = out + p * g.Cf;
     for (int o = 0; o < g.Cf; o += 4) {
       float r[4];
 #pragma unroll
@@ -48,14 +48,14 @@ __global__ __launch_bounds__(256) void intro_fwd(const float* __restrict__ img, 
         for (int k = 0; k < K; ++k) acc = fmaf(wr[k], in[k], acc);
         r[j] = acc;
       }
-      st4(op + o, make_float4(r[0], r[1], r[2], r[3]));
+      stq(op + o, make_float4(r[0], r[1], r[2], r[3]));
     }
   }
 }
 
 // intro weight gradient: slab_w[blk][Cf][CI*9], slab_b[blk][Cf]
-template <int CI>
-__global__ __launch_bounds__(256) void intro_bwd_w(const float* __restrict__ img, const float* __restrict__ dout, float* __restrict__ slab_w,
+template <int CI, typename T>
+__global__ __launch_bounds__(256) void intro_bwd_w(const float* __restrict__ img, const T* __restrict__ dout, float* __restrict__ slab_w,
                             float* __restrict__ slab_b, Img g, long px_per_blk) {
   extern __shared__ float red[];  // [blockDim][4]
   constexpr int K = CI * 9;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void intro_bwd_w(const float* __restrict__ img
   if (pl < PPI) {
     for (long p = p0 + pl; p < p1; p += PPI) {
       const int x = p % g.Wp, y = (p / g.Wp) % g.Hp, b = p / ((long)g.Wp * g.Hp);
-      const float4 d = ld4(dout + p * g.Cf + q * 4);
+      const float4 d = ldq(dout + p * g.Cf + q * 4);
       acc[K] += d;
 #pragma unroll
       for (int c = 0; c < CI; ++c)
@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256) void intro_bwd_w(const float* __restrict__ img
 }
 
 // intro input gradient (only when the image requires grad): d img = conv^T over the padded grid, restricted to H0 x W0
-__global__ void intro_bwd_x(const float* __restrict__ dout, const float* __restrict__ w, float* __restrict__ dimg, Img g) {
+template <typename T>
+__global__ void intro_bwd_x(const T* __restrict__ dout, const float* __restrict__ w, float* __restrict__ dimg, Img g) {
   const long total = (long)g.B * g.Cimg * g.H0 * g.W0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int x = i % g.W0, y = (i / g.W0) % g.H0;
@@ -112,8 +113,8 @@ __global__ void intro_bwd_x(const float* __restrict__ dout, const float* __restr
     for (int t = 0; t < 9; ++t) {
       const int yo = y - (t / 3 - 1), xo = x - (t % 3 - 1);
       if (yo < 0 || yo >= g.Hp || xo < 0 || xo >= g.Wp) continue;
-      const float* dp = dout + (((long)b * g.Hp + yo) * g.Wp + xo) * g.Cf;
-      for (int o = 0; o < g.Cf; ++o) a = fmaf(w[((long)o * g.Cimg + c) * 9 + t], dp[o], a);
+      const T* dp = dout + (((long)b * g.Hp + yo) * g.Wp + xo) * g.Cf;
+      for (int o = 0; o < g.Cf; ++o) a = fmaf(w[((long)o * g.Cimg + c) * 9 + t], (float)dp[o], a);
     }
     dimg[i] = a;
   }
@@ -121,7 +122,8 @@ __global__ void intro_bwd_x(const float* __restrict__ dout, const float* __restr
 
 // ------------------------------------------------------------------ ending forward
 // wl layout: [t][Cf][4] with o < Cimg (<= 4) in the last dimension
-__global__ void ending_fwd(const float* __restrict__ feat, const float* __restrict__ w, const float* __restrict__ bias,
+template <typename T>
+__global__ void ending_fwd(const T* __restrict__ feat, const float* __restrict__ w, const float* __restrict__ bias,
                            const float* __restrict__ img, float* __restrict__ out, Img g) {
   extern __shared__ float wl[];
   for (int i = threadIdx.x; i < 9 * g.Cf * 4; i += blockDim.x) {
@@ -136,10 +138,10 @@ __global__ void ending_fwd(const float* __restrict__ feat, const float* __restri
     for (int t = 0; t < 9; ++t) {
       const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
       if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) continue;
-      const float* fp = feat + (((long)b * g.Hp + yy) * g.Wp + xx) * g.Cf;
+      const T* fp = feat + (((long)b * g.Hp + yy) * g.Wp + xx) * g.Cf;
       const float* wt = wl + t * g.Cf * 4;
       for (int c = 0; c < g.Cf; c += 4) {
-        const float4 v = ld4(fp + c);
+        const float4 v = ldq(fp + c);
         acc = fma4(ld4(wt + (c + 0) * 4), f4(v.x), acc);
         acc = fma4(ld4(wt + (c + 1) * 4), f4(v.y), acc);
         acc = fma4(ld4(wt + (c + 2) * 4), f4(v.z), acc);
@@ -154,7 +156,8 @@ __global__ void ending_fwd(const float* __restrict__ feat, const float* __restri
 }
 
 // ending input gradient on the padded grid: dfeat(p)[c] = sum_t sum_o w[o][c][t] dy(p - off_t)[o], dy zero off-crop
-__global__ void ending_bwd_x(const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ dfeat, Img g) {
+template <typename T>
+__global__ void ending_bwd_x(const float* __restrict__ dy, const float* __restrict__ w, T* __restrict__ dfeat, Img g) {
   extern __shared__ float wl[];  // [t][o][Cf]
   for (int i = threadIdx.x; i < 9 * g.Cimg * g.Cf; i += blockDim.x) {
     const int c = i % g.Cf, o = (i / g.Cf) % g.Cimg, t = i / (g.Cf * g.Cimg);
@@ -176,13 +179,13 @@ __global__ void ending_bwd_x(const float* __restrict__ dy, const float* __restri
         acc = fma4(ld4(wl + (t * g.Cimg + o) * g.Cf + q * 4), f4(d), acc);
       }
     }
-    st4(dfeat + p * g.Cf + q * 4, acc);
+    stq(dfeat + p * g.Cf + q * 4, acc);
   }
 }
 
 // ending weight gradient: slab_w[blk][CI][Cf][9], slab_b[blk][CI]
-template <int CI>
-__global__ __launch_bounds__(256) void ending_bwd_w(const float* __restrict__ dy, const float* __restrict__ feat, float* __restrict__ slab_w,
+template <int CI, typename T>
+__global__ __launch_bounds__(256) void ending_bwd_w(const float* __restrict__ dy, const T* __restrict__ feat, float* __restrict__ slab_w,
                              float* __restrict__ slab_b, Img g, long px_per_blk) {
   extern __shared__ float red[];  // [blockDim][4]
   const int Q = g.Cf / 4;
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(256) void ending_bwd_w(const float* __restrict__ dy
       for (int t = 0; t < 9; ++t) {
         const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
         if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) continue;
-        const float4 v = ld4(feat + (((long)b * g.Hp + yy) * g.Wp + xx) * g.Cf + q * 4);
+        const float4 v = ldq(feat + (((long)b * g.Hp + yy) * g.Wp + xx) * g.Cf + q * 4);
 #pragma unroll
         for (int o = 0; o < CI; ++o) acc[o][t] = fma4(v, f4(d[o]), acc[o][t]);
       }
@@ -264,15 +267,16 @@ int blocks_for(long total, long want_px) {
 
 extern "C" {
 
-int nbp_intro_fwd(const float* img, const float* w, const float* bias, float* out, int B, int Cimg, int H0, int W0,
-                  int Hp, int Wp, int Cf, nbp_stream_t s) {
+int nbp_intro_fwd(const float* img, const float* w, const float* bias, void* out, int B, int Cimg, int H0, int W0,
+                  int Hp, int Wp, int Cf, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(img && w && bias && out && B > 0 && Cimg > 0 && Cimg <= kMaxCin && Cf % 4 == 0, "nbp_intro_fwd: bad args");
   NBP_REQUIRE(Hp >= H0 && Wp >= W0, "nbp_intro_fwd: padded grid smaller than image");
   Img g{B, Cimg, H0, W0, Hp, Wp, Cf};
   const long total = (long)B * Hp * Wp;
   long grid = (total + 255) / 256;
-  NBP_DISPATCH_CI(Cimg, intro_fwd<CI><<<(int)(grid > 4096 ? 4096 : grid), 256, Cf * Cimg * 9 * sizeof(float), S(s)>>>(
-                            img, w, bias, out, g));
+  const int gr = (int)(grid > 4096 ? 4096 : grid);
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, intro_fwd<CI, T><<<gr, 256, Cf * Cimg * 9 * sizeof(float), S(s)>>>(
+                                                  img, w, bias, (T*)out, g)));
   return check_launch("intro_fwd");
 }
 
@@ -280,8 +284,8 @@ size_t nbp_intro_bwd_workspace_floats(int B, int Cimg, int Hp, int Wp, int Cf) {
   return (size_t)blocks_for((long)B * Hp * Wp, 1024) * Cf * (Cimg * 9 + 1);
 }
 
-int nbp_intro_bwd(const float* img, const float* dout, const float* w, float* dw, float* db, float* dimg, float* ws,
-                  int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s) {
+int nbp_intro_bwd(const float* img, const void* dout, const float* w, float* dw, float* db, float* dimg, float* ws,
+                  int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(img && dout && w && dw && db && ws && Cimg <= kMaxCin && Cf % 4 == 0 && Cf / 4 <= 256,
               "nbp_intro_bwd: bad args");
   Img g{B, Cimg, H0, W0, Hp, Wp, Cf};
@@ -290,7 +294,8 @@ int nbp_intro_bwd(const float* img, const float* dout, const float* w, float* dw
   const long ppb = (total + nb - 1) / nb;
   float* slab_w = ws;
   float* slab_b = ws + (long)nb * Cf * Cimg * 9;
-  NBP_DISPATCH_CI(Cimg, intro_bwd_w<CI><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(img, dout, slab_w, slab_b, g, ppb));
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, intro_bwd_w<CI, T><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(
+                                                  img, (const T*)dout, slab_w, slab_b, g, ppb)));
   int rc = check_launch("intro_bwd_w");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, nb, (long)Cf * Cimg * 9, dw, s);
@@ -300,18 +305,20 @@ int nbp_intro_bwd(const float* img, const float* dout, const float* w, float* dw
   if (dimg) {
     const long ti = (long)B * Cimg * H0 * W0;
     long gr = (ti + 255) / 256;
-    intro_bwd_x<<<(int)(gr > 4096 ? 4096 : gr), 256, 0, S(s)>>>(dout, w, dimg, g);
+    const int gx = (int)(gr > 4096 ? 4096 : gr);
+    NBP_DISPATCH_T(dtype, intro_bwd_x<T><<<gx, 256, 0, S(s)>>>((const T*)dout, w, dimg, g));
   }
   return check_launch("intro_bwd");
 }
 
-int nbp_ending_fwd(const float* feat, const float* w, const float* bias, const float* img, float* out, int B, int Cimg,
-                   int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s) {
+int nbp_ending_fwd(const void* feat, const float* w, const float* bias, const float* img, float* out, int B, int Cimg,
+                   int H0, int W0, int Hp, int Wp, int Cf, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(feat && w && bias && img && out && Cimg > 0 && Cimg <= kMaxCin && Cf % 4 == 0, "nbp_ending_fwd: bad args");
   Img g{B, Cimg, H0, W0, Hp, Wp, Cf};
   const long total = (long)B * H0 * W0;
   long grid = (total + 255) / 256;
-  ending_fwd<<<(int)(grid > 4096 ? 4096 : grid), 256, 9 * Cf * 4 * sizeof(float), S(s)>>>(feat, w, bias, img, out, g);
+  const int gr = (int)(grid > 4096 ? 4096 : grid);
+  NBP_DISPATCH_T(dtype, ending_fwd<T><<<gr, 256, 9 * Cf * 4 * sizeof(float), S(s)>>>((const T*)feat, w, bias, img, out, g));
   return check_launch("ending_fwd");
 }
 
@@ -319,20 +326,22 @@ size_t nbp_ending_bwd_workspace_floats(int B, int Cimg, int H0, int W0, int Cf) 
   return (size_t)blocks_for((long)B * H0 * W0, 1024) * ((size_t)Cimg * Cf * 9 + Cimg);
 }
 
-int nbp_ending_bwd(const float* dy, const float* feat, const float* w, float* dfeat, float* dw, float* db, float* ws,
-                   int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, nbp_stream_t s) {
+int nbp_ending_bwd(const float* dy, const void* feat, const float* w, void* dfeat, float* dw, float* db, float* ws,
+                   int B, int Cimg, int H0, int W0, int Hp, int Wp, int Cf, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dy && feat && w && dfeat && dw && db && ws && Cimg <= kMaxCin && Cf % 4 == 0 && Cf / 4 <= 256,
               "nbp_ending_bwd: bad args");
   Img g{B, Cimg, H0, W0, Hp, Wp, Cf};
   const long tx = (long)B * Hp * Wp * (Cf / 4);
   long gx = (tx + 255) / 256;
-  ending_bwd_x<<<(int)(gx > 4096 ? 4096 : gx), 256, 9 * Cimg * Cf * sizeof(float), S(s)>>>(dy, w, dfeat, g);
+  const int gxx = (int)(gx > 4096 ? 4096 : gx);
+  NBP_DISPATCH_T(dtype, ending_bwd_x<T><<<gxx, 256, 9 * Cimg * Cf * sizeof(float), S(s)>>>(dy, w, (T*)dfeat, g));
   const long total = (long)B * H0 * W0;
   const int nb = blocks_for(total, 1024);
   const long ppb = (total + nb - 1) / nb;
   float* slab_w = ws;
   float* slab_b = ws + (long)nb * Cimg * Cf * 9;
-  NBP_DISPATCH_CI(Cimg, ending_bwd_w<CI><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(dy, feat, slab_w, slab_b, g, ppb));
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, ending_bwd_w<CI, T><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(
+                                                  dy, (const T*)feat, slab_w, slab_b, g, ppb)));
   int rc = check_launch("ending_bwd_w");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, nb, (long)Cimg * Cf * 9, dw, s);

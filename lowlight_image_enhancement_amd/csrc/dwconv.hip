@@ -16,8 +16,9 @@ struct Geo {
 };
 
 // thread layout: quad q (4 channels) = tid % Q, pixel lane = tid / Q, PPI = blockDim / Q pixels per step
-__global__ void dw_sg_pool_fwd(const float* __restrict__ t1, const float* __restrict__ wdw, const float* __restrict__ bdw,
-                               float* __restrict__ t2, float* __restrict__ g, float* __restrict__ pool_slab, Geo geo) {
+template <typename T>
+__global__ void dw_sg_pool_fwd(const T* __restrict__ t1, const float* __restrict__ wdw, const float* __restrict__ bdw,
+                               T* __restrict__ t2, T* __restrict__ g, float* __restrict__ pool_slab, Geo geo) {
   extern __shared__ float red[];  // [blockDim][4]
   const int C = geo.C, C2 = 2 * C, Q = C / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
@@ -34,7 +35,7 @@ __global__ void dw_sg_pool_fwd(const float* __restrict__ t1, const float* __rest
     }
   float4 pacc = f4(0.f);
   const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
-  const float* base = t1 + (long)b * HW * C2;
+  const T* base = t1 + (long)b * HW * C2;
   if (pl < PPI) {
     for (int p = p0 + pl; p < p1; p += PPI) {
       const int h = p / geo.W, w = p - h * geo.W;
@@ -48,8 +49,8 @@ __global__ void dw_sg_pool_fwd(const float* __restrict__ t1, const float* __rest
           const int ww = w + dw;
           if (ww < 0 || ww >= geo.W) continue;
           const int t = (dh + 1) * 3 + (dw + 1);
-          const float* src = base + ((long)hh * geo.W + ww) * C2 + q * 4;
-          const float4 va = ld4(src), vb = ld4(src + C);
+          const T* src = base + ((long)hh * geo.W + ww) * C2 + q * 4;
+          const float4 va = ldq(src), vb = ldq(src + C);
           aa.x = fmaf(wa[0][t], va.x, aa.x); aa.y = fmaf(wa[1][t], va.y, aa.y);
           aa.z = fmaf(wa[2][t], va.z, aa.z); aa.w = fmaf(wa[3][t], va.w, aa.w);
           ab.x = fmaf(wb[0][t], vb.x, ab.x); ab.y = fmaf(wb[1][t], vb.y, ab.y);
@@ -57,10 +58,10 @@ __global__ void dw_sg_pool_fwd(const float* __restrict__ t1, const float* __rest
         }
       }
       const long m = (long)b * HW + p;
-      st4(t2 + m * C2 + q * 4, aa);
-      st4(t2 + m * C2 + C + q * 4, ab);
+      stq(t2 + m * C2 + q * 4, aa);
+      stq(t2 + m * C2 + C + q * 4, ab);
       const float4 gv = aa * ab;
-      st4(g + m * C + q * 4, gv);
+      stq(g + m * C + q * 4, gv);
       pacc += gv;
     }
   }
@@ -89,8 +90,8 @@ __global__ void sca_gemv(const float* __restrict__ mean, const float* __restrict
 }
 
 // per-image channel reduction: slab[b][chunk][c] = sum_{p in chunk} x[p][c] * (y ? y[p][c] : 1)
-__global__ void img_chan_dot(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ slab,
-                             Geo geo) {
+template <typename T>
+__global__ void img_chan_dot(const T* __restrict__ x, const T* __restrict__ y, float* __restrict__ slab, Geo geo) {
   extern __shared__ float red[];
   const int C = geo.C, Q = C / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
@@ -101,8 +102,8 @@ __global__ void img_chan_dot(const float* __restrict__ x, const float* __restric
   if (pl < PPI) {
     for (int p = p0 + pl; p < p1; p += PPI) {
       const long o = ((long)b * HW + p) * C + q * 4;
-      float4 v = ld4(x + o);
-      if (y) v = v * ld4(y + o);
+      float4 v = ldq(x + o);
+      if (y) v = v * ldq(y + o);
       acc += v;
     }
   }
@@ -148,25 +149,27 @@ __global__ void sca_bwd_b(const float* __restrict__ da, const float* __restrict_
 }
 
 // dg = dh * a[b] + ds[b] / HW ; SimpleGate backward: dt2[:C] = dg * t2[C:], dt2[C:] = dg * t2[:C]
-__global__ void sca_sg_bwd(const float* __restrict__ dh, const float* __restrict__ a, const float* __restrict__ ds,
-                           const float* __restrict__ t2, float* __restrict__ dt2, long M, int C, int HW, float inv_hw) {
+template <typename T>
+__global__ void sca_sg_bwd(const T* __restrict__ dh, const float* __restrict__ a, const float* __restrict__ ds,
+                           const T* __restrict__ t2, T* __restrict__ dt2, long M, int C, int HW, float inv_hw) {
   const int Q = C / 4;
   const long total = M * Q;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long m = e / Q;
     const int q = e % Q;
     const int b = m / HW;
-    const float4 dg = fma4(ld4(dh + m * C + q * 4), ld4(a + (long)b * C + q * 4), ld4(ds + (long)b * C + q * 4) * f4(inv_hw));
-    const float4 ta = ld4(t2 + m * 2 * C + q * 4), tb = ld4(t2 + m * 2 * C + C + q * 4);
-    st4(dt2 + m * 2 * C + q * 4, dg * tb);
-    st4(dt2 + m * 2 * C + C + q * 4, dg * ta);
+    const float4 dg = fma4(ldq(dh + m * C + q * 4), ld4(a + (long)b * C + q * 4), ld4(ds + (long)b * C + q * 4) * f4(inv_hw));
+    const float4 ta = ldq(t2 + m * 2 * C + q * 4), tb = ldq(t2 + m * 2 * C + C + q * 4);
+    stq(dt2 + m * 2 * C + q * 4, dg * tb);
+    stq(dt2 + m * 2 * C + C + q * 4, dg * ta);
   }
 }
 
 // depthwise 3x3 backward on C2 channels: dt1 = sum_t w[t] dt2(p - off_t) ; partial dW[c][t] = sum dt2(p) t1(p+off_t),
 // partial db[c] = sum dt2(p).  slab: [B*chunks][C2][10]
-__global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ t1, const float* __restrict__ wdw,
-                       float* __restrict__ dt1, float* __restrict__ slab_w, float* __restrict__ slab_b, Geo geo) {
+template <typename T>
+__global__ void dw_bwd(const T* __restrict__ dt2, const T* __restrict__ t1, const float* __restrict__ wdw,
+                       T* __restrict__ dt1, float* __restrict__ slab_w, float* __restrict__ slab_b, Geo geo) {
   extern __shared__ float red[];  // [blockDim][4]
   const int C2 = 2 * geo.C, Q = C2 / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
@@ -181,12 +184,12 @@ __global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ 
 #pragma unroll
   for (int t = 0; t < 9; ++t) aw[t] = f4(0.f);
   const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
-  const float* gb = dt2 + (long)b * HW * C2 + q * 4;
-  const float* xb = t1 + (long)b * HW * C2 + q * 4;
+  const T* gb = dt2 + (long)b * HW * C2 + q * 4;
+  const T* xb = t1 + (long)b * HW * C2 + q * 4;
   if (pl < PPI) {
     for (int p = p0 + pl; p < p1; p += PPI) {
       const int h = p / geo.W, w = p - h * geo.W;
-      const float4 gc = ld4(gb + (long)p * C2);
+      const float4 gc = ldq(gb + (long)p * C2);
       ab += gc;
       float4 acc = f4(0.f);
 #pragma unroll
@@ -197,17 +200,17 @@ __global__ void dw_bwd(const float* __restrict__ dt2, const float* __restrict__ 
           // forward: t2(q) += w[t] t1(q + off)  ->  dt1(p) += w[t] dt2(p - off) ; dW[t] += dt2(p) t1(p + off)
           const int hs = h - dh, ws = w - dw;
           if (hs >= 0 && hs < geo.H && ws >= 0 && ws < geo.W) {
-            const float4 gv = ld4(gb + ((long)hs * geo.W + ws) * C2);
+            const float4 gv = ldq(gb + ((long)hs * geo.W + ws) * C2);
             acc.x = fmaf(wk[0][t], gv.x, acc.x); acc.y = fmaf(wk[1][t], gv.y, acc.y);
             acc.z = fmaf(wk[2][t], gv.z, acc.z); acc.w = fmaf(wk[3][t], gv.w, acc.w);
           }
           const int hp = h + dh, wp = w + dw;
           if (hp >= 0 && hp < geo.H && wp >= 0 && wp < geo.W) {
-            aw[t] = fma4(gc, ld4(xb + ((long)hp * geo.W + wp) * C2), aw[t]);
+            aw[t] = fma4(gc, ldq(xb + ((long)hp * geo.W + wp) * C2), aw[t]);
           }
         }
       }
-      st4(dt1 + ((long)b * HW + p) * C2 + q * 4, acc);
+      stq(dt1 + ((long)b * HW + p) * C2 + q * 4, acc);
     }
   }
   // block reduction over pixel lanes sharing quad q, one tap at a time through a [blockDim][4] buffer
@@ -265,14 +268,15 @@ int nbp_dw_chunks(int B, int H, int W, int C, int which) {
   return make_geo(B, H, W, C, Q, blk, cap).chunks;
 }
 
-int nbp_dw_sg_pool_fwd(const float* t1, const float* wdw, const float* bdw, float* t2, float* g, float* pool_slab, int B,
-                       int H, int W, int C, nbp_stream_t s) {
+int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
+                       int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(t1 && wdw && bdw && t2 && g && pool_slab && B > 0 && H > 0 && W > 0, "nbp_dw_sg_pool_fwd: bad args");
   NBP_REQUIRE(C % 4 == 0 && C / 4 <= 1024, "nbp_dw_sg_pool_fwd: C");
   const int Q = C / 4, blk = block_for_quads(Q);
   Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
   dim3 grid(geo.chunks, B);
-  dw_sg_pool_fwd<<<grid, blk, blk * 4 * sizeof(float), S(s)>>>(t1, wdw, bdw, t2, g, pool_slab, geo);
+  NBP_DISPATCH_T(dtype, dw_sg_pool_fwd<T><<<grid, blk, blk * 4 * sizeof(float), S(s)>>>((const T*)t1, wdw, bdw, (T*)t2,
+                                                                                       (T*)g, pool_slab, geo));
   return check_launch("dw_sg_pool_fwd");
 }
 
@@ -285,11 +289,12 @@ int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const flo
   return check_launch("sca_fwd");
 }
 
-int nbp_img_chan_dot(const float* x, const float* y, float* slab, int B, int H, int W, int C, nbp_stream_t s) {
+int nbp_img_chan_dot(const void* x, const void* y, float* slab, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && slab && B > 0 && C % 4 == 0 && C / 4 <= 1024, "nbp_img_chan_dot: bad args");
   const int Q = C / 4, blk = block_for_quads(Q);
   Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
-  img_chan_dot<<<dim3(geo.chunks, B), blk, blk * 4 * sizeof(float), S(s)>>>(x, y, slab, geo);
+  NBP_DISPATCH_T(dtype, img_chan_dot<T><<<dim3(geo.chunks, B), blk, blk * 4 * sizeof(float), S(s)>>>(
+                            (const T*)x, (const T*)y, slab, geo));
   return check_launch("img_chan_dot");
 }
 
@@ -304,12 +309,13 @@ int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float
   return check_launch("sca_bwd");
 }
 
-int nbp_sca_sg_bwd(const float* dh, const float* a, const float* ds, const float* t2, float* dt2, long M, int C, int HW,
-                   nbp_stream_t s) {
+int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* t2, void* dt2, long M, int C, int HW,
+                   int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dh && a && ds && t2 && dt2 && M > 0 && C % 4 == 0 && HW > 0, "nbp_sca_sg_bwd: bad args");
   const long tot = M * (C / 4);
-  sca_sg_bwd<<<cdiv(tot, 256) > 4096 ? 4096 : cdiv(tot, 256), 256, 0, S(s)>>>(dh, a, ds, t2, dt2, M, C, HW,
-                                                                             1.f / (float)HW);
+  const int gr = cdiv(tot, 256) > 4096 ? 4096 : cdiv(tot, 256);
+  NBP_DISPATCH_T(dtype, sca_sg_bwd<T><<<gr, 256, 0, S(s)>>>((const T*)dh, a, ds, (const T*)t2, (T*)dt2, M, C, HW,
+                                                            1.f / (float)HW));
   return check_launch("sca_sg_bwd");
 }
 
@@ -317,8 +323,8 @@ size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
   return (size_t)B * nbp_dw_chunks(B, H, W, C, 1) * 2 * C * 10;
 }
 
-int nbp_dw_bwd(const float* dt2, const float* t1, const float* wdw, float* dt1, float* dwdw, float* dbdw, float* ws,
-               int B, int H, int W, int C, nbp_stream_t s) {
+int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws,
+               int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dt2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && C % 2 == 0, "nbp_dw_bwd: bad args");
   const int Q = C / 2;  // quads over 2C channels
   NBP_REQUIRE(Q <= 1024, "nbp_dw_bwd: too many channels");
@@ -329,7 +335,8 @@ int nbp_dw_bwd(const float* dt2, const float* t1, const float* wdw, float* dt1, 
   const long nrow = (long)B * geo.chunks;
   float* slab_w = ws;
   float* slab_b = ws + nrow * 2 * C * 9;
-  dw_bwd<<<dim3(geo.chunks, B), blk, (size_t)blk * 4 * sizeof(float), S(s)>>>(dt2, t1, wdw, dt1, slab_w, slab_b, geo);
+  NBP_DISPATCH_T(dtype, dw_bwd<T><<<dim3(geo.chunks, B), blk, (size_t)blk * 4 * sizeof(float), S(s)>>>(
+                            (const T*)dt2, (const T*)t1, wdw, (T*)dt1, slab_w, slab_b, geo));
   int rc = check_launch("dw_bwd");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, (int)nrow, 2L * C * 9, dwdw, s);

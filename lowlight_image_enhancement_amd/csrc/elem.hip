@@ -7,32 +7,35 @@ using namespace nbp;
 
 namespace {
 
-__global__ void sg_fwd(const float* __restrict__ t, float* __restrict__ g, long M, int C) {
+template <typename T>
+__global__ void sg_fwd(const T* __restrict__ t, T* __restrict__ g, long M, int C) {
   const int Q = C / 4;
   const long total = M * Q;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long m = e / Q;
     const int q = e % Q;
-    st4(g + m * C + q * 4, ld4(t + m * 2 * C + q * 4) * ld4(t + m * 2 * C + C + q * 4));
+    stq(g + m * C + q * 4, ldq(t + m * 2 * C + q * 4) * ldq(t + m * 2 * C + C + q * 4));
   }
 }
 
-__global__ void sg_bwd(const float* __restrict__ dg, const float* __restrict__ t, float* __restrict__ dt, long M, int C) {
+template <typename T>
+__global__ void sg_bwd(const T* __restrict__ dg, const T* __restrict__ t, T* __restrict__ dt, long M, int C) {
   const int Q = C / 4;
   const long total = M * Q;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long m = e / Q;
     const int q = e % Q;
-    const float4 d = ld4(dg + m * C + q * 4);
-    const float4 a = ld4(t + m * 2 * C + q * 4), b = ld4(t + m * 2 * C + C + q * 4);
-    st4(dt + m * 2 * C + q * 4, d * b);
-    st4(dt + m * 2 * C + C + q * 4, d * a);
+    const float4 d = ldq(dg + m * C + q * 4);
+    const float4 a = ldq(t + m * 2 * C + q * 4), b = ldq(t + m * 2 * C + C + q * 4);
+    stq(dt + m * 2 * C + q * 4, d * b);
+    stq(dt + m * 2 * C + C + q * 4, d * a);
   }
 }
 
 // ds[m][c] = d[m][c] * scale[c] ; slab[blk][c] = sum_m d[m][c] * t[m][c]
-__global__ void scale_dot(const float* __restrict__ d, const float* __restrict__ t, const float* __restrict__ scale,
-                          float* __restrict__ ds, float* __restrict__ slab, long M, int C) {
+template <typename T>
+__global__ void scale_dot(const T* __restrict__ d, const T* __restrict__ t, const float* __restrict__ scale,
+                          T* __restrict__ ds, float* __restrict__ slab, long M, int C) {
   extern __shared__ float red[];
   const int Q = C / 4;
   const int tid = threadIdx.x, q = tid % Q, rl = tid / Q, RPS = blockDim.x / Q;
@@ -40,9 +43,9 @@ __global__ void scale_dot(const float* __restrict__ d, const float* __restrict__
   const float4 sc = ld4(scale + q * 4);
   if (rl < RPS) {
     for (long m = (long)blockIdx.x * RPS + rl; m < M; m += (long)gridDim.x * RPS) {
-      const float4 dv = ld4(d + m * C + q * 4);
-      acc = fma4(dv, ld4(t + m * C + q * 4), acc);
-      st4(ds + m * C + q * 4, dv * sc);
+      const float4 dv = ldq(d + m * C + q * 4);
+      acc = fma4(dv, ldq(t + m * C + q * 4), acc);
+      stq(ds + m * C + q * 4, dv * sc);
     }
   }
   st4(red + tid * 4, acc);
@@ -93,8 +96,10 @@ __global__ void nhwc_to_nchw(const float* __restrict__ x, float* __restrict__ y,
   }
 }
 
-__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y, long n) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] = a[i] + b[i];
+template <typename T>
+__global__ void add_kernel(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    y[i] = (T)((float)a[i] + (float)b[i]);
 }
 
 inline int g_elem(long total) {
@@ -106,15 +111,15 @@ inline int g_elem(long total) {
 
 extern "C" {
 
-int nbp_sg_fwd(const float* t, float* g, long M, int C, nbp_stream_t s) {
+int nbp_sg_fwd(const void* t, void* g, long M, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(t && g && M > 0 && C % 4 == 0, "nbp_sg_fwd: bad args");
-  sg_fwd<<<g_elem(M * (C / 4)), 256, 0, S(s)>>>(t, g, M, C);
+  NBP_DISPATCH_T(dtype, sg_fwd<T><<<g_elem(M * (C / 4)), 256, 0, S(s)>>>((const T*)t, (T*)g, M, C));
   return check_launch("sg_fwd");
 }
 
-int nbp_sg_bwd(const float* dg, const float* t, float* dt, long M, int C, nbp_stream_t s) {
+int nbp_sg_bwd(const void* dg, const void* t, void* dt, long M, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dg && t && dt && M > 0 && C % 4 == 0, "nbp_sg_bwd: bad args");
-  sg_bwd<<<g_elem(M * (C / 4)), 256, 0, S(s)>>>(dg, t, dt, M, C);
+  NBP_DISPATCH_T(dtype, sg_bwd<T><<<g_elem(M * (C / 4)), 256, 0, S(s)>>>((const T*)dg, (const T*)t, (T*)dt, M, C));
   return check_launch("sg_bwd");
 }
 
@@ -126,11 +131,12 @@ int nbp_scale_dot_grid(long M, int C) {
 }
 
 // slab: [nbp_scale_dot_grid(M, C)][C]
-int nbp_scale_dot(const float* d, const float* t, const float* scale, float* ds, float* slab, long M, int C,
+int nbp_scale_dot(const void* d, const void* t, const float* scale, void* ds, float* slab, long M, int C, int dtype,
                   nbp_stream_t s) {
   NBP_REQUIRE(d && t && scale && ds && slab && M > 0 && C % 4 == 0 && C / 4 <= 1024, "nbp_scale_dot: bad args");
   const int Q = C / 4, blk = Q >= 256 ? Q : 256;
-  scale_dot<<<nbp_scale_dot_grid(M, C), blk, blk * 4 * sizeof(float), S(s)>>>(d, t, scale, ds, slab, M, C);
+  NBP_DISPATCH_T(dtype, scale_dot<T><<<nbp_scale_dot_grid(M, C), blk, blk * 4 * sizeof(float), S(s)>>>(
+                            (const T*)d, (const T*)t, scale, (T*)ds, slab, M, C));
   return check_launch("scale_dot");
 }
 
@@ -146,9 +152,9 @@ int nbp_nhwc_to_nchw(const float* x, float* y, int N, int C, long HW, nbp_stream
   return check_launch("nhwc_to_nchw");
 }
 
-int nbp_add(const float* a, const float* b, float* y, long n, nbp_stream_t s) {
+int nbp_add(const void* a, const void* b, void* y, long n, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && y && n > 0, "nbp_add: bad args");
-  add_kernel<<<g_elem(n), 256, 0, S(s)>>>(a, b, y, n);
+  NBP_DISPATCH_T(dtype, add_kernel<T><<<g_elem(n), 256, 0, S(s)>>>((const T*)a, (const T*)b, (T*)y, n));
   return check_launch("add");
 }
 

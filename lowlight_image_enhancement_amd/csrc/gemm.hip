@@ -168,9 +168,9 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
 
 // ---------------------------------------------------------------- weight gradient: dW[n][k] = sum_m G(m,n) X(m,k)
 struct WgradP {
-  const float* G;
+  const void* G;
   long ldg;
-  const float* X;
+  const void* X;
   long ldx;
   const float* x_scale;
   int rows_per_img;
@@ -181,8 +181,10 @@ struct WgradP {
   int chunk;
 };
 
-template <int GMODE, int XMODE>
+template <int GMODE, int XMODE, typename T>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
+  const T* G = reinterpret_cast<const T*>(p.G);
+  const T* X = reinterpret_cast<const T*>(p.X);
   constexpr int RM = 32, TNW = 64, TKW = 64, LS = 68;
   __shared__ float Gs[RM * LS];
   __shared__ float Xs[RM * LS];
@@ -207,12 +209,12 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
       const int n = n0 + q * 4, k = k0 + q * 4;
       if (m < me) {
         if (n < p.N) {
-          if (GMODE == AM_S2D) g = ld4(p.G + s2d_off(m, n, p.gh, p.gw, p.cs_g));
-          else g = ld4(p.G + (long)m * p.ldg + n);
+          if (GMODE == AM_S2D) g = ldq(G + s2d_off(m, n, p.gh, p.gw, p.cs_g));
+          else g = ldq(G + (long)m * p.ldg + n);
         }
         if (k < p.K) {
-          if (XMODE == AM_S2D) x = ld4(p.X + s2d_off(m, k, p.gh, p.gw, p.cs_x));
-          else x = ld4(p.X + (long)m * p.ldx + k);
+          if (XMODE == AM_S2D) x = ldq(X + s2d_off(m, k, p.gh, p.gw, p.cs_x));
+          else x = ldq(X + (long)m * p.ldx + k);
           if (XMODE == AM_SCALE) x = x * ld4(p.x_scale + (long)(m / p.rows_per_img) * p.K + k);
         }
       }
@@ -367,9 +369,9 @@ size_t nbp_wgrad_workspace_floats(int M, int N, int K) {
   return (size_t)S_ * N * K + (size_t)S_ * N;
 }
 
-int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx, int x_mode, const float* x_scale,
+int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, int x_mode, const float* x_scale,
                   int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
-                  float* ws, size_t ws_floats, nbp_stream_t s) {
+                  float* ws, size_t ws_floats, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(G && X && dW && ws && M > 0 && N > 0 && K > 0, "nbp_wgrad_f32: null pointer or empty shape");
   NBP_REQUIRE(N % 4 == 0 && K % 4 == 0, "nbp_wgrad_f32: N, K multiples of 4");
   NBP_REQUIRE((g_mode == AM_PLAIN || g_mode == AM_S2D) && x_mode >= 0 && x_mode <= 2, "nbp_wgrad_f32: mode");
@@ -385,11 +387,15 @@ int nbp_wgrad_f32(const float* G, long ldg, int g_mode, const float* X, long ldx
   WgradP p{G, ldg, X, ldx, x_scale, rows_per_img, M, N, K, gh, gw, cs_g, cs_x, slab, slab_b, chunk};
   dim3 grid(cdiv(N, 64), cdiv(K, 64), S_);
   hipStream_t st = S(s);
-  if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
-  else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_f32_kernel<AM_PLAIN, AM_SCALE><<<grid, 256, 0, st>>>(p);
-  else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_f32_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
-  else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);
-  else { set_error("nbp_wgrad_f32: unsupported mode combination"); return NBP_ERR_ARG; }
+  bool ok = true;
+  NBP_DISPATCH_T(dtype, {
+    if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_PLAIN, AM_PLAIN, T><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_f32_kernel<AM_PLAIN, AM_SCALE, T><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_f32_kernel<AM_PLAIN, AM_S2D, T><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_S2D, AM_PLAIN, T><<<grid, 256, 0, st>>>(p);
+    else ok = false;
+  });
+  if (!ok) { set_error("nbp_wgrad_f32: unsupported mode combination"); return NBP_ERR_ARG; }
   launch_reduce(slab, 1, S_, (long)N * K, 1.f, dW, st);
   if (db) launch_reduce(slab_b, 1, S_, N, 1.f, db, st);
   return check_launch("wgrad_f32");

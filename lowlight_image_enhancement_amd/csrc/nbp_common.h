@@ -8,6 +8,8 @@
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace nbp {
 
@@ -35,6 +37,43 @@ __device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
   return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z), fmaf(a.w, b.w, c.w));
 }
 __device__ __forceinline__ float get(float4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// storage-type generic quad (4 consecutive channels) access: fp32 storage or bf16 storage, fp32 math
+template <typename T>
+__device__ __forceinline__ float4 ldq(const T* p) {
+  if constexpr (sizeof(T) == 4) {
+    return *reinterpret_cast<const float4*>(p);
+  } else {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void stq(T* p, float4 v) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = v;
+  } else {
+    bf16x4 o;
+    o[0] = (__bf16)v.x; o[1] = (__bf16)v.y; o[2] = (__bf16)v.z; o[3] = (__bf16)v.w;
+    *reinterpret_cast<bf16x4*>(p) = o;
+  }
+}
+template <typename T>
+__device__ __forceinline__ float lds1(const T* p) { return (float)*p; }
+template <typename T>
+__device__ __forceinline__ void sts1(T* p, float v) { *p = (T)v; }
+
+// dtype code of the C-ABI: 0 fp32, 1 bf16
+#define NBP_DISPATCH_T(dtype, ...)                   \
+  do {                                               \
+    if ((dtype) == 0) {                              \
+      using T = float;                               \
+      __VA_ARGS__;                                   \
+    } else {                                         \
+      using T = __bf16;                              \
+      __VA_ARGS__;                                   \
+    }                                                \
+  } while (0)
 
 // sum over the 64 lanes of a wave
 __device__ __forceinline__ float wave_sum(float v) {

@@ -9,10 +9,10 @@ namespace {
 
 constexpr int kMaxV = 4;  // C <= 4 * 4 * 64 = 1024
 
-template <int G>
-__global__ __launch_bounds__(256) void ln_fwd_nhwc(const float* __restrict__ x, const float* __restrict__ w,
-                                                   const float* __restrict__ b, float* __restrict__ yhat,
-                                                   float* __restrict__ nout, float* __restrict__ den, long M, int C,
+template <int G, typename T>
+__global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ b, T* __restrict__ yhat,
+                                                   T* __restrict__ nout, float* __restrict__ den, long M, int C,
                                                    float eps) {
   const int lane = threadIdx.x & 63, lg = lane % G;
   constexpr int RPW = 64 / G;
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const float* __restrict__ x, 
 #pragma unroll
     for (int j = 0; j < kMaxV; ++j) {
       if (j < V) {
-        v[j] = ok ? ld4(x + row * C + (j * G + lg) * 4) : f4(0.f);
+        v[j] = ok ? ldq(x + row * C + (j * G + lg) * 4) : f4(0.f);
         s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
       }
     }
@@ -51,8 +51,8 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const float* __restrict__ x, 
         const int c = (j * G + lg) * 4;
         const float4 d = v[j] - f4(mu);
         const float4 yh = make_float4(d.x / dd, d.y / dd, d.z / dd, d.w / dd);
-        if (yhat) st4(yhat + row * C + c, yh);
-        st4(nout + row * C + c, fma4(ld4(w + c), yh, ld4(b + c)));
+        if (yhat) stq(yhat + row * C + c, yh);
+        stq(nout + row * C + c, fma4(ld4(w + c), yh, ld4(b + c)));
       }
     }
     if (lg == 0) den[row] = dd;
@@ -60,10 +60,10 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const float* __restrict__ x, 
 }
 
 // dx = (g - yhat * mean(g*yhat) - mean(g)) / den + dres,  g = dn * w;  per-block partials of sum(dn*yhat), sum(dn)
-template <int G>
-__global__ __launch_bounds__(256) void ln_bwd_nhwc(const float* __restrict__ dn, const float* __restrict__ yhat,
+template <int G, typename T>
+__global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, const T* __restrict__ yhat,
                                                    const float* __restrict__ den, const float* __restrict__ w,
-                                                   const float* __restrict__ dres, float* __restrict__ dx,
+                                                   const T* __restrict__ dres, T* __restrict__ dx,
                                                    float* __restrict__ slab_w, float* __restrict__ slab_b, long M,
                                                    int C) {
   __shared__ float red[4][2][1024];
@@ -84,8 +84,8 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const float* __restrict__ dn,
     for (int j = 0; j < kMaxV; ++j) {
       if (j < V) {
         const int c = (j * G + lg) * 4;
-        const float4 d = ok ? ld4(dn + row * C + c) : f4(0.f);
-        yh[j] = ok ? ld4(yhat + row * C + c) : f4(0.f);
+        const float4 d = ok ? ldq(dn + row * C + c) : f4(0.f);
+        yh[j] = ok ? ldq(yhat + row * C + c) : f4(0.f);
         g[j] = d * ld4(w + c);
         aw[j] = fma4(d, yh[j], aw[j]);
         ab[j] += d;
@@ -104,8 +104,8 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const float* __restrict__ dn,
       if (j < V) {
         const int c = (j * G + lg) * 4;
         float4 o = (g[j] - yh[j] * f4(mgy) - f4(mg)) * f4(inv);
-        if (dres) o += ld4(dres + row * C + c);
-        st4(dx + row * C + c, o);
+        if (dres) o += ldq(dres + row * C + c);
+        stq(dx + row * C + c, o);
       }
     }
   }
@@ -234,38 +234,49 @@ int nbp_ln_nhwc_grid(long M, int C) {
   }
 }
 
-int nbp_ln_fwd_nhwc(const float* x, const float* w, const float* b, float* yhat, float* nout, float* den, long M, int C,
-                    float eps, nbp_stream_t s) {
+int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* yhat, void* nout, float* den, long M, int C,
+                    float eps, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && b && nout && den && M > 0, "nbp_ln_fwd_nhwc: bad args");
   NBP_REQUIRE(C >= 8 && C <= 1024 && (C & (C - 1)) == 0, "nbp_ln_fwd_nhwc: C must be a power of two in [8,1024]");
   const int g = nbp_ln_nhwc_grid(M, C);
   hipStream_t st = S(s);
-  switch (pick_G(C)) {
-    case 64: ln_fwd_nhwc<64><<<g, 256, 0, st>>>(x, w, b, yhat, nout, den, M, C, eps); break;
-    case 32: ln_fwd_nhwc<32><<<g, 256, 0, st>>>(x, w, b, yhat, nout, den, M, C, eps); break;
-    case 16: ln_fwd_nhwc<16><<<g, 256, 0, st>>>(x, w, b, yhat, nout, den, M, C, eps); break;
-    case 8: ln_fwd_nhwc<8><<<g, 256, 0, st>>>(x, w, b, yhat, nout, den, M, C, eps); break;
-    case 4: ln_fwd_nhwc<4><<<g, 256, 0, st>>>(x, w, b, yhat, nout, den, M, C, eps); break;
-    default: ln_fwd_nhwc<2><<<g, 256, 0, st>>>(x, w, b, yhat, nout, den, M, C, eps); break;
-  }
+  NBP_DISPATCH_T(dtype, {
+    const T* xx = (const T*)x;
+    T* yy = (T*)yhat;
+    T* nn = (T*)nout;
+    switch (pick_G(C)) {
+      case 64: ln_fwd_nhwc<64, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
+      case 32: ln_fwd_nhwc<32, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
+      case 16: ln_fwd_nhwc<16, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
+      case 8: ln_fwd_nhwc<8, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
+      case 4: ln_fwd_nhwc<4, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
+      default: ln_fwd_nhwc<2, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
+    }
+  });
   return check_launch("ln_fwd_nhwc");
 }
 
 // slab_w / slab_b: [grid][C] floats each (grid = nbp_ln_nhwc_grid(M, C)); reduced by the caller (nbp_reduce_slab)
-int nbp_ln_bwd_nhwc(const float* dn, const float* yhat, const float* den, const float* w, const float* dres, float* dx,
-                    float* slab_w, float* slab_b, long M, int C, nbp_stream_t s) {
+int nbp_ln_bwd_nhwc(const void* dn, const void* yhat, const float* den, const float* w, const void* dres, void* dx,
+                    float* slab_w, float* slab_b, long M, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dn && yhat && den && w && dx && slab_w && slab_b && M > 0, "nbp_ln_bwd_nhwc: bad args");
   NBP_REQUIRE(C >= 8 && C <= 1024 && (C & (C - 1)) == 0, "nbp_ln_bwd_nhwc: C must be a power of two in [8,1024]");
   const int g = nbp_ln_nhwc_grid(M, C);
   hipStream_t st = S(s);
-  switch (pick_G(C)) {
-    case 64: ln_bwd_nhwc<64><<<g, 256, 0, st>>>(dn, yhat, den, w, dres, dx, slab_w, slab_b, M, C); break;
-    case 32: ln_bwd_nhwc<32><<<g, 256, 0, st>>>(dn, yhat, den, w, dres, dx, slab_w, slab_b, M, C); break;
-    case 16: ln_bwd_nhwc<16><<<g, 256, 0, st>>>(dn, yhat, den, w, dres, dx, slab_w, slab_b, M, C); break;
-    case 8: ln_bwd_nhwc<8><<<g, 256, 0, st>>>(dn, yhat, den, w, dres, dx, slab_w, slab_b, M, C); break;
-    case 4: ln_bwd_nhwc<4><<<g, 256, 0, st>>>(dn, yhat, den, w, dres, dx, slab_w, slab_b, M, C); break;
-    default: ln_bwd_nhwc<2><<<g, 256, 0, st>>>(dn, yhat, den, w, dres, dx, slab_w, slab_b, M, C); break;
-  }
+  NBP_DISPATCH_T(dtype, {
+    const T* a = (const T*)dn;
+    const T* yh = (const T*)yhat;
+    const T* r = (const T*)dres;
+    T* o = (T*)dx;
+    switch (pick_G(C)) {
+      case 64: ln_bwd_nhwc<64, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
+      case 32: ln_bwd_nhwc<32, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
+      case 16: ln_bwd_nhwc<16, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
+      case 8: ln_bwd_nhwc<8, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
+      case 4: ln_bwd_nhwc<4, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
+      default: ln_bwd_nhwc<2, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
+    }
+  });
   return check_launch("ln_bwd_nhwc");
 }
 

@@ -171,6 +171,15 @@ class NAFNet(nn.Module):
         call("weights_bf16", P, self.numel, wb, self._tdesc, self._tdesc.shape[0], wt)
         return wb, wt
 
+    @property
+    def adt(self) -> torch.dtype:
+        """storage dtype of NHWC activations and activation gradients"""
+        return torch.float32 if self.precision == "fp32" else torch.bfloat16
+
+    @property
+    def dt(self) -> int:
+        return 0 if self.precision == "fp32" else 1
+
     def _mm(self, W, A, lda, amode, ascale, rows, wkey, C, ldc, cmode, M, N, K, gh=0, gw=0, cs=0, bias=None,
             R=None, rscale=None, pre=None, dgrad=False):
         """One GEMM launch.  W = (fp32 flat,) or (fp32 flat, bf16 copy, bf16 transposed copy).
@@ -181,7 +190,7 @@ class NAFNet(nn.Module):
                  M, N, K, gh, gw, cs, bias, R, rscale, pre)
         else:
             Wb = self._slice(W[2] if dgrad else W[1], wkey)
-            call("gemm_bf16", A, lda, amode, ascale, rows, 0, Wb, K, C, ldc, cmode, 0, M, N, K, gh, gw, cs, bias,
+            call("gemm_bf16", A, lda, amode, ascale, rows, 1, Wb, K, C, ldc, cmode, 1, M, N, K, gh, gw, cs, bias,
                  R, rscale, pre)
 
     # reference layout <-> internal layout
@@ -283,9 +292,9 @@ class NAFNet(nn.Module):
         Wt = (P,) if self.precision == "fp32" else (P,) + self._prep_weights(P)
         self._W = Wt
         w = self.width
-        feat = torch.empty(B, Hp, Wp, w, device=x.device)
+        feat = torch.empty(B, Hp, Wp, w, device=x.device, dtype=self.adt)
         call("intro_fwd", x, self._slice(P, "intro.weight"), self._slice(P, "intro.bias"), feat, B, Ci, H0, W0, Hp,
-             Wp, w)
+             Wp, w, self.dt)
         if save:
             tape.append(("intro", x, (B, Ci, H0, W0, Hp, Wp, w)))
         h, wd = Hp, Wp
@@ -308,7 +317,7 @@ class NAFNet(nn.Module):
                 feat = self._block_fwd(P, f"decoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None)
         out = torch.empty(B, Ci, H0, W0, device=x.device)
         call("ending_fwd", feat, self._slice(P, "ending.weight"), self._slice(P, "ending.bias"), x, out, B, Ci, H0,
-             W0, Hp, Wp, w)
+             W0, Hp, Wp, w, self.dt)
         if save:
             tape.append(("ending", feat, (B, Ci, H0, W0, Hp, Wp, w)))
             tape.append(("weights", Wt))
@@ -318,31 +327,33 @@ class NAFNet(nn.Module):
     def _block_fwd(self, P, pre, x, B, h, w, c, tape):
         M = B * h * w
         dev = x.device
-        E = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
-        yh1, n1, den1 = E(M, c), E(M, c), E(M)
+        E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
+        F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
+        dt = self.dt
+        yh1, n1, den1 = E(M, c), E(M, c), F(M)
         call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), yh1, n1,
-             den1, M, c, LN_EPS)
+             den1, M, c, LN_EPS, dt)
         t1 = E(M, 2 * c)
         self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv1.bias"))
         chunks = query("dw_chunks", B, h, w, c, 0)
-        t2, g, pool = E(M, 2 * c), E(M, c), E(B * chunks * c)
+        t2, g, pool = E(M, 2 * c), E(M, c), F(B * chunks * c)
         call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2, g,
-             pool, B, h, w, c)
-        mean, a = E(B, c), E(B, c)
+             pool, B, h, w, c, dt)
+        mean, a = F(B, c), F(B, c)
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
              a, B, h * w, c)
         y, t3 = E(M, c), E(M, c)
         self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
                  bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"), pre=t3)
-        yh2, n2, den2 = E(M, c), E(M, c), E(M)
+        yh2, n2, den2 = E(M, c), E(M, c), F(M)
         call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), yh2, n2,
-             den2, M, c, LN_EPS)
+             den2, M, c, LN_EPS, dt)
         t4 = E(M, 2 * c)
         self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv4.bias"))
         g2 = E(M, c)
-        call("sg_fwd", t4, g2, M, c)
+        call("sg_fwd", t4, g2, M, c, dt)
         out, t5 = E(M, c), E(M, c)
         self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
                  bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"), pre=t5)
@@ -354,7 +365,7 @@ class NAFNet(nn.Module):
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
         ho, wo = h // 2, w // 2
         M = B * ho * wo
-        out = torch.empty(B, ho, wo, 2 * c, device=x.device)
+        out = torch.empty(B, ho, wo, 2 * c, device=x.device, dtype=self.adt)
         self._mm(self._W, x, 0, AM_S2D, None, 1, f"downs.{i}.weight", out, 2 * c, CM_PLAIN, M, 2 * c, 4 * c, ho, wo,
                  c, bias=self._slice(P, f"downs.{i}.bias"))
         if tape is not None:
@@ -363,7 +374,7 @@ class NAFNet(nn.Module):
 
     def _up_fwd(self, P, i, x, skip, B, h, w, chan, tape):
         M = B * h * w
-        out = torch.empty(B, 2 * h, 2 * w, chan // 2, device=x.device)
+        out = torch.empty(B, 2 * h, 2 * w, chan // 2, device=x.device, dtype=self.adt)
         self._mm(self._W, x, chan, AM_PLAIN, None, 1, f"ups.{i}.0.weight", out, 0, CM_D2S, M, 2 * chan, chan, h, w,
                  chan // 2, R=skip)
         if tape is not None:
@@ -389,11 +400,11 @@ class NAFNet(nn.Module):
                 continue
             if kind == "ending":
                 feat, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
-                dfeat = torch.empty(B, Hp, Wp, w, device=dout.device)
+                dfeat = torch.empty(B, Hp, Wp, w, device=dout.device, dtype=self.adt)
                 ws = torch.empty(query("ending_bwd_workspace_floats", B, Ci, H0, W0, w), device=dout.device)
                 call("ending_bwd", dout, feat, self._slice(P, "ending.weight"), dfeat,
                      self._slice(dflat, "ending.weight"), self._slice(dflat, "ending.bias"), ws, B, Ci, H0, W0, Hp,
-                     Wp, w)
+                     Wp, w, self.dt)
                 self._stage_done("ending", hook)
             elif kind == "block":
                 pre, geo, S = rec[1], rec[2], rec[3]
@@ -403,7 +414,7 @@ class NAFNet(nn.Module):
                 i, (B, h, w, chan), x = rec[1], rec[2], rec[3]
                 dskips.append(dfeat)  # d(skip) = d(up output): the skip add is an identity branch
                 M = B * h * w
-                dx = torch.empty(B, h, w, chan, device=dout.device)
+                dx = torch.empty(B, h, w, chan, device=dout.device, dtype=self.adt)
                 self._mm(Wt, dfeat, 0, AM_S2D, None, 1, f"ups.{i}.0.weight", dx, chan, CM_PLAIN, M, chan, 2 * chan,
                          h, w, chan // 2, dgrad=True)
                 self._wgrad(dfeat, 0, AM_S2D, x, chan, AM_PLAIN, None, 1, M, 2 * chan, chan, h, w, chan // 2, 0,
@@ -415,7 +426,7 @@ class NAFNet(nn.Module):
                 ho, wo = h // 2, w // 2
                 M = B * ho * wo
                 dskip = dskips.pop()
-                dx = torch.empty(B, h, w, c, device=dout.device)
+                dx = torch.empty(B, h, w, c, device=dout.device, dtype=self.adt)
                 # d enc = D2S(dout . Wd) + d skip
                 self._mm(Wt, dfeat, 2 * c, AM_PLAIN, None, 1, f"downs.{i}.weight", dx, 0, CM_D2S, M, 4 * c, 2 * c,
                          ho, wo, c, R=dskip, dgrad=True)
@@ -429,11 +440,11 @@ class NAFNet(nn.Module):
                 if need_dx:
                     dx_img = torch.empty(B, Ci, H0, W0, device=dout.device)
                 call("intro_bwd", x, dfeat, self._slice(P, "intro.weight"), self._slice(dflat, "intro.weight"),
-                     self._slice(dflat, "intro.bias"), dx_img, ws, B, Ci, H0, W0, Hp, Wp, w)
+                     self._slice(dflat, "intro.bias"), dx_img, ws, B, Ci, H0, W0, Hp, Wp, w, self.dt)
                 self._stage_done("intro", hook)
         if need_dx:
             # global residual x + inp (NAFNet_arch.py:153): d inp += d out
-            call("add", dx_img, dout, dx_img, dx_img.numel())
+            call("add", dx_img, dout, dx_img, dx_img.numel(), 0)
         return dx_img
 
     def _stage_done(self, name, hook):
@@ -443,7 +454,8 @@ class NAFNet(nn.Module):
     def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db):
         n_ws = query("wgrad_workspace_floats", M, N, K)
         ws = torch.empty(n_ws, device=G.device)
-        call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws, n_ws)
+        call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws, n_ws,
+             self.dt)
 
     def _reduce(self, slab, S, L, out):
         call("reduce_slab", slab, S, L, out)
@@ -453,13 +465,15 @@ class NAFNet(nn.Module):
         M = B * h * w
         HW = h * w
         dev = dout.device
-        E = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
+        F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        dt = self.dt
         dout = dout.reshape(M, c)
         # out = y + gamma * t5
         gs = query("scale_dot_grid", M, c)
-        slab = E(gs * c)
+        slab = F(gs * c)
         dt5 = E(M, c)
-        call("scale_dot", dout, S["t5"], self._slice(P, pre + "gamma"), dt5, slab, M, c)
+        call("scale_dot", dout, S["t5"], self._slice(P, pre + "gamma"), dt5, slab, M, c, dt)
         self._reduce(slab, gs, c, self._slice(dflat, pre + "gamma"))
         # conv5
         dg2 = E(M, c)
@@ -468,7 +482,7 @@ class NAFNet(nn.Module):
                     self._slice(dflat, pre + "conv5.weight"), self._slice(dflat, pre + "conv5.bias"))
         # SimpleGate (FFN)
         dt4 = E(M, 2 * c)
-        call("sg_bwd", dg2, S["t4"], dt4, M, c)
+        call("sg_bwd", dg2, S["t4"], dt4, M, c, dt)
         # conv4
         dn2 = E(M, c)
         self._mm(Wt, dt4, 2 * c, AM_PLAIN, None, 1, pre + "conv4.weight", dn2, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
@@ -476,14 +490,14 @@ class NAFNet(nn.Module):
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
         # norm2 + residual
         lg = query("ln_nhwc_grid", M, c)
-        sw, sb = E(lg * c), E(lg * c)
+        sw, sb = F(lg * c), F(lg * c)
         dy = E(M, c)
-        call("ln_bwd_nhwc", dn2, S["yh2"], S["den2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb, M, c)
+        call("ln_bwd_nhwc", dn2, S["yh2"], S["den2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb, M, c, dt)
         self._reduce(sw, lg, c, self._slice(dflat, pre + "norm2.weight"))
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
         # y = x + beta * t3
         dt3 = E(M, c)
-        call("scale_dot", dy, S["t3"], self._slice(P, pre + "beta"), dt3, slab, M, c)
+        call("scale_dot", dy, S["t3"], self._slice(P, pre + "beta"), dt3, slab, M, c, dt)
         self._reduce(slab, gs, c, self._slice(dflat, pre + "beta"))
         # conv3 (input h = g * a)
         dh = E(M, c)
@@ -492,18 +506,18 @@ class NAFNet(nn.Module):
                     self._slice(dflat, pre + "conv3.weight"), self._slice(dflat, pre + "conv3.bias"))
         # SCA
         chunks = query("dw_chunks", B, h, w, c, 0)
-        da_slab = E(B * chunks * c)
-        call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c)
-        da, ds = E(B, c), E(B, c)
+        da_slab = F(B * chunks * c)
+        call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
+        da, ds = F(B, c), F(B, c)
         call("sca_bwd", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], da, ds,
              self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
         dt2 = E(M, 2 * c)
-        call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW)
+        call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW, dt)
         # depthwise conv2
         dt1 = E(M, 2 * c)
-        ws = E(query("dw_bwd_workspace_floats", B, h, w, c))
+        ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
         call("dw_bwd", dt2, S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
-             self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c)
+             self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
         # conv1
         dn1 = E(M, c)
         self._mm(Wt, dt1, 2 * c, AM_PLAIN, None, 1, pre + "conv1.weight", dn1, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
@@ -511,7 +525,7 @@ class NAFNet(nn.Module):
                     self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
         # norm1 + residual
         dx = E(M, c)
-        call("ln_bwd_nhwc", dn1, S["yh1"], S["den1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb, M, c)
+        call("ln_bwd_nhwc", dn1, S["yh1"], S["den1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb, M, c, dt)
         self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))
         return dx.view(B, h, w, c)

@@ -112,7 +112,7 @@ class NBPTrainer:
             ss_ws = torch.empty(query("ssim_workspace_floats", n), device=lq.device)
             call("ssim_loss_fwd", out, gt, B, C, H, W, 11, 1.0, 1, 1, ss_ws, self.loss_buf[1:2])
             call("ssim_loss_bwd", out, gt, B, C, H, W, 1, self.up[1:2], ss_ws, tmp)
-            call("add", d_out, tmp, d_out, n)
+            call("add", d_out, tmp, d_out, n, 0)
         if wph != 0.0 and short is not None:
             if expo_ratio is None:  # ones [B,1,1,1] when the batch has no ratio (image_restoration_model.py:281-287)
                 expo_ratio = torch.ones(B, 1, 1, 1, device=lq.device)
@@ -122,7 +122,7 @@ class NBPTrainer:
             call("phys_l1_fwd", out, short.contiguous(), r, full, self.kernel, self.k_shared, B, C, H, W, 3, 3, 0, 1, 1,
                  1, ph_ws, self.loss_buf[2:3], sign)
             call("phys_l1_bwd", sign, out, self.kernel, self.k_shared, self.up[2:3], B, C, H, W, 3, 3, 0, 1, tmp)
-            call("add", d_out, tmp, d_out, n)
+            call("add", d_out, tmp, d_out, n, 0)
         hook = self._on_stage if self.world > 1 else None
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
         if self.world > 1:

@@ -284,9 +284,33 @@ def test_nafnet_bf16_mode_close_to_reference(dev):
     net.precision = "bf16"
     lq, gt = C(g["lq"], dev), C(g["gt"], dev)
     out = net(lq)
-    err = (out.detach().cpu() - T(g["out"])).abs().max().item()
-    assert err < 3e-2, err
+    ref = T(g["out"])
+    diff = out.detach().cpu() - ref
+    rel_rms = (diff.norm() / ref.norm()).item()
+    assert rel_rms < 1e-2 and diff.abs().max().item() < 0.1, (rel_rms, diff.abs().max().item())
     L1 = l1_loss(out, gt)
     L1.backward()
     assert abs(L1.item() - float(g["L1"])) <= 5e-3 * float(g["L1"])
     assert torch.isfinite(net.flat.grad).all()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_integration_training_loss_decreases(dev, precision):
+    """core_tests/test_integration_forward_amp.py:88-136 re-expressed: 5 steps on one batch, the loss decreases and
+    the PSF buffer is unchanged."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    torch.manual_seed(0)
+    net = create_newbp_net(in_channels=3, width=16, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]).to(dev)
+    net.precision = precision
+    tr = NBPTrainer(net, w_l1=1.0, w_ssim=0.05, w_phys=0.1, lr=1e-3, max_norm=None)
+    k0 = tr.kernel.clone()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    lq = torch.rand(2, 3, 64, 64, device=dev, generator=gen)
+    gt = (lq * 1.3).clamp(0, 1)
+    losses = []
+    for _ in range(5):
+        tr.step(lq, gt, lq, torch.ones(2, 1, 1, 1, device=dev))
+        losses.append(tr.logs()["Total"])
+    assert losses[-1] < losses[0], losses
+    assert torch.equal(tr.kernel, k0)
