@@ -265,6 +265,105 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
 
+// bf16 storage: v_mfma_f32_32x32x16_bf16 with both operands read transposed from natural row-major LDS images by
+// ds_read_b64_tr_b16 (the reduction index m is the ROW of G and X).  Lane 4q+p of a 16-lane group supplies the
+// address of row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.  Two reads give the
+// 8 consecutive-m values of one fragment.  Rows are padded to 96 elements (192 B) so the four rows x two groups of
+// a half-wave hit 64 distinct banks.
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+template <int GMODE, int XMODE>
+__global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
+  constexpr int RM = 32, TNW = 64, TKW = 64, LS = 96;
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[RM * LS];
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[RM * LS];
+  const __bf16* G = reinterpret_cast<const __bf16*>(p.G);
+  const __bf16* X = reinterpret_cast<const __bf16*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * TNW, k0 = blockIdx.y * TKW, s = blockIdx.z;
+  const int mb = s * p.chunk;
+  const int me = min(p.M, mb + p.chunk);
+  const bool do_b = p.slab_b && blockIdx.y == 0;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bsum = 0.f;
+  // loader: one 16-byte chunk of G and one of X per thread: row r = tid >> 3, 8 columns at (tid & 7) * 8
+  const int lr = tid >> 3, lc = (tid & 7) * 8;
+  bf16x8 rg, rx;
+  auto load = [&](int m0) {
+    const int m = m0 + lr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rg[j] = rx[j] = (__bf16)0.f;
+    if (m < me) {
+      const int n = n0 + lc, k = k0 + lc;
+      if (n < p.N) {
+        const long off = GMODE == AM_S2D ? s2d_off(m, n, p.gh, p.gw, p.cs_g) : (long)m * p.ldg + n;
+        rg = *reinterpret_cast<const bf16x8*>(G + off);
+      }
+      if (k < p.K) {
+        const long off = XMODE == AM_S2D ? s2d_off(m, k, p.gh, p.gw, p.cs_x) : (long)m * p.ldx + k;
+        rx = *reinterpret_cast<const bf16x8*>(X + off);
+        if (XMODE == AM_SCALE) {
+          const float* sc = p.x_scale + (long)(m / p.rows_per_img) * p.K + k;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rx[j] = (__bf16)((float)rx[j] * sc[j]);
+        }
+      }
+    }
+  };
+  auto store = [&]() {
+    *reinterpret_cast<bf16x8*>(Gs + lr * LS + lc) = rg;
+    *reinterpret_cast<bf16x8*>(Xs + lr * LS + lc) = rx;
+  };
+  // tr-read addressing (see header comment)
+  const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
+  const int gcol = wn * 32 + 16 * (grp & 1) + 4 * pp;
+  const int xcol = wk * 32 + 16 * (grp & 1) + 4 * pp;
+  if (mb < me) {
+    load(mb);
+    store();
+    __syncthreads();
+    for (int m0 = mb; m0 < me; m0 += RM) {
+      const bool more = m0 + RM < me;
+      if (more) load(m0 + RM);
+#pragma unroll
+      for (int ks = 0; ks < RM; ks += 16) {
+        bf16x8 a, b;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int row = ks + 8 * h + 4 * t + q;
+          const bf16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Gs + row * LS + gcol));
+          const bf16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Xs + row * LS + xcol));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[4 * t + j] = va[j];
+            b[4 * t + j] = vb[j];
+          }
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+      }
+      if (do_b && tid < TNW) {
+#pragma unroll 8
+        for (int r = 0; r < RM; ++r) bsum += (float)Gs[r * LS + tid];
+      }
+      __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int k = k0 + wk * 32 + (lane & 31);
+    if (n < p.N && k < p.K) p.slab[((long)s * p.N + n) * p.K + k] = acc[r];
+  }
+  if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
+}
+
 // out[b][i] = scale * sum_{s < S} slab[b][s][i].  TY row-lanes per column, each summing a fixed strided subset of
 // rows with 4 independent accumulators, then a fixed-order combine: bitwise reproducible, latency-tolerant.
 template <int TY>
@@ -388,7 +487,17 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
   dim3 grid(cdiv(N, 64), cdiv(K, 64), S_);
   hipStream_t st = S(s);
   bool ok = true;
-  NBP_DISPATCH_T(dtype, {
+  if (dtype == 1) {
+    NBP_REQUIRE(N % 8 == 0 && K % 8 == 0 && (g_mode != AM_S2D || cs_g % 8 == 0) && (x_mode != AM_S2D || cs_x % 8 == 0),
+                "nbp_wgrad_f32(bf16): N, K and S2D channel counts must be multiples of 8");
+    NBP_REQUIRE((g_mode == AM_S2D || ldg % 8 == 0) && (x_mode == AM_S2D || ldx % 8 == 0),
+                "nbp_wgrad_f32(bf16): leading dimensions must be multiples of 8");
+    if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_bf16_kernel<AM_PLAIN, AM_SCALE><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_bf16_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);
+    else ok = false;
+  } else NBP_DISPATCH_T(dtype, {
     if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_PLAIN, AM_PLAIN, T><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_f32_kernel<AM_PLAIN, AM_SCALE, T><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_f32_kernel<AM_PLAIN, AM_S2D, T><<<grid, 256, 0, st>>>(p);

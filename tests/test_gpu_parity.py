@@ -161,7 +161,7 @@ def test_gemm_nt_nn_against_torch(dev, M, N, K):
     db = torch.empty(N, device=dev)
     n_ws = query("wgrad_workspace_floats", M, N, K)
     ws = torch.empty(n_ws, device=dev)
-    call("wgrad_f32", G, N, 0, A, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws)
+    call("wgrad_f32", G, N, 0, A, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws, 0)
     close(dW, (G.double().t() @ A.double()).cpu().numpy(), atol=2e-4, rtol=1e-5)
     close(db, G.double().sum(0).cpu().numpy(), atol=1e-4, rtol=1e-5)
 
@@ -314,3 +314,47 @@ def test_integration_training_loss_decreases(dev, precision):
         losses.append(tr.logs()["Total"])
     assert losses[-1] < losses[0], losses
     assert torch.equal(tr.kernel, k0)
+
+
+def _s2d_rows(full):
+    """[B, 2gh, 2gw, cs] NHWC -> [B*gh*gw, 4*cs] rows (tap order (kh, kw), channel fastest), as s2d_off gathers."""
+    B, H2, W2, cs = full.shape
+    v = full.view(B, H2 // 2, 2, W2 // 2, 2, cs).permute(0, 1, 3, 2, 4, 5)
+    return v.reshape(B * (H2 // 2) * (W2 // 2), 4 * cs)
+
+
+@pytest.mark.parametrize("M,N,K,gmode,xmode", [(4096, 64, 128, 0, 0), (1000, 40, 72, 0, 0), (70000, 128, 64, 0, 0),
+                                              (2048, 64, 64, 0, 2), (512, 128, 128, 0, 1), (512, 64, 128, 1, 0)])
+def test_wgrad_bf16_against_float64(dev, M, N, K, gmode, xmode):
+    """bf16 weight gradient (v_mfma_f32_32x32x16_bf16 on ds_read_b64_tr_b16 fragments): dW = G^T X and db = colsum G
+    on bf16 storage equal float64 math on the bf16 values up to fp32 accumulation (x_scale products are rounded to
+    bf16 before the MFMA, as the kernel feeds them)."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(M + 7 * N + K + gmode)
+    rows, gh, gw, cs_g, cs_x = 64, 0, 0, 0, 0
+    if gmode == 1:  # S2D gradient rows (the down conv's input-grad view)
+        gh, gw, cs_g = 16, 32, N // 4
+        Gf = torch.randn(M // (gh * gw), 2 * gh, 2 * gw, cs_g, device=dev, generator=gen).to(torch.bfloat16)
+        Gm, ldg = _s2d_rows(Gf), 0
+    else:
+        Gf = Gm = torch.randn(M, N, device=dev, generator=gen).to(torch.bfloat16)
+        ldg = N
+    if xmode == 1:  # S2D input rows (the down conv)
+        gh, gw, cs_x = 16, 32, K // 4
+        Xf = torch.randn(M // (gh * gw), 2 * gh, 2 * gw, cs_x, device=dev, generator=gen).to(torch.bfloat16)
+        Xm, ldx = _s2d_rows(Xf), 0
+    else:
+        Xf = Xm = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+        ldx = K
+    xs = torch.rand(M // rows + 1, K, device=dev, generator=gen) if xmode == 2 else None
+    dW = torch.empty(N, K, device=dev)
+    db = torch.empty(N, device=dev)
+    n_ws = query("wgrad_workspace_floats", M, N, K)
+    ws = torch.empty(n_ws, device=dev)
+    # mode codes of the ABI: 0 plain, 1 space-to-depth gather, 2 per-(image, column) scale
+    call("wgrad_f32", Gf, ldg, gmode, Xf, ldx, xmode, xs, rows, M, N, K, gh, gw, cs_g, cs_x, dW, db,
+         ws, n_ws, 1)
+    Xe = Xm.double() if xs is None else (Xm.float() * xs.repeat_interleave(rows, 0)[:M]).to(torch.bfloat16).double()
+    ref = Gm.double().t() @ Xe
+    close(dW, ref.cpu().numpy(), atol=3e-5 * M ** 0.5, rtol=1e-4)
+    close(db, Gm.double().sum(0).cpu().numpy(), atol=3e-5 * M ** 0.5, rtol=1e-4)
