@@ -143,6 +143,12 @@ int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* 
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C);
 int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws,
                int B, int H, int W, int C, int dtype, nbp_stream_t s);
+/* SCA + SimpleGate backward fused into the depthwise backward (NAFNet_arch.py:64-67 adjoint): dt2 is formed in LDS as
+   (dg * t2[:, C:], dg * t2[:, :C]) with dg = dh * a[b] + ds[b] / (H*W), never written to HBM; outputs as nbp_dw_bwd.
+   Requires C % 16 == 0 (bf16) or C % 8 == 0 (fp32); ws as nbp_dw_bwd_workspace_floats. */
+int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const void* t2, const void* t1, const float* wdw,
+                      void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C, int dtype,
+                      nbp_stream_t s);
 
 /* SimpleGate on the FFN half (NAFNet_arch.py:75): g = t[:C]*t[C:], and its backward. */
 int nbp_sg_fwd(const void* t, void* g, long M, int C, int dtype, nbp_stream_t s);

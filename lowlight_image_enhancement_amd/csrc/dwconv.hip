@@ -234,6 +234,202 @@ __global__ void dw_bwd(const T* __restrict__ dt2, const T* __restrict__ t1, cons
   }
 }
 
+// ---------------------------------------------------------------- LDS-tiled depthwise 3x3 backward
+// One block = a TH x TW pixel tile of one image x one 64-byte channel slice (HS gate channels c and their SimpleGate
+// partners C + c, so the fused prologue below can form both halves of dt2 from one gate gradient).  The tile plus a
+// one-pixel halo of dt2 and t1 is staged once in LDS with 16-byte loads (zeros outside the image = the conv's zero
+// padding); each thread then owns one channel quad x one column and walks the TH rows with a 3x3 rolling register
+// window, so LDS is read 6 times per output pixel instead of 18 and HBM once per tile (halo re-read 1.2x).
+//   dt1(p) = sum_t w[t] dt2(p - off_t) ;  dW[c][t] += dt2(p) t1(p + off_t) ;  db[c] += dt2(p)
+// FUSED: dt2 is not materialised; the loader computes dg = dh * a[b] + ds[b] / HW and dt2 = (dg * t2[C:], dg * t2[:C])
+// (SCA + SimpleGate backward, NAFNet_arch.py:64-67) straight into LDS.
+// Per-tile dW/db partials go to slab row b * tiles + tile (disjoint channel columns per slice), reduced in fixed order.
+struct DwTileP {
+  const void* dt2;  // [M][2C]           (unfused)
+  const void* dh;   // [M][C]            (fused)
+  const float* a;   // [B][C]            (fused)
+  const float* ds;  // [B][C]            (fused)
+  const void* t2;   // [M][2C]           (fused)
+  const void* t1;   // [M][2C]
+  const float* wdw; // [2C][9]
+  void* dt1;        // [M][2C]
+  float* slab_w;    // [rows][2C][9]
+  float* slab_b;    // [rows][2C]
+  int B, H, W, C, tiles_x, tiles, slices;
+  float inv_hw;
+};
+
+constexpr int DWT_TH = 16, DWT_TW = 32;
+
+template <typename T>
+__device__ __forceinline__ void ld16f(const T* p, float* f) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+  } else {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st16f(T* p, const float* f) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  } else {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)f[j];
+    *reinterpret_cast<bf16x8*>(p) = v;
+  }
+}
+
+template <typename T, bool FUSED>
+__global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
+  constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
+  constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
+  constexpr int HS = CSL / 2;            // gate channels per slice
+  constexpr int NQ = CSL / 4;            // channel quads per slice
+  constexpr int NT = NQ * DWT_TW;        // threads
+  constexpr int LW = DWT_TW + 2, LH = DWT_TH + 2;
+  __shared__ __attribute__((aligned(16))) T sg[LH * LW * CSL];
+  __shared__ __attribute__((aligned(16))) T sx[LH * LW * CSL];
+  const int tid = threadIdx.x;
+  const int slice = blockIdx.x % p.slices, tile = blockIdx.x / p.slices, b = blockIdx.y;
+  const int y0 = (tile / p.tiles_x) * DWT_TH, x0 = (tile % p.tiles_x) * DWT_TW;
+  const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
+  const long img = (long)b * H * W;
+  const int cbase = slice * HS;
+  // ---- stage t1 (and dt2 when unfused): 4 chunks per pixel = 2 halves x 2 chunks
+  {
+    const T* t1 = reinterpret_cast<const T*>(p.t1);
+    const T* dt2 = reinterpret_cast<const T*>(p.dt2);
+    for (int i = tid; i < LH * LW * 4; i += NT) {
+      const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
+      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+      const int lo = pix * CSL + hh * HS + k * E;
+      uint4 vx = make_uint4(0, 0, 0, 0), vg = make_uint4(0, 0, 0, 0);
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const long go = (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E;
+        vx = *reinterpret_cast<const uint4*>(t1 + go);
+        if (!FUSED) vg = *reinterpret_cast<const uint4*>(dt2 + go);
+      }
+      *reinterpret_cast<uint4*>(sx + lo) = vx;
+      if (!FUSED) *reinterpret_cast<uint4*>(sg + lo) = vg;
+    }
+  }
+  if (FUSED) {
+    const T* dh = reinterpret_cast<const T*>(p.dh);
+    const T* t2 = reinterpret_cast<const T*>(p.t2);
+    for (int i = tid; i < LH * LW * 2; i += NT) {
+      const int pix = i >> 1, k = i & 1;
+      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+      float lo[E], hi[E];
+#pragma unroll
+      for (int j = 0; j < E; ++j) lo[j] = hi[j] = 0.f;
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+        const long m = img + (long)gy * W + gx;
+        const int c = cbase + k * E;
+        float d[E], ta[E], tb[E];
+        ld16f(dh + m * C + c, d);
+        ld16f(t2 + m * C2 + c, ta);
+        ld16f(t2 + m * C2 + C + c, tb);
+        const float* av = p.a + (long)b * C + c;
+        const float* sv = p.ds + (long)b * C + c;
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          const float dg = fmaf(d[j], av[j], sv[j] * p.inv_hw);
+          lo[j] = dg * tb[j];
+          hi[j] = dg * ta[j];
+        }
+      }
+      st16f(sg + pix * CSL + k * E, lo);
+      st16f(sg + pix * CSL + HS + k * E, hi);
+    }
+  }
+  __syncthreads();
+  // ---- compute: thread = (quad q, column x)
+  const int q = tid % NQ, x = tid / NQ;
+  const int lc = 4 * q;
+  const int gc = lc < HS ? cbase + lc : C + cbase + (lc - HS);
+  float wk[4][9];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wk[j][t] = p.wdw[(gc + j) * 9 + t];
+  float4 aw[9], ab = f4(0.f);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) aw[t] = f4(0.f);
+  float4 gw[3][3], xw[3][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    gw[1][j] = ldq(sg + (0 * LW + x + j) * CSL + lc);
+    gw[2][j] = ldq(sg + (1 * LW + x + j) * CSL + lc);
+    xw[1][j] = ldq(sx + (0 * LW + x + j) * CSL + lc);
+    xw[2][j] = ldq(sx + (1 * LW + x + j) * CSL + lc);
+  }
+  T* dt1 = reinterpret_cast<T*>(p.dt1);
+  const bool col_ok = x0 + x < W;
+#pragma unroll
+  for (int r = 0; r < DWT_TH; ++r) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      gw[0][j] = gw[1][j]; gw[1][j] = gw[2][j];
+      xw[0][j] = xw[1][j]; xw[1][j] = xw[2][j];
+      gw[2][j] = ldq(sg + ((r + 2) * LW + x + j) * CSL + lc);
+      xw[2][j] = ldq(sx + ((r + 2) * LW + x + j) * CSL + lc);
+    }
+    float4 acc = f4(0.f);
+    const float4 gc4 = gw[1][1];
+#pragma unroll
+    for (int dh = -1; dh <= 1; ++dh)
+#pragma unroll
+      for (int dw = -1; dw <= 1; ++dw) {
+        const int t = (dh + 1) * 3 + (dw + 1);
+        const float4 gv = gw[1 - dh][1 - dw];
+        acc.x = fmaf(wk[0][t], gv.x, acc.x); acc.y = fmaf(wk[1][t], gv.y, acc.y);
+        acc.z = fmaf(wk[2][t], gv.z, acc.z); acc.w = fmaf(wk[3][t], gv.w, acc.w);
+        aw[t] = fma4(gc4, xw[1 + dh][1 + dw], aw[t]);
+      }
+    ab += gc4;
+    if (col_ok && y0 + r < H) stq(dt1 + (img + (long)(y0 + r) * W + x0 + x) * C2 + gc, acc);
+  }
+  // ---- reduce the 40 partials over the tile's columns: lanes of one quad differ in bits >= log2(NQ)
+  float v[40];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) {
+    const float4 a4 = t < 9 ? aw[t] : ab;
+    v[4 * t] = a4.x; v[4 * t + 1] = a4.y; v[4 * t + 2] = a4.z; v[4 * t + 3] = a4.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 40; ++i)
+#pragma unroll
+    for (int o = NQ; o < 64; o <<= 1) v[i] += __shfl_xor(v[i], o, 64);
+  __syncthreads();  // tiles are dead: reuse sg as the cross-wave buffer
+  float* red = reinterpret_cast<float*>(sg);
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = NT / 64;
+  if (lane < NQ) {
+#pragma unroll
+    for (int i = 0; i < 40; ++i) red[(wave * NQ + lane) * 40 + i] = v[i];
+  }
+  __syncthreads();
+  const long row = (long)b * p.tiles + tile;
+  for (int i = tid; i < NQ * 40; i += NT) {
+    const int qq = i / 40, e = i % 40, t = e >> 2, j = e & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[(w * NQ + qq) * 40 + e];
+    const int l = 4 * qq + j;
+    const int ch = l < HS ? cbase + l : C + cbase + (l - HS);
+    if (t < 9) p.slab_w[(row * C2 + ch) * 9 + t] = s;
+    else p.slab_b[row * C2 + ch] = s;
+  }
+}
+
+int dw_tiles(int H, int W) { return cdiv(H, DWT_TH) * cdiv(W, DWT_TW); }
+bool dw_tiled_ok(int C, int dtype) { return C % (dtype == 1 ? 16 : 8) == 0; }
+
 int block_for_quads(int Q) {
   if (Q >= 256) return Q;  // one pixel per step, one thread per quad (Q <= 1024)
   return 256;
@@ -252,6 +448,30 @@ Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
   g.chunk_px = px;
   g.chunks = (HW + px - 1) / px;
   return g;
+}
+
+int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float* ds, const void* t2, const void* t1,
+                    const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C,
+                    int dtype, nbp_stream_t s) {
+  const int hs = dtype == 1 ? 16 : 8;
+  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, DWT_TW), dw_tiles(H, W), C / hs,
+            1.f / (float)(H * W)};
+  const long nrow = (long)B * p.tiles;
+  p.slab_w = ws;
+  p.slab_b = ws + nrow * 2 * C * 9;
+  NBP_REQUIRE((long)p.tiles * p.slices < (1L << 31) && B <= 65535, "dw_bwd: grid too large");
+  dim3 grid(p.tiles * p.slices, B);
+  const bool fused = dh != nullptr;
+  NBP_DISPATCH_T(dtype, {
+    constexpr int NT = (64 / sizeof(T)) / 4 * DWT_TW;
+    if (fused) dw_bwd_tiled<T, true><<<grid, NT, 0, S(s)>>>(p);
+    else dw_bwd_tiled<T, false><<<grid, NT, 0, S(s)>>>(p);
+  });
+  int rc = check_launch("dw_bwd_tiled");
+  if (rc) return rc;
+  rc = nbp_reduce_slab(p.slab_w, (int)nrow, 2L * C * 9, dwdw, s);
+  if (rc) return rc;
+  return nbp_reduce_slab(p.slab_b, (int)nrow, 2L * C, dbdw, s);
 }
 
 }  // namespace
@@ -320,12 +540,15 @@ int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* 
 }
 
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
-  return (size_t)B * nbp_dw_chunks(B, H, W, C, 1) * 2 * C * 10;
+  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * dw_tiles(H, W);
+  return (a > t ? a : t) * 2 * C * 10;
 }
 
 int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws,
                int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dt2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && C % 2 == 0, "nbp_dw_bwd: bad args");
+  if (dw_tiled_ok(C, dtype)) return launch_dw_tiled(dt2, nullptr, nullptr, nullptr, nullptr, t1, wdw, dt1, dwdw, dbdw, ws,
+                                                     B, H, W, C, dtype, s);
   const int Q = C / 2;  // quads over 2C channels
   NBP_REQUIRE(Q <= 1024, "nbp_dw_bwd: too many channels");
   const int blk = block_for_quads(Q);
@@ -342,6 +565,17 @@ int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, flo
   rc = nbp_reduce_slab(slab_w, (int)nrow, 2L * C * 9, dwdw, s);
   if (rc) return rc;
   return nbp_reduce_slab(slab_b, (int)nrow, 2L * C, dbdw, s);
+}
+
+// SCA + SimpleGate backward fused into the depthwise backward (dt2 never materialised):
+// dt2 = (dg * t2[C:], dg * t2[:C]) with dg = dh * a[b] + ds[b] / HW, then dt1 / dW / db as nbp_dw_bwd.
+int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const void* t2, const void* t1, const float* wdw,
+                      void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C, int dtype,
+                      nbp_stream_t s) {
+  NBP_REQUIRE(dh && a && ds && t2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
+              "nbp_sca_sg_dw_bwd: bad args");
+  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd: C must be a multiple of %d", dtype == 1 ? 16 : 8);
+  return launch_dw_tiled(nullptr, dh, a, ds, t2, t1, wdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
 }
 
 }  // extern "C"

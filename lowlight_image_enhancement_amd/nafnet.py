@@ -511,13 +511,17 @@ class NAFNet(nn.Module):
         da, ds = F(B, c), F(B, c)
         call("sca_bwd", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], da, ds,
              self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
-        dt2 = E(M, 2 * c)
-        call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW, dt)
-        # depthwise conv2
+        # SimpleGate + depthwise conv2 (fused when the channel slicing allows: dt2 stays in LDS)
         dt1 = E(M, 2 * c)
         ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
-        call("dw_bwd", dt2, S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
-             self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
+        dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
+                   self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
+        if c % (16 if dt == 1 else 8) == 0:
+            call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
+        else:
+            dt2 = E(M, 2 * c)
+            call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW, dt)
+            call("dw_bwd", dt2, *dw_args)
         # conv1
         dn1 = E(M, c)
         self._mm(Wt, dt1, 2 * c, AM_PLAIN, None, 1, pre + "conv1.weight", dn1, c, CM_PLAIN, M, c, 2 * c, dgrad=True)

@@ -358,3 +358,50 @@ def test_wgrad_bf16_against_float64(dev, M, N, K, gmode, xmode):
     ref = Gm.double().t() @ Xe
     close(dW, ref.cpu().numpy(), atol=3e-5 * M ** 0.5, rtol=1e-4)
     close(db, Gm.double().sum(0).cpu().numpy(), atol=3e-5 * M ** 0.5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (1, 16, 32, 8, 0), (2, 33, 70, 32, 1), (3, 8, 8, 64, 1),
+                                           (2, 19, 23, 12, 0)])
+def test_dw_bwd_against_float64(dev, B, H, W, C, dtype):
+    """Depthwise 3x3 backward (tiled LDS kernel; C=12 exercises the untiled kernel) and the fused SCA+SimpleGate
+    prologue variant vs float64 autograd of F.conv2d(groups=2C) on the same (dtype-rounded) tensors."""
+    import torch.nn.functional as Fn
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(B * H + W * C + dtype)
+    td = torch.bfloat16 if dtype == 1 else torch.float32
+    M, C2 = B * H * W, 2 * C
+    t1 = torch.randn(M, C2, device=dev, generator=gen).to(td)
+    dt2 = torch.randn(M, C2, device=dev, generator=gen).to(td)
+    w = torch.randn(C2, 9, device=dev, generator=gen)
+    ws = torch.empty(query("dw_bwd_workspace_floats", B, H, W, C), device=dev)
+    dt1 = torch.empty(M, C2, device=dev, dtype=td)
+    dW, db = torch.empty(C2, 9, device=dev), torch.empty(C2, device=dev)
+
+    def ref(dt2_nhwc):
+        x = t1.double().view(B, H, W, C2).permute(0, 3, 1, 2).requires_grad_(True)
+        wt = w.double().view(C2, 1, 3, 3).requires_grad_(True)
+        bias = torch.zeros(C2, dtype=torch.float64, device=dev, requires_grad=True)
+        y = Fn.conv2d(x, wt, bias, padding=1, groups=C2)
+        y.backward(dt2_nhwc.double().view(B, H, W, C2).permute(0, 3, 1, 2))
+        return x.grad.permute(0, 2, 3, 1).reshape(M, C2), wt.grad.view(C2, 9), bias.grad
+
+    tol = dict(atol=2e-2, rtol=1e-2) if dtype == 1 else dict(atol=1e-4, rtol=1e-5)
+    call("dw_bwd", dt2, t1, w, dt1, dW, db, ws, B, H, W, C, dtype)
+    rx, rw, rb = ref(dt2)
+    close(dt1.float(), rx.cpu().numpy(), **tol)
+    close(dW, rw.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-4)
+    close(db, rb.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-4)
+    if C % (16 if dtype == 1 else 8):
+        return
+    # fused: dt2 = (dg * t2[C:], dg * t2[:C]), dg = dh * a[b] + ds[b] / HW
+    dh = torch.randn(M, C, device=dev, generator=gen).to(td)
+    t2 = torch.randn(M, C2, device=dev, generator=gen).to(td)
+    a = torch.randn(B, C, device=dev, generator=gen)
+    ds = torch.randn(B, C, device=dev, generator=gen)
+    dg = dh.float() * a.repeat_interleave(H * W, 0) + ds.repeat_interleave(H * W, 0) / (H * W)
+    dt2f = torch.cat([dg * t2[:, C:].float(), dg * t2[:, :C].float()], 1).to(td)
+    call("sca_sg_dw_bwd", dh, a, ds, t2, t1, w, dt1, dW, db, ws, B, H, W, C, dtype)
+    rx, rw, rb = ref(dt2f)
+    close(dt1.float(), rx.cpu().numpy(), **tol)
+    close(dW, rw.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-3)
+    close(db, rb.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-3)
