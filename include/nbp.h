@@ -105,6 +105,13 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
                   float* ws, size_t ws_floats, int dtype, nbp_stream_t s);
 /* out[i] = sum_{s<S} slab[s*L + i] (fixed order); batched: out[b][i] = scale * sum_s slab[b][s][i]. */
 int nbp_reduce_slab(const float* slab, int S, long L, float* out, nbp_stream_t s);
+/* Deferred gradient reductions (thread-local): after nbp_grad_reduce_defer(s), scale-1 gradient-slab reductions
+   issued on stream s (nbp_reduce_slab and the internal ones of nbp_wgrad_f32 / nbp_dw_bwd / nbp_sca_sg_dw_bwd /
+   intro / ending / LN backward) are queued; nbp_grad_reduce_flush(stop, s) executes the queue with one launch per
+   48 slabs (bitwise identical to immediate mode) and, if stop, ends deferral.  The caller keeps every queued slab
+   alive and unmodified until the flush. */
+int nbp_grad_reduce_defer(nbp_stream_t s);
+int nbp_grad_reduce_flush(int stop, nbp_stream_t s);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
 /* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC:

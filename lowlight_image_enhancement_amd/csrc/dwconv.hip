@@ -74,18 +74,36 @@ __global__ void dw_sg_pool_fwd(const T* __restrict__ t1, const float* __restrict
   }
 }
 
-// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i]  (one wave per output o)
-__global__ void sca_gemv(const float* __restrict__ mean, const float* __restrict__ wsca, const float* __restrict__ bsca,
-                         float* __restrict__ a_out, int C) {
-  const int b = blockIdx.y;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int o0 = blockIdx.x * 64;
-  const float* mb = mean + (long)b * C;
-  for (int o = o0 + wv; o < min(C, o0 + 64); o += nw) {
-    float acc = 0.f;
-    for (int i = lane; i < C; i += 64) acc = fmaf(wsca[(long)o * C + i], mb[i], acc);
-    acc = wave_sum(acc);
-    if (lane == 0) a_out[(long)b * C + o] = acc + bsca[o];
+// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
+// One wave per output o; W row read once for all images (SCA_NB images per pass, means staged in LDS).
+constexpr int SCA_NB = 16;
+__global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ mean, const float* __restrict__ wsca,
+                                                const float* __restrict__ bsca, float* __restrict__ a_out, int B,
+                                                int C) {
+  extern __shared__ float sm[];  // [SCA_NB][C]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int o = blockIdx.x * 4 + wv;
+  for (int b0 = 0; b0 < B; b0 += SCA_NB) {
+    const int nb = min(SCA_NB, B - b0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nb * C; e += blockDim.x) sm[e] = mean[(long)b0 * C + e];
+    __syncthreads();
+    if (o < C) {
+      float acc[SCA_NB];
+#pragma unroll
+      for (int b = 0; b < SCA_NB; ++b) acc[b] = 0.f;
+      for (int i = lane; i < C; i += 64) {
+        const float w = wsca[(long)o * C + i];
+#pragma unroll
+        for (int b = 0; b < SCA_NB; ++b)
+          if (b < nb) acc[b] = fmaf(w, sm[b * C + i], acc[b]);
+      }
+#pragma unroll
+      for (int b = 0; b < SCA_NB; ++b) {
+        const float v = wave_sum(acc[b]);
+        if (lane == 0 && b < nb) a_out[(long)(b0 + b) * C + o] = v + bsca[o];
+      }
+    }
   }
 }
 
@@ -116,18 +134,52 @@ __global__ void img_chan_dot(const T* __restrict__ x, const T* __restrict__ y, f
   }
 }
 
-// SCA backward, per image: ds[b][i] = sum_o W[o][i] da[b][o]  (da already reduced over chunks)
-__global__ void sca_bwd_ds(const float* __restrict__ da, const float* __restrict__ wsca, float* __restrict__ ds_out,
-                           int C) {
-  extern __shared__ float dab[];
-  const int b = blockIdx.y;
-  for (int o = threadIdx.x; o < C; o += blockDim.x) dab[o] = da[(long)b * C + o];
+// SCA backward: ds[b][i] = sum_o W[o][i] da[b][o]  (da already reduced over chunks).
+// Block = 64 columns x SCA_BW waves splitting the o range (4 loads in flight per lane); W read once for SCA_NB
+// images; fixed-order cross-wave sum.
+constexpr int SCA_BW = 16;
+__global__ __launch_bounds__(1024) void sca_bwd_ds(const float* __restrict__ da, const float* __restrict__ wsca,
+                                                   float* __restrict__ ds_out, int B, int C) {
+  extern __shared__ float sh[];  // da [SCA_NB][C] then partials [SCA_BW][SCA_NB][64]
+  float* sda = sh;
+  float* part = sh + SCA_NB * C;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int b0 = blockIdx.y * SCA_NB, nb = min(SCA_NB, B - b0);
+  for (int e = threadIdx.x; e < SCA_NB * C; e += blockDim.x) sda[e] = e < nb * C ? da[(long)b0 * C + e] : 0.f;
   __syncthreads();
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float acc[SCA_NB];
+#pragma unroll
+  for (int b = 0; b < SCA_NB; ++b) acc[b] = 0.f;
+  const int per = (C + SCA_BW - 1) / SCA_BW, o0 = wv * per, o1 = min(C, o0 + per);
   if (i < C) {
-    float acc = 0.f;
-    for (int o = 0; o < C; ++o) acc = fmaf(wsca[(long)o * C + i], dab[o], acc);
-    ds_out[(long)b * C + i] = acc;
+    int o = o0;
+    for (; o + 3 < o1; o += 4) {
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = wsca[(long)(o + u) * C + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int b = 0; b < SCA_NB; ++b) acc[b] = fmaf(w[u], sda[b * C + o + u], acc[b]);
+    }
+    for (; o < o1; ++o) {
+      const float w = wsca[(long)o * C + i];
+#pragma unroll
+      for (int b = 0; b < SCA_NB; ++b) acc[b] = fmaf(w, sda[b * C + o], acc[b]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < SCA_NB; ++b) part[(wv * SCA_NB + b) * 64 + lane] = acc[b];
+  __syncthreads();
+  for (int e = threadIdx.x; e < nb * 64; e += blockDim.x) {
+    const int b = e >> 6, l = e & 63, ii = blockIdx.x * 64 + l;
+    if (ii < C) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < SCA_BW; ++w) v += part[(w * SCA_NB + b) * 64 + l];
+      ds_out[(long)(b0 + b) * C + ii] = v;
+    }
   }
 }
 
@@ -505,7 +557,8 @@ int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const flo
   NBP_REQUIRE(pool_slab && wsca && bsca && mean && a && B > 0 && C > 0 && chunks > 0, "nbp_sca_fwd: bad args");
   int rc = nbp_reduce_slab_batched(pool_slab, B, chunks, C, 1.f / (float)HW, mean, s);
   if (rc) return rc;
-  sca_gemv<<<dim3(cdiv(C, 64), B), 256, 0, S(s)>>>(mean, wsca, bsca, a, C);
+  NBP_REQUIRE(C <= 1024, "nbp_sca_fwd: C <= 1024");
+  sca_gemv<<<cdiv(C, 4), 256, (size_t)SCA_NB * C * sizeof(float), S(s)>>>(mean, wsca, bsca, a, B, C);
   return check_launch("sca_fwd");
 }
 
@@ -523,7 +576,9 @@ int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float
   NBP_REQUIRE(da_slab && wsca && mean && da && ds && dwsca && dbsca && B > 0 && C > 0, "nbp_sca_bwd: bad args");
   int rc = nbp_reduce_slab_batched(da_slab, B, chunks, C, 1.f, da, s);
   if (rc) return rc;
-  sca_bwd_ds<<<dim3(cdiv(C, 256), B), 256, C * sizeof(float), S(s)>>>(da, wsca, ds, C);
+  NBP_REQUIRE(C <= 1024, "nbp_sca_bwd: C <= 1024");
+  sca_bwd_ds<<<dim3(cdiv(C, 64), cdiv(B, SCA_NB)), 64 * SCA_BW,
+               ((size_t)SCA_NB * C + SCA_BW * SCA_NB * 64) * sizeof(float), S(s)>>>(da, wsca, ds, B, C);
   const long tot = (long)C * C;
   sca_bwd_b<<<cdiv(tot, 256) > 2048 ? 2048 : cdiv(tot, 256), 256, 0, S(s)>>>(da, mean, B, C, dwsca, dbsca);
   return check_launch("sca_bwd");

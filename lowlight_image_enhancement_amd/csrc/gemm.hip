@@ -3,6 +3,8 @@
 //   as a GEMM over a space-to-depth gather), the 1x1 up conv + PixelShuffle(2) (:117-122, as a GEMM whose
 //   epilogue scatters depth-to-space and adds the skip, :148-149), and their dgrad / wgrad.
 // v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation (one rounding per fma).
+#include <vector>
+
 #include "nbp_common.h"
 
 using namespace nbp;
@@ -395,12 +397,91 @@ __global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restric
   }
 }
 
+int reduce_ty(int S, long L) { return (L < 4096 && S >= 64) ? 16 : 4; }
+
 void launch_reduce(const float* slab, int batch, int S, long L, float scale, float* out, hipStream_t st) {
-  if (L < 4096 && S >= 64) {
+  if (reduce_ty(S, L) == 16) {
     reduce_slab_kernel<16><<<dim3(cdiv(L, 16), batch), 256, 0, st>>>(slab, S, L, scale, out);
   } else {
     reduce_slab_kernel<4><<<dim3(cdiv(L, 64), batch), 256, 0, st>>>(slab, S, L, scale, out);
   }
+}
+
+// ---------------------------------------------------------------- deferred gradient reductions
+// While deferral is on for a stream, gradient-slab reductions issued on it are queued and later executed by ONE
+// launch of reduce_multi_kernel (descriptors passed by value in the kernel arguments).  Each descriptor is reduced
+// with exactly the row-lane split and summation order reduce_slab_kernel would use: results are bitwise identical
+// to immediate mode.  The queue is thread-local; callers keep the slabs alive until the flush.
+struct RDesc {
+  const float* slab;
+  float* out;
+  long L;
+  int S, ty, blk0, pad;
+};
+constexpr int RB_MAX = 48;
+struct RBatch {
+  RDesc d[RB_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
+  __shared__ float red[16 * 17 + 16];
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < rb.n && rb.d[k + 1].blk0 <= bid) ++k;
+  const float* base = rb.d[k].slab;
+  const long L = rb.d[k].L;
+  const int S = rb.d[k].S, TY = rb.d[k].ty, TX = 256 / TY;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const long col = (long)(bid - rb.d[k].blk0) * TX + tx;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < L) {
+    int s = ty;
+    for (; s + 3 * TY < S; s += 4 * TY) {
+      a0 += base[(long)s * L + col];
+      a1 += base[(long)(s + TY) * L + col];
+      a2 += base[(long)(s + 2 * TY) * L + col];
+      a3 += base[(long)(s + 3 * TY) * L + col];
+    }
+    for (; s < S; s += TY) a0 += base[(long)s * L + col];
+  }
+  red[ty * (TX + 1) + tx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (ty == 0 && col < L) {
+    float t = 0.f;
+    for (int j = 0; j < TY; ++j) t += red[j * (TX + 1) + tx];
+    rb.d[k].out[col] = t;
+  }
+}
+
+thread_local std::vector<RDesc> g_pending;
+thread_local bool g_defer = false;
+thread_local hipStream_t g_defer_stream = nullptr;
+
+// scale-1 reduction of a gradient slab: queued while deferral is on for this stream, launched otherwise
+void grad_reduce(const float* slab, int S, long L, float* out, hipStream_t st) {
+  if (g_defer && st == g_defer_stream) {
+    g_pending.push_back(RDesc{slab, out, L, S, reduce_ty(S, L), 0, 0});
+    return;
+  }
+  launch_reduce(slab, 1, S, L, 1.f, out, st);
+}
+
+void flush_pending() {
+  size_t i = 0;
+  while (i < g_pending.size()) {
+    RBatch rb;
+    rb.n = 0;
+    int blocks = 0;
+    for (; i < g_pending.size() && rb.n < RB_MAX; ++i) {
+      RDesc d = g_pending[i];
+      d.blk0 = blocks;
+      blocks += cdiv(d.L, 256 / d.ty);
+      rb.d[rb.n++] = d;
+    }
+    reduce_multi_kernel<<<blocks, 256, 0, g_defer_stream>>>(rb);
+  }
+  g_pending.clear();
 }
 
 template <int BM, int BN, bool B_NK, int AMODE, int CMODE>
@@ -505,14 +586,14 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
     else ok = false;
   });
   if (!ok) { set_error("nbp_wgrad_f32: unsupported mode combination"); return NBP_ERR_ARG; }
-  launch_reduce(slab, 1, S_, (long)N * K, 1.f, dW, st);
-  if (db) launch_reduce(slab_b, 1, S_, N, 1.f, db, st);
+  grad_reduce(slab, S_, (long)N * K, dW, st);
+  if (db) grad_reduce(slab_b, S_, N, db, st);
   return check_launch("wgrad_f32");
 }
 
 int nbp_reduce_slab(const float* slab, int S_, long L, float* out, nbp_stream_t s) {
   NBP_REQUIRE(slab && out && S_ > 0 && L > 0, "nbp_reduce_slab: bad args");
-  launch_reduce(slab, 1, S_, L, 1.f, out, S(s));
+  grad_reduce(slab, S_, L, out, S(s));
   return check_launch("reduce_slab");
 }
 
@@ -520,6 +601,21 @@ int nbp_reduce_slab_batched(const float* slab, int batch, int S_, long L, float 
   NBP_REQUIRE(slab && out && batch > 0 && batch <= 65535 && S_ > 0 && L > 0, "nbp_reduce_slab_batched: bad args");
   launch_reduce(slab, batch, S_, L, scale, out, S(s));
   return check_launch("reduce_slab_batched");
+}
+
+int nbp_grad_reduce_defer(nbp_stream_t s) {
+  NBP_REQUIRE(!g_defer || g_pending.empty() || g_defer_stream == S(s),
+              "nbp_grad_reduce_defer: reductions pending on another stream");
+  g_defer = true;
+  g_defer_stream = S(s);
+  return NBP_OK;
+}
+
+int nbp_grad_reduce_flush(int stop, nbp_stream_t s) {
+  NBP_REQUIRE(!g_defer || g_defer_stream == S(s), "nbp_grad_reduce_flush: deferral is active on another stream");
+  if (g_defer) flush_pending();
+  if (stop) g_defer = false;
+  return check_launch("grad_reduce_flush");
 }
 
 }  // extern "C"

@@ -82,13 +82,50 @@ __device__ __forceinline__ bf16x8 load8(const void* A, long off, const float* sc
   return r;
 }
 
-template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC>
+// 8 consecutive fp32 values -> storage type (16 bytes bf16 / 32 bytes fp32) and back
+template <typename T>
+__device__ __forceinline__ void ld8f(const void* base, long off, float* v) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = ld4(reinterpret_cast<const float*>(base) + off), b = ld4(reinterpret_cast<const float*>(base) + off + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    const bf16x8 r = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(base) + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)r[j];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st8f(void* base, long off, const float* v) {
+  if constexpr (sizeof(T) == 4) {
+    float* d = reinterpret_cast<float*>(base) + off;
+    st4(d, make_float4(v[0], v[1], v[2], v[3]));
+    st4(d + 4, make_float4(v[4], v[5], v[6], v[7]));
+  } else {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(base) + off) = r;
+  }
+}
+
+// 4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32 MFMA tiles.  K-loop: BK-wide tiles, double-buffered
+// LDS (one barrier per K step; the next tile's global loads are in flight during the current tile's MFMAs).
+// Epilogue: the fp32 accumulators are staged through LDS (aliasing the operand buffers) so that bias / pre-activation /
+// residual R + rscale * v / the C store all move 8 consecutive columns (16 bytes of bf16) per thread.
+template <int BM, int BN, int BK, int AMODE, int CMODE, typename TA, typename TC>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
-  constexpr int BK = 32, LS = 40;  // 80-byte LDS rows: conflict-free 16-byte fragment reads
+  constexpr int LS = BK + 8;  // 80 / 144-byte LDS rows: conflict-free 16-byte fragment reads
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int A_IT = BM / 64, B_IT = BN / 64;  // 8-element chunks per thread per K-tile
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * LS];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * LS];
+  constexpr int KC = BK / 8;  // 8-element chunks per tile row
+  constexpr int A_IT = BM * KC / 256, B_IT = BN * KC / 256;
+  constexpr int AB_BYTES = 2 * (BM + BN) * LS * 2;
+  constexpr int CLS = BN + 4;  // fp32 C-tile row stride
+  constexpr int C_BYTES = BM * CLS * 4;
+  constexpr int SM_BYTES = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
+  __bf16* As = reinterpret_cast<__bf16*>(smem);       // [2][BM][LS]
+  __bf16* Bs = As + 2 * BM * LS;                       // [2][BN][LS]
+  float* Cs = reinterpret_cast<float*>(smem);          // [BM][CLS] (after the K loop)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
@@ -107,7 +144,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int idx = tid + it * 256;
-      const int r = idx >> 2, kc = idx & 3;
+      const int r = idx / KC, kc = idx % KC;
       const int m = m0 + r, k = k0 + kc * 8;
       bf16x8 v;
 #pragma unroll
@@ -124,7 +161,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int idx = tid + it * 256;
-      const int r = idx >> 2, kc = idx & 3;
+      const int r = idx / KC, kc = idx % KC;
       const int n = n0 + r, k = k0 + kc * 8;
       bf16x8 v;
 #pragma unroll
@@ -133,68 +170,103 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       rb[it] = v;
     }
   };
-  auto store_tiles = [&]() {
+  auto store_tiles = [&](int buf) {
+    __bf16* a = As + buf * BM * LS;
+    __bf16* b = Bs + buf * BN * LS;
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int idx = tid + it * 256;
-      *reinterpret_cast<bf16x8*>(As + (idx >> 2) * LS + (idx & 3) * 8) = ra[it];
+      *reinterpret_cast<bf16x8*>(a + (idx / KC) * LS + (idx % KC) * 8) = ra[it];
     }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int idx = tid + it * 256;
-      *reinterpret_cast<bf16x8*>(Bs + (idx >> 2) * LS + (idx & 3) * 8) = rb[it];
+      *reinterpret_cast<bf16x8*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
     }
   };
 
   const int nk = (K + BK - 1) / BK;
   load_tiles(0);
-  store_tiles();
+  store_tiles(0);
   __syncthreads();
   const int arow = wm * (BM / 2) + (lane & 31);
   const int brow = wn * (BN / 2) + (lane & 31);
   const int kh = (lane >> 5) * 8;
   for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
     if (t + 1 < nk) load_tiles((t + 1) * BK);
+    const __bf16* a_s = As + buf * BM * LS;
+    const __bf16* b_s = Bs + buf * BN * LS;
 #pragma unroll
     for (int s = 0; s < BK; s += 16) {
       bf16x8 a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (arow + i * 32) * LS + s + kh);
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(a_s + (arow + i * 32) * LS + s + kh);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (brow + j * 32) * LS + s + kh);
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(b_s + (brow + j * 32) * LS + s + kh);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    if (t + 1 < nk) store_tiles(buf ^ 1);
     __syncthreads();
-    if (t + 1 < nk) {
-      store_tiles();
-      __syncthreads();
-    }
   }
 
+  // ---- epilogue through LDS
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * (BN / 2) + j * 32 + (lane & 31);
-      if (col >= N) continue;
-      const float bcol = p.bias ? p.bias[col] : 0.f;
-      const float scol = p.rscale ? p.rscale[col] : 1.f;
+      const int col = wn * (BN / 2) + j * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row >= M) continue;
-        long off;
-        if (CMODE == CM_D2S) off = s2d_off(row, col, p.gh, p.gw, p.cs);
-        else off = (long)row * p.ldc + col;
-        float v = acc[i][j][r] + bcol;
-        if (p.pre) stf<TC>(p.pre, off, v);
-        if (p.R) v = ldf<TC>(p.R, off) + scol * v;
-        stf<TC>(p.C, off, v);
+        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        Cs[row * CLS + col] = acc[i][j][r];
       }
     }
+  __syncthreads();
+  constexpr int G8 = BN / 8;
+  const bool vec = (N % 8 == 0) && (CMODE == CM_D2S || p.ldc % 8 == 0);
+  for (int e = tid; e < BM * G8; e += 256) {
+    const int row = e / G8, c8 = (e % G8) * 8;
+    const int grow = m0 + row, gcol = n0 + c8;
+    if (grow >= M || gcol >= N) continue;
+    float v[8];
+    const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
+    v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
+    if (vec) {
+      const long off = CMODE == CM_D2S ? s2d_off(grow, gcol, p.gh, p.gw, p.cs) : (long)grow * p.ldc + gcol;
+      if (p.bias) {
+        const float4 b0 = ld4(p.bias + gcol), b1 = ld4(p.bias + gcol + 4);
+        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      }
+      if (p.pre) st8f<TC>(p.pre, off, v);
+      if (p.R) {
+        float rv[8];
+        ld8f<TC>(p.R, off, rv);
+        if (p.rscale) {
+          const float4 s0 = ld4(p.rscale + gcol), s1 = ld4(p.rscale + gcol + 4);
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = rv[j] + sc[j] * v[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = rv[j] + v[j];
+        }
+      }
+      st8f<TC>(p.C, off, v);
+    } else {
+      for (int j = 0; j < 8 && gcol + j < N; ++j) {
+        const int col = gcol + j;
+        const long off = CMODE == CM_D2S ? s2d_off(grow, col, p.gh, p.gw, p.cs) : (long)grow * p.ldc + col;
+        float x = v[j] + (p.bias ? p.bias[col] : 0.f);
+        if (p.pre) stf<TC>(p.pre, off, x);
+        if (p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
+        stf<TC>(p.C, off, x);
+      }
+    }
+  }
 }
 
 // fp32 flat parameters -> bf16 copy (all), plus transposed bf16 copies of the listed [rows][cols] matrices
@@ -228,17 +300,19 @@ __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long*
 template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC>
 void launch(const GemmPB& p, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
-  gemm_bf16_kernel<BM, BN, AMODE, CMODE, TA, TC><<<grid, 256, 0, st>>>(p);
+  if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC><<<grid, 256, 0, st>>>(p);
+  else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC><<<grid, 256, 0, st>>>(p);
 }
 
+// largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 1024 blocks (4 per CU);
+// otherwise 64x64, the most blocks available.
 template <int AMODE, int CMODE, typename TA, typename TC>
 void dispatch(const GemmPB& p, hipStream_t st) {
-  const bool bn128 = p.N >= 128;
-  const long tiles128 = (long)cdiv(p.M, 128) * cdiv(p.N, bn128 ? 128 : 64);
-  const bool bm128 = tiles128 >= 1024;
-  if (bm128 && bn128) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
-  else if (bm128) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
-  else if (bn128) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
+  auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
+  const bool n128 = p.N > 64, m128 = p.M > 64;
+  if (m128 && n128 && blocks(128, 128) >= 1024) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
+  else if (m128 && blocks(128, 64) >= 1024) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
+  else if (n128 && blocks(64, 128) >= 1024) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
   else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
 }
 

@@ -18,6 +18,7 @@ tensors the backward needs in a tape.
 """
 from __future__ import annotations
 
+import math
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -86,6 +87,7 @@ class NAFNet(nn.Module):
         self.flat = nn.Parameter(torch.zeros(self.numel, dtype=torch.float32))
         self._init_reference_like()
         self.grad_ready_hook: Optional[Callable[[Stage], None]] = None
+        self._keep: Optional[List[torch.Tensor]] = None  # slabs awaiting a deferred gradient reduction
         # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
         # (the reference's AMP training, image_restoration_model.py:255), fp32 storage and statistics.
         self.precision = "fp32"
@@ -387,6 +389,15 @@ class NAFNet(nn.Module):
         """Walk the tape in reverse.  Writes every parameter gradient (exactly once) into dflat, calls
         hook(stage) as each stage's gradient slice is complete, returns d(input) or None."""
         P = self.flat.data if flat is None else flat
+        self._keep = []
+        call("grad_reduce_defer")
+        try:
+            return self._walk_backward(tape, dout, dflat, need_dx, P, hook)
+        finally:
+            call("grad_reduce_flush", 1)
+            self._keep = None
+
+    def _walk_backward(self, tape, dout, dflat, need_dx, P, hook):
         Wt = (P,)
         for rec in tape:
             if rec[0] == "weights":
@@ -401,7 +412,7 @@ class NAFNet(nn.Module):
             if kind == "ending":
                 feat, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
                 dfeat = torch.empty(B, Hp, Wp, w, device=dout.device, dtype=self.adt)
-                ws = torch.empty(query("ending_bwd_workspace_floats", B, Ci, H0, W0, w), device=dout.device)
+                ws = self._ws(query("ending_bwd_workspace_floats", B, Ci, H0, W0, w), dout.device)
                 call("ending_bwd", dout, feat, self._slice(P, "ending.weight"), dfeat,
                      self._slice(dflat, "ending.weight"), self._slice(dflat, "ending.bias"), ws, B, Ci, H0, W0, Hp,
                      Wp, w, self.dt)
@@ -436,7 +447,7 @@ class NAFNet(nn.Module):
                 dfeat = dx
             elif kind == "intro":
                 x, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
-                ws = torch.empty(query("intro_bwd_workspace_floats", B, Ci, Hp, Wp, w), device=dout.device)
+                ws = self._ws(query("intro_bwd_workspace_floats", B, Ci, Hp, Wp, w), dout.device)
                 if need_dx:
                     dx_img = torch.empty(B, Ci, H0, W0, device=dout.device)
                 call("intro_bwd", x, dfeat, self._slice(P, "intro.weight"), self._slice(dflat, "intro.weight"),
@@ -448,12 +459,23 @@ class NAFNet(nn.Module):
         return dx_img
 
     def _stage_done(self, name, hook):
+        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice
+        call("grad_reduce_flush", 0)
+        self._keep.clear()
         if hook is not None:
             hook(self.stages[name])
 
+    def _ws(self, n, dev):
+        """fp32 workspace that stays referenced until the next gradient-reduction flush (deferred reductions read
+        it after this call returns)."""
+        t = torch.empty(n, device=dev)
+        if self._keep is not None:
+            self._keep.append(t)
+        return t
+
     def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db):
         n_ws = query("wgrad_workspace_floats", M, N, K)
-        ws = torch.empty(n_ws, device=G.device)
+        ws = self._ws(n_ws, G.device)
         call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws, n_ws,
              self.dt)
 
@@ -466,7 +488,7 @@ class NAFNet(nn.Module):
         HW = h * w
         dev = dout.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
-        F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
         dt = self.dt
         dout = dout.reshape(M, c)
         # out = y + gamma * t5
@@ -497,6 +519,7 @@ class NAFNet(nn.Module):
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
         # y = x + beta * t3
         dt3 = E(M, c)
+        slab = F(gs * c)
         call("scale_dot", dy, S["t3"], self._slice(P, pre + "beta"), dt3, slab, M, c, dt)
         self._reduce(slab, gs, c, self._slice(dflat, pre + "beta"))
         # conv3 (input h = g * a)
@@ -529,6 +552,7 @@ class NAFNet(nn.Module):
                     self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
         # norm1 + residual
         dx = E(M, c)
+        sw, sb = F(lg * c), F(lg * c)
         call("ln_bwd_nhwc", dn1, S["yh1"], S["den1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb, M, c, dt)
         self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))

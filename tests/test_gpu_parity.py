@@ -249,7 +249,8 @@ def test_nan_fill_every_grad_written(dev):
 
 
 # ---------------------------------------------------------------- bf16 perf mode
-@pytest.mark.parametrize("M,N,K,amode", [(1000, 64, 32, 0), (4096, 1024, 512, 0), (300, 40, 72, 0), (2048, 64, 64, 2)])
+@pytest.mark.parametrize("M,N,K,amode", [(1000, 64, 32, 0), (4096, 1024, 512, 0), (300, 40, 72, 0), (2048, 64, 64, 2),
+                                         (300, 36, 40, 0), (70000, 256, 128, 2), (129, 200, 1024, 0)])
 def test_gemm_bf16_against_torch(dev, M, N, K, amode):
     """bf16 operands, fp32 accumulate: equals float64 math on the bf16-rounded operands up to fp32 summation."""
     from lowlight_image_enhancement_amd._lib import call
