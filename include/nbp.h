@@ -111,6 +111,11 @@ int nbp_reduce_slab(const float* slab, int S, long L, float* out, nbp_stream_t s
    48 slabs (bitwise identical to immediate mode) and, if stop, ends deferral.  The caller keeps every queued slab
    alive and unmodified until the flush. */
 int nbp_grad_reduce_defer(nbp_stream_t s);
+/* Layer-scale residual y = x + s * (h W^T + b) (NAFNet_arch.py:72,80) gradients from U = dy^T h [N][K] and
+   V = colsum(dy) [N] of the UNSCALED dy: dW = s (.) U (row-wise), db = s (.) V, ds = rowsum(W (.) U) + b (.) V.
+   Queued behind the reductions while deferral is on for s (U/V may then be deferred reduction outputs). */
+int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const float* b, const float* scale, float* dW,
+                         float* db, float* dscale, int N, int K, nbp_stream_t s);
 int nbp_grad_reduce_flush(int stop, nbp_stream_t s);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
@@ -133,6 +138,8 @@ int nbp_ln_bwd_nchw(const float* dy, const float* yhat, const float* den, const 
 /* NAFBlock spatial branch: conv2 depthwise 3x3 + bias on 2C channels (NAFNet_arch.py:32-33) -> SimpleGate
  * (:22-25) -> AdaptiveAvgPool2d(1) partial sums (:38) in pool_slab [B][chunks][C]. */
 int nbp_dw_chunks(int B, int H, int W, int C, int which);
+/* Rows per image of the pool_slab nbp_dw_sg_pool_fwd writes for this shape and dtype ([B][rows][C]). */
+int nbp_dw_fwd_slab_rows(int B, int H, int W, int C, int dtype);
 int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
                        int H, int W, int C, int dtype, nbp_stream_t s);
 /* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
@@ -205,6 +212,10 @@ int nbp_grad_clip_coef(const float* grad, long n, float grad_scale, float max_no
 /* torch.optim.AdamW step over the flat buffer with gradient * state[1]. */
 int nbp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
                    float lr, float beta1, float beta2, float eps, float weight_decay, int step, nbp_stream_t s);
+/* The same step with hyper[3] = {lr, lr / (1 - beta1^t), sqrt(1 - beta2^t)} read from device memory (HIP-graph
+   replayable: the host updates hyper between replays). */
+int nbp_adamw_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
+                       const float* hyper, float beta1, float beta2, float eps, float weight_decay, nbp_stream_t s);
 
 #ifdef __cplusplus
 }

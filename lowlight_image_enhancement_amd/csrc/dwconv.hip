@@ -311,7 +311,8 @@ struct DwTileP {
   float inv_hw;
 };
 
-constexpr int DWT_TH = 16, DWT_TW = 32;
+constexpr int DWT_TH = 16;
+inline int dw_bwd_tw(int W) { return W >= 32 ? 32 : 16; }
 
 template <typename T>
 __device__ __forceinline__ void ld16f(const T* p, float* f) {
@@ -336,7 +337,7 @@ __device__ __forceinline__ void st16f(T* p, const float* f) {
   }
 }
 
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, int DWT_TW>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
   constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
@@ -347,7 +348,8 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   __shared__ __attribute__((aligned(16))) T sg[LH * LW * CSL];
   __shared__ __attribute__((aligned(16))) T sx[LH * LW * CSL];
   const int tid = threadIdx.x;
-  const int slice = blockIdx.x % p.slices, tile = blockIdx.x / p.slices, b = blockIdx.y;
+  const int u = xcd_remap(blockIdx.x, gridDim.x);  // the slices of one tile share an XCD (and its L2)
+  const int slice = u % p.slices, tile = (u / p.slices) % p.tiles, b = u / (p.slices * p.tiles);
   const int y0 = (tile / p.tiles_x) * DWT_TH, x0 = (tile % p.tiles_x) * DWT_TW;
   const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
   const long img = (long)b * H * W;
@@ -479,7 +481,120 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   }
 }
 
-int dw_tiles(int H, int W) { return cdiv(H, DWT_TH) * cdiv(W, DWT_TW); }
+// ---------------------------------------------------------------- LDS-tiled depthwise 3x3 + SimpleGate + pool partials
+// Same tiling as the backward: a TH x TW pixel tile x one 64-byte channel slice (HS gate channels c and partners C + c)
+// staged once in LDS with its halo.  Thread = (gate quad, column): it convolves the 4 channels c.. and the 4 partners
+// C + c.. with rolling 3x3 register windows, writes t2 (both halves), g = t2[:C] * t2[C:] and accumulates the pool
+// partial of g, reduced over the tile into pool_slab[b][tile][C] (fixed order).
+struct DwFwdP {
+  const void* t1;
+  const float* wdw;
+  const float* bdw;
+  void* t2;
+  void* g;
+  float* pool_slab;
+  int B, H, W, C, tiles_x, tiles, slices;
+};
+// tile width: 64 / 32 / 16 columns by image width; fp32 (2 gate quads per slice) never below 32 (whole waves)
+inline int dw_fwd_tw(int W, int dtype) { return W >= 64 ? 64 : ((W >= 32 || dtype == 0) ? 32 : 16); }
+int dw_fwd_tiles(int H, int W, int dtype) { return cdiv(H, DWT_TH) * cdiv(W, dw_fwd_tw(W, dtype)); }
+
+template <typename T, int TW>
+__global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
+  constexpr int E = 16 / sizeof(T), CSL = 64 / sizeof(T), HS = CSL / 2, NQG = HS / 4, NT = NQG * TW;
+  constexpr int LW = TW + 2, LH = DWT_TH + 2;
+  __shared__ __attribute__((aligned(16))) T sx[LH * LW * CSL];
+  const int tid = threadIdx.x;
+  const int u = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = u % p.slices, tile = (u / p.slices) % p.tiles, b = u / (p.slices * p.tiles);
+  const int y0 = (tile / p.tiles_x) * DWT_TH, x0 = (tile % p.tiles_x) * TW;
+  const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
+  const long img = (long)b * H * W;
+  const int cbase = slice * HS;
+  {
+    const T* t1 = reinterpret_cast<const T*>(p.t1);
+    for (int i = tid; i < LH * LW * 4; i += NT) {
+      const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
+      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W)
+        v = *reinterpret_cast<const uint4*>(t1 + (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E);
+      *reinterpret_cast<uint4*>(sx + pix * CSL + hh * HS + k * E) = v;
+    }
+  }
+  __syncthreads();
+  const int qg = tid % NQG, x = tid / NQG;
+  const int la = 4 * qg, lb = HS + 4 * qg;       // local channels (LDS)
+  const int gca = cbase + 4 * qg, gcb = C + gca;  // global conv channels
+  float wa[4][9], wb[4][9];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      wa[j][t] = p.wdw[(gca + j) * 9 + t];
+      wb[j][t] = p.wdw[(gcb + j) * 9 + t];
+    }
+  const float4 ba = ld4(p.bdw + gca), bb = ld4(p.bdw + gcb);
+  float4 xa[3][3], xb[3][3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    xa[1][j] = ldq(sx + (0 * LW + x + j) * CSL + la);
+    xa[2][j] = ldq(sx + (1 * LW + x + j) * CSL + la);
+    xb[1][j] = ldq(sx + (0 * LW + x + j) * CSL + lb);
+    xb[2][j] = ldq(sx + (1 * LW + x + j) * CSL + lb);
+  }
+  T* t2 = reinterpret_cast<T*>(p.t2);
+  T* g = reinterpret_cast<T*>(p.g);
+  float4 pacc = f4(0.f);
+  const bool col_ok = x0 + x < W;
+#pragma unroll
+  for (int r = 0; r < DWT_TH; ++r) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      xa[0][j] = xa[1][j]; xa[1][j] = xa[2][j];
+      xb[0][j] = xb[1][j]; xb[1][j] = xb[2][j];
+      xa[2][j] = ldq(sx + ((r + 2) * LW + x + j) * CSL + la);
+      xb[2][j] = ldq(sx + ((r + 2) * LW + x + j) * CSL + lb);
+    }
+    float4 aa = ba, ab = bb;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const float4 va = xa[t / 3][t % 3], vb = xb[t / 3][t % 3];
+      aa.x = fmaf(wa[0][t], va.x, aa.x); aa.y = fmaf(wa[1][t], va.y, aa.y);
+      aa.z = fmaf(wa[2][t], va.z, aa.z); aa.w = fmaf(wa[3][t], va.w, aa.w);
+      ab.x = fmaf(wb[0][t], vb.x, ab.x); ab.y = fmaf(wb[1][t], vb.y, ab.y);
+      ab.z = fmaf(wb[2][t], vb.z, ab.z); ab.w = fmaf(wb[3][t], vb.w, ab.w);
+    }
+    if (col_ok && y0 + r < H) {
+      const long m = img + (long)(y0 + r) * W + x0 + x;
+      stq(t2 + m * C2 + gca, aa);
+      stq(t2 + m * C2 + gcb, ab);
+      const float4 gv = aa * ab;
+      stq(g + m * C + gca, gv);
+      pacc += gv;
+    }
+  }
+  // reduce pacc over the tile's columns (lanes of one gate quad differ in bits >= log2(NQG)), then across waves
+#pragma unroll
+  for (int o = NQG; o < 64; o <<= 1) {
+    pacc.x += __shfl_xor(pacc.x, o, 64); pacc.y += __shfl_xor(pacc.y, o, 64);
+    pacc.z += __shfl_xor(pacc.z, o, 64); pacc.w += __shfl_xor(pacc.w, o, 64);
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(sx);
+  const int lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = (NT + 63) / 64;
+  if (lane < NQG) st4(red + (wave * NQG + lane) * 4, pacc);
+  __syncthreads();
+  if (tid < NQG * 4) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += red[w * NQG * 4 + tid];
+    p.pool_slab[((long)b * p.tiles + tile) * C + cbase + tid] = sum;
+  }
+}
+
+int dw_tiles(int H, int W) { return cdiv(H, DWT_TH) * cdiv(W, dw_bwd_tw(W)); }
 bool dw_tiled_ok(int C, int dtype) { return C % (dtype == 1 ? 16 : 8) == 0; }
 
 int block_for_quads(int Q) {
@@ -506,18 +621,24 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
                     const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C,
                     int dtype, nbp_stream_t s) {
   const int hs = dtype == 1 ? 16 : 8;
-  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, DWT_TW), dw_tiles(H, W), C / hs,
+  const int tw = dw_bwd_tw(W);
+  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W), C / hs,
             1.f / (float)(H * W)};
   const long nrow = (long)B * p.tiles;
   p.slab_w = ws;
   p.slab_b = ws + nrow * 2 * C * 9;
-  NBP_REQUIRE((long)p.tiles * p.slices < (1L << 31) && B <= 65535, "dw_bwd: grid too large");
-  dim3 grid(p.tiles * p.slices, B);
+  const long nblk = nrow * p.slices;
+  NBP_REQUIRE(nblk < (1L << 31), "dw_bwd: grid too large");
   const bool fused = dh != nullptr;
   NBP_DISPATCH_T(dtype, {
-    constexpr int NT = (64 / sizeof(T)) / 4 * DWT_TW;
-    if (fused) dw_bwd_tiled<T, true><<<grid, NT, 0, S(s)>>>(p);
-    else dw_bwd_tiled<T, false><<<grid, NT, 0, S(s)>>>(p);
+    constexpr int NQ = (64 / sizeof(T)) / 4;
+    if (tw == 32) {
+      if (fused) dw_bwd_tiled<T, true, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
+    } else {
+      if (fused) dw_bwd_tiled<T, true, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
+    }
   });
   int rc = check_launch("dw_bwd_tiled");
   if (rc) return rc;
@@ -540,10 +661,29 @@ int nbp_dw_chunks(int B, int H, int W, int C, int which) {
   return make_geo(B, H, W, C, Q, blk, cap).chunks;
 }
 
+int nbp_dw_fwd_slab_rows(int B, int H, int W, int C, int dtype) {
+  if (dw_tiled_ok(C, dtype)) return dw_fwd_tiles(H, W, dtype);
+  return nbp_dw_chunks(B, H, W, C, 0);
+}
+
 int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
                        int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(t1 && wdw && bdw && t2 && g && pool_slab && B > 0 && H > 0 && W > 0, "nbp_dw_sg_pool_fwd: bad args");
   NBP_REQUIRE(C % 4 == 0 && C / 4 <= 1024, "nbp_dw_sg_pool_fwd: C");
+  if (dw_tiled_ok(C, dtype)) {
+    const int tw = dw_fwd_tw(W, dtype), hs = dtype == 1 ? 16 : 8;
+    DwFwdP p{t1, wdw, bdw, t2, g, pool_slab, B, H, W, C, cdiv(W, tw), dw_fwd_tiles(H, W, dtype), C / hs};
+    const long nblk = (long)B * p.tiles * p.slices;
+    NBP_REQUIRE(nblk < (1L << 31), "nbp_dw_sg_pool_fwd: grid too large");
+    NBP_DISPATCH_T(dtype, {
+      constexpr int NQG = (32 / sizeof(T)) / 4;
+      // whole waves only (the column reduction shuffles across all 64 lanes): fp32 uses TW >= 32
+      if (tw == 64) dw_sg_pool_tiled<T, 64><<<nblk, NQG * 64, 0, S(s)>>>(p);
+      else if (tw == 32 || NQG * 16 < 64) dw_sg_pool_tiled<T, 32><<<nblk, NQG * 32, 0, S(s)>>>(p);
+      else dw_sg_pool_tiled<T, 16><<<nblk, NQG * 16, 0, S(s)>>>(p);
+    });
+    return check_launch("dw_sg_pool_tiled");
+  }
   const int Q = C / 4, blk = block_for_quads(Q);
   Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
   dim3 grid(geo.chunks, B);

@@ -454,7 +454,62 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
   }
 }
 
+// Layer-scale gradient post-op (NAFBlock y = x + beta * conv(h), NAFNet_arch.py:72,80), from U = dOut^T h and
+// V = colsum dOut of the UNSCALED output gradient:  dW = s (.) U (rows), db = s (.) V,
+// ds[k] = sum_n W[k][n] U[k][n] + b[k] V[k]   (= sum_m dOut[m][k] * conv(h)[m][k]).
+// One wave per row k; descriptors by value like RBatch; fixed-order wave sum (deterministic).
+struct PDesc {
+  const float *U, *V, *W, *b, *scale;
+  float *dW, *db, *dscale;
+  int N, K, blk0, pad;
+};
+constexpr int PB_MAX = 24;
+struct PBatch {
+  PDesc d[PB_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(64) void layer_scale_grad_kernel(PBatch pb) {
+  const int bid = blockIdx.x;
+  int k = 0;
+  while (k + 1 < pb.n && pb.d[k + 1].blk0 <= bid) ++k;
+  const PDesc& d = pb.d[k];
+  const int row = bid - d.blk0, K = d.K, lane = threadIdx.x;
+  const float sc = d.scale[row];
+  const float* u = d.U + (long)row * K;
+  const float* w = d.W + (long)row * K;
+  float acc = 0.f;
+  for (int i = lane; i < K; i += 64) {
+    const float ui = u[i];
+    acc = fmaf(w[i], ui, acc);
+    d.dW[(long)row * K + i] = sc * ui;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const float v = d.V[row];
+    d.dscale[row] = acc + d.b[row] * v;
+    d.db[row] = sc * v;
+  }
+}
+
+void launch_post(const std::vector<PDesc>& ops, hipStream_t st) {
+  size_t i = 0;
+  while (i < ops.size()) {
+    PBatch pb;
+    pb.n = 0;
+    int blocks = 0;
+    for (; i < ops.size() && pb.n < PB_MAX; ++i) {
+      PDesc d = ops[i];
+      d.blk0 = blocks;
+      blocks += d.N;
+      pb.d[pb.n++] = d;
+    }
+    layer_scale_grad_kernel<<<blocks, 64, 0, st>>>(pb);
+  }
+}
+
 thread_local std::vector<RDesc> g_pending;
+thread_local std::vector<PDesc> g_post;
 thread_local bool g_defer = false;
 thread_local hipStream_t g_defer_stream = nullptr;
 
@@ -482,6 +537,8 @@ void flush_pending() {
     reduce_multi_kernel<<<blocks, 256, 0, g_defer_stream>>>(rb);
   }
   g_pending.clear();
+  launch_post(g_post, g_defer_stream);  // post-ops read reduction outputs: after every reduction of the flush
+  g_post.clear();
 }
 
 template <int BM, int BN, bool B_NK, int AMODE, int CMODE>
@@ -501,11 +558,15 @@ void dispatch_tiles(const GemmP& p, hipStream_t st) {
   else launch_gemm<64, 64, B_NK, AMODE, CMODE>(p, st);
 }
 
+// split-M count: enough blocks to fill the chip (~2048), >= 256 rows per split, and fp32 slab bytes
+// (S * N * K * 4, written once and read once by the reduction) no larger than the operand bytes M * (N + K) * 2.
 int wgrad_splits(int M, int N, int K) {
   const long tiles = (long)cdiv(N, 64) * cdiv(K, 64);
   long s = (2048 + tiles - 1) / tiles;
   const long maxs = cdiv(M, 256);  // keep >= 256 rows per split
   if (s > maxs) s = maxs;
+  const long slab_cap = (long)M * (N + K) / (2L * N * K);
+  if (s > slab_cap) s = slab_cap;
   if (s < 1) s = 1;
   if (s > 1024) s = 1024;
   return (int)s;
@@ -539,6 +600,7 @@ int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int
     if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch_tiles<false, AM_PLAIN, CM_PLAIN>(p, st);
     else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch_tiles<false, AM_PLAIN, CM_D2S>(p, st);
     else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch_tiles<false, AM_S2D, CM_PLAIN>(p, st);
+    else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch_tiles<false, AM_SCALE, CM_PLAIN>(p, st);
     else { set_error("nbp_gemm_f32: unsupported KN mode combination"); return NBP_ERR_ARG; }
   }
   return check_launch("gemm_f32");
@@ -603,8 +665,20 @@ int nbp_reduce_slab_batched(const float* slab, int batch, int S_, long L, float 
   return check_launch("reduce_slab_batched");
 }
 
+int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const float* b, const float* scale, float* dW,
+                         float* db, float* dscale, int N, int K, nbp_stream_t s) {
+  NBP_REQUIRE(U && V && W && b && scale && dW && db && dscale && N > 0 && K > 0, "nbp_layer_scale_grad: bad args");
+  PDesc d{U, V, W, b, scale, dW, db, dscale, N, K, 0, 0};
+  if (g_defer && S(s) == g_defer_stream) {
+    g_post.push_back(d);
+    return NBP_OK;
+  }
+  launch_post(std::vector<PDesc>{d}, S(s));
+  return check_launch("layer_scale_grad");
+}
+
 int nbp_grad_reduce_defer(nbp_stream_t s) {
-  NBP_REQUIRE(!g_defer || g_pending.empty() || g_defer_stream == S(s),
+  NBP_REQUIRE(!g_defer || (g_pending.empty() && g_post.empty()) || g_defer_stream == S(s),
               "nbp_grad_reduce_defer: reductions pending on another stream");
   g_defer = true;
   g_defer_stream = S(s);

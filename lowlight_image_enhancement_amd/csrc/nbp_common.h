@@ -106,6 +106,15 @@ __device__ __forceinline__ double block_sum_d(double v, double* red /*>=16*/) {
   return t;
 }
 
+// Workgroups are dealt round-robin to the 8 XCDs (each with its own L2).  Remap the linear block id so that runs of
+// consecutive LOGICAL ids land on one XCD: blocks that share input cache lines (e.g. channel slices of one pixel tile)
+// then hit the same L2.  Bijective on [0, T): the last T % 8 blocks keep their id.
+__device__ __forceinline__ int xcd_remap(int L, int T) {
+  const int T8 = T & ~7;
+  if (L >= T8) return L;
+  return (L & 7) * (T8 >> 3) + (L >> 3);
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline hipStream_t S(nbp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

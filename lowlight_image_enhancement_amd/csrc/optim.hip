@@ -42,7 +42,12 @@ __global__ void clip_coef_kernel(const double* __restrict__ partial, int nb, flo
 
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, long n, const float* __restrict__ state, float lr, float b1, float b2,
-                             float eps, float wd, float step_size, float bc2_sqrt) {
+                             float eps, float wd, float step_size, float bc2_sqrt, const float* __restrict__ hyper) {
+  if (hyper) {  // graph-replayable form: {lr, lr / bc1, sqrt(bc2)} of this step read from device memory
+    lr = hyper[0];
+    step_size = hyper[1];
+    bc2_sqrt = hyper[2];
+  }
   const float gs = state[1];
   const float decay = 1.f - lr * wd;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -87,8 +92,18 @@ int nbp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_a
   const double bc1 = 1.0 - pow((double)beta1, step);
   const double bc2 = 1.0 - pow((double)beta2, step);
   adamw_kernel<<<grid_for(n), 256, 0, S(s)>>>(param, grad, exp_avg, exp_avg_sq, n, state, lr, beta1, beta2, eps,
-                                              weight_decay, (float)(lr / bc1), (float)sqrt(bc2));
+                                              weight_decay, (float)(lr / bc1), (float)sqrt(bc2), nullptr);
   return check_launch("adamw_step");
+}
+
+// Same step with {lr, lr / (1 - beta1^t), sqrt(1 - beta2^t)} taken from device memory (hyper[3]), so that one
+// captured HIP graph replays every step of a schedule.
+int nbp_adamw_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
+                       const float* hyper, float beta1, float beta2, float eps, float weight_decay, nbp_stream_t s) {
+  NBP_REQUIRE(param && grad && exp_avg && exp_avg_sq && state && hyper && n > 0, "nbp_adamw_step_dev: bad args");
+  adamw_kernel<<<grid_for(n), 256, 0, S(s)>>>(param, grad, exp_avg, exp_avg_sq, n, state, 0.f, beta1, beta2, eps,
+                                              weight_decay, 0.f, 1.f, hyper);
+  return check_launch("adamw_step_dev");
 }
 
 }  // extern "C"

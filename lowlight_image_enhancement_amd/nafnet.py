@@ -338,16 +338,16 @@ class NAFNet(nn.Module):
         t1 = E(M, 2 * c)
         self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv1.bias"))
-        chunks = query("dw_chunks", B, h, w, c, 0)
+        chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
         t2, g, pool = E(M, 2 * c), E(M, c), F(B * chunks * c)
         call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2, g,
              pool, B, h, w, c, dt)
         mean, a = F(B, c), F(B, c)
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
              a, B, h * w, c)
-        y, t3 = E(M, c), E(M, c)
+        y = E(M, c)
         self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
-                 bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"), pre=t3)
+                 bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
         yh2, n2, den2 = E(M, c), E(M, c), F(M)
         call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), yh2, n2,
              den2, M, c, LN_EPS, dt)
@@ -356,12 +356,12 @@ class NAFNet(nn.Module):
                  bias=self._slice(P, pre + "conv4.bias"))
         g2 = E(M, c)
         call("sg_fwd", t4, g2, M, c, dt)
-        out, t5 = E(M, c), E(M, c)
+        out = E(M, c)
         self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
-                 bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"), pre=t5)
+                 bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
         if tape is not None:
             tape.append(("block", pre, (B, h, w, c), dict(x=x, yh1=yh1, n1=n1, den1=den1, t1=t1, t2=t2, g=g, mean=mean,
-                                                           a=a, t3=t3, yh2=yh2, n2=n2, den2=den2, t4=t4, g2=g2, t5=t5)))
+                                                           a=a, yh2=yh2, n2=n2, den2=den2, t4=t4, g2=g2)))
         return out.view(B, h, w, c)
 
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
@@ -491,17 +491,17 @@ class NAFNet(nn.Module):
         F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
         dt = self.dt
         dout = dout.reshape(M, c)
-        # out = y + gamma * t5
-        gs = query("scale_dot_grid", M, c)
-        slab = F(gs * c)
-        dt5 = E(M, c)
-        call("scale_dot", dout, S["t5"], self._slice(P, pre + "gamma"), dt5, slab, M, c, dt)
-        self._reduce(slab, gs, c, self._slice(dflat, pre + "gamma"))
-        # conv5
+        # out = y + gamma * conv5(g2): no stored pre-activation, no scaled-gradient pass.  dg2 = (gamma (.) dout) W5
+        # (gamma as the A-operand column scale); U5 = dout^T g2, V5 = colsum dout feed dW5 = gamma (.) U5,
+        # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
         dg2 = E(M, c)
-        self._mm(Wt, dt5, c, AM_PLAIN, None, 1, pre + "conv5.weight", dg2, c, CM_PLAIN, M, c, c, dgrad=True)
-        self._wgrad(dt5, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0,
-                    self._slice(dflat, pre + "conv5.weight"), self._slice(dflat, pre + "conv5.bias"))
+        self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dg2, c, CM_PLAIN, M,
+                 c, c, dgrad=True)
+        U5, V5 = F(c * c), F(c)
+        self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
+        call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
+             self._slice(P, pre + "gamma"), self._slice(dflat, pre + "conv5.weight"),
+             self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
         # SimpleGate (FFN)
         dt4 = E(M, 2 * c)
         call("sg_bwd", dg2, S["t4"], dt4, M, c, dt)
@@ -517,16 +517,15 @@ class NAFNet(nn.Module):
         call("ln_bwd_nhwc", dn2, S["yh2"], S["den2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb, M, c, dt)
         self._reduce(sw, lg, c, self._slice(dflat, pre + "norm2.weight"))
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
-        # y = x + beta * t3
-        dt3 = E(M, c)
-        slab = F(gs * c)
-        call("scale_dot", dy, S["t3"], self._slice(P, pre + "beta"), dt3, slab, M, c, dt)
-        self._reduce(slab, gs, c, self._slice(dflat, pre + "beta"))
-        # conv3 (input h = g * a)
+        # y = x + beta * conv3(h), h = g (.) a: same layer-scale identity as conv5 (dh = (beta (.) dy) W3)
         dh = E(M, c)
-        self._mm(Wt, dt3, c, AM_PLAIN, None, 1, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c, dgrad=True)
-        self._wgrad(dt3, c, AM_PLAIN, S["g"], c, AM_SCALE, S["a"], HW, M, c, c, 0, 0, 0, 0,
-                    self._slice(dflat, pre + "conv3.weight"), self._slice(dflat, pre + "conv3.bias"))
+        self._mm(Wt, dy, c, AM_SCALE, self._slice(P, pre + "beta"), M, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c,
+                 dgrad=True)
+        U3, V3 = F(c * c), F(c)
+        self._wgrad(dy, c, AM_PLAIN, S["g"], c, AM_SCALE, S["a"], HW, M, c, c, 0, 0, 0, 0, U3, V3)
+        call("layer_scale_grad", U3, V3, self._slice(P, pre + "conv3.weight"), self._slice(P, pre + "conv3.bias"),
+             self._slice(P, pre + "beta"), self._slice(dflat, pre + "conv3.weight"),
+             self._slice(dflat, pre + "conv3.bias"), self._slice(dflat, pre + "beta"), c, c)
         # SCA
         chunks = query("dw_chunks", B, h, w, c, 0)
         da_slab = F(B * chunks * c)

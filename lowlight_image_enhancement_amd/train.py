@@ -22,6 +22,7 @@ instead of reduce-to-rank-0 (:351).
 from __future__ import annotations
 
 import math
+import struct
 from typing import Dict, List, Optional
 
 import torch
@@ -142,6 +143,69 @@ class NBPTrainer:
              self.clip_state, float(lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
              self.t)
         return out
+
+    # ------------------------------------------------------------------ HIP-graph step (single process)
+    def graph_step(self, lq, gt, short=None, expo_ratio=None):
+        """One training step replayed from a captured HIP graph: every kernel of step() (forward, loss head,
+        backward with its deferred reductions, clip, AdamW) recorded once and relaunched with no host work but the
+        input copies and the 3-float hyper-parameter upload.  Numerically identical to step().  The first call
+        captures with these tensors' shapes; later calls copy their inputs into the captured buffers."""
+        if self.world > 1:
+            raise RuntimeError("graph_step is single-process; use step() with torch.distributed")
+        ins = (lq, gt, short, expo_ratio)
+        if getattr(self, "_graph", None) is None:
+            self._capture(ins)
+        else:
+            for dst, src in zip(self._static, ins):
+                if (dst is None) != (src is None):
+                    raise ValueError("graph_step: inputs must keep the structure of the captured step")
+                if dst is not None and src is not dst:
+                    dst.copy_(src, non_blocking=True)
+        self.t += 1
+        lr = self.scheduler(self.t - 1) if self.scheduler is not None else self.lr
+        # the eager C entry receives lr, beta1, beta2 as float32 and forms the bias corrections in double from those
+        f32 = lambda v: struct.unpack("f", struct.pack("f", v))[0]  # noqa: E731
+        lr, b1, b2 = f32(lr), f32(self.betas[0]), f32(self.betas[1])
+        slot = self.t % len(self._hyper_host)
+        ev = self._hyper_ev[slot]
+        if ev is not None:
+            ev.synchronize()  # the upload that last used this pinned slot has been consumed
+        h = self._hyper_host[slot]
+        h[0], h[1], h[2] = lr, lr / (1.0 - b1 ** self.t), math.sqrt(1.0 - b2 ** self.t)
+        self._hyper.copy_(h, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._hyper_ev[slot] = ev
+        self._graph.replay()
+        return self._graph_out
+
+    def _graph_body(self):
+        lq, gt, short, ratio = self._static
+        out = self.loss_and_grad(lq, gt, short, ratio)
+        call("grad_clip_coef", self.grad, self.grad.numel(), 1.0, float(self.max_norm), self.clip_ws, self.clip_state)
+        call("adamw_step_dev", self.net.flat.data, self.grad, self.exp_avg, self.exp_avg_sq, self.grad.numel(),
+             self.clip_state, self._hyper, float(self.betas[0]), float(self.betas[1]), float(self.eps),
+             float(self.wd))
+        return out
+
+    def _capture(self, ins):
+        self._static = tuple(None if x is None else x.detach().clone() for x in ins)
+        self._hyper = torch.zeros(3, device=self.dev)
+        self._hyper_host = [torch.zeros(3, pin_memory=True) for _ in range(8)]
+        self._hyper_ev = [None] * 8
+        # the capture itself must not move the parameters: snapshot the state a side-stream warm-up touches
+        saved = [x.clone() for x in (self.net.flat.data, self.exp_avg, self.exp_avg_sq)]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self._hyper.copy_(torch.tensor([0.0, 0.0, 1.0]))  # lr-0 warm-up: lazy init happens outside the capture
+            self._graph_body()
+        torch.cuda.current_stream().wait_stream(side)
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            self._graph_out = self._graph_body()
+        for dst, src in zip((self.net.flat.data, self.exp_avg, self.exp_avg_sq), saved):
+            dst.copy_(src)
 
     def logs(self, reduce: bool = True) -> Dict[str, float]:
         """Loss dict of the last step (host sync), averaged over ranks like reduce_loss_dict (base_model.py:335-360)."""

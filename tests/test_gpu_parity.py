@@ -406,3 +406,66 @@ def test_dw_bwd_against_float64(dev, B, H, W, C, dtype):
     close(dt1.float(), rx.cpu().numpy(), **tol)
     close(dW, rw.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-3)
     close(db, rb.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 8, 8, 64, 1), (1, 16, 16, 8, 0),
+                                           (2, 19, 23, 12, 0), (2, 20, 130, 16, 1)])
+def test_dw_sg_pool_fwd_against_float64(dev, B, H, W, C, dtype):
+    """Depthwise 3x3 + bias -> SimpleGate -> pool partials -> SCA (tiled LDS kernel for C % 16 (bf16) / 8 (fp32),
+    the chunked kernel otherwise) vs float64 torch on the same (dtype-rounded) input."""
+    import torch.nn.functional as Fn
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(B + H * W + C + dtype)
+    td = torch.bfloat16 if dtype == 1 else torch.float32
+    M, C2 = B * H * W, 2 * C
+    t1 = torch.randn(M, C2, device=dev, generator=gen).to(td)
+    w = torch.randn(C2, 9, device=dev, generator=gen)
+    bias = torch.randn(C2, device=dev, generator=gen)
+    wsca = torch.randn(C, C, device=dev, generator=gen)
+    bsca = torch.randn(C, device=dev, generator=gen)
+    rows = query("dw_fwd_slab_rows", B, H, W, C, dtype)
+    t2, g = torch.empty(M, C2, device=dev, dtype=td), torch.empty(M, C, device=dev, dtype=td)
+    pool = torch.empty(B * rows * C, device=dev)
+    call("dw_sg_pool_fwd", t1, w, bias, t2, g, pool, B, H, W, C, dtype)
+    mean, a = torch.empty(B, C, device=dev), torch.empty(B, C, device=dev)
+    call("sca_fwd", pool, rows, wsca, bsca, mean, a, B, H * W, C)
+    x = t1.double().view(B, H, W, C2).permute(0, 3, 1, 2)
+    y = Fn.conv2d(x, w.double().view(C2, 1, 3, 3), bias.double(), padding=1, groups=C2)
+    rt2 = y.permute(0, 2, 3, 1).reshape(M, C2)
+    rg = rt2[:, :C] * rt2[:, C:]
+    rmean = rg.view(B, H * W, C).mean(1)
+    tol = dict(atol=3e-2, rtol=1e-2) if dtype == 1 else dict(atol=1e-4, rtol=1e-5)
+    close(t2.float(), rt2.cpu().numpy(), **tol)
+    close(g.float(), rg.cpu().numpy(), atol=tol["atol"] * 8, rtol=tol["rtol"])
+    close(mean, rmean.cpu().numpy(), atol=1e-4, rtol=1e-4)
+    close(a, (rmean @ wsca.double().t() + bsca.double()).cpu().numpy(), atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_graph_step_bitwise_equals_eager(dev, precision):
+    """The captured HIP-graph step replays exactly the eager step's kernels: parameters, optimizer state and losses
+    agree bit for bit over several steps of a cosine schedule, including an input swap between replays."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    from lowlight_image_enhancement_amd.train import NBPTrainer, TrueCosineAnnealingLR
+    cfg = dict(width=16, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1])
+    torch.manual_seed(0)
+    net_a = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **cfg)
+    net_b = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **cfg)
+    net_b.load_state_dict(net_a.state_dict())
+    trs = []
+    for net in (net_a, net_b):
+        net.to(dev)
+        net.precision = precision
+        trs.append(NBPTrainer(net, w_l1=1.0, w_ssim=0.05, w_phys=0.1, lr=1e-3,
+                              scheduler=TrueCosineAnnealingLR(1e-3, 10)))
+    g = torch.Generator(device=dev).manual_seed(5)
+    batches = [tuple(torch.rand(2, 3, 64, 48, device=dev, generator=g) for _ in range(2)) for _ in range(2)]
+    ratio = torch.full((2, 1, 1, 1), 2.0, device=dev)
+    for i in range(4):
+        lq, gt = batches[i % 2]
+        short = (lq / 2).clamp(0, 1)
+        trs[0].step(lq, gt, short, ratio)
+        trs[1].graph_step(lq, gt, short, ratio)
+        assert torch.equal(net_a.flat, net_b.flat), f"params differ at step {i}"
+        assert torch.equal(trs[0].exp_avg_sq, trs[1].exp_avg_sq)
+        assert trs[0].logs() == trs[1].logs()
