@@ -204,6 +204,43 @@ int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W
 int nbp_ssim_loss_bwd(const float* x, const float* y, int N, int C, int H, int W, int clamp_in, const float* up,
                       float* ws, float* gx, nbp_stream_t s);
 
+/* ------------------------------------------------------------------ colour difference (NCHW sRGB [B][3][H][W] fp32) */
+/* DeltaE00Loss (NewBP_model/losses.py:92-143): out[0] = mean over pixels of the loss-form CIEDE2000 between
+   rgb_to_lab(clamp01 gen) and rgb_to_lab(clamp01 tgt) (kornia 0.6.12 conversion; clamp = 0 skips the clamps);
+   ws: nbp_de00_workspace_doubles(B*H*W) doubles.  The backward writes dgen = up[0] / (B*H*W) * d dE / d gen. */
+size_t nbp_de00_workspace_doubles(long npix);
+int nbp_de00_loss_fwd(const float* gen, const float* tgt, int B, int H, int W, int clamp, float eps, double* ws,
+                      float* out, nbp_stream_t s);
+int nbp_de00_loss_bwd(const float* gen, const float* tgt, int B, int H, int W, int clamp, float eps, const float* up,
+                      float* dgen, nbp_stream_t s);
+/* deltaE2000_map (metrics/color_error.py:235-267 -> _deltaE00_lab_map :105-210): map [B][H][W]. */
+int nbp_de00_metric_map(const float* pred, const float* tgt, int B, int H, int W, float kL, float kC, float kH,
+                        float eps, float* map, nbp_stream_t s);
+/* Per-pixel CIEDE2000 on Lab inputs [B][3][H][W] -> out [B][H][W]: form 0 = the loss form (losses.py:98-136,
+   eps), 1 = the metric form (color_error.py:105-210, kL kC kH eps). */
+int nbp_de00_lab(const float* lab1, const float* lab2, int B, int H, int W, int form, float kL, float kC, float kH,
+                 float eps, float* out, nbp_stream_t s);
+/* kornia rgb_to_lab of NCHW sRGB into lab [B][3][H][W]. */
+int nbp_rgb_to_lab(const float* rgb, int B, int H, int W, float* lab, nbp_stream_t s);
+
+/* ------------------------------------------------------------------ validation metrics (rows 26-27) */
+/* Per-sample PSNR over N samples of L fp32 elements: psnr_linear (metrics/linear.py:140-215, diff_double = 0: fp32
+   difference squared in float64) or calculate_psnr (metrics/psnr.py:18-67, diff_double = 1, N = 1); mse / psnr are
+   float64 [N] (mse may be null); inf where mse <= eps.  ws: nbp_psnr_workspace_doubles(N, L) doubles. */
+size_t nbp_psnr_workspace_doubles(int N, long L);
+int nbp_psnr(const float* pred, const float* tgt, int N, long L, double data_range, double eps, int diff_double,
+             double* ws, double* mse, double* psnr, nbp_stream_t s);
+/* Windowed SSIM per-plane means out [N*C] float64: ssim_linear (metrics/linear.py:218-324: clamp_var = 1, crop = 0,
+   eps) or the torchmetrics-1.2.0 form behind calculate_ssim (metrics/ssim.py:341-377: clamp_var = 0, eps = 0,
+   crop = 1: the k/2 border of the map is excluded).  win: the k normalised 1-D window weights (device);
+   pad_mode 0 reflect, 1 replicate, 2 circular, 3 constant(0). */
+size_t nbp_ssim_linear_workspace_floats(int N, int C, int H, int W);
+int nbp_ssim_linear(const float* pred, const float* tgt, int N, int C, int H, int W, const float* win, int k,
+                    int pad_mode, float c1, float c2, float eps, int clamp_var, int crop, float* ws, double* out,
+                    nbp_stream_t s);
+/* |Sobel| of channel 0 of lab [B][3][H][W] (zero padding, +1e-12 under the root; color_error.py:296-302). */
+int nbp_sobel_mag(const float* lab, int B, int H, int W, float* out, nbp_stream_t s);
+
 /* ------------------------------------------------------------------ optimizer (image_restoration_model.py:313-320) */
 /* clip_grad_norm_(params, max_norm): state[0] = ||grad*grad_scale||, state[1] = clip coef * grad_scale. */
 size_t nbp_clip_workspace_doubles(long n);

@@ -3,10 +3,11 @@
 Same class/function names, constructor arguments, term order and return values as the reference; every term's
 forward and backward runs as HIP kernels (include/nbp.h): L1 / Charbonnier (nbp_pix_loss_*), SSIM
 (nbp_ssim_loss_*), the physics-consistency L1 with the crosstalk PSF (nbp_phys_l1_*), exposure alignment
-(nbp_align_exposure).  Scalars stay on the device; the upstream gradient is read from device memory.
+(nbp_align_exposure), ΔE00 (nbp_de00_loss_*).  Scalars stay on the device; the upstream gradient is read from device
+memory.
 
 Not yet on the MI355X path (raise NotImplementedError when used, never a silent CPU/torch fallback):
-the VGG19 perceptual term, LPIPS and ΔE00 (SURVEY §8a rows 19-22, cfg3 — scheduled next).
+the VGG19 perceptual term and LPIPS.
 """
 from __future__ import annotations
 
@@ -189,15 +190,50 @@ class HybridLoss(nn.Module):
         return total, l1_val, perceptual_val
 
 
+class _DeltaE00Fn(torch.autograd.Function):
+    """mean CIEDE2000 (loss form) of rgb_to_lab(clamp01 gen) vs rgb_to_lab(clamp01 tgt); d/d gen by forward-mode AD
+    in the kernel (color.hip)."""
+
+    @staticmethod
+    def forward(ctx, gen, tgt, eps):
+        _lib.require_cuda(gen, tgt)
+        if gen.shape != tgt.shape or gen.dim() != 4 or gen.shape[1] != 3:
+            raise ValueError("DeltaE00Loss expects two [N,3,H,W] sRGB tensors of the same shape")
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("DeltaE00 gradient w.r.t. the target is not implemented on the MI355X path")
+        gen = gen.detach().float().contiguous()
+        tgt = tgt.detach().float().contiguous()
+        N, _, H, W = gen.shape
+        ws = torch.empty(query("de00_workspace_doubles", N * H * W), dtype=torch.float64, device=gen.device)
+        out = torch.empty((), device=gen.device)
+        call("de00_loss_fwd", gen, tgt, N, H, W, 1, float(eps), ws, out)
+        ctx.save_for_backward(gen, tgt)
+        ctx.eps = float(eps)
+        return out
+
+    @staticmethod
+    def backward(ctx, up):
+        gen, tgt = ctx.saved_tensors
+        N, _, H, W = gen.shape
+        g = torch.empty_like(gen)
+        call("de00_loss_bwd", gen, tgt, N, H, W, 1, ctx.eps, up.float().contiguous().view(1), g)
+        return g, None, None
+
+
 class DeltaE00Loss(nn.Module):
-    """losses.py:92-143 — ΔE00 on sRGB via kornia rgb_to_lab.  Scheduled (cfg3); raises when called."""
+    """losses.py:92-143 — mean ΔE00 (the reference's loss-form _ciede2000, eps 1e-6) between kornia-0.6.12
+    rgb_to_lab(gen.clamp(0,1)) and rgb_to_lab(tgt.clamp(0,1)); one HIP kernel per direction (color.hip)."""
 
     def __init__(self, eps: float = 1e-6):
         super().__init__()
         self.eps = eps
 
+    @staticmethod
+    def _ciede2000(Lab1: torch.Tensor, Lab2: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
+        raise NotImplementedError("the Lab-domain helper is not exposed on the MI355X path; call forward() on sRGB")
+
     def forward(self, gen_srgb01, tgt_srgb01):
-        raise NotImplementedError("DeltaE00Loss is not implemented on the MI355X path yet")
+        return _DeltaE00Fn.apply(gen_srgb01, tgt_srgb01, self.eps)
 
 
 class SSIMLoss(nn.Module):

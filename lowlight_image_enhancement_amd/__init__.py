@@ -6,7 +6,8 @@ reference's Python API (RUA1027/Lowlight_Image_Enhancement: NewBP_model.*, metri
     from lowlight_image_enhancement_amd.NewBP_model.losses import HybridLossPlus
     from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_srgb
 
-`install_aliases()` registers the reference's top-level module names (NewBP_model, metrics.phys_consistency)
+`install_aliases()` registers the reference's module names (NewBP_model.*, metrics.{phys_consistency, linear, psnr,
+ssim, color_error}, basicsr.metrics.lowlight_metrics)
 so unmodified train/eval scripts import this implementation.
 """
 import sys
@@ -17,10 +18,15 @@ __version__ = "0.1.0"
 def install_aliases():
     from . import NewBP_model, metrics
     from .NewBP_model import losses, newbp_layer, newbp_net_arch
-    from .metrics import phys_consistency
+    from .metrics import color_error, linear, lowlight_metrics, phys_consistency, psnr, ssim
     sys.modules.setdefault("NewBP_model", NewBP_model)
     sys.modules.setdefault("NewBP_model.newbp_layer", newbp_layer)
     sys.modules.setdefault("NewBP_model.newbp_net_arch", newbp_net_arch)
     sys.modules.setdefault("NewBP_model.losses", losses)
     sys.modules.setdefault("metrics", metrics)
     sys.modules.setdefault("metrics.phys_consistency", phys_consistency)
+    sys.modules.setdefault("metrics.linear", linear)
+    sys.modules.setdefault("metrics.psnr", psnr)
+    sys.modules.setdefault("metrics.ssim", ssim)
+    sys.modules.setdefault("metrics.color_error", color_error)
+    sys.modules.setdefault("basicsr.metrics.lowlight_metrics", lowlight_metrics)
