@@ -50,6 +50,19 @@ def nafblock_bytes(net, B, H, W):
     return 5 * tot * 4
 
 
+def _pmc_traffic(cls):
+    """HBM bytes per launch of a kernel class from the newest committed PMC record (profiles/*pmc_traffic.json,
+    scripts/pmc_pass.sh + scripts/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None, None
+    rec = json.load(open(files[-1])).get("classes", {}).get(cls)
+    if rec is None:
+        return None, None
+    return round(rec["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(state_dict, B=2, steps=2):
     """Time the oracle's training step (oracle/train_step.py, torch CPU fp32) on a bounded sample."""
     from oracle.train_step import OracleTrainer
@@ -215,7 +228,8 @@ def main():
     else:
         roof = {"bound": "mfma", "achieved": round(tflops, 3), "peak": peak_tf, "unit": "TFLOP/s",
                 "frac": round(tflops / peak_tf, 4)}
-    roof.update({"traffic": None, "kernel": dom, "launches_per_step": nl // args.steps,
+    traffic, tsrc = _pmc_traffic(dom)
+    roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel": dom, "launches_per_step": nl // args.steps,
                  "ms_per_step": round(ms / args.steps, 3), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
                  "flop_intensity": round(fl / max(by, 1), 2), "tflops": round(tflops, 2),
                  "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in classes.items()}})

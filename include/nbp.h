@@ -241,6 +241,42 @@ int nbp_ssim_linear(const float* pred, const float* tgt, int N, int C, int H, in
 /* |Sobel| of channel 0 of lab [B][3][H][W] (zero padding, +1e-12 under the root; color_error.py:296-302). */
 int nbp_sobel_mag(const float* lab, int B, int H, int W, float* out, nbp_stream_t s);
 
+/* ------------------------------------------------------------------ VGG feature losses (rows 19, 22) */
+/* 3x3 zero-padded conv over NHWC bf16 as an implicit GEMM on bf16 MFMA (K = 9*Cin gathered on the fly):
+   y = epi(sum_{t,c} x[i + t/3 - 1][j + t%3 - 1][c] * w[n][t][c]); mode 0 = + bias then ReLU, 1 = + bias,
+   2 = keep where R > 0 (ReLU mask of a saved post-ReLU map; the input-gradient pass uses the tap-flipped,
+   transposed weights).  Cin, Cout multiples of 8; y bf16 (y_dtype 1) or fp32 (y_dtype 0, mode 1). */
+int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
+                     const void* R, void* y, int y_dtype, nbp_stream_t s);
+/* PerceptualLoss input (losses.py:56-66): NCHW fp32 sRGB -> NHWC bf16 [B][H][W][8] = (clamp01(x) - m) / s, c >= 3
+   zero.  The input gradient maps d[B][H][W][8] fp32 back to NCHW (/ s, clamp mask). */
+int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float m1, float m2, float s0, float s1,
+                 float s2, void* y, nbp_stream_t s);
+int nbp_vgg_input_grad(const float* d8, const float* x, int B, int H, int W, int clamp, float s0, float s1, float s2,
+                       float* dx, nbp_stream_t s);
+/* 2x2 max pool over NHWC bf16 (floor) with the argmax (window order, first maximum); the backward scatters dy to
+   the argmax and applies the ReLU mask of the (post-ReLU) pool input. */
+int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, nbp_stream_t s);
+int nbp_maxpool2_bwd(const void* dy, const unsigned char* idx, const void* post_in, int B, int H, int W, int C, void* dx,
+                     nbp_stream_t s);
+/* LPIPS tap (lpips 0.1.4 net='vgg'): out[n] (+)= mean over the HW pixels of sum_c w_c (u_c - v_c)^2 with
+   u = a / (|a|_C + 1e-10), v likewise for b (a, b: NHWC bf16 [N][HW][C]); the backward writes
+   da = up[n] * d out[n] / da (zero for all-zero pixels).  ws: nbp_lpips_tap_workspace_doubles(N, HW). */
+size_t nbp_lpips_tap_workspace_doubles(int N, long HW);
+int nbp_lpips_tap_fwd(const void* a, const void* b, const float* w, int N, long HW, int C, int accumulate, double* ws,
+                      float* out, nbp_stream_t s);
+int nbp_lpips_tap_bwd(const void* a, const void* b, const float* w, int N, long HW, int C, const float* up, void* da,
+                      nbp_stream_t s);
+/* d += g * (post > 0) over n bf16 elements (a tapped post-ReLU map's gradient joining the backward walk). */
+int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, nbp_stream_t s);
+/* Feature distance over n bf16 elements: out = scale * sum (a-b)^2 (mode 0) or |a-b| (mode 1); the backward writes
+   da = up[0] * scale * d/da, optionally masked by (a > 0) (the last ReLU).  ws: nbp_feat_dist_workspace_doubles(n). */
+size_t nbp_feat_dist_workspace_doubles(long n);
+int nbp_feat_dist_fwd(const void* a, const void* b, long n, int mode, double scale, double* ws, float* out,
+                      nbp_stream_t s);
+int nbp_feat_dist_bwd(const void* a, const void* b, long n, int mode, float scale, int relu_mask, const float* up,
+                      void* da, nbp_stream_t s);
+
 /* ------------------------------------------------------------------ optimizer (image_restoration_model.py:313-320) */
 /* clip_grad_norm_(params, max_norm): state[0] = ||grad*grad_scale||, state[1] = clip coef * grad_scale. */
 size_t nbp_clip_workspace_doubles(long n);

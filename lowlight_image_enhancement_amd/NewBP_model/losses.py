@@ -6,8 +6,7 @@ forward and backward runs as HIP kernels (include/nbp.h): L1 / Charbonnier (nbp_
 (nbp_align_exposure), ΔE00 (nbp_de00_loss_*).  Scalars stay on the device; the upstream gradient is read from device
 memory.
 
-Not yet on the MI355X path (raise NotImplementedError when used, never a silent CPU/torch fallback):
-the VGG19 perceptual term and LPIPS.
+The VGG19 perceptual term runs as implicit-GEMM bf16 MFMA convs (vgg.py); LPIPS is lpips.py.
 """
 from __future__ import annotations
 
@@ -18,6 +17,8 @@ import torch
 import torch.nn as nn
 
 from .. import _lib
+from .. import vgg as _vgg
+from ..lpips import LPIPS
 from .._lib import call, query
 from .newbp_layer import CrosstalkPSF
 
@@ -156,18 +157,70 @@ class _PhysL1Fn(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------- public classes (reference names)
-class PerceptualLoss(nn.Module):
-    """losses.py:32-69 — VGG19 features[:36] perceptual MSE.  The VGG19 conv stack is not on the MI355X path
-    yet; constructing is allowed, calling raises."""
+class _PerceptualFn(torch.autograd.Function):
+    """mean/sum of (VGG(prep(gen)) - VGG(prep(tgt)))^2 (or |.|); d/d gen through the frozen stack (vgg.py)."""
 
-    def __init__(self, device: Union[str, torch.device] = "cuda", use_mse: bool = True, reduction: str = "mean"):
+    @staticmethod
+    def forward(ctx, gen, tgt, module):
+        _lib.require_cuda(gen, tgt)
+        if gen.shape != tgt.shape:
+            raise ValueError(f"PerceptualLoss: shape mismatch {tuple(gen.shape)} vs {tuple(tgt.shape)}")
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("PerceptualLoss gradient w.r.t. the target is not implemented on MI355X")
+        stack = module.stack(gen.device)
+        want = ctx.needs_input_grad[0]
+        with torch.no_grad():
+            ft, _, _ = stack.forward(_vgg.prep_input(tgt.detach()), save=False)
+            fg, tape, _ = stack.forward(_vgg.prep_input(gen.detach()), save=want)
+        n = fg.numel()
+        mode = 0 if module.use_mse else 1
+        scale = 1.0 / n if module.reduction == "mean" else 1.0
+        ws = torch.empty(query("feat_dist_workspace_doubles", n), dtype=torch.float64, device=gen.device)
+        out = torch.empty((), device=gen.device)
+        call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out)
+        if want:
+            ctx.tape, ctx.fg, ctx.ft, ctx.stack = tape, fg, ft, stack
+            ctx.mode, ctx.scale = mode, scale
+            ctx.save_for_backward(gen.detach())
+        return out
+
+    @staticmethod
+    def backward(ctx, up):
+        (gen,) = ctx.saved_tensors
+        d = torch.empty_like(ctx.fg)
+        call("feat_dist_bwd", ctx.fg, ctx.ft, ctx.fg.numel(), ctx.mode, float(ctx.scale), 1,
+             up.float().contiguous().view(1), d)
+        d8 = ctx.stack.backward(ctx.tape, d)
+        ctx.tape = ctx.fg = ctx.ft = None
+        return _vgg.input_grad(d8, gen), None, None
+
+
+class PerceptualLoss(nn.Module):
+    """losses.py:32-69 — clamp01 -> ImageNet mean/std -> vgg19.features[:36] (through relu5_4) for both images ->
+    MSE (use_mse) or L1, reduction 'mean' / 'sum'.  The conv stack is implicit-GEMM bf16 MFMA (vgg.py).
+    `weights`: None (deterministic synthetic VGG19 — the ImageNet download is unavailable offline), a state_dict of
+    vgg19 (`features.N.*` or `N.*` keys) or a checkpoint path (loaded with weights_only=True)."""
+
+    def __init__(self, device: Union[str, torch.device] = "cuda", use_mse: bool = True, reduction: str = "mean",
+                 weights=None):
         super().__init__()
+        if reduction not in ("mean", "sum"):
+            raise NotImplementedError("PerceptualLoss on MI355X supports reduction 'mean' and 'sum'")
         self.use_mse = use_mse
         self.reduction = reduction
+        self._weights = weights
+        self._stacks = {}
+
+    def stack(self, device) -> "_vgg.VGGStack":
+        key = str(device)
+        if key not in self._stacks:
+            self._stacks[key] = _vgg.VGGStack(_vgg.VGG19_CFG, 36, device, self._weights)
+        return self._stacks[key]
 
     def forward(self, generated_img, target_img):
-        raise NotImplementedError("PerceptualLoss (VGG19) is not implemented on the MI355X path yet; "
-                                  "set w_perc=0 / lambda_perceptual=0")
+        if target_img.device != generated_img.device:
+            target_img = target_img.to(generated_img.device)
+        return _PerceptualFn.apply(generated_img, target_img, self)
 
 
 class HybridLoss(nn.Module):
@@ -318,9 +371,7 @@ class HybridLossPlus(nn.Module):
         self.perc = PerceptualLoss(device=device)
         self.deltaE = DeltaE00Loss() if use_deltaE else None
         self.ssim = SSIMLoss() if use_ssim else None
-        self.lpips = None
-        if use_lpips:
-            warnings.warn("Disabling LPIPS term: LPIPS is not implemented on the MI355X path yet", RuntimeWarning)
+        self.lpips = LPIPS(net="vgg") if use_lpips else None  # lpips.LPIPS(net='vgg') restated (lpips.py)
         self.phys = PhysicsConsistencyLoss(physics_kernel, device=device) if use_phys and physics_kernel is not None else None
         self.phys_srgb = PhysicalConsistencyLossSRGB(physics_psf_module.to(device)) if (
             use_phys and physics_psf_module is not None) else None
@@ -361,6 +412,11 @@ class HybridLossPlus(nn.Module):
             L_p = self.perc(Bhat_srgb01, B_srgb01)
             self._ensure_finite("Perc", L_p)
             Lw, logs["Perc"] = self._weighted("perc", L_p)
+            L_total = L_total + Lw
+        if self.lpips is not None:
+            L_lp = self.lpips(Bhat_srgb01, B_srgb01).mean()
+            self._ensure_finite("LPIPS", L_lp)
+            Lw, logs["LPIPS"] = self._weighted("lpips", L_lp)
             L_total = L_total + Lw
         if self.deltaE is not None and self._active("de"):
             L_de = self.deltaE(Bhat_srgb01, B_srgb01)

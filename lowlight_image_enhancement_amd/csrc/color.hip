@@ -56,8 +56,10 @@ __device__ __forceinline__ D3 vexp(const D3& x) {
   return scl(x, e, e);
 }
 __device__ __forceinline__ float vatan2(float y, float x) { return atan2f(y, x); }
+// torch's atan2 backward is defined as 0 at the origin (a grey pixel: a' = b = 0)
 __device__ __forceinline__ D3 vatan2(const D3& y, const D3& x) {
   const float den = x.v * x.v + y.v * y.v, v = atan2f(y.v, x.v);
+  if (den == 0.f) return mk(v);
   return D3{v, (x.v * y.d0 - y.v * x.d0) / den, (x.v * y.d1 - y.v * x.d1) / den, (x.v * y.d2 - y.v * x.d2) / den};
 }
 // torch remainder (sign of the divisor): a - b * floor(a / b); d/da = 1

@@ -15,8 +15,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
-enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2 };
-enum { CM_PLAIN = 0, CM_D2S = 1 };
+// A modes: plain rows, space-to-depth gather, per-(image, column) scale, and 3x3 neighbourhood gather (implicit GEMM
+// of a zero-padded 3x3 conv over an NHWC map: row m = pixel, k = tap * Cin + c with gh = H, gw = W, cs = Cin).
+// C modes: plain, depth-to-space scatter, bias + ReLU, and ReLU-mask by R (C = acc where R > 0, else 0).
+enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
+enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3 };
 
 struct GemmPB {
   const void* A;
@@ -149,7 +152,15 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-      if (m < M && k < K) {
+      if (AMODE == AM_IM2COL) {
+        if (m < M && k < K) {
+          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, i = rem / p.gw, j = rem - i * p.gw;
+          const int t = k / p.cs, c = k - t * p.cs;
+          const int ii = i + t / 3 - 1, jj = j + t % 3 - 1;
+          if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
+            v = load8<TA, AM_PLAIN>(p.A, ((long)(b * p.gh + ii) * p.gw + jj) * p.cs + c, nullptr);
+        }
+      } else if (m < M && k < K) {
         long off;
         if (AMODE == AM_S2D) off = s2d_off(m, k, p.gh, p.gw, p.cs);
         else off = (long)m * p.lda + k;
@@ -241,8 +252,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         const float4 b0 = ld4(p.bias + gcol), b1 = ld4(p.bias + gcol + 4);
         v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
       }
+      if (CMODE == CM_RELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      } else if (CMODE == CM_MASK) {
+        float rv[8];
+        ld8f<TC>(p.R, off, rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = rv[j] > 0.f ? v[j] : 0.f;
+      }
       if (p.pre) st8f<TC>(p.pre, off, v);
-      if (p.R) {
+      if (CMODE != CM_MASK && p.R) {
         float rv[8];
         ld8f<TC>(p.R, off, rv);
         if (p.rscale) {
@@ -261,8 +281,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         const int col = gcol + j;
         const long off = CMODE == CM_D2S ? s2d_off(grow, col, p.gh, p.gw, p.cs) : (long)grow * p.ldc + col;
         float x = v[j] + (p.bias ? p.bias[col] : 0.f);
+        if (CMODE == CM_RELU) x = fmaxf(x, 0.f);
+        if (CMODE == CM_MASK) x = ldf<TC>(p.R, off) > 0.f ? x : 0.f;
         if (p.pre) stf<TC>(p.pre, off, x);
-        if (p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
+        if (CMODE != CM_MASK && p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
         stf<TC>(p.C, off, x);
       }
     }
@@ -365,6 +387,29 @@ int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int
   if (ndesc > 0)
     transpose_bf16_kernel<<<dim3(256, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<__bf16*>(out_t));
   return check_launch("weights_bf16");
+}
+
+// 3x3 zero-padded convolution over NHWC bf16 as an implicit GEMM on the bf16 MFMA kernel:
+//   y[b][i][j][n] = epi( sum_{t, c} x[b][i + t/3 - 1][j + t%3 - 1][c] * w[n][t][c] (+ bias[n]) )
+// epi: mode 0 bias + ReLU, 1 bias only, 2 ReLU-mask by R (y = acc where R > 0 else 0; no bias).  y is bf16
+// (y_dtype 1) or fp32 (y_dtype 0, modes 1 only).  Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
+int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
+                     const void* R, void* y, int y_dtype, nbp_stream_t s) {
+  NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0, "nbp_conv3x3_bf16: bad args");
+  NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv3x3_bf16: Cin and Cout must be multiples of 8 (%d, %d)", Cin,
+              Cout);
+  NBP_REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || R) && (y_dtype == 1 || mode == 1),
+              "nbp_conv3x3_bf16: mode / R / y_dtype");
+  const long M = (long)B * H * W;
+  NBP_REQUIRE(M < (1L << 31), "nbp_conv3x3_bf16: too many pixels");
+  GemmPB p{x, 0, nullptr, 1, reinterpret_cast<const __bf16*>(w), 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
+           mode == 2 ? nullptr : bias, mode == 2 ? R : nullptr, nullptr, nullptr};
+  hipStream_t st = S(s);
+  if (mode == 0) dispatch<AM_IM2COL, CM_RELU, __bf16, __bf16>(p, st);
+  else if (mode == 2) dispatch<AM_IM2COL, CM_MASK, __bf16, __bf16>(p, st);
+  else if (y_dtype == 1) dispatch<AM_IM2COL, CM_PLAIN, __bf16, __bf16>(p, st);
+  else dispatch<AM_IM2COL, CM_PLAIN, __bf16, float>(p, st);
+  return check_launch("conv3x3_bf16");
 }
 
 }  // extern "C"

@@ -1,0 +1,356 @@
+// VGG feature-loss glue around the implicit-GEMM 3x3 convs (nbp_conv3x3_bf16), NHWC bf16 activations:
+//   PerceptualLoss (NewBP_model/losses.py:32-69): (clamp01(x) - mean) / std -> vgg19.features[:36] -> MSE / L1;
+//   the LPIPS backbone taps reuse the same pieces.
+// Kernels: the input prologue (NCHW fp32 -> NHWC bf16 with the channel dim padded to 8), 2x2 max-pool with argmax
+// (first maximum in window order, as torch's max_pool2d) and its backward fused with the ReLU mask of the pool input,
+// the feature distance with its gradient (fused with the last ReLU's mask), and the input-gradient epilogue.
+#include "nbp_common.h"
+
+using namespace nbp;
+
+namespace {
+
+__global__ __launch_bounds__(256) void vgg_prep_kernel(const float* __restrict__ x, long HW, long npix, int clamp,
+                                                       float m0, float m1, float m2, float s0, float s1, float s2,
+                                                       __bf16* __restrict__ y) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+    const long b = p / HW, q = p - b * HW;
+    const float* xb = x + b * 3 * HW + q;
+    float v0 = xb[0], v1 = xb[HW], v2 = xb[2 * HW];
+    if (clamp) {
+      v0 = fminf(fmaxf(v0, 0.f), 1.f);
+      v1 = fminf(fmaxf(v1, 0.f), 1.f);
+      v2 = fminf(fmaxf(v2, 0.f), 1.f);
+    }
+    bf16x8 o;
+    o[0] = (__bf16)((v0 - m0) / s0);
+    o[1] = (__bf16)((v1 - m1) / s1);
+    o[2] = (__bf16)((v2 - m2) / s2);
+#pragma unroll
+    for (int j = 3; j < 8; ++j) o[j] = (__bf16)0.f;
+    *reinterpret_cast<bf16x8*>(y + p * 8) = o;
+  }
+}
+
+// 2x2 / stride-2 max pool over NHWC (floor), 8 channels per thread; idx = window position 0..3 of the maximum
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restrict__ x, int H, int W, int C, long total8,
+                                                          __bf16* __restrict__ y, unsigned char* __restrict__ idx) {
+  const int Ho = H / 2, Wo = W / 2, C8 = C / 8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    const long o = e / C8;  // output pixel
+    const int j = o % Wo;
+    const long t = o / Wo;
+    const int i = t % Ho;
+    const long b = t / Ho;
+    const __bf16* base = x + (((b * H + 2 * i) * W + 2 * j) * C + c8 * 8);
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(base);
+    const bf16x8 bq = *reinterpret_cast<const bf16x8*>(base + C);
+    const bf16x8 cq = *reinterpret_cast<const bf16x8*>(base + (long)W * C);
+    const bf16x8 dq = *reinterpret_cast<const bf16x8*>(base + (long)W * C + C);
+    bf16x8 out;
+    unsigned long long packed = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float best = (float)a[k];
+      int bi = 0;
+      const float v1 = (float)bq[k], v2 = (float)cq[k], v3 = (float)dq[k];
+      if (v1 > best || v1 != v1) { best = v1; bi = 1; }
+      if (v2 > best || v2 != v2) { best = v2; bi = 2; }
+      if (v3 > best || v3 != v3) { best = v3; bi = 3; }
+      out[k] = (__bf16)best;
+      packed |= (unsigned long long)bi << (8 * k);
+    }
+    *reinterpret_cast<bf16x8*>(y + o * C + c8 * 8) = out;
+    *reinterpret_cast<unsigned long long*>(idx + o * C + c8 * 8) = packed;
+  }
+}
+
+// din = scatter(dout at the argmax) * (post_in > 0)   (the pool input is a post-ReLU map)
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restrict__ dy,
+                                                          const unsigned char* __restrict__ idx,
+                                                          const __bf16* __restrict__ post_in, int H, int W, int C,
+                                                          long total8, __bf16* __restrict__ dx) {
+  const int Ho = H / 2, Wo = W / 2, C8 = C / 8;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    const long pix = e / C8;  // input pixel
+    const int j = pix % W;
+    const long t = pix / W;
+    const int i = t % H;
+    const long b = t / H;
+    bf16x8 out;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = (__bf16)0.f;
+    const int io = i / 2, jo = j / 2;
+    if (io < Ho && jo < Wo) {
+      const long o = ((b * Ho + io) * Wo + jo) * C + c8 * 8;
+      const int pos = (i & 1) * 2 + (j & 1);
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + o);
+      const unsigned long long packed = *reinterpret_cast<const unsigned long long*>(idx + o);
+      const bf16x8 pin = *reinterpret_cast<const bf16x8*>(post_in + pix * C + c8 * 8);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if ((int)((packed >> (8 * k)) & 0xff) == pos && (float)pin[k] > 0.f) out[k] = g[k];
+    }
+    *reinterpret_cast<bf16x8*>(dx + pix * C + c8 * 8) = out;
+  }
+}
+
+// loss partials of mode 0: (a - b)^2, mode 1: |a - b|
+__global__ __launch_bounds__(256) void feat_dist_fwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b, long n,
+                                                     int mode, double* __restrict__ part) {
+  __shared__ double red[16];
+  double acc = 0.0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float d = (float)a[i] - (float)b[i];
+    acc += mode == 0 ? (double)(d * d) : (double)fabsf(d);
+  }
+  const double t = block_sum_d(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+__global__ void feat_dist_finalize(const double* __restrict__ part, int n, double scale, float* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += part[i];
+    out[0] = (float)(s * scale);
+  }
+}
+
+// da = up[0] * scale * (mode 0: 2 (a - b), mode 1: sign(a - b)) * (relu_mask ? (a > 0) : 1)
+__global__ __launch_bounds__(256) void feat_dist_bwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b, long n,
+                                                     int mode, float scale, int relu_mask, const float* __restrict__ up,
+                                                     __bf16* __restrict__ da) {
+  const float g = up[0] * scale;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float av = (float)a[i], d = av - (float)b[i];
+    float v = mode == 0 ? 2.f * d : (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
+    if (relu_mask && !(av > 0.f)) v = 0.f;
+    da[i] = (__bf16)(g * v);
+  }
+}
+
+// dx (NCHW fp32) = d8[..][c] / std[c] * (clamp ? (0 <= x <= 1) : 1), c < 3
+__global__ __launch_bounds__(256) void vgg_input_grad_kernel(const float* __restrict__ d8, const float* __restrict__ x,
+                                                             long HW, long npix, int clamp, float s0, float s1,
+                                                             float s2, float* __restrict__ dx) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+    const long b = p / HW, q = p - b * HW;
+    const float sd[3] = {s0, s1, s2};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const long o = (b * 3 + c) * HW + q;
+      const float xv = x[o];
+      const bool pass = !clamp || (xv >= 0.f && xv <= 1.f);
+      dx[o] = pass ? d8[p * 8 + c] / sd[c] : 0.f;
+    }
+  }
+}
+
+// d += g * (post > 0)  (a tapped post-ReLU map's gradient joining the backward walk), all bf16
+__global__ __launch_bounds__(256) void add_relu_masked_kernel(__bf16* __restrict__ d, const __bf16* __restrict__ g,
+                                                              const __bf16* __restrict__ post, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    if ((float)post[i] > 0.f) d[i] = (__bf16)((float)d[i] + (float)g[i]);
+}
+
+// ---------------------------------------------------------------- LPIPS tap distance (lpips 0.1.4, net='vgg')
+// per pixel: u = a / (|a| + 1e-10), v = b / (|b| + 1e-10) over the C channels (normalize_tensor),
+// d = sum_c w_c (u_c - v_c)^2 (the 1x1 'lin' head); per image out[n] (+)= mean over pixels (spatial_average).
+__global__ __launch_bounds__(256) void lpips_tap_fwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+                                                     const float* __restrict__ w, long HW, int C, int chunks,
+                                                     double* __restrict__ slab) {
+  __shared__ double red[16];
+  const int n = blockIdx.y;
+  const long per = (HW + chunks - 1) / chunks, q0 = (long)blockIdx.x * per, q1 = min(HW, q0 + per);
+  double acc = 0.0;
+  for (long q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const __bf16* pa = a + ((long)n * HW + q) * C;
+    const __bf16* pb = b + ((long)n * HW + q) * C;
+    float sa = 0.f, sb = 0.f;
+    for (int c = 0; c < C; c += 8) {
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sa = fmaf((float)va[j], (float)va[j], sa);
+        sb = fmaf((float)vb[j], (float)vb[j], sb);
+      }
+    }
+    const float ia = 1.f / (sqrtf(sa) + 1e-10f), ib = 1.f / (sqrtf(sb) + 1e-10f);
+    float d = 0.f;
+    for (int c = 0; c < C; c += 8) {
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float t = (float)va[j] * ia - (float)vb[j] * ib;
+        d = fmaf(w[c + j] * t, t, d);
+      }
+    }
+    acc += (double)d;
+  }
+  const double t = block_sum_d(acc, red);
+  if (threadIdx.x == 0) slab[(long)n * chunks + blockIdx.x] = t;
+}
+
+__global__ void lpips_finalize(const double* __restrict__ slab, int N, int chunks, double inv_hw, int accumulate,
+                               float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += slab[(long)n * chunks + c];
+  out[n] = (float)((accumulate ? (double)out[n] : 0.0) + s * inv_hw);
+}
+
+// d a_k = up[n] / HW * (g_k / na - a_k (sum_c g_c a_c) / (na^2 |a|)),  g_c = 2 w_c (u_c - v_c), na = |a| + 1e-10.
+// A pixel whose feature vector is all zero gets zero gradient (torch's sqrt backward yields NaN there).
+__global__ __launch_bounds__(256) void lpips_tap_bwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+                                                     const float* __restrict__ w, long HW, int C, long npix,
+                                                     const float* __restrict__ up, __bf16* __restrict__ da) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+    const long n = p / HW;
+    const __bf16* pa = a + p * C;
+    const __bf16* pb = b + p * C;
+    __bf16* pd = da + p * C;
+    float sa = 0.f, sb = 0.f;
+    for (int c = 0; c < C; c += 8) {
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sa = fmaf((float)va[j], (float)va[j], sa);
+        sb = fmaf((float)vb[j], (float)vb[j], sb);
+      }
+    }
+    if (sa == 0.f) {
+      bf16x8 z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+      for (int c = 0; c < C; c += 8) *reinterpret_cast<bf16x8*>(pd + c) = z;
+      continue;
+    }
+    const float ra = sqrtf(sa), na = ra + 1e-10f, ia = 1.f / na, ib = 1.f / (sqrtf(sb) + 1e-10f);
+    float G = 0.f;
+    for (int c = 0; c < C; c += 8) {
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float av = (float)va[j];
+        G = fmaf(2.f * w[c + j] * (av * ia - (float)vb[j] * ib), av, G);
+      }
+    }
+    const float s = up[n] / (float)HW, k2 = G / (na * na * ra);
+    for (int c = 0; c < C; c += 8) {
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float av = (float)va[j];
+        const float g = 2.f * w[c + j] * (av * ia - (float)vb[j] * ib);
+        o[j] = (__bf16)(s * (g * ia - av * k2));
+      }
+      *reinterpret_cast<bf16x8*>(pd + c) = o;
+    }
+  }
+}
+
+inline int grid_for(long n) {
+  long g = (n + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float m1, float m2, float s0, float s1,
+                 float s2, void* y, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && B > 0 && H > 0 && W > 0, "nbp_vgg_prep: bad args");
+  const long HW = (long)H * W, n = B * HW;
+  vgg_prep_kernel<<<grid_for(n), 256, 0, S(s)>>>(x, HW, n, clamp, m0, m1, m2, s0, s1, s2, reinterpret_cast<__bf16*>(y));
+  return check_launch("vgg_prep");
+}
+
+int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && idx && B > 0 && H >= 2 && W >= 2 && C % 8 == 0, "nbp_maxpool2_fwd: bad args");
+  const long total8 = (long)B * (H / 2) * (W / 2) * (C / 8);
+  maxpool_fwd_kernel<<<grid_for(total8), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(x), H, W, C, total8,
+                                                         reinterpret_cast<__bf16*>(y), idx);
+  return check_launch("maxpool2_fwd");
+}
+
+int nbp_maxpool2_bwd(const void* dy, const unsigned char* idx, const void* post_in, int B, int H, int W, int C, void* dx,
+                     nbp_stream_t s) {
+  NBP_REQUIRE(dy && idx && post_in && dx && B > 0 && H >= 2 && W >= 2 && C % 8 == 0, "nbp_maxpool2_bwd: bad args");
+  const long total8 = (long)B * H * W * (C / 8);
+  maxpool_bwd_kernel<<<grid_for(total8), 256, 0, S(s)>>>(
+      reinterpret_cast<const __bf16*>(dy), idx, reinterpret_cast<const __bf16*>(post_in), H, W, C, total8,
+      reinterpret_cast<__bf16*>(dx));
+  return check_launch("maxpool2_bwd");
+}
+
+size_t nbp_feat_dist_workspace_doubles(long n) {
+  long g = (n + 255) / 256;
+  return (size_t)(g > 2048 ? 2048 : (g < 1 ? 1 : g));
+}
+
+int nbp_feat_dist_fwd(const void* a, const void* b, long n, int mode, double scale, double* ws, float* out,
+                      nbp_stream_t s) {
+  NBP_REQUIRE(a && b && ws && out && n > 0 && (mode == 0 || mode == 1), "nbp_feat_dist_fwd: bad args");
+  const int g = (int)nbp_feat_dist_workspace_doubles(n);
+  feat_dist_fwd<<<g, 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a), reinterpret_cast<const __bf16*>(b), n, mode, ws);
+  feat_dist_finalize<<<1, 64, 0, S(s)>>>(ws, g, scale, out);
+  return check_launch("feat_dist_fwd");
+}
+
+int nbp_feat_dist_bwd(const void* a, const void* b, long n, int mode, float scale, int relu_mask, const float* up,
+                      void* da, nbp_stream_t s) {
+  NBP_REQUIRE(a && b && up && da && n > 0 && (mode == 0 || mode == 1), "nbp_feat_dist_bwd: bad args");
+  feat_dist_bwd<<<grid_for(n), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a), reinterpret_cast<const __bf16*>(b),
+                                               n, mode, scale, relu_mask, up, reinterpret_cast<__bf16*>(da));
+  return check_launch("feat_dist_bwd");
+}
+
+int nbp_vgg_input_grad(const float* d8, const float* x, int B, int H, int W, int clamp, float s0, float s1, float s2,
+                       float* dx, nbp_stream_t s) {
+  NBP_REQUIRE(d8 && x && dx && B > 0 && H > 0 && W > 0, "nbp_vgg_input_grad: bad args");
+  const long HW = (long)H * W, n = B * HW;
+  vgg_input_grad_kernel<<<grid_for(n), 256, 0, S(s)>>>(d8, x, HW, n, clamp, s0, s1, s2, dx);
+  return check_launch("vgg_input_grad");
+}
+
+int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, nbp_stream_t s) {
+  NBP_REQUIRE(d && g && post && n > 0, "nbp_add_relu_masked: bad args");
+  add_relu_masked_kernel<<<grid_for(n), 256, 0, S(s)>>>(reinterpret_cast<__bf16*>(d), reinterpret_cast<const __bf16*>(g),
+                                                        reinterpret_cast<const __bf16*>(post), n);
+  return check_launch("add_relu_masked");
+}
+
+inline int lpips_chunks(long HW, int N) {
+  long c = (HW + 2047) / 2048, want = (1024 + N - 1) / N;
+  if (c > want) c = want;
+  return (int)(c < 1 ? 1 : (c > 1024 ? 1024 : c));
+}
+
+size_t nbp_lpips_tap_workspace_doubles(int N, long HW) { return (size_t)N * lpips_chunks(HW, N); }
+
+int nbp_lpips_tap_fwd(const void* a, const void* b, const float* w, int N, long HW, int C, int accumulate, double* ws,
+                      float* out, nbp_stream_t s) {
+  NBP_REQUIRE(a && b && w && ws && out && N > 0 && N <= 65535 && HW > 0 && C % 8 == 0, "nbp_lpips_tap_fwd: bad args");
+  const int chunks = lpips_chunks(HW, N);
+  lpips_tap_fwd<<<dim3(chunks, N), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a),
+                                                   reinterpret_cast<const __bf16*>(b), w, HW, C, chunks, ws);
+  lpips_finalize<<<cdiv(N, 256), 256, 0, S(s)>>>(ws, N, chunks, 1.0 / (double)HW, accumulate, out);
+  return check_launch("lpips_tap_fwd");
+}
+
+int nbp_lpips_tap_bwd(const void* a, const void* b, const float* w, int N, long HW, int C, const float* up, void* da,
+                      nbp_stream_t s) {
+  NBP_REQUIRE(a && b && w && up && da && N > 0 && HW > 0 && C % 8 == 0, "nbp_lpips_tap_bwd: bad args");
+  const long npix = (long)N * HW;
+  lpips_tap_bwd<<<grid_for(npix), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a),
+                                                  reinterpret_cast<const __bf16*>(b), w, HW, C, npix, up,
+                                                  reinterpret_cast<__bf16*>(da));
+  return check_launch("lpips_tap_bwd");
+}
+
+}  // extern "C"

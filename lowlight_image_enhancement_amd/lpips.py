@@ -1,0 +1,129 @@
+"""LPIPS (lpips==0.1.4, `lpips.LPIPS(net='vgg')`) on MI355X — the HybridLossPlus LPIPS term (NewBP_model/losses.py:
+265-274, 342-346).
+
+Restated from the package's published algorithm (the package and its weights are absent here: parity unpinned):
+ScalingLayer (x - shift) / scale with shift (-.030, -.088, -.188), scale (.458, .448, .450) (inputs taken as [-1, 1];
+`normalize=True` maps [0, 1] first); VGG16 features with taps relu1_2, relu2_2, relu3_3, relu4_3, relu5_3; per tap
+normalize_tensor over channels, squared difference, the non-negative 1x1 'lin' head, spatial average; sum over taps.
+Output [N, 1, 1, 1] per image like lpips.  The VGG16 trunk is the implicit-GEMM bf16 MFMA stack of vgg.py; the tap
+distances and their gradients are nbp_lpips_tap_* kernels; the tap gradients join the VGG backward walk.
+
+Weights: pretrained VGG16 + 'lin' weights cannot be downloaded here.  `weights` takes an lpips-style state_dict
+(`net.sliceK.N.*`, `linK.model.1.weight`) or a path (torch.load(weights_only=True)); None gives a deterministic
+synthetic model (kaiming VGG16, lin = |N(0, 0.1)|, seed 0).
+"""
+from __future__ import annotations
+
+import re
+import warnings
+from typing import Dict, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import vgg as _vgg
+from ._lib import call, query
+
+SHIFT = (-0.030, -0.088, -0.188)
+SCALE = (0.458, 0.448, 0.450)
+TAPS = (3, 8, 15, 22, 29)        # relu1_2, relu2_2, relu3_3, relu4_3, relu5_3 in vgg16.features
+TAP_CH = (64, 128, 256, 512, 512)
+
+
+def _split_state_dict(sd: Dict[str, torch.Tensor]):
+    feats, lins = {}, {}
+    for k, v in sd.items():
+        m = re.match(r"(?:net\.)?slice\d\.(\d+)\.(weight|bias)$", k)
+        if m:
+            feats[f"{m.group(1)}.{m.group(2)}"] = v
+            continue
+        m = re.match(r"lin(\d)\.model\.1\.weight$", k)
+        if m:
+            lins[int(m.group(1))] = v.reshape(-1).float()
+    return feats, lins
+
+
+class _LPIPSFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, in0, in1, module, normalize):
+        _lib.require_cuda(in0, in1)
+        if in0.shape != in1.shape or in0.dim() != 4 or in0.shape[1] != 3:
+            raise ValueError("LPIPS expects two [N,3,H,W] tensors of the same shape")
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("LPIPS gradient w.r.t. the second input is not implemented on MI355X")
+        x0 = in0.detach().float()
+        x1 = in1.detach().float()
+        if normalize:  # [0,1] -> [-1,1]
+            x0, x1 = 2 * x0 - 1, 2 * x1 - 1
+        stack, lins = module.parts(in0.device)
+        want = ctx.needs_input_grad[0]
+        with torch.no_grad():
+            # the ScalingLayer is the prologue's (x - mean) / std with mean = shift, std = scale (no clamp)
+            f0, tape, t0 = stack.forward(_vgg.prep_input(x0, SHIFT, SCALE, clamp=False), save=want, taps=TAPS)
+            _, _, t1 = stack.forward(_vgg.prep_input(x1, SHIFT, SCALE, clamp=False), save=False, taps=TAPS)
+        N = in0.shape[0]
+        out = torch.zeros(N, device=in0.device)
+        for k, tap in enumerate(TAPS):
+            a, b = t0[tap], t1[tap]
+            HW = a.shape[1] * a.shape[2]
+            ws = torch.empty(query("lpips_tap_workspace_doubles", N, HW), dtype=torch.float64, device=a.device)
+            call("lpips_tap_fwd", a, b, lins[k], N, HW, a.shape[3], 1, ws, out)
+        if want:
+            ctx.tape, ctx.t0, ctx.t1, ctx.stack, ctx.lins = tape, t0, t1, stack, lins
+            ctx.normalize = normalize
+            ctx.save_for_backward(x0)
+        return out.view(N, 1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, up):
+        (x0,) = ctx.saved_tensors
+        up = up.float().contiguous().view(-1)
+        grads = {}
+        for k, tap in enumerate(TAPS):
+            a, b = ctx.t0[tap], ctx.t1[tap]
+            g = torch.empty_like(a)
+            call("lpips_tap_bwd", a, b, ctx.lins[k], a.shape[0], a.shape[1] * a.shape[2], a.shape[3], up, g)
+            grads[tap] = g
+        last = TAPS[-1]
+        d_last = torch.empty_like(grads[last])  # relu5_3 is the stack's last map: its pre-ReLU gradient
+        call("add_relu_masked", d_last.zero_(), grads.pop(last), ctx.t0[last], d_last.numel())
+        d8 = ctx.stack.backward(ctx.tape, d_last, tap_grads=grads)
+        dx = _vgg.input_grad(d8, x0, SCALE, clamp=False)
+        if ctx.normalize:
+            dx = dx * 2
+        ctx.tape = ctx.t0 = ctx.t1 = None
+        return dx, None, None, None
+
+
+class LPIPS(nn.Module):
+    """lpips.LPIPS(net='vgg') drop-in: forward(in0, in1, retPerLayer=False, normalize=False) -> [N,1,1,1]."""
+
+    def __init__(self, net: str = "vgg", weights=None, version: str = "0.1", **_):
+        super().__init__()
+        if net != "vgg":
+            raise NotImplementedError("LPIPS on MI355X implements net='vgg' (the HybridLossPlus term)")
+        self._weights = weights
+        self._parts = {}
+
+    def parts(self, device):
+        key = str(device)
+        if key not in self._parts:
+            if self._weights is None:
+                warnings.warn("LPIPS: pretrained VGG16 / lin weights are not available offline; using a deterministic "
+                              "synthetic model", RuntimeWarning)
+                feats = _vgg.synthetic_state_dict(_vgg.VGG16_CFG, 30, seed=0)
+                g = torch.Generator().manual_seed(0)
+                lins = {k: (torch.randn(c, generator=g) * 0.1).abs() for k, c in enumerate(TAP_CH)}
+            else:
+                sd = torch.load(self._weights, map_location="cpu", weights_only=True) if isinstance(
+                    self._weights, str) else dict(self._weights)
+                feats, lins = _split_state_dict(sd)
+            stack = _vgg.VGGStack(_vgg.VGG16_CFG, 30, device, feats)
+            self._parts[key] = (stack, [lins[k].to(device).float().contiguous() for k in range(5)])
+        return self._parts[key]
+
+    def forward(self, in0, in1, retPerLayer: bool = False, normalize: bool = False):
+        if retPerLayer:
+            raise NotImplementedError("retPerLayer is not supported on MI355X")
+        return _LPIPSFn.apply(in0, in1.to(in0.device), self, bool(normalize))
