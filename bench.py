@@ -30,6 +30,16 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "training images/sec at 256×256 bs=16 (1/2/4/8 GPU) + PSNR vs CPU ref"
 CFG = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+# BASELINE.json configs[1] (the headline) and configs[2] (VGG19 perceptual + LPIPS + ΔE00, bs8 512²; weights from
+# configs/colab/sid_newbp_rgb.yml:78-96; LPIPS is the HybridLossPlus term's net='vgg', synthetic offline weights)
+WORKLOADS = {
+    "cfg2": dict(batch=16, img=256, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1),
+                 desc="cfg2: NAFNet w32 enc[2,2,4,8] mid12 dec[2,2,2,2] (29.16M), rgb/B2 PSF, bs16/GPU 256x256, "
+                      "L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW"),
+    "cfg3": dict(batch=8, img=512, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1, w_perc=0.02, w_lpips=0.05, w_deltaE=0.02),
+                 desc="cfg3: cfg2 model, rgb/B2 PSF, bs8/GPU 512x512, L1 + 0.05*SSIM + 0.1*Phys_srgb + 0.02*VGG19 perc "
+                      "+ 0.05*LPIPS(vgg) + 0.02*DeltaE00, clip 0.01 + AdamW (synthetic VGG/LPIPS weights)"),
+}
 BATCH, IMG = 16, 256
 W_L1, W_SSIM, W_PHYS = 1.0, 0.05, 0.1
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
@@ -108,7 +118,11 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="bf16: bf16 MFMA operands + fp32 accumulation (the reference's AMP training); "
                          "fp32: fp32 everywhere (parity mode)")
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     args = ap.parse_args()
+    global BATCH, IMG
+    wl = WORKLOADS[args.workload]
+    BATCH, IMG = wl["batch"], wl["img"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -127,7 +141,7 @@ def main():
     init_sd = {k: v.clone() for k, v in net.state_dict().items()}
     net = net.to(dev)
     net.precision = args.precision
-    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", w_l1=W_L1, w_ssim=W_SSIM, w_phys=W_PHYS)
+    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", **wl["w"])
     g = torch.Generator(device=dev).manual_seed(0 + rank)
     lq = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
     gt = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
@@ -162,8 +176,14 @@ def main():
         eb = 2 if a[-1] == 1 else 4
         return 2.0 * M * N * K, M * (N + K) * eb + N * K * 4
 
+    def conv3x3_cost(a):  # (x,B,H,W,Cin,w,Cout,bias,mode,R,y,y_dtype): VGG implicit-GEMM conv, K = 9*Cin
+        M, N, K = a[1] * a[2] * a[3], a[6], 9 * a[4]
+        by = M * a[4] * 2 + N * K * 2 + M * N * (2 if a[11] else 4) + (M * N * 2 if a[9] is not None else 0)
+        return 2.0 * M * N * K, by
+
     gemm_name = "gemm_f32" if args.precision == "fp32" else "gemm_bf16"
-    prof = {gemm_name: [], "wgrad_f32": []}
+    prof = {gemm_name: [], "wgrad_f32": [], "conv3x3_bf16": []}
+    _lib.PROFILE["conv3x3_bf16"] = mk("conv3x3_bf16", conv3x3_cost)
     _lib.PROFILE[gemm_name] = mk(gemm_name, gemm_f32_cost if args.precision == "fp32" else gemm_bf16_cost)
     _lib.PROFILE["wgrad_f32"] = mk("wgrad_f32", wgrad_cost)
     blk_events = []
@@ -214,6 +234,8 @@ def main():
 
     classes = {}
     for name, recs in prof.items():
+        if not recs:
+            continue
         ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in recs)
         classes[name] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), len(recs))
     dom = max(classes, key=lambda k: classes[k][0])
@@ -240,7 +262,7 @@ def main():
     if rank == 0:
         step_ms = elapsed / args.steps * 1e3
         res = {
-            "metric": METRIC,
+            "metric": METRIC if args.workload == "cfg2" else f"training images/sec ({args.workload})",
             "value": round(BATCH * world * args.steps / elapsed, 3),
             "unit": "img/s",
             "n_gpus": world,
@@ -252,8 +274,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision if args.precision == "bf16" else "f32",
             "data": "synthetic (U[0,1) sRGB, expo_ratio 1, torch default init, seed 0+rank)",
-            "config": {"workload": "cfg2: NAFNet w32 enc[2,2,4,8] mid12 dec[2,2,2,2] (29.16M), rgb/B2 PSF, "
-                                   "bs16/GPU 256x256, L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW",
+            "config": {"workload": wl["desc"],
                        "global_batch": BATCH * world, "image": IMG, "parallelism": f"dp{world}",
                        "launch": "hip-graph replay" if use_graph else "eager"},
             "roofline": roof,
@@ -266,7 +287,7 @@ def main():
             psnr, maxabs = psnr_vs_cpu(net, dev)
             res["psnr_vs_cpu_ref_db"] = round(psnr, 2) if psnr != float("inf") else "inf"
             res["max_abs_vs_cpu_ref"] = maxabs
-            if not args.no_cpu_baseline:
+            if not args.no_cpu_baseline and args.workload == "cfg2":
                 res["cpu_baseline"] = cpu_baseline(init_sd)
         print(json.dumps(res), flush=True)
     if world > 1:

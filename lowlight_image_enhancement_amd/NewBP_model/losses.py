@@ -222,6 +222,21 @@ class PerceptualLoss(nn.Module):
             target_img = target_img.to(generated_img.device)
         return _PerceptualFn.apply(generated_img, target_img, self)
 
+    def value_and_grad(self, gen, tgt, up: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Autograd-free form for the fused trainer (no host sync, HIP-graph capturable): writes the loss into
+        out[0] and returns up[0] * d loss / d gen (NCHW fp32)."""
+        stack = self.stack(gen.device)
+        ft, _, _ = stack.forward(_vgg.prep_input(tgt), save=False)
+        fg, tape, _ = stack.forward(_vgg.prep_input(gen), save=True)
+        n = fg.numel()
+        mode = 0 if self.use_mse else 1
+        scale = 1.0 / n if self.reduction == "mean" else 1.0
+        ws = torch.empty(query("feat_dist_workspace_doubles", n), dtype=torch.float64, device=gen.device)
+        call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out)
+        d = torch.empty_like(fg)
+        call("feat_dist_bwd", fg, ft, n, mode, float(scale), 1, up, d)
+        return _vgg.input_grad(stack.backward(tape, d), gen)
+
 
 class HybridLoss(nn.Module):
     """losses.py:72-89: total = l1 * L1 + lp * Perc; returns (total, l1, perc)."""

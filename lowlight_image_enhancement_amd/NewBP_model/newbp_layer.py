@@ -24,6 +24,17 @@ def _table(name: str) -> torch.Tensor:
     return torch.tensor([[c, e, c], [e, m, e], [c, e, c]], dtype=torch.float32).view(1, 1, 3, 3)
 
 
+# "Stressed" RGB crosstalk family (R > G > B leakage) — a BUILD artefact, not a reference table: the reference only
+# describes it (README.md:24,64,214).  S1/S2/S3 leak 1.5x/2x/2.5x of B2's off-centre mass (R .14, G .12,
+# B .10) with B2's edge:corner = 2:1 split: corner = leak / 12, edge = leak / 6, centre = 1 - leak.
+STRESSED = {f"S{i}": tuple(round(f * l, 6) for l in (0.14, 0.12, 0.10)) for i, f in ((1, 1.5), (2, 2.0), (3, 2.5))}
+
+
+def _stressed(spec: str, leak: float) -> torch.Tensor:
+    c, e, m = leak / 12.0, leak / 6.0, 1.0 - leak
+    return torch.tensor([[c, e, c], [e, m, e], [c, e, c]], dtype=torch.float32).view(1, 1, 3, 3)
+
+
 def build_psf_kernels(mode: str, kernel_spec: str = "P2") -> torch.Tensor:
     """newbp_layer.py:129-173: mono/P2 -> [1,1,3,3]; rgb/B2 -> [3,1,3,3]."""
     if mode not in {"mono", "rgb"}:
@@ -32,8 +43,10 @@ def build_psf_kernels(mode: str, kernel_spec: str = "P2") -> torch.Tensor:
         if kernel_spec != "P2":
             raise ValueError("mono mode expects kernel_spec 'P2'")
         return _table("P2")
+    if kernel_spec in STRESSED:
+        return torch.cat([_stressed(kernel_spec, leak) for leak in STRESSED[kernel_spec]], 0)
     if kernel_spec != "B2":
-        raise ValueError("rgb mode expects kernel_spec 'B2'")
+        raise ValueError("rgb mode expects kernel_spec 'B2' (or the stressed family 'S1', 'S2', 'S3')")
     return torch.cat((_table("R"), _table("G"), _table("B")), dim=0)
 
 

@@ -123,6 +123,27 @@ class LPIPS(nn.Module):
             self._parts[key] = (stack, [lins[k].to(device).float().contiguous() for k in range(5)])
         return self._parts[key]
 
+    def value_and_grad(self, in0, in1, up: torch.Tensor, out: torch.Tensor, clamp: bool = True) -> torch.Tensor:
+        """Autograd-free form for the fused trainer: out[N] = LPIPS(clamp01(in0), clamp01(in1)) per image (the
+        HybridLossPlus call on Bhat_srgb01 / B_srgb01), returns d(sum_n up[n] out[n]) / d in0 (through the clamp)."""
+        stack, lins = self.parts(in0.device)
+        f0, tape, t0 = stack.forward(_vgg.prep_input(in0, SHIFT, SCALE, clamp=clamp), save=True, taps=TAPS)
+        _, _, t1 = stack.forward(_vgg.prep_input(in1, SHIFT, SCALE, clamp=clamp), save=False, taps=TAPS)
+        N = in0.shape[0]
+        grads = {}
+        for k, tap in enumerate(TAPS):
+            a, b = t0[tap], t1[tap]
+            HW, C = a.shape[1] * a.shape[2], a.shape[3]
+            ws = torch.empty(query("lpips_tap_workspace_doubles", N, HW), dtype=torch.float64, device=a.device)
+            call("lpips_tap_fwd", a, b, lins[k], N, HW, C, int(k > 0), ws, out)
+            g = torch.empty_like(a)
+            call("lpips_tap_bwd", a, b, lins[k], N, HW, C, up, g)
+            grads[tap] = g
+        last = TAPS[-1]
+        d_last = torch.zeros_like(grads[last])
+        call("add_relu_masked", d_last, grads.pop(last), t0[last], d_last.numel())
+        return _vgg.input_grad(stack.backward(tape, d_last, tap_grads=grads), in0, SCALE, clamp=clamp)
+
     def forward(self, in0, in1, retPerLayer: bool = False, normalize: bool = False):
         if retPerLayer:
             raise NotImplementedError("retPerLayer is not supported on MI355X")

@@ -49,14 +49,29 @@ class NBPTrainer:
     def __init__(self, net: NAFNet, psf_mode: str = "rgb", psf_spec: str = "B2", w_l1: float = 1.0,
                  w_ssim: float = 0.0, w_phys: float = 0.1, lr: float = 5e-4, betas=(0.9, 0.999),
                  weight_decay: float = 0.01, eps: float = 1e-8, max_norm: Optional[float] = 0.01,
-                 scheduler: Optional[TrueCosineAnnealingLR] = None, process_group=None, bucket_mb: float = 25.0):
+                 scheduler: Optional[TrueCosineAnnealingLR] = None, process_group=None, bucket_mb: float = 25.0,
+                 w_deltaE: float = 0.0, w_perc: float = 0.0, w_lpips: float = 0.0, perceptual=None, lpips=None):
+        """Loss terms and weights as HybridLossPlus (losses.py:223-372): L1 (raw), Perc (VGG19), LPIPS (vgg), ΔE00,
+        SSIM, Phys_srgb; a zero weight skips the term.  `perceptual` / `lpips`: PerceptualLoss / LPIPS modules
+        (constructed with the synthetic offline weights when needed and not given)."""
         self.net = net
         dev = net.flat.device
         self.dev = dev
         self.kernel = normalize_kernels(build_psf_kernels(psf_mode, psf_spec)).to(dev)
         self.k_shared = int(psf_mode == "mono")
         self.w = (float(w_l1), float(w_ssim), float(w_phys))
-        self.up = torch.tensor(self.w, dtype=torch.float32, device=dev)  # upstream gradients of the loss terms
+        self.w_extra = dict(de=float(w_deltaE), perc=float(w_perc), lpips=float(w_lpips))
+        # upstream gradients of the loss terms, read by the kernels from device memory
+        self.up = torch.tensor(self.w + (float(w_deltaE), float(w_perc)), dtype=torch.float32, device=dev)
+        if w_perc and perceptual is None:
+            from .NewBP_model.losses import PerceptualLoss
+            perceptual = PerceptualLoss(device=dev)
+        if w_lpips and lpips is None:
+            from .lpips import LPIPS
+            lpips = LPIPS(net="vgg")
+        self.perceptual, self.lpips = perceptual, lpips
+        self.lpips_buf: Optional[torch.Tensor] = None
+        self.lpips_up: Optional[torch.Tensor] = None
         self.lr, self.betas, self.wd, self.eps = lr, betas, weight_decay, eps
         self.max_norm = max_norm if max_norm is not None else 0.0
         self.scheduler = scheduler
@@ -66,7 +81,7 @@ class NBPTrainer:
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.clip_ws = torch.empty(query("clip_workspace_doubles", n), dtype=torch.float64, device=dev)
         self.clip_state = torch.zeros(2, device=dev)
-        self.loss_buf = torch.zeros(4, device=dev)  # L1, SSIM, Phys, Total
+        self.loss_buf = torch.zeros(6, device=dev)  # L1, SSIM, Phys, DeltaE, Perc, Total
         self.finite_flag = torch.zeros(1, dtype=torch.int32, device=dev)
         self.t = 0
         self.pg = process_group
@@ -124,6 +139,21 @@ class NBPTrainer:
                  1, ph_ws, self.loss_buf[2:3], sign)
             call("phys_l1_bwd", sign, out, self.kernel, self.k_shared, self.up[2:3], B, C, H, W, 3, 3, 0, 1, tmp)
             call("add", d_out, tmp, d_out, n, 0)
+        wde, wpe, wlp = self.w_extra["de"], self.w_extra["perc"], self.w_extra["lpips"]
+        if wde != 0.0:
+            de_ws = torch.empty(query("de00_workspace_doubles", B * H * W), dtype=torch.float64, device=lq.device)
+            call("de00_loss_fwd", out, gt, B, H, W, 1, 1e-6, de_ws, self.loss_buf[3:4])
+            call("de00_loss_bwd", out, gt, B, H, W, 1, 1e-6, self.up[3:4], tmp)
+            call("add", d_out, tmp, d_out, n, 0)
+        if wpe != 0.0:
+            g = self.perceptual.value_and_grad(out, gt, self.up[4:5], self.loss_buf[4:5])
+            call("add", d_out, g, d_out, n, 0)
+        if wlp != 0.0:
+            if self.lpips_buf is None or self.lpips_buf.numel() != B:
+                self.lpips_buf = torch.zeros(B, device=lq.device)
+                self.lpips_up = torch.full((B,), wlp / B, device=lq.device)  # d(w * mean_n LPIPS_n)
+            g = self.lpips.value_and_grad(out, gt, self.lpips_up, self.lpips_buf, clamp=True)
+            call("add", d_out, g, d_out, n, 0)
         hook = self._on_stage if self.world > 1 else None
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
         if self.world > 1:
@@ -210,8 +240,11 @@ class NBPTrainer:
     def logs(self, reduce: bool = True) -> Dict[str, float]:
         """Loss dict of the last step (host sync), averaged over ranks like reduce_loss_dict (base_model.py:335-360)."""
         wl1, wss, wph = self.w
+        wde, wpe, wlp = self.w_extra["de"], self.w_extra["perc"], self.w_extra["lpips"]
         buf = self.loss_buf.clone()
-        buf[3] = wl1 * buf[0] + wss * buf[1] + wph * buf[2]
+        lp = self.lpips_buf.mean().view(1) if (wlp and self.lpips_buf is not None) else torch.zeros(1, device=buf.device)
+        buf = torch.cat([buf, lp])  # L1, SSIM, Phys, DeltaE, Perc, Total, LPIPS
+        buf[5] = wl1 * buf[0] + wss * buf[1] + wph * buf[2] + wde * buf[3] + wpe * buf[4] + wlp * buf[6]
         if reduce and self.world > 1:
             dist.all_reduce(buf, group=self.pg)
             buf /= self.world
@@ -219,10 +252,16 @@ class NBPTrainer:
         if not torch.isfinite(vals).all():
             raise RuntimeError(f"HybridLossPlus detected non-finite values: {vals.tolist()}")
         out = {"L1_raw": float(vals[0])}
+        if wpe:
+            out["Perc"] = float(vals[4])
+        if wlp:
+            out["LPIPS"] = float(vals[6])
+        if wde:
+            out["DeltaE"] = float(vals[3])
         if wss:
             out["SSIM"] = float(vals[1])
         if wph:
             out["Phys"] = float(vals[2])
-        out["Total"] = float(vals[3])
+        out["Total"] = float(vals[5])
         out["grad_norm"] = float(self.clip_state[0].cpu())
         return out

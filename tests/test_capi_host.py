@@ -141,3 +141,21 @@ def test_trainer_cosine_schedule():
     s = TrueCosineAnnealingLR(5e-4, 300000, 1e-6)
     assert abs(s(0) - 5e-4) < 1e-12 and abs(s(300000) - 1e-6) < 1e-12
     assert abs(s(150000) - (1e-6 + (5e-4 - 1e-6) / 2)) < 1e-12
+
+
+def test_stressed_psf_family():
+    """S1/S2/S3 (the build's stressed R > G > B family): leakage ordered R > G > B and growing with the level; the
+    bit-exact host normalisation agrees with the oracle's torch order."""
+    import oracle.physics as P
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_layer import build_psf_kernels, normalize_kernels
+    prev = None
+    for spec in ("S1", "S2", "S3"):
+        k = build_psf_kernels("rgb", spec)
+        centre = k[:, 0, 1, 1]
+        assert centre[0] < centre[1] < centre[2]          # R leaks most
+        if prev is not None:
+            assert (centre < prev).all()
+        prev = centre
+        assert torch.equal(normalize_kernels(k), P.normalize_psf(P.build_psf_kernels("rgb", spec)))
+    with pytest.raises(ValueError):
+        build_psf_kernels("mono", "S1")

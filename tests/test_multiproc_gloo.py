@@ -49,7 +49,7 @@ def _worker(rank, world, port, bucket_mb, q):
         tr._handles.clear()
         expect = torch.arange(net.numel, dtype=torch.float32) * sum(r + 1 for r in range(world))
         ok_sum = torch.equal(tr.grad, expect)
-        tr.loss_buf.copy_(torch.tensor([1.0 + rank, 2.0, 3.0 * (rank + 1), 0.0]))
+        tr.loss_buf.copy_(torch.tensor([1.0 + rank, 2.0, 3.0 * (rank + 1), 0.0, 0.0, 0.0]))
         logs = tr.logs()
         q.put((rank, same, ok_sum, n_buckets, sum(calls), logs))
     finally:
