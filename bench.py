@@ -189,18 +189,19 @@ def main():
     blk_events = []
     orig_fwd, orig_bwd = net._block_fwd, net._block_bwd
 
-    def timed(fn):
+    def timed(fn, kind):
         def w(*a, **k):
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record()
             r = fn(*a, **k)
             e1.record()
-            blk_events.append((e0, e1))
+            geo = (a[3], a[4], a[5], a[6]) if kind == "fwd" else a[4]  # (B, h, w, c)
+            blk_events.append((e0, e1, kind, f"{geo[1]}x{geo[2]}xC{geo[3]}"))
             return r
         return w
 
-    net._block_fwd, net._block_bwd = timed(orig_fwd), timed(orig_bwd)
+    net._block_fwd, net._block_bwd = timed(orig_fwd, "fwd"), timed(orig_bwd, "bwd")
 
     # profiled pass: K eager steps with per-kernel HIP events on the launch stream (graph replays cannot carry them)
     for _ in range(args.steps):
@@ -255,7 +256,16 @@ def main():
                  "ms_per_step": round(ms / args.steps, 3), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
                  "flop_intensity": round(fl / max(by, 1), 2), "tflops": round(tflops, 2),
                  "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in classes.items()}})
-    blk_ms = sum(e0.elapsed_time(e1) for e0, e1 in blk_events) / args.steps
+    blk_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in blk_events) / args.steps
+    per_level = {}
+    for e0, e1, kind, lvl in blk_events:
+        d = per_level.setdefault(lvl, {"blocks_fwd": 0, "fwd_ms": 0.0, "bwd_ms": 0.0})
+        d[kind + "_ms"] += e0.elapsed_time(e1) / args.steps
+        if kind == "fwd":
+            d["blocks_fwd"] += 1
+    for d in per_level.values():
+        d["blocks_fwd"] //= args.steps
+        d["fwd_ms"], d["bwd_ms"] = round(d["fwd_ms"], 3), round(d["bwd_ms"], 3)
     blk_bytes = nafblock_bytes(net, BATCH, IMG, IMG)
     blk_gbps = blk_bytes / (blk_ms * 1e-3) / 1e9
 
@@ -279,6 +289,7 @@ def main():
                        "launch": "hip-graph replay" if use_graph else "eager"},
             "roofline": roof,
             "nafblock_roofline": {"bytes_per_step": blk_bytes, "ms_per_step": round(blk_ms, 3),
+                                  "per_level_eager": per_level,
                                   "achieved_GBps": round(blk_gbps, 1), "peak_GBps": HBM_PEAK_GBPS,
                                   "frac": round(blk_gbps / HBM_PEAK_GBPS, 4)},
             "losses": logs,

@@ -106,10 +106,10 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
 /* out[i] = sum_{s<S} slab[s*L + i] (fixed order); batched: out[b][i] = scale * sum_s slab[b][s][i]. */
 int nbp_reduce_slab(const float* slab, int S, long L, float* out, nbp_stream_t s);
 /* Deferred gradient reductions (thread-local): after nbp_grad_reduce_defer(s), scale-1 gradient-slab reductions
-   issued on stream s (nbp_reduce_slab and the internal ones of nbp_wgrad_f32 / nbp_dw_bwd / nbp_sca_sg_dw_bwd /
-   intro / ending / LN backward) are queued; nbp_grad_reduce_flush(stop, s) executes the queue with one launch per
-   48 slabs (bitwise identical to immediate mode) and, if stop, ends deferral.  The caller keeps every queued slab
-   alive and unmodified until the flush. */
+   issued by this thread (nbp_reduce_slab and the internal ones of nbp_wgrad_f32 / nbp_dw_bwd / nbp_sca_sg_dw_bwd /
+   intro / ending / LN backward, on s or on a side stream) are queued; nbp_grad_reduce_flush(stop, s) executes the
+   queue on s with one launch per 48 slabs (bitwise identical to immediate mode) and, if stop, ends deferral.  The
+   caller orders s after every stream that produced a queued slab and keeps the slabs alive until the flush. */
 int nbp_grad_reduce_defer(nbp_stream_t s);
 /* Layer-scale residual y = x + s * (h W^T + b) (NAFNet_arch.py:72,80) gradients from U = dy^T h [N][K] and
    V = colsum(dy) [N] of the UNSCALED dy: dW = s (.) U (row-wise), db = s (.) V, ds = rowsum(W (.) U) + b (.) V.
@@ -119,14 +119,15 @@ int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const f
 int nbp_grad_reduce_flush(int stop, nbp_stream_t s);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
-/* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC:
- * writes yhat (normalised, optional), nout = w*yhat + b and den = sqrt(var + eps) per pixel. */
-int nbp_ln_nhwc_grid(long M, int C);
-int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* yhat, void* nout, float* den, long M, int C,
-                    float eps, int dtype, nbp_stream_t s);
-/* closed-form backward (:277-289) + residual gradient dres; per-block partials of dw/db in slab_w/slab_b
- * ([nbp_ln_nhwc_grid][C] each, fold with nbp_reduce_slab). */
-int nbp_ln_bwd_nhwc(const void* dn, const void* yhat, const float* den, const float* w, const void* dres, void* dx,
+/* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC, C a power of two
+ * (multiple of 16 bytes): writes nout = w * (x - mu) / den + b and stats[M][2] = {mu, den = sqrt(var + eps)}.
+ * The closed-form backward (:277-289) recomputes yhat from x and stats, adds the residual gradient dres and writes
+ * per-block partials of dw / db into slab_w / slab_b ([nbp_ln_nhwc_grid(M, C, dtype)][C] each, fold with
+ * nbp_reduce_slab). */
+int nbp_ln_nhwc_grid(long M, int C, int dtype);
+int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* nout, float* stats, long M, int C, float eps,
+                    int dtype, nbp_stream_t s);
+int nbp_ln_bwd_nhwc(const void* dn, const void* x, const float* stats, const float* w, const void* dres, void* dx,
                     float* slab_w, float* slab_b, long M, int C, int dtype, nbp_stream_t s);
 /* NCHW variants for the standalone LayerNorm2d module. */
 int nbp_ln_fwd_nchw(const float* x, const float* w, const float* b, float* y, float* yhat, float* den, int N, int C,

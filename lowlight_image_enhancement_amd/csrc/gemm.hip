@@ -513,9 +513,10 @@ thread_local std::vector<PDesc> g_post;
 thread_local bool g_defer = false;
 thread_local hipStream_t g_defer_stream = nullptr;
 
-// scale-1 reduction of a gradient slab: queued while deferral is on for this stream, launched otherwise
+// scale-1 reduction of a gradient slab: queued while deferral is on (from any stream of this thread: the caller orders
+// the flush after every stream that produced a queued slab), launched otherwise
 void grad_reduce(const float* slab, int S, long L, float* out, hipStream_t st) {
-  if (g_defer && st == g_defer_stream) {
+  if (g_defer) {
     g_pending.push_back(RDesc{slab, out, L, S, reduce_ty(S, L), 0, 0});
     return;
   }
@@ -669,7 +670,7 @@ int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const f
                          float* db, float* dscale, int N, int K, nbp_stream_t s) {
   NBP_REQUIRE(U && V && W && b && scale && dW && db && dscale && N > 0 && K > 0, "nbp_layer_scale_grad: bad args");
   PDesc d{U, V, W, b, scale, dW, db, dscale, N, K, 0, 0};
-  if (g_defer && S(s) == g_defer_stream) {
+  if (g_defer) {
     g_post.push_back(d);
     return NBP_OK;
   }

@@ -142,8 +142,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  bf16x8 ra[A_IT], rb[B_IT];
-  auto load_tiles = [&](int k0) {
+  // two register sets: with BK = 64 the loads of K-tiles t+1 and t+2 are in flight while tile t is multiplied
+  bf16x8 ra0[A_IT], rb0[B_IT], ra1[A_IT], rb1[B_IT];
+  auto load_tiles = [&](int k0, bf16x8* ra, bf16x8* rb) {
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int idx = tid + it * 256;
@@ -181,7 +182,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       rb[it] = v;
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const bf16x8* ra, const bf16x8* rb) {
     __bf16* a = As + buf * BM * LS;
     __bf16* b = Bs + buf * BN * LS;
 #pragma unroll
@@ -195,17 +196,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       *reinterpret_cast<bf16x8*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
     }
   };
-
-  const int nk = (K + BK - 1) / BK;
-  load_tiles(0);
-  store_tiles(0);
-  __syncthreads();
   const int arow = wm * (BM / 2) + (lane & 31);
   const int brow = wn * (BN / 2) + (lane & 31);
   const int kh = (lane >> 5) * 8;
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nk) load_tiles((t + 1) * BK);
+  auto compute = [&](int buf) {
     const __bf16* a_s = As + buf * BM * LS;
     const __bf16* b_s = Bs + buf * BN * LS;
 #pragma unroll
@@ -220,8 +214,45 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < nk) store_tiles(buf ^ 1);
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  if constexpr (BK == 32) {
+    // short K (one or two tiles): one register set, the next tile's loads in flight during the MFMAs
+    load_tiles(0, ra0, rb0);
+    store_tiles(0, ra0, rb0);
     __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < nk) load_tiles((t + 1) * BK, ra0, rb0);
+      compute(buf);
+      if (t + 1 < nk) store_tiles(buf ^ 1, ra0, rb0);
+      __syncthreads();
+    }
+  } else {
+    load_tiles(0, ra0, rb0);
+    store_tiles(0, ra0, rb0);
+    if (nk > 1) load_tiles(BK, ra1, rb1);
+    if (nk > 2) load_tiles(2 * BK, ra0, rb0);
+    __syncthreads();
+    // steady state, unrolled by two so each register set is addressed statically:
+    //   even step t: tile t in LDS buf 0, t+1 in set 1, t+2 in flight in set 0
+    //   odd step t+1: tile t+1 in LDS buf 1, t+2 in set 0, t+3 in flight in set 1
+    for (int t = 0; t < nk; t += 2) {
+      compute(0);
+      if (t + 1 < nk) {
+        store_tiles(1, ra1, rb1);
+        if (t + 3 < nk) load_tiles((t + 3) * BK, ra1, rb1);
+      }
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      compute(1);
+      if (t + 2 < nk) {
+        store_tiles(0, ra0, rb0);
+        if (t + 4 < nk) load_tiles((t + 4) * BK, ra0, rb0);
+      }
+      __syncthreads();
+    }
   }
 
   // ---- epilogue through LDS

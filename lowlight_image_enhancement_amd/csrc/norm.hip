@@ -7,126 +7,201 @@ using namespace nbp;
 
 namespace {
 
-constexpr int kMaxV = 4;  // C <= 4 * 4 * 64 = 1024
-
-template <int G, typename T>
-__global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, const float* __restrict__ w,
-                                                   const float* __restrict__ b, T* __restrict__ yhat,
-                                                   T* __restrict__ nout, float* __restrict__ den, long M, int C,
-                                                   float eps) {
-  const int lane = threadIdx.x & 63, lg = lane % G;
-  constexpr int RPW = 64 / G;
-  const int V = C / (4 * G);
-  const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const long nwaves = (long)gridDim.x * (blockDim.x / 64);
-  for (long r0 = wave_global * RPW; r0 < M; r0 += nwaves * RPW) {
-    const long row = r0 + lane / G;
-    const bool ok = row < M;
-    float4 v[kMaxV];
-    float s = 0.f;
+// NHWC kernels: a row (pixel) of C channels = G lanes x V chunks of 16 bytes (E = 8 bf16 / 4 fp32 elements);
+// each wave handles 2 x (64 / G) rows per iteration (two independent rows per lane group for load-level
+// parallelism).  The forward writes the affine output and per-row stats (mu, den = sqrt(var + eps)); the backward
+// recomputes yhat = (x - mu) / den from the block input it keeps anyway, so yhat is never stored.
+template <typename T>
+__device__ __forceinline__ void ld_chunk(const T* p, float* f) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+  } else {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
 #pragma unroll
-    for (int j = 0; j < kMaxV; ++j) {
-      if (j < V) {
-        v[j] = ok ? ldq(x + row * C + (j * G + lg) * 4) : f4(0.f);
-        s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
-      }
-    }
-    s = group_sum<G>(s);
-    const float mu = s / (float)C;
-    float q = 0.f;
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st_chunk(T* p, const float* f) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  } else {
+    bf16x8 v;
 #pragma unroll
-    for (int j = 0; j < kMaxV; ++j) {
-      if (j < V) {
-        const float4 d = v[j] - f4(mu);
-        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-      }
-    }
-    q = group_sum<G>(q);
-    const float var = q / (float)C;
-    const float dd = sqrtf(var + eps);
-    if (!ok) continue;
-#pragma unroll
-    for (int j = 0; j < kMaxV; ++j) {
-      if (j < V) {
-        const int c = (j * G + lg) * 4;
-        const float4 d = v[j] - f4(mu);
-        const float4 yh = make_float4(d.x / dd, d.y / dd, d.z / dd, d.w / dd);
-        if (yhat) stq(yhat + row * C + c, yh);
-        stq(nout + row * C + c, fma4(ld4(w + c), yh, ld4(b + c)));
-      }
-    }
-    if (lg == 0) den[row] = dd;
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)f[j];
+    *reinterpret_cast<bf16x8*>(p) = v;
   }
 }
 
-// dx = (g - yhat * mean(g*yhat) - mean(g)) / den + dres,  g = dn * w;  per-block partials of sum(dn*yhat), sum(dn)
-template <int G, typename T>
-__global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, const T* __restrict__ yhat,
-                                                   const float* __restrict__ den, const float* __restrict__ w,
+template <int G, int V, typename T>
+__global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ b, T* __restrict__ nout,
+                                                   float2* __restrict__ stats, long M, float eps) {
+  constexpr int E = 16 / sizeof(T), C = G * V * E, RPW = 64 / G;
+  const int lane = threadIdx.x & 63, lg = lane % G;
+  const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const long nwaves = (long)gridDim.x * (blockDim.x / 64);
+  float wr[V][E], br[V][E];
+#pragma unroll
+  for (int j = 0; j < V; ++j)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      wr[j][e] = w[(j * G + lg) * E + e];
+      br[j][e] = b[(j * G + lg) * E + e];
+    }
+  for (long r0 = wave_global * 2 * RPW; r0 < M; r0 += nwaves * 2 * RPW) {
+    long row[2];
+    bool ok[2];
+    float v[2][V][E];
+    float s[2] = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      row[r] = r0 + r * RPW + lane / G;
+      ok[r] = row[r] < M;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        if (ok[r]) ld_chunk(x + row[r] * C + (j * G + lg) * E, v[r][j]);
+        else
+#pragma unroll
+          for (int e = 0; e < E; ++e) v[r][j][e] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e) s[r] += v[r][j][e];
+    s[0] = group_sum<G>(s[0]);
+    s[1] = group_sum<G>(s[1]);
+    float q[2] = {0.f, 0.f}, mu[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      mu[r] = s[r] / (float)C;
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float d = v[r][j][e] - mu[r];
+          q[r] = fmaf(d, d, q[r]);
+        }
+    }
+    q[0] = group_sum<G>(q[0]);
+    q[1] = group_sum<G>(q[1]);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (!ok[r]) continue;
+      const float dd = sqrtf(q[r] / (float)C + eps), inv = 1.f / dd;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = (j * G + lg) * E;
+        float o[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) o[e] = fmaf(wr[j][e], (v[r][j][e] - mu[r]) * inv, br[j][e]);
+        st_chunk(nout + row[r] * C + c, o);
+      }
+      if (lg == 0) stats[row[r]] = make_float2(mu[r], dd);
+    }
+  }
+}
+
+// dx = (g - yhat * mean(g * yhat) - mean(g)) / den + dres,  g = dn * w,  yhat = (x - mu) / den;
+// per-block partials of sum(dn * yhat) and sum(dn) into slab_w / slab_b ([grid][C], fixed-order fold)
+template <int G, int V, typename T>
+__global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, const T* __restrict__ x,
+                                                   const float2* __restrict__ stats, const float* __restrict__ w,
                                                    const T* __restrict__ dres, T* __restrict__ dx,
-                                                   float* __restrict__ slab_w, float* __restrict__ slab_b, long M,
-                                                   int C) {
-  __shared__ float red[4][2][1024];
+                                                   float* __restrict__ slab_w, float* __restrict__ slab_b, long M) {
+  constexpr int E = 16 / sizeof(T), C = G * V * E, RPW = 64 / G;
+  __shared__ float red[4][2][C];
   const int lane = threadIdx.x & 63, lg = lane % G, wv = threadIdx.x >> 6;
-  constexpr int RPW = 64 / G;
-  const int V = C / (4 * G);
   const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + wv;
   const long nwaves = (long)gridDim.x * (blockDim.x / 64);
-  float4 aw[kMaxV], ab[kMaxV];
+  float aw[V][E], ab[V][E], wr[V][E];
 #pragma unroll
-  for (int j = 0; j < kMaxV; ++j) aw[j] = ab[j] = f4(0.f);
-  for (long r0 = wave_global * RPW; r0 < M; r0 += nwaves * RPW) {
-    const long row = r0 + lane / G;
-    const bool ok = row < M;
-    float4 g[kMaxV], yh[kMaxV];
-    float sg = 0.f, sgy = 0.f;
+  for (int j = 0; j < V; ++j)
 #pragma unroll
-    for (int j = 0; j < kMaxV; ++j) {
-      if (j < V) {
-        const int c = (j * G + lg) * 4;
-        const float4 d = ok ? ldq(dn + row * C + c) : f4(0.f);
-        yh[j] = ok ? ldq(yhat + row * C + c) : f4(0.f);
-        g[j] = d * ld4(w + c);
-        aw[j] = fma4(d, yh[j], aw[j]);
-        ab[j] += d;
-        sg += (g[j].x + g[j].y) + (g[j].z + g[j].w);
-        const float4 gy = g[j] * yh[j];
-        sgy += (gy.x + gy.y) + (gy.z + gy.w);
+    for (int e = 0; e < E; ++e) {
+      aw[j][e] = ab[j][e] = 0.f;
+      wr[j][e] = w[(j * G + lg) * E + e];
+    }
+  for (long r0 = wave_global * 2 * RPW; r0 < M; r0 += nwaves * 2 * RPW) {
+    long row[2];
+    bool ok[2];
+    float d[2][V][E], yh[2][V][E];
+    float2 st[2];
+    float sg[2] = {0.f, 0.f}, sgy[2] = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      row[r] = r0 + r * RPW + lane / G;
+      ok[r] = row[r] < M;
+      st[r] = ok[r] ? stats[row[r]] : make_float2(0.f, 1.f);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = (j * G + lg) * E;
+        if (ok[r]) {
+          ld_chunk(dn + row[r] * C + c, d[r][j]);
+          ld_chunk(x + row[r] * C + c, yh[r][j]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) d[r][j][e] = yh[r][j][e] = 0.f;
+        }
       }
     }
-    sg = group_sum<G>(sg);
-    sgy = group_sum<G>(sgy);
-    if (!ok) continue;
-    const float mg = sg / (float)C, mgy = sgy / (float)C;
-    const float inv = 1.f / den[row];
+    const float rinv[2] = {1.f / st[0].y, 1.f / st[1].y};
 #pragma unroll
-    for (int j = 0; j < kMaxV; ++j) {
-      if (j < V) {
-        const int c = (j * G + lg) * 4;
-        float4 o = (g[j] - yh[j] * f4(mgy) - f4(mg)) * f4(inv);
-        if (dres) o += ldq(dres + row * C + c);
-        stq(dx + row * C + c, o);
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float y = ok[r] ? (yh[r][j][e] - st[r].x) * rinv[r] : 0.f;
+          yh[r][j][e] = y;
+          const float g = d[r][j][e] * wr[j][e];
+          sg[r] += g;
+          sgy[r] = fmaf(g, y, sgy[r]);
+          aw[j][e] = fmaf(d[r][j][e], y, aw[j][e]);
+          ab[j][e] += d[r][j][e];
+        }
+      }
+    sg[0] = group_sum<G>(sg[0]);
+    sg[1] = group_sum<G>(sg[1]);
+    sgy[0] = group_sum<G>(sgy[0]);
+    sgy[1] = group_sum<G>(sgy[1]);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (!ok[r]) continue;
+      const float mg = sg[r] / (float)C, mgy = sgy[r] / (float)C, inv = rinv[r];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = (j * G + lg) * E;
+        float o[E], rr[E];
+        if (dres) ld_chunk(dres + row[r] * C + c, rr);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          o[e] = (d[r][j][e] * wr[j][e] - yh[r][j][e] * mgy - mg) * inv;
+          if (dres) o[e] += rr[e];
+        }
+        st_chunk(dx + row[r] * C + c, o);
       }
     }
   }
-  // reduce partials over lanes sharing lg, then over the block's waves
+  // fold the partials over lanes sharing lg, then over the block's waves (fixed order)
 #pragma unroll
-  for (int j = 0; j < kMaxV; ++j) {
-    if (j < V) {
+  for (int j = 0; j < V; ++j)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
 #pragma unroll
       for (int o = G; o < 64; o <<= 1) {
-        aw[j].x += __shfl_xor(aw[j].x, o, 64); aw[j].y += __shfl_xor(aw[j].y, o, 64);
-        aw[j].z += __shfl_xor(aw[j].z, o, 64); aw[j].w += __shfl_xor(aw[j].w, o, 64);
-        ab[j].x += __shfl_xor(ab[j].x, o, 64); ab[j].y += __shfl_xor(ab[j].y, o, 64);
-        ab[j].z += __shfl_xor(ab[j].z, o, 64); ab[j].w += __shfl_xor(ab[j].w, o, 64);
+        aw[j][e] += __shfl_xor(aw[j][e], o, 64);
+        ab[j][e] += __shfl_xor(ab[j][e], o, 64);
       }
       if (lane < G) {
-        const int c = (j * G + lg) * 4;
-        st4(&red[wv][0][c], aw[j]);
-        st4(&red[wv][1][c], ab[j]);
+        red[wv][0][(j * G + lg) * E + e] = aw[j][e];
+        red[wv][1][(j * G + lg) * E + e] = ab[j][e];
       }
     }
-  }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float sw = 0.f, sb = 0.f;
@@ -206,76 +281,61 @@ __global__ void ln_wb_nchw(const float* __restrict__ dy, const float* __restrict
   }
 }
 
-template <int G>
-int ln_grid(long M) {
-  const long rows_per_block = 4L * (64 / G);
+int ln_grid(long M, int C, int dtype) {
+  const int chunks = C / (dtype == 1 ? 8 : 4);
+  const int G = chunks >= 64 ? 64 : chunks;
+  const long rows_per_block = 4L * 2 * (64 / G);
   long g = (M + rows_per_block - 1) / rows_per_block;
   if (g > 1024) g = 1024;
   return (int)(g < 1 ? 1 : g);
 }
 
-int pick_G(int C) {
-  const int q = C / 4;
-  return q >= 64 ? 64 : q;
-}
+// (G, V) from the chunk count: G = min(64, C / E), V = C / E / G
+#define NBP_LN_DISPATCH(KERNEL, ...)                                                          \
+  switch (C / E) {                                                                            \
+    case 1: KERNEL<1, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
+    case 2: KERNEL<2, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
+    case 4: KERNEL<4, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
+    case 8: KERNEL<8, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
+    case 16: KERNEL<16, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                         \
+    case 32: KERNEL<32, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                         \
+    case 64: KERNEL<64, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                         \
+    case 128: KERNEL<64, 2, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                        \
+    default: KERNEL<64, 4, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                         \
+  }
 
 }  // namespace
 
 extern "C" {
 
-int nbp_ln_nhwc_grid(long M, int C) {
-  switch (pick_G(C)) {
-    case 64: return ln_grid<64>(M);
-    case 32: return ln_grid<32>(M);
-    case 16: return ln_grid<16>(M);
-    case 8: return ln_grid<8>(M);
-    case 4: return ln_grid<4>(M);
-    default: return ln_grid<2>(M);
-  }
-}
+int nbp_ln_nhwc_grid(long M, int C, int dtype) { return ln_grid(M, C, dtype); }
 
-int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* yhat, void* nout, float* den, long M, int C,
-                    float eps, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(x && w && b && nout && den && M > 0, "nbp_ln_fwd_nhwc: bad args");
-  NBP_REQUIRE(C >= 8 && C <= 1024 && (C & (C - 1)) == 0, "nbp_ln_fwd_nhwc: C must be a power of two in [8,1024]");
-  const int g = nbp_ln_nhwc_grid(M, C);
+int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* nout, float* stats, long M, int C, float eps,
+                    int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(x && w && b && nout && stats && M > 0, "nbp_ln_fwd_nhwc: bad args");
+  const int E = dtype == 1 ? 8 : 4;
+  NBP_REQUIRE(C >= E && C / E <= 256 && (C & (C - 1)) == 0, "nbp_ln_fwd_nhwc: C must be a power of two in [%d, %d]",
+              E, 256 * E);
+  const int g = ln_grid(M, C, dtype);
   hipStream_t st = S(s);
   NBP_DISPATCH_T(dtype, {
-    const T* xx = (const T*)x;
-    T* yy = (T*)yhat;
-    T* nn = (T*)nout;
-    switch (pick_G(C)) {
-      case 64: ln_fwd_nhwc<64, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
-      case 32: ln_fwd_nhwc<32, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
-      case 16: ln_fwd_nhwc<16, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
-      case 8: ln_fwd_nhwc<8, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
-      case 4: ln_fwd_nhwc<4, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
-      default: ln_fwd_nhwc<2, T><<<g, 256, 0, st>>>(xx, w, b, yy, nn, den, M, C, eps); break;
-    }
+    NBP_LN_DISPATCH(ln_fwd_nhwc, (const T*)x, w, b, (T*)nout, reinterpret_cast<float2*>(stats), M, eps);
   });
   return check_launch("ln_fwd_nhwc");
 }
 
-// slab_w / slab_b: [grid][C] floats each (grid = nbp_ln_nhwc_grid(M, C)); reduced by the caller (nbp_reduce_slab)
-int nbp_ln_bwd_nhwc(const void* dn, const void* yhat, const float* den, const float* w, const void* dres, void* dx,
+// slab_w / slab_b: [nbp_ln_nhwc_grid(M, C, dtype)][C] floats each; reduced by the caller (nbp_reduce_slab)
+int nbp_ln_bwd_nhwc(const void* dn, const void* x, const float* stats, const float* w, const void* dres, void* dx,
                     float* slab_w, float* slab_b, long M, int C, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(dn && yhat && den && w && dx && slab_w && slab_b && M > 0, "nbp_ln_bwd_nhwc: bad args");
-  NBP_REQUIRE(C >= 8 && C <= 1024 && (C & (C - 1)) == 0, "nbp_ln_bwd_nhwc: C must be a power of two in [8,1024]");
-  const int g = nbp_ln_nhwc_grid(M, C);
+  NBP_REQUIRE(dn && x && stats && w && dx && slab_w && slab_b && M > 0, "nbp_ln_bwd_nhwc: bad args");
+  const int E = dtype == 1 ? 8 : 4;
+  NBP_REQUIRE(C >= E && C / E <= 256 && (C & (C - 1)) == 0, "nbp_ln_bwd_nhwc: C must be a power of two in [%d, %d]",
+              E, 256 * E);
+  const int g = ln_grid(M, C, dtype);
   hipStream_t st = S(s);
   NBP_DISPATCH_T(dtype, {
-    const T* a = (const T*)dn;
-    const T* yh = (const T*)yhat;
-    const T* r = (const T*)dres;
-    T* o = (T*)dx;
-    switch (pick_G(C)) {
-      case 64: ln_bwd_nhwc<64, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
-      case 32: ln_bwd_nhwc<32, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
-      case 16: ln_bwd_nhwc<16, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
-      case 8: ln_bwd_nhwc<8, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
-      case 4: ln_bwd_nhwc<4, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
-      default: ln_bwd_nhwc<2, T><<<g, 256, 0, st>>>(a, yh, den, w, r, o, slab_w, slab_b, M, C); break;
-    }
+    NBP_LN_DISPATCH(ln_bwd_nhwc, (const T*)dn, (const T*)x, reinterpret_cast<const float2*>(stats), w, (const T*)dres,
+                    (T*)dx, slab_w, slab_b, M);
   });
   return check_launch("ln_bwd_nhwc");
 }

@@ -19,6 +19,7 @@ tensors the backward needs in a tape.
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -88,6 +89,11 @@ class NAFNet(nn.Module):
         self._init_reference_like()
         self.grad_ready_hook: Optional[Callable[[Stage], None]] = None
         self._keep: Optional[List[torch.Tensor]] = None  # slabs awaiting a deferred gradient reduction
+        # weight gradients on a side stream (joined at each stage flush), NBP_OVERLAP_WGRAD=1.  Off by default:
+        # measured slower on MI355X at cfg2 (803.8 -> 759.6 img/s graph, 808.9 -> 791.8 eager; scripts/ab_overlap.sh)
+        self.overlap_wgrad = os.environ.get("NBP_OVERLAP_WGRAD", "0") == "1"
+        self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
+        self._side_used: Optional[torch.cuda.Stream] = None
         # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
         # (the reference's AMP training, image_restoration_model.py:255), fp32 storage and statistics.
         self.precision = "fp32"
@@ -332,9 +338,9 @@ class NAFNet(nn.Module):
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
-        yh1, n1, den1 = E(M, c), E(M, c), F(M)
-        call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), yh1, n1,
-             den1, M, c, LN_EPS, dt)
+        n1, st1 = E(M, c), F(M, 2)
+        call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), n1, st1, M, c,
+             LN_EPS, dt)
         t1 = E(M, 2 * c)
         self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv1.bias"))
@@ -348,9 +354,9 @@ class NAFNet(nn.Module):
         y = E(M, c)
         self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
                  bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
-        yh2, n2, den2 = E(M, c), E(M, c), F(M)
-        call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), yh2, n2,
-             den2, M, c, LN_EPS, dt)
+        n2, st2 = E(M, c), F(M, 2)
+        call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, M, c,
+             LN_EPS, dt)
         t4 = E(M, 2 * c)
         self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv4.bias"))
@@ -360,8 +366,8 @@ class NAFNet(nn.Module):
         self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
                  bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
         if tape is not None:
-            tape.append(("block", pre, (B, h, w, c), dict(x=x, yh1=yh1, n1=n1, den1=den1, t1=t1, t2=t2, g=g, mean=mean,
-                                                           a=a, yh2=yh2, n2=n2, den2=den2, t4=t4, g2=g2)))
+            tape.append(("block", pre, (B, h, w, c), dict(x=x, n1=n1, st1=st1, t1=t1, t2=t2, g=g, mean=mean, a=a, y=y,
+                                                           n2=n2, st2=st2, t4=t4, g2=g2)))
         return out.view(B, h, w, c)
 
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
@@ -394,6 +400,9 @@ class NAFNet(nn.Module):
         try:
             return self._walk_backward(tape, dout, dflat, need_dx, P, hook)
         finally:
+            if self._side_used:
+                torch.cuda.current_stream().wait_stream(self._side_used)
+                self._side_used = None
             call("grad_reduce_flush", 1)
             self._keep = None
 
@@ -458,8 +467,19 @@ class NAFNet(nn.Module):
             call("add", dx_img, dout, dx_img, dx_img.numel(), 0)
         return dx_img
 
+    def _side(self, dev) -> torch.cuda.Stream:
+        """The wgrad side stream of this device (created lazily)."""
+        st = self._side_streams.get(dev)
+        if st is None:
+            st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
+        return st
+
     def _stage_done(self, name, hook):
-        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice
+        # join the wgrad side stream, then the stage's queued gradient reductions run before anyone (the DP
+        # all-reduce hook) reads its slice
+        if self._side_used:
+            torch.cuda.current_stream().wait_stream(self._side_used)
+            self._side_used = None
         call("grad_reduce_flush", 0)
         self._keep.clear()
         if hook is not None:
@@ -474,10 +494,22 @@ class NAFNet(nn.Module):
         return t
 
     def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db):
+        """Weight gradient.  Off the backward's critical path (its output only feeds the stage's deferred
+        reductions), so with overlap_wgrad it runs on a side stream forked from the current one; the inputs stay
+        referenced until the stage flush, which joins the side stream first."""
         n_ws = query("wgrad_workspace_floats", M, N, K)
         ws = self._ws(n_ws, G.device)
-        call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws, n_ws,
-             self.dt)
+        if not (self.overlap_wgrad and self._keep is not None):
+            call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
+                 n_ws, self.dt)
+            return
+        side = self._side(G.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
+                 n_ws, self.dt)
+        self._keep.extend(t for t in (G, X, xscale) if t is not None)
+        self._side_used = side
 
     def _reduce(self, slab, S, L, out):
         call("reduce_slab", slab, S, L, out)
@@ -511,10 +543,11 @@ class NAFNet(nn.Module):
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
         # norm2 + residual
-        lg = query("ln_nhwc_grid", M, c)
+        lg = query("ln_nhwc_grid", M, c, dt)
         sw, sb = F(lg * c), F(lg * c)
         dy = E(M, c)
-        call("ln_bwd_nhwc", dn2, S["yh2"], S["den2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb, M, c, dt)
+        call("ln_bwd_nhwc", dn2, S["y"].reshape(M, c), S["st2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb,
+             M, c, dt)
         self._reduce(sw, lg, c, self._slice(dflat, pre + "norm2.weight"))
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
         # y = x + beta * conv3(h), h = g (.) a: same layer-scale identity as conv5 (dh = (beta (.) dy) W3)
@@ -552,7 +585,8 @@ class NAFNet(nn.Module):
         # norm1 + residual
         dx = E(M, c)
         sw, sb = F(lg * c), F(lg * c)
-        call("ln_bwd_nhwc", dn1, S["yh1"], S["den1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb, M, c, dt)
+        call("ln_bwd_nhwc", dn1, S["x"].reshape(M, c), S["st1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb,
+             M, c, dt)
         self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
         self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))
         return dx.view(B, h, w, c)
