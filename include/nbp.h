@@ -91,7 +91,10 @@ int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int
                  const float* bias, const float* R, const float* rscale, float* pre, nbp_stream_t s);
 /* bf16-operand MFMA variant (perf mode; AMP-equivalent operands, fp32 accumulate): C = A . Bw^T, Bw bf16 [N][ldb];
  * a_dtype / c_dtype: 0 fp32, 1 bf16 storage of A and of C/R/pre.  Same a_mode/c_mode/epilogue as nbp_gemm_f32;
- * dgrads pass the transposed weight copy.  K, ldb multiples of 8; S2D/D2S need cs % 8 == 0. */
+ * dgrads pass the transposed weight copy.  K, ldb multiples of 8; S2D/D2S need cs % 8 == 0.  Extra c_modes fusing
+ * SimpleGate (NAFNet_arch.py:22-25,75-76) on interleaved channel pairs: 4 = forward (C = t, pre <- g[M][N/2] with
+ * g[c] = t[2c] * t[2c+1]), 5 = backward (acc = dg[M][N]; R = t [M][2N] interleaved; C[2c] = dg[c] * t[2c+1],
+ * C[2c+1] = dg[c] * t[2c], row stride ldc). */
 int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, int a_dtype,
                   const void* Bw, long ldb, void* C, long ldc, int c_mode, int c_dtype, int M, int N, int K, int gh,
                   int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s);
@@ -148,9 +151,10 @@ int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const flo
                 int HW, int C, nbp_stream_t s);
 /* per-image channel sums slab[b][chunk][c] = sum_p x*y (y may be NULL). */
 int nbp_img_chan_dot(const void* x, const void* y, float* slab, int B, int H, int W, int C, int dtype, nbp_stream_t s);
-/* SCA backward: da, ds = W^T da, dW = da^T mean, db = sum_b da. */
-int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float* mean, float* da, float* ds, float* dwsca,
-                float* dbsca, int B, int C, nbp_stream_t s);
+/* SCA backward: da[B][C] = the reduced img_chan_dot slab, ds = da . W (the pooled-vector gradient).  The weight
+   gradients dW = da^T mean, db = sum_b da are a K = B weight-gradient GEMM (nbp_wgrad_f32 on da and mean). */
+int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, float* da, float* ds, int B, int C,
+                nbp_stream_t s);
 /* dg = dh*a + ds/HW, then SimpleGate backward into dt2 [M][2C]. */
 int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* t2, void* dt2, long M, int C, int HW,
                    int dtype, nbp_stream_t s);
@@ -166,8 +170,9 @@ int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const voi
                       nbp_stream_t s);
 
 /* SimpleGate on the FFN half (NAFNet_arch.py:75): g = t[:C]*t[C:], and its backward. */
-int nbp_sg_fwd(const void* t, void* g, long M, int C, int dtype, nbp_stream_t s);
-int nbp_sg_bwd(const void* dg, const void* t, void* dt, long M, int C, int dtype, nbp_stream_t s);
+/* layout 0: t = [t_a | t_b] halves; layout 1: pairs (a_c, b_c) interleaved (the internal conv4 channel order). */
+int nbp_sg_fwd(const void* t, void* g, long M, int C, int layout, int dtype, nbp_stream_t s);
+int nbp_sg_bwd(const void* dg, const void* t, void* dt, long M, int C, int layout, int dtype, nbp_stream_t s);
 /* layer-scale residual gradients (NAFNet_arch.py:72,80): ds = d*scale, slab partials of sum d*t (dbeta/dgamma). */
 int nbp_scale_dot_grid(long M, int C);
 int nbp_scale_dot(const void* d, const void* t, const float* scale, void* ds, float* slab, long M, int C, int dtype,

@@ -74,19 +74,54 @@ __global__ void dw_sg_pool_fwd(const T* __restrict__ t1, const float* __restrict
   }
 }
 
-// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
-// One wave per output o; W row read once for all images (SCA_NB images per pass, means staged in LDS).
+// out[b][c] = scale * sum_{k < chunks} slab[b][k][c]: 8 lanes per element, lane j sums chunks k = j (mod 8) with
+// independent loads, then a fixed-order xor combine (deterministic).  Feeds the SCA GEMVs with finished vectors.
+__global__ __launch_bounds__(256) void reduce_rows8(const float* __restrict__ slab, int B, int chunks, int C,
+                                                    float scale, float* __restrict__ out) {
+  const int e = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
+  float acc = 0.f;
+  if (e < B * C) {
+    const int b = e / C, c = e - b * C;
+    const float* src = slab + (long)b * chunks * C + c;
+    float a0 = 0.f, a1 = 0.f;
+    int k = j;
+    for (; k + 8 < chunks; k += 16) {
+      a0 += src[(long)k * C];
+      a1 += src[(long)(k + 8) * C];
+    }
+    if (k < chunks) a0 += src[(long)k * C];
+    acc = a0 + a1;
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (j == 0 && e < B * C) out[e] = acc * scale;
+}
+
+// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i] (mean from reduce_rows8).
+// 16 waves per block, one output o per wave; the means of SCA_NB images are staged in LDS (a few loads per thread),
+// the W row read once for all of them.
 constexpr int SCA_NB = 16;
-__global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ mean, const float* __restrict__ wsca,
-                                                const float* __restrict__ bsca, float* __restrict__ a_out, int B,
-                                                int C) {
+__global__ __launch_bounds__(1024) void sca_gemv(const float* __restrict__ mean, const float* __restrict__ wsca,
+                                                 const float* __restrict__ bsca, float* __restrict__ a_out, int B,
+                                                 int C) {
   extern __shared__ float sm[];  // [SCA_NB][C]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int o = blockIdx.x * 4 + wv;
+  const int o = blockIdx.x * 16 + wv;
   for (int b0 = 0; b0 < B; b0 += SCA_NB) {
     const int nb = min(SCA_NB, B - b0);
     __syncthreads();
-    for (int e = threadIdx.x; e < nb * C; e += blockDim.x) sm[e] = mean[(long)b0 * C + e];
+    for (int e0 = threadIdx.x; e0 < nb * C; e0 += 4 * blockDim.x) {
+      float m[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * blockDim.x;
+        m[u] = e < nb * C ? mean[(long)b0 * C + e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (e0 + u * blockDim.x < nb * C) sm[e0 + u * blockDim.x] = m[u];
+    }
     __syncthreads();
     if (o < C) {
       float acc[SCA_NB];
@@ -107,19 +142,20 @@ __global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ mean, 
   }
 }
 
-// per-image channel reduction: slab[b][chunk][c] = sum_{p in chunk} x[p][c] * (y ? y[p][c] : 1)
+// per-image channel reduction: slab[b][chunk][c] = sum_{p in chunk} x[p][c] * (y ? y[p][c] : 1).
+// grid (chunks, B, channel groups of CG = min(C, 64) channels): each block a pixel chunk x channel group.
 template <typename T>
 __global__ void img_chan_dot(const T* __restrict__ x, const T* __restrict__ y, float* __restrict__ slab, Geo geo) {
   extern __shared__ float red[];
-  const int C = geo.C, Q = C / 4;
+  const int C = geo.C, CG = C < 64 ? C : 64, Q = CG / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
-  const int b = blockIdx.y, chunk = blockIdx.x;
+  const int b = blockIdx.y, chunk = blockIdx.x, c0 = blockIdx.z * CG;
   const int HW = geo.H * geo.W;
   const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
   float4 acc = f4(0.f);
   if (pl < PPI) {
     for (int p = p0 + pl; p < p1; p += PPI) {
-      const long o = ((long)b * HW + p) * C + q * 4;
+      const long o = ((long)b * HW + p) * C + c0 + q * 4;
       float4 v = ldq(x + o);
       if (y) v = v * ldq(y + o);
       acc += v;
@@ -130,13 +166,12 @@ __global__ void img_chan_dot(const T* __restrict__ x, const T* __restrict__ y, f
   if (pl == 0) {
     float4 s = f4(0.f);
     for (int k = 0; k < PPI; ++k) s += ld4(red + (k * Q + q) * 4);
-    st4(slab + ((long)b * geo.chunks + chunk) * C + q * 4, s);
+    st4(slab + ((long)b * geo.chunks + chunk) * C + c0 + q * 4, s);
   }
 }
 
-// SCA backward: ds[b][i] = sum_o W[o][i] da[b][o]  (da already reduced over chunks).
-// Block = 64 columns x SCA_BW waves splitting the o range (4 loads in flight per lane); W read once for SCA_NB
-// images; fixed-order cross-wave sum.
+// SCA backward: ds[b][i] = sum_o W[o][i] da[b][o] (da reduced by reduce_rows8, staged in LDS).  Block = 64 columns
+// x SCA_BW waves splitting the o range (4 W loads in flight per lane); fixed-order cross-wave sum.
 constexpr int SCA_BW = 16;
 __global__ __launch_bounds__(1024) void sca_bwd_ds(const float* __restrict__ da, const float* __restrict__ wsca,
                                                    float* __restrict__ ds_out, int B, int C) {
@@ -146,7 +181,17 @@ __global__ __launch_bounds__(1024) void sca_bwd_ds(const float* __restrict__ da,
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   const int b0 = blockIdx.y * SCA_NB, nb = min(SCA_NB, B - b0);
-  for (int e = threadIdx.x; e < SCA_NB * C; e += blockDim.x) sda[e] = e < nb * C ? da[(long)b0 * C + e] : 0.f;
+  for (int e0 = threadIdx.x; e0 < SCA_NB * C; e0 += 4 * blockDim.x) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * blockDim.x;
+      v[u] = e < nb * C ? da[(long)b0 * C + e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + u * blockDim.x < SCA_NB * C) sda[e0 + u * blockDim.x] = v[u];
+  }
   __syncthreads();
   float acc[SCA_NB];
 #pragma unroll
@@ -179,23 +224,6 @@ __global__ __launch_bounds__(1024) void sca_bwd_ds(const float* __restrict__ da,
 #pragma unroll
       for (int w = 0; w < SCA_BW; ++w) v += part[(w * SCA_NB + b) * 64 + l];
       ds_out[(long)(b0 + b) * C + ii] = v;
-    }
-  }
-}
-
-// dW[o][i] = sum_b da[b][o] * mean[b][i] ; db[o] = sum_b da[b][o]
-__global__ void sca_bwd_b(const float* __restrict__ da, const float* __restrict__ mean, int B, int C,
-                          float* __restrict__ dw, float* __restrict__ db) {
-  const long total = (long)C * C;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int o = e / C, i = e % C;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc = fmaf(da[(long)b * C + o], mean[(long)b * C + i], acc);
-    dw[e] = acc;
-    if (i == 0) {
-      float s = 0.f;
-      for (int b = 0; b < B; ++b) s += da[(long)b * C + o];
-      db[o] = s;
     }
   }
 }
@@ -602,6 +630,14 @@ int block_for_quads(int Q) {
   return 256;
 }
 
+// per-image pixel-chunk budget for the per-image channel reductions (pool, img_chan_dot): chunks of >= 128 pixels,
+// at most 64 per image — their consumers re-reduce the partial slab in every block, so it must stay small.
+long img_cap(int B, int H, int W) {
+  long c = (long)H * W / 128;
+  c = c < 1 ? 1 : (c > 64 ? 64 : c);
+  return (long)B * c;
+}
+
 Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
   Geo g{B, H, W, C, 1, H * W};
   const int HW = H * W;
@@ -656,7 +692,7 @@ int nbp_dw_chunks(int B, int H, int W, int C, int which) {
   // which 0: forward/pool (quads = C/4), 1: dw backward (quads = 2C/4)
   const int Q = which == 0 ? C / 4 : C / 2;
   const int blk = block_for_quads(Q);
-  long cap = which == 0 ? 2048 : (4L << 20) / (2L * C * 10) ;
+  long cap = which == 0 ? img_cap(B, H, W) : (4L << 20) / (2L * C * 10);
   if (cap > 2048) cap = 2048;
   return make_geo(B, H, W, C, Q, blk, cap).chunks;
 }
@@ -685,7 +721,7 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
     return check_launch("dw_sg_pool_tiled");
   }
   const int Q = C / 4, blk = block_for_quads(Q);
-  Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
+  Geo geo = make_geo(B, H, W, C, Q, blk, img_cap(B, H, W));
   dim3 grid(geo.chunks, B);
   NBP_DISPATCH_T(dtype, dw_sg_pool_fwd<T><<<grid, blk, blk * 4 * sizeof(float), S(s)>>>((const T*)t1, wdw, bdw, (T*)t2,
                                                                                        (T*)g, pool_slab, geo));
@@ -695,32 +731,30 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s) {
   NBP_REQUIRE(pool_slab && wsca && bsca && mean && a && B > 0 && C > 0 && chunks > 0, "nbp_sca_fwd: bad args");
-  int rc = nbp_reduce_slab_batched(pool_slab, B, chunks, C, 1.f / (float)HW, mean, s);
-  if (rc) return rc;
   NBP_REQUIRE(C <= 1024, "nbp_sca_fwd: C <= 1024");
-  sca_gemv<<<cdiv(C, 4), 256, (size_t)SCA_NB * C * sizeof(float), S(s)>>>(mean, wsca, bsca, a, B, C);
+  reduce_rows8<<<cdiv((long)B * C, 32), 256, 0, S(s)>>>(pool_slab, B, chunks, C, 1.f / (float)HW, mean);
+  sca_gemv<<<cdiv(C, 16), 1024, (size_t)SCA_NB * C * sizeof(float), S(s)>>>(mean, wsca, bsca, a, B, C);
   return check_launch("sca_fwd");
 }
 
 int nbp_img_chan_dot(const void* x, const void* y, float* slab, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && slab && B > 0 && C % 4 == 0 && C / 4 <= 1024, "nbp_img_chan_dot: bad args");
+  NBP_REQUIRE(C <= 64 || C % 64 == 0, "nbp_img_chan_dot: C must be <= 64 or a multiple of 64");
   const int Q = C / 4, blk = block_for_quads(Q);
-  Geo geo = make_geo(B, H, W, C, Q, blk, 2048);
-  NBP_DISPATCH_T(dtype, img_chan_dot<T><<<dim3(geo.chunks, B), blk, blk * 4 * sizeof(float), S(s)>>>(
+  Geo geo = make_geo(B, H, W, C, Q, blk, img_cap(B, H, W));  // chunk geometry shared with nbp_dw_chunks(.., 0)
+  const int groups = C <= 64 ? 1 : C / 64;
+  NBP_DISPATCH_T(dtype, img_chan_dot<T><<<dim3(geo.chunks, B, groups), 256, 256 * 4 * sizeof(float), S(s)>>>(
                             (const T*)x, (const T*)y, slab, geo));
   return check_launch("img_chan_dot");
 }
 
-int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, const float* mean, float* da, float* ds, float* dwsca,
-                float* dbsca, int B, int C, nbp_stream_t s) {
-  NBP_REQUIRE(da_slab && wsca && mean && da && ds && dwsca && dbsca && B > 0 && C > 0, "nbp_sca_bwd: bad args");
-  int rc = nbp_reduce_slab_batched(da_slab, B, chunks, C, 1.f, da, s);
-  if (rc) return rc;
+int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, float* da, float* ds, int B, int C,
+                nbp_stream_t s) {
+  NBP_REQUIRE(da_slab && wsca && da && ds && B > 0 && C > 0, "nbp_sca_bwd: bad args");
   NBP_REQUIRE(C <= 1024, "nbp_sca_bwd: C <= 1024");
+  reduce_rows8<<<cdiv((long)B * C, 32), 256, 0, S(s)>>>(da_slab, B, chunks, C, 1.f, da);
   sca_bwd_ds<<<dim3(cdiv(C, 64), cdiv(B, SCA_NB)), 64 * SCA_BW,
                ((size_t)SCA_NB * C + SCA_BW * SCA_NB * 64) * sizeof(float), S(s)>>>(da, wsca, ds, B, C);
-  const long tot = (long)C * C;
-  sca_bwd_b<<<cdiv(tot, 256) > 2048 ? 2048 : cdiv(tot, 256), 256, 0, S(s)>>>(da, mean, B, C, dwsca, dbsca);
   return check_launch("sca_bwd");
 }
 

@@ -7,28 +7,42 @@ using namespace nbp;
 
 namespace {
 
+// layout 0: t = [first half | second half] (g = t[:C] * t[C:]); layout 1: channel pairs interleaved
+// (g[c] = t[2c] * t[2c+1]) — the order of the fused-epilogue path (conv4's rows stored interleaved)
 template <typename T>
-__global__ void sg_fwd(const T* __restrict__ t, T* __restrict__ g, long M, int C) {
+__global__ void sg_fwd(const T* __restrict__ t, T* __restrict__ g, long M, int C, int layout) {
   const int Q = C / 4;
   const long total = M * Q;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long m = e / Q;
     const int q = e % Q;
-    stq(g + m * C + q * 4, ldq(t + m * 2 * C + q * 4) * ldq(t + m * 2 * C + C + q * 4));
+    if (layout == 0) {
+      stq(g + m * C + q * 4, ldq(t + m * 2 * C + q * 4) * ldq(t + m * 2 * C + C + q * 4));
+    } else {
+      const float4 a = ldq(t + m * 2 * C + q * 8), b = ldq(t + m * 2 * C + q * 8 + 4);
+      stq(g + m * C + q * 4, make_float4(a.x * a.y, a.z * a.w, b.x * b.y, b.z * b.w));
+    }
   }
 }
 
 template <typename T>
-__global__ void sg_bwd(const T* __restrict__ dg, const T* __restrict__ t, T* __restrict__ dt, long M, int C) {
+__global__ void sg_bwd(const T* __restrict__ dg, const T* __restrict__ t, T* __restrict__ dt, long M, int C,
+                       int layout) {
   const int Q = C / 4;
   const long total = M * Q;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const long m = e / Q;
     const int q = e % Q;
     const float4 d = ldq(dg + m * C + q * 4);
-    const float4 a = ldq(t + m * 2 * C + q * 4), b = ldq(t + m * 2 * C + C + q * 4);
-    stq(dt + m * 2 * C + q * 4, d * b);
-    stq(dt + m * 2 * C + C + q * 4, d * a);
+    if (layout == 0) {
+      const float4 a = ldq(t + m * 2 * C + q * 4), b = ldq(t + m * 2 * C + C + q * 4);
+      stq(dt + m * 2 * C + q * 4, d * b);
+      stq(dt + m * 2 * C + C + q * 4, d * a);
+    } else {
+      const float4 a = ldq(t + m * 2 * C + q * 8), b = ldq(t + m * 2 * C + q * 8 + 4);
+      stq(dt + m * 2 * C + q * 8, make_float4(d.x * a.y, d.x * a.x, d.y * a.w, d.y * a.z));
+      stq(dt + m * 2 * C + q * 8 + 4, make_float4(d.z * b.y, d.z * b.x, d.w * b.w, d.w * b.z));
+    }
   }
 }
 
@@ -111,15 +125,16 @@ inline int g_elem(long total) {
 
 extern "C" {
 
-int nbp_sg_fwd(const void* t, void* g, long M, int C, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(t && g && M > 0 && C % 4 == 0, "nbp_sg_fwd: bad args");
-  NBP_DISPATCH_T(dtype, sg_fwd<T><<<g_elem(M * (C / 4)), 256, 0, S(s)>>>((const T*)t, (T*)g, M, C));
+int nbp_sg_fwd(const void* t, void* g, long M, int C, int layout, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(t && g && M > 0 && C % 4 == 0 && (layout == 0 || layout == 1), "nbp_sg_fwd: bad args");
+  NBP_DISPATCH_T(dtype, sg_fwd<T><<<g_elem(M * (C / 4)), 256, 0, S(s)>>>((const T*)t, (T*)g, M, C, layout));
   return check_launch("sg_fwd");
 }
 
-int nbp_sg_bwd(const void* dg, const void* t, void* dt, long M, int C, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(dg && t && dt && M > 0 && C % 4 == 0, "nbp_sg_bwd: bad args");
-  NBP_DISPATCH_T(dtype, sg_bwd<T><<<g_elem(M * (C / 4)), 256, 0, S(s)>>>((const T*)dg, (const T*)t, (T*)dt, M, C));
+int nbp_sg_bwd(const void* dg, const void* t, void* dt, long M, int C, int layout, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dg && t && dt && M > 0 && C % 4 == 0 && (layout == 0 || layout == 1), "nbp_sg_bwd: bad args");
+  NBP_DISPATCH_T(dtype, sg_bwd<T><<<g_elem(M * (C / 4)), 256, 0, S(s)>>>((const T*)dg, (const T*)t, (T*)dt, M, C,
+                                                                         layout));
   return check_launch("sg_bwd");
 }
 

@@ -17,9 +17,11 @@ namespace {
 
 // A modes: plain rows, space-to-depth gather, per-(image, column) scale, and 3x3 neighbourhood gather (implicit GEMM
 // of a zero-padded 3x3 conv over an NHWC map: row m = pixel, k = tap * Cin + c with gh = H, gw = W, cs = Cin).
-// C modes: plain, depth-to-space scatter, bias + ReLU, and ReLU-mask by R (C = acc where R > 0, else 0).
+// C modes: plain, depth-to-space scatter, bias + ReLU, ReLU-mask by R (C = acc where R > 0, else 0), SimpleGate
+// forward (C = t with channel pairs (c, C+c) interleaved, and pre <- g = t[2c] * t[2c+1]) and SimpleGate backward
+// (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
-enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3 };
+enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5 };
 
 struct GemmPB {
   const void* A;
@@ -277,6 +279,31 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
     float v[8];
     const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
     v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
+    if (CMODE == CM_SGBWD) {
+      // 8 gate channels -> 16 interleaved (t, dt) values
+      const long off = (long)grow * p.ldc + 2 * gcol;
+      if (vec) {
+        float ta[8], tb[8], oa[8], ob[8];
+        ld8f<TC>(p.R, off, ta);
+        ld8f<TC>(p.R, off + 8, tb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          oa[2 * j] = v[j] * ta[2 * j + 1];
+          oa[2 * j + 1] = v[j] * ta[2 * j];
+          ob[2 * j] = v[4 + j] * tb[2 * j + 1];
+          ob[2 * j + 1] = v[4 + j] * tb[2 * j];
+        }
+        st8f<TC>(p.C, off, oa);
+        st8f<TC>(p.C, off + 8, ob);
+      } else {
+        for (int j = 0; j < 8 && gcol + j < N; ++j) {
+          const float t0 = ldf<TC>(p.R, off + 2 * j), t1 = ldf<TC>(p.R, off + 2 * j + 1);
+          stf<TC>(p.C, off + 2 * j, v[j] * t1);
+          stf<TC>(p.C, off + 2 * j + 1, v[j] * t0);
+        }
+      }
+      continue;
+    }
     if (vec) {
       const long off = CMODE == CM_D2S ? s2d_off(grow, gcol, p.gh, p.gw, p.cs) : (long)grow * p.ldc + gcol;
       if (p.bias) {
@@ -292,7 +319,21 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = rv[j] > 0.f ? v[j] : 0.f;
       }
-      if (p.pre) st8f<TC>(p.pre, off, v);
+      if (CMODE == CM_SG) {
+        float g[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = v[2 * j] * v[2 * j + 1];
+        // 4 gate values (8 bytes of bf16 / 16 of fp32) at row grow, column gcol / 2 of the [M][N/2] map
+        if constexpr (sizeof(TC) == 4) {
+          st4(reinterpret_cast<float*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2, make_float4(g[0], g[1], g[2], g[3]));
+        } else {
+          bf16x4 o;
+          o[0] = (__bf16)g[0]; o[1] = (__bf16)g[1]; o[2] = (__bf16)g[2]; o[3] = (__bf16)g[3];
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2) = o;
+        }
+      } else if (p.pre) {
+        st8f<TC>(p.pre, off, v);
+      }
       if (CMODE != CM_MASK && p.R) {
         float rv[8];
         ld8f<TC>(p.R, off, rv);
@@ -314,7 +355,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         float x = v[j] + (p.bias ? p.bias[col] : 0.f);
         if (CMODE == CM_RELU) x = fmaxf(x, 0.f);
         if (CMODE == CM_MASK) x = ldf<TC>(p.R, off) > 0.f ? x : 0.f;
-        if (p.pre) stf<TC>(p.pre, off, x);
+        if (CMODE == CM_SG) {
+          v[j] = x;
+          if (j & 1) stf<TC>(p.pre, (long)grow * (p.ldc / 2) + col / 2, v[j - 1] * x);
+        } else if (p.pre) {
+          stf<TC>(p.pre, off, x);
+        }
         if (CMODE != CM_MASK && p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
         stf<TC>(p.C, off, x);
       }
@@ -375,6 +421,9 @@ int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {
   else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch<AM_SCALE, CM_PLAIN, TA, TC>(p, st);
   else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch<AM_S2D, CM_PLAIN, TA, TC>(p, st);
   else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch<AM_PLAIN, CM_D2S, TA, TC>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_SG) dispatch<AM_PLAIN, CM_SG, TA, TC>(p, st);
+  else if (a_mode == AM_SCALE && c_mode == CM_SGBWD) dispatch<AM_SCALE, CM_SGBWD, TA, TC>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_SGBWD) dispatch<AM_PLAIN, CM_SGBWD, TA, TC>(p, st);
   else {
     set_error("nbp_gemm_bf16: unsupported mode combination");
     return NBP_ERR_ARG;
@@ -391,7 +440,12 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
                   int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s) {
   NBP_REQUIRE(A && Bw && C && M > 0 && N > 0 && K > 0, "nbp_gemm_bf16: null pointer or empty shape");
   NBP_REQUIRE(K % 8 == 0 && N % 4 == 0 && ldb % 8 == 0, "nbp_gemm_bf16: K, ldb multiples of 8, N of 4 (K=%d N=%d)", K, N);
-  NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && c_mode >= 0 && c_mode <= 1, "nbp_gemm_bf16: mode");
+  NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && (c_mode == CM_PLAIN || c_mode == CM_D2S || c_mode == CM_SG ||
+              c_mode == CM_SGBWD), "nbp_gemm_bf16: mode");
+  NBP_REQUIRE(c_mode != CM_SG || (pre && N % 2 == 0 && ldc % 2 == 0 && !R),
+              "nbp_gemm_bf16: SimpleGate epilogue needs pre (the gate map), even N and ldc, no residual");
+  NBP_REQUIRE(c_mode != CM_SGBWD || (R && !bias && !pre && ldc >= 2L * N),
+              "nbp_gemm_bf16: SimpleGate-backward epilogue needs R (the interleaved gate input) and ldc >= 2N");
   NBP_REQUIRE((a_dtype == 0 || a_dtype == 1) && (c_dtype == 0 || c_dtype == 1), "nbp_gemm_bf16: dtype");
   NBP_REQUIRE(a_mode != AM_SCALE || (a_scale && rows_per_img > 0), "nbp_gemm_bf16: a_scale");
   NBP_REQUIRE((a_mode != AM_S2D && c_mode != CM_D2S) || (gh > 0 && gw > 0 && cs > 0 && cs % 8 == 0),

@@ -31,6 +31,7 @@ from . import _lib
 from ._lib import call, query
 
 AM_PLAIN, AM_S2D, AM_SCALE = 0, 1, 2
+CM_SG, CM_SGBWD = 4, 5  # SimpleGate forward / backward fused into the GEMM epilogue (bf16 mode)
 CM_PLAIN, CM_D2S = 0, 1
 LN_EPS = 1e-6
 
@@ -41,7 +42,7 @@ class PEntry:
     ref_shape: Tuple[int, ...]
     offset: int
     numel: int
-    kind: str = "plain"  # plain | down | up
+    kind: str = "plain"  # plain | down | up | sg (conv4: SimpleGate pairs interleaved)
 
 
 @dataclass
@@ -159,7 +160,7 @@ class NAFNet(nn.Module):
                 for s in shp:
                     n *= s
                 kind = "down" if k.startswith("downs.") and k.endswith("weight") else (
-                    "up" if k.startswith("ups.") else "plain")
+                    "up" if k.startswith("ups.") else ("sg" if ".conv4." in k else "plain"))
                 self.entries[k] = PEntry(k, shp, off, n, kind)
                 off += n if k == "ending.bias" else _ceil_to(n, 4)  # 16-byte aligned slices for float4 access
             self.stages[gname] = Stage(gname, lo, off)
@@ -205,12 +206,18 @@ class NAFNet(nn.Module):
     def _to_internal(self, e: PEntry, t: torch.Tensor) -> torch.Tensor:
         if e.kind == "down":  # [2C, C, 2, 2] -> [2C, 2, 2, C]
             return t.permute(0, 2, 3, 1).reshape(-1)
+        if e.kind == "sg":  # conv4 output rows h*C + c -> 2c + h: SimpleGate pairs adjacent (fused epilogues)
+            n2 = t.shape[0]
+            return t.reshape(2, n2 // 2, -1).permute(1, 0, 2).reshape(-1)
         if e.kind == "up":  # row n_ref = c'*4 + r1*2 + r2 -> n_int = (r1*2 + r2)*(C/2) + c'
             n2, c = t.shape[0], t.shape[1]
             return t.reshape(n2 // 4, 4, c).permute(1, 0, 2).reshape(-1)
         return t.reshape(-1)
 
     def _to_reference(self, e: PEntry, flat_slice: torch.Tensor) -> torch.Tensor:
+        if e.kind == "sg":
+            n2 = e.ref_shape[0]
+            return flat_slice.view(n2 // 2, 2, -1).permute(1, 0, 2).reshape(e.ref_shape).contiguous()
         if e.kind == "down":
             o, c = e.ref_shape[0], e.ref_shape[1]
             return flat_slice.view(o, 2, 2, c).permute(0, 3, 1, 2).contiguous()
@@ -357,11 +364,14 @@ class NAFNet(nn.Module):
         n2, st2 = E(M, c), F(M, 2)
         call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, M, c,
              LN_EPS, dt)
-        t4 = E(M, 2 * c)
-        self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c, c,
-                 bias=self._slice(P, pre + "conv4.bias"))
-        g2 = E(M, c)
-        call("sg_fwd", t4, g2, M, c, dt)
+        t4, g2 = E(M, 2 * c), E(M, c)  # t4 channel pairs interleaved (conv4 rows stored so)
+        if dt == 1:  # SimpleGate in the GEMM epilogue
+            self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
+                     bias=self._slice(P, pre + "conv4.bias"), pre=g2)
+        else:
+            self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c, c,
+                     bias=self._slice(P, pre + "conv4.bias"))
+            call("sg_fwd", t4, g2, M, c, 1, dt)
         out = E(M, c)
         self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
                  bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
@@ -493,7 +503,7 @@ class NAFNet(nn.Module):
             self._keep.append(t)
         return t
 
-    def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db):
+    def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, dtype=None):
         """Weight gradient.  Off the backward's critical path (its output only feeds the stage's deferred
         reductions), so with overlap_wgrad it runs on a side stream forked from the current one; the inputs stay
         referenced until the stage flush, which joins the side stream first."""
@@ -501,13 +511,13 @@ class NAFNet(nn.Module):
         ws = self._ws(n_ws, G.device)
         if not (self.overlap_wgrad and self._keep is not None):
             call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
-                 n_ws, self.dt)
+                 n_ws, self.dt if dtype is None else dtype)
             return
         side = self._side(G.device)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
-                 n_ws, self.dt)
+                 n_ws, self.dt if dtype is None else dtype)
         self._keep.extend(t for t in (G, X, xscale) if t is not None)
         self._side_used = side
 
@@ -526,17 +536,20 @@ class NAFNet(nn.Module):
         # out = y + gamma * conv5(g2): no stored pre-activation, no scaled-gradient pass.  dg2 = (gamma (.) dout) W5
         # (gamma as the A-operand column scale); U5 = dout^T g2, V5 = colsum dout feed dW5 = gamma (.) U5,
         # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
-        dg2 = E(M, c)
-        self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dg2, c, CM_PLAIN, M,
-                 c, c, dgrad=True)
+        dt4 = E(M, 2 * c)
+        if dt == 1:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises
+            self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dt4, 2 * c,
+                     CM_SGBWD, M, c, c, R=S["t4"], dgrad=True)
+        else:
+            dg2 = E(M, c)
+            self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dg2, c, CM_PLAIN,
+                     M, c, c, dgrad=True)
+            call("sg_bwd", dg2, S["t4"], dt4, M, c, 1, dt)
         U5, V5 = F(c * c), F(c)
         self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
         call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
              self._slice(P, pre + "gamma"), self._slice(dflat, pre + "conv5.weight"),
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
-        # SimpleGate (FFN)
-        dt4 = E(M, 2 * c)
-        call("sg_bwd", dg2, S["t4"], dt4, M, c, dt)
         # conv4
         dn2 = E(M, c)
         self._mm(Wt, dt4, 2 * c, AM_PLAIN, None, 1, pre + "conv4.weight", dn2, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
@@ -564,8 +577,10 @@ class NAFNet(nn.Module):
         da_slab = F(B * chunks * c)
         call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
         da, ds = F(B, c), F(B, c)
-        call("sca_bwd", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], da, ds,
-             self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
+        call("sca_bwd", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), da, ds, B, c)
+        # dW_sca = da^T mean, db_sca = colsum(da): an fp32 weight-gradient GEMM with K = B rows
+        self._wgrad(da, c, AM_PLAIN, S["mean"], c, AM_PLAIN, None, 1, B, c, c, 0, 0, 0, 0,
+                    self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), dtype=0)
         # SimpleGate + depthwise conv2 (fused when the channel slicing allows: dt2 stays in LDS)
         dt1 = E(M, 2 * c)
         ws = F(query("dw_bwd_workspace_floats", B, h, w, c))

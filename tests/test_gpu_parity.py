@@ -469,3 +469,33 @@ def test_graph_step_bitwise_equals_eager(dev, precision):
         assert torch.equal(net_a.flat, net_b.flat), f"params differ at step {i}"
         assert torch.equal(trs[0].exp_avg_sq, trs[1].exp_avg_sq)
         assert trs[0].logs() == trs[1].logs()
+
+
+@pytest.mark.parametrize("M,C", [(1000, 32), (4096, 64), (300, 24)])
+def test_gemm_bf16_simplegate_epilogues(dev, M, C):
+    """c_mode 4: t = A W^T + b stored with (c, C+c) pairs interleaved and g[c] = t[2c] t[2c+1];
+    c_mode 5: acc = dg (A W^T with the column scale), dt[2c] = dg[c] t[2c+1], dt[2c+1] = dg[c] t[2c]."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M + C)
+    K = C
+    A = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+    W = (torch.randn(2 * C, K, device=dev, generator=gen) * 0.2).to(torch.bfloat16)
+    b = torch.randn(2 * C, device=dev, generator=gen)
+    t = torch.empty(M, 2 * C, device=dev, dtype=torch.bfloat16)
+    g = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    call("gemm_bf16", A, K, 0, None, 1, 1, W, K, t, 2 * C, 4, 1, M, 2 * C, K, 0, 0, 0, b, None, None, g)
+    tr = A.double() @ W.double().t() + b.double()
+    close(t.float(), tr.cpu().numpy(), atol=3e-2, rtol=1e-2)
+    gr = t.double()[:, 0::2] * t.double()[:, 1::2]
+    close(g.float(), gr.cpu().numpy(), atol=5e-2, rtol=2e-2)
+    # backward: dg = (gamma (.) D) Wd^T with Wd [C][C] (the dgrad operand), then the interleaved SimpleGate adjoint
+    D = torch.randn(M, C, device=dev, generator=gen).to(torch.bfloat16)
+    Wd = (torch.randn(C, C, device=dev, generator=gen) * 0.2).to(torch.bfloat16)
+    gamma = torch.randn(C, device=dev, generator=gen)
+    dt = torch.empty(M, 2 * C, device=dev, dtype=torch.bfloat16)
+    call("gemm_bf16", D, C, 2, gamma, M, 1, Wd, C, dt, 2 * C, 5, 1, M, C, C, 0, 0, 0, None, t, None, None)
+    dg = (D.float() * gamma).to(torch.bfloat16).double() @ Wd.double().t()
+    ref = torch.empty(M, 2 * C, dtype=torch.float64, device=dev)
+    ref[:, 0::2] = dg * t.double()[:, 1::2]
+    ref[:, 1::2] = dg * t.double()[:, 0::2]
+    close(dt.float(), ref.cpu().numpy(), atol=5e-2, rtol=2e-2)
