@@ -6,6 +6,7 @@
 // + residual for the up conv).  Weights come from a per-step bf16 copy of the flat parameter buffer; dgrads use
 // the transposed copy so every launch is NT.
 #include <hip/hip_bf16.h>
+#include <stdlib.h>
 
 #include "nbp_common.h"
 
@@ -368,6 +369,194 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
   }
 }
 
+// ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
+// The transposed product C^T = W . A^T on 32x32x16 MFMA: the weight is the A-operand (kept in registers for the whole
+// launch: N, K <= 64), the pixel rows are the B-operand, loaded straight from global memory in fragment order (lane l
+// reads 16 bytes of row l & 31 — no LDS, no barriers).  Each wave streams 32-pixel tiles, prefetching the next tile's
+// fragments while the current one is multiplied; a lane ends up owning one pixel's channels (4 consecutive per
+// register group), so the epilogue (bias, layer-scale residual, SimpleGate forward / backward) runs in registers and
+// stores 8 / 16-byte pieces that complete whole rows in L2.
+struct SkinnyP {
+  const __bf16* A;
+  long lda;
+  const float* a_scale;
+  int rows_per_img;
+  const __bf16* W;
+  long ldw;
+  __bf16* C;
+  long ldc;
+  int M, N, K;
+  const float* bias;
+  const __bf16* R;
+  const float* rscale;
+  __bf16* aux;
+};
+
+template <int NT, int KS, int AMODE, int CMODE>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
+  constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
+  __shared__ float stage[4][32 * LDT];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  float* tileS = stage[threadIdx.x >> 6];
+  const int M = p.M, N = p.N, K = p.K;
+  bf16x8 w[NT][KS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int n = t * 32 + r, k = ks * 16 + 8 * h;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      if (n < N && k < K) v = *reinterpret_cast<const bf16x8*>(p.W + (long)n * p.ldw + k);
+      w[t][ks] = v;
+    }
+  // coalesced epilogue geometry: chunks of 8 output elements, row-major over the 32-row tile.  The output row holds
+  // N elements (2N for the SimpleGate backward), so a lane's chunk column is fixed across its chunks.
+  const int outw = (CMODE == CM_SGBWD ? 2 : 1) * N;
+  const int cpr = outw / 8;                                    // chunks per row (divides 64: outw in {8..128})
+  const int ccol = (lane % cpr) * 8;                           // this lane's output column
+  const int rstep = 64 / cpr;                                  // rows advanced per pass
+  float bia[8], rsc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bia[j] = 0.f; rsc[j] = 1.f; }
+  if (CMODE != CM_SGBWD) {
+    if (p.bias) {
+      const float4 b0 = ld4(p.bias + ccol), b1 = ld4(p.bias + ccol + 4);
+      bia[0] = b0.x; bia[1] = b0.y; bia[2] = b0.z; bia[3] = b0.w; bia[4] = b1.x; bia[5] = b1.y; bia[6] = b1.z; bia[7] = b1.w;
+    }
+    if (p.rscale) {
+      const float4 s0 = ld4(p.rscale + ccol), s1 = ld4(p.rscale + ccol + 4);
+      rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
+    }
+  }
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (long)gridDim.x * 4;
+  const long ntiles = (M + 31) / 32;
+  auto load_a = [&](long tile, bf16x8* a) {
+    const long m = tile * 32 + r;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = ks * 16 + 8 * h;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      if (m < M && k < K) {
+        v = *reinterpret_cast<const bf16x8*>(p.A + m * p.lda + k);
+        if (AMODE == AM_SCALE) {
+          const float* sc = p.a_scale + (m / p.rows_per_img) * K + k;
+          const float4 s0 = ld4(sc), s1 = ld4(sc + 4);
+          const float f[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)v[j] * f[j]);
+        }
+      }
+      a[ks] = v;
+    }
+  };
+  bf16x8 a0[KS], a1[KS];
+  long tile = wave;
+  if (tile < ntiles) load_a(tile, a0);
+  for (; tile < ntiles; tile += nwaves) {
+    if (tile + nwaves < ntiles) load_a(tile + nwaves, a1);
+    floatx16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[t][ks], a0[ks], acc[t], 0, 0, 0);
+    // lane (r, h) owns pixel r, channels t*32 + 8g + 4h + {0..3}: stage as rows of the tile
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(tileS + r * LDT + t * 32 + 8 * g + 4 * h) =
+            make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+    __builtin_amdgcn_wave_barrier();
+    const long m0 = tile * 32;
+    for (int rr = lane / cpr; rr < 32; rr += rstep) {
+      const long m = m0 + rr;
+      if (m >= M) break;
+      if (CMODE == CM_SGBWD) {  // chunk = 4 gates (interleaved pairs): dg from the tile, t from R
+        const float4 dg = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol / 2);
+        const long off = m * p.ldc + ccol;
+        const bf16x8 tv = *reinterpret_cast<const bf16x8*>(p.R + off);
+        const float d[4] = {dg.x, dg.y, dg.z, dg.w};
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[2 * j] = (__bf16)(d[j] * (float)tv[2 * j + 1]);
+          o[2 * j + 1] = (__bf16)(d[j] * (float)tv[2 * j]);
+        }
+        *reinterpret_cast<bf16x8*>(p.C + off) = o;
+        continue;
+      }
+      const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
+      const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
+      float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += bia[j];
+      const long off = m * p.ldc + ccol;
+      if (CMODE == CM_PLAIN && p.R) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.R + off);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (float)rv[j] + rsc[j] * v[j];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
+      *reinterpret_cast<bf16x8*>(p.C + off) = o;
+      if (CMODE == CM_SG) {  // g[c] = t[2c] * t[2c+1]: 4 gates of this chunk
+        bf16x4 gv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gv[j] = (__bf16)(v[2 * j] * v[2 * j + 1]);
+        *reinterpret_cast<bf16x4*>(p.aux + m * (p.ldc / 2) + ccol / 2) = gv;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) a0[ks] = a1[ks];
+  }
+}
+
+template <int AMODE, int CMODE>
+void launch_skinny(const SkinnyP& p, hipStream_t st) {
+  const long ntiles = (p.M + 31) / 32;
+  long blocks = (ntiles + 3) / 4;
+  if (blocks > 1024) blocks = 1024;  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs
+  const dim3 g((unsigned)blocks);
+  const int nt = (p.N + 31) / 32, ks = (p.K + 15) / 16;
+#define NBP_SKINNY(NT_, KS_) gemm_skinny_kernel<NT_, KS_, AMODE, CMODE><<<g, 256, 0, st>>>(p)
+  if (nt == 1) {
+    if (ks == 1) NBP_SKINNY(1, 1); else if (ks == 2) NBP_SKINNY(1, 2); else if (ks == 3) NBP_SKINNY(1, 3); else NBP_SKINNY(1, 4);
+  } else {
+    if (ks == 1) NBP_SKINNY(2, 1); else if (ks == 2) NBP_SKINNY(2, 2); else if (ks == 3) NBP_SKINNY(2, 3); else NBP_SKINNY(2, 4);
+  }
+#undef NBP_SKINNY
+}
+
+// whether the skinny path serves this call (bf16 in / out, N and K <= 64, supported modes, aligned rows)
+bool try_skinny(const void* A, long lda, int a_mode, const float* a_scale, int rows, const void* Bw, long ldb, void* C,
+                long ldc, int c_mode, int M, int N, int K, const float* bias, const void* R, const float* rscale,
+                void* pre, hipStream_t st) {
+  if (N > 64 || K > 64 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc % 8) return false;
+  const bool ok = (a_mode == AM_PLAIN && c_mode == CM_PLAIN && !pre) || (a_mode == AM_SCALE && c_mode == CM_PLAIN && !pre) ||
+                  (a_mode == AM_PLAIN && c_mode == CM_SG) || (a_mode == AM_SCALE && c_mode == CM_SGBWD) ||
+                  (a_mode == AM_PLAIN && c_mode == CM_SGBWD);
+  if (!ok) return false;
+  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, a_scale, rows, reinterpret_cast<const __bf16*>(Bw), ldb,
+            reinterpret_cast<__bf16*>(C), ldc, M, N, K, bias, reinterpret_cast<const __bf16*>(R), rscale,
+            reinterpret_cast<__bf16*>(pre)};
+  if (c_mode == CM_SG) launch_skinny<AM_PLAIN, CM_SG>(p, st);
+  else if (c_mode == CM_SGBWD && a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_SGBWD>(p, st);
+  else if (c_mode == CM_SGBWD) launch_skinny<AM_PLAIN, CM_SGBWD>(p, st);
+  else if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_PLAIN>(p, st);
+  else launch_skinny<AM_PLAIN, CM_PLAIN>(p, st);
+  return true;
+}
+
 // fp32 flat parameters -> bf16 copy (all), plus transposed bf16 copies of the listed [rows][cols] matrices
 __global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, __bf16* __restrict__ dst) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -415,6 +604,15 @@ void dispatch(const GemmPB& p, hipStream_t st) {
   else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
 }
 
+// NBP_SKINNY=0 disables the skinny path (A/B measurement)
+bool getenv_skinny() {
+  static const bool on = [] {
+    const char* v = getenv("NBP_SKINNY");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 template <typename TA, typename TC>
 int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {
   if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch<AM_PLAIN, CM_PLAIN, TA, TC>(p, st);
@@ -456,6 +654,9 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   GemmPB p{A, lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb, C, ldc, M, N, K, gh, gw, cs,
            bias, R, rscale, pre};
   hipStream_t st = S(s);
+  if (a_dtype == 1 && c_dtype == 1 && getenv_skinny() &&
+      try_skinny(A, lda, a_mode, a_scale, rows_per_img, Bw, ldb, C, ldc, c_mode, M, N, K, bias, R, rscale, pre, st))
+    return check_launch("gemm_bf16(skinny)");
   int rc;
   if (a_dtype == 0 && c_dtype == 0) rc = dispatch_modes<float, float>(p, a_mode, c_mode, st);
   else if (a_dtype == 1 && c_dtype == 1) rc = dispatch_modes<__bf16, __bf16>(p, a_mode, c_mode, st);

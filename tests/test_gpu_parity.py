@@ -499,3 +499,30 @@ def test_gemm_bf16_simplegate_epilogues(dev, M, C):
     ref[:, 0::2] = dg * t.double()[:, 1::2]
     ref[:, 1::2] = dg * t.double()[:, 0::2]
     close(dt.float(), ref.cpu().numpy(), atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 32, 32), (4097, 64, 64), (333, 48, 24), (300001, 64, 32), (5000, 32, 64),
+                                   (77, 8, 8), (2048, 64, 16)])
+def test_gemm_bf16_skinny_path(dev, M, N, K):
+    """bf16 in / out with N, K <= 64 runs the register-resident skinny kernel (weights in registers, pixel rows as
+    the MFMA B-operand, persistent 32-row tiles): plain, bias + layer-scale residual, per-image A scale."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=gen) * 0.3).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev, generator=gen)
+    R = torch.randn(M, N, device=dev, generator=gen).to(torch.bfloat16)
+    sc = torch.randn(N, device=dev, generator=gen)
+    rows = 97
+    ascale = torch.rand(M // rows + 1, K, device=dev, generator=gen)
+    tol = dict(atol=2e-2 * max(1.0, K ** 0.5 / 4), rtol=1e-2)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    call("gemm_bf16", A, K, 0, None, 1, 1, W, K, out, N, 0, 1, M, N, K, 0, 0, 0, None, None, None, None)
+    close(out.float(), (A.double() @ W.double().t()).cpu().numpy(), **tol)
+    call("gemm_bf16", A, K, 0, None, 1, 1, W, K, out, N, 0, 1, M, N, K, 0, 0, 0, bias, R, sc, None)
+    ref = R.double() + sc.double() * (A.double() @ W.double().t() + bias.double())
+    close(out.float(), ref.cpu().numpy(), **tol)
+    call("gemm_bf16", A, K, 2, ascale, rows, 1, W, K, out, N, 0, 1, M, N, K, 0, 0, 0, bias, R, None, None)
+    Aeff = (A.float() * ascale.repeat_interleave(rows, 0)[:M]).to(torch.bfloat16)
+    ref = R.double() + (Aeff.double() @ W.double().t() + bias.double())
+    close(out.float(), ref.cpu().numpy(), **tol)
