@@ -3,6 +3,8 @@
 //           reads the NCHW image, writes NHWC features on the padded grid.
 //   ending: 3x3 pad 1, width -> img_channel on the padded grid, + global residual, cropped to the input size;
 //           reads NHWC features, writes the NCHW image.
+#include <algorithm>
+
 #include "nbp_common.h"
 
 using namespace nbp;
@@ -50,54 +52,6 @@ __global__ __launch_bounds__(256) void intro_fwd(const float* __restrict__ img, 
       }
       stq(op + o, make_float4(r[0], r[1], r[2], r[3]));
     }
-  }
-}
-
-// intro weight gradient: slab_w[blk][Cf][CI*9], slab_b[blk][Cf]
-template <int CI, typename T>
-__global__ __launch_bounds__(256) void intro_bwd_w(const float* __restrict__ img, const T* __restrict__ dout, float* __restrict__ slab_w,
-                            float* __restrict__ slab_b, Img g, long px_per_blk) {
-  extern __shared__ float red[];  // [blockDim][4]
-  constexpr int K = CI * 9;
-  const int Q = g.Cf / 4;
-  const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
-  float4 acc[K + 1];
-#pragma unroll
-  for (int k = 0; k <= K; ++k) acc[k] = f4(0.f);
-  const long total = (long)g.B * g.Hp * g.Wp;
-  const long p0 = blockIdx.x * px_per_blk, p1 = min(total, p0 + px_per_blk);
-  if (pl < PPI) {
-    for (long p = p0 + pl; p < p1; p += PPI) {
-      const int x = p % g.Wp, y = (p / g.Wp) % g.Hp, b = p / ((long)g.Wp * g.Hp);
-      const float4 d = ldq(dout + p * g.Cf + q * 4);
-      acc[K] += d;
-#pragma unroll
-      for (int c = 0; c < CI; ++c)
-#pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-          const float v = (yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
-                              ? img[(((long)b * CI + c) * g.H0 + yy) * g.W0 + xx] : 0.f;
-          acc[c * 9 + t] = fma4(d, f4(v), acc[c * 9 + t]);
-        }
-    }
-  }
-  float* dw = slab_w + (long)blockIdx.x * g.Cf * K;
-  float* db = slab_b + (long)blockIdx.x * g.Cf;
-#pragma unroll
-  for (int kk = 0; kk <= K; ++kk) {
-    st4(red + tid * 4, acc[kk]);
-    __syncthreads();
-    if (pl == 0) {
-      float4 s4 = f4(0.f);
-      for (int i = 0; i < PPI; ++i) s4 += ld4(red + (i * Q + q) * 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (kk < K) dw[(long)(q * 4 + j) * K + kk] = get(s4, j);
-        else db[q * 4 + j] = get(s4, j);
-      }
-    }
-    __syncthreads();
   }
 }
 
@@ -183,71 +137,263 @@ __global__ void ending_bwd_x(const float* __restrict__ dy, const float* __restri
   }
 }
 
-// ending weight gradient: slab_w[blk][CI][Cf][9], slab_b[blk][CI]
-template <int CI, typename T>
-__global__ __launch_bounds__(256) void ending_bwd_w(const float* __restrict__ dy, const T* __restrict__ feat, float* __restrict__ slab_w,
-                             float* __restrict__ slab_b, Img g, long px_per_blk) {
-  extern __shared__ float red[];  // [blockDim][4]
-  const int Q = g.Cf / 4;
-  const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
-  float4 acc[CI][9];
-  float bacc[CI];
+
+// ------------------------------------------------------------------ thread-per-pixel kernels, width templated
+// One workgroup per feature row; each lane owns one pixel and all of its channels.  The weights are wave-uniform
+// (indices are compile-time after unrolling), so they are read through the scalar cache into SGPRs: no LDS, no
+// broadcast reads, one FMA per weight use.  Rows are decoded once per workgroup (32-bit), not per pixel.
+template <typename T, int CF>
+__device__ __forceinline__ void store_row(T* __restrict__ op, const float (&a)[CF]) {
+  if constexpr (sizeof(T) == 2) {
 #pragma unroll
-  for (int o = 0; o < CI; ++o) {
-    bacc[o] = 0.f;
+    for (int c = 0; c < CF; c += 8) {
+      bf16x8 v;
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc[o][t] = f4(0.f);
-  }
-  const long total = (long)g.B * g.H0 * g.W0;
-  const long p0 = blockIdx.x * px_per_blk, p1 = min(total, p0 + px_per_blk);
-  if (pl < PPI) {
-    for (long p = p0 + pl; p < p1; p += PPI) {
-      const int x = p % g.W0, y = (p / g.W0) % g.H0, b = p / ((long)g.W0 * g.H0);
-      float d[CI];
-#pragma unroll
-      for (int o = 0; o < CI; ++o) {
-        d[o] = dy[(((long)b * CI + o) * g.H0 + y) * g.W0 + x];
-        bacc[o] += d[o];
-      }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) continue;
-        const float4 v = ldq(feat + (((long)b * g.Hp + yy) * g.Wp + xx) * g.Cf + q * 4);
-#pragma unroll
-        for (int o = 0; o < CI; ++o) acc[o][t] = fma4(v, f4(d[o]), acc[o][t]);
-      }
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)a[c + j];
+      *reinterpret_cast<bf16x8*>(op + c) = v;
     }
-  }
-  float* dw = slab_w + (long)blockIdx.x * CI * g.Cf * 9;
+  } else {
 #pragma unroll
-  for (int o = 0; o < CI; ++o) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      st4(red + tid * 4, acc[o][t]);
-      __syncthreads();
-      if (pl == 0) {
-        float4 s4 = f4(0.f);
-        for (int i = 0; i < PPI; ++i) s4 += ld4(red + (i * Q + q) * 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dw[((long)o * g.Cf + q * 4 + j) * 9 + t] = get(s4, j);
-      }
-      __syncthreads();
-    }
-  }
-  // bias: lanes with q == 0 hold the pixel-lane sums of every output channel
-#pragma unroll
-  for (int o = 0; o < CI; ++o) {
-    red[tid] = (q == 0 && pl < PPI) ? bacc[o] : 0.f;
-    __syncthreads();
-    if (tid == 0) {
-      float s1 = 0.f;
-      for (int i = 0; i < PPI; ++i) s1 += red[i * Q];
-      slab_b[(long)blockIdx.x * CI + o] = s1;
-    }
-    __syncthreads();
+    for (int c = 0; c < CF; c += 4) st4(reinterpret_cast<float*>(op) + c, make_float4(a[c], a[c + 1], a[c + 2], a[c + 3]));
   }
 }
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* __restrict__ p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
+  } else {
+    const float4 a = ld4(reinterpret_cast<const float*>(p)), b = ld4(reinterpret_cast<const float*>(p) + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+// intro forward on MFMA: out[px][o] = sum_k patch[px][k] W[o][k] with k = c*9 + t, plus k = 9*CI -> 1 x bias[o].
+// v_mfma_f32_32x32x2f32 (fp32 in / out, exact fp32 products): a wave computes 32 pixels x 32 channels per tile in
+// (9*CI + 1)/2 rounded-up MFMAs; lane l supplies patch(px = l%32, k = 2s + l/32) (gathered image taps) and keeps
+// W[o = l%32][k = 2s + l/32] in VGPRs.  Tiles go through LDS to leave as 16-byte row vectors.
+template <int CI, typename T>
+__global__ __launch_bounds__(256) void intro_fwd_mfma(const float* __restrict__ img, const float* __restrict__ w,
+                                                      const float* __restrict__ bias, T* __restrict__ out, Img g) {
+  constexpr int K = CI * 9, NS = (K + 2) / 2;
+  __shared__ float tile[4][32][33];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, li = lane & 31;
+  const int row = blockIdx.x, y = row % g.Hp, b = row / g.Hp;
+  const int ntiles = (g.Wp + 31) >> 5;
+  int tc[NS], tdy[NS], tdx[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int k = 2 * s + half;
+    tc[s] = k / 9;
+    tdy[s] = (k % 9) / 3 - 1;
+    tdx[s] = (k % 9) % 3 - 1;
+  }
+  for (int oc = 0; oc < g.Cf; oc += 32) {
+    const int o = oc + li;
+    float wb[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int k = 2 * s + half;
+      wb[s] = o < g.Cf ? (k < K ? w[(long)o * K + k] : (k == K ? bias[o] : 0.f)) : 0.f;
+    }
+    const int cw = min(32, g.Cf - oc);  // channels of this chunk
+    for (int tix = wave; tix < ntiles; tix += 4) {
+      const int x = tix * 32 + li;
+      float pa[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const int k = 2 * s + half;
+        const int yy = y + tdy[s], xx = x + tdx[s];
+        if (k < K) {
+          pa[s] = (x < g.Wp && yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
+                      ? img[(((long)b * CI + tc[s]) * g.H0 + yy) * g.W0 + xx] : 0.f;
+        } else {
+          pa[s] = k == K ? 1.f : 0.f;
+        }
+      }
+      floatx16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], wb[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tile[wave][8 * (r >> 2) + 4 * half + (r & 3)][li] = acc[r];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int c8 = cw >> 3;  // 8-channel chunks per pixel in this tile
+      for (int e = lane; e < 32 * c8; e += 64) {
+        const int px = e / c8, ch = (e % c8) * 8, xo = tix * 32 + px;
+        if (xo >= g.Wp) continue;
+        T* op = out + ((long)row * g.Wp + xo) * g.Cf + oc + ch;
+        const float* tp = &tile[wave][px][ch];
+        if constexpr (sizeof(T) == 2) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (__bf16)tp[j];
+          *reinterpret_cast<bf16x8*>(op) = v;
+        } else {
+          st4(reinterpret_cast<float*>(op), make_float4(tp[0], tp[1], tp[2], tp[3]));
+          st4(reinterpret_cast<float*>(op) + 4, make_float4(tp[4], tp[5], tp[6], tp[7]));
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
+// ending forward on the crop: out[b][o][y][x] = (sum_t sum_c w[o][c][t] feat(y+dy, x+dx)[c] + bias[o]) + img
+template <int CI, int CF, typename T>
+__global__ __launch_bounds__(256) void ending_fwd_px(const T* __restrict__ feat, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, const float* __restrict__ img,
+                                                     float* __restrict__ out, Img g) {
+  const int row = blockIdx.x, y = row % g.H0, b = row / g.H0;
+  for (int x = threadIdx.x; x < g.W0; x += blockDim.x) {
+    float acc[CI];
+#pragma unroll
+    for (int o = 0; o < CI; ++o) acc[o] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) continue;
+      const T* fp = feat + (((long)b * g.Hp + yy) * g.Wp + xx) * CF;
+#pragma unroll
+      for (int c = 0; c < CF; c += 8) {
+        float v[8];
+        load8(fp + c, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int o = 0; o < CI; ++o) acc[o] = fmaf(w[(o * CF + c + j) * 9 + t], v[j], acc[o]);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < CI; ++o) {
+      const long oi = (((long)b * CI + o) * g.H0 + y) * g.W0 + x;
+      out[oi] = (acc[o] + bias[o]) + img[oi];
+    }
+  }
+}
+
+// ending input gradient on the padded grid (dy is zero off the crop)
+template <int CI, int CF, typename T>
+__global__ __launch_bounds__(256) void ending_bwd_x_px(const float* __restrict__ dy, const float* __restrict__ w,
+                                                       T* __restrict__ dfeat, Img g) {
+  const int row = blockIdx.x, y = row % g.Hp, b = row / g.Hp;
+  for (int x = threadIdx.x; x < g.Wp; x += blockDim.x) {
+    float acc[CF];
+#pragma unroll
+    for (int c = 0; c < CF; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yo = y - (t / 3 - 1), xo = x - (t % 3 - 1);
+      if (yo < 0 || yo >= g.H0 || xo < 0 || xo >= g.W0) continue;
+#pragma unroll
+      for (int o = 0; o < CI; ++o) {
+        const float d = dy[(((long)b * CI + o) * g.H0 + yo) * g.W0 + xo];
+#pragma unroll
+        for (int c = 0; c < CF; ++c) acc[c] = fmaf(w[(o * CF + c) * 9 + t], d, acc[c]);
+      }
+    }
+    store_row<T, CF>(dfeat + ((long)row * g.Wp + x) * CF, acc);
+  }
+}
+
+// ------------------------------------------------------------------ boundary-conv weight gradients on MFMA
+// D[m][n] = sum_px A(m, px) B(px, n) with v_mfma_f32_32x32x2f32: one MFMA per pixel pair (lane l supplies
+// A(m = l%32, px = 2i + l/32) and B(px = 2i + l/32, n = l%32)), fp32 operands and accumulation.
+//   MODE 0 (intro):  m = output channel o, A = dout[px][o]; n = c*9 + t -> image tap, n == 9*CI -> 1 (bias column)
+//   MODE 1 (ending): m = feature channel c, A = feat[px][c]; n = o*9 + t -> dy[o] at px - tap offset (0 off-crop);
+//                    db[o] = sum of the centre-tap column (n = o*9 + 4), accumulated beside the MFMA
+// Grid (blocks over feature rows, M chunks of 32, N chunks of 32); block x writes slab x (fixed-order reductions).
+template <int MODE, int CI, typename T>
+__global__ __launch_bounds__(256) void bconv_wgrad(const float* __restrict__ src, const T* __restrict__ nhwc,
+                                                   float* __restrict__ slab_w, float* __restrict__ slab_b, Img g) {
+  __shared__ float red[4][32][33];
+  __shared__ float bred[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int m = blockIdx.y * 32 + (lane & 31), n = blockIdx.z * 32 + (lane & 31);
+  constexpr int NK = 9 * CI;
+  const int nc = n / 9, nt = n % 9, ndy = nt / 3 - 1, ndx = nt % 3 - 1;
+  const bool mval = m < g.Cf;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bacc = 0.f;
+  const int rows = g.B * g.Hp, pairs = (g.Wp + 1) >> 1;
+  // U pixel pairs per step: all 2U operand loads are issued before the MFMAs that consume them (latency hiding)
+  constexpr int U = 8;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int y = row % g.Hp, b = row / g.Hp;
+    const T* arow = nhwc + (long)row * g.Wp * g.Cf;
+    for (int i0 = wave; i0 < pairs; i0 += 4 * U) {
+      float av[U], bv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int x = 2 * (i0 + 4 * u) + half;
+        const bool xval = x < g.Wp;
+        av[u] = (mval && xval) ? (float)arow[(long)x * g.Cf + m] : 0.f;
+        bv[u] = 0.f;
+        if (MODE == 0) {
+          const int yy = y + ndy, xx = x + ndx;
+          if (n < NK) {
+            if (xval && yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
+              bv[u] = src[(((long)b * CI + nc) * g.H0 + yy) * g.W0 + xx];
+          } else if (n == NK) {
+            bv[u] = xval ? 1.f : 0.f;
+          }
+        } else {
+          const int yo = y - ndy, xo = x - ndx;
+          if (n < NK && xval && yo >= 0 && yo < g.H0 && xo >= 0 && xo < g.W0)
+            bv[u] = src[(((long)b * CI + nc) * g.H0 + yo) * g.W0 + xo];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (MODE == 1 && nt == 4) bacc += bv[u];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][8 * (r >> 2) + 4 * half + (r & 3)][lane & 31] = acc[r];
+  if (MODE == 1) bred[wave][lane] = bacc;
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+    const int mi = e >> 5, ni = e & 31;
+    const int mm = blockIdx.y * 32 + mi, nn = blockIdx.z * 32 + ni;
+    const float v = ((red[0][mi][ni] + red[1][mi][ni]) + red[2][mi][ni]) + red[3][mi][ni];
+    if (mm >= g.Cf) continue;
+    if (MODE == 0) {
+      if (nn < NK) slab_w[((long)blockIdx.x * g.Cf + mm) * NK + nn] = v;
+      else if (nn == NK) slab_b[(long)blockIdx.x * g.Cf + mm] = v;
+    } else if (nn < NK) {
+      slab_w[(long)blockIdx.x * CI * g.Cf * 9 + ((long)(nn / 9) * g.Cf + mm) * 9 + nn % 9] = v;
+    }
+  }
+  if (MODE == 1 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < CI) {
+    const int l = threadIdx.x * 9 + 4;  // lane of column o*9+4 (< 32 for CI <= 4), both half-waves
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += bred[w][l] + bred[w][l + 32];
+    slab_b[(long)blockIdx.x * CI + threadIdx.x] = s;
+  }
+}
+
+#define NBP_DISPATCH_CF(cf, ok, ...)                     \
+  switch (cf) {                                          \
+    case 8: { constexpr int CF = 8; __VA_ARGS__; } break;  \
+    case 16: { constexpr int CF = 16; __VA_ARGS__; } break; \
+    case 32: { constexpr int CF = 32; __VA_ARGS__; } break; \
+    case 64: { constexpr int CF = 64; __VA_ARGS__; } break; \
+    default: ok = false;                                 \
+  }
+
+constexpr int kWgradBlocks = 1024;
 
 #define NBP_DISPATCH_CI(ci, ...)                        \
   switch (ci) {                                          \
@@ -256,12 +402,6 @@ __global__ __launch_bounds__(256) void ending_bwd_w(const float* __restrict__ dy
     case 3: { constexpr int CI = 3; __VA_ARGS__; } break; \
     default: { constexpr int CI = 4; __VA_ARGS__; } break; \
   }
-
-int blocks_for(long total, long want_px) {
-  long g = (total + want_px - 1) / want_px;
-  if (g > 1024) g = 1024;
-  return (int)(g < 1 ? 1 : g);
-}
 
 }  // namespace
 
@@ -275,13 +415,18 @@ int nbp_intro_fwd(const float* img, const float* w, const float* bias, void* out
   const long total = (long)B * Hp * Wp;
   long grid = (total + 255) / 256;
   const int gr = (int)(grid > 4096 ? 4096 : grid);
-  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, intro_fwd<CI, T><<<gr, 256, Cf * Cimg * 9 * sizeof(float), S(s)>>>(
-                                                  img, w, bias, (T*)out, g)));
+  if (Cf % 8 == 0) {
+    NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, intro_fwd_mfma<CI, T><<<B * Hp, 256, 0, S(s)>>>(img, w, bias, (T*)out, g)));
+  } else {
+    NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, intro_fwd<CI, T><<<gr, 256, Cf * Cimg * 9 * sizeof(float), S(s)>>>(
+                                                    img, w, bias, (T*)out, g)));
+  }
   return check_launch("intro_fwd");
 }
 
 size_t nbp_intro_bwd_workspace_floats(int B, int Cimg, int Hp, int Wp, int Cf) {
-  return (size_t)blocks_for((long)B * Hp * Wp, 1024) * Cf * (Cimg * 9 + 1);
+  (void)Wp;
+  return (size_t)std::min(kWgradBlocks, B * Hp) * Cf * (Cimg * 9 + 1);
 }
 
 int nbp_intro_bwd(const float* img, const void* dout, const float* w, float* dw, float* db, float* dimg, float* ws,
@@ -289,13 +434,12 @@ int nbp_intro_bwd(const float* img, const void* dout, const float* w, float* dw,
   NBP_REQUIRE(img && dout && w && dw && db && ws && Cimg <= kMaxCin && Cf % 4 == 0 && Cf / 4 <= 256,
               "nbp_intro_bwd: bad args");
   Img g{B, Cimg, H0, W0, Hp, Wp, Cf};
-  const long total = (long)B * Hp * Wp;
-  const int nb = blocks_for(total, 1024);
-  const long ppb = (total + nb - 1) / nb;
+  const int nb = std::min(kWgradBlocks, B * Hp);
   float* slab_w = ws;
   float* slab_b = ws + (long)nb * Cf * Cimg * 9;
-  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, intro_bwd_w<CI, T><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(
-                                                  img, (const T*)dout, slab_w, slab_b, g, ppb)));
+  const dim3 grid(nb, cdiv(Cf, 32), cdiv(Cimg * 9 + 1, 32));
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, bconv_wgrad<0, CI, T><<<grid, 256, 0, S(s)>>>(
+                                                  img, (const T*)dout, slab_w, slab_b, g)));
   int rc = check_launch("intro_bwd_w");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, nb, (long)Cf * Cimg * 9, dw, s);
@@ -318,12 +462,18 @@ int nbp_ending_fwd(const void* feat, const float* w, const float* bias, const fl
   const long total = (long)B * H0 * W0;
   long grid = (total + 255) / 256;
   const int gr = (int)(grid > 4096 ? 4096 : grid);
-  NBP_DISPATCH_T(dtype, ending_fwd<T><<<gr, 256, 9 * Cf * 4 * sizeof(float), S(s)>>>((const T*)feat, w, bias, img, out, g));
+  bool px = true;
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, NBP_DISPATCH_CF(Cf, px, ending_fwd_px<CI, CF, T><<<B * H0, 256, 0, S(s)>>>(
+                                                  (const T*)feat, w, bias, img, out, g))));
+  if (!px)
+    NBP_DISPATCH_T(dtype, ending_fwd<T><<<gr, 256, 9 * Cf * 4 * sizeof(float), S(s)>>>((const T*)feat, w, bias, img,
+                                                                                          out, g));
   return check_launch("ending_fwd");
 }
 
 size_t nbp_ending_bwd_workspace_floats(int B, int Cimg, int H0, int W0, int Cf) {
-  return (size_t)blocks_for((long)B * H0 * W0, 1024) * ((size_t)Cimg * Cf * 9 + Cimg);
+  (void)W0;
+  return (size_t)std::min(kWgradBlocks, B * H0) * ((size_t)Cimg * Cf * 9 + Cimg);
 }
 
 int nbp_ending_bwd(const float* dy, const void* feat, const float* w, void* dfeat, float* dw, float* db, float* ws,
@@ -334,14 +484,17 @@ int nbp_ending_bwd(const float* dy, const void* feat, const float* w, void* dfea
   const long tx = (long)B * Hp * Wp * (Cf / 4);
   long gx = (tx + 255) / 256;
   const int gxx = (int)(gx > 4096 ? 4096 : gx);
-  NBP_DISPATCH_T(dtype, ending_bwd_x<T><<<gxx, 256, 9 * Cimg * Cf * sizeof(float), S(s)>>>(dy, w, (T*)dfeat, g));
-  const long total = (long)B * H0 * W0;
-  const int nb = blocks_for(total, 1024);
-  const long ppb = (total + nb - 1) / nb;
+  bool px = true;
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, NBP_DISPATCH_CF(Cf, px, ending_bwd_x_px<CI, CF, T><<<B * Hp, 256, 0, S(s)>>>(
+                                                  dy, w, (T*)dfeat, g))));
+  if (!px)
+    NBP_DISPATCH_T(dtype, ending_bwd_x<T><<<gxx, 256, 9 * Cimg * Cf * sizeof(float), S(s)>>>(dy, w, (T*)dfeat, g));
+  const int nb = std::min(kWgradBlocks, B * H0);
   float* slab_w = ws;
   float* slab_b = ws + (long)nb * Cimg * Cf * 9;
-  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, ending_bwd_w<CI, T><<<nb, 256, 256 * 4 * sizeof(float), S(s)>>>(
-                                                  dy, (const T*)feat, slab_w, slab_b, g, ppb)));
+  const dim3 grid(nb, cdiv(Cf, 32), cdiv(Cimg * 9, 32));
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, bconv_wgrad<1, CI, T><<<grid, 256, 0, S(s)>>>(
+                                                  dy, (const T*)feat, slab_w, slab_b, g)));
   int rc = check_launch("ending_bwd_w");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, nb, (long)Cimg * Cf * 9, dw, s);

@@ -365,6 +365,17 @@ __device__ __forceinline__ void st16f(T* p, const float* f) {
   }
 }
 
+template <typename T>
+__device__ __forceinline__ void unpack16(uint4 r, float* f) {
+  if constexpr (sizeof(T) == 4) {
+    f[0] = __uint_as_float(r.x); f[1] = __uint_as_float(r.y); f[2] = __uint_as_float(r.z); f[3] = __uint_as_float(r.w);
+  } else {
+    const bf16x8 v = __builtin_bit_cast(bf16x8, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
+  }
+}
+
 template <typename T, bool FUSED, int DWT_TW>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
@@ -382,40 +393,67 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
   const long img = (long)b * H * W;
   const int cbase = slice * HS;
-  // ---- stage t1 (and dt2 when unfused): 4 chunks per pixel = 2 halves x 2 chunks
+  // ---- stage t1 (and dt2 when unfused): 4 chunks per pixel = 2 halves x 2 chunks.  Every load of the stage is
+  // issued before the first LDS store (register batches): one memory latency per tile instead of one per pass.
   {
     const T* t1 = reinterpret_cast<const T*>(p.t1);
     const T* dt2 = reinterpret_cast<const T*>(p.dt2);
-    for (int i = tid; i < LH * LW * 4; i += NT) {
+    constexpr int TOT1 = LH * LW * 4, N1 = (TOT1 + NT - 1) / NT;
+    uint4 vx[N1], vg[FUSED ? 1 : N1];
+#pragma unroll
+    for (int it = 0; it < N1; ++it) {
+      const int i = tid + it * NT;
+      vx[it] = make_uint4(0, 0, 0, 0);
+      if (!FUSED) vg[it] = make_uint4(0, 0, 0, 0);
       const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
       const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
-      const int lo = pix * CSL + hh * HS + k * E;
-      uint4 vx = make_uint4(0, 0, 0, 0), vg = make_uint4(0, 0, 0, 0);
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+      if (i < TOT1 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
         const long go = (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E;
-        vx = *reinterpret_cast<const uint4*>(t1 + go);
-        if (!FUSED) vg = *reinterpret_cast<const uint4*>(dt2 + go);
+        vx[it] = *reinterpret_cast<const uint4*>(t1 + go);
+        if (!FUSED) vg[it] = *reinterpret_cast<const uint4*>(dt2 + go);
       }
-      *reinterpret_cast<uint4*>(sx + lo) = vx;
-      if (!FUSED) *reinterpret_cast<uint4*>(sg + lo) = vg;
     }
-  }
-  if (FUSED) {
-    const T* dh = reinterpret_cast<const T*>(p.dh);
-    const T* t2 = reinterpret_cast<const T*>(p.t2);
-    for (int i = tid; i < LH * LW * 2; i += NT) {
-      const int pix = i >> 1, k = i & 1;
-      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
-      float lo[E], hi[E];
+    constexpr int TOT2 = LH * LW * 2, N2 = FUSED ? (TOT2 + NT - 1) / NT : 1;
+    uint4 rd[N2], ra[N2], rb[N2];
+    if (FUSED) {
+      const T* dh = reinterpret_cast<const T*>(p.dh);
+      const T* t2 = reinterpret_cast<const T*>(p.t2);
 #pragma unroll
-      for (int j = 0; j < E; ++j) lo[j] = hi[j] = 0.f;
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const long m = img + (long)gy * W + gx;
+      for (int it = 0; it < N2; ++it) {
+        const int i = tid + it * NT;
+        const int pix = i >> 1, k = i & 1;
+        const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+        rd[it] = ra[it] = rb[it] = make_uint4(0, 0, 0, 0);
+        if (i < TOT2 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
+          const long m = img + (long)gy * W + gx;
+          const int c = cbase + k * E;
+          rd[it] = *reinterpret_cast<const uint4*>(dh + m * C + c);
+          ra[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + c);
+          rb[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + C + c);
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < N1; ++it) {
+      const int i = tid + it * NT;
+      if (i < TOT1) {
+        const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
+        const int lo = pix * CSL + hh * HS + k * E;
+        *reinterpret_cast<uint4*>(sx + lo) = vx[it];
+        if (!FUSED) *reinterpret_cast<uint4*>(sg + lo) = vg[it];
+      }
+    }
+    if (FUSED) {
+#pragma unroll
+      for (int it = 0; it < N2; ++it) {
+        const int i = tid + it * NT;
+        if (i >= TOT2) continue;
+        const int pix = i >> 1, k = i & 1;
         const int c = cbase + k * E;
-        float d[E], ta[E], tb[E];
-        ld16f(dh + m * C + c, d);
-        ld16f(t2 + m * C2 + c, ta);
-        ld16f(t2 + m * C2 + C + c, tb);
+        float d[E], ta[E], tb[E], lo[E], hi[E];
+        unpack16<T>(rd[it], d);
+        unpack16<T>(ra[it], ta);
+        unpack16<T>(rb[it], tb);
         const float* av = p.a + (long)b * C + c;
         const float* sv = p.ds + (long)b * C + c;
 #pragma unroll
@@ -424,9 +462,9 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
           lo[j] = dg * tb[j];
           hi[j] = dg * ta[j];
         }
+        st16f(sg + pix * CSL + k * E, lo);
+        st16f(sg + pix * CSL + HS + k * E, hi);
       }
-      st16f(sg + pix * CSL + k * E, lo);
-      st16f(sg + pix * CSL + HS + k * E, hi);
     }
   }
   __syncthreads();
@@ -539,15 +577,24 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
   const long img = (long)b * H * W;
   const int cbase = slice * HS;
-  {
+  {  // all staging loads issued before the LDS stores (one memory latency per tile)
     const T* t1 = reinterpret_cast<const T*>(p.t1);
-    for (int i = tid; i < LH * LW * 4; i += NT) {
+    constexpr int TOT = LH * LW * 4, N1 = (TOT + NT - 1) / NT;
+    uint4 v[N1];
+#pragma unroll
+    for (int it = 0; it < N1; ++it) {
+      const int i = tid + it * NT;
       const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
       const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (gy >= 0 && gy < H && gx >= 0 && gx < W)
-        v = *reinterpret_cast<const uint4*>(t1 + (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E);
-      *reinterpret_cast<uint4*>(sx + pix * CSL + hh * HS + k * E) = v;
+      v[it] = make_uint4(0, 0, 0, 0);
+      if (i < TOT && gy >= 0 && gy < H && gx >= 0 && gx < W)
+        v[it] = *reinterpret_cast<const uint4*>(t1 + (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E);
+    }
+#pragma unroll
+    for (int it = 0; it < N1; ++it) {
+      const int i = tid + it * NT;
+      const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
+      if (i < TOT) *reinterpret_cast<uint4*>(sx + pix * CSL + hh * HS + k * E) = v[it];
     }
   }
   __syncthreads();

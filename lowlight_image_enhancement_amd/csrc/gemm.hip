@@ -366,6 +366,133 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
 
+
+// bf16 weight gradient for the wide layers (N, K multiples of 128: NAFBlock 1x1 convs at C >= 128): a 128 x 128
+// output tile per workgroup, each wave a 64 x 64 quadrant (2 x 2 MFMA tiles of 32 x 32 x 16), 64-row stages
+// (16 MFMAs per wave between barrier pairs, 8x the old 64 x 64 tile's), next stage prefetched into registers.
+// Each operand tile lives in LDS as two 64-column panels with the conflict-free 96-element rows of
+// wgrad_bf16_kernel, read transposed by ds_read_b64_tr_b16.  Bias (column sums of G) from the loader's registers.
+template <int XMODE>
+__global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
+  constexpr int RM = 64, LS = 96, PAN = RM * LS;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PAN];  // G panels 0, 1; X panels 2, 3
+  const __bf16* G = reinterpret_cast<const __bf16*>(p.G);
+  const __bf16* X = reinterpret_cast<const __bf16*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * 128, k0 = blockIdx.y * 128, s = blockIdx.z;
+  const int mb = s * p.chunk;
+  const int me = min(p.M, mb + p.chunk);
+  const bool do_b = p.slab_b && blockIdx.y == 0;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float bs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bs[i] = 0.f;
+  // loader: 16-byte chunk cc of rows lrow + 16 j (j < 4) for both operands
+  const int lrow = tid >> 4, cc = tid & 15, pan = cc >> 3, lcol = (cc & 7) * 8;
+  bf16x8 rg[4], rx[4];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + lrow + 16 * j;
+      if (m < me) {
+        rg[j] = *reinterpret_cast<const bf16x8*>(G + (long)m * p.ldg + n0 + cc * 8);
+        rx[j] = *reinterpret_cast<const bf16x8*>(X + (long)m * p.ldx + k0 + cc * 8);
+        if (XMODE == AM_SCALE) {
+          const float* sc = p.x_scale + (long)(m / p.rows_per_img) * p.K + k0 + cc * 8;
+          const float4 s0 = ld4(sc), s1 = ld4(sc + 4);
+          const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rx[j][e] = (__bf16)((float)rx[j][e] * sv[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rg[j][e] = rx[j][e] = (__bf16)0.f;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      *reinterpret_cast<bf16x8*>(lds + pan * PAN + (lrow + 16 * j) * LS + lcol) = rg[j];
+      *reinterpret_cast<bf16x8*>(lds + (2 + pan) * PAN + (lrow + 16 * j) * LS + lcol) = rx[j];
+      if (do_b) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bs[e] += (float)rg[j][e];
+      }
+    }
+  };
+  const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
+  const int fcol = 16 * (grp & 1) + 4 * pp;
+  const __bf16* gpan = lds + wn * PAN;
+  const __bf16* xpan = lds + (2 + wk) * PAN;
+  if (mb < me) {
+    load(mb);
+    store();
+    __syncthreads();
+    for (int m0 = mb; m0 < me; m0 += RM) {
+      const bool more = m0 + RM < me;
+      if (more) load(m0 + RM);
+#pragma unroll
+      for (int ks = 0; ks < RM; ks += 16) {
+        bf16x8 a[2], b[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int row = ks + 8 * h + 4 * t + q;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const bf16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(gpan + row * LS + i * 32 + fcol));
+            const bf16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(xpan + row * LS + i * 32 + fcol));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              a[i][4 * t + e] = va[e];
+              b[i][4 * t + e] = vb[e];
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+      if (more) {
+        store();
+        __syncthreads();
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int k = k0 + wk * 64 + j * 32 + (lane & 31);
+        p.slab[((long)s * p.N + n) * p.K + k] = acc[i][j][r];
+      }
+  if (do_b) {  // 16 loader rows share a column chunk: fixed-order LDS combine
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[lrow * 128 + cc * 8 + e] = bs[e];
+    __syncthreads();
+    if (tid < 128) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t += red[r * 128 + tid];
+      p.slab_b[(long)s * p.N + n0 + tid] = t;
+    }
+  }
+}
+
 // out[b][i] = scale * sum_{s < S} slab[b][s][i].  TY row-lanes per column, each summing a fixed strided subset of
 // rows with 4 independent accumulators, then a fixed-order combine: bitwise reproducible, latency-tolerant.
 template <int TY>
@@ -559,9 +686,18 @@ void dispatch_tiles(const GemmP& p, hipStream_t st) {
   else launch_gemm<64, 64, B_NK, AMODE, CMODE>(p, st);
 }
 
+bool wide_wgrad(int N, int K) { return N % 128 == 0 && K % 128 == 0; }
+
 // split-M count: enough blocks to fill the chip (~2048), >= 256 rows per split, and fp32 slab bytes
 // (S * N * K * 4, written once and read once by the reduction) no larger than the operand bytes M * (N + K) * 2.
 int wgrad_splits(int M, int N, int K) {
+  if (wide_wgrad(N, K)) {  // 128 x 128 tiles: ~256 workgroups, >= 256 rows per split
+    const long tiles = (long)(N / 128) * (K / 128);
+    long s = (256 + tiles - 1) / tiles;
+    const long maxs = M / 256 > 1 ? M / 256 : 1;
+    if (s > maxs) s = maxs;
+    return (int)(s > 1024 ? 1024 : s);
+  }
   const long tiles = (long)cdiv(N, 64) * cdiv(K, 64);
   long s = (2048 + tiles - 1) / tiles;
   const long maxs = cdiv(M, 256);  // keep >= 256 rows per split
@@ -624,7 +760,7 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
   const int S_ = wgrad_splits(M, N, K);
   NBP_REQUIRE(ws_floats >= (size_t)S_ * N * K + (size_t)S_ * N, "nbp_wgrad_f32: workspace too small");
   int chunk = cdiv(M, S_);
-  chunk = cdiv(chunk, 32) * 32;
+  chunk = cdiv(chunk, 64) * 64;
   float* slab = ws;
   float* slab_b = db ? ws + (size_t)S_ * N * K : nullptr;
   WgradP p{G, ldg, X, ldx, x_scale, rows_per_img, M, N, K, gh, gw, cs_g, cs_x, slab, slab_b, chunk};
@@ -636,7 +772,11 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
                 "nbp_wgrad_f32(bf16): N, K and S2D channel counts must be multiples of 8");
     NBP_REQUIRE((g_mode == AM_S2D || ldg % 8 == 0) && (x_mode == AM_S2D || ldx % 8 == 0),
                 "nbp_wgrad_f32(bf16): leading dimensions must be multiples of 8");
-    if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
+    const bool wide = wide_wgrad(N, K) && g_mode == AM_PLAIN && x_mode != AM_S2D;
+    const dim3 wgrid(N / 128, K / 128, S_);
+    if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN><<<wgrid, 256, 0, st>>>(p);
+    else if (wide) wgrad_bf16_wide<AM_SCALE><<<wgrid, 256, 0, st>>>(p);
+    else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_bf16_kernel<AM_PLAIN, AM_SCALE><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_bf16_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);

@@ -325,7 +325,10 @@ def _s2d_rows(full):
 
 
 @pytest.mark.parametrize("M,N,K,gmode,xmode", [(4096, 64, 128, 0, 0), (1000, 40, 72, 0, 0), (70000, 128, 64, 0, 0),
-                                              (2048, 64, 64, 0, 2), (512, 128, 128, 0, 1), (512, 64, 128, 1, 0)])
+                                              (2048, 64, 64, 0, 2), (512, 128, 128, 0, 1), (512, 64, 128, 1, 0),
+                                              # wide 128 x 128-tile kernel: split rows, x_scale, ragged M
+                                              (4096, 1024, 512, 0, 0), (16384, 256, 256, 0, 2), (1000, 128, 256, 0, 0),
+                                              (65536, 256, 128, 0, 0)])
 def test_wgrad_bf16_against_float64(dev, M, N, K, gmode, xmode):
     """bf16 weight gradient (v_mfma_f32_32x32x16_bf16 on ds_read_b64_tr_b16 fragments): dW = G^T X and db = colsum G
     on bf16 storage equal float64 math on the bf16 values up to fp32 accumulation (x_scale products are rounded to
