@@ -404,13 +404,6 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
       if (m < me) {
         rg[j] = *reinterpret_cast<const bf16x8*>(G + (long)m * p.ldg + n0 + cc * 8);
         rx[j] = *reinterpret_cast<const bf16x8*>(X + (long)m * p.ldx + k0 + cc * 8);
-        if (XMODE == AM_SCALE) {
-          const float* sc = p.x_scale + (long)(m / p.rows_per_img) * p.K + k0 + cc * 8;
-          const float4 s0 = ld4(sc), s1 = ld4(sc + 4);
-          const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) rx[j][e] = (__bf16)((float)rx[j][e] * sv[e]);
-        }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) rg[j][e] = rx[j][e] = (__bf16)0.f;
@@ -432,6 +425,30 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
   const int fcol = 16 * (grp & 1) + 4 * pp;
   const __bf16* gpan = lds + wn * PAN;
   const __bf16* xpan = lds + (2 + wk) * PAN;
+  // AM_SCALE (X columns scaled per image; the launcher guarantees rows_per_img % 64 == 0, so no stage straddles two
+  // images): the MFMAs run on the unscaled X and each image's partial sum is scaled in fp32 when the rows move on.
+  constexpr int NT_ = XMODE == AM_SCALE ? 2 : 1;
+  floatx16 tot[NT_][NT_];
+#pragma unroll
+  for (int i = 0; i < NT_; ++i)
+#pragma unroll
+    for (int j = 0; j < NT_; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tot[i][j][r] = 0.f;
+  int cur_img = mb / p.rows_per_img;
+  auto fold = [&](int im) {
+#pragma unroll
+    for (int j = 0; j < NT_; ++j) {
+      const float sc = p.x_scale[(long)im * p.K + k0 + wk * 64 + j * 32 + (lane & 31)];
+#pragma unroll
+      for (int i = 0; i < NT_; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          tot[i][j][r] = fmaf(acc[i][j][r], sc, tot[i][j][r]);
+          acc[i][j][r] = 0.f;
+        }
+    }
+  };
   if (mb < me) {
     load(mb);
     store();
@@ -439,6 +456,13 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
     for (int m0 = mb; m0 < me; m0 += RM) {
       const bool more = m0 + RM < me;
       if (more) load(m0 + RM);
+      if constexpr (XMODE == AM_SCALE) {
+        const int im = m0 / p.rows_per_img;
+        if (im != cur_img) {
+          fold(cur_img);
+          cur_img = im;
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < RM; ks += 16) {
         bf16x8 a[2], b[2];
@@ -467,6 +491,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
         __syncthreads();
       }
     }
+    if constexpr (XMODE == AM_SCALE) fold(cur_img);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -476,7 +501,10 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
       for (int r = 0; r < 16; ++r) {
         const int n = n0 + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int k = k0 + wk * 64 + j * 32 + (lane & 31);
-        p.slab[((long)s * p.N + n) * p.K + k] = acc[i][j][r];
+        float v;
+        if constexpr (XMODE == AM_SCALE) v = tot[i % NT_][j % NT_][r];
+        else v = acc[i][j][r];
+        p.slab[((long)s * p.N + n) * p.K + k] = v;
       }
   if (do_b) {  // 16 loader rows share a column chunk: fixed-order LDS combine
     float* red = reinterpret_cast<float*>(lds);
@@ -772,7 +800,8 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
                 "nbp_wgrad_f32(bf16): N, K and S2D channel counts must be multiples of 8");
     NBP_REQUIRE((g_mode == AM_S2D || ldg % 8 == 0) && (x_mode == AM_S2D || ldx % 8 == 0),
                 "nbp_wgrad_f32(bf16): leading dimensions must be multiples of 8");
-    const bool wide = wide_wgrad(N, K) && g_mode == AM_PLAIN && x_mode != AM_S2D;
+    const bool wide = wide_wgrad(N, K) && g_mode == AM_PLAIN &&
+                      (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0));
     const dim3 wgrid(N / 128, K / 128, S_);
     if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN><<<wgrid, 256, 0, st>>>(p);
     else if (wide) wgrad_bf16_wide<AM_SCALE><<<wgrid, 256, 0, st>>>(p);

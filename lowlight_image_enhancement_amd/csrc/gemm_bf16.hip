@@ -594,13 +594,23 @@ void launch(const GemmPB& p, hipStream_t st) {
 
 // largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 1024 blocks (4 per CU);
 // otherwise 64x64, the most blocks available.
+// NBP_GEMM_MINBLK overrides the block-count threshold (A/B measurement)
+long gemm_minblk() {
+  static const long v = [] {
+    const char* e = getenv("NBP_GEMM_MINBLK");
+    return e ? atol(e) : 1024L;
+  }();
+  return v;
+}
+
 template <int AMODE, int CMODE, typename TA, typename TC>
 void dispatch(const GemmPB& p, hipStream_t st) {
   auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
   const bool n128 = p.N > 64, m128 = p.M > 64;
-  if (m128 && n128 && blocks(128, 128) >= 1024) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
-  else if (m128 && blocks(128, 64) >= 1024) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
-  else if (n128 && blocks(64, 128) >= 1024) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
+  const long mb = gemm_minblk();
+  if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
+  else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
+  else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
   else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
 }
 

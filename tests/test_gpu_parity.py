@@ -358,7 +358,12 @@ def test_wgrad_bf16_against_float64(dev, M, N, K, gmode, xmode):
     # mode codes of the ABI: 0 plain, 1 space-to-depth gather, 2 per-(image, column) scale
     call("wgrad_f32", Gf, ldg, gmode, Xf, ldx, xmode, xs, rows, M, N, K, gh, gw, cs_g, cs_x, dW, db,
          ws, n_ws, 1)
-    Xe = Xm.double() if xs is None else (Xm.float() * xs.repeat_interleave(rows, 0)[:M]).to(torch.bfloat16).double()
+    if xs is None:
+        Xe = Xm.double()
+    elif N % 128 == 0 and K % 128 == 0 and gmode == 0 and rows % 64 == 0:  # wide kernel: per-image fp32 scaling
+        Xe = Xm.double() * xs.repeat_interleave(rows, 0)[:M].double()
+    else:  # x_scale products rounded to bf16 before the MFMA
+        Xe = (Xm.float() * xs.repeat_interleave(rows, 0)[:M]).to(torch.bfloat16).double()
     ref = Gm.double().t() @ Xe
     close(dW, ref.cpu().numpy(), atol=3e-5 * M ** 0.5, rtol=1e-4)
     close(db, Gm.double().sum(0).cpu().numpy(), atol=3e-5 * M ** 0.5, rtol=1e-4)
