@@ -3,6 +3,7 @@
 //   as a GEMM over a space-to-depth gather), the 1x1 up conv + PixelShuffle(2) (:117-122, as a GEMM whose
 //   epilogue scatters depth-to-space and adds the skip, :148-149), and their dgrad / wgrad.
 // v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation (one rounding per fma).
+#include <cstdint>
 #include <vector>
 
 #include "nbp_common.h"
@@ -521,57 +522,55 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
   }
 }
 
-// out[b][i] = scale * sum_{s < S} slab[b][s][i].  TY row-lanes per column, each summing a fixed strided subset of
-// rows with 4 independent accumulators, then a fixed-order combine: bitwise reproducible, latency-tolerant.
-template <int TY>
-__global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, int S, long L, float scale,
-                                                          float* __restrict__ out) {
-  constexpr int TX = 256 / TY;
-  __shared__ float red[TY][TX + 1];
-  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
-  const long col = (long)blockIdx.x * TX + tx;
-  const float* base = slab + (long)blockIdx.y * S * L;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (col < L) {
-    int s = ty;
-    for (; s + 3 * TY < S; s += 4 * TY) {
-      a0 += base[(long)s * L + col];
-      a1 += base[(long)(s + TY) * L + col];
-      a2 += base[(long)(s + 2 * TY) * L + col];
-      a3 += base[(long)(s + 3 * TY) * L + col];
-    }
-    for (; s < S; s += TY) a0 += base[(long)s * L + col];
-  }
-  red[ty][tx] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (ty == 0 && col < L) {
-    float t = 0.f;
+// Column sums of a [S][L] fp32 slab.  A lane sums VEC adjacent columns (float4 loads when VEC = 4) over the rows
+// s = ty (mod TY) with 8 independent accumulators (8 loads in flight), combined in a fixed tree; the TY row-lanes of
+// a column are then combined in fixed order through LDS.  Bitwise reproducible.
+template <int VEC>
+__device__ __forceinline__ void slab_col_partial(const float* __restrict__ base, int S, long L, long col, int ty,
+                                                 int TY, float* out) {
+  typedef float vf __attribute__((ext_vector_type(VEC)));
+  vf a[8];
 #pragma unroll
-    for (int k = 0; k < TY; ++k) t += red[k][tx];
-    out[(long)blockIdx.y * L + col] = t * scale;
+  for (int u = 0; u < 8; ++u) a[u] = (vf)0.f;
+  int s = ty;
+  for (; s + 7 * TY < S; s += 8 * TY) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += *reinterpret_cast<const vf*>(base + (long)(s + u * TY) * L + col);
   }
+  for (int u = 0; s < S; s += TY, ++u) a[u & 7] += *reinterpret_cast<const vf*>(base + (long)s * L + col);
+  const vf t = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) out[v] = t[v];
 }
 
-int reduce_ty(int S, long L) { return (L < 4096 && S >= 64) ? 16 : 4; }
+// out[b][i] = scale * sum_{s < S} slab[b][s][i] (exported batched form; 4 row-lanes x 64 columns per block)
+__global__ __launch_bounds__(256) void reduce_slab_kernel(const float* __restrict__ slab, int S, long L, float scale,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long col = (long)blockIdx.x * 64 + tx;
+  float v = 0.f;
+  if (col < L) slab_col_partial<1>(slab + (long)blockIdx.y * S * L, S, L, col, ty, 4, &v);
+  red[ty][tx] = v;
+  __syncthreads();
+  if (ty == 0 && col < L) out[(long)blockIdx.y * L + col] = (((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx]) * scale;
+}
 
 void launch_reduce(const float* slab, int batch, int S, long L, float scale, float* out, hipStream_t st) {
-  if (reduce_ty(S, L) == 16) {
-    reduce_slab_kernel<16><<<dim3(cdiv(L, 16), batch), 256, 0, st>>>(slab, S, L, scale, out);
-  } else {
-    reduce_slab_kernel<4><<<dim3(cdiv(L, 64), batch), 256, 0, st>>>(slab, S, L, scale, out);
-  }
+  reduce_slab_kernel<<<dim3(cdiv(L, 64), batch), 256, 0, st>>>(slab, S, L, scale, out);
 }
 
 // ---------------------------------------------------------------- deferred gradient reductions
 // While deferral is on for a stream, gradient-slab reductions issued on it are queued and later executed by ONE
-// launch of reduce_multi_kernel (descriptors passed by value in the kernel arguments).  Each descriptor is reduced
-// with exactly the row-lane split and summation order reduce_slab_kernel would use: results are bitwise identical
-// to immediate mode.  The queue is thread-local; callers keep the slabs alive until the flush.
+// launch of reduce_multi_kernel (descriptors passed by value in the kernel arguments); with deferral off a single
+// descriptor is launched at once through the same kernel (bitwise identical results).  Per descriptor: TY row-lanes
+// (each summing <= 32 rows) x (256 / TY) lanes of VEC columns per block.  The queue is thread-local; callers keep
+// the slabs alive until the flush.
 struct RDesc {
   const float* slab;
   float* out;
   long L;
-  int S, ty, blk0, pad;
+  int S, ty, vec, blk0;
 };
 constexpr int RB_MAX = 48;
 struct RBatch {
@@ -579,33 +578,54 @@ struct RBatch {
   int n;
 };
 
+RDesc make_rdesc(const float* slab, int S, long L, float* out) {
+  int ty = 1;
+  while (ty < 64 && (long)ty * 32 < S) ty <<= 1;
+  const bool v4 = L % 4 == 0 && (reinterpret_cast<uintptr_t>(slab) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  return RDesc{slab, out, L, S, ty, v4 ? 4 : 1, 0};
+}
+long rdesc_blocks(const RDesc& d) { return cdiv(d.L, (long)(256 / d.ty) * d.vec); }
+
 __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
-  __shared__ float red[16 * 17 + 16];
+  __shared__ float red[256 * 4];
   const int bid = blockIdx.x;
   int k = 0;
   while (k + 1 < rb.n && rb.d[k + 1].blk0 <= bid) ++k;
-  const float* base = rb.d[k].slab;
-  const long L = rb.d[k].L;
-  const int S = rb.d[k].S, TY = rb.d[k].ty, TX = 256 / TY;
-  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
-  const long col = (long)(bid - rb.d[k].blk0) * TX + tx;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (col < L) {
-    int s = ty;
-    for (; s + 3 * TY < S; s += 4 * TY) {
-      a0 += base[(long)s * L + col];
-      a1 += base[(long)(s + TY) * L + col];
-      a2 += base[(long)(s + 2 * TY) * L + col];
-      a3 += base[(long)(s + 3 * TY) * L + col];
-    }
-    for (; s < S; s += TY) a0 += base[(long)s * L + col];
+  const RDesc& d = rb.d[k];
+  const int TY = d.ty, TXQ = 256 / TY, VEC = d.vec;
+  const int tx = threadIdx.x % TXQ, ty = threadIdx.x / TXQ;
+  const long col = ((long)(bid - d.blk0) * TXQ + tx) * VEC;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col < d.L) {
+    if (VEC == 4) slab_col_partial<4>(d.slab, d.S, d.L, col, ty, TY, v);
+    else slab_col_partial<1>(d.slab, d.S, d.L, col, ty, TY, v);
   }
-  red[ty * (TX + 1) + tx] = (a0 + a1) + (a2 + a3);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[(ty * TXQ + tx) * 4 + e] = v[e];
   __syncthreads();
-  if (ty == 0 && col < L) {
-    float t = 0.f;
-    for (int j = 0; j < TY; ++j) t += red[j * (TX + 1) + tx];
-    rb.d[k].out[col] = t;
+  if (ty == 0 && col < d.L) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TY; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] += red[(j * TXQ + tx) * 4 + e];
+    if (VEC == 4) st4(d.out + col, make_float4(t[0], t[1], t[2], t[3]));
+    else d.out[col] = t[0];
+  }
+}
+
+void launch_multi(const std::vector<RDesc>& ds, hipStream_t st) {
+  size_t i = 0;
+  while (i < ds.size()) {
+    RBatch rb;
+    rb.n = 0;
+    long blocks = 0;
+    for (; i < ds.size() && rb.n < RB_MAX; ++i) {
+      RDesc d = ds[i];
+      d.blk0 = (int)blocks;
+      blocks += rdesc_blocks(d);
+      rb.d[rb.n++] = d;
+    }
+    reduce_multi_kernel<<<(unsigned)blocks, 256, 0, st>>>(rb);
   }
 }
 
@@ -672,26 +692,14 @@ thread_local hipStream_t g_defer_stream = nullptr;
 // the flush after every stream that produced a queued slab), launched otherwise
 void grad_reduce(const float* slab, int S, long L, float* out, hipStream_t st) {
   if (g_defer) {
-    g_pending.push_back(RDesc{slab, out, L, S, reduce_ty(S, L), 0, 0});
+    g_pending.push_back(make_rdesc(slab, S, L, out));
     return;
   }
-  launch_reduce(slab, 1, S, L, 1.f, out, st);
+  launch_multi(std::vector<RDesc>{make_rdesc(slab, S, L, out)}, st);
 }
 
 void flush_pending() {
-  size_t i = 0;
-  while (i < g_pending.size()) {
-    RBatch rb;
-    rb.n = 0;
-    int blocks = 0;
-    for (; i < g_pending.size() && rb.n < RB_MAX; ++i) {
-      RDesc d = g_pending[i];
-      d.blk0 = blocks;
-      blocks += cdiv(d.L, 256 / d.ty);
-      rb.d[rb.n++] = d;
-    }
-    reduce_multi_kernel<<<blocks, 256, 0, g_defer_stream>>>(rb);
-  }
+  launch_multi(g_pending, g_defer_stream);
   g_pending.clear();
   launch_post(g_post, g_defer_stream);  // post-ops read reduction outputs: after every reduction of the flush
   g_post.clear();
