@@ -155,6 +155,11 @@ int nbp_img_chan_dot(const void* x, const void* y, float* slab, int B, int H, in
    gradients dW = da^T mean, db = sum_b da are a K = B weight-gradient GEMM (nbp_wgrad_f32 on da and mean). */
 int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, float* da, float* ds, int B, int C,
                 nbp_stream_t s);
+/* The whole SCA backward in one launch: ds = da . W with da reduced from the img_chan_dot slab, and the SCA weight
+   gradients dW[o][i] = sum_b da[b][o] mean[b][i], db[o] = sum_b da[b][o] written in place (replaces nbp_sca_bwd +
+   the K = B nbp_wgrad_f32; NAFNet_arch.py:39-41,67). */
+int nbp_sca_bwd_fused(const float* da_slab, int chunks, const float* wsca, const float* mean, float* ds, float* dW,
+                      float* db, int B, int C, nbp_stream_t s);
 /* dg = dh*a + ds/HW, then SimpleGate backward into dt2 [M][2C]. */
 int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* t2, void* dt2, long M, int C, int HW,
                    int dtype, nbp_stream_t s);

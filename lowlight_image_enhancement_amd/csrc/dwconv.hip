@@ -98,11 +98,30 @@ __global__ __launch_bounds__(256) void reduce_rows8(const float* __restrict__ sl
   if (j == 0 && e < B * C) out[e] = acc * scale;
 }
 
-// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i] (mean from reduce_rows8).
+// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
 // 16 waves per block, one output o per wave; the means of SCA_NB images are staged in LDS (a few loads per thread),
 // the W row read once for all of them.
 constexpr int SCA_NB = 16;
-__global__ __launch_bounds__(1024) void sca_gemv(const float* __restrict__ mean, const float* __restrict__ wsca,
+
+// sum_{k < chunks} slab[b][k][c] with 4 independent accumulators, fixed order (the pooled / reduced vector element)
+__device__ __forceinline__ float chunk_sum(const float* __restrict__ slab, int chunks, int C, int b, int c) {
+  const float* src = slab + (long)b * chunks * C + c;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int k = 0;
+  for (; k + 3 < chunks; k += 4) {
+    a0 += src[(long)k * C];
+    a1 += src[(long)(k + 1) * C];
+    a2 += src[(long)(k + 2) * C];
+    a3 += src[(long)(k + 3) * C];
+  }
+  for (; k < chunks; ++k) a0 += src[(long)k * C];
+  return (a0 + a1) + (a2 + a3);
+}
+
+// One launch for the SCA forward: every block reduces the pool slab of SCA_NB images into LDS (mean = sum / HW; block
+// 0 also stores it for the backward), then one wave per output o forms a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
+__global__ __launch_bounds__(1024) void sca_gemv(const float* __restrict__ pool, int chunks, float inv_hw,
+                                                 float* __restrict__ mean_out, const float* __restrict__ wsca,
                                                  const float* __restrict__ bsca, float* __restrict__ a_out, int B,
                                                  int C) {
   extern __shared__ float sm[];  // [SCA_NB][C]
@@ -111,16 +130,11 @@ __global__ __launch_bounds__(1024) void sca_gemv(const float* __restrict__ mean,
   for (int b0 = 0; b0 < B; b0 += SCA_NB) {
     const int nb = min(SCA_NB, B - b0);
     __syncthreads();
-    for (int e0 = threadIdx.x; e0 < nb * C; e0 += 4 * blockDim.x) {
-      float m[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = e0 + u * blockDim.x;
-        m[u] = e < nb * C ? mean[(long)b0 * C + e] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (e0 + u * blockDim.x < nb * C) sm[e0 + u * blockDim.x] = m[u];
+    for (int e = threadIdx.x; e < nb * C; e += blockDim.x) {
+      const int bb = e / C, c = e - bb * C;
+      const float m = chunk_sum(pool, chunks, C, b0 + bb, c) * inv_hw;
+      sm[e] = m;
+      if (blockIdx.x == 0) mean_out[(long)b0 * C + e] = m;
     }
     __syncthreads();
     if (o < C) {
@@ -219,6 +233,83 @@ __global__ __launch_bounds__(1024) void sca_bwd_ds(const float* __restrict__ da,
   __syncthreads();
   for (int e = threadIdx.x; e < nb * 64; e += blockDim.x) {
     const int b = e >> 6, l = e & 63, ii = blockIdx.x * 64 + l;
+    if (ii < C) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < SCA_BW; ++w) v += part[(w * SCA_NB + b) * 64 + l];
+      ds_out[(long)(b0 + b) * C + ii] = v;
+    }
+  }
+}
+
+// One launch for the SCA backward (NAFNet_arch.py:39-41, 67).  Blocks [0, nds): ds[b][i] = sum_o W[o][i] da[b][o]
+// as sca_bwd_ds, with da reduced from the img_chan_dot slab in the block itself.  Blocks [nds, nds + C/8): the
+// weight gradients of 8 rows o: dW[o][i] = sum_b da[b][o] mean[b][i], db[o] = sum_b da[b][o] (written to their
+// final place: no slab, no separate K = B GEMM).  Fixed summation orders throughout.
+constexpr int SCA_OB = 8;
+__global__ __launch_bounds__(1024) void sca_bwd_fused(const float* __restrict__ slab, int chunks,
+                                                      const float* __restrict__ wsca, const float* __restrict__ mean,
+                                                      float* __restrict__ ds_out, float* __restrict__ dW,
+                                                      float* __restrict__ db, int B, int C, int nds) {
+  extern __shared__ float sh[];
+  if ((int)blockIdx.x >= nds) {
+    const int o0 = (blockIdx.x - nds) * SCA_OB, no = min(SCA_OB, C - o0);
+    float* sda = sh;  // [B][SCA_OB]
+    for (int e = threadIdx.x; e < B * SCA_OB; e += blockDim.x) {
+      const int b = e / SCA_OB, r = e % SCA_OB;
+      sda[e] = r < no ? chunk_sum(slab, chunks, C, b, o0 + r) : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < no * C; e += blockDim.x) {
+      const int r = e / C, i = e - r * C;
+      float acc = 0.f;
+      for (int b = 0; b < B; ++b) acc = fmaf(sda[b * SCA_OB + r], mean[(long)b * C + i], acc);
+      dW[(long)(o0 + r) * C + i] = acc;
+    }
+    if ((int)threadIdx.x < no) {
+      float t = 0.f;
+      for (int b = 0; b < B; ++b) t += sda[b * SCA_OB + threadIdx.x];
+      db[o0 + threadIdx.x] = t;
+    }
+    return;
+  }
+  float* sda = sh;
+  float* part = sh + SCA_NB * C;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int cb = blockIdx.x % ((C + 63) / 64), bt = blockIdx.x / ((C + 63) / 64);
+  const int i = cb * 64 + lane;
+  const int b0 = bt * SCA_NB, nb = min(SCA_NB, B - b0);
+  for (int e = threadIdx.x; e < SCA_NB * C; e += blockDim.x) {
+    const int bb = e / C, c = e - bb * C;
+    sda[e] = bb < nb ? chunk_sum(slab, chunks, C, b0 + bb, c) : 0.f;
+  }
+  __syncthreads();
+  float acc[SCA_NB];
+#pragma unroll
+  for (int b = 0; b < SCA_NB; ++b) acc[b] = 0.f;
+  const int per = (C + SCA_BW - 1) / SCA_BW, o0 = wv * per, o1 = min(C, o0 + per);
+  if (i < C) {
+    int o = o0;
+    for (; o + 3 < o1; o += 4) {
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = wsca[(long)(o + u) * C + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int b = 0; b < SCA_NB; ++b) acc[b] = fmaf(w[u], sda[b * C + o + u], acc[b]);
+    }
+    for (; o < o1; ++o) {
+      const float w = wsca[(long)o * C + i];
+#pragma unroll
+      for (int b = 0; b < SCA_NB; ++b) acc[b] = fmaf(w, sda[b * C + o], acc[b]);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < SCA_NB; ++b) part[(wv * SCA_NB + b) * 64 + lane] = acc[b];
+  __syncthreads();
+  for (int e = threadIdx.x; e < nb * 64; e += blockDim.x) {
+    const int b = e >> 6, l = e & 63, ii = cb * 64 + l;
     if (ii < C) {
       float v = 0.f;
 #pragma unroll
@@ -779,8 +870,8 @@ int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const flo
                 int HW, int C, nbp_stream_t s) {
   NBP_REQUIRE(pool_slab && wsca && bsca && mean && a && B > 0 && C > 0 && chunks > 0, "nbp_sca_fwd: bad args");
   NBP_REQUIRE(C <= 1024, "nbp_sca_fwd: C <= 1024");
-  reduce_rows8<<<cdiv((long)B * C, 32), 256, 0, S(s)>>>(pool_slab, B, chunks, C, 1.f / (float)HW, mean);
-  sca_gemv<<<cdiv(C, 16), 1024, (size_t)SCA_NB * C * sizeof(float), S(s)>>>(mean, wsca, bsca, a, B, C);
+  sca_gemv<<<cdiv(C, 16), 1024, (size_t)SCA_NB * C * sizeof(float), S(s)>>>(pool_slab, chunks, 1.f / (float)HW, mean,
+                                                                            wsca, bsca, a, B, C);
   return check_launch("sca_fwd");
 }
 
@@ -803,6 +894,18 @@ int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, float* da, 
   sca_bwd_ds<<<dim3(cdiv(C, 64), cdiv(B, SCA_NB)), 64 * SCA_BW,
                ((size_t)SCA_NB * C + SCA_BW * SCA_NB * 64) * sizeof(float), S(s)>>>(da, wsca, ds, B, C);
   return check_launch("sca_bwd");
+}
+
+int nbp_sca_bwd_fused(const float* da_slab, int chunks, const float* wsca, const float* mean, float* ds, float* dW,
+                      float* db, int B, int C, nbp_stream_t s) {
+  NBP_REQUIRE(da_slab && wsca && mean && ds && dW && db && B > 0 && C > 0 && chunks > 0, "nbp_sca_bwd_fused: bad args");
+  NBP_REQUIRE(C <= 1024 && B <= 4096, "nbp_sca_bwd_fused: C <= 1024, B <= 4096");
+  const int nds = cdiv(C, 64) * cdiv(B, SCA_NB), ndw = cdiv(C, SCA_OB);
+  const size_t sm_ds = ((size_t)SCA_NB * C + SCA_BW * SCA_NB * 64) * sizeof(float);
+  const size_t sm_dw = (size_t)B * SCA_OB * sizeof(float);
+  sca_bwd_fused<<<nds + ndw, 64 * SCA_BW, sm_ds > sm_dw ? sm_ds : sm_dw, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db,
+                                                                             B, C, nds);
+  return check_launch("sca_bwd_fused");
 }
 
 int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* t2, void* dt2, long M, int C, int HW,

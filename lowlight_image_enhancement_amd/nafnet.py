@@ -576,11 +576,10 @@ class NAFNet(nn.Module):
         chunks = query("dw_chunks", B, h, w, c, 0)
         da_slab = F(B * chunks * c)
         call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
-        da, ds = F(B, c), F(B, c)
-        call("sca_bwd", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), da, ds, B, c)
-        # dW_sca = da^T mean, db_sca = colsum(da): an fp32 weight-gradient GEMM with K = B rows
-        self._wgrad(da, c, AM_PLAIN, S["mean"], c, AM_PLAIN, None, 1, B, c, c, 0, 0, 0, 0,
-                    self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), dtype=0)
+        # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch
+        ds = F(B, c)
+        call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,
+             self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
         # SimpleGate + depthwise conv2 (fused when the channel slicing allows: dt2 stays in LDS)
         dt1 = E(M, 2 * c)
         ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
