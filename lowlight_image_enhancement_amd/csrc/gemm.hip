@@ -288,10 +288,22 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   const int mb = s * p.chunk;
   const int me = min(p.M, mb + p.chunk);
   const bool do_b = p.slab_b && blockIdx.y == 0;
-  floatx16 acc;
+  floatx16 acc, tot;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = tot[r] = 0.f;
   float bsum = 0.f;
+  // XMODE 3 = AM_SCALE with rows_per_img % 32 == 0: the MFMAs run on the unscaled X and each image's partial sum
+  // is scaled by its column factor in fp32 when the 32-row stages move on to the next image (no per-element rescale)
+  int cur_img = mb / p.rows_per_img;
+  auto fold = [&](int im) {
+    const int kk = k0 + wk * 32 + (lane & 31);
+    const float sc = kk < p.K ? p.x_scale[(long)im * p.K + kk] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      tot[r] = fmaf(acc[r], sc, tot[r]);
+      acc[r] = 0.f;
+    }
+  };
   // loader: one 16-byte chunk of G and one of X per thread: row r = tid >> 3, 8 columns at (tid & 7) * 8
   const int lr = tid >> 3, lc = (tid & 7) * 8;
   bf16x8 rg, rx;
@@ -331,6 +343,13 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
     for (int m0 = mb; m0 < me; m0 += RM) {
       const bool more = m0 + RM < me;
       if (more) load(m0 + RM);
+      if constexpr (XMODE == 3) {
+        const int im = m0 / p.rows_per_img;
+        if (im != cur_img) {
+          fold(cur_img);
+          cur_img = im;
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < RM; ks += 16) {
         bf16x8 a, b;
@@ -358,11 +377,14 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
       }
     }
   }
+  if constexpr (XMODE == 3) {
+    if (mb < me) fold(cur_img);
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int n = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     const int k = k0 + wk * 32 + (lane & 31);
-    if (n < p.N && k < p.K) p.slab[((long)s * p.N + n) * p.K + k] = acc[r];
+    if (n < p.N && k < p.K) p.slab[((long)s * p.N + n) * p.K + k] = XMODE == 3 ? tot[r] : acc[r];
   }
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
@@ -814,6 +836,8 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
     if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN><<<wgrid, 256, 0, st>>>(p);
     else if (wide) wgrad_bf16_wide<AM_SCALE><<<wgrid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
+    else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
+      wgrad_bf16_kernel<AM_PLAIN, 3><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_bf16_kernel<AM_PLAIN, AM_SCALE><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_bf16_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);
