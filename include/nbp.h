@@ -98,6 +98,15 @@ int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int
 int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, int a_dtype,
                   const void* Bw, long ldb, void* C, long ldc, int c_mode, int c_dtype, int M, int N, int K, int gh,
                   int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s);
+/* 1x1-conv input gradient fused with the LayerNorm2d backward that follows it (bf16; NAFBlock conv4 -> norm2 and
+ * conv1 -> norm1 at N = C in {32, 64}, NAFNet_arch.py:60-80 + arch_util.py:277-289):
+ *   dn = A[M,K] . Wt[N,K]^T (never stored),  dx = (g - yhat*mean(g*yhat) - mean(g)) / den + dres,  g = dn * lnw,
+ *   yhat = (x - mu) / den from stats = (mu, den) per row;  dlnw = sum dn*yhat, dlnb = sum dn (slab reductions into
+ *   ws, deferred like nbp_wgrad_f32's).  ws: nbp_dgrad_ln_workspace_floats(M, N). */
+size_t nbp_dgrad_ln_workspace_floats(long M, int N);
+int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
+                     const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
+                     float* ws, size_t ws_floats, nbp_stream_t s);
 /* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols} (int64, device) out_t[offset..] =
  * bf16(flat matrix)^T. */
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);

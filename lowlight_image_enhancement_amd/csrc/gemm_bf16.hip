@@ -22,7 +22,7 @@ namespace {
 // forward (C = t with channel pairs (c, C+c) interleaved, and pre <- g = t[2c] * t[2c+1]) and SimpleGate backward
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
-enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5 };
+enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6 };
 
 struct GemmPB {
   const void* A;
@@ -390,6 +390,14 @@ struct SkinnyP {
   const __bf16* R;
   const float* rscale;
   __bf16* aux;
+  // CM_LNBWD (LayerNorm2d backward in the epilogue, arch_util.py:277-289): the GEMM output is dn; R = the LN input x,
+  // stats = (mu, sqrt(var + eps)) per row, lnw = the LN weight, dres = the residual-branch gradient added to dx;
+  // per-block partials of sum(dn * yhat) / sum(dn) go to slab_w / slab_b [grid][N]
+  const float2* stats;
+  const float* lnw;
+  const __bf16* dres;
+  float* slab_w;
+  float* slab_b;
 };
 
 template <int NT, int KS, int AMODE, int CMODE>
@@ -417,10 +425,13 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
   const int cpr = outw / 8;                                    // chunks per row (divides 64: outw in {8..128})
   const int ccol = (lane % cpr) * 8;                           // this lane's output column
   const int rstep = 64 / cpr;                                  // rows advanced per pass
-  float bia[8], rsc[8];
+  float bia[8], rsc[8], aw[8], ab[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { bia[j] = 0.f; rsc[j] = 1.f; }
-  if (CMODE != CM_SGBWD) {
+  for (int j = 0; j < 8; ++j) { bia[j] = 0.f; rsc[j] = 1.f; aw[j] = ab[j] = 0.f; }
+  if (CMODE == CM_LNBWD) {  // rsc holds the LN weight of this lane's 8 columns
+    const float4 s0 = ld4(p.lnw + ccol), s1 = ld4(p.lnw + ccol + 4);
+    rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
+  } else if (CMODE != CM_SGBWD) {
     if (p.bias) {
       const float4 b0 = ld4(p.bias + ccol), b1 = ld4(p.bias + ccol + 4);
       bia[0] = b0.x; bia[1] = b0.y; bia[2] = b0.z; bia[3] = b0.w; bia[4] = b1.x; bia[5] = b1.y; bia[6] = b1.z; bia[7] = b1.w;
@@ -496,6 +507,32 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
       const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
       const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
       float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      if constexpr (CMODE == CM_LNBWD) {  // the row's cpr lanes are consecutive: shuffle sums within the group
+        constexpr int G = 4 * NT;
+        const long off = m * p.ldc + ccol;
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(p.R + off);
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.dres + off);
+        const float2 st = p.stats[m];
+        const float inv = 1.f / st.y;
+        float yh[8], sg = 0.f, sgy = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          yh[j] = ((float)xv[j] - st.x) * inv;
+          const float g = v[j] * rsc[j];
+          sg += g;
+          sgy = fmaf(g, yh[j], sgy);
+          aw[j] = fmaf(v[j], yh[j], aw[j]);
+          ab[j] += v[j];
+        }
+        sg = group_sum<G>(sg);
+        sgy = group_sum<G>(sgy);
+        const float mg = sg / (float)N, mgy = sgy / (float)N;
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (__bf16)((v[j] * rsc[j] - yh[j] * mgy - mg) * inv + (float)rv[j]);
+        *reinterpret_cast<bf16x8*>(p.C + off) = o;
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bia[j];
       const long off = m * p.ldc + ccol;
@@ -519,20 +556,51 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) a0[ks] = a1[ks];
   }
+  if constexpr (CMODE == CM_LNBWD) {  // LN weight / bias gradient partials: lanes sharing ccol, then the 4 waves
+    constexpr int G = 4 * NT;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = G; o < 64; o <<= 1) {
+        aw[j] += __shfl_xor(aw[j], o, 64);
+        ab[j] += __shfl_xor(ab[j], o, 64);
+      }
+    __syncthreads();
+    float* red = &stage[0][0];  // [4 waves][2][N]
+    const int wv = threadIdx.x >> 6;
+    if (lane < G) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wv * 2 + 0) * N + ccol + j] = aw[j];
+        red[(wv * 2 + 1) * N + ccol + j] = ab[j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < N; c += blockDim.x) {
+      p.slab_w[(long)blockIdx.x * N + c] = ((red[0 * N + c] + red[2 * N + c]) + red[4 * N + c]) + red[6 * N + c];
+      p.slab_b[(long)blockIdx.x * N + c] = ((red[1 * N + c] + red[3 * N + c]) + red[5 * N + c]) + red[7 * N + c];
+    }
+  }
 }
 
+long skinny_blocks(long M) {
+  const long ntiles = (M + 31) / 32;
+  const long blocks = (ntiles + 3) / 4;
+  return blocks > 1024 ? 1024 : blocks;  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs
+}
+
+// K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads)
 template <int AMODE, int CMODE>
 void launch_skinny(const SkinnyP& p, hipStream_t st) {
-  const long ntiles = (p.M + 31) / 32;
-  long blocks = (ntiles + 3) / 4;
-  if (blocks > 1024) blocks = 1024;  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs
-  const dim3 g((unsigned)blocks);
+  const dim3 g((unsigned)skinny_blocks(p.M));
   const int nt = (p.N + 31) / 32, ks = (p.K + 15) / 16;
 #define NBP_SKINNY(NT_, KS_) gemm_skinny_kernel<NT_, KS_, AMODE, CMODE><<<g, 256, 0, st>>>(p)
   if (nt == 1) {
-    if (ks == 1) NBP_SKINNY(1, 1); else if (ks == 2) NBP_SKINNY(1, 2); else if (ks == 3) NBP_SKINNY(1, 3); else NBP_SKINNY(1, 4);
+    if (ks == 1) NBP_SKINNY(1, 1); else if (ks == 2) NBP_SKINNY(1, 2); else if (ks == 3) NBP_SKINNY(1, 3);
+    else if (ks == 4) NBP_SKINNY(1, 4); else NBP_SKINNY(1, 8);
   } else {
-    if (ks == 1) NBP_SKINNY(2, 1); else if (ks == 2) NBP_SKINNY(2, 2); else if (ks == 3) NBP_SKINNY(2, 3); else NBP_SKINNY(2, 4);
+    if (ks == 1) NBP_SKINNY(2, 1); else if (ks == 2) NBP_SKINNY(2, 2); else if (ks == 3) NBP_SKINNY(2, 3);
+    else if (ks == 4) NBP_SKINNY(2, 4); else NBP_SKINNY(2, 8);
   }
 #undef NBP_SKINNY
 }
@@ -541,14 +609,14 @@ void launch_skinny(const SkinnyP& p, hipStream_t st) {
 bool try_skinny(const void* A, long lda, int a_mode, const float* a_scale, int rows, const void* Bw, long ldb, void* C,
                 long ldc, int c_mode, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                 void* pre, hipStream_t st) {
-  if (N > 64 || K > 64 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc % 8) return false;
+  if (N > 64 || K > 128 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc % 8) return false;
   const bool ok = (a_mode == AM_PLAIN && c_mode == CM_PLAIN && !pre) || (a_mode == AM_SCALE && c_mode == CM_PLAIN && !pre) ||
                   (a_mode == AM_PLAIN && c_mode == CM_SG) || (a_mode == AM_SCALE && c_mode == CM_SGBWD) ||
                   (a_mode == AM_PLAIN && c_mode == CM_SGBWD);
   if (!ok) return false;
   SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, a_scale, rows, reinterpret_cast<const __bf16*>(Bw), ldb,
             reinterpret_cast<__bf16*>(C), ldc, M, N, K, bias, reinterpret_cast<const __bf16*>(R), rscale,
-            reinterpret_cast<__bf16*>(pre)};
+            reinterpret_cast<__bf16*>(pre), nullptr, nullptr, nullptr, nullptr, nullptr};
   if (c_mode == CM_SG) launch_skinny<AM_PLAIN, CM_SG>(p, st);
   else if (c_mode == CM_SGBWD && a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_SGBWD>(p, st);
   else if (c_mode == CM_SGBWD) launch_skinny<AM_PLAIN, CM_SGBWD>(p, st);
@@ -674,6 +742,27 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   else rc = dispatch_modes<__bf16, float>(p, a_mode, c_mode, st);
   if (rc) return rc;
   return check_launch("gemm_bf16");
+}
+
+size_t nbp_dgrad_ln_workspace_floats(long M, int N) { return (size_t)2 * skinny_blocks(M) * N; }
+
+int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
+                     const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
+                     float* ws, size_t ws_floats, nbp_stream_t s) {
+  NBP_REQUIRE(A && Wt && x && stats && lnw && dres && dx && dlnw && dlnb && ws && M > 0, "nbp_dgrad_ln_bwd: bad args");
+  NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
+              "nbp_dgrad_ln_bwd: N must be 32 or 64, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
+  const long nb = skinny_blocks(M);
+  NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
+  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb,
+            reinterpret_cast<__bf16*>(dx), N, M, N, K, nullptr, reinterpret_cast<const __bf16*>(x), nullptr, nullptr,
+            reinterpret_cast<const float2*>(stats), lnw, reinterpret_cast<const __bf16*>(dres), ws, ws + nb * N};
+  launch_skinny<AM_PLAIN, CM_LNBWD>(p, S(s));
+  int rc = check_launch("dgrad_ln_bwd");
+  if (rc) return rc;
+  rc = nbp_reduce_slab(p.slab_w, (int)nb, N, dlnw, s);
+  if (rc) return rc;
+  return nbp_reduce_slab(p.slab_b, (int)nb, N, dlnb, s);
 }
 
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s) {

@@ -550,19 +550,24 @@ class NAFNet(nn.Module):
         call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
              self._slice(P, pre + "gamma"), self._slice(dflat, pre + "conv5.weight"),
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
-        # conv4
-        dn2 = E(M, c)
-        self._mm(Wt, dt4, 2 * c, AM_PLAIN, None, 1, pre + "conv4.weight", dn2, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
+        # conv4 input gradient + norm2 backward + residual
+        fuse_ln = dt == 1 and c in (32, 64)  # LN backward in the skinny dgrad's epilogue (dn2 never stored)
+        dy = E(M, c)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
-        # norm2 + residual
-        lg = query("ln_nhwc_grid", M, c, dt)
-        sw, sb = F(lg * c), F(lg * c)
-        dy = E(M, c)
-        call("ln_bwd_nhwc", dn2, S["y"].reshape(M, c), S["st2"], self._slice(P, pre + "norm2.weight"), dout, dy, sw, sb,
-             M, c, dt)
-        self._reduce(sw, lg, c, self._slice(dflat, pre + "norm2.weight"))
-        self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
+        if fuse_ln:
+            self._dgrad_ln(Wt, dflat, P, pre, "conv4.weight", "norm2", dt4, S["y"].reshape(M, c), S["st2"], dout, dy,
+                           M, c)
+        else:
+            dn2 = E(M, c)
+            self._mm(Wt, dt4, 2 * c, AM_PLAIN, None, 1, pre + "conv4.weight", dn2, c, CM_PLAIN, M, c, 2 * c,
+                     dgrad=True)
+            lg = query("ln_nhwc_grid", M, c, dt)
+            sw, sb = F(lg * c), F(lg * c)
+            call("ln_bwd_nhwc", dn2, S["y"].reshape(M, c), S["st2"], self._slice(P, pre + "norm2.weight"), dout, dy,
+                 sw, sb, M, c, dt)
+            self._reduce(sw, lg, c, self._slice(dflat, pre + "norm2.weight"))
+            self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
         # y = x + beta * conv3(h), h = g (.) a: same layer-scale identity as conv5 (dh = (beta (.) dy) W3)
         dh = E(M, c)
         self._mm(Wt, dy, c, AM_SCALE, self._slice(P, pre + "beta"), M, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c,
@@ -591,19 +596,33 @@ class NAFNet(nn.Module):
             dt2 = E(M, 2 * c)
             call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW, dt)
             call("dw_bwd", dt2, *dw_args)
-        # conv1
-        dn1 = E(M, c)
-        self._mm(Wt, dt1, 2 * c, AM_PLAIN, None, 1, pre + "conv1.weight", dn1, c, CM_PLAIN, M, c, 2 * c, dgrad=True)
+        # conv1 input gradient + norm1 backward + residual
+        dx = E(M, c)
         self._wgrad(dt1, 2 * c, AM_PLAIN, S["n1"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
-        # norm1 + residual
-        dx = E(M, c)
-        sw, sb = F(lg * c), F(lg * c)
-        call("ln_bwd_nhwc", dn1, S["x"].reshape(M, c), S["st1"], self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb,
-             M, c, dt)
-        self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
-        self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))
+        if fuse_ln:
+            self._dgrad_ln(Wt, dflat, P, pre, "conv1.weight", "norm1", dt1, S["x"].reshape(M, c), S["st1"], dy, dx,
+                           M, c)
+        else:
+            dn1 = E(M, c)
+            self._mm(Wt, dt1, 2 * c, AM_PLAIN, None, 1, pre + "conv1.weight", dn1, c, CM_PLAIN, M, c, 2 * c,
+                     dgrad=True)
+            lg = query("ln_nhwc_grid", M, c, dt)
+            sw, sb = F(lg * c), F(lg * c)
+            call("ln_bwd_nhwc", dn1, S["x"].reshape(M, c), S["st1"], self._slice(P, pre + "norm1.weight"), dy, dx,
+                 sw, sb, M, c, dt)
+            self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
+            self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))
         return dx.view(B, h, w, c)
+
+    def _dgrad_ln(self, Wt, dflat, P, pre, wkey, norm, dt, x, st, dres, out, M, c):
+        """dn = dt . W (bf16 transposed weight copy) and the LayerNorm2d backward + residual in one launch
+        (nbp_dgrad_ln_bwd); the LN weight / bias gradients are slab-reduced with the stage's deferred reductions."""
+        n_ws = query("dgrad_ln_workspace_floats", M, c)
+        ws = self._ws(n_ws, dt.device)
+        call("dgrad_ln_bwd", dt, 2 * c, self._slice(Wt[2], pre + wkey), 2 * c, M, c, 2 * c, x, st,
+             self._slice(P, pre + norm + ".weight"), dres, out, self._slice(dflat, pre + norm + ".weight"),
+             self._slice(dflat, pre + norm + ".bias"), ws, n_ws)
 
 
 class _NAFNetFn(torch.autograd.Function):

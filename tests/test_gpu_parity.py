@@ -534,3 +534,32 @@ def test_gemm_bf16_skinny_path(dev, M, N, K):
     Aeff = (A.float() * ascale.repeat_interleave(rows, 0)[:M]).to(torch.bfloat16)
     ref = R.double() + (Aeff.double() @ W.double().t() + bias.double())
     close(out.float(), ref.cpu().numpy(), **tol)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 32, 64), (3000, 64, 128), (777, 32, 32)])
+def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
+    """Fused 1x1-conv input gradient + LayerNorm2d backward + residual (skinny bf16 GEMM epilogue) vs float64 math on
+    the same bf16 operands: dn = A W^T, dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * w."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+    Wt = (torch.randn(N, K, device=dev, generator=gen) / K ** 0.5).to(torch.bfloat16)
+    x = (torch.randn(M, N, device=dev, generator=gen) * 2 + 0.5).to(torch.bfloat16)
+    xd = x.double()
+    mu = xd.mean(1, keepdim=True)
+    den = ((xd - mu) ** 2).mean(1, keepdim=True).add(1e-6).sqrt()
+    stats = torch.cat([mu, den], 1).float().contiguous()
+    lnw = torch.randn(N, device=dev, generator=gen)
+    dres = torch.randn(M, N, device=dev, generator=gen).to(torch.bfloat16)
+    dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    dlnw, dlnb = torch.empty(N, device=dev), torch.empty(N, device=dev)
+    n_ws = query("dgrad_ln_workspace_floats", M, N)
+    ws = torch.empty(n_ws, device=dev)
+    call("dgrad_ln_bwd", A, K, Wt, K, M, N, K, x, stats, lnw, dres, dx, dlnw, dlnb, ws, n_ws)
+    dn = A.double() @ Wt.double().t()
+    yh = (xd - stats[:, :1].double()) / stats[:, 1:].double()
+    g = dn * lnw.double()
+    ref = (g - yh * (g * yh).mean(1, keepdim=True) - g.mean(1, keepdim=True)) / stats[:, 1:].double() + dres.double()
+    close(dx.float(), ref.float().cpu().numpy(), atol=2e-2, rtol=1e-2)  # bf16 output rounding
+    close(dlnw, (dn * yh).sum(0).cpu().numpy(), atol=2e-4 * M ** 0.5, rtol=1e-4)
+    close(dlnb, dn.sum(0).cpu().numpy(), atol=2e-4 * M ** 0.5, rtol=1e-4)
