@@ -119,10 +119,11 @@ def main():
                     help="bf16: bf16 MFMA operands + fp32 accumulation (the reference's AMP training); "
                          "fp32: fp32 everywhere (parity mode)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=0, help="per-GPU batch override (diagnostics; 0 = the workload's)")
     args = ap.parse_args()
     global BATCH, IMG
     wl = WORKLOADS[args.workload]
-    BATCH, IMG = wl["batch"], wl["img"]
+    BATCH, IMG = (args.batch or wl["batch"]), wl["img"]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

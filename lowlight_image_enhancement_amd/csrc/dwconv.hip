@@ -423,6 +423,7 @@ struct DwTileP {
   const void* t2;   // [M][2C]           (fused)
   const void* t1;   // [M][2C]
   const float* wdw; // [2C][9]
+  const float* bdw; // [2C]               (REC: the conv2 bias for the t2 recompute)
   void* dt1;        // [M][2C]
   float* slab_w;    // [rows][2C][9]
   float* slab_b;    // [rows][2C]
@@ -431,6 +432,7 @@ struct DwTileP {
 };
 
 constexpr int DWT_TH = 16;
+constexpr int DWT_TH_REC = 12;
 inline int dw_bwd_tw(int W) { return W >= 32 ? 32 : 16; }
 
 template <typename T>
@@ -467,29 +469,47 @@ __device__ __forceinline__ void unpack16(uint4 r, float* f) {
   }
 }
 
-template <typename T, bool FUSED, int DWT_TW>
+// REC (with FUSED): t2 is not read from HBM either - the forward never stored it.  t1 is staged with a two-pixel
+// halo, t2 = bias + conv(t1) is recomputed into LDS on the one-pixel halo (the forward's FMA order), and the SCA /
+// SimpleGate backward turns it into dt2 in place.  Shorter tiles (TH 12) keep two blocks per CU.
+template <typename T, bool FUSED, int DWT_TW, bool REC>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
   constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
   constexpr int HS = CSL / 2;            // gate channels per slice
   constexpr int NQ = CSL / 4;            // channel quads per slice
   constexpr int NT = NQ * DWT_TW;        // threads
-  constexpr int LW = DWT_TW + 2, LH = DWT_TH + 2;
+  constexpr int TH = REC ? DWT_TH_REC : DWT_TH;
+  constexpr int XO = REC ? 1 : 0;        // extra t1 halo
+  constexpr int LW = DWT_TW + 2, LH = TH + 2;
+  constexpr int LWX = LW + 2 * XO, LHX = LH + 2 * XO;
   __shared__ __attribute__((aligned(16))) T sg[LH * LW * CSL];
-  __shared__ __attribute__((aligned(16))) T sx[LH * LW * CSL];
+  __shared__ __attribute__((aligned(16))) T sx[LHX * LWX * CSL];
+  // t1 at (row, col) of the one-pixel-halo frame
+  auto SX = [&](int row, int col) { return sx + ((row + XO) * LWX + col + XO) * CSL; };
   const int tid = threadIdx.x;
   const int u = xcd_remap(blockIdx.x, gridDim.x);  // the slices of one tile share an XCD (and its L2)
   const int slice = u % p.slices, tile = (u / p.slices) % p.tiles, b = u / (p.slices * p.tiles);
-  const int y0 = (tile / p.tiles_x) * DWT_TH, x0 = (tile % p.tiles_x) * DWT_TW;
+  const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * DWT_TW;
   const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
   const long img = (long)b * H * W;
   const int cbase = slice * HS;
+  const int q = tid % NQ, x = tid / NQ;
+  const int lc = 4 * q;
+  const int gc = lc < HS ? cbase + lc : C + cbase + (lc - HS);
+  float wk[4][9];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wk[j][t] = p.wdw[(gc + j) * 9 + t];
   // ---- stage t1 (and dt2 when unfused): 4 chunks per pixel = 2 halves x 2 chunks.  Every load of the stage is
   // issued before the first LDS store (register batches): one memory latency per tile instead of one per pass.
+  constexpr int TOT2 = LH * LW * 2, N2 = FUSED ? (TOT2 + NT - 1) / NT : 1;
+  uint4 rd[N2], ra[REC ? 1 : N2], rb[REC ? 1 : N2];
   {
     const T* t1 = reinterpret_cast<const T*>(p.t1);
     const T* dt2 = reinterpret_cast<const T*>(p.dt2);
-    constexpr int TOT1 = LH * LW * 4, N1 = (TOT1 + NT - 1) / NT;
+    constexpr int TOT1 = LHX * LWX * 4, N1 = (TOT1 + NT - 1) / NT;
     uint4 vx[N1], vg[FUSED ? 1 : N1];
 #pragma unroll
     for (int it = 0; it < N1; ++it) {
@@ -497,15 +517,13 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       vx[it] = make_uint4(0, 0, 0, 0);
       if (!FUSED) vg[it] = make_uint4(0, 0, 0, 0);
       const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
-      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+      const int gy = y0 - 1 - XO + pix / LWX, gx = x0 - 1 - XO + pix % LWX;
       if (i < TOT1 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
         const long go = (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E;
         vx[it] = *reinterpret_cast<const uint4*>(t1 + go);
         if (!FUSED) vg[it] = *reinterpret_cast<const uint4*>(dt2 + go);
       }
     }
-    constexpr int TOT2 = LH * LW * 2, N2 = FUSED ? (TOT2 + NT - 1) / NT : 1;
-    uint4 rd[N2], ra[N2], rb[N2];
     if (FUSED) {
       const T* dh = reinterpret_cast<const T*>(p.dh);
       const T* t2 = reinterpret_cast<const T*>(p.t2);
@@ -514,13 +532,16 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
         const int i = tid + it * NT;
         const int pix = i >> 1, k = i & 1;
         const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
-        rd[it] = ra[it] = rb[it] = make_uint4(0, 0, 0, 0);
+        rd[it] = make_uint4(0, 0, 0, 0);
+        if (!REC) ra[it] = rb[it] = make_uint4(0, 0, 0, 0);
         if (i < TOT2 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
           const long m = img + (long)gy * W + gx;
           const int c = cbase + k * E;
           rd[it] = *reinterpret_cast<const uint4*>(dh + m * C + c);
-          ra[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + c);
-          rb[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + C + c);
+          if (!REC) {
+            ra[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + c);
+            rb[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + C + c);
+          }
         }
       }
     }
@@ -534,40 +555,56 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
         if (!FUSED) *reinterpret_cast<uint4*>(sg + lo) = vg[it];
       }
     }
-    if (FUSED) {
+  }
+  if (REC) {
+    // t2 on the one-pixel-halo frame into sg: thread = (quad q, column), rows in steps (FMA order of the forward)
+    __syncthreads();
+    const float4 bq = ld4(p.bdw + gc);
+    for (int pix = x; pix < LH * LW; pix += DWT_TW) {
+      const int row = pix / LW, col = pix % LW;
+      float4 a = bq;
 #pragma unroll
-      for (int it = 0; it < N2; ++it) {
-        const int i = tid + it * NT;
-        if (i >= TOT2) continue;
-        const int pix = i >> 1, k = i & 1;
-        const int c = cbase + k * E;
-        float d[E], ta[E], tb[E], lo[E], hi[E];
-        unpack16<T>(rd[it], d);
+      for (int t = 0; t < 9; ++t) {
+        const float4 v = ldq(SX(row + t / 3 - 1, col + t % 3 - 1) + lc);
+        a.x = fmaf(wk[0][t], v.x, a.x); a.y = fmaf(wk[1][t], v.y, a.y);
+        a.z = fmaf(wk[2][t], v.z, a.z); a.w = fmaf(wk[3][t], v.w, a.w);
+      }
+      stq(sg + pix * CSL + lc, a);
+    }
+  }
+  if (FUSED) {
+    if (REC) __syncthreads();
+#pragma unroll
+    for (int it = 0; it < N2; ++it) {
+      const int i = tid + it * NT;
+      if (i >= TOT2) continue;
+      const int pix = i >> 1, k = i & 1;
+      const int c = cbase + k * E;
+      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+      const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
+      float d[E], ta[E], tb[E], lo[E], hi[E];
+      unpack16<T>(rd[it], d);
+      if (REC) {
+        ld16f(sg + pix * CSL + k * E, ta);
+        ld16f(sg + pix * CSL + HS + k * E, tb);
+      } else {
         unpack16<T>(ra[it], ta);
         unpack16<T>(rb[it], tb);
-        const float* av = p.a + (long)b * C + c;
-        const float* sv = p.ds + (long)b * C + c;
-#pragma unroll
-        for (int j = 0; j < E; ++j) {
-          const float dg = fmaf(d[j], av[j], sv[j] * p.inv_hw);
-          lo[j] = dg * tb[j];
-          hi[j] = dg * ta[j];
-        }
-        st16f(sg + pix * CSL + k * E, lo);
-        st16f(sg + pix * CSL + HS + k * E, hi);
       }
+      const float* av = p.a + (long)b * C + c;
+      const float* sv = p.ds + (long)b * C + c;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const float dg = inside ? fmaf(d[j], av[j], sv[j] * p.inv_hw) : 0.f;
+        lo[j] = dg * tb[j];
+        hi[j] = dg * ta[j];
+      }
+      st16f(sg + pix * CSL + k * E, lo);
+      st16f(sg + pix * CSL + HS + k * E, hi);
     }
   }
   __syncthreads();
   // ---- compute: thread = (quad q, column x)
-  const int q = tid % NQ, x = tid / NQ;
-  const int lc = 4 * q;
-  const int gc = lc < HS ? cbase + lc : C + cbase + (lc - HS);
-  float wk[4][9];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) wk[j][t] = p.wdw[(gc + j) * 9 + t];
   float4 aw[9], ab = f4(0.f);
 #pragma unroll
   for (int t = 0; t < 9; ++t) aw[t] = f4(0.f);
@@ -576,19 +613,19 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   for (int j = 0; j < 3; ++j) {
     gw[1][j] = ldq(sg + (0 * LW + x + j) * CSL + lc);
     gw[2][j] = ldq(sg + (1 * LW + x + j) * CSL + lc);
-    xw[1][j] = ldq(sx + (0 * LW + x + j) * CSL + lc);
-    xw[2][j] = ldq(sx + (1 * LW + x + j) * CSL + lc);
+    xw[1][j] = ldq(SX(0, x + j) + lc);
+    xw[2][j] = ldq(SX(1, x + j) + lc);
   }
   T* dt1 = reinterpret_cast<T*>(p.dt1);
   const bool col_ok = x0 + x < W;
 #pragma unroll
-  for (int r = 0; r < DWT_TH; ++r) {
+  for (int r = 0; r < TH; ++r) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       gw[0][j] = gw[1][j]; gw[1][j] = gw[2][j];
       xw[0][j] = xw[1][j]; xw[1][j] = xw[2][j];
       gw[2][j] = ldq(sg + ((r + 2) * LW + x + j) * CSL + lc);
-      xw[2][j] = ldq(sx + ((r + 2) * LW + x + j) * CSL + lc);
+      xw[2][j] = ldq(SX(r + 2, x + j) + lc);
     }
     float4 acc = f4(0.f);
     const float4 gc4 = gw[1][1];
@@ -733,8 +770,10 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
     }
     if (col_ok && y0 + r < H) {
       const long m = img + (long)(y0 + r) * W + x0 + x;
-      stq(t2 + m * C2 + gca, aa);
-      stq(t2 + m * C2 + gcb, ab);
+      if (t2) {  // null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
+        stq(t2 + m * C2 + gca, aa);
+        stq(t2 + m * C2 + gcb, ab);
+      }
       const float4 gv = aa * ab;
       stq(g + m * C + gca, gv);
       pacc += gv;
@@ -760,7 +799,7 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   }
 }
 
-int dw_tiles(int H, int W) { return cdiv(H, DWT_TH) * cdiv(W, dw_bwd_tw(W)); }
+int dw_tiles(int H, int W, bool rec = false) { return cdiv(H, rec ? DWT_TH_REC : DWT_TH) * cdiv(W, dw_bwd_tw(W)); }
 bool dw_tiled_ok(int C, int dtype) { return C % (dtype == 1 ? 16 : 8) == 0; }
 
 int block_for_quads(int Q) {
@@ -792,12 +831,13 @@ Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
 }
 
 int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float* ds, const void* t2, const void* t1,
-                    const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C,
-                    int dtype, nbp_stream_t s) {
+                    const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
+                    int W, int C, int dtype, nbp_stream_t s) {
   const int hs = dtype == 1 ? 16 : 8;
   const int tw = dw_bwd_tw(W);
-  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W), C / hs,
-            1.f / (float)(H * W)};
+  const bool rec = dh != nullptr && t2 == nullptr;  // fused, t2 recomputed from t1
+  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, bdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W, rec),
+            C / hs, 1.f / (float)(H * W)};
   const long nrow = (long)B * p.tiles;
   p.slab_w = ws;
   p.slab_b = ws + nrow * 2 * C * 9;
@@ -807,11 +847,13 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   NBP_DISPATCH_T(dtype, {
     constexpr int NQ = (64 / sizeof(T)) / 4;
     if (tw == 32) {
-      if (fused) dw_bwd_tiled<T, true, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
-      else dw_bwd_tiled<T, false, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      if (rec) dw_bwd_tiled<T, true, 32, true><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      else if (fused) dw_bwd_tiled<T, true, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
     } else {
-      if (fused) dw_bwd_tiled<T, true, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
-      else dw_bwd_tiled<T, false, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      if (rec) dw_bwd_tiled<T, true, 16, true><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      else if (fused) dw_bwd_tiled<T, true, 16, false><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 16, false><<<nblk, NQ * 16, 0, S(s)>>>(p);
     }
   });
   int rc = check_launch("dw_bwd_tiled");
@@ -842,7 +884,8 @@ int nbp_dw_fwd_slab_rows(int B, int H, int W, int C, int dtype) {
 
 int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
                        int H, int W, int C, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(t1 && wdw && bdw && t2 && g && pool_slab && B > 0 && H > 0 && W > 0, "nbp_dw_sg_pool_fwd: bad args");
+  NBP_REQUIRE(t1 && wdw && bdw && g && pool_slab && B > 0 && H > 0 && W > 0, "nbp_dw_sg_pool_fwd: bad args");
+  NBP_REQUIRE(t2 || dw_tiled_ok(C, dtype), "nbp_dw_sg_pool_fwd: t2 may be NULL only on the tiled path (nbp_dw_tiled)");
   NBP_REQUIRE(C % 4 == 0 && C / 4 <= 1024, "nbp_dw_sg_pool_fwd: C");
   if (dw_tiled_ok(C, dtype)) {
     const int tw = dw_fwd_tw(W, dtype), hs = dtype == 1 ? 16 : 8;
@@ -919,15 +962,15 @@ int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* 
 }
 
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
-  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * dw_tiles(H, W);
+  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * dw_tiles(H, W, true);
   return (a > t ? a : t) * 2 * C * 10;
 }
 
 int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws,
                int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dt2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && C % 2 == 0, "nbp_dw_bwd: bad args");
-  if (dw_tiled_ok(C, dtype)) return launch_dw_tiled(dt2, nullptr, nullptr, nullptr, nullptr, t1, wdw, dt1, dwdw, dbdw, ws,
-                                                     B, H, W, C, dtype, s);
+  if (dw_tiled_ok(C, dtype)) return launch_dw_tiled(dt2, nullptr, nullptr, nullptr, nullptr, t1, wdw, nullptr, dt1, dwdw,
+                                                     dbdw, ws, B, H, W, C, dtype, s);
   const int Q = C / 2;  // quads over 2C channels
   NBP_REQUIRE(Q <= 1024, "nbp_dw_bwd: too many channels");
   const int blk = block_for_quads(Q);
@@ -954,7 +997,19 @@ int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const voi
   NBP_REQUIRE(dh && a && ds && t2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
               "nbp_sca_sg_dw_bwd: bad args");
   NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd: C must be a multiple of %d", dtype == 1 ? 16 : 8);
-  return launch_dw_tiled(nullptr, dh, a, ds, t2, t1, wdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
+  NBP_REQUIRE(t2, "nbp_sca_sg_dw_bwd: t2 required (nbp_sca_sg_dw_bwd_rec recomputes it)");
+  return launch_dw_tiled(nullptr, dh, a, ds, t2, t1, wdw, nullptr, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
+}
+
+int nbp_dw_tiled(int C, int dtype) { return dw_tiled_ok(C, dtype) ? 1 : 0; }
+
+int nbp_sca_sg_dw_bwd_rec(const void* dh, const float* a, const float* ds, const void* t1, const float* wdw,
+                          const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C,
+                          int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dh && a && ds && t1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
+              "nbp_sca_sg_dw_bwd_rec: bad args");
+  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd_rec: C must be a multiple of %d", dtype == 1 ? 16 : 8);
+  return launch_dw_tiled(nullptr, dh, a, ds, nullptr, t1, wdw, bdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
 }
 
 }  // extern "C"

@@ -93,6 +93,7 @@ class NAFNet(nn.Module):
         # weight gradients on a side stream (joined at each stage flush), NBP_OVERLAP_WGRAD=1.  Off by default:
         # measured slower on MI355X at cfg2 (803.8 -> 759.6 img/s graph, 808.9 -> 791.8 eager; scripts/ab_overlap.sh)
         self.overlap_wgrad = os.environ.get("NBP_OVERLAP_WGRAD", "0") == "1"
+        self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
         # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
@@ -352,7 +353,10 @@ class NAFNet(nn.Module):
         self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv1.bias"))
         chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
-        t2, g, pool = E(M, 2 * c), E(M, c), F(B * chunks * c)
+        # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec).  Off by default:
+        # measured slower at cfg2 (L0 dw backward 138 -> 211 us vs 25 us saved in the forward; profiles/r01_v9)
+        rec = self.dw_rec and query("dw_tiled", c, dt) == 1
+        t2, g, pool = (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
         call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2, g,
              pool, B, h, w, c, dt)
         mean, a = F(B, c), F(B, c)
@@ -590,7 +594,11 @@ class NAFNet(nn.Module):
         ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
         dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
                    self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        if c % (16 if dt == 1 else 8) == 0:
+        if S["t2"] is None:
+            call("sca_sg_dw_bwd_rec", dh, S["a"], ds, S["t1"], self._slice(P, pre + "conv2.weight"),
+                 self._slice(P, pre + "conv2.bias"), dt1, self._slice(dflat, pre + "conv2.weight"),
+                 self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
+        elif c % (16 if dt == 1 else 8) == 0:
             call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
         else:
             dt2 = E(M, 2 * c)
