@@ -676,8 +676,9 @@ void dispatch(const GemmPB& p, hipStream_t st) {
   auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
   const bool n128 = p.N > 64, m128 = p.M > 64;
   const long mb = gemm_minblk();
-  // 128 x 128 already at >= 512 blocks (measured per shape, scripts/gemm_micro.py: M 16K-64K, N 128-512)
-  if (m128 && n128 && blocks(128, 128) >= mb / 2) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
+  // (128 x 128 from 512 blocks won in isolation on M 16K-64K shapes, scripts/gemm_micro.py, but lost 0.3 ms/step in
+  // the training step: kept at >= 1024 blocks)
+  if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
   else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
   else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
   else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);

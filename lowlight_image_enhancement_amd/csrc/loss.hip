@@ -63,14 +63,15 @@ __global__ void finalize_mean(const double* __restrict__ partial, int n, double 
 }
 
 // pass 1: horizontal filter of {x, y, x^2, y^2, xy} (clamped inputs) into h[5][plane][H][W]
+// (all SSIM kernels: planes * H * W < 2^31, checked on the host: 32-bit index arithmetic, 64-bit map offsets)
 __global__ void ssim_h(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ hbuf, long planes,
                        int H, int W, int clamp_in, Win win) {
-  const long total = planes * H * W;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  const int total = (int)(planes * H * W);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int w = i % W;
-    const long row = i / W;
-    const float* xr = x + row * W;
-    const float* yr = y + row * W;
+    const int row = i / W;
+    const float* xr = x + (long)row * W;
+    const float* yr = y + (long)row * W;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
 #pragma unroll
     for (int t = 0; t < 11; ++t) {
@@ -84,11 +85,12 @@ __global__ void ssim_h(const float* __restrict__ x, const float* __restrict__ y,
       s3 = fmaf(k, yv * yv, s3);
       s4 = fmaf(k, xv * yv, s4);
     }
+    const long tl = total;
     hbuf[i] = s0;
-    hbuf[total + i] = s1;
-    hbuf[2 * total + i] = s2;
-    hbuf[3 * total + i] = s3;
-    hbuf[4 * total + i] = s4;
+    hbuf[tl + i] = s1;
+    hbuf[2 * tl + i] = s2;
+    hbuf[3 * tl + i] = s3;
+    hbuf[4 * tl + i] = s4;
   }
 }
 
@@ -97,19 +99,20 @@ __global__ void ssim_h(const float* __restrict__ x, const float* __restrict__ y,
 __global__ void ssim_v(const float* __restrict__ hbuf, long planes, int H, int W, Win win, float C1, float C2, float eps,
                        float inv_n, double* __restrict__ partial, float* __restrict__ coef) {
   __shared__ double red[16];
-  const long total = planes * H * W;
+  const int total = (int)(planes * H * W);
+  const long tl = total;
   double s = 0.0;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W;
-    const int h = (i / W) % H;
-    const long plane = i / ((long)H * W);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W;
+    const int h = hw % H;
+    const int plane = hw / H;
     float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 11; ++t) {
-      const long o = (plane * H + refl(h + t - 5, H)) * W + w;
+      const int o = (plane * H + refl(h + t - 5, H)) * W + w;
       const float k = win.k[t];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) v[j] = fmaf(k, hbuf[j * total + o], v[j]);
+      for (int j = 0; j < 5; ++j) v[j] = fmaf(k, hbuf[j * tl + o], v[j]);
     }
     const float mx = v[0], my = v[1];
     const float mx2 = mx * mx, my2 = my * my, mxy = mx * my;
@@ -127,8 +130,8 @@ __global__ void ssim_v(const float* __restrict__ hbuf, long planes, int H, int W
       const float dxx = -S * B1 / D;
       const float dxy = 2.f * A1 / D;
       coef[i] = dS * dmx;
-      coef[total + i] = dS * dxx;
-      coef[2 * total + i] = dS * dxy;
+      coef[tl + i] = dS * dxx;
+      coef[2 * tl + i] = dS * dxy;
     }
   }
   s = block_sum_d(s, red);
@@ -137,11 +140,12 @@ __global__ void ssim_v(const float* __restrict__ hbuf, long planes, int H, int W
 
 // adjoint of one reflect-padded 1-D pass along rows (vertical) for three maps: out[j] = sum_{q->j} sum_t k[t] in[q-t+5]
 __global__ void ssim_vT(const float* __restrict__ coef, float* __restrict__ tbuf, long planes, int H, int W, Win win) {
-  const long total = planes * H * W;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W;
-    const int j = (i / W) % H;
-    const long plane = i / ((long)H * W);
+  const int total = (int)(planes * H * W);
+  const long tl = total;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W;
+    const int j = hw % H;
+    const int plane = hw / H;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     int qs[3];
     int nq = 0;
@@ -154,16 +158,16 @@ __global__ void ssim_vT(const float* __restrict__ coef, float* __restrict__ tbuf
       for (int t = 0; t < 11; ++t) {
         const int r = q - t + 5;
         if (r < 0 || r >= H) continue;
-        const long o = (plane * H + r) * W + w;
+        const int o = (plane * H + r) * W + w;
         const float k = win.k[t];
         a0 = fmaf(k, coef[o], a0);
-        a1 = fmaf(k, coef[total + o], a1);
-        a2 = fmaf(k, coef[2 * total + o], a2);
+        a1 = fmaf(k, coef[tl + o], a1);
+        a2 = fmaf(k, coef[2 * tl + o], a2);
       }
     }
     tbuf[i] = a0;
-    tbuf[total + i] = a1;
-    tbuf[2 * total + i] = a2;
+    tbuf[tl + i] = a1;
+    tbuf[2 * tl + i] = a2;
   }
 }
 
@@ -171,11 +175,12 @@ __global__ void ssim_vT(const float* __restrict__ coef, float* __restrict__ tbuf
 __global__ void ssim_hT(const float* __restrict__ tbuf, const float* __restrict__ x, const float* __restrict__ y,
                         long planes, int H, int W, Win win, int clamp_in, const float* __restrict__ up,
                         float* __restrict__ gx) {
-  const long total = planes * H * W;
+  const int total = (int)(planes * H * W);
+  const long tl = total;
   const float g0 = up[0];
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int j = i % W;
-    const long row = i / W;
+    const int row = i / W;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     int qs[3];
     int nq = 0;
@@ -188,11 +193,11 @@ __global__ void ssim_hT(const float* __restrict__ tbuf, const float* __restrict_
       for (int t = 0; t < 11; ++t) {
         const int c = q - t + 5;
         if (c < 0 || c >= W) continue;
-        const long o = row * W + c;
+        const int o = row * W + c;
         const float k = win.k[t];
         a0 = fmaf(k, tbuf[o], a0);
-        a1 = fmaf(k, tbuf[total + o], a1);
-        a2 = fmaf(k, tbuf[2 * total + o], a2);
+        a1 = fmaf(k, tbuf[tl + o], a1);
+        a2 = fmaf(k, tbuf[2 * tl + o], a2);
       }
     }
     const float xr = x[i];
@@ -252,6 +257,7 @@ int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W
   NBP_REQUIRE(x && y && ws && loss && N > 0 && C > 0, "nbp_ssim_loss_fwd: bad args");
   NBP_REQUIRE(window == 11, "nbp_ssim_loss_fwd: only the 11-tap window (SSIMLoss default) is implemented");
   NBP_REQUIRE(H > 5 && W > 5, "nbp_ssim_loss_fwd: reflect padding needs H, W > 5");
+  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "nbp_ssim_loss_fwd: N*C*H*W must be < 2^31");
   const long planes = (long)N * C, n = planes * H * W;
   const Win win = make_window(11, 1.5f);
   float* hbuf = ws;
@@ -270,6 +276,7 @@ int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W
 int nbp_ssim_loss_bwd(const float* x, const float* y, int N, int C, int H, int W, int clamp_in, const float* up,
                       float* ws, float* gx, nbp_stream_t s) {
   NBP_REQUIRE(x && y && ws && up && gx && N > 0 && C > 0 && H > 5 && W > 5, "nbp_ssim_loss_bwd: bad args");
+  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "nbp_ssim_loss_bwd: N*C*H*W must be < 2^31");
   const long planes = (long)N * C, n = planes * H * W;
   const Win win = make_window(11, 1.5f);
   float* tbuf = ws;  // reuse the filtered-map space

@@ -35,12 +35,12 @@ __device__ __forceinline__ void rep_range(int p, int d, int n, int& lo, int& hi)
 template <int PAD>
 __global__ void dw_conv_fwd(const float* __restrict__ x, const float* __restrict__ k, int k_shared, float* __restrict__ y,
                             int N, int C, int H, int W, int KH, int KW, int pre_clamp) {
-  const long total = (long)N * C * H * W;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W, h = (i / W) % H;
-    const long plane = i / ((long)H * W);
+  const int total = N * C * H * W;  // < 2^31 (host check): 32-bit index arithmetic
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W, h = hw % H;
+    const int plane = hw / H;
     const int c = plane % C;
-    const float* xp = x + plane * H * W;
+    const float* xp = x + (long)plane * H * W;
     const float* kc = k + (k_shared ? 0 : (long)c * KH * KW);
     float acc = 0.f;
     for (int a = 0; a < KH; ++a) {
@@ -66,12 +66,12 @@ __global__ void dw_conv_fwd(const float* __restrict__ x, const float* __restrict
 // adjoint of the zero-padded depthwise conv: gx(p) = sum_t k[t] * gy(p - (t - K/2))
 __global__ void dw_conv_bwd_zero(const float* __restrict__ gy, const float* __restrict__ k, int k_shared,
                                  float* __restrict__ gx, int N, int C, int H, int W, int KH, int KW) {
-  const long total = (long)N * C * H * W;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W, h = (i / W) % H;
-    const long plane = i / ((long)H * W);
+  const int total = N * C * H * W;  // < 2^31 (host check): 32-bit index arithmetic
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W, h = hw % H;
+    const int plane = hw / H;
     const int c = plane % C;
-    const float* gp = gy + plane * H * W;
+    const float* gp = gy + (long)plane * H * W;
     const float* kc = k + (k_shared ? 0 : (long)c * KH * KW);
     float acc = 0.f;
     for (int a = 0; a < KH; ++a) {
@@ -96,13 +96,13 @@ __global__ void phys_l1_fwd(const float* __restrict__ bhat, const float* __restr
                             int KW, int clamp_bhat, int clamp_a_in, int clamp_align, double* __restrict__ partial,
                             float* __restrict__ sign_map) {
   __shared__ double red[16];
-  const long total = (long)N * C * H * W;
+  const int total = N * C * H * W;  // < 2^31 (host check): 32-bit index arithmetic
   double s = 0.0;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W, h = (i / W) % H;
-    const long plane = i / ((long)H * W);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W, h = hw % H;
+    const int plane = hw / H;
     const int c = plane % C;
-    const float* xp = bhat + plane * H * W;
+    const float* xp = bhat + (long)plane * H * W;
     const float* kc = k + (k_shared ? 0 : (long)c * KH * KW);
     float y = 0.f;
     for (int aa = 0; aa < KH; ++aa) {
@@ -138,13 +138,13 @@ template <int PAD>
 __global__ void phys_l1_bwd(const float* __restrict__ sign_map, const float* __restrict__ bhat,
                             const float* __restrict__ k, int k_shared, const float* __restrict__ up, float scale,
                             int N, int C, int H, int W, int KH, int KW, int clamp_bhat, float* __restrict__ gx) {
-  const long total = (long)N * C * H * W;
+  const int total = N * C * H * W;  // < 2^31 (host check): 32-bit index arithmetic
   const float g0 = up[0] * scale;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int w = i % W, h = (i / W) % H;
-    const long plane = i / ((long)H * W);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W, h = hw % H;
+    const int plane = hw / H;
     const int c = plane % C;
-    const float* sp = sign_map + plane * H * W;
+    const float* sp = sign_map + (long)plane * H * W;
     const float* kc = k + (k_shared ? 0 : (long)c * KH * KW);
     float acc = 0.f;
     if (PAD == 0) {
@@ -306,6 +306,7 @@ int nbp_psf_normalize_host(const float* k, int n_kernels, int len, float* out) {
 int nbp_dwconv_nchw_fwd(const float* x, const float* k, int k_shared, float* y, int N, int C, int H, int W, int KH,
                         int KW, int pad_mode, int pre_clamp, nbp_stream_t s) {
   NBP_REQUIRE(x && k && y && N > 0 && C > 0 && H > 0 && W > 0 && (KH & 1) && (KW & 1), "nbp_dwconv_nchw_fwd: bad args");
+  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
   NBP_REQUIRE(pad_mode >= 0 && pad_mode <= 2, "nbp_dwconv_nchw_fwd: pad_mode");
   NBP_REQUIRE(pad_mode != 2 || (KH / 2 < H && KW / 2 < W), "reflect padding needs pad < size");
   const long total = (long)N * C * H * W;
@@ -318,6 +319,7 @@ int nbp_dwconv_nchw_fwd(const float* x, const float* k, int k_shared, float* y, 
 int nbp_dwconv_nchw_bwd_zero(const float* gy, const float* k, int k_shared, float* gx, int N, int C, int H, int W,
                              int KH, int KW, nbp_stream_t s) {
   NBP_REQUIRE(gy && k && gx && N > 0 && C > 0 && H > 0 && W > 0 && (KH & 1) && (KW & 1), "nbp_dwconv_nchw_bwd_zero: bad args");
+  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
   const long total = (long)N * C * H * W;
   dw_conv_bwd_zero<<<grid_for(total), kBlk, 0, S(s)>>>(gy, k, k_shared, gx, N, C, H, W, KH, KW);
   return check_launch("dw_conv_bwd_zero");
@@ -332,6 +334,7 @@ int nbp_phys_l1_fwd(const float* bhat, const float* a, const float* ratio, int r
                     int clamp_align, double* ws, float* loss, float* sign_map, nbp_stream_t s) {
   NBP_REQUIRE(bhat && a && ratio && k && ws && loss && N > 0 && C > 0 && H > 0 && W > 0, "nbp_phys_l1_fwd: bad args");
   NBP_REQUIRE((KH & 1) && (KW & 1) && (pad_mode == 0 || pad_mode == 1), "nbp_phys_l1_fwd: kernel/pad");
+  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
   const long total = (long)N * C * H * W;
   const int g = grid_for(total);
   if (pad_mode == 0)
@@ -348,6 +351,7 @@ int nbp_phys_l1_bwd(const float* sign_map, const float* bhat, const float* k, in
                     int C, int H, int W, int KH, int KW, int pad_mode, int clamp_bhat, float* gx, nbp_stream_t s) {
   NBP_REQUIRE(sign_map && k && up && gx && (!clamp_bhat || bhat), "nbp_phys_l1_bwd: bad args");
   NBP_REQUIRE(pad_mode == 0 || pad_mode == 1, "nbp_phys_l1_bwd: pad");
+  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
   const long total = (long)N * C * H * W;
   const float scale = (float)(1.0 / (double)total);
   if (pad_mode == 0)

@@ -92,7 +92,9 @@ class NAFNet(nn.Module):
         self._keep: Optional[List[torch.Tensor]] = None  # slabs awaiting a deferred gradient reduction
         # weight gradients on a side stream (joined at each stage flush), NBP_OVERLAP_WGRAD=1.  Off by default:
         # measured slower on MI355X at cfg2 (803.8 -> 759.6 img/s graph, 808.9 -> 791.8 eager; scripts/ab_overlap.sh)
-        self.overlap_wgrad = os.environ.get("NBP_OVERLAP_WGRAD", "0") == "1"
+        # 2: side stream for the weight gradients and ONE join + reduction flush at the end of the backward (only
+        # when no per-stage hook needs the gradient slices early, i.e. single-GPU)
+        self.overlap_wgrad = int(os.environ.get("NBP_OVERLAP_WGRAD", "0"))
         self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
@@ -489,6 +491,8 @@ class NAFNet(nn.Module):
         return st
 
     def _stage_done(self, name, hook):
+        if self.overlap_wgrad == 2 and hook is None:
+            return  # everything is joined and flushed once at the end of exec_backward
         # join the wgrad side stream, then the stage's queued gradient reductions run before anyone (the DP
         # all-reduce hook) reads its slice
         if self._side_used:
