@@ -62,57 +62,77 @@ __global__ void finalize_mean(const double* __restrict__ partial, int n, double 
   if (threadIdx.x == 0) out[0] = (float)(s * scale);
 }
 
-// pass 1: horizontal filter of {x, y, x^2, y^2, xy} (clamped inputs) into h[5][plane][H][W]
-// (all SSIM kernels: planes * H * W < 2^31, checked on the host: 32-bit index arithmetic, 64-bit map offsets)
-__global__ void ssim_h(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ hbuf, long planes,
-                       int H, int W, int clamp_in, Win win) {
-  const int total = (int)(planes * H * W);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int w = i % W;
-    const int row = i / W;
-    const float* xr = x + (long)row * W;
-    const float* yr = y + (long)row * W;
+// ---------------------------------------------------------------- SSIM, LDS-tiled (one launch forward, one backward)
+// Forward: a TH x TW output tile of one plane.  x, y (clamped) are staged with a 5-pixel halo at reflected
+// coordinates (reflect padding = the reflected pixel itself), the horizontal 11-tap pass of {x, y, x^2, y^2, xy}
+// runs LDS -> LDS, the vertical pass LDS -> registers, then the SSIM map, the per-block loss partial and the three
+// gradient-coefficient maps (the only global writes).  Every input pixel is read from HBM once (+halo).
+constexpr int SS_TH = 32, SS_TW = 64, SS_R = 5;
+
+__global__ __launch_bounds__(256) void ssim_fwd_tiled(const float* __restrict__ x, const float* __restrict__ y, int H,
+                                                       int W, int clamp_in, Win win, float C1, float C2, float eps,
+                                                       float inv_n, double* __restrict__ partial,
+                                                       float* __restrict__ coef, long n) {
+  constexpr int LH = SS_TH + 2 * SS_R, LW = SS_TW + 2 * SS_R;
+  __shared__ float xs[LH][LW + 1], ys[LH][LW + 1];
+  __shared__ float hm[5][LH][SS_TW + 1];
+  __shared__ double red[16];
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * SS_TW, y0 = blockIdx.y * SS_TH;
+  const long plane = blockIdx.z;
+  const float* xp = x + plane * H * W;
+  const float* yp = y + plane * H * W;
+  // staging in batches of 4 positions per thread: all 8 loads issued before the LDS stores
+  for (int e0 = tid; e0 < LH * LW; e0 += 4 * 256) {
+    float xv[4], yv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      const int r = e / LW, c = e % LW;
+      const int gy = y0 - SS_R + r, gx = x0 - SS_R + c;
+      xv[u] = yv[u] = 0.f;
+      if (e < LH * LW && gy < H + SS_R && gx < W + SS_R) {  // positions further out feed no valid output
+        const long o = (long)refl(gy, H) * W + refl(gx, W);
+        xv[u] = xp[o];
+        yv[u] = yp[o];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      if (e >= LH * LW) break;
+      const int r = e / LW, c = e % LW;
+      xs[r][c] = clamp_in ? clamp01(xv[u]) : xv[u];
+      ys[r][c] = clamp_in ? clamp01(yv[u]) : yv[u];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < LH * SS_TW; e += 256) {
+    const int r = e / SS_TW, c = e % SS_TW;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
 #pragma unroll
     for (int t = 0; t < 11; ++t) {
-      const int c = refl(w + t - 5, W);
-      float xv = xr[c], yv = yr[c];
-      if (clamp_in) { xv = clamp01(xv); yv = clamp01(yv); }
-      const float k = win.k[t];
+      const float xv = xs[r][c + t], yv = ys[r][c + t], k = win.k[t];
       s0 = fmaf(k, xv, s0);
       s1 = fmaf(k, yv, s1);
       s2 = fmaf(k, xv * xv, s2);
       s3 = fmaf(k, yv * yv, s3);
       s4 = fmaf(k, xv * yv, s4);
     }
-    const long tl = total;
-    hbuf[i] = s0;
-    hbuf[tl + i] = s1;
-    hbuf[2 * tl + i] = s2;
-    hbuf[3 * tl + i] = s3;
-    hbuf[4 * tl + i] = s4;
+    hm[0][r][c] = s0; hm[1][r][c] = s1; hm[2][r][c] = s2; hm[3][r][c] = s3; hm[4][r][c] = s4;
   }
-}
-
-// pass 2: vertical filter -> ssim map -> loss partials and the three gradient coefficient maps
-//   gm = dL/dmu_x, gxx = dL/dE[x^2], gxy = dL/dE[xy]   (dL/dS = -0.5 * inv_n inside the clamp window)
-__global__ void ssim_v(const float* __restrict__ hbuf, long planes, int H, int W, Win win, float C1, float C2, float eps,
-                       float inv_n, double* __restrict__ partial, float* __restrict__ coef) {
-  __shared__ double red[16];
-  const int total = (int)(planes * H * W);
-  const long tl = total;
-  double s = 0.0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int w = i % W, hw = i / W;
-    const int h = hw % H;
-    const int plane = hw / H;
+  __syncthreads();
+  double sacc = 0.0;
+  for (int e = tid; e < SS_TH * SS_TW; e += 256) {
+    const int r = e / SS_TW, c = e % SS_TW;
+    const int gy = y0 + r, gx = x0 + c;
+    if (gy >= H || gx >= W) continue;
     float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 11; ++t) {
-      const int o = (plane * H + refl(h + t - 5, H)) * W + w;
       const float k = win.k[t];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) v[j] = fmaf(k, hbuf[j * tl + o], v[j]);
+      for (int m = 0; m < 5; ++m) v[m] = fmaf(k, hm[m][r + t][c], v[m]);
     }
     const float mx = v[0], my = v[1];
     const float mx2 = mx * mx, my2 = my * my, mxy = mx * my;
@@ -122,90 +142,157 @@ __global__ void ssim_v(const float* __restrict__ hbuf, long planes, int H, int W
     const float num = A1 * A2, D = B1 * B2 + eps;
     const float S = num / D;
     const float l = (1.f - S) / 2.f;
-    s += fminf(fmaxf(l, 0.f), 1.f);
+    sacc += fminf(fmaxf(l, 0.f), 1.f);
     if (coef) {
       const float dS = (l >= 0.f && l <= 1.f) ? -0.5f * inv_n : 0.f;
       // dnum/dmx = 2 my (A2 - A1); dden/dmx = 2 mx (B2 - B1); dS/dE[x^2] = -S B1 / D; dS/dE[xy] = 2 A1 / D
       const float dmx = (2.f * my * (A2 - A1) - S * 2.f * mx * (B2 - B1)) / D;
       const float dxx = -S * B1 / D;
       const float dxy = 2.f * A1 / D;
-      coef[i] = dS * dmx;
-      coef[tl + i] = dS * dxx;
-      coef[2 * tl + i] = dS * dxy;
+      const long o = (plane * H + gy) * W + gx;
+      coef[o] = dS * dmx;
+      coef[n + o] = dS * dxx;
+      coef[2 * n + o] = dS * dxy;
     }
   }
-  s = block_sum_d(s, red);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  sacc = block_sum_d(sacc, red);
+  if (tid == 0) partial[((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = sacc;
 }
 
-// adjoint of one reflect-padded 1-D pass along rows (vertical) for three maps: out[j] = sum_{q->j} sum_t k[t] in[q-t+5]
-__global__ void ssim_vT(const float* __restrict__ coef, float* __restrict__ tbuf, long planes, int H, int W, Win win) {
-  const int total = (int)(planes * H * W);
-  const long tl = total;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int w = i % W, hw = i / W;
-    const int j = hw % H;
-    const int plane = hw / H;
+// Backward: gx = F^T gm + 2 x F^T gxx + y F^T gxy with F = V . H the reflect-padded separable filter, so
+// F^T = H^T . V^T.  A TH x TW tile stages the three coefficient maps with a 5-pixel margin, applies the vertical
+// adjoint into LDS and the horizontal adjoint from LDS; 1-D adjoint of reflect padding: output j gathers
+// q in {j, -j (1 <= j <= 5), 2(n-1) - j (n-6 <= j <= n-2)}, taps q - t + 5 inside [0, n).  The reflected sources
+// stay inside the margin: -j only occurs in the first tile (TH > 5) and reads rows [0, 5 - j]; 2(n-1) - j reads
+// rows [n-5, n) with j >= y0.
+constexpr int SB_TH = 32, SB_TW = 64, SB_M = 5;
+
+__device__ __forceinline__ int refl_sources(int j, int n, int* qs) {
+  int nq = 0;
+  qs[nq++] = j;
+  if (j >= 1 && j <= 5) qs[nq++] = -j;
+  if (j <= n - 2 && j >= n - 6) qs[nq++] = 2 * (n - 1) - j;
+  return nq;
+}
+
+__global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ coef, const float* __restrict__ x,
+                                                       const float* __restrict__ y, int H, int W, Win win,
+                                                       int clamp_in, const float* __restrict__ up,
+                                                       float* __restrict__ gx, long n) {
+  constexpr int LH = SB_TH + 2 * SB_M, LW = SB_TW + 2 * SB_M;
+  __shared__ float cs[3][LH][LW + 1];
+  __shared__ float tv[3][SB_TH][LW + 1];
+  const int tid = threadIdx.x;
+  const int x0 = blockIdx.x * SB_TW, y0 = blockIdx.y * SB_TH;
+  const long plane = blockIdx.z;
+  const long pb = plane * H * W;
+  for (int e0 = tid; e0 < LH * LW; e0 += 4 * 256) {  // 12 loads in flight per thread, then the LDS stores
+    float v[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      const int r = e / LW, c = e % LW;
+      const int gy = y0 - SB_M + r, gxx = x0 - SB_M + c;
+      const bool in = e < LH * LW && gy >= 0 && gy < H && gxx >= 0 && gxx < W;
+      const long o = pb + (long)gy * W + gxx;
+#pragma unroll
+      for (int m = 0; m < 3; ++m) v[u][m] = in ? coef[m * n + o] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256;
+      if (e >= LH * LW) break;
+      const int r = e / LW, c = e % LW;
+#pragma unroll
+      for (int m = 0; m < 3; ++m) cs[m][r][c] = v[u][m];
+    }
+  }
+  // this thread's output pixels of x / y, loaded now so their latency overlaps the two adjoint passes
+  constexpr int PER = SB_TH * SB_TW / 256;
+  float xo[PER], yo[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + k * 256, r = e / SB_TW, c = e % SB_TW;
+    const int j = y0 + r, i = x0 + c;
+    const long o = pb + (long)j * W + i;
+    const bool ok = j < H && i < W;
+    xo[k] = ok ? x[o] : 0.f;
+    yo[k] = ok ? y[o] : 0.f;
+  }
+  __syncthreads();
+  // vertical adjoint for the tile's rows and every staged column
+  for (int e = tid; e < SB_TH * LW; e += 256) {
+    const int r = e / LW, c = e % LW;
+    const int j = y0 + r;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    int qs[3];
-    int nq = 0;
-    qs[nq++] = j;
-    if (j >= 1 && j <= 5) qs[nq++] = -j;
-    if (j <= H - 2 && j >= H - 6) qs[nq++] = 2 * (H - 1) - j;
-    for (int u = 0; u < nq; ++u) {
-      const int q = qs[u];
+    if (j >= 6 && j <= H - 7) {  // interior row: the plain 11-tap window, no reflected sources
+      const int lb = j - (y0 - SB_M) + 5;
 #pragma unroll
       for (int t = 0; t < 11; ++t) {
-        const int r = q - t + 5;
-        if (r < 0 || r >= H) continue;
-        const int o = (plane * H + r) * W + w;
         const float k = win.k[t];
-        a0 = fmaf(k, coef[o], a0);
-        a1 = fmaf(k, coef[tl + o], a1);
-        a2 = fmaf(k, coef[2 * tl + o], a2);
+        a0 = fmaf(k, cs[0][lb - t][c], a0);
+        a1 = fmaf(k, cs[1][lb - t][c], a1);
+        a2 = fmaf(k, cs[2][lb - t][c], a2);
+      }
+    } else if (j < H) {
+      int qs[3];
+      const int nq = refl_sources(j, H, qs);
+      for (int u = 0; u < nq; ++u) {
+#pragma unroll
+        for (int t = 0; t < 11; ++t) {
+          const int rr = qs[u] - t + 5;
+          if (rr < 0 || rr >= H) continue;
+          const int lr = rr - (y0 - SB_M);  // inside [0, LH) by the margin
+          const float k = win.k[t];
+          a0 = fmaf(k, cs[0][lr][c], a0);
+          a1 = fmaf(k, cs[1][lr][c], a1);
+          a2 = fmaf(k, cs[2][lr][c], a2);
+        }
       }
     }
-    tbuf[i] = a0;
-    tbuf[tl + i] = a1;
-    tbuf[2 * tl + i] = a2;
+    tv[0][r][c] = a0; tv[1][r][c] = a1; tv[2][r][c] = a2;
   }
-}
-
-// adjoint along columns, then combine: gx = F^T gm + 2 x F^T gxx + y F^T gxy  (x, y clamped; clamp mask on x)
-__global__ void ssim_hT(const float* __restrict__ tbuf, const float* __restrict__ x, const float* __restrict__ y,
-                        long planes, int H, int W, Win win, int clamp_in, const float* __restrict__ up,
-                        float* __restrict__ gx) {
-  const int total = (int)(planes * H * W);
-  const long tl = total;
+  __syncthreads();
   const float g0 = up[0];
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const int j = i % W;
-    const int row = i / W;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + k * 256;
+    const int r = e / SB_TW, c = e % SB_TW;
+    const int j = y0 + r, i = x0 + c;
+    if (j >= H || i >= W) continue;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    int qs[3];
-    int nq = 0;
-    qs[nq++] = j;
-    if (j >= 1 && j <= 5) qs[nq++] = -j;
-    if (j <= W - 2 && j >= W - 6) qs[nq++] = 2 * (W - 1) - j;
-    for (int u = 0; u < nq; ++u) {
-      const int q = qs[u];
+    if (i >= 6 && i <= W - 7) {  // interior column
+      const int lb = i - (x0 - SB_M) + 5;
 #pragma unroll
       for (int t = 0; t < 11; ++t) {
-        const int c = q - t + 5;
-        if (c < 0 || c >= W) continue;
-        const int o = row * W + c;
         const float k = win.k[t];
-        a0 = fmaf(k, tbuf[o], a0);
-        a1 = fmaf(k, tbuf[tl + o], a1);
-        a2 = fmaf(k, tbuf[2 * tl + o], a2);
+        a0 = fmaf(k, tv[0][r][lb - t], a0);
+        a1 = fmaf(k, tv[1][r][lb - t], a1);
+        a2 = fmaf(k, tv[2][r][lb - t], a2);
+      }
+    } else {
+    int qs[3];
+    const int nq = refl_sources(i, W, qs);
+    for (int u = 0; u < nq; ++u) {
+#pragma unroll
+      for (int t = 0; t < 11; ++t) {
+        const int cc = qs[u] - t + 5;
+        if (cc < 0 || cc >= W) continue;
+        const int lc = cc - (x0 - SB_M);
+        const float k = win.k[t];
+        a0 = fmaf(k, tv[0][r][lc], a0);
+        a1 = fmaf(k, tv[1][r][lc], a1);
+        a2 = fmaf(k, tv[2][r][lc], a2);
       }
     }
-    const float xr = x[i];
-    float xv = xr, yv = y[i];
+    }
+    const long o = pb + (long)j * W + i;
+    const float xr = xo[k];
+    float xv = xr, yv = yo[k];
     if (clamp_in) { xv = clamp01(xv); yv = clamp01(yv); }
     float g = a0 + 2.f * xv * a1 + yv * a2;
     if (clamp_in && !(xr >= 0.f && xr <= 1.f)) g = 0.f;
-    gx[i] = g0 * g;
+    gx[o] = g0 * g;
   }
 }
 
@@ -249,26 +336,25 @@ int nbp_pix_loss_bwd(const float* a, const float* b, long n, int mode, float eps
   return check_launch("pix_loss_bwd");
 }
 
-// ws: 5 * n floats (filtered maps) + 3 * n (coefficients) + grid doubles
-size_t nbp_ssim_workspace_floats(long n) { return (size_t)8 * n + 2 * (size_t)grid_for(n) + 2; }
+// ws: 3 * n floats (gradient coefficients) + one double per forward block (<= n blocks)
+size_t nbp_ssim_workspace_floats(long n) { return (size_t)5 * n + 4; }
 
 int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W, int window, float max_val,
                       int clamp_in, int want_grad, float* ws, float* loss, nbp_stream_t s) {
   NBP_REQUIRE(x && y && ws && loss && N > 0 && C > 0, "nbp_ssim_loss_fwd: bad args");
   NBP_REQUIRE(window == 11, "nbp_ssim_loss_fwd: only the 11-tap window (SSIMLoss default) is implemented");
   NBP_REQUIRE(H > 5 && W > 5, "nbp_ssim_loss_fwd: reflect padding needs H, W > 5");
-  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "nbp_ssim_loss_fwd: N*C*H*W must be < 2^31");
+  NBP_REQUIRE((long)N * C <= 65535, "nbp_ssim_loss_fwd: N*C <= 65535 planes");
   const long planes = (long)N * C, n = planes * H * W;
   const Win win = make_window(11, 1.5f);
-  float* hbuf = ws;
-  float* coef = ws + 5 * n;
-  double* partial = reinterpret_cast<double*>(ws + 8 * n + ((8 * n) & 1));
-  const int g = grid_for(n);
+  float* coef = ws;
+  double* partial = reinterpret_cast<double*>(ws + 3 * n + ((3 * n) & 1));
+  const dim3 g(cdiv(W, SS_TW), cdiv(H, SS_TH), (unsigned)planes);
+  const int nb = (int)(g.x * g.y * g.z);
   const float C1 = (0.01f * max_val) * (0.01f * max_val), C2 = (0.03f * max_val) * (0.03f * max_val);
-  ssim_h<<<g, 256, 0, S(s)>>>(x, y, hbuf, planes, H, W, clamp_in, win);
-  ssim_v<<<g, 256, 0, S(s)>>>(hbuf, planes, H, W, win, C1, C2, 1e-12f, (float)(1.0 / (double)n), partial,
-                               want_grad ? coef : nullptr);
-  finalize_mean<<<1, 256, 0, S(s)>>>(partial, g, 1.0 / (double)n, loss);
+  ssim_fwd_tiled<<<g, 256, 0, S(s)>>>(x, y, H, W, clamp_in, win, C1, C2, 1e-12f, (float)(1.0 / (double)n), partial,
+                                      want_grad ? coef : nullptr, n);
+  finalize_mean<<<1, 256, 0, S(s)>>>(partial, nb, 1.0 / (double)n, loss);
   return check_launch("ssim_loss_fwd");
 }
 
@@ -276,14 +362,11 @@ int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W
 int nbp_ssim_loss_bwd(const float* x, const float* y, int N, int C, int H, int W, int clamp_in, const float* up,
                       float* ws, float* gx, nbp_stream_t s) {
   NBP_REQUIRE(x && y && ws && up && gx && N > 0 && C > 0 && H > 5 && W > 5, "nbp_ssim_loss_bwd: bad args");
-  NBP_REQUIRE((long)N * C * H * W < (1L << 31), "nbp_ssim_loss_bwd: N*C*H*W must be < 2^31");
+  NBP_REQUIRE((long)N * C <= 65535, "nbp_ssim_loss_bwd: N*C <= 65535 planes");
   const long planes = (long)N * C, n = planes * H * W;
   const Win win = make_window(11, 1.5f);
-  float* tbuf = ws;  // reuse the filtered-map space
-  const float* coef = ws + 5 * n;
-  const int g = grid_for(n);
-  ssim_vT<<<g, 256, 0, S(s)>>>(coef, tbuf, planes, H, W, win);
-  ssim_hT<<<g, 256, 0, S(s)>>>(tbuf, x, y, planes, H, W, win, clamp_in, up, gx);
+  const dim3 g(cdiv(W, SB_TW), cdiv(H, SB_TH), (unsigned)planes);
+  ssim_bwd_tiled<<<g, 256, 0, S(s)>>>(ws, x, y, H, W, win, clamp_in, up, gx, n);
   return check_launch("ssim_loss_bwd");
 }
 

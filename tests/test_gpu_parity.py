@@ -115,12 +115,13 @@ def test_phys_cons_validation_errors(dev):
 
 
 # ---------------------------------------------------------------- loss terms vs the oracle (torch fp32 on the GPU)
-def test_l1_charbonnier_ssim_against_oracle(dev):
+@pytest.mark.parametrize("shape", [(2, 3, 37, 29), (1, 3, 70, 133)])  # one tile / several tiles each way
+def test_l1_charbonnier_ssim_against_oracle(dev, shape):
     from lowlight_image_enhancement_amd.NewBP_model import losses as HL
     from oracle import losses as OL
     gen = torch.Generator(device=dev).manual_seed(5)
-    a = (torch.rand(2, 3, 37, 29, device=dev, generator=gen) * 1.2 - 0.1)
-    b = torch.rand(2, 3, 37, 29, device=dev, generator=gen)
+    a = (torch.rand(*shape, device=dev, generator=gen) * 1.2 - 0.1)
+    b = torch.rand(*shape, device=dev, generator=gen)
     for mine_fn, ref_fn in ((HL.l1_loss, OL.l1), (HL.charbonnier_loss, OL.charbonnier),
                             (HL.SSIMLoss(), OL.ssim_loss)):
         x1 = a.clone().requires_grad_(True)
