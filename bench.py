@@ -205,8 +205,14 @@ def main():
     net._block_fwd, net._block_bwd = timed(orig_fwd, "fwd"), timed(orig_bwd, "bwd")
 
     # profiled pass: K eager steps with per-kernel HIP events on the launch stream (graph replays cannot carry them)
+    step_events = []
     for _ in range(args.steps):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
         tr.step(lq, gt, short, ratio)
+        e1.record()
+        step_events.append((e0, e1))
     torch.cuda.synchronize()
     _lib.PROFILE.clear()
     net._block_fwd, net._block_bwd = orig_fwd, orig_bwd
@@ -258,6 +264,7 @@ def main():
                  "flop_intensity": round(fl / max(by, 1), 2), "tflops": round(tflops, 2),
                  "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in classes.items()}})
     blk_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in blk_events) / args.steps
+    eager_step_ms = sum(e0.elapsed_time(e1) for e0, e1 in step_events) / args.steps
     per_level = {}
     for e0, e1, kind, lvl in blk_events:
         d = per_level.setdefault(lvl, {"blocks_fwd": 0, "fwd_ms": 0.0, "bwd_ms": 0.0})
@@ -268,7 +275,13 @@ def main():
         d["blocks_fwd"] //= args.steps
         d["fwd_ms"], d["bwd_ms"] = round(d["fwd_ms"], 3), round(d["bwd_ms"], 3)
     blk_bytes = nafblock_bytes(net, BATCH, IMG, IMG)
-    blk_gbps = blk_bytes / (blk_ms * 1e-3) / 1e9
+    # The eager per-block events include host-dispatch stalls at the small levels (the GPU outruns the launches
+    # there); the NAFBlock GPU time is the timed step minus the non-NAFBlock part of the eager step (boundary convs,
+    # down/up, loss head, optimizer: few large kernels, not dispatch-bound).
+    step_ms_timed = elapsed / args.steps * 1e3
+    nonblock_ms = max(eager_step_ms - blk_ms, 0.0)
+    blk_ms_gpu = max(step_ms_timed - nonblock_ms, 1e-6)
+    blk_gbps = blk_bytes / (blk_ms_gpu * 1e-3) / 1e9
 
     if rank == 0:
         step_ms = elapsed / args.steps * 1e3
@@ -289,7 +302,9 @@ def main():
                        "global_batch": BATCH * world, "image": IMG, "parallelism": f"dp{world}",
                        "launch": "hip-graph replay" if use_graph else "eager"},
             "roofline": roof,
-            "nafblock_roofline": {"bytes_per_step": blk_bytes, "ms_per_step": round(blk_ms, 3),
+            "nafblock_roofline": {"bytes_per_step": blk_bytes, "ms_per_step": round(blk_ms_gpu, 3),
+                                  "ms_method": "timed step - non-NAFBlock part of the eager step",
+                                  "eager_blocks_ms_per_step": round(blk_ms, 3),
                                   "per_level_eager": per_level,
                                   "achieved_GBps": round(blk_gbps, 1), "peak_GBps": HBM_PEAK_GBPS,
                                   "frac": round(blk_gbps / HBM_PEAK_GBPS, 4)},

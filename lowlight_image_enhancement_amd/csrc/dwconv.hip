@@ -98,9 +98,7 @@ __global__ __launch_bounds__(256) void reduce_rows8(const float* __restrict__ sl
   if (j == 0 && e < B * C) out[e] = acc * scale;
 }
 
-// SCA 1x1 conv on the pooled vector: a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
-// 16 waves per block, one output o per wave; the means of SCA_NB images are staged in LDS (a few loads per thread),
-// the W row read once for all of them.
+// images per block of the unfused SCA backward (sca_bwd_ds)
 constexpr int SCA_NB = 16;
 
 // sum_{k < chunks} slab[b][k][c] with 4 independent accumulators, fixed order (the pooled / reduced vector element)
@@ -118,41 +116,104 @@ __device__ __forceinline__ float chunk_sum(const float* __restrict__ slab, int c
   return (a0 + a1) + (a2 + a3);
 }
 
-// One launch for the SCA forward: every block reduces the pool slab of SCA_NB images into LDS (mean = sum / HW; block
-// 0 also stores it for the backward), then one wave per output o forms a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
-__global__ __launch_bounds__(1024) void sca_gemv(const float* __restrict__ pool, int chunks, float inv_hw,
-                                                 float* __restrict__ mean_out, const float* __restrict__ wsca,
-                                                 const float* __restrict__ bsca, float* __restrict__ a_out, int B,
-                                                 int C) {
-  extern __shared__ float sm[];  // [SCA_NB][C]
+// Stage sm[e] = scale * sum_{k < chunks} slab[b0 + e / CW][k][c0 + e % CW] for e < nE with the loads batched (16 in flight
+// per thread: 4 elements x 4 chunks).  When the block has more threads than elements, SP = blockDim / nE (a power of
+// two) threads share an element's chunks (thread s of it sums k = s, s + SP, ...) and the SP partials are added in
+// fixed order through `part` (>= blockDim floats).  Fixed summation order throughout.
+__device__ __forceinline__ void stage_chunk_sums(const float* __restrict__ slab, int chunks, int C, int b0, int c0,
+                                                 int CW, int nE, float scale, float* __restrict__ sm,
+                                                 float* __restrict__ part) {
+  const int nt = blockDim.x, t = threadIdx.x;
+  int sp = 1;
+  while (sp * 2 * nE <= nt && sp * 2 <= chunks) sp *= 2;
+  if (sp == 1) {
+    for (int e0 = t; e0 < nE; e0 += 4 * nt) {
+      const float* src[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = min(e0 + u * nt, nE - 1), bb = e / CW, c = c0 + e - bb * CW;
+        src[u] = slab + (long)(b0 + bb) * chunks * C + c;
+      }
+      float a[4][4] = {};
+      for (int k = 0; k < chunks; k += 4) {  // chunk k + q into accumulator q (the tail group guarded, not serial)
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] = k + q < chunks ? src[u][(long)(k + q) * C] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a[u][q] += v[u][q];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (e0 + u * nt < nE) sm[e0 + u * nt] = ((a[u][0] + a[u][1]) + (a[u][2] + a[u][3])) * scale;
+    }
+    return;
+  }
+  // sp > 1: one (element, share) per thread
+  const int e = t % nE, sh = t / nE;
+  if (sh < sp) {
+    const int bb = e / CW, c = c0 + e - bb * CW;
+    const float* src = slab + (long)(b0 + bb) * chunks * C + c;
+    float a[4] = {};
+    for (int k = sh; k < chunks; k += 4 * sp) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = k + q * sp < chunks ? src[(long)(k + q * sp) * C] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += v[q];
+    }
+    part[sh * nE + e] = (a[0] + a[1]) + (a[2] + a[3]);
+  }
+  __syncthreads();
+  if (t < nE) {
+    float v = 0.f;
+    for (int j = 0; j < sp; ++j) v += part[j * nE + t];
+    sm[t] = v * scale;
+  }
+}
+
+// SCA forward (NAFNet_arch.py:39-41, 62): mean[b][i] = pool / HW, a[b][o] = bsca[o] + sum_i W[o][i] mean[b][i].
+// grid (C / 4, B / NB), 4 waves: each block stages the means of its NB images (blockIdx.x == 0 also stores them for
+// the backward), then one wave per output o: the W row is loaded at once (C / 64 <= 16 values per lane), NB dots.
+template <int NB>
+__global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ pool, int chunks, float inv_hw,
+                                                float* __restrict__ mean_out, const float* __restrict__ wsca,
+                                                const float* __restrict__ bsca, float* __restrict__ a_out, int B,
+                                                int C) {
+  extern __shared__ float sm[];  // [NB][C] then [256] partials
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int o = blockIdx.x * 16 + wv;
-  for (int b0 = 0; b0 < B; b0 += SCA_NB) {
-    const int nb = min(SCA_NB, B - b0);
-    __syncthreads();
-    for (int e = threadIdx.x; e < nb * C; e += blockDim.x) {
-      const int bb = e / C, c = e - bb * C;
-      const float m = chunk_sum(pool, chunks, C, b0 + bb, c) * inv_hw;
-      sm[e] = m;
-      if (blockIdx.x == 0) mean_out[(long)b0 * C + e] = m;
+  const int o = blockIdx.x * 4 + wv, b0 = blockIdx.y * NB, nb = min(NB, B - b0);
+  float w[16];
+  if (o < C) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = lane + 64 * j;
+      w[j] = i < C ? wsca[(long)o * C + i] : 0.f;
     }
-    __syncthreads();
-    if (o < C) {
-      float acc[SCA_NB];
+  }
+  stage_chunk_sums(pool, chunks, C, b0, 0, C, nb * C, inv_hw, sm, sm + NB * C);
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int e = threadIdx.x; e < nb * C; e += blockDim.x) mean_out[(long)b0 * C + e] = sm[e];
+  if (o >= C) return;
+  float acc[NB];
 #pragma unroll
-      for (int b = 0; b < SCA_NB; ++b) acc[b] = 0.f;
-      for (int i = lane; i < C; i += 64) {
-        const float w = wsca[(long)o * C + i];
+  for (int b = 0; b < NB; ++b) acc[b] = 0.f;
 #pragma unroll
-        for (int b = 0; b < SCA_NB; ++b)
-          if (b < nb) acc[b] = fmaf(w, sm[b * C + i], acc[b]);
-      }
+  for (int j = 0; j < 16; ++j) {
+    const int i = lane + 64 * j;
+    if (i < C)
 #pragma unroll
-      for (int b = 0; b < SCA_NB; ++b) {
-        const float v = wave_sum(acc[b]);
-        if (lane == 0 && b < nb) a_out[(long)(b0 + b) * C + o] = v + bsca[o];
-      }
-    }
+      for (int b = 0; b < NB; ++b)
+        if (b < nb) acc[b] = fmaf(w[j], sm[b * C + i], acc[b]);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float v = wave_sum(acc[b]);
+    if (lane == 0 && b < nb) a_out[(long)(b0 + b) * C + o] = v + bsca[o];
   }
 }
 
@@ -242,78 +303,115 @@ __global__ __launch_bounds__(1024) void sca_bwd_ds(const float* __restrict__ da,
   }
 }
 
-// One launch for the SCA backward (NAFNet_arch.py:39-41, 67).  Blocks [0, nds): ds[b][i] = sum_o W[o][i] da[b][o]
-// as sca_bwd_ds, with da reduced from the img_chan_dot slab in the block itself.  Blocks [nds, nds + C/8): the
-// weight gradients of 8 rows o: dW[o][i] = sum_b da[b][o] mean[b][i], db[o] = sum_b da[b][o] (written to their
-// final place: no slab, no separate K = B GEMM).  Fixed summation orders throughout.
+// One launch for the SCA backward (NAFNet_arch.py:39-41, 67), 16 waves per block.  Blocks [0, nds): ds[b][i] =
+// sum_o W[o][i] da[b][o] for 64 columns i x NB images, the waves splitting the o range (16 W loads in flight per
+// lane) and summed in fixed order, da reduced from the img_chan_dot slab in the block itself.  Blocks [nds, nds +
+// C/8): the weight gradients of 8 rows o: dW[o][i] = sum_b da[b][o] mean[b][i], db[o] = sum_b da[b][o] (written to
+// their final place: no slab, no separate K = B GEMM).  Fixed summation orders throughout.
 constexpr int SCA_OB = 8;
+template <int NB>
 __global__ __launch_bounds__(1024) void sca_bwd_fused(const float* __restrict__ slab, int chunks,
                                                       const float* __restrict__ wsca, const float* __restrict__ mean,
                                                       float* __restrict__ ds_out, float* __restrict__ dW,
                                                       float* __restrict__ db, int B, int C, int nds) {
-  extern __shared__ float sh[];
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int nt = blockDim.x;
   if ((int)blockIdx.x >= nds) {
     const int o0 = (blockIdx.x - nds) * SCA_OB, no = min(SCA_OB, C - o0);
-    float* sda = sh;  // [B][SCA_OB]
-    for (int e = threadIdx.x; e < B * SCA_OB; e += blockDim.x) {
-      const int b = e / SCA_OB, r = e % SCA_OB;
-      sda[e] = r < no ? chunk_sum(slab, chunks, C, b, o0 + r) : 0.f;
-    }
+    float* sda = sh;  // [B][no]
+    // thread = column i x a row group (rows rg, rg + G, ...): the mean column is loaded once per 16 images for all of
+    // its rows (the first 16 before the da staging, so both latencies overlap); the sum over b runs in ascending order
+    const int G = nt / C, i = threadIdx.x % C, rg = threadIdx.x / C;
+    const bool act = rg < G && rg < no;
+    float m[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) m[u] = act && u < B ? mean[(long)u * C + i] : 0.f;
+    stage_chunk_sums(slab, chunks, C, 0, o0, no, B * no, 1.f, sda, sh + B * SCA_OB);
     __syncthreads();
-    for (int e = threadIdx.x; e < no * C; e += blockDim.x) {
-      const int r = e / C, i = e - r * C;
-      float acc = 0.f;
-      for (int b = 0; b < B; ++b) acc = fmaf(sda[b * SCA_OB + r], mean[(long)b * C + i], acc);
-      dW[(long)(o0 + r) * C + i] = acc;
+    if (act) {
+      float acc[SCA_OB];
+#pragma unroll
+      for (int k = 0; k < SCA_OB; ++k) acc[k] = 0.f;
+      for (int b = 0; b < B; b += 16) {
+        if (b > 0)
+#pragma unroll
+          for (int u = 0; u < 16; ++u) m[u] = b + u < B ? mean[(long)(b + u) * C + i] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (b + u < B)
+#pragma unroll
+            for (int k = 0; k < SCA_OB; ++k) {
+              const int r = rg + k * G;
+              if (r < no) acc[k] = fmaf(sda[(b + u) * no + r], m[u], acc[k]);
+            }
+      }
+#pragma unroll
+      for (int k = 0; k < SCA_OB; ++k) {
+        const int r = rg + k * G;
+        if (r < no) dW[(long)(o0 + r) * C + i] = acc[k];
+      }
     }
     if ((int)threadIdx.x < no) {
       float t = 0.f;
-      for (int b = 0; b < B; ++b) t += sda[b * SCA_OB + threadIdx.x];
+      for (int b = 0; b < B; ++b) t += sda[b * no + threadIdx.x];
       db[o0 + threadIdx.x] = t;
     }
     return;
   }
-  float* sda = sh;
-  float* part = sh + SCA_NB * C;
+  float* sda = sh;            // [NB][C]
+  float* part = sh + NB * C;  // staging partials, then [SCA_BW][NB][64]
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int cb = blockIdx.x % ((C + 63) / 64), bt = blockIdx.x / ((C + 63) / 64);
+  const int ncb = (C + 63) / 64, cb = blockIdx.x % ncb, bt = blockIdx.x / ncb;
   const int i = cb * 64 + lane;
-  const int b0 = bt * SCA_NB, nb = min(SCA_NB, B - b0);
-  for (int e = threadIdx.x; e < SCA_NB * C; e += blockDim.x) {
-    const int bb = e / C, c = e - bb * C;
-    sda[e] = bb < nb ? chunk_sum(slab, chunks, C, b0 + bb, c) : 0.f;
-  }
-  __syncthreads();
-  float acc[SCA_NB];
-#pragma unroll
-  for (int b = 0; b < SCA_NB; ++b) acc[b] = 0.f;
+  const int b0 = bt * NB, nb = min(NB, B - b0);
   const int per = (C + SCA_BW - 1) / SCA_BW, o0 = wv * per, o1 = min(C, o0 + per);
+  // the first 16 W values of this wave's o range are loaded before the da staging (overlapping latencies)
+  float w[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) w[u] = i < C && o0 + u < o1 ? wsca[(long)(o0 + u) * C + i] : 0.f;
+  stage_chunk_sums(slab, chunks, C, b0, 0, C, nb * C, 1.f, sda, part);
+  __syncthreads();
+  float acc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) acc[b] = 0.f;
+  const bool vec = (per & 3) == 0 && (C & 3) == 0;  // o0, o1 multiples of 4: 16-byte LDS reads of 4 da values
   if (i < C) {
-    int o = o0;
-    for (; o + 3 < o1; o += 4) {
-      float w[4];
+    for (int o = o0; o < o1; o += 16) {
+      if (o > o0)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = wsca[(long)(o + u) * C + i];
+        for (int u = 0; u < 16; ++u) w[u] = o + u < o1 ? wsca[(long)(o + u) * C + i] : 0.f;
+      if (vec) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 16; u += 4)
+          if (o + u < o1)
 #pragma unroll
-        for (int b = 0; b < SCA_NB; ++b) acc[b] = fmaf(w[u], sda[b * C + o + u], acc[b]);
-    }
-    for (; o < o1; ++o) {
-      const float w = wsca[(long)o * C + i];
+            for (int b = 0; b < NB; ++b)
+              if (b < nb) {
+                const float4 d = *reinterpret_cast<const float4*>(sda + b * C + o + u);
+                acc[b] = fmaf(w[u], d.x, acc[b]);
+                acc[b] = fmaf(w[u + 1], d.y, acc[b]);
+                acc[b] = fmaf(w[u + 2], d.z, acc[b]);
+                acc[b] = fmaf(w[u + 3], d.w, acc[b]);
+              }
+      } else {
 #pragma unroll
-      for (int b = 0; b < SCA_NB; ++b) acc[b] = fmaf(w, sda[b * C + o], acc[b]);
+        for (int u = 0; u < 16; ++u)
+          if (o + u < o1)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+              if (b < nb) acc[b] = fmaf(w[u], sda[b * C + o + u], acc[b]);
+      }
     }
   }
 #pragma unroll
-  for (int b = 0; b < SCA_NB; ++b) part[(wv * SCA_NB + b) * 64 + lane] = acc[b];
+  for (int b = 0; b < NB; ++b) part[(wv * NB + b) * 64 + lane] = acc[b];
   __syncthreads();
-  for (int e = threadIdx.x; e < nb * 64; e += blockDim.x) {
+  for (int e = threadIdx.x; e < nb * 64; e += nt) {
     const int b = e >> 6, l = e & 63, ii = cb * 64 + l;
     if (ii < C) {
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < SCA_BW; ++w) v += part[(w * SCA_NB + b) * 64 + l];
+      for (int w = 0; w < SCA_BW; ++w) v += part[(w * NB + b) * 64 + l];
       ds_out[(long)(b0 + b) * C + ii] = v;
     }
   }
@@ -913,8 +1011,19 @@ int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const flo
                 int HW, int C, nbp_stream_t s) {
   NBP_REQUIRE(pool_slab && wsca && bsca && mean && a && B > 0 && C > 0 && chunks > 0, "nbp_sca_fwd: bad args");
   NBP_REQUIRE(C <= 1024, "nbp_sca_fwd: C <= 1024");
-  sca_gemv<<<cdiv(C, 16), 1024, (size_t)SCA_NB * C * sizeof(float), S(s)>>>(pool_slab, chunks, 1.f / (float)HW, mean,
-                                                                            wsca, bsca, a, B, C);
+  // images per block: the staged chunk sums stay at <= 8 per thread (the loads are latency, not bandwidth)
+  int nb = 16;
+  while (nb > 1 && (long)nb * C * chunks > 2048) nb /= 2;
+  const dim3 grid(cdiv(C, 4), cdiv(B, nb));
+  const size_t sm = ((size_t)nb * C + 256) * sizeof(float);
+  const float inv = 1.f / (float)HW;
+  switch (nb) {
+    case 16: sca_gemv<16><<<grid, 256, sm, S(s)>>>(pool_slab, chunks, inv, mean, wsca, bsca, a, B, C); break;
+    case 8: sca_gemv<8><<<grid, 256, sm, S(s)>>>(pool_slab, chunks, inv, mean, wsca, bsca, a, B, C); break;
+    case 4: sca_gemv<4><<<grid, 256, sm, S(s)>>>(pool_slab, chunks, inv, mean, wsca, bsca, a, B, C); break;
+    case 2: sca_gemv<2><<<grid, 256, sm, S(s)>>>(pool_slab, chunks, inv, mean, wsca, bsca, a, B, C); break;
+    default: sca_gemv<1><<<grid, 256, sm, S(s)>>>(pool_slab, chunks, inv, mean, wsca, bsca, a, B, C); break;
+  }
   return check_launch("sca_fwd");
 }
 
@@ -943,11 +1052,23 @@ int nbp_sca_bwd_fused(const float* da_slab, int chunks, const float* wsca, const
                       float* db, int B, int C, nbp_stream_t s) {
   NBP_REQUIRE(da_slab && wsca && mean && ds && dW && db && B > 0 && C > 0 && chunks > 0, "nbp_sca_bwd_fused: bad args");
   NBP_REQUIRE(C <= 1024 && B <= 4096, "nbp_sca_bwd_fused: C <= 1024, B <= 4096");
-  const int nds = cdiv(C, 64) * cdiv(B, SCA_NB), ndw = cdiv(C, SCA_OB);
-  const size_t sm_ds = ((size_t)SCA_NB * C + SCA_BW * SCA_NB * 64) * sizeof(float);
-  const size_t sm_dw = (size_t)B * SCA_OB * sizeof(float);
-  sca_bwd_fused<<<nds + ndw, 64 * SCA_BW, sm_ds > sm_dw ? sm_ds : sm_dw, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db,
-                                                                             B, C, nds);
+  // images per ds block: <= 8 staged chunk loads per thread, at most 4
+  int nb = 16;
+  while (nb > 1 && (long)nb * C * chunks > 8192) nb /= 2;
+  if (nb > 4) nb = 4;  // the per-wave FMA / LDS work grows with nb, the W re-reads (L2) shrink
+  const int nds = cdiv(C, 64) * cdiv(B, nb), ndw = cdiv(C, SCA_OB);
+  const size_t sm_ds = ((size_t)nb * C + (size_t)SCA_BW * nb * 64 + 1024) * sizeof(float);
+  const size_t sm_dw = ((size_t)B * SCA_OB + 1024) * sizeof(float);
+  const size_t sm = sm_ds > sm_dw ? sm_ds : sm_dw;
+  NBP_REQUIRE(sm <= 160 * 1024, "nbp_sca_bwd_fused: LDS");
+  const int g = nds + ndw, ndsx = nds;
+  switch (nb) {
+    case 16: sca_bwd_fused<16><<<g, 64 * SCA_BW, sm, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db, B, C, ndsx); break;
+    case 8: sca_bwd_fused<8><<<g, 64 * SCA_BW, sm, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db, B, C, ndsx); break;
+    case 4: sca_bwd_fused<4><<<g, 64 * SCA_BW, sm, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db, B, C, ndsx); break;
+    case 2: sca_bwd_fused<2><<<g, 64 * SCA_BW, sm, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db, B, C, ndsx); break;
+    default: sca_bwd_fused<1><<<g, 64 * SCA_BW, sm, S(s)>>>(da_slab, chunks, wsca, mean, ds, dW, db, B, C, ndsx); break;
+  }
   return check_launch("sca_bwd_fused");
 }
 

@@ -450,6 +450,31 @@ def test_dw_sg_pool_fwd_against_float64(dev, B, H, W, C, dtype):
     close(a, (rmean @ wsca.double().t() + bsca.double()).cpu().numpy(), atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("B,H,W,C", [(16, 256, 256, 32), (16, 16, 16, 512), (5, 64, 64, 128), (3, 9, 11, 12),
+                                     (17, 32, 32, 256)])
+def test_sca_fwd_bwd_against_float64(dev, B, H, W, C):
+    """SCA head on the pooled vector (NAFNet_arch.py:39-41): sca_fwd reduces the dw pool slab to the mean and forms
+    a = W mean + b; sca_bwd_fused reduces the img_chan_dot slab to da and forms ds = W^T da, dW = da^T mean,
+    db = sum_b da -- at the level shapes (many chunks / one chunk) and ragged ones, vs float64."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(B * C + H)
+    rows = query("dw_fwd_slab_rows", B, H, W, C, 1)
+    pool = torch.randn(B * rows * C, device=dev, generator=gen)
+    wsca, bsca = torch.randn(C, C, device=dev, generator=gen), torch.randn(C, device=dev, generator=gen)
+    mean, a = torch.empty(B, C, device=dev), torch.empty(B, C, device=dev)
+    call("sca_fwd", pool, rows, wsca, bsca, mean, a, B, H * W, C)
+    rmean = pool.double().view(B, rows, C).sum(1) / (H * W)
+    close(mean, rmean.cpu().numpy(), atol=1e-5, rtol=1e-5)
+    close(a, (rmean @ wsca.double().t() + bsca.double()).cpu().numpy(), atol=1e-4, rtol=1e-4)
+    ch = query("dw_chunks", B, H, W, C, 0)
+    da_slab = torch.randn(B * ch * C, device=dev, generator=gen)
+    ds, dW, db = torch.empty(B, C, device=dev), torch.empty(C, C, device=dev), torch.empty(C, device=dev)
+    call("sca_bwd_fused", da_slab, ch, wsca, mean, ds, dW, db, B, C)
+    rda = da_slab.double().view(B, ch, C).sum(1)
+    close(ds, (rda @ wsca.double()).cpu().numpy(), atol=1e-3 * ch ** 0.5, rtol=1e-4)
+    close(dW, (rda.t() @ mean.double()).cpu().numpy(), atol=1e-4 * ch ** 0.5, rtol=1e-4)
+    close(db, rda.sum(0).cpu().numpy(), atol=1e-4 * ch ** 0.5, rtol=1e-4)
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 def test_graph_step_bitwise_equals_eager(dev, precision):
     """The captured HIP-graph step replays exactly the eager step's kernels: parameters, optimizer state and losses
