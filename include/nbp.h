@@ -317,6 +317,30 @@ int nbp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_a
 int nbp_adamw_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
                        const float* hyper, float beta1, float beta2, float eps, float weight_decay, nbp_stream_t s);
 
+/* ------------------------------------------------------------------ SID input path
+ * Host-side (no GPU, no stream): the reference reads PNG bytes from LMDB (basicsr FileClient 'lmdb',
+ * NAFNet_base/basicsr/data/sony_sid_lmdb_dataset.py:110-125,150-156) or disk and decodes them with
+ * cv2.imdecode(IMREAD_UNCHANGED) (:38-56).  An LMDB environment is opened read-only (mmap) and named by an int
+ * handle; nbp_lmdb_get returns a pointer into the map (*vlen = -1: key absent, as txn.get -> None). */
+int nbp_lmdb_open(const char* path);
+int nbp_lmdb_close(int handle);
+int nbp_lmdb_stat(int handle, long* entries, long* psize);
+int nbp_lmdb_get(int handle, const char* key, int klen, const void** val, long* vlen);
+/* IHDR of a PNG: channels = those of the cv2 IMREAD_UNCHANGED array (1 gray, 3 RGB / palette, 4 with alpha or tRNS),
+ * depth = 8 or 16 after palette / low-depth expansion. */
+int nbp_png_info(const void* buf, long len, int* h, int* w, int* channels, int* depth);
+/* 3-channel PNG -> uint16 [crop_h][crop_w][3] in the file's R, G, B order, 8-bit values * 257 (the uint8 promotion
+ * of _load_png_uint16, :45-47); crop_h <= 0 decodes the whole image.  The crop is _maybe_random_crop's window
+ * (:162-192). */
+int nbp_png_decode_rgb16(const void* buf, long len, void* out, int top, int left, int crop_h, int crop_w);
+/* n PNGs decoded and cropped on nthreads host threads into out[n][crop_h][crop_w][3]. */
+int nbp_png_decode_batch(int n, const void* const* bufs, const long* lens, const int* tops, const int* lefts,
+                         int crop_h, int crop_w, void* out, int nthreads);
+/* Device: uint16 NHWC crops -> lq (= short = short_obs) = clip(short/65535 * ratio[b], 0, 1), short_raw =
+ * short/65535, long_raw (= gt = long) = long/65535, NCHW float32 [B][3][H][W] (sony_sid_lmdb_dataset.py:207-218). */
+int nbp_sid_to_float(const void* short_u16, const void* long_u16, const float* ratio, int B, int H, int W, float* lq,
+                     float* short_raw, float* long_raw, nbp_stream_t s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,6 +136,16 @@ def query(name: str, *args) -> int:
     return int(getattr(lib().dll, "nbp_" + name)(*args))
 
 
+def host_call(name: str, *args) -> int:
+    """Call a host-only entry point nbp_<name>(...) (no stream: LMDB / PNG); raise on a negative return, else
+    return the value (e.g. an LMDB handle)."""
+    L = lib()
+    rc = getattr(L.dll, "nbp_" + name)(*args)
+    if rc < 0:
+        raise NBPError(f"nbp_{name} failed ({rc}): {L.dll.nbp_last_error_string().decode()}")
+    return rc
+
+
 def require_cuda(*tensors):
     for t in tensors:
         if t is not None and (not t.is_cuda or t.dtype != torch.float32):

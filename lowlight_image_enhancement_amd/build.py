@@ -25,7 +25,7 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + os.path
 
 
 def _sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
 def _stale(obj, src):
@@ -50,14 +50,14 @@ def build_library(force: bool = False, verbose: bool = False, jobs: int = 8) -> 
     objdir = os.path.join(OUT_DIR, "obj")
     os.makedirs(objdir, exist_ok=True)
     srcs = _sources()
-    objs = [os.path.join(objdir, os.path.basename(s)[:-4] + ".o") for s in srcs]
+    objs = [os.path.join(objdir, os.path.splitext(os.path.basename(s))[0] + ".o") for s in srcs]
     todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(o, s)]
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
             list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
     if todo or force or not os.path.exists(LIB):
         tmp = LIB + ".tmp"
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-lz", "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
