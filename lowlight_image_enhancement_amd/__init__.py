@@ -30,3 +30,8 @@ def install_aliases():
     sys.modules.setdefault("metrics.ssim", ssim)
     sys.modules.setdefault("metrics.color_error", color_error)
     sys.modules.setdefault("basicsr.metrics.lowlight_metrics", lowlight_metrics)
+    from .data import data_sampler, file_client, prefetch_dataloader, sony_sid_lmdb_dataset
+    sys.modules.setdefault("basicsr.data.sony_sid_lmdb_dataset", sony_sid_lmdb_dataset)
+    sys.modules.setdefault("basicsr.data.prefetch_dataloader", prefetch_dataloader)
+    sys.modules.setdefault("basicsr.data.data_sampler", data_sampler)
+    sys.modules.setdefault("basicsr.utils.file_client", file_client)
