@@ -107,6 +107,12 @@ size_t nbp_dgrad_ln_workspace_floats(long M, int N);
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
                      float* ws, size_t ws_floats, nbp_stream_t s);
+/* NAFBlock conv3 / conv5 (N = C in {32, 64}, K <= 128, bf16) with the next LayerNorm2d forward in the epilogue:
+ * C = R + rscale * (A W^T + bias) (the block's y / out, NAFNet_arch.py:70-78) and nout / stats = LN(C) exactly as
+ * nbp_ln_fwd_nhwc computes them from the stored C (arch_util.py:266-275); C, nout row stride N. */
+int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
+                    long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
+                    const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s);
 /* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols} (int64, device) out_t[offset..] =
  * bf16(flat matrix)^T. */
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);

@@ -22,7 +22,7 @@ namespace {
 // forward (C = t with channel pairs (c, C+c) interleaved, and pre <- g = t[2c] * t[2c+1]) and SimpleGate backward
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
-enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6 };
+enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7 };
 
 struct GemmPB {
   const void* A;
@@ -398,6 +398,12 @@ struct SkinnyP {
   const __bf16* dres;
   float* slab_w;
   float* slab_b;
+  // CM_RESLN (bias + layer-scale residual, then the next LayerNorm2d forward, arch_util.py:266-275): C = the stored
+  // residual sum, nout = LN(C) with lnw / lnb_f, stats_out = (mu, sqrt(var + eps)) per row
+  const float* lnb_f;
+  __bf16* nout;
+  float2* stats_out;
+  float eps;
 };
 
 template <int NT, int KS, int AMODE, int CMODE>
@@ -428,6 +434,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
   float bia[8], rsc[8], aw[8], ab[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { bia[j] = 0.f; rsc[j] = 1.f; aw[j] = ab[j] = 0.f; }
+  if (CMODE == CM_RESLN) {  // aw / ab hold the LN weight / bias of this lane's 8 columns
+    const float4 w0 = ld4(p.lnw + ccol), w1 = ld4(p.lnw + ccol + 4), b0 = ld4(p.lnb_f + ccol), b1 = ld4(p.lnb_f + ccol + 4);
+    aw[0] = w0.x; aw[1] = w0.y; aw[2] = w0.z; aw[3] = w0.w; aw[4] = w1.x; aw[5] = w1.y; aw[6] = w1.z; aw[7] = w1.w;
+    ab[0] = b0.x; ab[1] = b0.y; ab[2] = b0.z; ab[3] = b0.w; ab[4] = b1.x; ab[5] = b1.y; ab[6] = b1.z; ab[7] = b1.w;
+  }
   if (CMODE == CM_LNBWD) {  // rsc holds the LN weight of this lane's 8 columns
     const float4 s0 = ld4(p.lnw + ccol), s1 = ld4(p.lnw + ccol + 4);
     rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
@@ -536,7 +547,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bia[j];
       const long off = m * p.ldc + ccol;
-      if (CMODE == CM_PLAIN && p.R) {
+      if ((CMODE == CM_PLAIN || CMODE == CM_RESLN) && p.R) {
         const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.R + off);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (float)rv[j] + rsc[j] * v[j];
@@ -545,6 +556,29 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
       *reinterpret_cast<bf16x8*>(p.C + off) = o;
+      if constexpr (CMODE == CM_RESLN) {  // LayerNorm2d of the stored (bf16) row, as ln_fwd_nhwc computes it
+        constexpr int G = 4 * NT;
+        float xv[8], sm = 0.f, q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xv[j] = (float)o[j];
+          sm += xv[j];
+        }
+        sm = group_sum<G>(sm);
+        const float mu = sm / (float)N;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = xv[j] - mu;
+          q = fmaf(d, d, q);
+        }
+        q = group_sum<G>(q);
+        const float dd = sqrtf(q / (float)N + p.eps), inv = 1.f / dd;
+        bf16x8 nn;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nn[j] = (__bf16)fmaf(aw[j], (xv[j] - mu) * inv, ab[j]);
+        *reinterpret_cast<bf16x8*>(p.nout + m * N + ccol) = nn;
+        if (ccol == 0) p.stats_out[m] = make_float2(mu, dd);
+      }
       if (CMODE == CM_SG) {  // g[c] = t[2c] * t[2c+1]: 4 gates of this chunk
         bf16x4 gv;
 #pragma unroll
@@ -765,6 +799,22 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
   rc = nbp_reduce_slab(p.slab_w, (int)nb, N, dlnw, s);
   if (rc) return rc;
   return nbp_reduce_slab(p.slab_b, (int)nb, N, dlnb, s);
+}
+
+int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
+                    long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
+                    const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s) {
+  NBP_REQUIRE(A && Bw && C && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args");
+  NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
+              "nbp_gemm_res_ln: N must be 32 or 64, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
+  NBP_REQUIRE(a_mode == AM_PLAIN || (a_mode == AM_SCALE && a_scale && rows_per_img > 0), "nbp_gemm_res_ln: a_mode");
+  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb,
+            reinterpret_cast<__bf16*>(C), N, M, N, K, bias, reinterpret_cast<const __bf16*>(R), rscale, nullptr,
+            nullptr, lnw, nullptr, nullptr, nullptr, lnb, reinterpret_cast<__bf16*>(nout),
+            reinterpret_cast<float2*>(stats), eps};
+  if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_RESLN>(p, S(s));
+  else launch_skinny<AM_PLAIN, CM_RESLN>(p, S(s));
+  return check_launch("gemm_res_ln");
 }
 
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s) {

@@ -96,6 +96,9 @@ class NAFNet(nn.Module):
         # when no per-stage hook needs the gradient slices early, i.e. single-GPU)
         self.overlap_wgrad = int(os.environ.get("NBP_OVERLAP_WGRAD", "0"))
         self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
+        # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
+        self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
+        self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
         # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
@@ -309,6 +312,7 @@ class NAFNet(nn.Module):
         tape: List[tuple] = []
         Wt = (P,) if self.precision == "fp32" else (P,) + self._prep_weights(P)
         self._W = Wt
+        self._ln_carry = None
         w = self.width
         feat = torch.empty(B, Hp, Wp, w, device=x.device, dtype=self.adt)
         call("intro_fwd", x, self._slice(P, "intro.weight"), self._slice(P, "intro.bias"), feat, B, Ci, H0, W0, Hp,
@@ -320,19 +324,22 @@ class NAFNet(nn.Module):
         for i, n in enumerate(self.enc_blk_nums):
             c = self.enc_chans[i]
             for j in range(n):
-                feat = self._block_fwd(P, f"encoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None)
+                nxt = f"encoders.{i}.{j + 1}." if j + 1 < n else None
+                feat = self._block_fwd(P, f"encoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None, nxt)
             skips.append(feat)
             feat = self._down_fwd(P, i, feat, B, h, wd, c, tape if save else None)
             h, wd = h // 2, wd // 2
         for j in range(self.middle_blk_num):
-            feat = self._block_fwd(P, f"middle_blks.{j}.", feat, B, h, wd, self.mid_chan, tape if save else None)
+            nxt = f"middle_blks.{j + 1}." if j + 1 < self.middle_blk_num else None
+            feat = self._block_fwd(P, f"middle_blks.{j}.", feat, B, h, wd, self.mid_chan, tape if save else None, nxt)
         for i, n in enumerate(self.dec_blk_nums):
             chan = self.dec_chans[i] * 2
             feat = self._up_fwd(P, i, feat, skips[::-1][i], B, h, wd, chan, tape if save else None)
             h, wd = h * 2, wd * 2
             c = self.dec_chans[i]
             for j in range(n):
-                feat = self._block_fwd(P, f"decoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None)
+                nxt = f"decoders.{i}.{j + 1}." if j + 1 < n else None
+                feat = self._block_fwd(P, f"decoders.{i}.{j}.", feat, B, h, wd, c, tape if save else None, nxt)
         out = torch.empty(B, Ci, H0, W0, device=x.device)
         call("ending_fwd", feat, self._slice(P, "ending.weight"), self._slice(P, "ending.bias"), x, out, B, Ci, H0,
              W0, Hp, Wp, w, self.dt)
@@ -342,15 +349,23 @@ class NAFNet(nn.Module):
         self._W = None
         return out, tape
 
-    def _block_fwd(self, P, pre, x, B, h, w, c, tape):
+    def _block_fwd(self, P, pre, x, B, h, w, c, tape, next_pre=None):
+        """One NAFBlock forward (NAFNet_arch.py:60-80).  At C in {32, 64} (bf16) the LayerNorms run in the epilogue
+        of the GEMM producing their input (nbp_gemm_res_ln): norm2 in conv3's, the next block's norm1 (next_pre)
+        in conv5's; that block then takes (n1, st1) from self._ln_carry."""
         M = B * h * w
         dev = x.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
-        n1, st1 = E(M, c), F(M, 2)
-        call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), n1, st1, M, c,
-             LN_EPS, dt)
+        fuse_ln = self.fuse_ln_fwd and dt == 1 and c in (32, 64) and len(self._W) == 3
+        carry, self._ln_carry = self._ln_carry, None
+        if carry is not None and carry[0] is x:
+            n1, st1 = carry[1], carry[2]
+        else:
+            n1, st1 = E(M, c), F(M, 2)
+            call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), n1, st1,
+                 M, c, LN_EPS, dt)
         t1 = E(M, 2 * c)
         self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
                  bias=self._slice(P, pre + "conv1.bias"))
@@ -365,11 +380,16 @@ class NAFNet(nn.Module):
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
              a, B, h * w, c)
         y = E(M, c)
-        self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
-                 bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
         n2, st2 = E(M, c), F(M, 2)
-        call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, M, c,
-             LN_EPS, dt)
+        if fuse_ln:
+            call("gemm_res_ln", g, c, AM_SCALE, a, h * w, self._slice(self._W[1], pre + "conv3.weight"), c, y, M, c, c,
+                 self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
+                 self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS)
+        else:
+            self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
+                     bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
+            call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2,
+                 M, c, LN_EPS, dt)
         t4, g2 = E(M, 2 * c), E(M, c)  # t4 channel pairs interleaved (conv4 rows stored so)
         if dt == 1:  # SimpleGate in the GEMM epilogue
             self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
@@ -379,12 +399,20 @@ class NAFNet(nn.Module):
                      bias=self._slice(P, pre + "conv4.bias"))
             call("sg_fwd", t4, g2, M, c, 1, dt)
         out = E(M, c)
-        self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
-                 bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
+        if fuse_ln and next_pre is not None:
+            nn1, nst1 = E(M, c), F(M, 2)
+            call("gemm_res_ln", g2, c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c, out, M, c,
+                 c, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"),
+                 self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), nn1, nst1,
+                 LN_EPS)
+            self._ln_carry = (out.view(B, h, w, c), nn1, nst1)
+        else:
+            self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
+                     bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
         if tape is not None:
             tape.append(("block", pre, (B, h, w, c), dict(x=x, n1=n1, st1=st1, t1=t1, t2=t2, g=g, mean=mean, a=a, y=y,
                                                            n2=n2, st2=st2, t4=t4, g2=g2)))
-        return out.view(B, h, w, c)
+        return self._ln_carry[0] if self._ln_carry is not None else out.view(B, h, w, c)
 
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
         ho, wo = h // 2, w // 2

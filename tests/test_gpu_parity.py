@@ -591,6 +591,48 @@ def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
     close(dlnb, dn.sum(0).cpu().numpy(), atol=2e-4 * M ** 0.5, rtol=1e-4)
 
 
+@pytest.mark.parametrize("M,N,K,amode", [(4096, 32, 32, 2), (3001, 64, 64, 0), (777, 32, 64, 0), (65, 64, 128, 2)])
+def test_gemm_res_ln_equals_gemm_then_ln_fwd(dev, M, N, K, amode):
+    """conv3 / conv5 with the LayerNorm2d forward in the epilogue (nbp_gemm_res_ln) equals the skinny GEMM with the
+    residual followed by the standalone ln_fwd_nhwc, bit for bit (same stored bf16 row, same summation order)."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M * 3 + N + K)
+    rows = 97 if M % 97 == 0 else M
+    A = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=gen) / K ** 0.5).to(torch.bfloat16)
+    scale = torch.rand(-(-M // rows), K, device=dev, generator=gen) + 0.5 if amode == 2 else None
+    bias, rs = torch.randn(N, device=dev, generator=gen), torch.randn(N, device=dev, generator=gen)
+    R = (torch.randn(M, N, device=dev, generator=gen) * 3 + 1).to(torch.bfloat16)
+    lnw, lnb = torch.randn(N, device=dev, generator=gen), torch.randn(N, device=dev, generator=gen)
+    y0, n0, s0 = (torch.empty(M, N, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev,
+                  dtype=torch.bfloat16), torch.empty(M, 2, device=dev))
+    call("gemm_bf16", A, K, amode, scale, rows, 1, W, K, y0, N, 0, 1, M, N, K, 0, 0, 0, bias, R, rs, None)
+    call("ln_fwd_nhwc", y0, lnw, lnb, n0, s0, M, N, 1e-6, 1)
+    y1, n1, s1 = torch.empty_like(y0), torch.empty_like(n0), torch.empty_like(s0)
+    call("gemm_res_ln", A, K, amode, scale, rows, W, K, y1, M, N, K, bias, R, rs, lnw, lnb, n1, s1, 1e-6)
+    assert torch.equal(y1, y0) and torch.equal(n1, n0) and torch.equal(s1, s0)
+
+
+def test_fused_ln_forward_network_bitwise(dev, monkeypatch):
+    """Whole bf16 forward with the LayerNorms in the conv3 / conv5 epilogues (default) vs standalone ln_fwd: the
+    output and every taped tensor are identical."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    torch.manual_seed(1)
+    net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[2, 2], middle_blk_num=1, dec_blk_nums=[2, 2]).to(dev)
+    net.precision = "bf16"
+    with torch.no_grad():
+        net.flat.add_(torch.randn_like(net.flat) * 0.05)  # non-zero beta / gamma: every residual branch is live
+    x = torch.rand(2, 3, 64, 48, device=dev)
+    outs = []
+    for fuse in (True, False):
+        net.fuse_ln_fwd = fuse
+        out, tape = net.exec_forward(x, save=True)
+        outs.append((out, [r for r in tape if r[0] == "block"]))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for ra, rb in zip(outs[0][1], outs[1][1]):
+        for k in ("n1", "st1", "y", "n2", "st2"):
+            assert torch.equal(ra[3][k], rb[3][k]), (ra[1], k)
+
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
 def test_dw_bwd_t2_recompute_matches_stored(dev, B, H, W, C, dtype):
     """The fused SCA/SimpleGate/depthwise backward that recomputes t2 = conv2(t1) + b in LDS (the forward then stores
