@@ -113,8 +113,9 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
 int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s);
-/* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols} (int64, device) out_t[offset..] =
- * bf16(flat matrix)^T. */
+/* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols, scale_offset} (int64, device)
+ * out_t[offset..] = bf16(diag(s) . flat matrix)^T with s = flat[scale_offset..] (rows values), or no scaling when
+ * scale_offset < 0 (the NAFBlock layer scales folded into the conv3 / conv5 dgrad operands). */
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);
 /* weight gradient dW[n][k] = sum_m G(m,n) X(m,k) (+ db[n] = sum_m G(m,n)): split over M, fixed-order slab reduce. */
 size_t nbp_wgrad_workspace_floats(int M, int N, int K);

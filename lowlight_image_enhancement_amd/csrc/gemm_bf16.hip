@@ -665,18 +665,20 @@ __global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, __bf16* _
     dst[i] = (__bf16)src[i];
 }
 
-// desc: [ndesc][3] int64 {offset, rows, cols}; block (x: tile index, y: matrix)
+// desc: [ndesc][4] int64 {offset, rows, cols, row-scale offset or -1}; block (x: tile index, y: matrix).  With a
+// row scale s (the layer scale beta / gamma of conv3 / conv5) the copy is (diag(s) W)^T.
 __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long* __restrict__ desc,
                                       __bf16* __restrict__ dst_t) {
   __shared__ float tile[32][33];
-  const long off = desc[blockIdx.y * 3], R = desc[blockIdx.y * 3 + 1], Cc = desc[blockIdx.y * 3 + 2];
+  const long off = desc[blockIdx.y * 4], R = desc[blockIdx.y * 4 + 1], Cc = desc[blockIdx.y * 4 + 2];
+  const long soff = desc[blockIdx.y * 4 + 3];
   const long tiles_c = (Cc + 31) / 32, ntiles = ((R + 31) / 32) * tiles_c;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const long r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
     for (int rr = ty; rr < 32; rr += 8) {
       const long r = r0 + rr, c = c0 + tx;
-      tile[rr][tx] = (r < R && c < Cc) ? src[off + r * Cc + c] : 0.f;
+      tile[rr][tx] = (r < R && c < Cc) ? src[off + r * Cc + c] * (soff >= 0 ? src[soff + r] : 1.f) : 0.f;
     }
     __syncthreads();
     for (int cc = ty; cc < 32; cc += 8) {

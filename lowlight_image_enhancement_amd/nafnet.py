@@ -104,9 +104,21 @@ class NAFNet(nn.Module):
         # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
         # (the reference's AMP training, image_restoration_model.py:255), fp32 storage and statistics.
         self.precision = "fp32"
-        self._tdesc_cpu = torch.tensor([[e.offset, e.ref_shape[0], e.numel // e.ref_shape[0]]
+        # bf16 mode: the layer scales beta / gamma are folded into the transposed conv3 / conv5 weight copies (the
+        # dgrad operands: dh = (beta (.) dy) W3 = dy (diag(beta) W3)), so those dgrads read A unscaled
+        # (NBP_FOLD_LS=0: A-column scale in the GEMM instead)
+        self.fold_ls = os.environ.get("NBP_FOLD_LS", "1") != "0"
+
+        def _scale_off(k):
+            if not self.fold_ls:
+                return -1
+            for wk, sk in (("conv3.weight", "beta"), ("conv5.weight", "gamma")):
+                if k.endswith(wk):
+                    return self.entries[k[:-len(wk)] + sk].offset
+            return -1
+        self._tdesc_cpu = torch.tensor([[e.offset, e.ref_shape[0], e.numel // e.ref_shape[0], _scale_off(k)]
                                         for k, e in self.entries.items() if self._is_gemm_weight(k)],
-                                       dtype=torch.int64).reshape(-1, 3)
+                                       dtype=torch.int64).reshape(-1, 4)
         self._tdesc = None
 
     # ------------------------------------------------------------------ layout
@@ -573,9 +585,14 @@ class NAFNet(nn.Module):
         # (gamma as the A-operand column scale); U5 = dout^T g2, V5 = colsum dout feed dW5 = gamma (.) U5,
         # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
         dt4 = E(M, 2 * c)
+        folded = len(Wt) == 3 and self.fold_ls  # gamma / beta already in the transposed bf16 weights
         if dt == 1:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises
-            self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dt4, 2 * c,
-                     CM_SGBWD, M, c, c, R=S["t4"], dgrad=True)
+            if folded:
+                self._mm(Wt, dout, c, AM_PLAIN, None, 1, pre + "conv5.weight", dt4, 2 * c, CM_SGBWD, M, c, c,
+                         R=S["t4"], dgrad=True)
+            else:
+                self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dt4, 2 * c,
+                         CM_SGBWD, M, c, c, R=S["t4"], dgrad=True)
         else:
             dg2 = E(M, c)
             self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dg2, c, CM_PLAIN,
@@ -606,8 +623,11 @@ class NAFNet(nn.Module):
             self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
         # y = x + beta * conv3(h), h = g (.) a: same layer-scale identity as conv5 (dh = (beta (.) dy) W3)
         dh = E(M, c)
-        self._mm(Wt, dy, c, AM_SCALE, self._slice(P, pre + "beta"), M, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c,
-                 dgrad=True)
+        if folded:
+            self._mm(Wt, dy, c, AM_PLAIN, None, 1, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c, dgrad=True)
+        else:
+            self._mm(Wt, dy, c, AM_SCALE, self._slice(P, pre + "beta"), M, pre + "conv3.weight", dh, c, CM_PLAIN, M,
+                     c, c, dgrad=True)
         U3, V3 = F(c * c), F(c)
         self._wgrad(dy, c, AM_PLAIN, S["g"], c, AM_SCALE, S["a"], HW, M, c, c, 0, 0, 0, 0, U3, V3)
         call("layer_scale_grad", U3, V3, self._slice(P, pre + "conv3.weight"), self._slice(P, pre + "conv3.bias"),
