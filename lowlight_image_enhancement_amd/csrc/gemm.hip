@@ -595,9 +595,20 @@ struct RDesc {
   int S, ty, vec, blk0;
 };
 constexpr int RB_MAX = 48;
+// Layer-scale gradient rows reduced straight from the U / V weight-gradient slabs in the same launch (one block per
+// row k: U[k][:] = sum_s slabU[s][k][:], V[k] = sum_s slabV[s][k], then the layer_scale_grad_kernel post-op below),
+// so a stage flush is one launch and U / V are never written.
+struct LDesc {
+  const float *slabU, *slabV, *W, *b, *scale;
+  float *dW, *db, *dscale;
+  int SU, SV, N, K, blk0;
+};
+constexpr int LB_MAX = 8;
 struct RBatch {
   RDesc d[RB_MAX];
   int n;
+  LDesc l[LB_MAX];
+  int nl, lblk0;
 };
 
 RDesc make_rdesc(const float* slab, int S, long L, float* out) {
@@ -608,9 +619,54 @@ RDesc make_rdesc(const float* slab, int S, long L, float* out) {
 }
 long rdesc_blocks(const RDesc& d) { return cdiv(d.L, (long)(256 / d.ty) * d.vec); }
 
+__device__ void layer_scale_row(const RBatch& rb, int lb, float* red) {
+  int j = 0;
+  while (j + 1 < rb.nl && rb.l[j + 1].blk0 <= lb) ++j;
+  const LDesc& d = rb.l[j];
+  const int row = lb - d.blk0, K = d.K, N = d.N;
+  int txq = 1;
+  while (txq * 4 < K) txq <<= 1;  // column lanes (4 columns each), a power of two <= 256 (K <= 1024)
+  const int TY = 256 / txq, tx = threadIdx.x % txq, ty = threadIdx.x / txq;
+  const int col = tx * 4;
+  float u[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col < K) slab_col_partial<4>(d.slabU + (long)row * K, d.SU, (long)N * K, col, ty, TY, u);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) red[threadIdx.x * 4 + e] = u[e];
+  // V[row]: 256 strided partial sums, folded in fixed order below
+  float v = 0.f;
+  for (int s2 = threadIdx.x; s2 < d.SV; s2 += 256) v += d.slabV[(long)s2 * N + row];
+  __syncthreads();
+  const float sc = d.scale[row];
+  float dot = 0.f;
+  if (ty == 0 && col < K) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < TY; ++y)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] += red[(y * txq + tx) * 4 + e];
+    const float4 w = ld4(d.W + (long)row * K + col);
+    dot = fmaf(w.x, t[0], fmaf(w.y, t[1], fmaf(w.z, t[2], w.w * t[3])));
+    st4(d.dW + (long)row * K + col, make_float4(sc * t[0], sc * t[1], sc * t[2], sc * t[3]));
+  }
+  __syncthreads();
+  red[threadIdx.x] = v;
+  red[256 + threadIdx.x] = dot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float vs = 0.f, ds = 0.f;
+    for (int i = 0; i < 256; ++i) vs += red[i];
+    for (int i = 0; i < txq; ++i) ds += red[256 + i];
+    d.dscale[row] = ds + d.b[row] * vs;
+    d.db[row] = sc * vs;
+  }
+}
+
 __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
   __shared__ float red[256 * 4];
   const int bid = blockIdx.x;
+  if (bid >= rb.lblk0) {
+    layer_scale_row(rb, bid - rb.lblk0, red);
+    return;
+  }
   int k = 0;
   while (k + 1 < rb.n && rb.d[k + 1].blk0 <= bid) ++k;
   const RDesc& d = rb.d[k];
@@ -635,11 +691,11 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
   }
 }
 
-void launch_multi(const std::vector<RDesc>& ds, hipStream_t st) {
-  size_t i = 0;
-  while (i < ds.size()) {
+void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vector<LDesc>& ls = {}) {
+  size_t i = 0, j = 0;
+  while (i < ds.size() || j < ls.size()) {
     RBatch rb;
-    rb.n = 0;
+    rb.n = rb.nl = 0;
     long blocks = 0;
     for (; i < ds.size() && rb.n < RB_MAX; ++i) {
       RDesc d = ds[i];
@@ -647,7 +703,15 @@ void launch_multi(const std::vector<RDesc>& ds, hipStream_t st) {
       blocks += rdesc_blocks(d);
       rb.d[rb.n++] = d;
     }
-    reduce_multi_kernel<<<(unsigned)blocks, 256, 0, st>>>(rb);
+    rb.lblk0 = (int)blocks;
+    int lblocks = 0;
+    for (; j < ls.size() && rb.nl < LB_MAX; ++j) {
+      LDesc d = ls[j];
+      d.blk0 = lblocks;
+      lblocks += d.N;
+      rb.l[rb.nl++] = d;
+    }
+    reduce_multi_kernel<<<(unsigned)(blocks + lblocks), 256, 0, st>>>(rb);
   }
 }
 
@@ -720,10 +784,42 @@ void grad_reduce(const float* slab, int S, long L, float* out, hipStream_t st) {
   launch_multi(std::vector<RDesc>{make_rdesc(slab, S, L, out)}, st);
 }
 
+// NBP_LS_FUSE=0 keeps the layer-scale post-op as its own launch after the reductions (A/B measurement)
+bool getenv_ls_fuse() {
+  static const bool on = [] {
+    const char* v = getenv("NBP_LS_FUSE");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 void flush_pending() {
-  launch_multi(g_pending, g_defer_stream);
+  // a post-op whose U and V are both reductions of this flush becomes a layer-scale row descriptor of the same launch
+  std::vector<LDesc> ls;
+  std::vector<PDesc> post;
+  for (const PDesc& p : g_post) {
+    int iu = -1, iv = -1;
+    for (int i = 0; i < (int)g_pending.size(); ++i) {
+      if (g_pending[i].out == p.U) iu = i;
+      if (g_pending[i].out == p.V) iv = i;
+    }
+    const bool ok = getenv_ls_fuse() && iu >= 0 && iv >= 0 && p.K % 4 == 0 && p.K <= 1024 &&
+                    g_pending[iu].L == (long)p.N * p.K && g_pending[iv].L == p.N &&
+                    (reinterpret_cast<uintptr_t>(g_pending[iu].slab) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(p.W) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.dW) & 15) == 0;
+    if (!ok) {
+      post.push_back(p);
+      continue;
+    }
+    ls.push_back(LDesc{g_pending[iu].slab, g_pending[iv].slab, p.W, p.b, p.scale, p.dW, p.db, p.dscale,
+                       g_pending[iu].S, g_pending[iv].S, p.N, p.K, 0});
+    const int hi = iu > iv ? iu : iv, lo = iu > iv ? iv : iu;
+    g_pending.erase(g_pending.begin() + hi);
+    g_pending.erase(g_pending.begin() + lo);
+  }
+  launch_multi(g_pending, g_defer_stream, ls);
   g_pending.clear();
-  launch_post(g_post, g_defer_stream);  // post-ops read reduction outputs: after every reduction of the flush
+  launch_post(post, g_defer_stream);  // post-ops read reduction outputs: after every reduction of the flush
   g_post.clear();
 }
 
