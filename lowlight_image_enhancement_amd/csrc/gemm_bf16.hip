@@ -22,7 +22,8 @@ namespace {
 // forward (C = t with channel pairs (c, C+c) interleaved, and pre <- g = t[2c] * t[2c+1]) and SimpleGate backward
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
-enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7 };
+enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7,
+       CM_CHANDOT = 8 };
 
 struct GemmPB {
   const void* A;
@@ -273,6 +274,12 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
   __syncthreads();
   constexpr int G8 = BN / 8;
   const bool vec = (N % 8 == 0) && (CMODE == CM_D2S || p.ldc % 8 == 0);
+  // CM_CHANDOT (SCA backward, NAFNet_arch.py:39-41): besides C, per-column partial sums over the tile's rows of
+  // C (bf16-rounded) * R (the SimpleGate output g) -> pre[image][tile within image][col] (fp32), the per-image channel
+  // dot img_chan_dot computes, without re-reading C.  The launcher guarantees BM | rows_per_img.
+  float cd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cd[j] = 0.f;
   for (int e = tid; e < BM * G8; e += 256) {
     const int row = e / G8, c8 = (e % G8) * 8;
     const int grow = m0 + row, gcol = n0 + c8;
@@ -280,6 +287,19 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
     float v[8];
     const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
     v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
+    if constexpr (CMODE == CM_CHANDOT) {
+      const long off = (long)grow * p.ldc + gcol;
+      float gv[8];
+      ld8f<TC>(p.R, off, gv);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = (__bf16)v[j];
+        cd[j] = fmaf((float)o[j], gv[j], cd[j]);
+      }
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(p.C) + off) = o;
+      continue;
+    }
     if (CMODE == CM_SGBWD) {
       // 8 gate channels -> 16 interleaved (t, dt) values
       const long off = (long)grow * p.ldc + 2 * gcol;
@@ -365,6 +385,25 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         if (CMODE != CM_MASK && p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
         stf<TC>(p.C, off, x);
       }
+    }
+  }
+  if constexpr (CMODE == CM_CHANDOT) {  // threads sharing a column chunk: lanes 8 apart, then the 4 waves (fixed order)
+    static_assert(G8 == 8 && BM == 64, "CM_CHANDOT: 64 x 64 tiles");
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cd[j] += __shfl_xor(cd[j], 8, 64);
+      cd[j] += __shfl_xor(cd[j], 16, 64);
+      cd[j] += __shfl_xor(cd[j], 32, 64);
+    }
+    __syncthreads();
+    if (lane < 8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Cs[wave * 64 + lane * 8 + j] = cd[j];
+    __syncthreads();
+    if (tid < 64 && n0 + tid < N) {
+      const int img = m0 / p.rows_per_img, chunk = (m0 - img * p.rows_per_img) / BM, chunks = p.rows_per_img / BM;
+      const float t = ((Cs[tid] + Cs[64 + tid]) + Cs[128 + tid]) + Cs[192 + tid];
+      reinterpret_cast<float*>(p.pre)[((long)img * chunks + chunk) * N + n0 + tid] = t;
     }
   }
 }
@@ -709,15 +748,19 @@ long gemm_minblk() {
 
 template <int AMODE, int CMODE, typename TA, typename TC>
 void dispatch(const GemmPB& p, hipStream_t st) {
-  auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
-  const bool n128 = p.N > 64, m128 = p.M > 64;
-  const long mb = gemm_minblk();
-  // (128 x 128 from 512 blocks won in isolation on M 16K-64K shapes, scripts/gemm_micro.py, but lost 0.3 ms/step in
-  // the training step: kept at >= 1024 blocks)
-  if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
-  else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
-  else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
-  else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
+  if constexpr (CMODE == CM_CHANDOT) {  // its partial-sum layout is per 64-row tile
+    launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
+  } else {
+    auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
+    const bool n128 = p.N > 64, m128 = p.M > 64;
+    const long mb = gemm_minblk();
+    // (128 x 128 from 512 blocks won in isolation on M 16K-64K shapes, scripts/gemm_micro.py, but lost 0.3 ms/step in
+    // the training step: kept at >= 1024 blocks)
+    if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
+    else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
+    else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
+    else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
+  }
 }
 
 // NBP_SKINNY=0 disables the skinny path (A/B measurement)
@@ -738,6 +781,7 @@ int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {
   else if (a_mode == AM_PLAIN && c_mode == CM_SG) dispatch<AM_PLAIN, CM_SG, TA, TC>(p, st);
   else if (a_mode == AM_SCALE && c_mode == CM_SGBWD) dispatch<AM_SCALE, CM_SGBWD, TA, TC>(p, st);
   else if (a_mode == AM_PLAIN && c_mode == CM_SGBWD) dispatch<AM_PLAIN, CM_SGBWD, TA, TC>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_CHANDOT) dispatch<AM_PLAIN, CM_CHANDOT, TA, TC>(p, st);
   else {
     set_error("nbp_gemm_bf16: unsupported mode combination");
     return NBP_ERR_ARG;
@@ -755,7 +799,12 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   NBP_REQUIRE(A && Bw && C && M > 0 && N > 0 && K > 0, "nbp_gemm_bf16: null pointer or empty shape");
   NBP_REQUIRE(K % 8 == 0 && N % 4 == 0 && ldb % 8 == 0, "nbp_gemm_bf16: K, ldb multiples of 8, N of 4 (K=%d N=%d)", K, N);
   NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && (c_mode == CM_PLAIN || c_mode == CM_D2S || c_mode == CM_SG ||
-              c_mode == CM_SGBWD), "nbp_gemm_bf16: mode");
+              c_mode == CM_SGBWD || c_mode == CM_CHANDOT), "nbp_gemm_bf16: mode");
+  NBP_REQUIRE(c_mode != CM_CHANDOT || (a_mode == AM_PLAIN && a_dtype == 1 && c_dtype == 1 && R && pre && !bias &&
+                                       rows_per_img > 0 && rows_per_img % 64 == 0 && M % rows_per_img == 0 &&
+                                       N % 8 == 0 && ldc % 8 == 0),
+              "nbp_gemm_bf16: channel-dot epilogue needs bf16, R (g), pre (the slab), rows_per_img a multiple of 64 "
+              "dividing M");
   NBP_REQUIRE(c_mode != CM_SG || (pre && N % 2 == 0 && ldc % 2 == 0 && !R),
               "nbp_gemm_bf16: SimpleGate epilogue needs pre (the gate map), even N and ldc, no residual");
   NBP_REQUIRE(c_mode != CM_SGBWD || (R && !bias && !pre && ldc >= 2L * N),

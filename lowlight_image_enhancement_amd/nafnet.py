@@ -32,6 +32,7 @@ from ._lib import call, query
 
 AM_PLAIN, AM_S2D, AM_SCALE = 0, 1, 2
 CM_SG, CM_SGBWD = 4, 5  # SimpleGate forward / backward fused into the GEMM epilogue (bf16 mode)
+CM_CHANDOT = 8  # dgrad with the SCA channel-dot partials in the epilogue (bf16 mode, C > 64)
 CM_PLAIN, CM_D2S = 0, 1
 LN_EPS = 1e-6
 
@@ -98,6 +99,8 @@ class NAFNet(nn.Module):
         self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
         # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
+        # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
+        self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
         self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
@@ -623,7 +626,15 @@ class NAFNet(nn.Module):
             self._reduce(sb, lg, c, self._slice(dflat, pre + "norm2.bias"))
         # y = x + beta * conv3(h), h = g (.) a: same layer-scale identity as conv5 (dh = (beta (.) dy) W3)
         dh = E(M, c)
-        if folded:
+        # tiled-GEMM levels (C > 64): the SCA channel dot sum_p dh (.) g rides in the dgrad epilogue (CM_CHANDOT,
+        # per-64-row-tile partials); levels 0/1 (skinny GEMM) keep img_chan_dot
+        chandot = folded and c > 64 and HW % 64 == 0 and self.fuse_chandot
+        if chandot:
+            chunks = HW // 64
+            da_slab = F(B * chunks * c)
+            call("gemm_bf16", dy, c, AM_PLAIN, None, HW, 1, self._slice(Wt[2], pre + "conv3.weight"), c, dh, c,
+                 CM_CHANDOT, 1, M, c, c, 0, 0, 0, None, S["g"], None, da_slab)
+        elif folded:
             self._mm(Wt, dy, c, AM_PLAIN, None, 1, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c, dgrad=True)
         else:
             self._mm(Wt, dy, c, AM_SCALE, self._slice(P, pre + "beta"), M, pre + "conv3.weight", dh, c, CM_PLAIN, M,
@@ -634,9 +645,10 @@ class NAFNet(nn.Module):
              self._slice(P, pre + "beta"), self._slice(dflat, pre + "conv3.weight"),
              self._slice(dflat, pre + "conv3.bias"), self._slice(dflat, pre + "beta"), c, c)
         # SCA
-        chunks = query("dw_chunks", B, h, w, c, 0)
-        da_slab = F(B * chunks * c)
-        call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
+        if not chandot:
+            chunks = query("dw_chunks", B, h, w, c, 0)
+            da_slab = F(B * chunks * c)
+            call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
         # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch
         ds = F(B, c)
         call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,

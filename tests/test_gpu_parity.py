@@ -633,6 +633,29 @@ def test_fused_ln_forward_network_bitwise(dev, monkeypatch):
         for k in ("n1", "st1", "y", "n2", "st2"):
             assert torch.equal(ra[3][k], rb[3][k]), (ra[1], k)
 
+@pytest.mark.parametrize("B,HW,C", [(16, 256, 512), (3, 1024, 256), (2, 4096, 128), (2, 64, 136)])
+def test_gemm_chandot_epilogue(dev, B, HW, C):
+    """conv3 dgrad with the SCA channel dot in the epilogue (CM_CHANDOT): C equals the plain dgrad bitwise, and the
+    per-tile partials summed per image equal sum_p bf16(dh) * g (float64)."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(B * HW + C)
+    M = B * HW
+    A = torch.randn(M, C, device=dev, generator=gen).to(torch.bfloat16)
+    Wt = (torch.randn(C, C, device=dev, generator=gen) / C ** 0.5).to(torch.bfloat16)
+    g = torch.randn(M, C, device=dev, generator=gen).to(torch.bfloat16)
+    d0, d1 = (torch.empty(M, C, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    call("gemm_bf16", A, C, 0, None, 1, 1, Wt, C, d0, C, 0, 1, M, C, C, 0, 0, 0, None, None, None, None)
+    chunks = HW // 64
+    slab = torch.full((B * chunks * C,), float("nan"), device=dev)
+    call("gemm_bf16", A, C, 0, None, HW, 1, Wt, C, d1, C, 8, 1, M, C, C, 0, 0, 0, None, g, None, slab)
+    if C % 64 == 0:
+        assert torch.equal(d1, d0)
+    else:  # the plain path may pick another tile shape; same values up to bf16 rounding
+        close(d1.float(), d0.float().cpu().numpy(), atol=2e-2, rtol=1e-2)
+    da = slab.view(B, chunks, C).double().sum(1)
+    ref = (d1.double() * g.double()).view(B, HW, C).sum(1)
+    close(da, ref.cpu().numpy(), atol=1e-3 * HW ** 0.5, rtol=1e-4)
+
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
 def test_dw_bwd_t2_recompute_matches_stored(dev, B, H, W, C, dtype):
     """The fused SCA/SimpleGate/depthwise backward that recomputes t2 = conv2(t1) + b in LDS (the forward then stores
