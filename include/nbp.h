@@ -119,6 +119,11 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);
 /* weight gradient dW[n][k] = sum_m G(m,n) X(m,k) (+ db[n] = sum_m G(m,n)): split over M, fixed-order slab reduce. */
 size_t nbp_wgrad_workspace_floats(int M, int N, int K);
+/* Grouping: between nbp_wgrad_group(1, s) and nbp_wgrad_group(0, s) the wide plain bf16 weight gradients
+ * (N, K multiples of 128, G and X row-major) issued on this thread are queued and launched together by the end call
+ * (one launch, each problem's tiles and results unchanged); the other forms launch at once.  The callers' slab
+ * reductions are queued as usual. */
+int nbp_wgrad_group(int begin, nbp_stream_t s);
 int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, int x_mode, const float* x_scale,
                   int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
                   float* ws, size_t ws_floats, int dtype, nbp_stream_t s);

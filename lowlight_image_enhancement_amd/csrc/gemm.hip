@@ -396,17 +396,17 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
 // Each operand tile lives in LDS as two 64-column panels with the conflict-free 96-element rows of
 // wgrad_bf16_kernel, read transposed by ds_read_b64_tr_b16.  Bias (column sums of G) from the loader's registers.
 template <int XMODE>
-__global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
+__device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by, int bz) {
   constexpr int RM = 64, LS = 96, PAN = RM * LS;
   __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PAN];  // G panels 0, 1; X panels 2, 3
   const __bf16* G = reinterpret_cast<const __bf16*>(p.G);
   const __bf16* X = reinterpret_cast<const __bf16*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
-  const int n0 = blockIdx.x * 128, k0 = blockIdx.y * 128, s = blockIdx.z;
+  const int n0 = bx * 128, k0 = by * 128, s = bz;
   const int mb = s * p.chunk;
   const int me = min(p.M, mb + p.chunk);
-  const bool do_b = p.slab_b && blockIdx.y == 0;
+  const bool do_b = p.slab_b && by == 0;
   floatx16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -542,6 +542,28 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
       p.slab_b[(long)s * p.N + n0 + tid] = t;
     }
   }
+}
+
+template <int XMODE>
+__global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
+  wgrad_wide_tile<XMODE>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Several independent wide weight gradients (plain X) in one launch: NAFBlock conv5 (U) and conv4 at the deep levels
+// run together (2 workgroups per CU instead of 1, one launch boundary fewer); each problem's tiles are exactly those
+// of its own launch (bitwise identical results).
+constexpr int WG_MAX = 4;
+struct WGroup {
+  WgradP p[WG_MAX];
+  int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
+  const int l = b - g.start[i], gx = g.gx[i], gy = g.gy[i];
+  wgrad_wide_tile<AM_PLAIN>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy));
 }
 
 // Column sums of a [S][L] fp32 slab.  A lane sums VEC adjacent columns (float4 loads when VEC = 4) over the rows
@@ -902,6 +924,30 @@ size_t nbp_wgrad_workspace_floats(int M, int N, int K) {
   return (size_t)S_ * N * K + (size_t)S_ * N;
 }
 
+thread_local bool g_wgroup = false;
+thread_local std::vector<WgradP> g_wqueue;
+
+void wgroup_launch(hipStream_t st) {
+  size_t i = 0;
+  while (i < g_wqueue.size()) {
+    WGroup g;
+    g.n = 0;
+    int blocks = 0;
+    for (; i < g_wqueue.size() && g.n < WG_MAX; ++i) {
+      const WgradP& p = g_wqueue[i];
+      g.p[g.n] = p;
+      g.gx[g.n] = p.N / 128;
+      g.gy[g.n] = p.K / 128;
+      g.start[g.n] = blocks;
+      blocks += g.gx[g.n] * g.gy[g.n] * cdiv(p.M, p.chunk);
+      ++g.n;
+    }
+    g.start[g.n] = blocks;
+    wgrad_bf16_wide_group<<<blocks, 256, 0, st>>>(g);
+  }
+  g_wqueue.clear();
+}
+
 int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, int x_mode, const float* x_scale,
                   int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
                   float* ws, size_t ws_floats, int dtype, nbp_stream_t s) {
@@ -929,7 +975,9 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
     const bool wide = wide_wgrad(N, K) && g_mode == AM_PLAIN &&
                       (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0));
     const dim3 wgrid(N / 128, K / 128, S_);
-    if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN><<<wgrid, 256, 0, st>>>(p);
+    // grouped only while the slab reductions are deferred (they must run after the queued launch)
+    if (wide && x_mode == AM_PLAIN && g_wgroup && g_defer) g_wqueue.push_back(p);  // nbp_wgrad_group(0, ...) launches
+    else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN><<<wgrid, 256, 0, st>>>(p);
     else if (wide) wgrad_bf16_wide<AM_SCALE><<<wgrid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
@@ -973,6 +1021,13 @@ int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const f
   }
   launch_post(std::vector<PDesc>{d}, S(s));
   return check_launch("layer_scale_grad");
+}
+
+int nbp_wgrad_group(int begin, nbp_stream_t s) {
+  NBP_REQUIRE(begin ? !g_wgroup : g_wgroup, "nbp_wgrad_group: unbalanced begin / end");
+  g_wgroup = begin != 0;
+  if (!begin) wgroup_launch(S(s));
+  return check_launch("wgrad_group");
 }
 
 int nbp_grad_reduce_defer(nbp_stream_t s) {

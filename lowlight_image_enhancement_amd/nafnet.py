@@ -101,6 +101,8 @@ class NAFNet(nn.Module):
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
         # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
         self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
+        # conv5 (U) and conv4 weight gradients as one grouped launch at C >= 128 (NBP_GROUP_WGRAD=0: two launches)
+        self.group_wgrad = os.environ.get("NBP_GROUP_WGRAD", "1") != "0"
         self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
@@ -601,6 +603,10 @@ class NAFNet(nn.Module):
             self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dg2, c, CM_PLAIN,
                      M, c, c, dgrad=True)
             call("sg_bwd", dg2, S["t4"], dt4, M, c, 1, dt)
+        # the two wide weight gradients that only need dout / dt4 run as one grouped launch (nbp_wgrad_group)
+        group = dt == 1 and c % 128 == 0 and self.group_wgrad and not self.overlap_wgrad
+        if group:
+            call("wgrad_group", 1)
         U5, V5 = F(c * c), F(c)
         self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
         call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
@@ -611,6 +617,8 @@ class NAFNet(nn.Module):
         dy = E(M, c)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
+        if group:
+            call("wgrad_group", 0)
         if fuse_ln:
             self._dgrad_ln(Wt, dflat, P, pre, "conv4.weight", "norm2", dt4, S["y"].reshape(M, c), S["st2"], dout, dy,
                            M, c)

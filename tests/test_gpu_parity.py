@@ -656,6 +656,26 @@ def test_gemm_chandot_epilogue(dev, B, HW, C):
     ref = (d1.double() * g.double()).view(B, HW, C).sum(1)
     close(da, ref.cpu().numpy(), atol=1e-3 * HW ** 0.5, rtol=1e-4)
 
+def test_grouped_wgrad_bitwise(dev):
+    """conv5 (U) + conv4 weight gradients as one grouped launch (C >= 128) give the same parameter gradients, bit
+    for bit, as two launches."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    torch.manual_seed(2)
+    net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[1, 1, 1], middle_blk_num=1,
+                           dec_blk_nums=[1, 1, 1]).to(dev)
+    net.precision = "bf16"
+    with torch.no_grad():
+        net.flat.add_(torch.randn_like(net.flat) * 0.05)
+    x = torch.rand(2, 3, 64, 64, device=dev)
+    grads = []
+    for grp in (True, False):
+        net.group_wgrad = grp
+        net.flat.grad = None
+        out = net(x)
+        out.square().mean().backward()
+        grads.append(net.flat.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
 def test_dw_bwd_t2_recompute_matches_stored(dev, B, H, W, C, dtype):
     """The fused SCA/SimpleGate/depthwise backward that recomputes t2 = conv2(t1) + b in LDS (the forward then stores
