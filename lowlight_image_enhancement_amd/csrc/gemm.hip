@@ -867,9 +867,10 @@ bool wide_wgrad(int N, int K) { return N % 128 == 0 && K % 128 == 0; }
 // split-M count: enough blocks to fill the chip (~2048), >= 256 rows per split, and fp32 slab bytes
 // (S * N * K * 4, written once and read once by the reduction) no larger than the operand bytes M * (N + K) * 2.
 int wgrad_splits(int M, int N, int K) {
-  if (wide_wgrad(N, K)) {  // 128 x 128 tiles: ~256 workgroups, >= 256 rows per split
+  if (wide_wgrad(N, K)) {  // 128 x 128 tiles: ~256 workgroups (NBP_WIDE_TARGET), >= 256 rows per split
+    static const long target = getenv("NBP_WIDE_TARGET") ? atol(getenv("NBP_WIDE_TARGET")) : 256;
     const long tiles = (long)(N / 128) * (K / 128);
-    long s = (256 + tiles - 1) / tiles;
+    long s = (target + tiles - 1) / tiles;
     const long maxs = M / 256 > 1 ? M / 256 : 1;
     if (s > maxs) s = maxs;
     return (int)(s > 1024 ? 1024 : s);
