@@ -570,14 +570,14 @@ __device__ __forceinline__ void unpack16(uint4 r, float* f) {
 // REC (with FUSED): t2 is not read from HBM either - the forward never stored it.  t1 is staged with a two-pixel
 // halo, t2 = bias + conv(t1) is recomputed into LDS on the one-pixel halo (the forward's FMA order), and the SCA /
 // SimpleGate backward turns it into dt2 in place.  Shorter tiles (TH 12) keep two blocks per CU.
-template <typename T, bool FUSED, int DWT_TW, bool REC>
+template <typename T, bool FUSED, int DWT_TW, bool REC, int THS = DWT_TH>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
   constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
   constexpr int HS = CSL / 2;            // gate channels per slice
   constexpr int NQ = CSL / 4;            // channel quads per slice
   constexpr int NT = NQ * DWT_TW;        // threads
-  constexpr int TH = REC ? DWT_TH_REC : DWT_TH;
+  constexpr int TH = REC ? DWT_TH_REC : THS;
   constexpr int XO = REC ? 1 : 0;        // extra t1 halo
   constexpr int LW = DWT_TW + 2, LH = TH + 2;
   constexpr int LWX = LW + 2 * XO, LHX = LH + 2 * XO;
@@ -789,17 +789,23 @@ struct DwFwdP {
 };
 // tile width: 64 / 32 / 16 columns by image width; fp32 (2 gate quads per slice) never below 32 (whole waves)
 inline int dw_fwd_tw(int W, int dtype) { return W >= 64 ? 64 : ((W >= 32 || dtype == 0) ? 32 : 16); }
-int dw_fwd_tiles(int H, int W, int dtype) { return cdiv(H, DWT_TH) * cdiv(W, dw_fwd_tw(W, dtype)); }
+// tile height: 16 rows, 8 at the small deep-level images (W <= 32: 2x the blocks, half of each thread's serial
+// row chain; the extra halo rows are L2 hits).  NBP_DW_FWD_TH overrides the small-image height (A/B measurement).
+inline int dw_fwd_th(int W) {
+  static const int small = getenv("NBP_DW_FWD_TH") ? atoi(getenv("NBP_DW_FWD_TH")) : 8;
+  return W <= 32 && (small == 4 || small == 8) ? small : DWT_TH;  // the instantiated heights
+}
+int dw_fwd_tiles(int H, int W, int dtype) { return cdiv(H, dw_fwd_th(W)) * cdiv(W, dw_fwd_tw(W, dtype)); }
 
-template <typename T, int TW>
+template <typename T, int TW, int TH = DWT_TH>
 __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   constexpr int E = 16 / sizeof(T), CSL = 64 / sizeof(T), HS = CSL / 2, NQG = HS / 4, NT = NQG * TW;
-  constexpr int LW = TW + 2, LH = DWT_TH + 2;
+  constexpr int LW = TW + 2, LH = TH + 2;
   __shared__ __attribute__((aligned(16))) T sx[LH * LW * CSL];
   const int tid = threadIdx.x;
   const int u = xcd_remap(blockIdx.x, gridDim.x);
   const int slice = u % p.slices, tile = (u / p.slices) % p.tiles, b = u / (p.slices * p.tiles);
-  const int y0 = (tile / p.tiles_x) * DWT_TH, x0 = (tile % p.tiles_x) * TW;
+  const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * TW;
   const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
   const long img = (long)b * H * W;
   const int cbase = slice * HS;
@@ -849,7 +855,7 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   float4 pacc = f4(0.f);
   const bool col_ok = x0 + x < W;
 #pragma unroll
-  for (int r = 0; r < DWT_TH; ++r) {
+  for (int r = 0; r < TH; ++r) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       xa[0][j] = xa[1][j]; xa[1][j] = xa[2][j];
@@ -897,7 +903,15 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   }
 }
 
-int dw_tiles(int H, int W, bool rec = false) { return cdiv(H, rec ? DWT_TH_REC : DWT_TH) * cdiv(W, dw_bwd_tw(W)); }
+// backward tile height: 16 rows; NBP_DW_BWD_TH=8 selects 8 at W <= 32 (measured neutral in the step: the shorter
+// row chain is offset by the doubled weight-gradient slab)
+inline int dw_bwd_th(int W) {
+  static const int small = getenv("NBP_DW_BWD_TH") ? atoi(getenv("NBP_DW_BWD_TH")) : 16;
+  return W <= 32 && small == 8 ? 8 : DWT_TH;  // the instantiated heights
+}
+int dw_tiles(int H, int W, bool rec = false) {
+  return cdiv(H, rec ? DWT_TH_REC : dw_bwd_th(W)) * cdiv(W, dw_bwd_tw(W));
+}
 bool dw_tiled_ok(int C, int dtype) { return C % (dtype == 1 ? 16 : 8) == 0; }
 
 int block_for_quads(int Q) {
@@ -944,10 +958,17 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   const bool fused = dh != nullptr;
   NBP_DISPATCH_T(dtype, {
     constexpr int NQ = (64 / sizeof(T)) / 4;
-    if (tw == 32) {
+    const bool th8 = !rec && dw_bwd_th(W) == 8;
+    if (tw == 32 && th8) {
+      if (fused) dw_bwd_tiled<T, true, 32, false, 8><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 32, false, 8><<<nblk, NQ * 32, 0, S(s)>>>(p);
+    } else if (tw == 32) {
       if (rec) dw_bwd_tiled<T, true, 32, true><<<nblk, NQ * 32, 0, S(s)>>>(p);
       else if (fused) dw_bwd_tiled<T, true, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
       else dw_bwd_tiled<T, false, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
+    } else if (th8) {
+      if (fused) dw_bwd_tiled<T, true, 16, false, 8><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 16, false, 8><<<nblk, NQ * 16, 0, S(s)>>>(p);
     } else {
       if (rec) dw_bwd_tiled<T, true, 16, true><<<nblk, NQ * 16, 0, S(s)>>>(p);
       else if (fused) dw_bwd_tiled<T, true, 16, false><<<nblk, NQ * 16, 0, S(s)>>>(p);
@@ -993,8 +1014,13 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
     NBP_DISPATCH_T(dtype, {
       constexpr int NQG = (32 / sizeof(T)) / 4;
       // whole waves only (the column reduction shuffles across all 64 lanes): fp32 uses TW >= 32
+      const int th = dw_fwd_th(W);
       if (tw == 64) dw_sg_pool_tiled<T, 64><<<nblk, NQG * 64, 0, S(s)>>>(p);
+      else if ((tw == 32 || NQG * 16 < 64) && th == 4) dw_sg_pool_tiled<T, 32, 4><<<nblk, NQG * 32, 0, S(s)>>>(p);
+      else if ((tw == 32 || NQG * 16 < 64) && th == 8) dw_sg_pool_tiled<T, 32, 8><<<nblk, NQG * 32, 0, S(s)>>>(p);
       else if (tw == 32 || NQG * 16 < 64) dw_sg_pool_tiled<T, 32><<<nblk, NQG * 32, 0, S(s)>>>(p);
+      else if (th == 4) dw_sg_pool_tiled<T, 16, 4><<<nblk, NQG * 16, 0, S(s)>>>(p);
+      else if (th == 8) dw_sg_pool_tiled<T, 16, 8><<<nblk, NQG * 16, 0, S(s)>>>(p);
       else dw_sg_pool_tiled<T, 16><<<nblk, NQG * 16, 0, S(s)>>>(p);
     });
     return check_launch("dw_sg_pool_tiled");
@@ -1083,7 +1109,8 @@ int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* 
 }
 
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
-  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * dw_tiles(H, W, true);
+  const size_t tr = dw_tiles(H, W, true), tp = dw_tiles(H, W, false);
+  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * (tr > tp ? tr : tp);
   return (a > t ? a : t) * 2 * C * 10;
 }
 
