@@ -107,7 +107,8 @@ size_t nbp_dgrad_ln_workspace_floats(long M, int N);
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
                      float* ws, size_t ws_floats, nbp_stream_t s);
-/* NAFBlock conv3 / conv5 (N = C in {32, 64}, K <= 128, bf16) with the next LayerNorm2d forward in the epilogue:
+/* NAFBlock conv3 / conv5 (N = C in {32, 64} on the skinny kernel with K <= 128, or 128 on 64 x 128 tiles; bf16) with
+ * the next LayerNorm2d forward in the epilogue:
  * C = R + rscale * (A W^T + bias) (the block's y / out, NAFNet_arch.py:70-78) and nout / stats = LN(C) exactly as
  * nbp_ln_fwd_nhwc computes them from the stored C (arch_util.py:266-275); C, nout row stride N. */
 int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,

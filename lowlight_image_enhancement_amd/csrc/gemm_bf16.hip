@@ -40,6 +40,12 @@ struct GemmPB {
   const void* R;
   const float* rscale;
   void* pre;
+  // CM_RESLN (tiled, N == BN == 128): the LayerNorm2d forward of each stored C row in the epilogue
+  const float* lnw;
+  const float* lnb;
+  void* nout;
+  float2* stats;
+  float eps;
 };
 
 __device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
@@ -369,6 +375,32 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         }
       }
       st8f<TC>(p.C, off, v);
+      if constexpr (CMODE == CM_RESLN) {  // the row's 16 chunks are 16 consecutive lanes (BN 128): group sums
+        static_assert(BN == 128, "CM_RESLN (tiled): full 128-column rows");
+        float xv[8], sm = 0.f, q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xv[j] = (float)(__bf16)v[j];
+          sm += xv[j];
+        }
+        sm = group_sum<16>(sm);
+        const float mu = sm / (float)N;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = xv[j] - mu;
+          q = fmaf(d, d, q);
+        }
+        q = group_sum<16>(q);
+        const float dd = sqrtf(q / (float)N + p.eps), inv = 1.f / dd;
+        const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4), b0 = ld4(p.lnb + gcol), b1 = ld4(p.lnb + gcol + 4);
+        const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const float lb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaf(lw[j], (xv[j] - mu) * inv, lb[j]);
+        st8f<TC>(p.nout, (long)grow * N + gcol, o);
+        if (gcol == 0) p.stats[grow] = make_float2(mu, dd);
+      }
     } else {
       for (int j = 0; j < 8 && gcol + j < N; ++j) {
         const int col = gcol + j;
@@ -856,9 +888,17 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s) {
   NBP_REQUIRE(A && Bw && C && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args");
-  NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
-              "nbp_gemm_res_ln: N must be 32 or 64, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
   NBP_REQUIRE(a_mode == AM_PLAIN || (a_mode == AM_SCALE && a_scale && rows_per_img > 0), "nbp_gemm_res_ln: a_mode");
+  if (N == 128) {  // 64 x 128 tiles of the tiled kernel: a whole row per tile
+    NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_gemm_res_ln: K, lda, ldb multiples of 8");
+    GemmPB p{A, lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb, C, N, M, N, K, 0, 0, 0, bias,
+             R, rscale, nullptr, lnw, lnb, nout, reinterpret_cast<float2*>(stats), eps};
+    if (a_mode == AM_SCALE) launch<64, 128, AM_SCALE, CM_RESLN, __bf16, __bf16>(p, S(s));
+    else launch<64, 128, AM_PLAIN, CM_RESLN, __bf16, __bf16>(p, S(s));
+    return check_launch("gemm_res_ln(tiled)");
+  }
+  NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
+              "nbp_gemm_res_ln: N must be 32, 64 or 128, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
   SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb,
             reinterpret_cast<__bf16*>(C), N, M, N, K, bias, reinterpret_cast<const __bf16*>(R), rscale, nullptr,
             nullptr, lnw, nullptr, nullptr, nullptr, lnb, reinterpret_cast<__bf16*>(nout),

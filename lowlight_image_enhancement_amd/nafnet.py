@@ -97,7 +97,7 @@ class NAFNet(nn.Module):
         # when no per-stage hook needs the gradient slices early, i.e. single-GPU)
         self.overlap_wgrad = int(os.environ.get("NBP_OVERLAP_WGRAD", "0"))
         self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
-        # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
+        # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64, 128} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
         # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
         self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
@@ -367,7 +367,7 @@ class NAFNet(nn.Module):
         return out, tape
 
     def _block_fwd(self, P, pre, x, B, h, w, c, tape, next_pre=None):
-        """One NAFBlock forward (NAFNet_arch.py:60-80).  At C in {32, 64} (bf16) the LayerNorms run in the epilogue
+        """One NAFBlock forward (NAFNet_arch.py:60-80).  At C in {32, 64, 128} (bf16) the LayerNorms run in the epilogue
         of the GEMM producing their input (nbp_gemm_res_ln): norm2 in conv3's, the next block's norm1 (next_pre)
         in conv5's; that block then takes (n1, st1) from self._ln_carry."""
         M = B * h * w
@@ -375,7 +375,7 @@ class NAFNet(nn.Module):
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
-        fuse_ln = self.fuse_ln_fwd and dt == 1 and c in (32, 64) and len(self._W) == 3
+        fuse_ln = self.fuse_ln_fwd and dt == 1 and c in (32, 64, 128) and len(self._W) == 3
         carry, self._ln_carry = self._ln_carry, None
         if carry is not None and carry[0] is x:
             n1, st1 = carry[1], carry[2]

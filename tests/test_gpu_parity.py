@@ -591,7 +591,8 @@ def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
     close(dlnb, dn.sum(0).cpu().numpy(), atol=2e-4 * M ** 0.5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("M,N,K,amode", [(4096, 32, 32, 2), (3001, 64, 64, 0), (777, 32, 64, 0), (65, 64, 128, 2)])
+@pytest.mark.parametrize("M,N,K,amode", [(4096, 32, 32, 2), (3001, 64, 64, 0), (777, 32, 64, 0), (65, 64, 128, 2),
+                                         (4096, 128, 128, 2), (3001, 128, 256, 0), (100, 128, 128, 0)])
 def test_gemm_res_ln_equals_gemm_then_ln_fwd(dev, M, N, K, amode):
     """conv3 / conv5 with the LayerNorm2d forward in the epilogue (nbp_gemm_res_ln) equals the skinny GEMM with the
     residual followed by the standalone ln_fwd_nhwc, bit for bit (same stored bf16 row, same summation order)."""
