@@ -46,6 +46,12 @@ struct GemmPB {
   void* nout;
   float2* stats;
   float eps;
+  // CM_LNBWD (tiled, N == BN == 128): R = the LN input x, stats_in = (mu, den), lnw, dres; LN weight / bias gradient
+  // partials per 64-row tile into slab_w / slab_b [M / 64][N]
+  const float2* stats_in;
+  const void* dres;
+  float* slab_w;
+  float* slab_b;
 };
 
 __device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
@@ -283,9 +289,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
   // CM_CHANDOT (SCA backward, NAFNet_arch.py:39-41): besides C, per-column partial sums over the tile's rows of
   // C (bf16-rounded) * R (the SimpleGate output g) -> pre[image][tile within image][col] (fp32), the per-image channel
   // dot img_chan_dot computes, without re-reading C.  The launcher guarantees BM | rows_per_img.
-  float cd[8];
+  float cd[8], cb[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) cd[j] = 0.f;
+  for (int j = 0; j < 8; ++j) cd[j] = cb[j] = 0.f;
   for (int e = tid; e < BM * G8; e += 256) {
     const int row = e / G8, c8 = (e % G8) * 8;
     const int grow = m0 + row, gcol = n0 + c8;
@@ -293,6 +299,35 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
     float v[8];
     const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
     v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
+    if constexpr (CMODE == CM_LNBWD) {  // dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * lnw
+      static_assert(BN == 128, "CM_LNBWD (tiled): full 128-column rows");
+      const long off = (long)grow * N + gcol;
+      float xv[8], rv[8];
+      ld8f<TC>(p.R, off, xv);
+      ld8f<TC>(p.dres, off, rv);
+      const float2 st = p.stats_in[grow];
+      const float inv = 1.f / st.y;
+      const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4);
+      const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float yh[8], sg = 0.f, sgy = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        yh[j] = (xv[j] - st.x) * inv;
+        const float gg = v[j] * lw[j];
+        sg += gg;
+        sgy = fmaf(gg, yh[j], sgy);
+        cd[j] = fmaf(v[j], yh[j], cd[j]);  // dlnw partial
+        cb[j] += v[j];                      // dlnb partial
+      }
+      sg = group_sum<16>(sg);
+      sgy = group_sum<16>(sgy);
+      const float mg = sg / (float)N, mgy = sgy / (float)N;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[j] * lw[j] - yh[j] * mgy - mg) * inv + rv[j];
+      st8f<TC>(p.C, off, o);
+      continue;
+    }
     if constexpr (CMODE == CM_CHANDOT) {
       const long off = (long)grow * p.ldc + gcol;
       float gv[8];
@@ -417,6 +452,29 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         if (CMODE != CM_MASK && p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
         stf<TC>(p.C, off, x);
       }
+    }
+  }
+  if constexpr (CMODE == CM_LNBWD) {  // threads sharing a column chunk: lanes 16 apart, then the 4 waves (fixed order)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cd[j] += __shfl_xor(cd[j], 16, 64);
+      cd[j] += __shfl_xor(cd[j], 32, 64);
+      cb[j] += __shfl_xor(cb[j], 16, 64);
+      cb[j] += __shfl_xor(cb[j], 32, 64);
+    }
+    __syncthreads();
+    if (lane < 16)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Cs[(wave * 2 + 0) * 128 + lane * 8 + j] = cd[j];
+        Cs[(wave * 2 + 1) * 128 + lane * 8 + j] = cb[j];
+      }
+    __syncthreads();
+    if (tid < 128) {
+      const float tw = ((Cs[0 * 128 + tid] + Cs[2 * 128 + tid]) + Cs[4 * 128 + tid]) + Cs[6 * 128 + tid];
+      const float tb = ((Cs[1 * 128 + tid] + Cs[3 * 128 + tid]) + Cs[5 * 128 + tid]) + Cs[7 * 128 + tid];
+      p.slab_w[(long)blockIdx.x * N + tid] = tw;
+      p.slab_b[(long)blockIdx.x * N + tid] = tb;
     }
   }
   if constexpr (CMODE == CM_CHANDOT) {  // threads sharing a column chunk: lanes 8 apart, then the 4 waves (fixed order)
@@ -863,12 +921,28 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   return check_launch("gemm_bf16");
 }
 
-size_t nbp_dgrad_ln_workspace_floats(long M, int N) { return (size_t)2 * skinny_blocks(M) * N; }
+size_t nbp_dgrad_ln_workspace_floats(long M, int N) {
+  return (size_t)2 * (N == 128 ? (M + 63) / 64 : skinny_blocks(M)) * N;
+}
 
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
                      float* ws, size_t ws_floats, nbp_stream_t s) {
   NBP_REQUIRE(A && Wt && x && stats && lnw && dres && dx && dlnw && dlnb && ws && M > 0, "nbp_dgrad_ln_bwd: bad args");
+  if (N == 128) {  // 64 x 128 tiles of the tiled kernel: a whole row per tile
+    NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_ln_bwd: K, lda, ldb multiples of 8");
+    const long nb = (M + 63) / 64;
+    NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
+    GemmPB p{A, lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb, dx, N, M, N, K, 0, 0, 0, nullptr, x,
+             nullptr, nullptr, lnw, nullptr, nullptr, nullptr, 0.f, reinterpret_cast<const float2*>(stats), dres, ws,
+             ws + nb * N};
+    launch<64, 128, AM_PLAIN, CM_LNBWD, __bf16, __bf16>(p, S(s));
+    int rc = check_launch("dgrad_ln_bwd(tiled)");
+    if (rc) return rc;
+    rc = nbp_reduce_slab(p.slab_w, (int)nb, N, dlnw, s);
+    if (rc) return rc;
+    return nbp_reduce_slab(p.slab_b, (int)nb, N, dlnb, s);
+  }
   NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
               "nbp_dgrad_ln_bwd: N must be 32 or 64, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
   const long nb = skinny_blocks(M);

@@ -101,6 +101,8 @@ class NAFNet(nn.Module):
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
         # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
         self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
+        # LayerNorm backward in the conv4 / conv1 dgrad epilogue at C = 128 (NBP_FUSE_LN_BWD128=0: standalone ln_bwd)
+        self.fuse_ln_bwd128 = os.environ.get("NBP_FUSE_LN_BWD128", "1") != "0"
         # conv5 (U) and conv4 weight gradients as one grouped launch at C >= 128 (NBP_GROUP_WGRAD=0: two launches)
         self.group_wgrad = os.environ.get("NBP_GROUP_WGRAD", "1") != "0"
         self._ln_carry = None
@@ -613,7 +615,8 @@ class NAFNet(nn.Module):
              self._slice(P, pre + "gamma"), self._slice(dflat, pre + "conv5.weight"),
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
         # conv4 input gradient + norm2 backward + residual
-        fuse_ln = dt == 1 and c in (32, 64)  # LN backward in the skinny dgrad's epilogue (dn2 never stored)
+        # LN backward in the dgrad's epilogue (dn never stored): skinny kernel at C 32 / 64, 64 x 128 tiles at 128
+        fuse_ln = dt == 1 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128))
         dy = E(M, c)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))

@@ -562,7 +562,8 @@ def test_gemm_bf16_skinny_path(dev, M, N, K):
     close(out.float(), ref.cpu().numpy(), **tol)
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 32, 64), (3000, 64, 128), (777, 32, 32)])
+@pytest.mark.parametrize("M,N,K", [(4096, 32, 64), (3000, 64, 128), (777, 32, 32), (4096, 128, 256), (3000, 128, 256),
+                                   (100, 128, 128)])
 def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
     """Fused 1x1-conv input gradient + LayerNorm2d backward + residual (skinny bf16 GEMM epilogue) vs float64 math on
     the same bf16 operands: dn = A W^T, dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * w."""
