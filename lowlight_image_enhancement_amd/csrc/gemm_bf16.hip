@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
     const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
     v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
     if constexpr (CMODE == CM_LNBWD) {  // dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * lnw
-      static_assert(BN == 128, "CM_LNBWD (tiled): full 128-column rows");
+      static_assert(BN == 128 || BN == 256, "CM_LNBWD (tiled): full-row tiles");
       const long off = (long)grow * N + gcol;
       float xv[8], rv[8];
       ld8f<TC>(p.R, off, xv);
@@ -319,8 +319,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         cd[j] = fmaf(v[j], yh[j], cd[j]);  // dlnw partial
         cb[j] += v[j];                      // dlnb partial
       }
-      sg = group_sum<16>(sg);
-      sgy = group_sum<16>(sgy);
+      sg = group_sum<G8>(sg);
+      sgy = group_sum<G8>(sgy);
       const float mg = sg / (float)N, mgy = sgy / (float)N;
       float o[8];
 #pragma unroll
@@ -410,22 +410,22 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         }
       }
       st8f<TC>(p.C, off, v);
-      if constexpr (CMODE == CM_RESLN) {  // the row's 16 chunks are 16 consecutive lanes (BN 128): group sums
-        static_assert(BN == 128, "CM_RESLN (tiled): full 128-column rows");
+      if constexpr (CMODE == CM_RESLN) {  // the row's G8 chunks are G8 consecutive lanes (BN = N): group sums
+        static_assert(BN == 128 || BN == 256, "CM_RESLN (tiled): full-row tiles");
         float xv[8], sm = 0.f, q = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xv[j] = (float)(__bf16)v[j];
           sm += xv[j];
         }
-        sm = group_sum<16>(sm);
+        sm = group_sum<G8>(sm);
         const float mu = sm / (float)N;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float d = xv[j] - mu;
           q = fmaf(d, d, q);
         }
-        q = group_sum<16>(q);
+        q = group_sum<G8>(q);
         const float dd = sqrtf(q / (float)N + p.eps), inv = 1.f / dd;
         const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4), b0 = ld4(p.lnb + gcol), b1 = ld4(p.lnb + gcol + 4);
         const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
@@ -454,25 +454,25 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       }
     }
   }
-  if constexpr (CMODE == CM_LNBWD) {  // threads sharing a column chunk: lanes 16 apart, then the 4 waves (fixed order)
+  if constexpr (CMODE == CM_LNBWD) {  // threads sharing a column chunk: lanes G8 apart, then the 4 waves (fixed order)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      cd[j] += __shfl_xor(cd[j], 16, 64);
-      cd[j] += __shfl_xor(cd[j], 32, 64);
-      cb[j] += __shfl_xor(cb[j], 16, 64);
-      cb[j] += __shfl_xor(cb[j], 32, 64);
-    }
-    __syncthreads();
-    if (lane < 16)
+    for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Cs[(wave * 2 + 0) * 128 + lane * 8 + j] = cd[j];
-        Cs[(wave * 2 + 1) * 128 + lane * 8 + j] = cb[j];
+      for (int o = G8; o < 64; o <<= 1) {
+        cd[j] += __shfl_xor(cd[j], o, 64);
+        cb[j] += __shfl_xor(cb[j], o, 64);
       }
     __syncthreads();
-    if (tid < 128) {
-      const float tw = ((Cs[0 * 128 + tid] + Cs[2 * 128 + tid]) + Cs[4 * 128 + tid]) + Cs[6 * 128 + tid];
-      const float tb = ((Cs[1 * 128 + tid] + Cs[3 * 128 + tid]) + Cs[5 * 128 + tid]) + Cs[7 * 128 + tid];
+    if (lane < G8)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Cs[(wave * 2 + 0) * BN + lane * 8 + j] = cd[j];
+        Cs[(wave * 2 + 1) * BN + lane * 8 + j] = cb[j];
+      }
+    __syncthreads();
+    if (tid < BN) {
+      const float tw = ((Cs[0 * BN + tid] + Cs[2 * BN + tid]) + Cs[4 * BN + tid]) + Cs[6 * BN + tid];
+      const float tb = ((Cs[1 * BN + tid] + Cs[3 * BN + tid]) + Cs[5 * BN + tid]) + Cs[7 * BN + tid];
       p.slab_w[(long)blockIdx.x * N + tid] = tw;
       p.slab_b[(long)blockIdx.x * N + tid] = tb;
     }
@@ -922,21 +922,22 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
 }
 
 size_t nbp_dgrad_ln_workspace_floats(long M, int N) {
-  return (size_t)2 * (N == 128 ? (M + 63) / 64 : skinny_blocks(M)) * N;
+  return (size_t)2 * (N == 128 || N == 256 ? (M + 63) / 64 : skinny_blocks(M)) * N;
 }
 
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
                      float* ws, size_t ws_floats, nbp_stream_t s) {
   NBP_REQUIRE(A && Wt && x && stats && lnw && dres && dx && dlnw && dlnb && ws && M > 0, "nbp_dgrad_ln_bwd: bad args");
-  if (N == 128) {  // 64 x 128 tiles of the tiled kernel: a whole row per tile
+  if (N == 128 || N == 256) {  // 64 x N tiles of the tiled kernel: a whole row per tile
     NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_ln_bwd: K, lda, ldb multiples of 8");
     const long nb = (M + 63) / 64;
     NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
     GemmPB p{A, lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb, dx, N, M, N, K, 0, 0, 0, nullptr, x,
              nullptr, nullptr, lnw, nullptr, nullptr, nullptr, 0.f, reinterpret_cast<const float2*>(stats), dres, ws,
              ws + nb * N};
-    launch<64, 128, AM_PLAIN, CM_LNBWD, __bf16, __bf16>(p, S(s));
+    if (N == 256) launch<64, 256, AM_PLAIN, CM_LNBWD, __bf16, __bf16>(p, S(s));
+    else launch<64, 128, AM_PLAIN, CM_LNBWD, __bf16, __bf16>(p, S(s));
     int rc = check_launch("dgrad_ln_bwd(tiled)");
     if (rc) return rc;
     rc = nbp_reduce_slab(p.slab_w, (int)nb, N, dlnw, s);
@@ -963,11 +964,13 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s) {
   NBP_REQUIRE(A && Bw && C && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args");
   NBP_REQUIRE(a_mode == AM_PLAIN || (a_mode == AM_SCALE && a_scale && rows_per_img > 0), "nbp_gemm_res_ln: a_mode");
-  if (N == 128) {  // 64 x 128 tiles of the tiled kernel: a whole row per tile
+  if (N == 128 || N == 256) {  // 64 x N tiles of the tiled kernel: a whole row per tile
     NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_gemm_res_ln: K, lda, ldb multiples of 8");
     GemmPB p{A, lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb, C, N, M, N, K, 0, 0, 0, bias,
              R, rscale, nullptr, lnw, lnb, nout, reinterpret_cast<float2*>(stats), eps};
-    if (a_mode == AM_SCALE) launch<64, 128, AM_SCALE, CM_RESLN, __bf16, __bf16>(p, S(s));
+    if (N == 256 && a_mode == AM_SCALE) launch<64, 256, AM_SCALE, CM_RESLN, __bf16, __bf16>(p, S(s));
+    else if (N == 256) launch<64, 256, AM_PLAIN, CM_RESLN, __bf16, __bf16>(p, S(s));
+    else if (a_mode == AM_SCALE) launch<64, 128, AM_SCALE, CM_RESLN, __bf16, __bf16>(p, S(s));
     else launch<64, 128, AM_PLAIN, CM_RESLN, __bf16, __bf16>(p, S(s));
     return check_launch("gemm_res_ln(tiled)");
   }
