@@ -64,7 +64,10 @@ def _pmc_traffic(cls):
     """HBM bytes per launch of a kernel class from the newest committed PMC record (profiles/*pmc_traffic.json,
     scripts/pmc_pass.sh + scripts/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    import re
+    # newest record by version number (natural order: r01_v10 after r01_v9)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")),
+                   key=lambda f: [int(t) for t in re.findall(r"\d+", os.path.basename(f))])
     if not files:
         return None, None
     rec = json.load(open(files[-1])).get("classes", {}).get(cls)
