@@ -103,8 +103,9 @@ class NAFNet(nn.Module):
         self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
         # LayerNorm backward in the conv4 / conv1 dgrad epilogue at C = 128 (NBP_FUSE_LN_BWD128=0: standalone ln_bwd)
         self.fuse_ln_bwd128 = os.environ.get("NBP_FUSE_LN_BWD128", "1") != "0"
-        # both LayerNorm fusions at C = 256 too (64 x 256 tiles, one workgroup per CU; NBP_FUSE_LN256=1)
-        self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "0") == "1"
+        # the LayerNorm fusions at C = 256 too (64 x 256 tiles, one workgroup per CU): NBP_FUSE_LN256 = bwd (default:
+        # +0.35 %), 1 (both), fwd (-0.4 %) or 0
+        self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "bwd")
         # conv5 (U) and conv4 weight gradients as one grouped launch at C >= 128 (NBP_GROUP_WGRAD=0: two launches)
         self.group_wgrad = os.environ.get("NBP_GROUP_WGRAD", "1") != "0"
         self._ln_carry = None
@@ -380,7 +381,7 @@ class NAFNet(nn.Module):
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
         fuse_ln = self.fuse_ln_fwd and dt == 1 and len(self._W) == 3 and (c in (32, 64, 128) or
-                                                                           (c == 256 and self.fuse_ln256))
+                                                                           (c == 256 and self.fuse_ln256 in ("1", "fwd")))
         carry, self._ln_carry = self._ln_carry, None
         if carry is not None and carry[0] is x:
             n1, st1 = carry[1], carry[2]
@@ -619,7 +620,8 @@ class NAFNet(nn.Module):
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
         # conv4 input gradient + norm2 backward + residual
         # LN backward in the dgrad's epilogue (dn never stored): skinny kernel at C 32 / 64, 64 x 128 tiles at 128
-        fuse_ln = dt == 1 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or (c == 256 and self.fuse_ln256))
+        fuse_ln = dt == 1 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
+                               (c == 256 and self.fuse_ln256 in ("1", "bwd")))
         dy = E(M, c)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
