@@ -114,6 +114,13 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
 int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s);
+/* conv5 input gradient + SimpleGate backward with the gate input recomputed (bf16, N = K = C = 32: level 0, whose conv4
+ * forward runs on the same skinny MFMA sequence): dg = A . Wt^T (the conv5 dgrad), t = A2 . W2^T + b2 rebuilt per tile (the conv4 forward: A2 = its input n2 [M][K],
+ * W2 [2N][K] bf16 with SimpleGate pairs interleaved, b2 fp32), C[m][2c] = dg[c] t[2c+1], C[m][2c+1] = dg[c] t[2c]
+ * (NAFNet_arch.py:22-25, 76-78); equals CM_SGBWD on the stored t bit for bit.  The forward then skips storing t
+ * (nbp_gemm_bf16 CM_SG with C = NULL). */
+int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,
+                    void* C, int M, int N, int K, nbp_stream_t s);
 /* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols, scale_offset} (int64, device)
  * out_t[offset..] = bf16(diag(s) . flat matrix)^T with s = flat[scale_offset..] (rows values), or no scaling when
  * scale_offset < 0 (the NAFBlock layer scales folded into the conv3 / conv5 dgrad operands). */

@@ -23,7 +23,7 @@ namespace {
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
 enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7,
-       CM_CHANDOT = 8 };
+       CM_CHANDOT = 8, CM_SGBWD_RC = 9 };
 
 struct GemmPB {
   const void* A;
@@ -533,15 +533,49 @@ struct SkinnyP {
   __bf16* nout;
   float2* stats_out;
   float eps;
+  // CM_SGBWD_RC (SimpleGate backward with the gate input recomputed): t = A2 W2^T + b2 (the conv4 forward, its
+  // output rows interleaved as stored, 2N columns) is rebuilt per tile on MFMA instead of being read from memory
+  const __bf16* A2;
+  const __bf16* W2;
+  const float* b2;
 };
 
 template <int NT, int KS, int AMODE, int CMODE>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
   constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
+  constexpr bool RC = CMODE == CM_SGBWD_RC;
+  constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : 8;  // bf16 row stride of the recomputed gate-input tile
   __shared__ float stage[4][32 * LDT];
+  __shared__ __attribute__((aligned(16))) __bf16 stage2[4][32 * LDT2];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   float* tileS = stage[threadIdx.x >> 6];
+  __bf16* tileT = stage2[threadIdx.x >> 6];
   const int M = p.M, N = p.N, K = p.K;
+  // RC: the conv4 weight (2N rows, K = the conv4 input width = this GEMM's K) and bias in registers
+  constexpr int NT2 = RC ? 2 * NT : 1;
+  bf16x8 w2[NT2][KS];
+  float b2r[NT2][4][4];
+  if constexpr (RC) {
+#pragma unroll
+    for (int t = 0; t < NT2; ++t) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int n = t * 32 + r, k = ks * 16 + 8 * h;
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+        if (n < 2 * N && k < K) v = *reinterpret_cast<const bf16x8*>(p.W2 + (long)n * K + k);
+        w2[t][ks] = v;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = t * 32 + 8 * g + 4 * h + q;
+          b2r[t][g][q] = c < 2 * N ? p.b2[c] : 0.f;
+        }
+    }
+  }
   bf16x8 w[NT][KS];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -556,7 +590,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
     }
   // coalesced epilogue geometry: chunks of 8 output elements, row-major over the 32-row tile.  The output row holds
   // N elements (2N for the SimpleGate backward), so a lane's chunk column is fixed across its chunks.
-  const int outw = (CMODE == CM_SGBWD ? 2 : 1) * N;
+  const int outw = (CMODE == CM_SGBWD || RC ? 2 : 1) * N;
   const int cpr = outw / 8;                                    // chunks per row (divides 64: outw in {8..128})
   const int ccol = (lane % cpr) * 8;                           // this lane's output column
   const int rstep = 64 / cpr;                                  // rows advanced per pass
@@ -571,7 +605,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
   if (CMODE == CM_LNBWD) {  // rsc holds the LN weight of this lane's 8 columns
     const float4 s0 = ld4(p.lnw + ccol), s1 = ld4(p.lnw + ccol + 4);
     rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
-  } else if (CMODE != CM_SGBWD) {
+  } else if (CMODE != CM_SGBWD && !RC) {
     if (p.bias) {
       const float4 b0 = ld4(p.bias + ccol), b1 = ld4(p.bias + ccol + 4);
       bia[0] = b0.x; bia[1] = b0.y; bia[2] = b0.z; bia[3] = b0.w; bia[4] = b1.x; bia[5] = b1.y; bia[6] = b1.z; bia[7] = b1.w;
@@ -604,11 +638,29 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
       a[ks] = v;
     }
   };
-  bf16x8 a0[KS], a1[KS];
+  auto load_a2 = [&](long tile, bf16x8* a) {  // RC: the conv4 input rows (plain, row stride K)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const long m = tile * 32 + r;
+      const int k = ks * 16 + 8 * h;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      if (m < M && k < K) v = *reinterpret_cast<const bf16x8*>(p.A2 + m * K + k);
+      a[ks] = v;
+    }
+  };
+  bf16x8 a0[KS], a1[KS], c0[RC ? KS : 1], c1[RC ? KS : 1];
   long tile = wave;
-  if (tile < ntiles) load_a(tile, a0);
+  if (tile < ntiles) {
+    load_a(tile, a0);
+    if constexpr (RC) load_a2(tile, c0);
+  }
   for (; tile < ntiles; tile += nwaves) {
-    if (tile + nwaves < ntiles) load_a(tile + nwaves, a1);
+    if (tile + nwaves < ntiles) {
+      load_a(tile + nwaves, a1);
+      if constexpr (RC) load_a2(tile + nwaves, c1);
+    }
     floatx16 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -625,15 +677,33 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<float4*>(tileS + r * LDT + t * 32 + 8 * g + 4 * h) =
             make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+    if constexpr (RC) {  // t = bf16(A2 W2^T + b2) exactly as the conv4 forward stored it (same MFMA sequence)
+#pragma unroll
+      for (int t = 0; t < NT2; ++t) {
+        floatx16 a2c;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a2c[i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a2c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[t][ks], c0[ks], a2c, 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (__bf16)(a2c[4 * g + q] + b2r[t][g][q]);
+          *reinterpret_cast<bf16x4*>(tileT + r * LDT2 + t * 32 + 8 * g + 4 * h) = o;
+        }
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     const long m0 = tile * 32;
     for (int rr = lane / cpr; rr < 32; rr += rstep) {
       const long m = m0 + rr;
       if (m >= M) break;
-      if (CMODE == CM_SGBWD) {  // chunk = 4 gates (interleaved pairs): dg from the tile, t from R
+      if (CMODE == CM_SGBWD || RC) {  // chunk = 4 gates (interleaved pairs): dg from the tile, t from R (or rebuilt)
         const float4 dg = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol / 2);
         const long off = m * p.ldc + ccol;
-        const bf16x8 tv = *reinterpret_cast<const bf16x8*>(p.R + off);
+        const bf16x8 tv = RC ? *reinterpret_cast<const bf16x8*>(tileT + rr * LDT2 + ccol)
+                             : *reinterpret_cast<const bf16x8*>(p.R + off);
         const float d[4] = {dg.x, dg.y, dg.z, dg.w};
         bf16x8 o;
 #pragma unroll
@@ -684,7 +754,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
-      *reinterpret_cast<bf16x8*>(p.C + off) = o;
+      if (CMODE != CM_SG || p.C) *reinterpret_cast<bf16x8*>(p.C + off) = o;  // SG: t may be dropped (recomputed)
       if constexpr (CMODE == CM_RESLN) {  // LayerNorm2d of the stored (bf16) row, as ln_fwd_nhwc computes it
         constexpr int G = 4 * NT;
         float xv[8], sm = 0.f, q = 0.f;
@@ -718,6 +788,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) a0[ks] = a1[ks];
+    if constexpr (RC)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) c0[ks] = c1[ks];
   }
   if constexpr (CMODE == CM_LNBWD) {  // LN weight / bias gradient partials: lanes sharing ccol, then the 4 waves
     constexpr int G = 4 * NT;
@@ -886,7 +959,10 @@ extern "C" {
 int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, int a_dtype,
                   const void* Bw, long ldb, void* C, long ldc, int c_mode, int c_dtype, int M, int N, int K, int gh,
                   int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s) {
-  NBP_REQUIRE(A && Bw && C && M > 0 && N > 0 && K > 0, "nbp_gemm_bf16: null pointer or empty shape");
+  NBP_REQUIRE(A && Bw && M > 0 && N > 0 && K > 0, "nbp_gemm_bf16: null pointer or empty shape");
+  // C may be null only for the skinny SimpleGate forward (the gate input is then recomputed by the backward)
+  NBP_REQUIRE(C || (c_mode == CM_SG && a_dtype == 1 && c_dtype == 1 && N <= 64 && K <= 128 && getenv_skinny()),
+              "nbp_gemm_bf16: C is null");
   NBP_REQUIRE(K % 8 == 0 && N % 4 == 0 && ldb % 8 == 0, "nbp_gemm_bf16: K, ldb multiples of 8, N of 4 (K=%d N=%d)", K, N);
   NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && (c_mode == CM_PLAIN || c_mode == CM_D2S || c_mode == CM_SG ||
               c_mode == CM_SGBWD || c_mode == CM_CHANDOT), "nbp_gemm_bf16: mode");
@@ -912,6 +988,7 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   if (a_dtype == 1 && c_dtype == 1 && getenv_skinny() &&
       try_skinny(A, lda, a_mode, a_scale, rows_per_img, Bw, ldb, C, ldc, c_mode, M, N, K, bias, R, rscale, pre, st))
     return check_launch("gemm_bf16(skinny)");
+  NBP_REQUIRE(C, "nbp_gemm_bf16: C is null and the skinny path does not serve this shape");
   int rc;
   if (a_dtype == 0 && c_dtype == 0) rc = dispatch_modes<float, float>(p, a_mode, c_mode, st);
   else if (a_dtype == 1 && c_dtype == 1) rc = dispatch_modes<__bf16, __bf16>(p, a_mode, c_mode, st);
@@ -983,6 +1060,19 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
   if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_RESLN>(p, S(s));
   else launch_skinny<AM_PLAIN, CM_RESLN>(p, S(s));
   return check_launch("gemm_res_ln");
+}
+
+int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,
+                    void* C, int M, int N, int K, nbp_stream_t s) {
+  NBP_REQUIRE(A && Wt && A2 && W2 && b2 && C && M > 0, "nbp_dgrad_sg_rc: bad args");
+  NBP_REQUIRE(N == 32 && K == 32 && lda % 8 == 0 && ldb % 8 == 0,
+              "nbp_dgrad_sg_rc: N = K = 32 (N=%d K=%d)", N, K);
+  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb,
+            reinterpret_cast<__bf16*>(C), 2L * N, M, N, K, nullptr, nullptr, nullptr, nullptr,
+            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
+            reinterpret_cast<const __bf16*>(A2), reinterpret_cast<const __bf16*>(W2), b2};
+  gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
+  return check_launch("dgrad_sg_rc");
 }
 
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s) {

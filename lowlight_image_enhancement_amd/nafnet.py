@@ -108,6 +108,9 @@ class NAFNet(nn.Module):
         self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "bwd")
         # conv5 (U) and conv4 weight gradients as one grouped launch at C >= 128 (NBP_GROUP_WGRAD=0: two launches)
         self.group_wgrad = os.environ.get("NBP_GROUP_WGRAD", "1") != "0"
+        # level 0 (C = 32): the conv4 output t4 is not stored; the conv5 dgrad rebuilds it per tile on MFMA
+        # (nbp_dgrad_sg_rc, bitwise equal) -- NBP_SG_RC=0 stores and re-reads it
+        self.sg_rc = os.environ.get("NBP_SG_RC", "1") != "0"
         self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
@@ -413,7 +416,10 @@ class NAFNet(nn.Module):
                      bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
             call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2,
                  M, c, LN_EPS, dt)
-        t4, g2 = E(M, 2 * c), E(M, c)  # t4 channel pairs interleaved (conv4 rows stored so)
+        # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
+        # it (sg_rc) or there is no backward
+        drop_t4 = dt == 1 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) == 3))
+        t4, g2 = (None if drop_t4 else E(M, 2 * c)), E(M, c)
         if dt == 1:  # SimpleGate in the GEMM epilogue
             self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
                      bias=self._slice(P, pre + "conv4.bias"), pre=g2)
@@ -598,7 +604,11 @@ class NAFNet(nn.Module):
         dt4 = E(M, 2 * c)
         folded = len(Wt) == 3 and self.fold_ls  # gamma / beta already in the transposed bf16 weights
         if dt == 1:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises
-            if folded:
+            if S["t4"] is None:  # t4 = conv4(n2) rebuilt per tile inside the dgrad (level 0, folded layer scale)
+                assert folded and c == 32
+                call("dgrad_sg_rc", dout, c, self._slice(Wt[2], pre + "conv5.weight"), c, S["n2"],
+                     self._slice(Wt[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"), dt4, M, c, c)
+            elif folded:
                 self._mm(Wt, dout, c, AM_PLAIN, None, 1, pre + "conv5.weight", dt4, 2 * c, CM_SGBWD, M, c, c,
                          R=S["t4"], dgrad=True)
             else:

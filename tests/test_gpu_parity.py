@@ -679,6 +679,56 @@ def test_grouped_wgrad_bitwise(dev):
         grads.append(net.flat.grad.clone())
     assert torch.equal(grads[0], grads[1])
 
+@pytest.mark.parametrize("M", [32, 2 * 37 * 41, 64 * 96])
+def test_dgrad_sg_recompute_matches_stored(dev, M):
+    """conv5 dgrad + SimpleGate backward with t4 = conv4(n2) rebuilt per tile (nbp_dgrad_sg_rc) equals the CM_SGBWD
+    epilogue reading the t4 the skinny conv4 forward stored, bit for bit; the forward with C = NULL still writes the
+    same gate map g2."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M)
+    c = 32
+    n2 = torch.randn(M, c, device=dev, generator=gen).to(torch.bfloat16)
+    W4 = (torch.randn(2 * c, c, device=dev, generator=gen) / c ** 0.5).to(torch.bfloat16)
+    b4 = torch.randn(2 * c, device=dev, generator=gen) * 0.1
+    t4 = torch.empty(M, 2 * c, device=dev, dtype=torch.bfloat16)
+    g2, g2b = (torch.empty(M, c, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    call("gemm_bf16", n2, c, 0, None, 1, 1, W4, c, t4, 2 * c, 4, 1, M, 2 * c, c, 0, 0, 0, b4, None, None, g2)
+    call("gemm_bf16", n2, c, 0, None, 1, 1, W4, c, None, 2 * c, 4, 1, M, 2 * c, c, 0, 0, 0, b4, None, None, g2b)
+    assert torch.equal(g2, g2b)
+    dout = torch.randn(M, c, device=dev, generator=gen).to(torch.bfloat16)
+    W5t = (torch.randn(c, c, device=dev, generator=gen) / c ** 0.5).to(torch.bfloat16)
+    d0, d1 = (torch.full((M, 2 * c), float("nan"), device=dev, dtype=torch.bfloat16) for _ in range(2))
+    call("gemm_bf16", dout, c, 0, None, 1, 1, W5t, c, d0, 2 * c, 5, 1, M, c, c, 0, 0, 0, None, t4, None, None)
+    call("dgrad_sg_rc", dout, c, W5t, c, n2, W4, b4, d1, M, c, c)
+    assert torch.equal(d0, d1)
+    # and against float64: dt4[2j] = dg[j] t[2j+1], dt4[2j+1] = dg[j] t[2j]
+    dg = dout.double() @ W5t.double().t()
+    ref = torch.stack([dg * t4.double()[:, 1::2], dg * t4.double()[:, 0::2]], -1).reshape(M, 2 * c)
+    close(d1.float(), ref.float().cpu().numpy(), atol=2e-2, rtol=1e-2)
+
+
+def test_sg_recompute_network_bitwise(dev):
+    """Whole bf16 training backward with t4 dropped at level 0 and rebuilt in the conv5 dgrad (default) vs stored:
+    identical parameter gradients."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    torch.manual_seed(3)
+    net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[2, 1], middle_blk_num=1,
+                           dec_blk_nums=[1, 2]).to(dev)
+    net.precision = "bf16"
+    with torch.no_grad():
+        net.flat.add_(torch.randn_like(net.flat) * 0.05)
+    x = torch.rand(2, 3, 48, 80, device=dev)
+    grads = []
+    for rc in (True, False):
+        net.sg_rc = rc
+        net.flat.grad = None
+        out = net(x)
+        out.square().mean().backward()
+        grads.append((out.detach().clone(), net.flat.grad.clone()))
+    assert torch.equal(grads[0][0], grads[1][0])
+    assert torch.equal(grads[0][1], grads[1][1])
+
+
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
 def test_dw_bwd_t2_recompute_matches_stored(dev, B, H, W, C, dtype):
     """The fused SCA/SimpleGate/depthwise backward that recomputes t2 = conv2(t1) + b in LDS (the forward then stores
