@@ -672,12 +672,22 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   }
   if (FUSED) {
     if (REC) __syncthreads();
+    // NT is even, so this thread's chunk k = tid & 1 (and its E channels) is the same in every pass: a and ds / HW once
+    static_assert(NT % 2 == 0, "chunk parity per thread");
+    float ak[E], sk[E];
+    {
+      const int c = cbase + (tid & 1) * E;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        ak[j] = p.a[(long)b * C + c + j];
+        sk[j] = p.ds[(long)b * C + c + j] * p.inv_hw;
+      }
+    }
 #pragma unroll
     for (int it = 0; it < N2; ++it) {
       const int i = tid + it * NT;
       if (i >= TOT2) continue;
       const int pix = i >> 1, k = i & 1;
-      const int c = cbase + k * E;
       const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
       const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
       float d[E], ta[E], tb[E], lo[E], hi[E];
@@ -689,11 +699,9 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
         unpack16<T>(ra[it], ta);
         unpack16<T>(rb[it], tb);
       }
-      const float* av = p.a + (long)b * C + c;
-      const float* sv = p.ds + (long)b * C + c;
 #pragma unroll
       for (int j = 0; j < E; ++j) {
-        const float dg = inside ? fmaf(d[j], av[j], sv[j] * p.inv_hw) : 0.f;
+        const float dg = inside ? fmaf(d[j], ak[j], sk[j]) : 0.f;
         lo[j] = dg * tb[j];
         hi[j] = dg * ta[j];
       }

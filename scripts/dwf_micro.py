@@ -24,7 +24,7 @@ for (B, H, W, C) in [(16, 256, 256, 32), (16, 128, 128, 64), (16, 64, 64, 128), 
           flush=True)
 
 # backward (fused SCA / SimpleGate / depthwise) at the same shapes
-for (B, H, W, C) in [(16, 64, 64, 128), (16, 32, 32, 256), (16, 16, 16, 512)]:
+for (B, H, W, C) in [(16, 256, 256, 32), (16, 128, 128, 64), (16, 64, 64, 128), (16, 32, 32, 256), (16, 16, 16, 512)]:
     M = B * H * W
     t1, t2 = (torch.randn(M, 2 * C, device=dev).to(torch.bfloat16) for _ in range(2))
     dh = torch.randn(M, C, device=dev).to(torch.bfloat16)
