@@ -822,7 +822,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 long skinny_blocks(long M) {
   const long ntiles = (M + 31) / 32;
   const long blocks = (ntiles + 3) / 4;
-  return blocks > 1024 ? 1024 : blocks;  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs
+  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs (NBP_SKINNY_BLOCKS overrides: A/B measurement)
+  static const long cap = getenv("NBP_SKINNY_BLOCKS") ? atol(getenv("NBP_SKINNY_BLOCKS")) : 1024L;
+  return blocks > cap ? cap : blocks;
 }
 
 // K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads)

@@ -727,6 +727,10 @@ def test_sg_recompute_network_bitwise(dev):
         grads.append((out.detach().clone(), net.flat.grad.clone()))
     assert torch.equal(grads[0][0], grads[1][0])
     assert torch.equal(grads[0][1], grads[1][1])
+    # inference (no tape): the level-0 conv4 forward writes only the gate map (C = NULL); same output
+    out_nt, _ = net.exec_forward(x, save=False)
+    out_t, _ = net.exec_forward(x, save=True)
+    assert torch.equal(out_nt, out_t)
 
 
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
