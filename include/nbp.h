@@ -325,17 +325,26 @@ int nbp_feat_dist_bwd(const void* a, const void* b, long n, int mode, float scal
                       void* da, nbp_stream_t s);
 
 /* ------------------------------------------------------------------ optimizer (image_restoration_model.py:313-320) */
-/* clip_grad_norm_(params, max_norm): state[0] = ||grad*grad_scale||, state[1] = clip coef * grad_scale. */
+/* Everything between backward and the AdamW update, decided on the device (no host sync, graph-replayable):
+   GradScaler.unscale_ + clip_grad_norm_(params, max_norm) + the inf/nan verdict + the AdamW step count / bias
+   corrections + GradScaler.update (torch.amp semantics: backoff on a non-finite step, growth every
+   growth_interval finite steps).  grad = sum over ranks of the (loss-scaled) gradients; grad_scale = 1/world.
+     state[8]: 0 ||averaged unscaled grad||, 1 gradient multiplier (clip coef * grad_scale / S), 2 skip flag (1 =
+               non-finite gradient: the AdamW update is skipped), 3 lr / (1 - beta1^t), 4 sqrt(1 - beta2^t), 5 lr,
+               6 the loss scale S of this step
+     ctl[4] (int): 0 AdamW steps taken t, 1 growth tracker, 2 skipped steps
+     lr: device float (this iteration's scheduled lr; written by the host between graph replays)
+     scaler[4] (NULL = no loss scaling): {S, growth_factor, backoff_factor, growth_interval}, updated in place
+     up[n_up] = up_base[n_up] * S_new: the loss terms' upstream gradients for the next step (n_up may be 0).
+   ws: nbp_clip_workspace_doubles(n). */
 size_t nbp_clip_workspace_doubles(long n);
-int nbp_grad_clip_coef(const float* grad, long n, float grad_scale, float max_norm, double* ws, float* state,
-                       nbp_stream_t s);
-/* torch.optim.AdamW step over the flat buffer with gradient * state[1]. */
-int nbp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
-                   float lr, float beta1, float beta2, float eps, float weight_decay, int step, nbp_stream_t s);
-/* The same step with hyper[3] = {lr, lr / (1 - beta1^t), sqrt(1 - beta2^t)} read from device memory (HIP-graph
-   replayable: the host updates hyper between replays). */
-int nbp_adamw_step_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
-                       const float* hyper, float beta1, float beta2, float eps, float weight_decay, nbp_stream_t s);
+int nbp_optim_prepare(const float* grad, long n, float grad_scale, float max_norm, double* ws, const float* lr,
+                      float beta1, float beta2, float* state, int* ctl, float* scaler, float* up, const float* up_base,
+                      int n_up, nbp_stream_t s);
+/* torch.optim.AdamW step (decoupled weight decay) over the flat buffer with gradient * state[1], lr = state[5] and
+   the bias corrections state[3..4]; a no-op when state[2] != 0 (scaler.step's skip). */
+int nbp_adamw_apply(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long n, const float* state,
+                    float beta1, float beta2, float eps, float weight_decay, nbp_stream_t s);
 
 /* ------------------------------------------------------------------ SID input path
  * Host-side (no GPU, no stream): the reference reads PNG bytes from LMDB (basicsr FileClient 'lmdb',

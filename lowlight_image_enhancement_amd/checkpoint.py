@@ -65,7 +65,7 @@ def adamw_state_dict(trainer) -> Dict:
         state[i] = {"step": step.clone(),
                     "exp_avg": net._to_reference(e, trainer.exp_avg[e.offset:e.offset + e.numel]).detach().cpu(),
                     "exp_avg_sq": net._to_reference(e, trainer.exp_avg_sq[e.offset:e.offset + e.numel]).detach().cpu()}
-    lr = trainer.scheduler(trainer.t) if trainer.scheduler is not None else trainer.lr
+    lr = _last_lr(trainer)
     group = {"lr": float(lr), "betas": tuple(float(b) for b in trainer.betas), "eps": float(trainer.eps),
              "weight_decay": float(trainer.wd), "amsgrad": False, "foreach": None, "maximize": False,
              "capturable": False, "differentiable": False, "fused": None, "initial_lr": float(trainer.lr),
@@ -102,13 +102,30 @@ def load_adamw_state_dict(trainer, sd: Dict) -> None:
     trainer.lr = float(g.get("initial_lr", g["lr"]))
 
 
-def scheduler_state_dict(trainer) -> Dict:
-    """The TrueCosineAnnealingLR state in torch LRScheduler form (last_epoch = completed steps)."""
+def _last_lr(trainer) -> float:
+    """The lr the last iteration ran with: base_model.update_learning_rate (:164-174) steps the scheduler only from
+    iteration 2 on, so after N iterations it has stepped N - 1 times (last_epoch = N - 1)."""
     s = trainer.scheduler
-    lr = s(trainer.t) if s is not None else trainer.lr
+    return float(s(max(trainer.iter - 1, 0))) if s is not None else float(trainer.lr)
+
+
+def scheduler_state_dict(trainer) -> Dict:
+    """The TrueCosineAnnealingLR state in torch CosineAnnealingLR.state_dict() form after trainer.iter iterations of
+    the reference loop: constructed (last_epoch 0, _step_count 1), then stepped once per iteration after the first."""
+    s = trainer.scheduler
+    it = max(trainer.iter - 1, 0)
     return {"T_max": s.T if s is not None else 0, "eta_min": s.eta_min if s is not None else 0.0,
-            "base_lrs": [s.base if s is not None else trainer.lr], "last_epoch": trainer.t,
-            "_step_count": trainer.t + 1, "verbose": False, "_get_lr_called_within_step": False, "_last_lr": [lr]}
+            "base_lrs": [s.base if s is not None else trainer.lr], "last_epoch": it, "_step_count": it + 1,
+            "verbose": False, "_get_lr_called_within_step": False, "_last_lr": [_last_lr(trainer)]}
+
+
+def scaler_state_dict(trainer) -> Optional[Dict]:
+    """torch.amp.GradScaler.state_dict() form of the trainer's device-side loss scaler (None without one)."""
+    if trainer.scaler is None:
+        return None
+    sc = trainer.scaler.cpu()
+    return {"scale": float(sc[0]), "growth_factor": float(sc[1]), "backoff_factor": float(sc[2]),
+            "growth_interval": int(sc[3]), "_growth_tracker": int(trainer.ctl[1].item())}
 
 
 def save_training_state(trainer, epoch: int, current_iter: int, states_dir: str) -> Optional[str]:
@@ -118,6 +135,9 @@ def save_training_state(trainer, epoch: int, current_iter: int, states_dir: str)
         return None
     state = {"epoch": int(epoch), "iter": int(current_iter), "optimizers": [adamw_state_dict(trainer)],
              "schedulers": [scheduler_state_dict(trainer)]}
+    amp = scaler_state_dict(trainer)
+    if amp is not None:  # base_model.py:309-310
+        state["amp_scaler"] = amp
     path = os.path.join(states_dir, f"{current_iter}.state")
     torch.save(state, path)
     return path
@@ -137,4 +157,11 @@ def resume_training(trainer, resume_state) -> Dict:
         trainer.scheduler.T = s.get("T_max", trainer.scheduler.T)
         trainer.scheduler.eta_min = s.get("eta_min", trainer.scheduler.eta_min)
         trainer.scheduler.base = s.get("base_lrs", [trainer.scheduler.base])[0]
+    if scheds:  # the iteration the scheduler stands at (see scheduler_state_dict)
+        trainer.iter = int(scheds[0].get("last_epoch", 0)) + 1
+    amp = resume_state.get("amp_scaler")
+    if amp is not None and trainer.scaler is not None:  # base_model.py:332-333
+        trainer.scaler.copy_(torch.tensor([amp["scale"], amp["growth_factor"], amp["backoff_factor"],
+                                           float(amp["growth_interval"])]))
+        trainer.ctl[1] = int(amp["_growth_tracker"])
     return resume_state

@@ -823,7 +823,14 @@ long skinny_blocks(long M) {
   const long ntiles = (M + 31) / 32;
   const long blocks = (ntiles + 3) / 4;
   // 4 blocks (16 waves) resident per CU: one round over the 256 CUs (NBP_SKINNY_BLOCKS overrides: A/B measurement)
-  static const long cap = getenv("NBP_SKINNY_BLOCKS") ? atol(getenv("NBP_SKINNY_BLOCKS")) : 1024L;
+  static const long cap = [] {
+    const long v = getenv("NBP_SKINNY_BLOCKS") ? atol(getenv("NBP_SKINNY_BLOCKS")) : 1024L;
+    if (v < 1 || v > 8192) {
+      fprintf(stderr, "NBP_SKINNY_BLOCKS=%ld out of [1, 8192]: using 1024\n", v);
+      return 1024L;
+    }
+    return v;
+  }();
   return blocks > cap ? cap : blocks;
 }
 

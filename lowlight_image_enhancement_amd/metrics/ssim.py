@@ -18,6 +18,21 @@ from .linear import ssim_plane_means
 __all__ = ["calculate_ssim"]
 
 
+def _valid_kernel_size(height: int, width: int, kernel_size: int) -> int:
+    """metrics/ssim.py:74-89: an odd window no larger than the smaller image side."""
+    k = int(kernel_size)
+    if k <= 0:
+        raise ValueError(f"kernel_size must be positive, received {kernel_size}.")
+    if k % 2 == 0:
+        k -= 1
+    k = max(1, min(k, height, width))
+    if k % 2 == 0:
+        k -= 1
+    if k < 1:
+        raise ValueError(f"kernel_size cannot be adjusted to a valid value for shape {(height, width)}.")
+    return k
+
+
 def calculate_ssim(img_true: torch.Tensor, img_pred: torch.Tensor, data_range: float, *, kernel_size: int = 11,
                    sigma: float = 1.5, k1: float = 0.01, k2: float = 0.03, win_size: Optional[int] = None,
                    color_space: str = "rgb", resize_policy: Optional[str] = None, resize_mode: str = "bilinear",
@@ -33,6 +48,7 @@ def calculate_ssim(img_true: torch.Tensor, img_pred: torch.Tensor, data_range: f
     if t.shape != p.shape:
         raise ValueError("SSIM requires the same batch size and channel count for target and prediction. "
                          f"Got target={t.shape}, prediction={p.shape}.")
+    kernel_size = _valid_kernel_size(t.shape[-2], t.shape[-1], kernel_size)
     c1 = (k1 * float(data_range)) ** 2
     c2 = (k2 * float(data_range)) ** 2
     planes = ssim_plane_means(p, t, kernel_size, sigma, True, c1, c2, 0.0, "reflect", clamp_var=False, crop=True)

@@ -111,6 +111,8 @@ class NAFNet(nn.Module):
         # level 0 (C = 32): the conv4 output t4 is not stored; the conv5 dgrad rebuilds it per tile on MFMA
         # (nbp_dgrad_sg_rc, bitwise equal) -- NBP_SG_RC=0 stores and re-reads it
         self.sg_rc = os.environ.get("NBP_SG_RC", "1") != "0"
+        # the rebuild lives in the skinny GEMM path (NBP_SKINNY=0 turns that path off, and with it the t4 drop)
+        self.sg_rc = self.sg_rc and os.environ.get("NBP_SKINNY", "1")[:1] != "0"
         self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None

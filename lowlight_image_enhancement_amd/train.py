@@ -50,10 +50,14 @@ class NBPTrainer:
                  w_ssim: float = 0.0, w_phys: float = 0.1, lr: float = 5e-4, betas=(0.9, 0.999),
                  weight_decay: float = 0.01, eps: float = 1e-8, max_norm: Optional[float] = 0.01,
                  scheduler: Optional[TrueCosineAnnealingLR] = None, process_group=None, bucket_mb: float = 25.0,
-                 w_deltaE: float = 0.0, w_perc: float = 0.0, w_lpips: float = 0.0, perceptual=None, lpips=None):
+                 w_deltaE: float = 0.0, w_perc: float = 0.0, w_lpips: float = 0.0, perceptual=None, lpips=None,
+                 loss_scale: Optional[str] = "auto", init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
+                 backoff_factor: float = 0.5, growth_interval: int = 2000):
         """Loss terms and weights as HybridLossPlus (losses.py:223-372): L1 (raw), Perc (VGG19), LPIPS (vgg), ΔE00,
         SSIM, Phys_srgb; a zero weight skips the term.  `perceptual` / `lpips`: PerceptualLoss / LPIPS modules
-        (constructed with the synthetic offline weights when needed and not given)."""
+        (constructed with the synthetic offline weights when needed and not given).  `loss_scale`: "auto" (dynamic
+        GradScaler scaling when net.precision == "fp16"), "dynamic" or None; the GradScaler arguments are torch's
+        defaults.  A step whose gradient is non-finite leaves parameters and moments untouched in every mode."""
         self.net = net
         dev = net.flat.device
         self.dev = dev
@@ -61,8 +65,10 @@ class NBPTrainer:
         self.k_shared = int(psf_mode == "mono")
         self.w = (float(w_l1), float(w_ssim), float(w_phys))
         self.w_extra = dict(de=float(w_deltaE), perc=float(w_perc), lpips=float(w_lpips))
-        # upstream gradients of the loss terms, read by the kernels from device memory
-        self.up = torch.tensor(self.w + (float(w_deltaE), float(w_perc)), dtype=torch.float32, device=dev)
+        # upstream gradients of the loss terms, read by the kernels from device memory: up = up_base * S (the loss
+        # scale), {L1, SSIM, Phys, DeltaE, Perc} then one LPIPS entry per image (d(w * mean_n LPIPS_n) / d LPIPS_n)
+        self.up_base: Optional[torch.Tensor] = None
+        self.up: Optional[torch.Tensor] = None
         if w_perc and perceptual is None:
             from .NewBP_model.losses import PerceptualLoss
             perceptual = PerceptualLoss(device=dev)
@@ -71,7 +77,6 @@ class NBPTrainer:
             lpips = LPIPS(net="vgg")
         self.perceptual, self.lpips = perceptual, lpips
         self.lpips_buf: Optional[torch.Tensor] = None
-        self.lpips_up: Optional[torch.Tensor] = None
         self.lr, self.betas, self.wd, self.eps = lr, betas, weight_decay, eps
         self.max_norm = max_norm if max_norm is not None else 0.0
         self.scheduler = scheduler
@@ -80,10 +85,19 @@ class NBPTrainer:
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.clip_ws = torch.empty(query("clip_workspace_doubles", n), dtype=torch.float64, device=dev)
-        self.clip_state = torch.zeros(2, device=dev)
+        # device-side step state (nbp_optim_prepare): state = {norm, grad multiplier, skip, lr/bc1, sqrt(bc2), lr, S},
+        # ctl = {AdamW steps taken, GradScaler growth tracker, skipped steps}
+        self.opt_state = torch.zeros(8, device=dev)
+        self.ctl = torch.zeros(4, dtype=torch.int32, device=dev)
+        self._lr_dev = torch.zeros(1, device=dev)
+        # GradScaler (image_restoration_model.py:104-106, torch.cuda.amp defaults): dynamic loss scaling whenever the
+        # activations are stored in fp16 (the reference's autocast dtype); fp32 / bf16 need none (8-bit exponent)
+        if loss_scale == "auto":
+            loss_scale = "dynamic" if net.precision == "fp16" else None
+        self.scaler = (torch.tensor([init_scale, growth_factor, backoff_factor, float(growth_interval)],
+                                    dtype=torch.float32, device=dev) if loss_scale == "dynamic" else None)
         self.loss_buf = torch.zeros(6, device=dev)  # L1, SSIM, Phys, DeltaE, Perc, Total
-        self.finite_flag = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.t = 0
+        self.iter = 0  # iterations run (the scheduler's position; AdamW's own step count self.t excludes skips)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.bucket_elems = int(bucket_mb * 1024 * 1024 / 4)
@@ -116,6 +130,7 @@ class NBPTrainer:
         _lib.require_cuda(lq, gt)
         lq, gt = lq.contiguous(), gt.contiguous()
         B, C, H, W = lq.shape
+        self._ensure_up(B)
         out, tape = net.exec_forward(lq, save=True)
         n = out.numel()
         wl1, wss, wph = self.w
@@ -151,8 +166,7 @@ class NBPTrainer:
         if wlp != 0.0:
             if self.lpips_buf is None or self.lpips_buf.numel() != B:
                 self.lpips_buf = torch.zeros(B, device=lq.device)
-                self.lpips_up = torch.full((B,), wlp / B, device=lq.device)  # d(w * mean_n LPIPS_n)
-            g = self.lpips.value_and_grad(out, gt, self.lpips_up, self.lpips_buf, clamp=True)
+            g = self.lpips.value_and_grad(out, gt, self.up[5:5 + B], self.lpips_buf, clamp=True)
             call("add", d_out, g, d_out, n, 0)
         hook = self._on_stage if self.world > 1 else None
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
@@ -163,23 +177,55 @@ class NBPTrainer:
             self._handles.clear()
         return out
 
+    def _ensure_up(self, B: int):
+        """Upstream-gradient buffers for a batch of B images (re-made when B changes; the current loss scale is
+        kept)."""
+        if self.up_base is not None and self.up_base.numel() == 5 + B:
+            return
+        wl1, wss, wph = self.w
+        base = [wl1, wss, wph, self.w_extra["de"], self.w_extra["perc"]] + [self.w_extra["lpips"] / B] * B
+        self.up_base = torch.tensor(base, dtype=torch.float32, device=self.dev)
+        self.up = self.up_base * self.scaler[0] if self.scaler is not None else self.up_base.clone()
+
+    def _optimizer(self, grad_scale: float):
+        """clip + finiteness verdict + GradScaler update (nbp_optim_prepare), then AdamW (nbp_adamw_apply)."""
+        call("optim_prepare", self.grad, self.grad.numel(), float(grad_scale), float(self.max_norm), self.clip_ws,
+             self._lr_dev, float(self.betas[0]), float(self.betas[1]), self.opt_state, self.ctl, self.scaler,
+             self.up, self.up_base, self.up.numel())
+        call("adamw_apply", self.net.flat.data, self.grad, self.exp_avg, self.exp_avg_sq, self.grad.numel(),
+             self.opt_state, float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd))
+
+    def _lr_now(self) -> float:
+        """base_model.update_learning_rate (:164-174): iteration i (1-based) runs with the schedule at i - 1."""
+        lr = self.scheduler(self.iter - 1) if self.scheduler is not None else self.lr
+        return struct.unpack("f", struct.pack("f", lr))[0]
+
+    @property
+    def t(self) -> int:
+        """AdamW steps taken (skipped non-finite steps excluded; a host sync)."""
+        return int(self.ctl[0].item())
+
+    @t.setter
+    def t(self, v: int):
+        self.ctl[0] = int(v)
+
+    @property
+    def skipped_steps(self) -> int:
+        return int(self.ctl[2].item())
+
     def step(self, lq, gt, short=None, expo_ratio=None):
         out = self.loss_and_grad(lq, gt, short, expo_ratio)
-        self.t += 1
-        lr = self.scheduler(self.t - 1) if self.scheduler is not None else self.lr
-        call("grad_clip_coef", self.grad, self.grad.numel(), 1.0 / self.world, float(self.max_norm), self.clip_ws,
-             self.clip_state)
-        call("adamw_step", self.net.flat.data, self.grad, self.exp_avg, self.exp_avg_sq, self.grad.numel(),
-             self.clip_state, float(lr), float(self.betas[0]), float(self.betas[1]), float(self.eps), float(self.wd),
-             self.t)
+        self.iter += 1
+        self._lr_dev.fill_(self._lr_now())
+        self._optimizer(1.0 / self.world)
         return out
 
     # ------------------------------------------------------------------ HIP-graph step (single process)
     def graph_step(self, lq, gt, short=None, expo_ratio=None):
         """One training step replayed from a captured HIP graph: every kernel of step() (forward, loss head,
         backward with its deferred reductions, clip, AdamW) recorded once and relaunched with no host work but the
-        input copies and the 3-float hyper-parameter upload.  Numerically identical to step().  The first call
-        captures with these tensors' shapes; later calls copy their inputs into the captured buffers."""
+        input copies and the lr upload.  Numerically identical to step().  The first call captures with these
+        tensors' shapes; later calls copy their inputs into the captured buffers."""
         if self.world > 1:
             raise RuntimeError("graph_step is single-process; use step() with torch.distributed")
         ins = (lq, gt, short, expo_ratio)
@@ -191,51 +237,46 @@ class NBPTrainer:
                     raise ValueError("graph_step: inputs must keep the structure of the captured step")
                 if dst is not None and src is not dst:
                     dst.copy_(src, non_blocking=True)
-        self.t += 1
-        lr = self.scheduler(self.t - 1) if self.scheduler is not None else self.lr
-        # the eager C entry receives lr, beta1, beta2 as float32 and forms the bias corrections in double from those
-        f32 = lambda v: struct.unpack("f", struct.pack("f", v))[0]  # noqa: E731
-        lr, b1, b2 = f32(lr), f32(self.betas[0]), f32(self.betas[1])
-        slot = self.t % len(self._hyper_host)
-        ev = self._hyper_ev[slot]
+        self.iter += 1
+        slot = self.iter % len(self._lr_host)
+        ev = self._lr_ev[slot]
         if ev is not None:
             ev.synchronize()  # the upload that last used this pinned slot has been consumed
-        h = self._hyper_host[slot]
-        h[0], h[1], h[2] = lr, lr / (1.0 - b1 ** self.t), math.sqrt(1.0 - b2 ** self.t)
-        self._hyper.copy_(h, non_blocking=True)
+        h = self._lr_host[slot]
+        h[0] = self._lr_now()
+        self._lr_dev.copy_(h, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._hyper_ev[slot] = ev
+        self._lr_ev[slot] = ev
         self._graph.replay()
         return self._graph_out
 
     def _graph_body(self):
         lq, gt, short, ratio = self._static
         out = self.loss_and_grad(lq, gt, short, ratio)
-        call("grad_clip_coef", self.grad, self.grad.numel(), 1.0, float(self.max_norm), self.clip_ws, self.clip_state)
-        call("adamw_step_dev", self.net.flat.data, self.grad, self.exp_avg, self.exp_avg_sq, self.grad.numel(),
-             self.clip_state, self._hyper, float(self.betas[0]), float(self.betas[1]), float(self.eps),
-             float(self.wd))
+        self._optimizer(1.0)
         return out
 
     def _capture(self, ins):
         self._static = tuple(None if x is None else x.detach().clone() for x in ins)
-        self._hyper = torch.zeros(3, device=self.dev)
-        self._hyper_host = [torch.zeros(3, pin_memory=True) for _ in range(8)]
-        self._hyper_ev = [None] * 8
-        # the capture itself must not move the parameters: snapshot the state a side-stream warm-up touches
-        saved = [x.clone() for x in (self.net.flat.data, self.exp_avg, self.exp_avg_sq)]
+        self._lr_host = [torch.zeros(1, pin_memory=True) for _ in range(8)]
+        self._lr_ev = [None] * 8
+        self._ensure_up(ins[0].shape[0])
+        # the capture itself must not move any state: snapshot what the side-stream warm-up touches
+        state = [self.net.flat.data, self.exp_avg, self.exp_avg_sq, self.ctl, self.opt_state, self.up] + (
+            [self.scaler] if self.scaler is not None else [])
+        saved = [x.clone() for x in state]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            self._hyper.copy_(torch.tensor([0.0, 0.0, 1.0]))  # lr-0 warm-up: lazy init happens outside the capture
+            self._lr_dev.zero_()  # lazy initialisation happens outside the capture
             self._graph_body()
         torch.cuda.current_stream().wait_stream(side)
+        for dst, src in zip(state, saved):
+            dst.copy_(src)
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph):
             self._graph_out = self._graph_body()
-        for dst, src in zip((self.net.flat.data, self.exp_avg, self.exp_avg_sq), saved):
-            dst.copy_(src)
 
     def logs(self, reduce: bool = True) -> Dict[str, float]:
         """Loss dict of the last step (host sync), averaged over ranks like reduce_loss_dict (base_model.py:335-360)."""
@@ -263,5 +304,10 @@ class NBPTrainer:
         if wph:
             out["Phys"] = float(vals[2])
         out["Total"] = float(vals[5])
-        out["grad_norm"] = float(self.clip_state[0].cpu())
+        st = self.opt_state.cpu()
+        out["grad_norm"] = float(st[0])
+        if self.scaler is not None:
+            out["loss_scale"] = float(st[6])
+        if st[2] != 0:
+            out["skipped"] = 1.0
         return out

@@ -23,6 +23,7 @@ class _FlatState:
             0.01, None
         self.exp_avg = torch.randn(net.numel, generator=g)
         self.exp_avg_sq = torch.rand(net.numel, generator=g)
+        self.iter, self.scaler = t, None
 
 
 def test_network_file_round_trip_reference_keys(tmp_path):
@@ -81,6 +82,34 @@ def test_optimizer_state_is_torch_adamw_form(tmp_path):
     st2.exp_avg_sq.zero_()
     ck.resume_training(st2, path)
     assert st2.t == 3 and torch.equal(st2.exp_avg, st.exp_avg) and torch.equal(st2.exp_avg_sq, st.exp_avg_sq)
+
+
+@pytest.mark.parametrize("n_iter", [1, 2, 7])
+def test_scheduler_state_matches_reference_loop(tmp_path, n_iter):
+    """After N iterations of the reference loop (base_model.update_learning_rate steps the scheduler only when
+    current_iter > 1) the saved scheduler / optimizer lr fields equal a torch CosineAnnealingLR driven that way."""
+    from lowlight_image_enhancement_amd.train import TrueCosineAnnealingLR
+    net = create_newbp_net(in_channels=3, **CFG)
+    st = _FlatState(net, t=n_iter)
+    st.scheduler = TrueCosineAnnealingLR(5e-4, T_max=10, eta_min=1e-7)
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.AdamW([p], lr=5e-4)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=10, eta_min=1e-7)
+    for it in range(1, n_iter + 1):
+        if it > 1:
+            sched.step()
+        opt.step()
+    path = ck.save_training_state(st, 0, n_iter, str(tmp_path))
+    state = torch.load(path, map_location="cpu", weights_only=True)
+    mine, ref = state["schedulers"][0], sched.state_dict()
+    assert mine["last_epoch"] == ref["last_epoch"] and mine["_step_count"] == ref["_step_count"]
+    assert abs(mine["_last_lr"][0] - ref["_last_lr"][0]) <= 1e-12
+    assert abs(state["optimizers"][0]["param_groups"][0]["lr"] - opt.param_groups[0]["lr"]) <= 1e-12
+    # resuming puts the trainer at the same iteration
+    st2 = _FlatState(net, t=0)
+    st2.scheduler = TrueCosineAnnealingLR(5e-4, T_max=10, eta_min=1e-7)
+    ck.resume_training(st2, path)
+    assert st2.iter == n_iter
 
 
 @pytest.mark.gpu
