@@ -416,6 +416,14 @@ class HybridLossPlus(nn.Module):
     def _active(self, name):
         return self.use_uncertainty or self.w[name] != 0
 
+    def _term(self, name, fn):
+        """A term the reference always evaluates: with weight 0 its value is still logged, but it is computed without
+        building a backward (0 * term contributes a zero gradient)."""
+        if self._active(name):
+            return fn()
+        with torch.no_grad():
+            return fn()
+
     def forward(self, *, Bhat_raw, B_raw, A_raw, expo_ratio, Bhat_srgb01, B_srgb01, A_srgb01=None):
         logs: Dict[str, torch.Tensor] = {}
         L_total = 0.0
@@ -423,18 +431,17 @@ class HybridLossPlus(nn.Module):
         self._ensure_finite("L1_raw", L_l1)
         Lw, logs["L1_raw"] = self._weighted("l1", L_l1)
         L_total = L_total + Lw
-        if self._active("perc"):  # the reference always evaluates VGG; a zero weight is skipped here
-            L_p = self.perc(Bhat_srgb01, B_srgb01)
-            self._ensure_finite("Perc", L_p)
-            Lw, logs["Perc"] = self._weighted("perc", L_p)
-            L_total = L_total + Lw
+        L_p = self._term("perc", lambda: self.perc(Bhat_srgb01, B_srgb01))  # always evaluated (losses.py:337)
+        self._ensure_finite("Perc", L_p)
+        Lw, logs["Perc"] = self._weighted("perc", L_p)
+        L_total = L_total + Lw
         if self.lpips is not None:
             L_lp = self.lpips(Bhat_srgb01, B_srgb01).mean()
             self._ensure_finite("LPIPS", L_lp)
             Lw, logs["LPIPS"] = self._weighted("lpips", L_lp)
             L_total = L_total + Lw
-        if self.deltaE is not None and self._active("de"):
-            L_de = self.deltaE(Bhat_srgb01, B_srgb01)
+        if self.deltaE is not None:
+            L_de = self._term("de", lambda: self.deltaE(Bhat_srgb01, B_srgb01))
             self._ensure_finite("DeltaE", L_de)
             Lw, logs["DeltaE"] = self._weighted("de", L_de)
             L_total = L_total + Lw

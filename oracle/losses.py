@@ -213,4 +213,62 @@ def ssim_linear(pred, target, data_range=1.0, kernel_size=11, sigma=1.5, k1=0.01
     return {"mean": pi.mean(0), "sum": pi.sum(0), "none": pi}[reduction]
 
 
+# ---- torchvision==0.17.1 vgg19 / vgg16 `features` and lpips==0.1.4, restated (losses.py:32-69, 265-274) ----
+# Weights: torchvision's pretrained files are a download (unavailable offline), so the oracle takes the state_dict
+# the caller passes (the product's deterministic synthetic one in the tests) -- parity unpinned for real weights.
+VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512, 512, 512, "M"]
+VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
+
+
+def vgg_features(sd, x, cfg=VGG19_CFG, n_modules=36, taps=()):
+    """torchvision vgg.features[:n_modules] (conv 3x3 pad 1 -> ReLU, 2x2 max pool); returns (out, {relu idx: map})."""
+    h, idx, res = x, 0, {}
+    for v in cfg:
+        if idx >= n_modules:
+            break
+        if v == "M":
+            h = F.max_pool2d(h, 2)
+            idx += 1
+        else:
+            h = F.relu(F.conv2d(h, sd[f"{idx}.weight"].to(x.dtype), sd[f"{idx}.bias"].to(x.dtype), padding=1))
+            if idx + 1 in taps:
+                res[idx + 1] = h
+            idx += 2
+    return h, res
+
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def perceptual_loss(sd, gen, tgt):
+    """PerceptualLoss.forward (losses.py:54-69): clamp01 -> ImageNet normalisation -> features[:36] -> MSE."""
+    mean = torch.tensor(IMAGENET_MEAN, dtype=gen.dtype).view(1, 3, 1, 1)
+    std = torch.tensor(IMAGENET_STD, dtype=gen.dtype).view(1, 3, 1, 1)
+    fg, _ = vgg_features(sd, (gen.clamp(0, 1) - mean) / std)
+    ft, _ = vgg_features(sd, (tgt.clamp(0, 1) - mean) / std)
+    return F.mse_loss(fg, ft)
+
+
+LPIPS_SHIFT = (-0.030, -0.088, -0.188)
+LPIPS_SCALE = (0.458, 0.448, 0.450)
+LPIPS_VGG_TAPS = (3, 8, 15, 22, 29)
+
+
+def lpips_vgg(feats, lins, in0, in1):
+    """lpips.LPIPS(net='vgg').forward(in0, in1) per image [N,1,1,1] (inputs taken as [-1,1], no normalize): ScalingLayer,
+    VGG16 relu1_2..relu5_3 taps, channel unit-normalisation (eps 1e-10), squared difference, lin head, spatial mean."""
+    shift = torch.tensor(LPIPS_SHIFT, dtype=in0.dtype).view(1, 3, 1, 1)
+    scale = torch.tensor(LPIPS_SCALE, dtype=in0.dtype).view(1, 3, 1, 1)
+    _, t0 = vgg_features(feats, (in0 - shift) / scale, VGG16_CFG, 30, LPIPS_VGG_TAPS)
+    _, t1 = vgg_features(feats, (in1 - shift) / scale, VGG16_CFG, 30, LPIPS_VGG_TAPS)
+    val = 0
+    for k, tap in enumerate(LPIPS_VGG_TAPS):
+        u = t0[tap] / (t0[tap].pow(2).sum(1, keepdim=True).sqrt() + 1e-10)
+        v = t1[tap] / (t1[tap].pow(2).sum(1, keepdim=True).sqrt() + 1e-10)
+        d = ((u - v) ** 2 * lins[k].to(in0.dtype).view(1, -1, 1, 1)).sum(1, keepdim=True)
+        val = val + d.mean((2, 3), keepdim=True)
+    return val
+
+
 _ = math  # keep import for callers that use math constants

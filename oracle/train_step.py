@@ -16,15 +16,17 @@ from . import physics as P
 
 class OracleTrainer:
     """image_restoration_model.py:247-322 (fp32 branch :316-320) with HybridLossPlus term order
-    (NewBP_model/losses.py:318-372) minus the VGG/LPIPS terms (weights unavailable offline)."""
+    (NewBP_model/losses.py:318-372).  The VGG19 perceptual and LPIPS(vgg) terms take the caller's weights
+    (`vgg19_sd`, `lpips_parts` = (vgg16 features sd, [5 lin weights])): pretrained ones are unavailable offline."""
 
     def __init__(self, params: Dict[str, torch.Tensor], cfg: dict, psf_mode="rgb", psf_spec="B2",
                  w_l1=1.0, w_ssim=0.0, w_phys=0.1, w_de=0.0, lr=5e-4, betas=(0.9, 0.999), wd=0.01, eps=1e-8,
-                 max_norm=0.01):
+                 max_norm=0.01, w_perc=0.0, w_lpips=0.0, vgg19_sd=None, lpips_parts=None):
         self.P = {k: v.detach().clone().float().requires_grad_(True) for k, v in params.items()}
         self.cfg = cfg
         self.k = P.normalize_psf(P.build_psf_kernels(psf_mode, psf_spec))
-        self.w = dict(l1=w_l1, ssim=w_ssim, phys=w_phys, de=w_de)
+        self.w = dict(l1=w_l1, ssim=w_ssim, phys=w_phys, de=w_de, perc=w_perc, lpips=w_lpips)
+        self.vgg19_sd, self.lpips_parts = vgg19_sd, lpips_parts
         self.lr, self.betas, self.wd, self.eps, self.max_norm = lr, betas, wd, eps, max_norm
         self.m = {k: torch.zeros_like(v) for k, v in self.P.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.P.items()}
@@ -38,6 +40,14 @@ class OracleTrainer:
         logs["L1_raw"] = l1.detach()
         tot = tot + self.w["l1"] * l1
         o01, g01 = out.clamp(0, 1), gt.clamp(0, 1)
+        if self.w["perc"]:
+            pe = L.perceptual_loss(self.vgg19_sd, o01, g01)
+            logs["Perc"] = pe.detach()
+            tot = tot + self.w["perc"] * pe
+        if self.w["lpips"]:
+            lp = L.lpips_vgg(*self.lpips_parts, o01, g01).mean()
+            logs["LPIPS"] = lp.detach()
+            tot = tot + self.w["lpips"] * lp
         if self.w["de"]:
             de = L.deltae00_loss(o01, g01)
             logs["DeltaE"] = de.detach()

@@ -30,6 +30,7 @@ import torch.nn.functional as F
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 from param_recipe import recipe_state  # noqa: E402
+from synth_inputs import cfg5_inputs  # noqa: E402
 
 
 def load_reference(ref: str):
@@ -291,6 +292,42 @@ def gen_nets(R):
          shapes=np.asarray([str(tuple(v.shape)) for v in net.state_dict().values()]))
 
 
+CFG2 = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+CFG4 = dict(width=64, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+
+
+def gen_cfg_nets(R):
+    """BASELINE configs[1] model (w32 [2,2,4,8]/12/[2,2,2,2], rgb B2) at bs 2 x 256^2 and configs[3] model (w64, the
+    per-GPU slice at 2 x 64^2): output, loss terms and per-tensor gradient sums / norms (the parameters come from the
+    seeded recipe; full tensors would be 117 / 464 MB)."""
+    _net_case(R, "nafnet_cfg2.npz", CFG2, 300, 2, 256, 256, "rgb", "B2", full=False)
+    _net_case(R, "nafnet_w64.npz", CFG4, 301, 2, 64, 64, "rgb", "B2", full=False)
+
+
+def gen_cfg5(R):
+    """BASELINE configs[4]: phys_cons_raw with expo_ratio in {100, 250, 300} at 8 x 3 x 1024^2 (per-GPU slice of bs 32
+    over 4 GPUs) + psnr_linear / ssim_linear at data_range 4095 on the unnormalised scale; fp16 inputs too (the metric
+    casts to fp32, phys_consistency.py:302-303)."""
+    pred, obs, ratios, sl, ss = cfg5_inputs()
+    P, O, r = torch.from_numpy(pred), torch.from_numpy(obs), torch.from_numpy(ratios)
+    psf = torch.zeros(3, 3, 3, 3)
+    k = R.nl.build_psf_kernels("rgb", "B2")
+    for c in range(3):
+        psf[c, c] = k[c, 0]
+    out = {"seed": np.asarray(500), "sum_long": np.asarray(sl), "sum_short": np.asarray(ss), "ratios": ratios,
+           "psf": t2n(psf)}
+    out["raw_mean"] = t2n(R.pc.phys_cons_raw(P, O, psf, r))
+    out["raw_none"] = t2n(R.pc.phys_cons_raw(P, O, psf, r, reduction="none"))
+    out["raw_charb_sum"] = t2n(R.pc.phys_cons_raw(P, O, psf, r, reduction="sum", robust="charbonnier",
+                                                  padding="replicate", crop="same"))
+    out["raw_fp16_none"] = t2n(R.pc.phys_cons_raw(P.half(), O.half(), psf, r, reduction="none"))
+    long12 = torch.from_numpy(pred * ratios[:, None, None, None] * np.float32(4095.0))
+    short12 = O * 4095.0
+    out["psnr4095_none"] = t2n(R.lin.psnr_linear(short12, long12, data_range=4095.0, reduction="none"))
+    out["ssim4095_none"] = t2n(R.lin.ssim_linear(short12, long12, data_range=4095.0, reduction="none"))
+    save("cfg5_raw.npz", **out)
+
+
 def gen_train_steps(R):
     """Two full optimize_parameters steps (image_restoration_model.py:247-322, fp32 path :316-320):
     zero_grad -> fwd -> L1 + 0.1*PhysSRGB + 0*sum(p) -> backward -> clip_grad_norm_(0.01) -> AdamW."""
@@ -371,19 +408,17 @@ def gen_linear(R):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated generator names (default: all)")
     args = ap.parse_args()
     torch.set_num_threads(8)
     R = load_reference(args.ref)
     R.ref = args.ref
-    gen_psf(R)
-    gen_phys_srgb(R)
-    gen_phys_cons(R)
-    gen_layernorm(R)
-    gen_nafblock(R)
-    gen_nets(R)
-    gen_train_steps(R)
-    gen_color(R)
-    gen_linear(R)
+    gens = dict(psf=gen_psf, phys_srgb=gen_phys_srgb, phys_cons=gen_phys_cons, layernorm=gen_layernorm,
+                nafblock=gen_nafblock, nets=gen_nets, cfg_nets=gen_cfg_nets, cfg5=gen_cfg5,
+                train_steps=gen_train_steps, color=gen_color, linear=gen_linear)
+    for name, fn in gens.items():
+        if not args.only or name in args.only.split(","):
+            fn(R)
 
 
 if __name__ == "__main__":
