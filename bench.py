@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of HIP-graph replays")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
                     help="bf16: bf16 MFMA operands + fp32 accumulation (the reference's AMP training); "
                          "fp32: fp32 everywhere (parity mode)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
@@ -251,7 +251,7 @@ def main():
         classes[name] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), len(recs))
     dom = max(classes, key=lambda k: classes[k][0])
     ms, fl, by, nl = classes[dom]
-    peak_tf = BF16_PEAK_TFLOPS if args.precision == "bf16" else FP32_PEAK_TFLOPS
+    peak_tf = FP32_PEAK_TFLOPS if args.precision == "fp32" else BF16_PEAK_TFLOPS
     tflops = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     gbps = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     # the binding roof is the one the kernel class is closer to (arithmetic intensity vs the ridge point)
@@ -299,7 +299,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.precision if args.precision == "bf16" else "f32",
+            "dtype": {"bf16": "bf16", "fp16": "f16", "fp32": "f32"}[args.precision],
             "data": "synthetic (U[0,1) sRGB, expo_ratio 1, torch default init, seed 0+rank)",
             "config": {"workload": wl["desc"],
                        "global_batch": BATCH * world, "image": IMG, "parallelism": f"dp{world}",

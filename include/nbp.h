@@ -16,8 +16,9 @@
  *    network boundary and the loss terms are NCHW, the reference's public layout.
  *  - Scalars produced on the device (losses, norms) are written to device memory; gradients of scalar losses
  *    read the upstream gradient from device memory (`up`), so nothing forces a host sync.
- *  - `dtype` selects the storage of NHWC activations/activation-gradients: 0 fp32, 1 bf16 (perf mode).  Math,
- *    statistics, parameters and parameter gradients are fp32 in both.
+ *  - `dtype` selects the storage of NHWC activations/activation-gradients: 0 fp32, 1 bf16, 2 fp16 (the 16-bit perf
+ *    modes; fp16 is the reference's autocast dtype).  16-bit storage means 16-bit MFMA operands of the same type.
+ *    Math, statistics, parameters and parameter gradients are fp32 in every mode.
  */
 #ifndef NBP_H_
 #define NBP_H_
@@ -89,8 +90,9 @@ int nbp_all_finite(const float* x, long n, int* flag_dev, nbp_stream_t s);
 int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const float* B,
                  long ldb, int b_nk, float* C, long ldc, int c_mode, int M, int N, int K, int gh, int gw, int cs,
                  const float* bias, const float* R, const float* rscale, float* pre, nbp_stream_t s);
-/* bf16-operand MFMA variant (perf mode; AMP-equivalent operands, fp32 accumulate): C = A . Bw^T, Bw bf16 [N][ldb];
- * a_dtype / c_dtype: 0 fp32, 1 bf16 storage of A and of C/R/pre.  Same a_mode/c_mode/epilogue as nbp_gemm_f32;
+/* 16-bit-operand MFMA variant (perf modes; AMP-equivalent operands, fp32 accumulate): C = A . Bw^T, Bw 16-bit
+ * [N][ldb]; a_dtype / c_dtype: 0 fp32, 1 bf16, 2 fp16 storage of A and of C/R/pre (16-bit ones agree).  The operand
+ * type (Bw, 16-bit A / C) is fp16 when either side is fp16, else bf16 (so fp32 A and C take bf16 weights).  Same a_mode/c_mode/epilogue as nbp_gemm_f32;
  * dgrads pass the transposed weight copy.  K, ldb multiples of 8; S2D/D2S need cs % 8 == 0.  Extra c_modes fusing
  * SimpleGate (NAFNet_arch.py:22-25,75-76) on interleaved channel pairs: 4 = forward (C = t, pre <- g[M][N/2] with
  * g[c] = t[2c] * t[2c+1]), 5 = backward (acc = dg[M][N]; R = t [M][2N] interleaved; C[2c] = dg[c] * t[2c+1],
@@ -106,25 +108,27 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
 size_t nbp_dgrad_ln_workspace_floats(long M, int N);
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
-                     float* ws, size_t ws_floats, nbp_stream_t s);
+                     float* ws, size_t ws_floats, int dtype, nbp_stream_t s);
 /* NAFBlock conv3 / conv5 (N = C in {32, 64} on the skinny kernel with K <= 128, or 128 on 64 x 128 tiles; bf16) with
  * the next LayerNorm2d forward in the epilogue:
  * C = R + rscale * (A W^T + bias) (the block's y / out, NAFNet_arch.py:70-78) and nout / stats = LN(C) exactly as
  * nbp_ln_fwd_nhwc computes them from the stored C (arch_util.py:266-275); C, nout row stride N. */
 int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
-                    const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s);
+                    const float* lnw, const float* lnb, void* nout, float* stats, float eps, int dtype,
+                    nbp_stream_t s);
 /* conv5 input gradient + SimpleGate backward with the gate input recomputed (bf16, N = K = C = 32: level 0, whose conv4
  * forward runs on the same skinny MFMA sequence): dg = A . Wt^T (the conv5 dgrad), t = A2 . W2^T + b2 rebuilt per tile (the conv4 forward: A2 = its input n2 [M][K],
  * W2 [2N][K] bf16 with SimpleGate pairs interleaved, b2 fp32), C[m][2c] = dg[c] t[2c+1], C[m][2c+1] = dg[c] t[2c]
  * (NAFNet_arch.py:22-25, 76-78); equals CM_SGBWD on the stored t bit for bit.  The forward then skips storing t
  * (nbp_gemm_bf16 CM_SG with C = NULL). */
 int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,
-                    void* C, int M, int N, int K, nbp_stream_t s);
-/* per-step weight prep: out = bf16(flat); for each desc {offset, rows, cols, scale_offset} (int64, device)
- * out_t[offset..] = bf16(diag(s) . flat matrix)^T with s = flat[scale_offset..] (rows values), or no scaling when
+                    void* C, int M, int N, int K, int dtype, nbp_stream_t s);
+/* per-step weight prep: out = h(flat); for each desc {offset, rows, cols, scale_offset} (int64, device)
+ * out_t[offset..] = h(diag(s) . flat matrix)^T, h = bf16 (dtype 1) or fp16 (dtype 2), with s = flat[scale_offset..] (rows values), or no scaling when
  * scale_offset < 0 (the NAFBlock layer scales folded into the conv3 / conv5 dgrad operands). */
-int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s);
+int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, int dtype,
+                     nbp_stream_t s);
 /* weight gradient dW[n][k] = sum_m G(m,n) X(m,k) (+ db[n] = sum_m G(m,n)): split over M, fixed-order slab reduce. */
 size_t nbp_wgrad_workspace_floats(int M, int N, int K);
 /* Grouping: between nbp_wgrad_group(1, s) and nbp_wgrad_group(0, s) the wide plain bf16 weight gradients
@@ -294,35 +298,35 @@ int nbp_sobel_mag(const float* lab, int B, int H, int W, float* out, nbp_stream_
    2 = keep where R > 0 (ReLU mask of a saved post-ReLU map; the input-gradient pass uses the tap-flipped,
    transposed weights).  Cin, Cout multiples of 8; y bf16 (y_dtype 1) or fp32 (y_dtype 0, mode 1). */
 int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
-                     const void* R, void* y, int y_dtype, nbp_stream_t s);
+                     const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s);
 /* PerceptualLoss input (losses.py:56-66): NCHW fp32 sRGB -> NHWC bf16 [B][H][W][8] = (clamp01(x) - m) / s, c >= 3
    zero.  The input gradient maps d[B][H][W][8] fp32 back to NCHW (/ s, clamp mask). */
 int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float m1, float m2, float s0, float s1,
-                 float s2, void* y, nbp_stream_t s);
+                 float s2, void* y, int dtype, nbp_stream_t s);
 int nbp_vgg_input_grad(const float* d8, const float* x, int B, int H, int W, int clamp, float s0, float s1, float s2,
                        float* dx, nbp_stream_t s);
 /* 2x2 max pool over NHWC bf16 (floor) with the argmax (window order, first maximum); the backward scatters dy to
    the argmax and applies the ReLU mask of the (post-ReLU) pool input. */
-int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, nbp_stream_t s);
+int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, int dtype, nbp_stream_t s);
 int nbp_maxpool2_bwd(const void* dy, const unsigned char* idx, const void* post_in, int B, int H, int W, int C, void* dx,
-                     nbp_stream_t s);
+                     int dtype, nbp_stream_t s);
 /* LPIPS tap (lpips 0.1.4 net='vgg'): out[n] (+)= mean over the HW pixels of sum_c w_c (u_c - v_c)^2 with
    u = a / (|a|_C + 1e-10), v likewise for b (a, b: NHWC bf16 [N][HW][C]); the backward writes
    da = up[n] * d out[n] / da (zero for all-zero pixels).  ws: nbp_lpips_tap_workspace_doubles(N, HW). */
 size_t nbp_lpips_tap_workspace_doubles(int N, long HW);
 int nbp_lpips_tap_fwd(const void* a, const void* b, const float* w, int N, long HW, int C, int accumulate, double* ws,
-                      float* out, nbp_stream_t s);
+                      float* out, int dtype, nbp_stream_t s);
 int nbp_lpips_tap_bwd(const void* a, const void* b, const float* w, int N, long HW, int C, const float* up, void* da,
-                      nbp_stream_t s);
+                      int dtype, nbp_stream_t s);
 /* d += g * (post > 0) over n bf16 elements (a tapped post-ReLU map's gradient joining the backward walk). */
-int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, nbp_stream_t s);
+int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, int dtype, nbp_stream_t s);
 /* Feature distance over n bf16 elements: out = scale * sum (a-b)^2 (mode 0) or |a-b| (mode 1); the backward writes
    da = up[0] * scale * d/da, optionally masked by (a > 0) (the last ReLU).  ws: nbp_feat_dist_workspace_doubles(n). */
 size_t nbp_feat_dist_workspace_doubles(long n);
 int nbp_feat_dist_fwd(const void* a, const void* b, long n, int mode, double scale, double* ws, float* out,
-                      nbp_stream_t s);
+                      int dtype, nbp_stream_t s);
 int nbp_feat_dist_bwd(const void* a, const void* b, long n, int mode, float scale, int relu_mask, const float* up,
-                      void* da, nbp_stream_t s);
+                      void* da, int dtype, nbp_stream_t s);
 
 /* ------------------------------------------------------------------ optimizer (image_restoration_model.py:313-320) */
 /* Everything between backward and the AdamW update, decided on the device (no host sync, graph-replayable):

@@ -170,14 +170,14 @@ class _PerceptualFn(torch.autograd.Function):
         stack = module.stack(gen.device)
         want = ctx.needs_input_grad[0]
         with torch.no_grad():
-            ft, _, _ = stack.forward(_vgg.prep_input(tgt.detach()), save=False)
-            fg, tape, _ = stack.forward(_vgg.prep_input(gen.detach()), save=want)
+            ft, _, _ = stack.forward(_vgg.prep_input(tgt.detach(), dtype=stack.dtype), save=False)
+            fg, tape, _ = stack.forward(_vgg.prep_input(gen.detach(), dtype=stack.dtype), save=want)
         n = fg.numel()
         mode = 0 if module.use_mse else 1
         scale = 1.0 / n if module.reduction == "mean" else 1.0
         ws = torch.empty(query("feat_dist_workspace_doubles", n), dtype=torch.float64, device=gen.device)
         out = torch.empty((), device=gen.device)
-        call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out)
+        call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out, stack.dtype)
         if want:
             ctx.tape, ctx.fg, ctx.ft, ctx.stack = tape, fg, ft, stack
             ctx.mode, ctx.scale = mode, scale
@@ -189,7 +189,7 @@ class _PerceptualFn(torch.autograd.Function):
         (gen,) = ctx.saved_tensors
         d = torch.empty_like(ctx.fg)
         call("feat_dist_bwd", ctx.fg, ctx.ft, ctx.fg.numel(), ctx.mode, float(ctx.scale), 1,
-             up.float().contiguous().view(1), d)
+             up.float().contiguous().view(1), d, ctx.stack.dtype)
         d8 = ctx.stack.backward(ctx.tape, d)
         ctx.tape = ctx.fg = ctx.ft = None
         return _vgg.input_grad(d8, gen), None, None
@@ -199,10 +199,12 @@ class PerceptualLoss(nn.Module):
     """losses.py:32-69 — clamp01 -> ImageNet mean/std -> vgg19.features[:36] (through relu5_4) for both images ->
     MSE (use_mse) or L1, reduction 'mean' / 'sum'.  The conv stack is implicit-GEMM bf16 MFMA (vgg.py).
     `weights`: None (deterministic synthetic VGG19 — the ImageNet download is unavailable offline), a state_dict of
-    vgg19 (`features.N.*` or `N.*` keys) or a checkpoint path (loaded with weights_only=True)."""
+    vgg19 (`features.N.*` or `N.*` keys) or a checkpoint path (loaded with weights_only=True).  `precision`: the trunk's
+    16-bit type, "bf16" (default: no loss scaling needed) or "fp16" (the reference's autocast dtype; pair it with loss
+    scaling, as NBPTrainer does in its fp16 mode)."""
 
     def __init__(self, device: Union[str, torch.device] = "cuda", use_mse: bool = True, reduction: str = "mean",
-                 weights=None):
+                 weights=None, precision: str = "bf16"):
         super().__init__()
         if reduction not in ("mean", "sum"):
             raise NotImplementedError("PerceptualLoss on MI355X supports reduction 'mean' and 'sum'")
@@ -210,11 +212,13 @@ class PerceptualLoss(nn.Module):
         self.reduction = reduction
         self._weights = weights
         self._stacks = {}
+        self.precision = precision
 
     def stack(self, device) -> "_vgg.VGGStack":
-        key = str(device)
+        dt = {"bf16": 1, "fp16": 2}[self.precision]
+        key = (str(device), dt)
         if key not in self._stacks:
-            self._stacks[key] = _vgg.VGGStack(_vgg.VGG19_CFG, 36, device, self._weights)
+            self._stacks[key] = _vgg.VGGStack(_vgg.VGG19_CFG, 36, device, self._weights, dtype=dt)
         return self._stacks[key]
 
     def forward(self, generated_img, target_img):
@@ -226,15 +230,15 @@ class PerceptualLoss(nn.Module):
         """Autograd-free form for the fused trainer (no host sync, HIP-graph capturable): writes the loss into
         out[0] and returns up[0] * d loss / d gen (NCHW fp32)."""
         stack = self.stack(gen.device)
-        ft, _, _ = stack.forward(_vgg.prep_input(tgt), save=False)
-        fg, tape, _ = stack.forward(_vgg.prep_input(gen), save=True)
+        ft, _, _ = stack.forward(_vgg.prep_input(tgt, dtype=stack.dtype), save=False)
+        fg, tape, _ = stack.forward(_vgg.prep_input(gen, dtype=stack.dtype), save=True)
         n = fg.numel()
         mode = 0 if self.use_mse else 1
         scale = 1.0 / n if self.reduction == "mean" else 1.0
         ws = torch.empty(query("feat_dist_workspace_doubles", n), dtype=torch.float64, device=gen.device)
-        call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out)
+        call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out, stack.dtype)
         d = torch.empty_like(fg)
-        call("feat_dist_bwd", fg, ft, n, mode, float(scale), 1, up, d)
+        call("feat_dist_bwd", fg, ft, n, mode, float(scale), 1, up, d, stack.dtype)
         return _vgg.input_grad(stack.backward(tape, d), gen)
 
 

@@ -147,10 +147,10 @@ __device__ __forceinline__ void store_row(T* __restrict__ op, const float (&a)[C
   if constexpr (sizeof(T) == 2) {
 #pragma unroll
     for (int c = 0; c < CF; c += 8) {
-      bf16x8 v;
+      vec_t<T, 8> v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)a[c + j];
-      *reinterpret_cast<bf16x8*>(op + c) = v;
+      for (int j = 0; j < 8; ++j) v[j] = (T)a[c + j];
+      *reinterpret_cast<vec_t<T, 8>*>(op + c) = v;
     }
   } else {
 #pragma unroll
@@ -161,7 +161,7 @@ __device__ __forceinline__ void store_row(T* __restrict__ op, const float (&a)[C
 template <typename T>
 __device__ __forceinline__ void load8(const T* __restrict__ p, float (&v)[8]) {
   if constexpr (sizeof(T) == 2) {
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(p);
+    const vec_t<T, 8> b = *reinterpret_cast<const vec_t<T, 8>*>(p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
   } else {
@@ -230,10 +230,10 @@ __global__ __launch_bounds__(256) void intro_fwd_mfma(const float* __restrict__ 
         T* op = out + ((long)row * g.Wp + xo) * g.Cf + oc + ch;
         const float* tp = &tile[wave][px][ch];
         if constexpr (sizeof(T) == 2) {
-          bf16x8 v;
+          vec_t<T, 8> v;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (__bf16)tp[j];
-          *reinterpret_cast<bf16x8*>(op) = v;
+          for (int j = 0; j < 8; ++j) v[j] = (T)tp[j];
+          *reinterpret_cast<vec_t<T, 8>*>(op) = v;
         } else {
           st4(reinterpret_cast<float*>(op), make_float4(tp[0], tp[1], tp[2], tp[3]));
           st4(reinterpret_cast<float*>(op) + 4, make_float4(tp[4], tp[5], tp[6], tp[7]));

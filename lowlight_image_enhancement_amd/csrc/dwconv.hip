@@ -539,7 +539,7 @@ __device__ __forceinline__ void ld16f(const T* p, float* f) {
     const float4 v = *reinterpret_cast<const float4*>(p);
     f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
   } else {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+    const vec_t<T, 8> v = *reinterpret_cast<const vec_t<T, 8>*>(p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
   }
@@ -549,10 +549,10 @@ __device__ __forceinline__ void st16f(T* p, const float* f) {
   if constexpr (sizeof(T) == 4) {
     *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
   } else {
-    bf16x8 v;
+    vec_t<T, 8> v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (__bf16)f[j];
-    *reinterpret_cast<bf16x8*>(p) = v;
+    for (int j = 0; j < 8; ++j) v[j] = (T)f[j];
+    *reinterpret_cast<vec_t<T, 8>*>(p) = v;
   }
 }
 
@@ -561,7 +561,7 @@ __device__ __forceinline__ void unpack16(uint4 r, float* f) {
   if constexpr (sizeof(T) == 4) {
     f[0] = __uint_as_float(r.x); f[1] = __uint_as_float(r.y); f[2] = __uint_as_float(r.z); f[3] = __uint_as_float(r.w);
   } else {
-    const bf16x8 v = __builtin_bit_cast(bf16x8, r);
+    const vec_t<T, 8> v = __builtin_bit_cast(vec_t<T, 8>, r);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
   }
@@ -920,7 +920,7 @@ inline int dw_bwd_th(int W) {
 int dw_tiles(int H, int W, bool rec = false) {
   return cdiv(H, rec ? DWT_TH_REC : dw_bwd_th(W)) * cdiv(W, dw_bwd_tw(W));
 }
-bool dw_tiled_ok(int C, int dtype) { return C % (dtype == 1 ? 16 : 8) == 0; }
+bool dw_tiled_ok(int C, int dtype) { return C % (dtype != 0 ? 16 : 8) == 0; }
 
 int block_for_quads(int Q) {
   if (Q >= 256) return Q;  // one pixel per step, one thread per quad (Q <= 1024)
@@ -953,7 +953,7 @@ Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
 int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float* ds, const void* t2, const void* t1,
                     const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
                     int W, int C, int dtype, nbp_stream_t s) {
-  const int hs = dtype == 1 ? 16 : 8;
+  const int hs = dtype != 0 ? 16 : 8;
   const int tw = dw_bwd_tw(W);
   const bool rec = dh != nullptr && t2 == nullptr;  // fused, t2 recomputed from t1
   DwTileP p{dt2, dh, a, ds, t2, t1, wdw, bdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W, rec),
@@ -1015,7 +1015,7 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
   NBP_REQUIRE(t2 || dw_tiled_ok(C, dtype), "nbp_dw_sg_pool_fwd: t2 may be NULL only on the tiled path (nbp_dw_tiled)");
   NBP_REQUIRE(C % 4 == 0 && C / 4 <= 1024, "nbp_dw_sg_pool_fwd: C");
   if (dw_tiled_ok(C, dtype)) {
-    const int tw = dw_fwd_tw(W, dtype), hs = dtype == 1 ? 16 : 8;
+    const int tw = dw_fwd_tw(W, dtype), hs = dtype != 0 ? 16 : 8;
     DwFwdP p{t1, wdw, bdw, t2, g, pool_slab, B, H, W, C, cdiv(W, tw), dw_fwd_tiles(H, W, dtype), C / hs};
     const long nblk = (long)B * p.tiles * p.slices;
     NBP_REQUIRE(nblk < (1L << 31), "nbp_dw_sg_pool_fwd: grid too large");
@@ -1152,7 +1152,7 @@ int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const voi
                       nbp_stream_t s) {
   NBP_REQUIRE(dh && a && ds && t2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
               "nbp_sca_sg_dw_bwd: bad args");
-  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd: C must be a multiple of %d", dtype == 1 ? 16 : 8);
+  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd: C must be a multiple of %d", dtype != 0 ? 16 : 8);
   NBP_REQUIRE(t2, "nbp_sca_sg_dw_bwd: t2 required (nbp_sca_sg_dw_bwd_rec recomputes it)");
   return launch_dw_tiled(nullptr, dh, a, ds, t2, t1, wdw, nullptr, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
 }
@@ -1164,7 +1164,7 @@ int nbp_sca_sg_dw_bwd_rec(const void* dh, const float* a, const float* ds, const
                           int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dh && a && ds && t1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
               "nbp_sca_sg_dw_bwd_rec: bad args");
-  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd_rec: C must be a multiple of %d", dtype == 1 ? 16 : 8);
+  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd_rec: C must be a multiple of %d", dtype != 0 ? 16 : 8);
   return launch_dw_tiled(nullptr, dh, a, ds, nullptr, t1, wdw, bdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
 }
 

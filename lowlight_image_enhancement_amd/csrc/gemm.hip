@@ -273,15 +273,13 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
 // address of row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.  Two reads give the
 // 8 consecutive-m values of one fragment.  Rows are padded to 96 elements (192 B) so the four rows x two groups of
 // a half-wave hit 64 distinct banks.
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-
-template <int GMODE, int XMODE>
+template <int GMODE, int XMODE, typename H>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   constexpr int RM = 32, TNW = 64, TKW = 64, LS = 96;
-  __shared__ __attribute__((aligned(16))) __bf16 Gs[RM * LS];
-  __shared__ __attribute__((aligned(16))) __bf16 Xs[RM * LS];
-  const __bf16* G = reinterpret_cast<const __bf16*>(p.G);
-  const __bf16* X = reinterpret_cast<const __bf16*>(p.X);
+  __shared__ __attribute__((aligned(16))) H Gs[RM * LS];
+  __shared__ __attribute__((aligned(16))) H Xs[RM * LS];
+  const H* G = reinterpret_cast<const H*>(p.G);
+  const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = blockIdx.x * TNW, k0 = blockIdx.y * TKW, s = blockIdx.z;
@@ -306,31 +304,31 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   };
   // loader: one 16-byte chunk of G and one of X per thread: row r = tid >> 3, 8 columns at (tid & 7) * 8
   const int lr = tid >> 3, lc = (tid & 7) * 8;
-  bf16x8 rg, rx;
+  vec_t<H, 8> rg, rx;
   auto load = [&](int m0) {
     const int m = m0 + lr;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rg[j] = rx[j] = (__bf16)0.f;
+    for (int j = 0; j < 8; ++j) rg[j] = rx[j] = (H)0.f;
     if (m < me) {
       const int n = n0 + lc, k = k0 + lc;
       if (n < p.N) {
         const long off = GMODE == AM_S2D ? s2d_off(m, n, p.gh, p.gw, p.cs_g) : (long)m * p.ldg + n;
-        rg = *reinterpret_cast<const bf16x8*>(G + off);
+        rg = *reinterpret_cast<const vec_t<H, 8>*>(G + off);
       }
       if (k < p.K) {
         const long off = XMODE == AM_S2D ? s2d_off(m, k, p.gh, p.gw, p.cs_x) : (long)m * p.ldx + k;
-        rx = *reinterpret_cast<const bf16x8*>(X + off);
+        rx = *reinterpret_cast<const vec_t<H, 8>*>(X + off);
         if (XMODE == AM_SCALE) {
           const float* sc = p.x_scale + (long)(m / p.rows_per_img) * p.K + k;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) rx[j] = (__bf16)((float)rx[j] * sc[j]);
+          for (int j = 0; j < 8; ++j) rx[j] = (H)((float)rx[j] * sc[j]);
         }
       }
     }
   };
   auto store = [&]() {
-    *reinterpret_cast<bf16x8*>(Gs + lr * LS + lc) = rg;
-    *reinterpret_cast<bf16x8*>(Xs + lr * LS + lc) = rx;
+    *reinterpret_cast<vec_t<H, 8>*>(Gs + lr * LS + lc) = rg;
+    *reinterpret_cast<vec_t<H, 8>*>(Xs + lr * LS + lc) = rx;
   };
   // tr-read addressing (see header comment)
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
@@ -352,19 +350,19 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
       }
 #pragma unroll
       for (int ks = 0; ks < RM; ks += 16) {
-        bf16x8 a, b;
+        vec_t<H, 8> a, b;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int row = ks + 8 * h + 4 * t + q;
-          const bf16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Gs + row * LS + gcol));
-          const bf16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(Xs + row * LS + xcol));
+          const vec_t<H, 4> va = ds_read_tr16<H>(Gs + row * LS + gcol);
+          const vec_t<H, 4> vb = ds_read_tr16<H>(Xs + row * LS + xcol);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             a[4 * t + j] = va[j];
             b[4 * t + j] = vb[j];
           }
         }
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        acc = mfma32x32x16(a, b, acc);
       }
       if (do_b && tid < TNW) {
 #pragma unroll 8
@@ -395,12 +393,12 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
 // (16 MFMAs per wave between barrier pairs, 8x the old 64 x 64 tile's), next stage prefetched into registers.
 // Each operand tile lives in LDS as two 64-column panels with the conflict-free 96-element rows of
 // wgrad_bf16_kernel, read transposed by ds_read_b64_tr_b16.  Bias (column sums of G) from the loader's registers.
-template <int XMODE>
+template <int XMODE, typename H>
 __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by, int bz) {
   constexpr int RM = 64, LS = 96, PAN = RM * LS;
-  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * PAN];  // G panels 0, 1; X panels 2, 3
-  const __bf16* G = reinterpret_cast<const __bf16*>(p.G);
-  const __bf16* X = reinterpret_cast<const __bf16*>(p.X);
+  __shared__ __attribute__((aligned(16))) H lds[4 * PAN];  // G panels 0, 1; X panels 2, 3
+  const H* G = reinterpret_cast<const H*>(p.G);
+  const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = bx * 128, k0 = by * 128, s = bz;
@@ -419,25 +417,25 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
   for (int i = 0; i < 8; ++i) bs[i] = 0.f;
   // loader: 16-byte chunk cc of rows lrow + 16 j (j < 4) for both operands
   const int lrow = tid >> 4, cc = tid & 15, pan = cc >> 3, lcol = (cc & 7) * 8;
-  bf16x8 rg[4], rx[4];
+  vec_t<H, 8> rg[4], rx[4];
   auto load = [&](int m0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + lrow + 16 * j;
       if (m < me) {
-        rg[j] = *reinterpret_cast<const bf16x8*>(G + (long)m * p.ldg + n0 + cc * 8);
-        rx[j] = *reinterpret_cast<const bf16x8*>(X + (long)m * p.ldx + k0 + cc * 8);
+        rg[j] = *reinterpret_cast<const vec_t<H, 8>*>(G + (long)m * p.ldg + n0 + cc * 8);
+        rx[j] = *reinterpret_cast<const vec_t<H, 8>*>(X + (long)m * p.ldx + k0 + cc * 8);
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) rg[j][e] = rx[j][e] = (__bf16)0.f;
+        for (int e = 0; e < 8; ++e) rg[j][e] = rx[j][e] = (H)0.f;
       }
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      *reinterpret_cast<bf16x8*>(lds + pan * PAN + (lrow + 16 * j) * LS + lcol) = rg[j];
-      *reinterpret_cast<bf16x8*>(lds + (2 + pan) * PAN + (lrow + 16 * j) * LS + lcol) = rx[j];
+      *reinterpret_cast<vec_t<H, 8>*>(lds + pan * PAN + (lrow + 16 * j) * LS + lcol) = rg[j];
+      *reinterpret_cast<vec_t<H, 8>*>(lds + (2 + pan) * PAN + (lrow + 16 * j) * LS + lcol) = rx[j];
       if (do_b) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) bs[e] += (float)rg[j][e];
@@ -446,8 +444,8 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
   };
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
   const int fcol = 16 * (grp & 1) + 4 * pp;
-  const __bf16* gpan = lds + wn * PAN;
-  const __bf16* xpan = lds + (2 + wk) * PAN;
+  const H* gpan = lds + wn * PAN;
+  const H* xpan = lds + (2 + wk) * PAN;
   // AM_SCALE (X columns scaled per image; the launcher guarantees rows_per_img % 64 == 0, so no stage straddles two
   // images): the MFMAs run on the unscaled X and each image's partial sum is scaled in fp32 when the rows move on.
   constexpr int NT_ = XMODE == AM_SCALE ? 2 : 1;
@@ -488,14 +486,14 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
       }
 #pragma unroll
       for (int ks = 0; ks < RM; ks += 16) {
-        bf16x8 a[2], b[2];
+        vec_t<H, 8> a[2], b[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int row = ks + 8 * h + 4 * t + q;
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            const bf16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(gpan + row * LS + i * 32 + fcol));
-            const bf16x4 vb = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(xpan + row * LS + i * 32 + fcol));
+            const vec_t<H, 4> va = ds_read_tr16<H>(gpan + row * LS + i * 32 + fcol);
+            const vec_t<H, 4> vb = ds_read_tr16<H>(xpan + row * LS + i * 32 + fcol);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               a[i][4 * t + e] = va[e];
@@ -506,7 +504,7 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
       }
       __syncthreads();
       if (more) {
@@ -544,9 +542,9 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
   }
 }
 
-template <int XMODE>
+template <int XMODE, typename H>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
-  wgrad_wide_tile<XMODE>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+  wgrad_wide_tile<XMODE, H>(p, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Several independent wide weight gradients (plain X) in one launch: NAFBlock conv5 (U) and conv4 at the deep levels
@@ -558,12 +556,13 @@ struct WGroup {
   int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
   int n;
 };
+template <typename H>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
   const int b = blockIdx.x;
   int i = 0;
   while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
   const int l = b - g.start[i], gx = g.gx[i], gy = g.gy[i];
-  wgrad_wide_tile<AM_PLAIN>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy));
+  wgrad_wide_tile<AM_PLAIN, H>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy));
 }
 
 // Column sums of a [S][L] fp32 slab.  A lane sums VEC adjacent columns (float4 loads when VEC = 4) over the rows
@@ -927,6 +926,7 @@ size_t nbp_wgrad_workspace_floats(int M, int N, int K) {
 
 thread_local bool g_wgroup = false;
 thread_local std::vector<WgradP> g_wqueue;
+thread_local int g_wqueue_dtype = 1;  // the 16-bit type of the queued problems (one per group)
 
 void wgroup_launch(hipStream_t st) {
   size_t i = 0;
@@ -944,7 +944,7 @@ void wgroup_launch(hipStream_t st) {
       ++g.n;
     }
     g.start[g.n] = blocks;
-    wgrad_bf16_wide_group<<<blocks, 256, 0, st>>>(g);
+    NBP_DISPATCH_H(g_wqueue_dtype, wgrad_bf16_wide_group<H><<<blocks, 256, 0, st>>>(g));
   }
   g_wqueue.clear();
 }
@@ -968,32 +968,38 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
   dim3 grid(cdiv(N, 64), cdiv(K, 64), S_);
   hipStream_t st = S(s);
   bool ok = true;
-  if (dtype == 1) {
+  if (dtype != 0) {
     NBP_REQUIRE(N % 8 == 0 && K % 8 == 0 && (g_mode != AM_S2D || cs_g % 8 == 0) && (x_mode != AM_S2D || cs_x % 8 == 0),
-                "nbp_wgrad_f32(bf16): N, K and S2D channel counts must be multiples of 8");
+                "nbp_wgrad_f32(16-bit): N, K and S2D channel counts must be multiples of 8");
     NBP_REQUIRE((g_mode == AM_S2D || ldg % 8 == 0) && (x_mode == AM_S2D || ldx % 8 == 0),
-                "nbp_wgrad_f32(bf16): leading dimensions must be multiples of 8");
+                "nbp_wgrad_f32(16-bit): leading dimensions must be multiples of 8");
     const bool wide = wide_wgrad(N, K) && g_mode == AM_PLAIN &&
                       (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0));
     const dim3 wgrid(N / 128, K / 128, S_);
     // grouped only while the slab reductions are deferred (they must run after the queued launch)
-    if (wide && x_mode == AM_PLAIN && g_wgroup && g_defer) g_wqueue.push_back(p);  // nbp_wgrad_group(0, ...) launches
-    else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN><<<wgrid, 256, 0, st>>>(p);
-    else if (wide) wgrad_bf16_wide<AM_SCALE><<<wgrid, 256, 0, st>>>(p);
-    else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN><<<grid, 256, 0, st>>>(p);
-    else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
-      wgrad_bf16_kernel<AM_PLAIN, 3><<<grid, 256, 0, st>>>(p);
-    else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_bf16_kernel<AM_PLAIN, AM_SCALE><<<grid, 256, 0, st>>>(p);
-    else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_bf16_kernel<AM_PLAIN, AM_S2D><<<grid, 256, 0, st>>>(p);
-    else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_S2D, AM_PLAIN><<<grid, 256, 0, st>>>(p);
-    else ok = false;
-  } else NBP_DISPATCH_T(dtype, {
+    if (wide && x_mode == AM_PLAIN && g_wgroup && g_defer) {  // nbp_wgrad_group(0, ...) launches
+      NBP_REQUIRE(g_wqueue.empty() || g_wqueue_dtype == dtype, "nbp_wgrad_f32: mixed dtypes in one group");
+      g_wqueue_dtype = dtype;
+      g_wqueue.push_back(p);
+    } else NBP_DISPATCH_H(dtype, {
+      if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
+      else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
+        wgrad_bf16_kernel<AM_PLAIN, 3, H><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_bf16_kernel<AM_PLAIN, AM_SCALE, H><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_bf16_kernel<AM_PLAIN, AM_S2D, H><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_S2D, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
+      else ok = false;
+    });
+  } else {
+    using T = float;
     if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_PLAIN, AM_PLAIN, T><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_f32_kernel<AM_PLAIN, AM_SCALE, T><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_PLAIN && x_mode == AM_S2D) wgrad_f32_kernel<AM_PLAIN, AM_S2D, T><<<grid, 256, 0, st>>>(p);
     else if (g_mode == AM_S2D && x_mode == AM_PLAIN) wgrad_f32_kernel<AM_S2D, AM_PLAIN, T><<<grid, 256, 0, st>>>(p);
     else ok = false;
-  });
+  }
   if (!ok) { set_error("nbp_wgrad_f32: unsupported mode combination"); return NBP_ERR_ARG; }
   grad_reduce(slab, S_, (long)N * K, dW, st);
   if (db) grad_reduce(slab_b, S_, N, db, st);

@@ -30,7 +30,7 @@ struct GemmPB {
   long lda;
   const float* a_scale;
   int rows_per_img;
-  const __bf16* B;
+  const void* B;  // 16-bit weights (the kernel's operand type H)
   long ldb;
   void* C;
   long ldc;
@@ -65,19 +65,17 @@ __device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
 
 template <typename T>
 __device__ __forceinline__ float ldf(const void* p, long off) {
-  if constexpr (sizeof(T) == 4) return reinterpret_cast<const float*>(p)[off];
-  else return (float)reinterpret_cast<const __bf16*>(p)[off];
+  return (float)reinterpret_cast<const T*>(p)[off];
 }
 template <typename T>
 __device__ __forceinline__ void stf(void* p, long off, float v) {
-  if constexpr (sizeof(T) == 4) reinterpret_cast<float*>(p)[off] = v;
-  else reinterpret_cast<__bf16*>(p)[off] = (__bf16)v;
+  reinterpret_cast<T*>(p)[off] = (T)v;
 }
 
-// 8 consecutive elements of A at element offset `off`, optionally scaled, as bf16x8
-template <typename TA, int AMODE>
-__device__ __forceinline__ bf16x8 load8(const void* A, long off, const float* scale) {
-  bf16x8 r;
+// 8 consecutive elements of A at element offset `off`, optionally scaled, as the 16-bit operand type H
+template <typename TA, int AMODE, typename H>
+__device__ __forceinline__ vec_t<H, 8> load8(const void* A, long off, const float* scale) {
+  vec_t<H, 8> r;
   if constexpr (sizeof(TA) == 4) {
     const float4 a = ld4(reinterpret_cast<const float*>(A) + off);
     const float4 b = ld4(reinterpret_cast<const float*>(A) + off + 4);
@@ -88,27 +86,28 @@ __device__ __forceinline__ bf16x8 load8(const void* A, long off, const float* sc
       v[4] *= s1.x; v[5] *= s1.y; v[6] *= s1.z; v[7] *= s1.w;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
+    for (int j = 0; j < 8; ++j) r[j] = (H)v[j];
   } else {
-    r = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(A) + off);
+    static_assert(sizeof(TA) == 2, "16-bit A is the operand type");
+    r = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(A) + off);
     if (AMODE == AM_SCALE) {
       const float4 s0 = ld4(scale), s1 = ld4(scale + 4);
       const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (__bf16)((float)r[j] * s[j]);
+      for (int j = 0; j < 8; ++j) r[j] = (H)((float)r[j] * s[j]);
     }
   }
   return r;
 }
 
-// 8 consecutive fp32 values -> storage type (16 bytes bf16 / 32 bytes fp32) and back
+// 8 consecutive fp32 values <-> storage type (16 bytes of 16-bit / 32 bytes of fp32)
 template <typename T>
 __device__ __forceinline__ void ld8f(const void* base, long off, float* v) {
   if constexpr (sizeof(T) == 4) {
     const float4 a = ld4(reinterpret_cast<const float*>(base) + off), b = ld4(reinterpret_cast<const float*>(base) + off + 4);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
   } else {
-    const bf16x8 r = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const __bf16*>(base) + off);
+    const vec_t<T, 8> r = *reinterpret_cast<const vec_t<T, 8>*>(reinterpret_cast<const T*>(base) + off);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (float)r[j];
   }
@@ -120,10 +119,10 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
     st4(d, make_float4(v[0], v[1], v[2], v[3]));
     st4(d + 4, make_float4(v[4], v[5], v[6], v[7]));
   } else {
-    bf16x8 r;
+    vec_t<T, 8> r;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (__bf16)v[j];
-    *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(base) + off) = r;
+    for (int j = 0; j < 8; ++j) r[j] = (T)v[j];
+    *reinterpret_cast<vec_t<T, 8>*>(reinterpret_cast<T*>(base) + off) = r;
   }
 }
 
@@ -131,8 +130,10 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
 // LDS (one barrier per K step; the next tile's global loads are in flight during the current tile's MFMAs).
 // Epilogue: the fp32 accumulators are staged through LDS (aliasing the operand buffers) so that bias / pre-activation /
 // residual R + rscale * v / the C store all move 8 consecutive columns (16 bytes of bf16) per thread.
-template <int BM, int BN, int BK, int AMODE, int CMODE, typename TA, typename TC>
+template <int BM, int BN, int BK, int AMODE, int CMODE, typename TA, typename TC, typename H>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
+  static_assert(sizeof(TA) == 4 || sizeof(TA) == sizeof(H), "A is fp32 or the operand type");
+  static_assert(sizeof(TC) == 4 || sizeof(TC) == sizeof(H), "C is fp32 or the operand type");
   constexpr int LS = BK + 8;  // 80 / 144-byte LDS rows: conflict-free 16-byte fragment reads
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int KC = BK / 8;  // 8-element chunks per tile row
@@ -142,8 +143,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
   constexpr int C_BYTES = BM * CLS * 4;
   constexpr int SM_BYTES = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
-  __bf16* As = reinterpret_cast<__bf16*>(smem);       // [2][BM][LS]
-  __bf16* Bs = As + 2 * BM * LS;                       // [2][BN][LS]
+  H* As = reinterpret_cast<H*>(smem);       // [2][BM][LS]
+  H* Bs = As + 2 * BM * LS;                       // [2][BN][LS]
   float* Cs = reinterpret_cast<float*>(smem);          // [BM][CLS] (after the K loop)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -159,30 +160,30 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // two register sets: with BK = 64 the loads of K-tiles t+1 and t+2 are in flight while tile t is multiplied
-  bf16x8 ra0[A_IT], rb0[B_IT], ra1[A_IT], rb1[B_IT];
-  auto load_tiles = [&](int k0, bf16x8* ra, bf16x8* rb) {
+  vec_t<H, 8> ra0[A_IT], rb0[B_IT], ra1[A_IT], rb1[B_IT];
+  auto load_tiles = [&](int k0, vec_t<H, 8>* ra, vec_t<H, 8>* rb) {
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int idx = tid + it * 256;
       const int r = idx / KC, kc = idx % KC;
       const int m = m0 + r, k = k0 + kc * 8;
-      bf16x8 v;
+      vec_t<H, 8> v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
       if (AMODE == AM_IM2COL) {
         if (m < M && k < K) {
           const int per = p.gh * p.gw, b = m / per, rem = m - b * per, i = rem / p.gw, j = rem - i * p.gw;
           const int t = k / p.cs, c = k - t * p.cs;
           const int ii = i + t / 3 - 1, jj = j + t % 3 - 1;
           if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
-            v = load8<TA, AM_PLAIN>(p.A, ((long)(b * p.gh + ii) * p.gw + jj) * p.cs + c, nullptr);
+            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.gh + ii) * p.gw + jj) * p.cs + c, nullptr);
         }
       } else if (m < M && k < K) {
         long off;
         if (AMODE == AM_S2D) off = s2d_off(m, k, p.gh, p.gw, p.cs);
         else off = (long)m * p.lda + k;
         const float* sc = AMODE == AM_SCALE ? p.a_scale + (long)(m / p.rows_per_img) * K + k : nullptr;
-        v = load8<TA, AMODE>(p.A, off, sc);
+        v = load8<TA, AMODE, H>(p.A, off, sc);
       }
       ra[it] = v;
     }
@@ -191,44 +192,44 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       const int idx = tid + it * 256;
       const int r = idx / KC, kc = idx % KC;
       const int n = n0 + r, k = k0 + kc * 8;
-      bf16x8 v;
+      vec_t<H, 8> v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-      if (n < N && k < K) v = *reinterpret_cast<const bf16x8*>(p.B + (long)n * p.ldb + k);
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
+      if (n < N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.B) + (long)n * p.ldb + k);
       rb[it] = v;
     }
   };
-  auto store_tiles = [&](int buf, const bf16x8* ra, const bf16x8* rb) {
-    __bf16* a = As + buf * BM * LS;
-    __bf16* b = Bs + buf * BN * LS;
+  auto store_tiles = [&](int buf, const vec_t<H, 8>* ra, const vec_t<H, 8>* rb) {
+    H* a = As + buf * BM * LS;
+    H* b = Bs + buf * BN * LS;
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int idx = tid + it * 256;
-      *reinterpret_cast<bf16x8*>(a + (idx / KC) * LS + (idx % KC) * 8) = ra[it];
+      *reinterpret_cast<vec_t<H, 8>*>(a + (idx / KC) * LS + (idx % KC) * 8) = ra[it];
     }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int idx = tid + it * 256;
-      *reinterpret_cast<bf16x8*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
+      *reinterpret_cast<vec_t<H, 8>*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
     }
   };
   const int arow = wm * (BM / 2) + (lane & 31);
   const int brow = wn * (BN / 2) + (lane & 31);
   const int kh = (lane >> 5) * 8;
   auto compute = [&](int buf) {
-    const __bf16* a_s = As + buf * BM * LS;
-    const __bf16* b_s = Bs + buf * BN * LS;
+    const H* a_s = As + buf * BM * LS;
+    const H* b_s = Bs + buf * BN * LS;
 #pragma unroll
     for (int s = 0; s < BK; s += 16) {
-      bf16x8 a[TM], b[TN];
+      vec_t<H, 8> a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(a_s + (arow + i * 32) * LS + s + kh);
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (arow + i * 32) * LS + s + kh);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(b_s + (brow + j * 32) * LS + s + kh);
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (brow + j * 32) * LS + s + kh);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
     }
   };
 
@@ -332,13 +333,13 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       const long off = (long)grow * p.ldc + gcol;
       float gv[8];
       ld8f<TC>(p.R, off, gv);
-      bf16x8 o;
+      vec_t<H, 8> o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        o[j] = (__bf16)v[j];
+        o[j] = (H)v[j];
         cd[j] = fmaf((float)o[j], gv[j], cd[j]);
       }
-      *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(p.C) + off) = o;
+      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.C) + off) = o;
       continue;
     }
     if (CMODE == CM_SGBWD) {
@@ -389,9 +390,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         if constexpr (sizeof(TC) == 4) {
           st4(reinterpret_cast<float*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2, make_float4(g[0], g[1], g[2], g[3]));
         } else {
-          bf16x4 o;
-          o[0] = (__bf16)g[0]; o[1] = (__bf16)g[1]; o[2] = (__bf16)g[2]; o[3] = (__bf16)g[3];
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2) = o;
+          vec_t<H, 4> o;
+          o[0] = (H)g[0]; o[1] = (H)g[1]; o[2] = (H)g[2]; o[3] = (H)g[3];
+          *reinterpret_cast<vec_t<H, 4>*>(reinterpret_cast<H*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2) = o;
         }
       } else if (p.pre) {
         st8f<TC>(p.pre, off, v);
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
         float xv[8], sm = 0.f, q = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xv[j] = (float)(__bf16)v[j];
+          xv[j] = (float)(H)v[j];
           sm += xv[j];
         }
         sm = group_sum<G8>(sm);
@@ -505,55 +506,56 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 // fragments while the current one is multiplied; a lane ends up owning one pixel's channels (4 consecutive per
 // register group), so the epilogue (bias, layer-scale residual, SimpleGate forward / backward) runs in registers and
 // stores 8 / 16-byte pieces that complete whole rows in L2.
+template <typename H>
 struct SkinnyP {
-  const __bf16* A;
+  const H* A;
   long lda;
   const float* a_scale;
   int rows_per_img;
-  const __bf16* W;
+  const H* W;
   long ldw;
-  __bf16* C;
+  H* C;
   long ldc;
   int M, N, K;
   const float* bias;
-  const __bf16* R;
+  const H* R;
   const float* rscale;
-  __bf16* aux;
+  H* aux;
   // CM_LNBWD (LayerNorm2d backward in the epilogue, arch_util.py:277-289): the GEMM output is dn; R = the LN input x,
   // stats = (mu, sqrt(var + eps)) per row, lnw = the LN weight, dres = the residual-branch gradient added to dx;
   // per-block partials of sum(dn * yhat) / sum(dn) go to slab_w / slab_b [grid][N]
   const float2* stats;
   const float* lnw;
-  const __bf16* dres;
+  const H* dres;
   float* slab_w;
   float* slab_b;
   // CM_RESLN (bias + layer-scale residual, then the next LayerNorm2d forward, arch_util.py:266-275): C = the stored
   // residual sum, nout = LN(C) with lnw / lnb_f, stats_out = (mu, sqrt(var + eps)) per row
   const float* lnb_f;
-  __bf16* nout;
+  H* nout;
   float2* stats_out;
   float eps;
   // CM_SGBWD_RC (SimpleGate backward with the gate input recomputed): t = A2 W2^T + b2 (the conv4 forward, its
   // output rows interleaved as stored, 2N columns) is rebuilt per tile on MFMA instead of being read from memory
-  const __bf16* A2;
-  const __bf16* W2;
+  const H* A2;
+  const H* W2;
   const float* b2;
 };
 
-template <int NT, int KS, int AMODE, int CMODE>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
+template <int NT, int KS, int AMODE, int CMODE, typename H>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
   constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
   constexpr bool RC = CMODE == CM_SGBWD_RC;
   constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : 8;  // bf16 row stride of the recomputed gate-input tile
   __shared__ float stage[4][32 * LDT];
-  __shared__ __attribute__((aligned(16))) __bf16 stage2[4][32 * LDT2];
+  __shared__ __attribute__((aligned(16))) H stage2[4][32 * LDT2];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   float* tileS = stage[threadIdx.x >> 6];
-  __bf16* tileT = stage2[threadIdx.x >> 6];
+  H* tileT = stage2[threadIdx.x >> 6];
   const int M = p.M, N = p.N, K = p.K;
   // RC: the conv4 weight (2N rows, K = the conv4 input width = this GEMM's K) and bias in registers
   constexpr int NT2 = RC ? 2 * NT : 1;
-  bf16x8 w2[NT2][KS];
+  vec_t<H, 8> w2[NT2][KS];
   float b2r[NT2][4][4];
   if constexpr (RC) {
 #pragma unroll
@@ -561,10 +563,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const int n = t * 32 + r, k = ks * 16 + 8 * h;
-        bf16x8 v;
+        vec_t<H, 8> v;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-        if (n < 2 * N && k < K) v = *reinterpret_cast<const bf16x8*>(p.W2 + (long)n * K + k);
+        for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
+        if (n < 2 * N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(p.W2 + (long)n * K + k);
         w2[t][ks] = v;
       }
 #pragma unroll
@@ -576,16 +578,16 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
         }
     }
   }
-  bf16x8 w[NT][KS];
+  vec_t<H, 8> w[NT][KS];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int n = t * 32 + r, k = ks * 16 + 8 * h;
-      bf16x8 v;
+      vec_t<H, 8> v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-      if (n < N && k < K) v = *reinterpret_cast<const bf16x8*>(p.W + (long)n * p.ldw + k);
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
+      if (n < N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(p.W + (long)n * p.ldw + k);
       w[t][ks] = v;
     }
   // coalesced epilogue geometry: chunks of 8 output elements, row-major over the 32-row tile.  The output row holds
@@ -617,40 +619,40 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
   }
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (long)gridDim.x * 4;
   const long ntiles = (M + 31) / 32;
-  auto load_a = [&](long tile, bf16x8* a) {
+  auto load_a = [&](long tile, vec_t<H, 8>* a) {
     const long m = tile * 32 + r;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = ks * 16 + 8 * h;
-      bf16x8 v;
+      vec_t<H, 8> v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
       if (m < M && k < K) {
-        v = *reinterpret_cast<const bf16x8*>(p.A + m * p.lda + k);
+        v = *reinterpret_cast<const vec_t<H, 8>*>(p.A + m * p.lda + k);
         if (AMODE == AM_SCALE) {
           const float* sc = p.a_scale + (m / p.rows_per_img) * K + k;
           const float4 s0 = ld4(sc), s1 = ld4(sc + 4);
           const float f[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)v[j] * f[j]);
+          for (int j = 0; j < 8; ++j) v[j] = (H)((float)v[j] * f[j]);
         }
       }
       a[ks] = v;
     }
   };
-  auto load_a2 = [&](long tile, bf16x8* a) {  // RC: the conv4 input rows (plain, row stride K)
+  auto load_a2 = [&](long tile, vec_t<H, 8>* a) {  // RC: the conv4 input rows (plain, row stride K)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const long m = tile * 32 + r;
       const int k = ks * 16 + 8 * h;
-      bf16x8 v;
+      vec_t<H, 8> v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-      if (m < M && k < K) v = *reinterpret_cast<const bf16x8*>(p.A2 + m * K + k);
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
+      if (m < M && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(p.A2 + m * K + k);
       a[ks] = v;
     }
   };
-  bf16x8 a0[KS], a1[KS], c0[RC ? KS : 1], c1[RC ? KS : 1];
+  vec_t<H, 8> a0[KS], a1[KS], c0[RC ? KS : 1], c1[RC ? KS : 1];
   long tile = wave;
   if (tile < ntiles) {
     load_a(tile, a0);
@@ -669,7 +671,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[t][ks], a0[ks], acc[t], 0, 0, 0);
+      for (int t = 0; t < NT; ++t) acc[t] = mfma32x32x16(w[t][ks], a0[ks], acc[t]);
     // lane (r, h) owns pixel r, channels t*32 + 8g + 4h + {0..3}: stage as rows of the tile
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -684,13 +686,13 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) a2c[i] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) a2c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[t][ks], c0[ks], a2c, 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks) a2c = mfma32x32x16(w2[t][ks], c0[ks], a2c);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          bf16x4 o;
+          vec_t<H, 4> o;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (__bf16)(a2c[4 * g + q] + b2r[t][g][q]);
-          *reinterpret_cast<bf16x4*>(tileT + r * LDT2 + t * 32 + 8 * g + 4 * h) = o;
+          for (int q = 0; q < 4; ++q) o[q] = (H)(a2c[4 * g + q] + b2r[t][g][q]);
+          *reinterpret_cast<vec_t<H, 4>*>(tileT + r * LDT2 + t * 32 + 8 * g + 4 * h) = o;
         }
       }
     }
@@ -702,16 +704,16 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
       if (CMODE == CM_SGBWD || RC) {  // chunk = 4 gates (interleaved pairs): dg from the tile, t from R (or rebuilt)
         const float4 dg = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol / 2);
         const long off = m * p.ldc + ccol;
-        const bf16x8 tv = RC ? *reinterpret_cast<const bf16x8*>(tileT + rr * LDT2 + ccol)
-                             : *reinterpret_cast<const bf16x8*>(p.R + off);
+        const vec_t<H, 8> tv = RC ? *reinterpret_cast<const vec_t<H, 8>*>(tileT + rr * LDT2 + ccol)
+                             : *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
         const float d[4] = {dg.x, dg.y, dg.z, dg.w};
-        bf16x8 o;
+        vec_t<H, 8> o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          o[2 * j] = (__bf16)(d[j] * (float)tv[2 * j + 1]);
-          o[2 * j + 1] = (__bf16)(d[j] * (float)tv[2 * j]);
+          o[2 * j] = (H)(d[j] * (float)tv[2 * j + 1]);
+          o[2 * j + 1] = (H)(d[j] * (float)tv[2 * j]);
         }
-        *reinterpret_cast<bf16x8*>(p.C + off) = o;
+        *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
         continue;
       }
       const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
@@ -720,8 +722,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
       if constexpr (CMODE == CM_LNBWD) {  // the row's cpr lanes are consecutive: shuffle sums within the group
         constexpr int G = 4 * NT;
         const long off = m * p.ldc + ccol;
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(p.R + off);
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.dres + off);
+        const vec_t<H, 8> xv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
+        const vec_t<H, 8> rv = *reinterpret_cast<const vec_t<H, 8>*>(p.dres + off);
         const float2 st = p.stats[m];
         const float inv = 1.f / st.y;
         float yh[8], sg = 0.f, sgy = 0.f;
@@ -737,24 +739,24 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
         sg = group_sum<G>(sg);
         sgy = group_sum<G>(sgy);
         const float mg = sg / (float)N, mgy = sgy / (float)N;
-        bf16x8 o;
+        vec_t<H, 8> o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (__bf16)((v[j] * rsc[j] - yh[j] * mgy - mg) * inv + (float)rv[j]);
-        *reinterpret_cast<bf16x8*>(p.C + off) = o;
+        for (int j = 0; j < 8; ++j) o[j] = (H)((v[j] * rsc[j] - yh[j] * mgy - mg) * inv + (float)rv[j]);
+        *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
         continue;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bia[j];
       const long off = m * p.ldc + ccol;
       if ((CMODE == CM_PLAIN || CMODE == CM_RESLN) && p.R) {
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.R + off);
+        const vec_t<H, 8> rv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (float)rv[j] + rsc[j] * v[j];
       }
-      bf16x8 o;
+      vec_t<H, 8> o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
-      if (CMODE != CM_SG || p.C) *reinterpret_cast<bf16x8*>(p.C + off) = o;  // SG: t may be dropped (recomputed)
+      for (int j = 0; j < 8; ++j) o[j] = (H)v[j];
+      if (CMODE != CM_SG || p.C) *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;  // SG: t may be dropped (recomputed)
       if constexpr (CMODE == CM_RESLN) {  // LayerNorm2d of the stored (bf16) row, as ln_fwd_nhwc computes it
         constexpr int G = 4 * NT;
         float xv[8], sm = 0.f, q = 0.f;
@@ -772,17 +774,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP p) {
         }
         q = group_sum<G>(q);
         const float dd = sqrtf(q / (float)N + p.eps), inv = 1.f / dd;
-        bf16x8 nn;
+        vec_t<H, 8> nn;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) nn[j] = (__bf16)fmaf(aw[j], (xv[j] - mu) * inv, ab[j]);
-        *reinterpret_cast<bf16x8*>(p.nout + m * N + ccol) = nn;
+        for (int j = 0; j < 8; ++j) nn[j] = (H)fmaf(aw[j], (xv[j] - mu) * inv, ab[j]);
+        *reinterpret_cast<vec_t<H, 8>*>(p.nout + m * N + ccol) = nn;
         if (ccol == 0) p.stats_out[m] = make_float2(mu, dd);
       }
       if (CMODE == CM_SG) {  // g[c] = t[2c] * t[2c+1]: 4 gates of this chunk
-        bf16x4 gv;
+        vec_t<H, 4> gv;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) gv[j] = (__bf16)(v[2 * j] * v[2 * j + 1]);
-        *reinterpret_cast<bf16x4*>(p.aux + m * (p.ldc / 2) + ccol / 2) = gv;
+        for (int j = 0; j < 4; ++j) gv[j] = (H)(v[2 * j] * v[2 * j + 1]);
+        *reinterpret_cast<vec_t<H, 4>*>(p.aux + m * (p.ldc / 2) + ccol / 2) = gv;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -835,11 +837,11 @@ long skinny_blocks(long M) {
 }
 
 // K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads)
-template <int AMODE, int CMODE>
-void launch_skinny(const SkinnyP& p, hipStream_t st) {
+template <int AMODE, int CMODE, typename H>
+void launch_skinny(const SkinnyP<H>& p, hipStream_t st) {
   const dim3 g((unsigned)skinny_blocks(p.M));
   const int nt = (p.N + 31) / 32, ks = (p.K + 15) / 16;
-#define NBP_SKINNY(NT_, KS_) gemm_skinny_kernel<NT_, KS_, AMODE, CMODE><<<g, 256, 0, st>>>(p)
+#define NBP_SKINNY(NT_, KS_) gemm_skinny_kernel<NT_, KS_, AMODE, CMODE, H><<<g, 256, 0, st>>>(p)
   if (nt == 1) {
     if (ks == 1) NBP_SKINNY(1, 1); else if (ks == 2) NBP_SKINNY(1, 2); else if (ks == 3) NBP_SKINNY(1, 3);
     else if (ks == 4) NBP_SKINNY(1, 4); else NBP_SKINNY(1, 8);
@@ -851,6 +853,7 @@ void launch_skinny(const SkinnyP& p, hipStream_t st) {
 }
 
 // whether the skinny path serves this call (bf16 in / out, N and K <= 64, supported modes, aligned rows)
+template <typename H>
 bool try_skinny(const void* A, long lda, int a_mode, const float* a_scale, int rows, const void* Bw, long ldb, void* C,
                 long ldc, int c_mode, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                 void* pre, hipStream_t st) {
@@ -859,27 +862,29 @@ bool try_skinny(const void* A, long lda, int a_mode, const float* a_scale, int r
                   (a_mode == AM_PLAIN && c_mode == CM_SG) || (a_mode == AM_SCALE && c_mode == CM_SGBWD) ||
                   (a_mode == AM_PLAIN && c_mode == CM_SGBWD);
   if (!ok) return false;
-  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, a_scale, rows, reinterpret_cast<const __bf16*>(Bw), ldb,
-            reinterpret_cast<__bf16*>(C), ldc, M, N, K, bias, reinterpret_cast<const __bf16*>(R), rscale,
-            reinterpret_cast<__bf16*>(pre), nullptr, nullptr, nullptr, nullptr, nullptr};
-  if (c_mode == CM_SG) launch_skinny<AM_PLAIN, CM_SG>(p, st);
-  else if (c_mode == CM_SGBWD && a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_SGBWD>(p, st);
-  else if (c_mode == CM_SGBWD) launch_skinny<AM_PLAIN, CM_SGBWD>(p, st);
-  else if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_PLAIN>(p, st);
-  else launch_skinny<AM_PLAIN, CM_PLAIN>(p, st);
+  SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, a_scale, rows, reinterpret_cast<const H*>(Bw), ldb,
+            reinterpret_cast<H*>(C), ldc, M, N, K, bias, reinterpret_cast<const H*>(R), rscale,
+            reinterpret_cast<H*>(pre), nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (c_mode == CM_SG) launch_skinny<AM_PLAIN, CM_SG, H>(p, st);
+  else if (c_mode == CM_SGBWD && a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_SGBWD, H>(p, st);
+  else if (c_mode == CM_SGBWD) launch_skinny<AM_PLAIN, CM_SGBWD, H>(p, st);
+  else if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_PLAIN, H>(p, st);
+  else launch_skinny<AM_PLAIN, CM_PLAIN, H>(p, st);
   return true;
 }
 
 // fp32 flat parameters -> bf16 copy (all), plus transposed bf16 copies of the listed [rows][cols] matrices
-__global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, __bf16* __restrict__ dst) {
+template <typename H>
+__global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, H* __restrict__ dst) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    dst[i] = (__bf16)src[i];
+    dst[i] = (H)src[i];
 }
 
 // desc: [ndesc][4] int64 {offset, rows, cols, row-scale offset or -1}; block (x: tile index, y: matrix).  With a
 // row scale s (the layer scale beta / gamma of conv3 / conv5) the copy is (diag(s) W)^T.
+template <typename H>
 __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long* __restrict__ desc,
-                                      __bf16* __restrict__ dst_t) {
+                                      H* __restrict__ dst_t) {
   __shared__ float tile[32][33];
   const long off = desc[blockIdx.y * 4], R = desc[blockIdx.y * 4 + 1], Cc = desc[blockIdx.y * 4 + 2];
   const long soff = desc[blockIdx.y * 4 + 3];
@@ -894,17 +899,17 @@ __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long*
     __syncthreads();
     for (int cc = ty; cc < 32; cc += 8) {
       const long c = c0 + cc, r = r0 + tx;
-      if (r < R && c < Cc) dst_t[off + c * R + r] = (__bf16)tile[tx][cc];
+      if (r < R && c < Cc) dst_t[off + c * R + r] = (H)tile[tx][cc];
     }
     __syncthreads();
   }
 }
 
-template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC>
+template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC, typename H>
 void launch(const GemmPB& p, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
-  if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC><<<grid, 256, 0, st>>>(p);
-  else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC><<<grid, 256, 0, st>>>(p);
+  if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
+  else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
 }
 
 // largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 1024 blocks (4 per CU);
@@ -918,20 +923,20 @@ long gemm_minblk() {
   return v;
 }
 
-template <int AMODE, int CMODE, typename TA, typename TC>
+template <int AMODE, int CMODE, typename TA, typename TC, typename H>
 void dispatch(const GemmPB& p, hipStream_t st) {
   if constexpr (CMODE == CM_CHANDOT) {  // its partial-sum layout is per 64-row tile
-    launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
+    launch<64, 64, AMODE, CMODE, TA, TC, H>(p, st);
   } else {
     auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
     const bool n128 = p.N > 64, m128 = p.M > 64;
     const long mb = gemm_minblk();
     // (128 x 128 from 512 blocks won in isolation on M 16K-64K shapes, scripts/gemm_micro.py, but lost 0.3 ms/step in
     // the training step: kept at >= 1024 blocks)
-    if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC>(p, st);
-    else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC>(p, st);
-    else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC>(p, st);
-    else launch<64, 64, AMODE, CMODE, TA, TC>(p, st);
+    if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC, H>(p, st);
+    else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC, H>(p, st);
+    else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC, H>(p, st);
+    else launch<64, 64, AMODE, CMODE, TA, TC, H>(p, st);
   }
 }
 
@@ -944,16 +949,16 @@ bool getenv_skinny() {
   return on;
 }
 
-template <typename TA, typename TC>
+template <typename TA, typename TC, typename H>
 int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {
-  if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch<AM_PLAIN, CM_PLAIN, TA, TC>(p, st);
-  else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch<AM_SCALE, CM_PLAIN, TA, TC>(p, st);
-  else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch<AM_S2D, CM_PLAIN, TA, TC>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch<AM_PLAIN, CM_D2S, TA, TC>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_SG) dispatch<AM_PLAIN, CM_SG, TA, TC>(p, st);
-  else if (a_mode == AM_SCALE && c_mode == CM_SGBWD) dispatch<AM_SCALE, CM_SGBWD, TA, TC>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_SGBWD) dispatch<AM_PLAIN, CM_SGBWD, TA, TC>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_CHANDOT) dispatch<AM_PLAIN, CM_CHANDOT, TA, TC>(p, st);
+  if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch<AM_PLAIN, CM_PLAIN, TA, TC, H>(p, st);
+  else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch<AM_SCALE, CM_PLAIN, TA, TC, H>(p, st);
+  else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch<AM_S2D, CM_PLAIN, TA, TC, H>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch<AM_PLAIN, CM_D2S, TA, TC, H>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_SG) dispatch<AM_PLAIN, CM_SG, TA, TC, H>(p, st);
+  else if (a_mode == AM_SCALE && c_mode == CM_SGBWD) dispatch<AM_SCALE, CM_SGBWD, TA, TC, H>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_SGBWD) dispatch<AM_PLAIN, CM_SGBWD, TA, TC, H>(p, st);
+  else if (a_mode == AM_PLAIN && c_mode == CM_CHANDOT) dispatch<AM_PLAIN, CM_CHANDOT, TA, TC, H>(p, st);
   else {
     set_error("nbp_gemm_bf16: unsupported mode combination");
     return NBP_ERR_ARG;
@@ -969,40 +974,47 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
                   const void* Bw, long ldb, void* C, long ldc, int c_mode, int c_dtype, int M, int N, int K, int gh,
                   int gw, int cs, const float* bias, const void* R, const float* rscale, void* pre, nbp_stream_t s) {
   NBP_REQUIRE(A && Bw && M > 0 && N > 0 && K > 0, "nbp_gemm_bf16: null pointer or empty shape");
+  NBP_REQUIRE(a_dtype >= 0 && a_dtype <= 2 && c_dtype >= 0 && c_dtype <= 2 &&
+              (a_dtype == 0 || c_dtype == 0 || a_dtype == c_dtype), "nbp_gemm_bf16: dtype");
+  // the 16-bit operand type (weights Bw and any 16-bit A / C): fp16 when either side is fp16, else bf16
+  const int hd = (a_dtype == 2 || c_dtype == 2) ? 2 : 1;
+  const bool h16 = a_dtype != 0 && c_dtype != 0;
   // C may be null only for the skinny SimpleGate forward (the gate input is then recomputed by the backward)
-  NBP_REQUIRE(C || (c_mode == CM_SG && a_dtype == 1 && c_dtype == 1 && N <= 64 && K <= 128 && getenv_skinny()),
-              "nbp_gemm_bf16: C is null");
+  NBP_REQUIRE(C || (c_mode == CM_SG && h16 && N <= 64 && K <= 128 && getenv_skinny()), "nbp_gemm_bf16: C is null");
   NBP_REQUIRE(K % 8 == 0 && N % 4 == 0 && ldb % 8 == 0, "nbp_gemm_bf16: K, ldb multiples of 8, N of 4 (K=%d N=%d)", K, N);
   NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && (c_mode == CM_PLAIN || c_mode == CM_D2S || c_mode == CM_SG ||
               c_mode == CM_SGBWD || c_mode == CM_CHANDOT), "nbp_gemm_bf16: mode");
-  NBP_REQUIRE(c_mode != CM_CHANDOT || (a_mode == AM_PLAIN && a_dtype == 1 && c_dtype == 1 && R && pre && !bias &&
+  NBP_REQUIRE(c_mode != CM_CHANDOT || (a_mode == AM_PLAIN && h16 && R && pre && !bias &&
                                        rows_per_img > 0 && rows_per_img % 64 == 0 && M % rows_per_img == 0 &&
                                        N % 8 == 0 && ldc % 8 == 0),
-              "nbp_gemm_bf16: channel-dot epilogue needs bf16, R (g), pre (the slab), rows_per_img a multiple of 64 "
-              "dividing M");
+              "nbp_gemm_bf16: channel-dot epilogue needs 16-bit storage, R (g), pre (the slab), rows_per_img a "
+              "multiple of 64 dividing M");
   NBP_REQUIRE(c_mode != CM_SG || (pre && N % 2 == 0 && ldc % 2 == 0 && !R),
               "nbp_gemm_bf16: SimpleGate epilogue needs pre (the gate map), even N and ldc, no residual");
   NBP_REQUIRE(c_mode != CM_SGBWD || (R && !bias && !pre && ldc >= 2L * N),
               "nbp_gemm_bf16: SimpleGate-backward epilogue needs R (the interleaved gate input) and ldc >= 2N");
-  NBP_REQUIRE((a_dtype == 0 || a_dtype == 1) && (c_dtype == 0 || c_dtype == 1), "nbp_gemm_bf16: dtype");
   NBP_REQUIRE(a_mode != AM_SCALE || (a_scale && rows_per_img > 0), "nbp_gemm_bf16: a_scale");
   NBP_REQUIRE((a_mode != AM_S2D && c_mode != CM_D2S) || (gh > 0 && gw > 0 && cs > 0 && cs % 8 == 0),
               "nbp_gemm_bf16: s2d geometry (cs multiple of 8)");
   NBP_REQUIRE(a_mode != AM_S2D || K == 4 * cs, "nbp_gemm_bf16: S2D needs K == 4*cs");
   NBP_REQUIRE(c_mode != CM_D2S || N == 4 * cs, "nbp_gemm_bf16: D2S needs N == 4*cs");
   NBP_REQUIRE(a_mode == AM_S2D || lda % 8 == 0, "nbp_gemm_bf16: lda alignment");
-  GemmPB p{A, lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb, C, ldc, M, N, K, gh, gw, cs,
-           bias, R, rscale, pre};
+  GemmPB p{A, lda, a_scale, rows_per_img, Bw, ldb, C, ldc, M, N, K, gh, gw, cs, bias, R, rscale, pre};
   hipStream_t st = S(s);
-  if (a_dtype == 1 && c_dtype == 1 && getenv_skinny() &&
-      try_skinny(A, lda, a_mode, a_scale, rows_per_img, Bw, ldb, C, ldc, c_mode, M, N, K, bias, R, rscale, pre, st))
-    return check_launch("gemm_bf16(skinny)");
+  int rc = NBP_OK;
+  bool done = false;
+  NBP_DISPATCH_H(hd, {
+    if (h16 && getenv_skinny() &&
+        try_skinny<H>(A, lda, a_mode, a_scale, rows_per_img, Bw, ldb, C, ldc, c_mode, M, N, K, bias, R, rscale, pre, st))
+      done = true;
+    else if (!C) rc = NBP_ERR_ARG;
+    else if (a_dtype == 0 && c_dtype == 0) rc = dispatch_modes<float, float, H>(p, a_mode, c_mode, st);
+    else if (h16) rc = dispatch_modes<H, H, H>(p, a_mode, c_mode, st);
+    else if (a_dtype == 0) rc = dispatch_modes<float, H, H>(p, a_mode, c_mode, st);
+    else rc = dispatch_modes<H, float, H>(p, a_mode, c_mode, st);
+  });
+  if (done) return check_launch("gemm_bf16(skinny)");
   NBP_REQUIRE(C, "nbp_gemm_bf16: C is null and the skinny path does not serve this shape");
-  int rc;
-  if (a_dtype == 0 && c_dtype == 0) rc = dispatch_modes<float, float>(p, a_mode, c_mode, st);
-  else if (a_dtype == 1 && c_dtype == 1) rc = dispatch_modes<__bf16, __bf16>(p, a_mode, c_mode, st);
-  else if (a_dtype == 0 && c_dtype == 1) rc = dispatch_modes<float, __bf16>(p, a_mode, c_mode, st);
-  else rc = dispatch_modes<__bf16, float>(p, a_mode, c_mode, st);
   if (rc) return rc;
   return check_launch("gemm_bf16");
 }
@@ -1013,106 +1025,137 @@ size_t nbp_dgrad_ln_workspace_floats(long M, int N) {
 
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
-                     float* ws, size_t ws_floats, nbp_stream_t s) {
+                     float* ws, size_t ws_floats, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(A && Wt && x && stats && lnw && dres && dx && dlnw && dlnb && ws && M > 0, "nbp_dgrad_ln_bwd: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_ln_bwd: 16-bit storage (dtype 1 bf16 / 2 fp16)");
+  float *slab_w, *slab_b;
+  long nb;
   if (N == 128 || N == 256) {  // 64 x N tiles of the tiled kernel: a whole row per tile
     NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_ln_bwd: K, lda, ldb multiples of 8");
-    const long nb = (M + 63) / 64;
+    nb = (M + 63) / 64;
     NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
-    GemmPB p{A, lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb, dx, N, M, N, K, 0, 0, 0, nullptr, x,
+    GemmPB p{A, lda, nullptr, 1, Wt, ldb, dx, N, M, N, K, 0, 0, 0, nullptr, x,
              nullptr, nullptr, lnw, nullptr, nullptr, nullptr, 0.f, reinterpret_cast<const float2*>(stats), dres, ws,
              ws + nb * N};
-    if (N == 256) launch<64, 256, AM_PLAIN, CM_LNBWD, __bf16, __bf16>(p, S(s));
-    else launch<64, 128, AM_PLAIN, CM_LNBWD, __bf16, __bf16>(p, S(s));
-    int rc = check_launch("dgrad_ln_bwd(tiled)");
-    if (rc) return rc;
-    rc = nbp_reduce_slab(p.slab_w, (int)nb, N, dlnw, s);
-    if (rc) return rc;
-    return nbp_reduce_slab(p.slab_b, (int)nb, N, dlnb, s);
+    NBP_DISPATCH_H(dtype, {
+      if (N == 256) launch<64, 256, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
+      else launch<64, 128, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
+    });
+    slab_w = p.slab_w;
+    slab_b = p.slab_b;
+  } else {
+    NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
+                "nbp_dgrad_ln_bwd: N must be 32, 64, 128 or 256, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
+    nb = skinny_blocks(M);
+    NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
+    slab_w = ws;
+    slab_b = ws + nb * N;
+    NBP_DISPATCH_H(dtype, {
+      SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, nullptr, 1, reinterpret_cast<const H*>(Wt), ldb,
+                   reinterpret_cast<H*>(dx), N, M, N, K, nullptr, reinterpret_cast<const H*>(x), nullptr, nullptr,
+                   reinterpret_cast<const float2*>(stats), lnw, reinterpret_cast<const H*>(dres), slab_w, slab_b};
+      launch_skinny<AM_PLAIN, CM_LNBWD, H>(p, S(s));
+    });
   }
-  NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
-              "nbp_dgrad_ln_bwd: N must be 32 or 64, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
-  const long nb = skinny_blocks(M);
-  NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
-  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb,
-            reinterpret_cast<__bf16*>(dx), N, M, N, K, nullptr, reinterpret_cast<const __bf16*>(x), nullptr, nullptr,
-            reinterpret_cast<const float2*>(stats), lnw, reinterpret_cast<const __bf16*>(dres), ws, ws + nb * N};
-  launch_skinny<AM_PLAIN, CM_LNBWD>(p, S(s));
   int rc = check_launch("dgrad_ln_bwd");
   if (rc) return rc;
-  rc = nbp_reduce_slab(p.slab_w, (int)nb, N, dlnw, s);
+  rc = nbp_reduce_slab(slab_w, (int)nb, N, dlnw, s);
   if (rc) return rc;
-  return nbp_reduce_slab(p.slab_b, (int)nb, N, dlnb, s);
+  return nbp_reduce_slab(slab_b, (int)nb, N, dlnb, s);
 }
 
 int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
-                    const float* lnw, const float* lnb, void* nout, float* stats, float eps, nbp_stream_t s) {
+                    const float* lnw, const float* lnb, void* nout, float* stats, float eps, int dtype,
+                    nbp_stream_t s) {
   NBP_REQUIRE(A && Bw && C && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_gemm_res_ln: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   NBP_REQUIRE(a_mode == AM_PLAIN || (a_mode == AM_SCALE && a_scale && rows_per_img > 0), "nbp_gemm_res_ln: a_mode");
   if (N == 128 || N == 256) {  // 64 x N tiles of the tiled kernel: a whole row per tile
     NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_gemm_res_ln: K, lda, ldb multiples of 8");
-    GemmPB p{A, lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb, C, N, M, N, K, 0, 0, 0, bias,
+    GemmPB p{A, lda, a_scale, rows_per_img, Bw, ldb, C, N, M, N, K, 0, 0, 0, bias,
              R, rscale, nullptr, lnw, lnb, nout, reinterpret_cast<float2*>(stats), eps};
-    if (N == 256 && a_mode == AM_SCALE) launch<64, 256, AM_SCALE, CM_RESLN, __bf16, __bf16>(p, S(s));
-    else if (N == 256) launch<64, 256, AM_PLAIN, CM_RESLN, __bf16, __bf16>(p, S(s));
-    else if (a_mode == AM_SCALE) launch<64, 128, AM_SCALE, CM_RESLN, __bf16, __bf16>(p, S(s));
-    else launch<64, 128, AM_PLAIN, CM_RESLN, __bf16, __bf16>(p, S(s));
+    NBP_DISPATCH_H(dtype, {
+      if (N == 256 && a_mode == AM_SCALE) launch<64, 256, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
+      else if (N == 256) launch<64, 256, AM_PLAIN, CM_RESLN, H, H, H>(p, S(s));
+      else if (a_mode == AM_SCALE) launch<64, 128, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
+      else launch<64, 128, AM_PLAIN, CM_RESLN, H, H, H>(p, S(s));
+    });
     return check_launch("gemm_res_ln(tiled)");
   }
   NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
-              "nbp_gemm_res_ln: N must be 32, 64 or 128, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
-  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, a_scale, rows_per_img, reinterpret_cast<const __bf16*>(Bw), ldb,
-            reinterpret_cast<__bf16*>(C), N, M, N, K, bias, reinterpret_cast<const __bf16*>(R), rscale, nullptr,
-            nullptr, lnw, nullptr, nullptr, nullptr, lnb, reinterpret_cast<__bf16*>(nout),
-            reinterpret_cast<float2*>(stats), eps};
-  if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_RESLN>(p, S(s));
-  else launch_skinny<AM_PLAIN, CM_RESLN>(p, S(s));
+              "nbp_gemm_res_ln: N must be 32, 64, 128 or 256, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
+  NBP_DISPATCH_H(dtype, {
+    SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, a_scale, rows_per_img, reinterpret_cast<const H*>(Bw), ldb,
+                 reinterpret_cast<H*>(C), N, M, N, K, bias, reinterpret_cast<const H*>(R), rscale, nullptr,
+                 nullptr, lnw, nullptr, nullptr, nullptr, lnb, reinterpret_cast<H*>(nout),
+                 reinterpret_cast<float2*>(stats), eps};
+    if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_RESLN, H>(p, S(s));
+    else launch_skinny<AM_PLAIN, CM_RESLN, H>(p, S(s));
+  });
   return check_launch("gemm_res_ln");
 }
 
 int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,
-                    void* C, int M, int N, int K, nbp_stream_t s) {
+                    void* C, int M, int N, int K, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(A && Wt && A2 && W2 && b2 && C && M > 0, "nbp_dgrad_sg_rc: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_sg_rc: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   NBP_REQUIRE(N == 32 && K == 32 && lda % 8 == 0 && ldb % 8 == 0,
               "nbp_dgrad_sg_rc: N = K = 32 (N=%d K=%d)", N, K);
-  SkinnyP p{reinterpret_cast<const __bf16*>(A), lda, nullptr, 1, reinterpret_cast<const __bf16*>(Wt), ldb,
-            reinterpret_cast<__bf16*>(C), 2L * N, M, N, K, nullptr, nullptr, nullptr, nullptr,
-            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
-            reinterpret_cast<const __bf16*>(A2), reinterpret_cast<const __bf16*>(W2), b2};
-  gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
+  NBP_DISPATCH_H(dtype, {
+    SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, nullptr, 1, reinterpret_cast<const H*>(Wt), ldb,
+                 reinterpret_cast<H*>(C), 2L * N, M, N, K, nullptr, nullptr, nullptr, nullptr,
+                 nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
+                 reinterpret_cast<const H*>(A2), reinterpret_cast<const H*>(W2), b2};
+    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC, H><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
+  });
   return check_launch("dgrad_sg_rc");
 }
 
-int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, nbp_stream_t s) {
+int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, int dtype,
+                     nbp_stream_t s) {
   NBP_REQUIRE(flat && out && n > 0 && (ndesc == 0 || (desc && out_t)) && ndesc <= 65535, "nbp_weights_bf16: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_weights_bf16: dtype 1 (bf16) or 2 (fp16)");
   long g = (n + 255) / 256;
-  cvt_bf16_kernel<<<(int)(g > 4096 ? 4096 : g), 256, 0, S(s)>>>(flat, n, reinterpret_cast<__bf16*>(out));
-  if (ndesc > 0)
-    transpose_bf16_kernel<<<dim3(256, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<__bf16*>(out_t));
+  NBP_DISPATCH_H(dtype, {
+    cvt_bf16_kernel<H><<<(int)(g > 4096 ? 4096 : g), 256, 0, S(s)>>>(flat, n, reinterpret_cast<H*>(out));
+    if (ndesc > 0)
+      transpose_bf16_kernel<H><<<dim3(256, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<H*>(out_t));
+  });
   return check_launch("weights_bf16");
 }
 
-// 3x3 zero-padded convolution over NHWC bf16 as an implicit GEMM on the bf16 MFMA kernel:
+// 3x3 zero-padded convolution over NHWC 16-bit maps as an implicit GEMM on the 16-bit MFMA kernel:
 //   y[b][i][j][n] = epi( sum_{t, c} x[b][i + t/3 - 1][j + t%3 - 1][c] * w[n][t][c] (+ bias[n]) )
-// epi: mode 0 bias + ReLU, 1 bias only, 2 ReLU-mask by R (y = acc where R > 0 else 0; no bias).  y is bf16
-// (y_dtype 1) or fp32 (y_dtype 0, modes 1 only).  Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
+// epi: mode 0 bias + ReLU, 1 bias only, 2 ReLU-mask by R (y = acc where R > 0 else 0; no bias).  x, w, R and a
+// 16-bit y share the type `dtype` (1 bf16, 2 fp16); y is that type (y_dtype 1) or fp32 (y_dtype 0, mode 1 only).
+// Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
 int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
-                     const void* R, void* y, int y_dtype, nbp_stream_t s) {
+                     const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0, "nbp_conv3x3_bf16: bad args");
   NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv3x3_bf16: Cin and Cout must be multiples of 8 (%d, %d)", Cin,
               Cout);
   NBP_REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || R) && (y_dtype == 1 || mode == 1),
               "nbp_conv3x3_bf16: mode / R / y_dtype");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_conv3x3_bf16: dtype 1 (bf16) or 2 (fp16)");
   const long M = (long)B * H * W;
   NBP_REQUIRE(M < (1L << 31), "nbp_conv3x3_bf16: too many pixels");
-  GemmPB p{x, 0, nullptr, 1, reinterpret_cast<const __bf16*>(w), 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
+  GemmPB p{x, 0, nullptr, 1, w, 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
            mode == 2 ? nullptr : bias, mode == 2 ? R : nullptr, nullptr, nullptr};
   hipStream_t st = S(s);
-  if (mode == 0) dispatch<AM_IM2COL, CM_RELU, __bf16, __bf16>(p, st);
-  else if (mode == 2) dispatch<AM_IM2COL, CM_MASK, __bf16, __bf16>(p, st);
-  else if (y_dtype == 1) dispatch<AM_IM2COL, CM_PLAIN, __bf16, __bf16>(p, st);
-  else dispatch<AM_IM2COL, CM_PLAIN, __bf16, float>(p, st);
+  if (dtype == 2) {
+    using T16 = _Float16;
+    if (mode == 0) dispatch<AM_IM2COL, CM_RELU, T16, T16, T16>(p, st);
+    else if (mode == 2) dispatch<AM_IM2COL, CM_MASK, T16, T16, T16>(p, st);
+    else if (y_dtype == 1) dispatch<AM_IM2COL, CM_PLAIN, T16, T16, T16>(p, st);
+    else dispatch<AM_IM2COL, CM_PLAIN, T16, float, T16>(p, st);
+  } else {
+    using T16 = __bf16;
+    if (mode == 0) dispatch<AM_IM2COL, CM_RELU, T16, T16, T16>(p, st);
+    else if (mode == 2) dispatch<AM_IM2COL, CM_MASK, T16, T16, T16>(p, st);
+    else if (y_dtype == 1) dispatch<AM_IM2COL, CM_PLAIN, T16, T16, T16>(p, st);
+    else dispatch<AM_IM2COL, CM_PLAIN, T16, float, T16>(p, st);
+  }
   return check_launch("conv3x3_bf16");
 }
 

@@ -10,6 +10,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// N-element vector of T (T = float, __bf16 or _Float16: the 16-bit storage / MFMA-operand types)
+template <typename T, int N>
+using vec_t = T __attribute__((ext_vector_type(N)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 namespace nbp {
 
@@ -38,13 +43,13 @@ __device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
 }
 __device__ __forceinline__ float get(float4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
-// storage-type generic quad (4 consecutive channels) access: fp32 storage or bf16 storage, fp32 math
+// storage-type generic quad (4 consecutive channels) access: fp32 or 16-bit (bf16 / fp16) storage, fp32 math
 template <typename T>
 __device__ __forceinline__ float4 ldq(const T* p) {
   if constexpr (sizeof(T) == 4) {
     return *reinterpret_cast<const float4*>(p);
   } else {
-    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(p);
     return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
   }
 }
@@ -53,27 +58,56 @@ __device__ __forceinline__ void stq(T* p, float4 v) {
   if constexpr (sizeof(T) == 4) {
     *reinterpret_cast<float4*>(p) = v;
   } else {
-    bf16x4 o;
-    o[0] = (__bf16)v.x; o[1] = (__bf16)v.y; o[2] = (__bf16)v.z; o[3] = (__bf16)v.w;
-    *reinterpret_cast<bf16x4*>(p) = o;
+    vec_t<T, 4> o;
+    o[0] = (T)v.x; o[1] = (T)v.y; o[2] = (T)v.z; o[3] = (T)v.w;
+    *reinterpret_cast<vec_t<T, 4>*>(p) = o;
   }
+}
+
+// 32x32x16 MFMA on 16-bit operands (8 per lane), fp32 accumulation: bf16 or fp16 by the operand type
+__device__ __forceinline__ floatx16 mfma32x32x16(vec_t<__bf16, 8> a, vec_t<__bf16, 8> b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx16 mfma32x32x16(vec_t<_Float16, 8> a, vec_t<_Float16, 8> b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+// ds_read_b64_tr_b16 for either 16-bit type (the transpose is type-agnostic)
+template <typename H>
+__device__ __forceinline__ vec_t<H, 4> ds_read_tr16(const H* lds) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)lds);
+  return __builtin_bit_cast(vec_t<H, 4>, v);
 }
 template <typename T>
 __device__ __forceinline__ float lds1(const T* p) { return (float)*p; }
 template <typename T>
 __device__ __forceinline__ void sts1(T* p, float v) { *p = (T)v; }
 
-// dtype code of the C-ABI: 0 fp32, 1 bf16
+// dtype code of the C-ABI: 0 fp32, 1 bf16, 2 fp16 (the reference's autocast dtype)
 #define NBP_DISPATCH_T(dtype, ...)                   \
   do {                                               \
     if ((dtype) == 0) {                              \
       using T = float;                               \
       __VA_ARGS__;                                   \
-    } else {                                         \
+    } else if ((dtype) == 1) {                       \
       using T = __bf16;                              \
+      __VA_ARGS__;                                   \
+    } else {                                         \
+      using T = _Float16;                            \
       __VA_ARGS__;                                   \
     }                                                \
   } while (0)
+// 16-bit storage only: 1 bf16, 2 fp16, as the type alias TN
+#define NBP_DISPATCH_16(dtype, TN, ...)              \
+  do {                                               \
+    if ((dtype) == 2) {                              \
+      using TN = _Float16;                           \
+      __VA_ARGS__;                                   \
+    } else {                                         \
+      using TN = __bf16;                             \
+      __VA_ARGS__;                                   \
+    }                                                \
+  } while (0)
+#define NBP_DISPATCH_H(dtype, ...) NBP_DISPATCH_16(dtype, H, __VA_ARGS__)
 
 // sum over the 64 lanes of a wave
 __device__ __forceinline__ float wave_sum(float v) {

@@ -17,7 +17,7 @@ __device__ __forceinline__ void ld_chunk(const T* p, float* f) {
     const float4 v = *reinterpret_cast<const float4*>(p);
     f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
   } else {
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+    const vec_t<T, 8> v = *reinterpret_cast<const vec_t<T, 8>*>(p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)v[j];
   }
@@ -27,10 +27,10 @@ __device__ __forceinline__ void st_chunk(T* p, const float* f) {
   if constexpr (sizeof(T) == 4) {
     *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
   } else {
-    bf16x8 v;
+    vec_t<T, 8> v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (__bf16)f[j];
-    *reinterpret_cast<bf16x8*>(p) = v;
+    for (int j = 0; j < 8; ++j) v[j] = (T)f[j];
+    *reinterpret_cast<vec_t<T, 8>*>(p) = v;
   }
 }
 
@@ -282,7 +282,7 @@ __global__ void ln_wb_nchw(const float* __restrict__ dy, const float* __restrict
 }
 
 int ln_grid(long M, int C, int dtype) {
-  const int chunks = C / (dtype == 1 ? 8 : 4);
+  const int chunks = C / (dtype != 0 ? 8 : 4);
   const int G = chunks >= 64 ? 64 : chunks;
   const long rows_per_block = 4L * 2 * (64 / G);
   long g = (M + rows_per_block - 1) / rows_per_block;
@@ -313,7 +313,7 @@ int nbp_ln_nhwc_grid(long M, int C, int dtype) { return ln_grid(M, C, dtype); }
 int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* nout, float* stats, long M, int C, float eps,
                     int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && b && nout && stats && M > 0, "nbp_ln_fwd_nhwc: bad args");
-  const int E = dtype == 1 ? 8 : 4;
+  const int E = dtype != 0 ? 8 : 4;
   NBP_REQUIRE(C >= E && C / E <= 256 && (C & (C - 1)) == 0, "nbp_ln_fwd_nhwc: C must be a power of two in [%d, %d]",
               E, 256 * E);
   const int g = ln_grid(M, C, dtype);
@@ -328,7 +328,7 @@ int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* nout, f
 int nbp_ln_bwd_nhwc(const void* dn, const void* x, const float* stats, const float* w, const void* dres, void* dx,
                     float* slab_w, float* slab_b, long M, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dn && x && stats && w && dx && slab_w && slab_b && M > 0, "nbp_ln_bwd_nhwc: bad args");
-  const int E = dtype == 1 ? 8 : 4;
+  const int E = dtype != 0 ? 8 : 4;
   NBP_REQUIRE(C >= E && C / E <= 256 && (C & (C - 1)) == 0, "nbp_ln_bwd_nhwc: C must be a power of two in [%d, %d]",
               E, 256 * E);
   const int g = ln_grid(M, C, dtype);

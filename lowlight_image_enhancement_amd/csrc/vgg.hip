@@ -10,9 +10,10 @@ using namespace nbp;
 
 namespace {
 
+template <typename HT>
 __global__ __launch_bounds__(256) void vgg_prep_kernel(const float* __restrict__ x, long HW, long npix, int clamp,
                                                        float m0, float m1, float m2, float s0, float s1, float s2,
-                                                       __bf16* __restrict__ y) {
+                                                       HT* __restrict__ y) {
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
     const long b = p / HW, q = p - b * HW;
     const float* xb = x + b * 3 * HW + q;
@@ -22,19 +23,20 @@ __global__ __launch_bounds__(256) void vgg_prep_kernel(const float* __restrict__
       v1 = fminf(fmaxf(v1, 0.f), 1.f);
       v2 = fminf(fmaxf(v2, 0.f), 1.f);
     }
-    bf16x8 o;
-    o[0] = (__bf16)((v0 - m0) / s0);
-    o[1] = (__bf16)((v1 - m1) / s1);
-    o[2] = (__bf16)((v2 - m2) / s2);
+    vec_t<HT, 8> o;
+    o[0] = (HT)((v0 - m0) / s0);
+    o[1] = (HT)((v1 - m1) / s1);
+    o[2] = (HT)((v2 - m2) / s2);
 #pragma unroll
-    for (int j = 3; j < 8; ++j) o[j] = (__bf16)0.f;
-    *reinterpret_cast<bf16x8*>(y + p * 8) = o;
+    for (int j = 3; j < 8; ++j) o[j] = (HT)0.f;
+    *reinterpret_cast<vec_t<HT, 8>*>(y + p * 8) = o;
   }
 }
 
 // 2x2 / stride-2 max pool over NHWC (floor), 8 channels per thread; idx = window position 0..3 of the maximum
-__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restrict__ x, int H, int W, int C, long total8,
-                                                          __bf16* __restrict__ y, unsigned char* __restrict__ idx) {
+template <typename HT>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const HT* __restrict__ x, int H, int W, int C, long total8,
+                                                          HT* __restrict__ y, unsigned char* __restrict__ idx) {
   const int Ho = H / 2, Wo = W / 2, C8 = C / 8;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
     const int c8 = e % C8;
@@ -43,12 +45,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
     const long t = o / Wo;
     const int i = t % Ho;
     const long b = t / Ho;
-    const __bf16* base = x + (((b * H + 2 * i) * W + 2 * j) * C + c8 * 8);
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(base);
-    const bf16x8 bq = *reinterpret_cast<const bf16x8*>(base + C);
-    const bf16x8 cq = *reinterpret_cast<const bf16x8*>(base + (long)W * C);
-    const bf16x8 dq = *reinterpret_cast<const bf16x8*>(base + (long)W * C + C);
-    bf16x8 out;
+    const HT* base = x + (((b * H + 2 * i) * W + 2 * j) * C + c8 * 8);
+    const vec_t<HT, 8> a = *reinterpret_cast<const vec_t<HT, 8>*>(base);
+    const vec_t<HT, 8> bq = *reinterpret_cast<const vec_t<HT, 8>*>(base + C);
+    const vec_t<HT, 8> cq = *reinterpret_cast<const vec_t<HT, 8>*>(base + (long)W * C);
+    const vec_t<HT, 8> dq = *reinterpret_cast<const vec_t<HT, 8>*>(base + (long)W * C + C);
+    vec_t<HT, 8> out;
     unsigned long long packed = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -58,19 +60,20 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const __bf16* __restri
       if (v1 > best || v1 != v1) { best = v1; bi = 1; }
       if (v2 > best || v2 != v2) { best = v2; bi = 2; }
       if (v3 > best || v3 != v3) { best = v3; bi = 3; }
-      out[k] = (__bf16)best;
+      out[k] = (HT)best;
       packed |= (unsigned long long)bi << (8 * k);
     }
-    *reinterpret_cast<bf16x8*>(y + o * C + c8 * 8) = out;
+    *reinterpret_cast<vec_t<HT, 8>*>(y + o * C + c8 * 8) = out;
     *reinterpret_cast<unsigned long long*>(idx + o * C + c8 * 8) = packed;
   }
 }
 
 // din = scatter(dout at the argmax) * (post_in > 0)   (the pool input is a post-ReLU map)
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restrict__ dy,
+template <typename HT>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const HT* __restrict__ dy,
                                                           const unsigned char* __restrict__ idx,
-                                                          const __bf16* __restrict__ post_in, int H, int W, int C,
-                                                          long total8, __bf16* __restrict__ dx) {
+                                                          const HT* __restrict__ post_in, int H, int W, int C,
+                                                          long total8, HT* __restrict__ dx) {
   const int Ho = H / 2, Wo = W / 2, C8 = C / 8;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
     const int c8 = e % C8;
@@ -79,26 +82,27 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const __bf16* __restri
     const long t = pix / W;
     const int i = t % H;
     const long b = t / H;
-    bf16x8 out;
+    vec_t<HT, 8> out;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) out[k] = (__bf16)0.f;
+    for (int k = 0; k < 8; ++k) out[k] = (HT)0.f;
     const int io = i / 2, jo = j / 2;
     if (io < Ho && jo < Wo) {
       const long o = ((b * Ho + io) * Wo + jo) * C + c8 * 8;
       const int pos = (i & 1) * 2 + (j & 1);
-      const bf16x8 g = *reinterpret_cast<const bf16x8*>(dy + o);
+      const vec_t<HT, 8> g = *reinterpret_cast<const vec_t<HT, 8>*>(dy + o);
       const unsigned long long packed = *reinterpret_cast<const unsigned long long*>(idx + o);
-      const bf16x8 pin = *reinterpret_cast<const bf16x8*>(post_in + pix * C + c8 * 8);
+      const vec_t<HT, 8> pin = *reinterpret_cast<const vec_t<HT, 8>*>(post_in + pix * C + c8 * 8);
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         if ((int)((packed >> (8 * k)) & 0xff) == pos && (float)pin[k] > 0.f) out[k] = g[k];
     }
-    *reinterpret_cast<bf16x8*>(dx + pix * C + c8 * 8) = out;
+    *reinterpret_cast<vec_t<HT, 8>*>(dx + pix * C + c8 * 8) = out;
   }
 }
 
 // loss partials of mode 0: (a - b)^2, mode 1: |a - b|
-__global__ __launch_bounds__(256) void feat_dist_fwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b, long n,
+template <typename HT>
+__global__ __launch_bounds__(256) void feat_dist_fwd(const HT* __restrict__ a, const HT* __restrict__ b, long n,
                                                      int mode, double* __restrict__ part) {
   __shared__ double red[16];
   double acc = 0.0;
@@ -119,15 +123,16 @@ __global__ void feat_dist_finalize(const double* __restrict__ part, int n, doubl
 }
 
 // da = up[0] * scale * (mode 0: 2 (a - b), mode 1: sign(a - b)) * (relu_mask ? (a > 0) : 1)
-__global__ __launch_bounds__(256) void feat_dist_bwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b, long n,
+template <typename HT>
+__global__ __launch_bounds__(256) void feat_dist_bwd(const HT* __restrict__ a, const HT* __restrict__ b, long n,
                                                      int mode, float scale, int relu_mask, const float* __restrict__ up,
-                                                     __bf16* __restrict__ da) {
+                                                     HT* __restrict__ da) {
   const float g = up[0] * scale;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float av = (float)a[i], d = av - (float)b[i];
     float v = mode == 0 ? 2.f * d : (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f));
     if (relu_mask && !(av > 0.f)) v = 0.f;
-    da[i] = (__bf16)(g * v);
+    da[i] = (HT)(g * v);
   }
 }
 
@@ -149,16 +154,18 @@ __global__ __launch_bounds__(256) void vgg_input_grad_kernel(const float* __rest
 }
 
 // d += g * (post > 0)  (a tapped post-ReLU map's gradient joining the backward walk), all bf16
-__global__ __launch_bounds__(256) void add_relu_masked_kernel(__bf16* __restrict__ d, const __bf16* __restrict__ g,
-                                                              const __bf16* __restrict__ post, long n) {
+template <typename HT>
+__global__ __launch_bounds__(256) void add_relu_masked_kernel(HT* __restrict__ d, const HT* __restrict__ g,
+                                                              const HT* __restrict__ post, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    if ((float)post[i] > 0.f) d[i] = (__bf16)((float)d[i] + (float)g[i]);
+    if ((float)post[i] > 0.f) d[i] = (HT)((float)d[i] + (float)g[i]);
 }
 
 // ---------------------------------------------------------------- LPIPS tap distance (lpips 0.1.4, net='vgg')
 // per pixel: u = a / (|a| + 1e-10), v = b / (|b| + 1e-10) over the C channels (normalize_tensor),
 // d = sum_c w_c (u_c - v_c)^2 (the 1x1 'lin' head); per image out[n] (+)= mean over pixels (spatial_average).
-__global__ __launch_bounds__(256) void lpips_tap_fwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+template <typename HT>
+__global__ __launch_bounds__(256) void lpips_tap_fwd(const HT* __restrict__ a, const HT* __restrict__ b,
                                                      const float* __restrict__ w, long HW, int C, int chunks,
                                                      double* __restrict__ slab) {
   __shared__ double red[16];
@@ -166,11 +173,11 @@ __global__ __launch_bounds__(256) void lpips_tap_fwd(const __bf16* __restrict__ 
   const long per = (HW + chunks - 1) / chunks, q0 = (long)blockIdx.x * per, q1 = min(HW, q0 + per);
   double acc = 0.0;
   for (long q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-    const __bf16* pa = a + ((long)n * HW + q) * C;
-    const __bf16* pb = b + ((long)n * HW + q) * C;
+    const HT* pa = a + ((long)n * HW + q) * C;
+    const HT* pb = b + ((long)n * HW + q) * C;
     float sa = 0.f, sb = 0.f;
     for (int c = 0; c < C; c += 8) {
-      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         sa = fmaf((float)va[j], (float)va[j], sa);
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(256) void lpips_tap_fwd(const __bf16* __restrict__ 
     const float ia = 1.f / (sqrtf(sa) + 1e-10f), ib = 1.f / (sqrtf(sb) + 1e-10f);
     float d = 0.f;
     for (int c = 0; c < C; c += 8) {
-      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float t = (float)va[j] * ia - (float)vb[j] * ib;
@@ -204,17 +211,18 @@ __global__ void lpips_finalize(const double* __restrict__ slab, int N, int chunk
 
 // d a_k = up[n] / HW * (g_k / na - a_k (sum_c g_c a_c) / (na^2 |a|)),  g_c = 2 w_c (u_c - v_c), na = |a| + 1e-10.
 // A pixel whose feature vector is all zero gets zero gradient (torch's sqrt backward yields NaN there).
-__global__ __launch_bounds__(256) void lpips_tap_bwd(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+template <typename HT>
+__global__ __launch_bounds__(256) void lpips_tap_bwd(const HT* __restrict__ a, const HT* __restrict__ b,
                                                      const float* __restrict__ w, long HW, int C, long npix,
-                                                     const float* __restrict__ up, __bf16* __restrict__ da) {
+                                                     const float* __restrict__ up, HT* __restrict__ da) {
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
     const long n = p / HW;
-    const __bf16* pa = a + p * C;
-    const __bf16* pb = b + p * C;
-    __bf16* pd = da + p * C;
+    const HT* pa = a + p * C;
+    const HT* pb = b + p * C;
+    HT* pd = da + p * C;
     float sa = 0.f, sb = 0.f;
     for (int c = 0; c < C; c += 8) {
-      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         sa = fmaf((float)va[j], (float)va[j], sa);
@@ -222,16 +230,16 @@ __global__ __launch_bounds__(256) void lpips_tap_bwd(const __bf16* __restrict__ 
       }
     }
     if (sa == 0.f) {
-      bf16x8 z;
+      vec_t<HT, 8> z;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
-      for (int c = 0; c < C; c += 8) *reinterpret_cast<bf16x8*>(pd + c) = z;
+      for (int j = 0; j < 8; ++j) z[j] = (HT)0.f;
+      for (int c = 0; c < C; c += 8) *reinterpret_cast<vec_t<HT, 8>*>(pd + c) = z;
       continue;
     }
     const float ra = sqrtf(sa), na = ra + 1e-10f, ia = 1.f / na, ib = 1.f / (sqrtf(sb) + 1e-10f);
     float G = 0.f;
     for (int c = 0; c < C; c += 8) {
-      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
+      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float av = (float)va[j];
@@ -240,15 +248,15 @@ __global__ __launch_bounds__(256) void lpips_tap_bwd(const __bf16* __restrict__ 
     }
     const float s = up[n] / (float)HW, k2 = G / (na * na * ra);
     for (int c = 0; c < C; c += 8) {
-      const bf16x8 va = *reinterpret_cast<const bf16x8*>(pa + c), vb = *reinterpret_cast<const bf16x8*>(pb + c);
-      bf16x8 o;
+      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
+      vec_t<HT, 8> o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float av = (float)va[j];
         const float g = 2.f * w[c + j] * (av * ia - (float)vb[j] * ib);
-        o[j] = (__bf16)(s * (g * ia - av * k2));
+        o[j] = (HT)(s * (g * ia - av * k2));
       }
-      *reinterpret_cast<bf16x8*>(pd + c) = o;
+      *reinterpret_cast<vec_t<HT, 8>*>(pd + c) = o;
     }
   }
 }
@@ -263,28 +271,29 @@ inline int grid_for(long n) {
 extern "C" {
 
 int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float m1, float m2, float s0, float s1,
-                 float s2, void* y, nbp_stream_t s) {
+                 float s2, void* y, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && y && B > 0 && H > 0 && W > 0, "nbp_vgg_prep: bad args");
   const long HW = (long)H * W, n = B * HW;
-  vgg_prep_kernel<<<grid_for(n), 256, 0, S(s)>>>(x, HW, n, clamp, m0, m1, m2, s0, s1, s2, reinterpret_cast<__bf16*>(y));
+  NBP_DISPATCH_16(dtype, HT, vgg_prep_kernel<HT><<<grid_for(n), 256, 0, S(s)>>>(x, HW, n, clamp, m0, m1, m2, s0, s1, s2,
+                                                                              reinterpret_cast<HT*>(y)));
   return check_launch("vgg_prep");
 }
 
-int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, nbp_stream_t s) {
+int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && y && idx && B > 0 && H >= 2 && W >= 2 && C % 8 == 0, "nbp_maxpool2_fwd: bad args");
   const long total8 = (long)B * (H / 2) * (W / 2) * (C / 8);
-  maxpool_fwd_kernel<<<grid_for(total8), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(x), H, W, C, total8,
-                                                         reinterpret_cast<__bf16*>(y), idx);
+  NBP_DISPATCH_16(dtype, HT, maxpool_fwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(x), H, W, C, total8, reinterpret_cast<HT*>(y), idx));
   return check_launch("maxpool2_fwd");
 }
 
 int nbp_maxpool2_bwd(const void* dy, const unsigned char* idx, const void* post_in, int B, int H, int W, int C, void* dx,
-                     nbp_stream_t s) {
+                     int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dy && idx && post_in && dx && B > 0 && H >= 2 && W >= 2 && C % 8 == 0, "nbp_maxpool2_bwd: bad args");
   const long total8 = (long)B * H * W * (C / 8);
-  maxpool_bwd_kernel<<<grid_for(total8), 256, 0, S(s)>>>(
-      reinterpret_cast<const __bf16*>(dy), idx, reinterpret_cast<const __bf16*>(post_in), H, W, C, total8,
-      reinterpret_cast<__bf16*>(dx));
+  NBP_DISPATCH_16(dtype, HT, maxpool_bwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(dy), idx, reinterpret_cast<const HT*>(post_in), H, W, C, total8,
+      reinterpret_cast<HT*>(dx)));
   return check_launch("maxpool2_bwd");
 }
 
@@ -294,19 +303,21 @@ size_t nbp_feat_dist_workspace_doubles(long n) {
 }
 
 int nbp_feat_dist_fwd(const void* a, const void* b, long n, int mode, double scale, double* ws, float* out,
-                      nbp_stream_t s) {
+                      int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && ws && out && n > 0 && (mode == 0 || mode == 1), "nbp_feat_dist_fwd: bad args");
   const int g = (int)nbp_feat_dist_workspace_doubles(n);
-  feat_dist_fwd<<<g, 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a), reinterpret_cast<const __bf16*>(b), n, mode, ws);
+  NBP_DISPATCH_16(dtype, HT, feat_dist_fwd<HT><<<g, 256, 0, S(s)>>>(reinterpret_cast<const HT*>(a),
+                                                                     reinterpret_cast<const HT*>(b), n, mode, ws));
   feat_dist_finalize<<<1, 64, 0, S(s)>>>(ws, g, scale, out);
   return check_launch("feat_dist_fwd");
 }
 
 int nbp_feat_dist_bwd(const void* a, const void* b, long n, int mode, float scale, int relu_mask, const float* up,
-                      void* da, nbp_stream_t s) {
+                      void* da, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && up && da && n > 0 && (mode == 0 || mode == 1), "nbp_feat_dist_bwd: bad args");
-  feat_dist_bwd<<<grid_for(n), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a), reinterpret_cast<const __bf16*>(b),
-                                               n, mode, scale, relu_mask, up, reinterpret_cast<__bf16*>(da));
+  NBP_DISPATCH_16(dtype, HT, feat_dist_bwd<HT><<<grid_for(n), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(a), reinterpret_cast<const HT*>(b), n, mode, scale, relu_mask, up,
+      reinterpret_cast<HT*>(da)));
   return check_launch("feat_dist_bwd");
 }
 
@@ -318,10 +329,10 @@ int nbp_vgg_input_grad(const float* d8, const float* x, int B, int H, int W, int
   return check_launch("vgg_input_grad");
 }
 
-int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, nbp_stream_t s) {
+int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(d && g && post && n > 0, "nbp_add_relu_masked: bad args");
-  add_relu_masked_kernel<<<grid_for(n), 256, 0, S(s)>>>(reinterpret_cast<__bf16*>(d), reinterpret_cast<const __bf16*>(g),
-                                                        reinterpret_cast<const __bf16*>(post), n);
+  NBP_DISPATCH_16(dtype, HT, add_relu_masked_kernel<HT><<<grid_for(n), 256, 0, S(s)>>>(
+      reinterpret_cast<HT*>(d), reinterpret_cast<const HT*>(g), reinterpret_cast<const HT*>(post), n));
   return check_launch("add_relu_masked");
 }
 
@@ -334,22 +345,21 @@ inline int lpips_chunks(long HW, int N) {
 size_t nbp_lpips_tap_workspace_doubles(int N, long HW) { return (size_t)N * lpips_chunks(HW, N); }
 
 int nbp_lpips_tap_fwd(const void* a, const void* b, const float* w, int N, long HW, int C, int accumulate, double* ws,
-                      float* out, nbp_stream_t s) {
+                      float* out, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && w && ws && out && N > 0 && N <= 65535 && HW > 0 && C % 8 == 0, "nbp_lpips_tap_fwd: bad args");
   const int chunks = lpips_chunks(HW, N);
-  lpips_tap_fwd<<<dim3(chunks, N), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a),
-                                                   reinterpret_cast<const __bf16*>(b), w, HW, C, chunks, ws);
+  NBP_DISPATCH_16(dtype, HT, lpips_tap_fwd<HT><<<dim3(chunks, N), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(a), reinterpret_cast<const HT*>(b), w, HW, C, chunks, ws));
   lpips_finalize<<<cdiv(N, 256), 256, 0, S(s)>>>(ws, N, chunks, 1.0 / (double)HW, accumulate, out);
   return check_launch("lpips_tap_fwd");
 }
 
 int nbp_lpips_tap_bwd(const void* a, const void* b, const float* w, int N, long HW, int C, const float* up, void* da,
-                      nbp_stream_t s) {
+                      int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && w && up && da && N > 0 && HW > 0 && C % 8 == 0, "nbp_lpips_tap_bwd: bad args");
   const long npix = (long)N * HW;
-  lpips_tap_bwd<<<grid_for(npix), 256, 0, S(s)>>>(reinterpret_cast<const __bf16*>(a),
-                                                  reinterpret_cast<const __bf16*>(b), w, HW, C, npix, up,
-                                                  reinterpret_cast<__bf16*>(da));
+  NBP_DISPATCH_16(dtype, HT, lpips_tap_bwd<HT><<<grid_for(npix), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(a), reinterpret_cast<const HT*>(b), w, HW, C, npix, up, reinterpret_cast<HT*>(da)));
   return check_launch("lpips_tap_bwd");
 }
 

@@ -60,15 +60,17 @@ class _LPIPSFn(torch.autograd.Function):
         want = ctx.needs_input_grad[0]
         with torch.no_grad():
             # the ScalingLayer is the prologue's (x - mean) / std with mean = shift, std = scale (no clamp)
-            f0, tape, t0 = stack.forward(_vgg.prep_input(x0, SHIFT, SCALE, clamp=False), save=want, taps=TAPS)
-            _, _, t1 = stack.forward(_vgg.prep_input(x1, SHIFT, SCALE, clamp=False), save=False, taps=TAPS)
+            f0, tape, t0 = stack.forward(_vgg.prep_input(x0, SHIFT, SCALE, clamp=False, dtype=stack.dtype), save=want,
+                                         taps=TAPS)
+            _, _, t1 = stack.forward(_vgg.prep_input(x1, SHIFT, SCALE, clamp=False, dtype=stack.dtype), save=False,
+                                     taps=TAPS)
         N = in0.shape[0]
         out = torch.zeros(N, device=in0.device)
         for k, tap in enumerate(TAPS):
             a, b = t0[tap], t1[tap]
             HW = a.shape[1] * a.shape[2]
             ws = torch.empty(query("lpips_tap_workspace_doubles", N, HW), dtype=torch.float64, device=a.device)
-            call("lpips_tap_fwd", a, b, lins[k], N, HW, a.shape[3], 1, ws, out)
+            call("lpips_tap_fwd", a, b, lins[k], N, HW, a.shape[3], 1, ws, out, stack.dtype)
         if want:
             ctx.tape, ctx.t0, ctx.t1, ctx.stack, ctx.lins = tape, t0, t1, stack, lins
             ctx.normalize = normalize
@@ -83,11 +85,12 @@ class _LPIPSFn(torch.autograd.Function):
         for k, tap in enumerate(TAPS):
             a, b = ctx.t0[tap], ctx.t1[tap]
             g = torch.empty_like(a)
-            call("lpips_tap_bwd", a, b, ctx.lins[k], a.shape[0], a.shape[1] * a.shape[2], a.shape[3], up, g)
+            call("lpips_tap_bwd", a, b, ctx.lins[k], a.shape[0], a.shape[1] * a.shape[2], a.shape[3], up, g,
+                 ctx.stack.dtype)
             grads[tap] = g
         last = TAPS[-1]
         d_last = torch.empty_like(grads[last])  # relu5_3 is the stack's last map: its pre-ReLU gradient
-        call("add_relu_masked", d_last.zero_(), grads.pop(last), ctx.t0[last], d_last.numel())
+        call("add_relu_masked", d_last.zero_(), grads.pop(last), ctx.t0[last], d_last.numel(), ctx.stack.dtype)
         d8 = ctx.stack.backward(ctx.tape, d_last, tap_grads=grads)
         dx = _vgg.input_grad(d8, x0, SCALE, clamp=False)
         if ctx.normalize:
@@ -99,15 +102,16 @@ class _LPIPSFn(torch.autograd.Function):
 class LPIPS(nn.Module):
     """lpips.LPIPS(net='vgg') drop-in: forward(in0, in1, retPerLayer=False, normalize=False) -> [N,1,1,1]."""
 
-    def __init__(self, net: str = "vgg", weights=None, version: str = "0.1", **_):
+    def __init__(self, net: str = "vgg", weights=None, version: str = "0.1", precision: str = "bf16", **_):
         super().__init__()
         if net != "vgg":
             raise NotImplementedError("LPIPS on MI355X implements net='vgg' (the HybridLossPlus term)")
         self._weights = weights
         self._parts = {}
+        self.precision = precision  # the VGG16 trunk's 16-bit type: "bf16" or "fp16" (see PerceptualLoss)
 
     def parts(self, device):
-        key = str(device)
+        key = (str(device), self.precision)
         if key not in self._parts:
             if self._weights is None:
                 warnings.warn("LPIPS: pretrained VGG16 / lin weights are not available offline; using a deterministic "
@@ -119,7 +123,7 @@ class LPIPS(nn.Module):
                 sd = torch.load(self._weights, map_location="cpu", weights_only=True) if isinstance(
                     self._weights, str) else dict(self._weights)
                 feats, lins = _split_state_dict(sd)
-            stack = _vgg.VGGStack(_vgg.VGG16_CFG, 30, device, feats)
+            stack = _vgg.VGGStack(_vgg.VGG16_CFG, 30, device, feats, dtype={"bf16": 1, "fp16": 2}[self.precision])
             self._parts[key] = (stack, [lins[k].to(device).float().contiguous() for k in range(5)])
         return self._parts[key]
 
@@ -127,21 +131,23 @@ class LPIPS(nn.Module):
         """Autograd-free form for the fused trainer: out[N] = LPIPS(clamp01(in0), clamp01(in1)) per image (the
         HybridLossPlus call on Bhat_srgb01 / B_srgb01), returns d(sum_n up[n] out[n]) / d in0 (through the clamp)."""
         stack, lins = self.parts(in0.device)
-        f0, tape, t0 = stack.forward(_vgg.prep_input(in0, SHIFT, SCALE, clamp=clamp), save=True, taps=TAPS)
-        _, _, t1 = stack.forward(_vgg.prep_input(in1, SHIFT, SCALE, clamp=clamp), save=False, taps=TAPS)
+        f0, tape, t0 = stack.forward(_vgg.prep_input(in0, SHIFT, SCALE, clamp=clamp, dtype=stack.dtype), save=True,
+                                     taps=TAPS)
+        _, _, t1 = stack.forward(_vgg.prep_input(in1, SHIFT, SCALE, clamp=clamp, dtype=stack.dtype), save=False,
+                                 taps=TAPS)
         N = in0.shape[0]
         grads = {}
         for k, tap in enumerate(TAPS):
             a, b = t0[tap], t1[tap]
             HW, C = a.shape[1] * a.shape[2], a.shape[3]
             ws = torch.empty(query("lpips_tap_workspace_doubles", N, HW), dtype=torch.float64, device=a.device)
-            call("lpips_tap_fwd", a, b, lins[k], N, HW, C, int(k > 0), ws, out)
+            call("lpips_tap_fwd", a, b, lins[k], N, HW, C, int(k > 0), ws, out, stack.dtype)
             g = torch.empty_like(a)
-            call("lpips_tap_bwd", a, b, lins[k], N, HW, C, up, g)
+            call("lpips_tap_bwd", a, b, lins[k], N, HW, C, up, g, stack.dtype)
             grads[tap] = g
         last = TAPS[-1]
         d_last = torch.zeros_like(grads[last])
-        call("add_relu_masked", d_last, grads.pop(last), t0[last], d_last.numel())
+        call("add_relu_masked", d_last, grads.pop(last), t0[last], d_last.numel(), stack.dtype)
         return _vgg.input_grad(stack.backward(tape, d_last, tap_grads=grads), in0, SCALE, clamp=clamp)
 
     def forward(self, in0, in1, retPerLayer: bool = False, normalize: bool = False):

@@ -116,8 +116,9 @@ class NAFNet(nn.Module):
         self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
-        # "fp32": fp32 operands everywhere (parity mode); "bf16": bf16 MFMA operands with fp32 accumulation
-        # (the reference's AMP training, image_restoration_model.py:255), fp32 storage and statistics.
+        # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
+        # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
+        # image_restoration_model.py:255; the trainer adds GradScaler-style dynamic loss scaling for it).
         self.precision = "fp32"
         # bf16 mode: the layer scales beta / gamma are folded into the transposed conv3 / conv5 weight copies (the
         # dgrad operands: dh = (beta (.) dy) W3 = dy (diag(beta) W3)), so those dgrads read A unscaled
@@ -205,22 +206,23 @@ class NAFNet(nn.Module):
             k.startswith(("downs.", "ups.")) and k.endswith("weight"))
 
     def _prep_weights(self, P: torch.Tensor):
-        """bf16 copy of the flat parameters + transposed copies of the GEMM weights (for the dgrads)."""
+        """16-bit copy of the flat parameters + transposed copies of the GEMM weights (for the dgrads)."""
         if self._tdesc is None or self._tdesc.device != P.device:
             self._tdesc = self._tdesc_cpu.to(P.device)
-        wb = torch.empty(self.numel, dtype=torch.bfloat16, device=P.device)
-        wt = torch.empty(self.numel, dtype=torch.bfloat16, device=P.device)
-        call("weights_bf16", P, self.numel, wb, self._tdesc, self._tdesc.shape[0], wt)
+        wb = torch.empty(self.numel, dtype=self.adt, device=P.device)
+        wt = torch.empty(self.numel, dtype=self.adt, device=P.device)
+        call("weights_bf16", P, self.numel, wb, self._tdesc, self._tdesc.shape[0], wt, self.dt)
         return wb, wt
 
     @property
     def adt(self) -> torch.dtype:
         """storage dtype of NHWC activations and activation gradients"""
-        return torch.float32 if self.precision == "fp32" else torch.bfloat16
+        return {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[self.precision]
 
     @property
     def dt(self) -> int:
-        return 0 if self.precision == "fp32" else 1
+        """dtype code of the C-ABI: 0 fp32, 1 bf16, 2 fp16"""
+        return {"fp32": 0, "bf16": 1, "fp16": 2}[self.precision]
 
     def _mm(self, W, A, lda, amode, ascale, rows, wkey, C, ldc, cmode, M, N, K, gh=0, gw=0, cs=0, bias=None,
             R=None, rscale=None, pre=None, dgrad=False):
@@ -232,8 +234,8 @@ class NAFNet(nn.Module):
                  M, N, K, gh, gw, cs, bias, R, rscale, pre)
         else:
             Wb = self._slice(W[2] if dgrad else W[1], wkey)
-            call("gemm_bf16", A, lda, amode, ascale, rows, 1, Wb, K, C, ldc, cmode, 1, M, N, K, gh, gw, cs, bias,
-                 R, rscale, pre)
+            call("gemm_bf16", A, lda, amode, ascale, rows, self.dt, Wb, K, C, ldc, cmode, self.dt, M, N, K, gh, gw, cs,
+                 bias, R, rscale, pre)
 
     # reference layout <-> internal layout
     def _to_internal(self, e: PEntry, t: torch.Tensor) -> torch.Tensor:
@@ -385,7 +387,7 @@ class NAFNet(nn.Module):
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
-        fuse_ln = self.fuse_ln_fwd and dt == 1 and len(self._W) == 3 and (c in (32, 64, 128) or
+        fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and (c in (32, 64, 128) or
                                                                            (c == 256 and self.fuse_ln256 in ("1", "fwd")))
         carry, self._ln_carry = self._ln_carry, None
         if carry is not None and carry[0] is x:
@@ -412,7 +414,7 @@ class NAFNet(nn.Module):
         if fuse_ln:
             call("gemm_res_ln", g, c, AM_SCALE, a, h * w, self._slice(self._W[1], pre + "conv3.weight"), c, y, M, c, c,
                  self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
-                 self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS)
+                 self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS, dt)
         else:
             self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
                      bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
@@ -420,9 +422,9 @@ class NAFNet(nn.Module):
                  M, c, LN_EPS, dt)
         # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
         # it (sg_rc) or there is no backward
-        drop_t4 = dt == 1 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) == 3))
+        drop_t4 = dt != 0 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) == 3))
         t4, g2 = (None if drop_t4 else E(M, 2 * c)), E(M, c)
-        if dt == 1:  # SimpleGate in the GEMM epilogue
+        if dt != 0:  # SimpleGate in the GEMM epilogue
             self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
                      bias=self._slice(P, pre + "conv4.bias"), pre=g2)
         else:
@@ -435,7 +437,7 @@ class NAFNet(nn.Module):
             call("gemm_res_ln", g2, c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c, out, M, c,
                  c, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"),
                  self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), nn1, nst1,
-                 LN_EPS)
+                 LN_EPS, dt)
             self._ln_carry = (out.view(B, h, w, c), nn1, nst1)
         else:
             self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
@@ -605,11 +607,11 @@ class NAFNet(nn.Module):
         # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
         dt4 = E(M, 2 * c)
         folded = len(Wt) == 3 and self.fold_ls  # gamma / beta already in the transposed bf16 weights
-        if dt == 1:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises
+        if dt != 0:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises
             if S["t4"] is None:  # t4 = conv4(n2) rebuilt per tile inside the dgrad (level 0, folded layer scale)
                 assert folded and c == 32
                 call("dgrad_sg_rc", dout, c, self._slice(Wt[2], pre + "conv5.weight"), c, S["n2"],
-                     self._slice(Wt[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"), dt4, M, c, c)
+                     self._slice(Wt[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"), dt4, M, c, c, dt)
             elif folded:
                 self._mm(Wt, dout, c, AM_PLAIN, None, 1, pre + "conv5.weight", dt4, 2 * c, CM_SGBWD, M, c, c,
                          R=S["t4"], dgrad=True)
@@ -622,7 +624,7 @@ class NAFNet(nn.Module):
                      M, c, c, dgrad=True)
             call("sg_bwd", dg2, S["t4"], dt4, M, c, 1, dt)
         # the two wide weight gradients that only need dout / dt4 run as one grouped launch (nbp_wgrad_group)
-        group = dt == 1 and c % 128 == 0 and self.group_wgrad and not self.overlap_wgrad
+        group = dt != 0 and c % 128 == 0 and self.group_wgrad and not self.overlap_wgrad
         if group:
             call("wgrad_group", 1)
         U5, V5 = F(c * c), F(c)
@@ -632,7 +634,7 @@ class NAFNet(nn.Module):
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
         # conv4 input gradient + norm2 backward + residual
         # LN backward in the dgrad's epilogue (dn never stored): skinny kernel at C 32 / 64, 64 x 128 tiles at 128
-        fuse_ln = dt == 1 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
+        fuse_ln = dt != 0 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
                                (c == 256 and self.fuse_ln256 in ("1", "bwd")))
         dy = E(M, c)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
@@ -660,8 +662,8 @@ class NAFNet(nn.Module):
         if chandot:
             chunks = HW // 64
             da_slab = F(B * chunks * c)
-            call("gemm_bf16", dy, c, AM_PLAIN, None, HW, 1, self._slice(Wt[2], pre + "conv3.weight"), c, dh, c,
-                 CM_CHANDOT, 1, M, c, c, 0, 0, 0, None, S["g"], None, da_slab)
+            call("gemm_bf16", dy, c, AM_PLAIN, None, HW, dt, self._slice(Wt[2], pre + "conv3.weight"), c, dh, c,
+                 CM_CHANDOT, dt, M, c, c, 0, 0, 0, None, S["g"], None, da_slab)
         elif folded:
             self._mm(Wt, dy, c, AM_PLAIN, None, 1, pre + "conv3.weight", dh, c, CM_PLAIN, M, c, c, dgrad=True)
         else:
@@ -690,7 +692,7 @@ class NAFNet(nn.Module):
             call("sca_sg_dw_bwd_rec", dh, S["a"], ds, S["t1"], self._slice(P, pre + "conv2.weight"),
                  self._slice(P, pre + "conv2.bias"), dt1, self._slice(dflat, pre + "conv2.weight"),
                  self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        elif c % (16 if dt == 1 else 8) == 0:
+        elif c % (16 if dt != 0 else 8) == 0:
             call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
         else:
             dt2 = E(M, 2 * c)
@@ -722,7 +724,7 @@ class NAFNet(nn.Module):
         ws = self._ws(n_ws, dt.device)
         call("dgrad_ln_bwd", dt, 2 * c, self._slice(Wt[2], pre + wkey), 2 * c, M, c, 2 * c, x, st,
              self._slice(P, pre + norm + ".weight"), dres, out, self._slice(dflat, pre + norm + ".weight"),
-             self._slice(dflat, pre + norm + ".bias"), ws, n_ws)
+             self._slice(dflat, pre + norm + ".bias"), ws, n_ws, self.dt)
 
 
 class _NAFNetFn(torch.autograd.Function):

@@ -75,6 +75,10 @@ class NBPTrainer:
         if w_lpips and lpips is None:
             from .lpips import LPIPS
             lpips = LPIPS(net="vgg")
+        if net.precision == "fp16":  # the VGG trunks follow the autocast dtype under the trainer's loss scaling
+            for m in (perceptual, lpips):
+                if m is not None:
+                    m.precision = "fp16"
         self.perceptual, self.lpips = perceptual, lpips
         self.lpips_buf: Optional[torch.Tensor] = None
         self.lr, self.betas, self.wd, self.eps = lr, betas, weight_decay, eps

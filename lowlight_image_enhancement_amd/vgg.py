@@ -6,7 +6,9 @@ A frozen VGG `features` prefix (3x3 conv + ReLU, 2x2 max pool) runs over NHWC bf
   * the input gradient (weights are frozen: no weight gradients) is the same implicit GEMM over the gradient map with
     the tap-flipped, transposed weights; the ReLU masks ride in the epilogue (conv -> conv) or in the pool backward
     (conv -> pool -> conv); max pools keep their argmax.
-bf16 operands with fp32 accumulation, the counterpart of the reference's fp16 autocast on GPU.
+16-bit operands with fp32 accumulation: bf16 (default; no loss scaling needed) or fp16 (`dtype=2`, the reference's
+autocast dtype, used under the trainer's dynamic loss scaling -- its 11-bit significand keeps the deep input gradient
+far closer to fp32).
 
 Pretrained ImageNet weights (torchvision / lpips downloads) are not available offline: `weights=None` builds the
 architecture with a deterministic synthetic initialisation (kaiming-normal fan-out as torchvision, seed 0); pass a
@@ -68,8 +70,12 @@ class VGGStack:
     plus optional tap gradients to d(prepared input) [B][H][W][8] fp32."""
 
     def __init__(self, cfg, n_modules: int, device, weights: Union[None, str, Dict[str, torch.Tensor]] = None,
-                 seed: int = 0):
+                 seed: int = 0, dtype: int = 1):
+        if dtype not in (1, 2):
+            raise ValueError("VGGStack dtype: 1 (bf16) or 2 (fp16)")
         self.cfg, self.n_modules, self.device = cfg, n_modules, torch.device(device)
+        self.dtype = dtype
+        self.tdt = torch.float16 if dtype == 2 else torch.bfloat16
         if weights is None:
             warnings.warn("VGG: ImageNet weights are not available offline; using a deterministic synthetic "
                           "initialisation (pass weights=<state_dict or path> for real weights)", RuntimeWarning)
@@ -95,21 +101,21 @@ class VGGStack:
             wf = wp.permute(0, 2, 3, 1).reshape(cout, 9, cp)
             wt = wf.flip(1).permute(2, 1, 0).contiguous()
             self.layers.append(dict(kind="conv", idx=idx, cin=cp, cout=cout,
-                                    wf=wf.to(self.device, torch.bfloat16).contiguous(),
-                                    wt=wt.to(self.device, torch.bfloat16).contiguous(),
+                                    wf=wf.to(self.device, self.tdt).contiguous(),
+                                    wt=wt.to(self.device, self.tdt).contiguous(),
                                     bias=b.to(self.device).contiguous()))
 
     # ------------------------------------------------------------------ forward
     def forward(self, x8: torch.Tensor, save: bool, taps: Sequence[int] = ()):
-        """x8: [B][H][W][8] bf16 prepared input.  Returns (final post-ReLU map, tape, {tap index: post map})."""
+        """x8: [B][H][W][8] 16-bit prepared input (prep_input with this stack's dtype).  Returns (final post-ReLU map, tape, {tap index: post map})."""
         B, H, W, _ = x8.shape
         h, w, feat = H, W, x8
         tape: List = []
         tapped = {}
         for L in self.layers:
             if L["kind"] == "conv":
-                y = torch.empty(B, h, w, L["cout"], device=x8.device, dtype=torch.bfloat16)
-                call("conv3x3_bf16", feat, B, h, w, L["cin"], L["wf"], L["cout"], L["bias"], 0, None, y, 1)
+                y = torch.empty(B, h, w, L["cout"], device=x8.device, dtype=self.tdt)
+                call("conv3x3_bf16", feat, B, h, w, L["cin"], L["wf"], L["cout"], L["bias"], 0, None, y, 1, self.dtype)
                 if save:
                     tape.append(("conv", L, (B, h, w), y))
                 if L["idx"] + 1 in taps:
@@ -118,9 +124,9 @@ class VGGStack:
             else:
                 C = feat.shape[-1]
                 ho, wo = h // 2, w // 2
-                y = torch.empty(B, ho, wo, C, device=x8.device, dtype=torch.bfloat16)
+                y = torch.empty(B, ho, wo, C, device=x8.device, dtype=self.tdt)
                 idx = torch.empty(B, ho, wo, C, device=x8.device, dtype=torch.uint8)
-                call("maxpool2_fwd", feat, B, h, w, C, y, idx)
+                call("maxpool2_fwd", feat, B, h, w, C, y, idx, self.dtype)
                 if save:
                     tape.append(("pool", (B, h, w, C), idx, feat))
                 feat, h, w = y, ho, wo
@@ -128,7 +134,7 @@ class VGGStack:
 
     # ------------------------------------------------------------------ input gradient
     def backward(self, tape, d_last_pre: torch.Tensor, tap_grads: Optional[Dict[int, torch.Tensor]] = None):
-        """d_last_pre: gradient w.r.t. the last conv's PRE-ReLU output (bf16 NHWC).  tap_grads: {relu index:
+        """d_last_pre: gradient w.r.t. the last conv's PRE-ReLU output (16-bit NHWC).  tap_grads: {relu index:
         gradient w.r.t. that post-ReLU map} added where the walk passes it.  Returns d(prepared input) fp32 [B,H,W,8]."""
         tap_grads = tap_grads or {}
         d = d_last_pre
@@ -141,39 +147,39 @@ class VGGStack:
             prev = tape[k - 1] if k > 0 else None
             if prev is None:  # first conv: gradient of the prepared input
                 d8 = torch.empty(B, h, w, L["cin"], device=d.device)
-                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 1, None, d8, 0)
+                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 1, None, d8, 0, self.dtype)
                 return d8
             if prev[0] == "conv":  # conv -> ReLU -> conv: mask by the previous post map in the epilogue
                 post = prev[3]
-                dn = torch.empty(B, h, w, L["cin"], device=d.device, dtype=torch.bfloat16)
-                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 2, post, dn, 1)
+                dn = torch.empty(B, h, w, L["cin"], device=d.device, dtype=self.tdt)
+                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 2, post, dn, 1, self.dtype)
                 tg = tap_grads.get(prev[1]["idx"] + 1)
                 if tg is not None:  # + d(tap) * relu mask
-                    call("add_relu_masked", dn, tg.to(torch.bfloat16).contiguous(), post, dn.numel())
+                    call("add_relu_masked", dn, tg.to(self.tdt).contiguous(), post, dn.numel(), self.dtype)
                 d = dn
             else:  # conv -> ReLU -> pool -> conv
                 (_, (Bp, hp, wp, C), idx, pool_in) = prev
-                dp = torch.empty(B, h, w, L["cin"], device=d.device, dtype=torch.bfloat16)
-                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 1, None, dp, 1)
-                dn = torch.empty(Bp, hp, wp, C, device=d.device, dtype=torch.bfloat16)
-                call("maxpool2_bwd", dp, idx, pool_in, Bp, hp, wp, C, dn)
+                dp = torch.empty(B, h, w, L["cin"], device=d.device, dtype=self.tdt)
+                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 1, None, dp, 1, self.dtype)
+                dn = torch.empty(Bp, hp, wp, C, device=d.device, dtype=self.tdt)
+                call("maxpool2_bwd", dp, idx, pool_in, Bp, hp, wp, C, dn, self.dtype)
                 conv_before = tape[k - 2]
                 tg = tap_grads.get(conv_before[1]["idx"] + 1)
                 if tg is not None:
-                    call("add_relu_masked", dn, tg.to(torch.bfloat16).contiguous(), pool_in, dn.numel())
+                    call("add_relu_masked", dn, tg.to(self.tdt).contiguous(), pool_in, dn.numel(), self.dtype)
                 d = dn
         raise RuntimeError("VGG backward: tape has no conv layer")
 
 
-def prep_input(x: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD, clamp: bool = True) -> torch.Tensor:
-    """NCHW fp32 [B,3,H,W] -> NHWC bf16 [B,H,W,8] of (clamp01(x) - mean) / std (nbp_vgg_prep)."""
+def prep_input(x: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD, clamp: bool = True, dtype: int = 1) -> torch.Tensor:
+    """NCHW fp32 [B,3,H,W] -> NHWC 16-bit [B,H,W,8] of (clamp01(x) - mean) / std (nbp_vgg_prep)."""
     _lib.require_cuda(x)
     if x.dim() != 4 or x.shape[1] != 3:
         raise ValueError(f"VGG input must be [B,3,H,W], got {tuple(x.shape)}")
     x = x.float().contiguous()
     B, _, H, W = x.shape
-    y = torch.empty(B, H, W, 8, device=x.device, dtype=torch.bfloat16)
-    call("vgg_prep", x, B, H, W, int(clamp), *[float(v) for v in mean], *[float(v) for v in std], y)
+    y = torch.empty(B, H, W, 8, device=x.device, dtype=torch.float16 if dtype == 2 else torch.bfloat16)
+    call("vgg_prep", x, B, H, W, int(clamp), *[float(v) for v in mean], *[float(v) for v in std], y, dtype)
     return y
 
 

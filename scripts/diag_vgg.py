@@ -48,26 +48,29 @@ gen = torch.rand(2, 3, 64, 48, generator=g)
 tgt = torch.rand(2, 3, 64, 48, generator=g)
 mean = torch.tensor([0.485, 0.456, 0.406], dtype=torch.float64).view(1, 3, 1, 1)
 std = torch.tensor([0.229, 0.224, 0.225], dtype=torch.float64).view(1, 3, 1, 1)
-for n in (4, 9, 18, 27, 36):
-    st = VGGStack(VGG19_CFG, n, dev, sd)
-    x = gen.to(dev)
-    fg, tape, _ = st.forward(prep_input(x), save=True)
-    ft, _, _ = st.forward(prep_input(tgt.to(dev)), save=False)
-    d = torch.empty_like(fg)
-    up = torch.ones(1, device=dev)
-    call("feat_dist_bwd", fg, ft, fg.numel(), 0, 1.0 / fg.numel(), 1, up, d)
-    dx = input_grad(st.backward(tape, d), x)
-    res = []
-    for rb in (False, True):
-        xr = gen.double().requires_grad_(True)
-        xin = (xr.clamp(0, 1) - mean) / std
-        if rb:
-            xin = RoundBF16.apply(xin)
-        fr = torch_stack(sdb if rb else sd, xin, n, rb)
-        with torch.no_grad():
-            xt = (tgt.double() - mean) / std
-            ftr = torch_stack(sdb if rb else sd, bf(xt) if rb else xt, n, rb)
-        Fn.mse_loss(fr, ftr).backward()
-        res.append(rel(dx, xr.grad))
-    print(f"features[:{n}]: feat rel err vs fp64 {rel(fg.float(), torch_stack(sd, (gen.double() - mean) / std, n, False).permute(0, 2, 3, 1)):.4f}"
-          f"  grad rel err vs fp64 {res[0]:.4f}  vs bf16-emulation {res[1]:.4f}", flush=True)
+for dt, scale in ((1, 1.0), (2, 65536.0)):  # fp16 under the trainer's initial loss scale (GradScaler's 2^16)
+    for n in (4, 9, 18, 27, 36):
+        st = VGGStack(VGG19_CFG, n, dev, sd, dtype=dt)
+        x = gen.to(dev)
+        fg, tape, _ = st.forward(prep_input(x, dtype=dt), save=True)
+        ft, _, _ = st.forward(prep_input(tgt.to(dev), dtype=dt), save=False)
+        d = torch.empty_like(fg)
+        up = torch.full((1,), scale, device=dev)
+        call("feat_dist_bwd", fg, ft, fg.numel(), 0, 1.0 / fg.numel(), 1, up, d, dt)
+        dx = input_grad(st.backward(tape, d), x) / scale
+        res = []
+        for rb in ((False, True) if dt == 1 else (False,)):
+            xr = gen.double().requires_grad_(True)
+            xin = (xr.clamp(0, 1) - mean) / std
+            if rb:
+                xin = RoundBF16.apply(xin)
+            fr = torch_stack(sdb if rb else sd, xin, n, rb)
+            with torch.no_grad():
+                xt = (tgt.double() - mean) / std
+                ftr = torch_stack(sdb if rb else sd, bf(xt) if rb else xt, n, rb)
+            Fn.mse_loss(fr, ftr).backward()
+            res.append(rel(dx, xr.grad))
+        fe = rel(fg.float(), torch_stack(sd, (gen.double() - mean) / std, n, False).permute(0, 2, 3, 1))
+        emu = f"  vs bf16-emulation {res[1]:.4f}" if len(res) > 1 else ""
+        print(f"{'bf16' if dt == 1 else 'fp16'} features[:{n}]: feat rel err vs fp64 {fe:.4f}  grad rel err vs fp64 "
+              f"{res[0]:.4f}{emu}", flush=True)

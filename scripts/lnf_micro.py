@@ -26,6 +26,6 @@ for (M, N, amode) in [(16 * 256 * 256, 32, 2), (16 * 256 * 256, 32, 0), (16 * 12
                               None), 50)
     t_l = timeit(lambda: call("ln_fwd_nhwc", y, lnw, lnb, n, st, M, N, 1e-6, 1), 50)
     t_f = timeit(lambda: call("gemm_res_ln", A, K, amode, scale, rows, W, K, y, M, N, K, bias, R, rs, lnw, lnb, n, st,
-                              1e-6), 50)
+                              1e-6, 1), 50)
     print(f"M={M} N={N} amode={amode}: gemm {t_g:.1f} + ln {t_l:.1f} = {t_g + t_l:.1f} us | fused {t_f:.1f} us",
           flush=True)

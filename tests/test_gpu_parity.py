@@ -296,7 +296,7 @@ def test_nafnet_bf16_mode_close_to_reference(dev):
     assert torch.isfinite(net.flat.grad).all()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_integration_training_loss_decreases(dev, precision):
     """core_tests/test_integration_forward_amp.py:88-136 re-expressed: 5 steps on one batch, the loss decreases and
     the PSF buffer is unchanged."""
@@ -371,14 +371,14 @@ def test_wgrad_bf16_against_float64(dev, M, N, K, gmode, xmode):
 
 
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (1, 16, 32, 8, 0), (2, 33, 70, 32, 1), (3, 8, 8, 64, 1),
-                                           (2, 19, 23, 12, 0)])
+                                           (2, 19, 23, 12, 0), (2, 33, 70, 32, 2), (3, 8, 8, 64, 2)])
 def test_dw_bwd_against_float64(dev, B, H, W, C, dtype):
     """Depthwise 3x3 backward (tiled LDS kernel; C=12 exercises the untiled kernel) and the fused SCA+SimpleGate
     prologue variant vs float64 autograd of F.conv2d(groups=2C) on the same (dtype-rounded) tensors."""
     import torch.nn.functional as Fn
     from lowlight_image_enhancement_amd._lib import call, query
     gen = torch.Generator(device=dev).manual_seed(B * H + W * C + dtype)
-    td = torch.bfloat16 if dtype == 1 else torch.float32
+    td = {0: torch.float32, 1: torch.bfloat16, 2: torch.float16}[dtype]
     M, C2 = B * H * W, 2 * C
     t1 = torch.randn(M, C2, device=dev, generator=gen).to(td)
     dt2 = torch.randn(M, C2, device=dev, generator=gen).to(td)
@@ -395,13 +395,13 @@ def test_dw_bwd_against_float64(dev, B, H, W, C, dtype):
         y.backward(dt2_nhwc.double().view(B, H, W, C2).permute(0, 3, 1, 2))
         return x.grad.permute(0, 2, 3, 1).reshape(M, C2), wt.grad.view(C2, 9), bias.grad
 
-    tol = dict(atol=2e-2, rtol=1e-2) if dtype == 1 else dict(atol=1e-4, rtol=1e-5)
+    tol = dict(atol=2e-2, rtol=1e-2) if dtype != 0 else dict(atol=1e-4, rtol=1e-5)
     call("dw_bwd", dt2, t1, w, dt1, dW, db, ws, B, H, W, C, dtype)
     rx, rw, rb = ref(dt2)
     close(dt1.float(), rx.cpu().numpy(), **tol)
     close(dW, rw.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-4)
     close(db, rb.cpu().numpy(), atol=1e-3 * M ** 0.5, rtol=1e-4)
-    if C % (16 if dtype == 1 else 8):
+    if C % (16 if dtype != 0 else 8):
         return
     # fused: dt2 = (dg * t2[C:], dg * t2[:C]), dg = dh * a[b] + ds[b] / HW
     dh = torch.randn(M, C, device=dev, generator=gen).to(td)
@@ -418,14 +418,14 @@ def test_dw_bwd_against_float64(dev, B, H, W, C, dtype):
 
 
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 8, 8, 64, 1), (1, 16, 16, 8, 0),
-                                           (2, 19, 23, 12, 0), (2, 20, 130, 16, 1)])
+                                           (2, 19, 23, 12, 0), (2, 20, 130, 16, 1), (2, 20, 130, 16, 2)])
 def test_dw_sg_pool_fwd_against_float64(dev, B, H, W, C, dtype):
     """Depthwise 3x3 + bias -> SimpleGate -> pool partials -> SCA (tiled LDS kernel for C % 16 (bf16) / 8 (fp32),
     the chunked kernel otherwise) vs float64 torch on the same (dtype-rounded) input."""
     import torch.nn.functional as Fn
     from lowlight_image_enhancement_amd._lib import call, query
     gen = torch.Generator(device=dev).manual_seed(B + H * W + C + dtype)
-    td = torch.bfloat16 if dtype == 1 else torch.float32
+    td = {0: torch.float32, 1: torch.bfloat16, 2: torch.float16}[dtype]
     M, C2 = B * H * W, 2 * C
     t1 = torch.randn(M, C2, device=dev, generator=gen).to(td)
     w = torch.randn(C2, 9, device=dev, generator=gen)
@@ -443,7 +443,7 @@ def test_dw_sg_pool_fwd_against_float64(dev, B, H, W, C, dtype):
     rt2 = y.permute(0, 2, 3, 1).reshape(M, C2)
     rg = rt2[:, :C] * rt2[:, C:]
     rmean = rg.view(B, H * W, C).mean(1)
-    tol = dict(atol=3e-2, rtol=1e-2) if dtype == 1 else dict(atol=1e-4, rtol=1e-5)
+    tol = dict(atol=3e-2, rtol=1e-2) if dtype != 0 else dict(atol=1e-4, rtol=1e-5)
     close(t2.float(), rt2.cpu().numpy(), **tol)
     close(g.float(), rg.cpu().numpy(), atol=tol["atol"] * 8, rtol=tol["rtol"])
     close(mean, rmean.cpu().numpy(), atol=1e-4, rtol=1e-4)
@@ -475,7 +475,7 @@ def test_sca_fwd_bwd_against_float64(dev, B, H, W, C):
     close(dW, (rda.t() @ mean.double()).cpu().numpy(), atol=1e-4 * ch ** 0.5, rtol=1e-4)
     close(db, rda.sum(0).cpu().numpy(), atol=1e-4 * ch ** 0.5, rtol=1e-4)
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 def test_graph_step_bitwise_equals_eager(dev, precision):
     """The captured HIP-graph step replays exactly the eager step's kernels: parameters, optimizer state and losses
     agree bit for bit over several steps of a cosine schedule, including an input swap between replays."""
@@ -582,7 +582,7 @@ def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
     dlnw, dlnb = torch.empty(N, device=dev), torch.empty(N, device=dev)
     n_ws = query("dgrad_ln_workspace_floats", M, N)
     ws = torch.empty(n_ws, device=dev)
-    call("dgrad_ln_bwd", A, K, Wt, K, M, N, K, x, stats, lnw, dres, dx, dlnw, dlnb, ws, n_ws)
+    call("dgrad_ln_bwd", A, K, Wt, K, M, N, K, x, stats, lnw, dres, dx, dlnw, dlnb, ws, n_ws, 1)
     dn = A.double() @ Wt.double().t()
     yh = (xd - stats[:, :1].double()) / stats[:, 1:].double()
     g = dn * lnw.double()
@@ -612,7 +612,7 @@ def test_gemm_res_ln_equals_gemm_then_ln_fwd(dev, M, N, K, amode):
     call("gemm_bf16", A, K, amode, scale, rows, 1, W, K, y0, N, 0, 1, M, N, K, 0, 0, 0, bias, R, rs, None)
     call("ln_fwd_nhwc", y0, lnw, lnb, n0, s0, M, N, 1e-6, 1)
     y1, n1, s1 = torch.empty_like(y0), torch.empty_like(n0), torch.empty_like(s0)
-    call("gemm_res_ln", A, K, amode, scale, rows, W, K, y1, M, N, K, bias, R, rs, lnw, lnb, n1, s1, 1e-6)
+    call("gemm_res_ln", A, K, amode, scale, rows, W, K, y1, M, N, K, bias, R, rs, lnw, lnb, n1, s1, 1e-6, 1)
     assert torch.equal(y1, y0) and torch.equal(n1, n0) and torch.equal(s1, s0)
 
 
@@ -699,7 +699,7 @@ def test_dgrad_sg_recompute_matches_stored(dev, M):
     W5t = (torch.randn(c, c, device=dev, generator=gen) / c ** 0.5).to(torch.bfloat16)
     d0, d1 = (torch.full((M, 2 * c), float("nan"), device=dev, dtype=torch.bfloat16) for _ in range(2))
     call("gemm_bf16", dout, c, 0, None, 1, 1, W5t, c, d0, 2 * c, 5, 1, M, c, c, 0, 0, 0, None, t4, None, None)
-    call("dgrad_sg_rc", dout, c, W5t, c, n2, W4, b4, d1, M, c, c)
+    call("dgrad_sg_rc", dout, c, W5t, c, n2, W4, b4, d1, M, c, c, 1)
     assert torch.equal(d0, d1)
     # and against float64: dt4[2j] = dg[j] t[2j+1], dt4[2j+1] = dg[j] t[2j]
     dg = dout.double() @ W5t.double().t()

@@ -24,10 +24,10 @@ def test_conv3x3_bf16_modes(dev, B, H, W, Cin, Cout):
     wf = w.permute(0, 2, 3, 1).reshape(Cout, 9, Cin).contiguous()
     ref = Fn.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1).permute(0, 2, 3, 1)
     y32 = torch.empty(B, H, W, Cout, device=dev)
-    call("conv3x3_bf16", x, B, H, W, Cin, wf, Cout, b, 1, None, y32, 0)
+    call("conv3x3_bf16", x, B, H, W, Cin, wf, Cout, b, 1, None, y32, 0, 1)
     assert (y32.double() - ref).abs().max().item() < 1e-4 * (9 * Cin) ** 0.5
     y = torch.empty(B, H, W, Cout, device=dev, dtype=torch.bfloat16)
-    call("conv3x3_bf16", x, B, H, W, Cin, wf, Cout, b, 0, None, y, 1)
+    call("conv3x3_bf16", x, B, H, W, Cin, wf, Cout, b, 0, None, y, 1, 1)
     torch.testing.assert_close(y.float(), ref.clamp_min(0).float().to(torch.bfloat16).float(), atol=2e-2, rtol=1e-2)
     # input gradient: same kernel on dy with W'[c][8 - t][n] = W[n][t][c]; mode 2 masks by R > 0
     dy = torch.randn(B, H, W, Cout, device=dev, generator=g).to(torch.bfloat16)
@@ -36,11 +36,11 @@ def test_conv3x3_bf16_modes(dev, B, H, W, Cin, Cout):
     Fn.conv2d(xr, w.double(), None, padding=1).backward(dy.double().permute(0, 3, 1, 2))
     dref = xr.grad.permute(0, 2, 3, 1)
     dx = torch.empty(B, H, W, Cin, device=dev)
-    call("conv3x3_bf16", dy, B, H, W, Cout, wt, Cin, None, 1, None, dx, 0)
+    call("conv3x3_bf16", dy, B, H, W, Cout, wt, Cin, None, 1, None, dx, 0, 1)
     assert (dx.double() - dref).abs().max().item() < 1e-4 * (9 * Cout) ** 0.5
     R = torch.randn(B, H, W, Cin, device=dev, generator=g).to(torch.bfloat16)
     dm = torch.empty(B, H, W, Cin, device=dev, dtype=torch.bfloat16)
-    call("conv3x3_bf16", dy, B, H, W, Cout, wt, Cin, None, 2, R, dm, 1)
+    call("conv3x3_bf16", dy, B, H, W, Cout, wt, Cin, None, 2, R, dm, 1, 1)
     torch.testing.assert_close(dm.float(), (dref * (R.double() > 0)).float(), atol=3e-2, rtol=1e-2)
 
 
@@ -51,14 +51,14 @@ def test_maxpool_fwd_bwd(dev):
     x = torch.randn(B, H, W, C, device=dev, generator=g).relu().to(torch.bfloat16)  # post-ReLU maps (ties at 0)
     y = torch.empty(B, H // 2, W // 2, C, device=dev, dtype=torch.bfloat16)
     idx = torch.empty(B, H // 2, W // 2, C, device=dev, dtype=torch.uint8)
-    call("maxpool2_fwd", x, B, H, W, C, y, idx)
+    call("maxpool2_fwd", x, B, H, W, C, y, idx, 1)
     xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
     yr = Fn.max_pool2d(xr, 2)
     assert torch.equal(y.double(), yr.permute(0, 2, 3, 1).detach())
     dy = torch.randn(B, H // 2, W // 2, C, device=dev, generator=g).to(torch.bfloat16)
     yr.backward(dy.double().permute(0, 3, 1, 2))
     dx = torch.empty_like(x)
-    call("maxpool2_bwd", dy, idx, x, B, H, W, C, dx)
+    call("maxpool2_bwd", dy, idx, x, B, H, W, C, dx, 1)
     ref = xr.grad.permute(0, 2, 3, 1) * (x.double() > 0)  # the pool input's ReLU mask rides along
     assert torch.equal(dx.double(), ref)
 
@@ -119,7 +119,7 @@ def test_vgg_shallow_input_gradient(dev, n_modules, tol):
     fg, tape, _ = st.forward(prep_input(gen.to(dev)), save=True)
     ft, _, _ = st.forward(prep_input(tgt.to(dev)), save=False)
     d = torch.empty_like(fg)
-    call("feat_dist_bwd", fg, ft, fg.numel(), 0, 1.0 / fg.numel(), 1, torch.ones(1, device=dev), d)
+    call("feat_dist_bwd", fg, ft, fg.numel(), 0, 1.0 / fg.numel(), 1, torch.ones(1, device=dev), d, st.dtype)
     dx = input_grad(st.backward(tape, d), gen.to(dev))
     mean = torch.tensor([0.485, 0.456, 0.406], dtype=torch.float64).view(1, 3, 1, 1)
     std = torch.tensor([0.229, 0.224, 0.225], dtype=torch.float64).view(1, 3, 1, 1)
