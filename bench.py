@@ -3,22 +3,34 @@
 Workload (BASELINE.json configs[1], the 1-GPU headline config): NAFNet width 32, enc [2,2,4,8], middle 12,
 dec [2,2,2,2] (29.16 M params), rgb/B2 crosstalk PSF, 16 x 3 x 256 x 256 synthetic sRGB per GPU,
 HybridLoss terms L1 + SSIM + Phys_srgb, global-norm clip 0.01 + AdamW.  One "step" = forward + loss + backward
-(+ bucketed RCCL all-reduce when N > 1) + clip + AdamW, all HIP kernels.
+(+ bucketed RCCL all-reduce when N > 1) + clip + AdamW, all HIP kernels.  Default precision fp16 (fp16 storage and
+MFMA operands, fp32 accumulation / statistics / parameters, dynamic loss scaling): the reference's AMP dtype.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp16|bf16|fp32] [--quick]
     (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...)
 
-Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel class measured live with HIP events on the launch
-stream during the timed steps; `nafblock_roofline` is the north-star figure (NAFBlock fwd+bwd algorithmic bytes,
-SURVEY §8d: 5*B*C*H*W*4 bytes per block per step, vs 8 TB/s); `cpu_baseline` is the CPU oracle (oracle/, kind
-"port") on a bounded sample, timed on this box's host cores; `psnr_vs_cpu_ref_db` compares the GPU output with
-the CPU oracle's on the same weights and input.
+Rank 0 prints ONE JSON line.
+* `roofline`: the dominant kernel class (by measured time among the classes below), timed live with HIP events on
+  the launch stream over K eager steps; achieved = its algorithmic bytes (or FLOPs) per launch / its average launch
+  duration.  Classes: `gemm16` (every 16-bit MFMA GEMM entry: nbp_gemm_bf16 + the fused-epilogue entries
+  nbp_gemm_res_ln / nbp_dgrad_ln_bwd / nbp_dgrad_sg_rc), `wgrad`, `dw_bwd` (nbp_sca_sg_dw_bwd), `dw_fwd`
+  (nbp_dw_sg_pool_fwd); rocprof kernel names in ROCPROF_KERNELS.
+* `nafblock_roofline`: the north-star figure, NAFBlock fwd+bwd algorithmic bytes (5*B*C*H*W*s per block,
+  s = the storage bytes per element of this precision) vs 8 TB/s.
+* `modes` / `cfg3` (rank 0, N = 1, unless --quick): the other precision modes on the same workload, and a bounded
+  BASELINE configs[2] sample (bs 8 x 512^2, all six HybridLossPlus terms, synthetic VGG / LPIPS weights).
+* `cpu_baseline`: the CPU oracle (oracle/, kind "port") at the full cfg2 batch on this box's host cores (median of 3
+  timed steps after 1 warm-up), as BASELINE.md prescribes.
+* `psnr_vs_cpu_ref_db`: GPU vs CPU-oracle output on the same weights and input, at the reference's init (zero layer
+  scales: every block an identity) and with active blocks (beta, gamma ~ N(0, 0.2), `psnr_active_blocks_db`).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -30,6 +42,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "training images/sec at 256×256 bs=16 (1/2/4/8 GPU) + PSNR vs CPU ref"
 CFG = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+BLK = {k: v for k, v in CFG.items() if k != "width"}
 # BASELINE.json configs[1] (the headline) and configs[2] (VGG19 perceptual + LPIPS + ΔE00, bs8 512²; weights from
 # configs/colab/sid_newbp_rgb.yml:78-96; LPIPS is the HybridLossPlus term's net='vgg', synthetic offline weights)
 WORKLOADS = {
@@ -40,14 +53,16 @@ WORKLOADS = {
                  desc="cfg3: cfg2 model, rgb/B2 PSF, bs8/GPU 512x512, L1 + 0.05*SSIM + 0.1*Phys_srgb + 0.02*VGG19 perc "
                       "+ 0.05*LPIPS(vgg) + 0.02*DeltaE00, clip 0.01 + AdamW (synthetic VGG/LPIPS weights)"),
 }
-BATCH, IMG = 16, 256
-W_L1, W_SSIM, W_PHYS = 1.0, 0.05, 0.1
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
-BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak
+MFMA16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA peak
 HBM_PEAK_GBPS = 8000.0
+ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
+ROCPROF_KERNELS = {"gemm16": ["gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
+                   "wgrad": ["wgrad_bf16_kernel", "wgrad_bf16_wide", "wgrad_f32_kernel"],
+                   "dw_bwd": ["dw_bwd_tiled"], "dw_fwd": ["dw_sg_pool_tiled"]}
 
 
-def nafblock_bytes(net, B, H, W):
+def nafblock_bytes(net, B, H, W, esize):
     tot = 0
     h, w = H, W
     for i, n in enumerate(net.enc_blk_nums):
@@ -57,7 +72,66 @@ def nafblock_bytes(net, B, H, W):
     for i, n in enumerate(net.dec_blk_nums):
         h, w = h * 2, w * 2
         tot += n * B * net.dec_chans[i] * h * w
-    return 5 * tot * 4
+    return 5 * tot * esize
+
+
+# ------------------------------------------------------------------ algorithmic work per launch, by C-ABI entry
+def _e(dt):
+    return 4 if dt == 0 else 2
+
+
+def cost_gemm16(a):  # (A,lda,amode,ascale,rows,adt,Bw,ldb,C,ldc,cmode,cdt,M,N,K,gh,gw,cs,bias,R,rscale,pre)
+    M, N, K, cm = a[12], a[13], a[14], a[10]
+    ea, ec = _e(a[5]), _e(a[11])
+    by = M * K * ea + N * K * 2
+    if cm == 5:  # SimpleGate backward: dt [M][2N] out, t [M][2N] in
+        by += 4 * M * N * ec
+    elif cm == 4:  # SimpleGate forward: t [M][N] (unless dropped) + g [M][N/2]
+        by += (M * N * ec if a[8] is not None else 0) + M * N // 2 * ec
+    else:
+        by += M * N * ec + (M * N * ec if a[19] is not None else 0) + (M * N * ec if a[21] is not None and cm != 8 else 0)
+    return 2.0 * M * N * K, by
+
+
+def cost_res_ln(a):  # (A,lda,amode,ascale,rows,Bw,ldb,C,M,N,K,bias,R,rscale,lnw,lnb,nout,stats,eps,dt)
+    M, N, K = a[8], a[9], a[10]
+    return 2.0 * M * N * K, (M * K + N * K + 3 * M * N) * 2 + 8 * M
+
+
+def cost_dgrad_ln(a):  # (A,lda,Wt,ldb,M,N,K,x,stats,lnw,dres,dx,dlnw,dlnb,ws,n_ws,dt)
+    M, N, K = a[4], a[5], a[6]
+    return 2.0 * M * N * K, (M * K + N * K + 3 * M * N) * 2 + 8 * M
+
+
+def cost_sg_rc(a):  # (A,lda,Wt,ldb,A2,W2,b2,C,M,N,K,dt): dgrad + the rebuilt conv4 forward
+    M, N, K = a[8], a[9], a[10]
+    return 2.0 * M * N * K + 4.0 * M * N * K, (2 * M * K + 3 * N * K + 2 * M * N) * 2
+
+
+def cost_wgrad(a):  # (G,ldg,gm,X,ldx,xm,xs,rows,M,N,K,gh,gw,csg,csx,dW,db,ws,n_ws,dtype)
+    M, N, K = a[8], a[9], a[10]
+    return 2.0 * M * N * K, M * (N + K) * _e(a[-1]) + N * K * 4
+
+
+def cost_dw_bwd(a):  # (dh,a,ds,t2,t1,wdw,dt1,dwdw,dbdw,ws,B,h,w,c,dt): dh C + t2 2C + t1 2C in, dt1 2C out
+    M, c = a[10] * a[11] * a[12], a[13]
+    return 2.0 * M * 2 * c * 18, 7 * M * c * _e(a[14])
+
+
+def cost_dw_fwd(a):  # (t1,w,b,t2,g,pool,B,h,w,c,dt): t1 2C in, t2 2C + g C out
+    M, c = a[6] * a[7] * a[8], a[9]
+    return 2.0 * M * 2 * c * 9, (2 + (2 if a[3] is not None else 0) + 1) * M * c * _e(a[10])
+
+
+def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
+    M, N, K = a[11], a[12], a[13]
+    return 2.0 * M * N * K, 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0))
+
+
+ENTRIES = {"gemm_bf16": ("gemm16", cost_gemm16), "gemm_res_ln": ("gemm16", cost_res_ln),
+           "dgrad_ln_bwd": ("gemm16", cost_dgrad_ln), "dgrad_sg_rc": ("gemm16", cost_sg_rc),
+           "gemm_f32": ("gemm_f32", cost_gemm_f32), "wgrad_f32": ("wgrad", cost_wgrad),
+           "sca_sg_dw_bwd": ("dw_bwd", cost_dw_bwd), "dw_sg_pool_fwd": ("dw_fwd", cost_dw_fwd)}
 
 
 def _pmc_traffic(cls):
@@ -65,50 +139,114 @@ def _pmc_traffic(cls):
     scripts/pmc_pass.sh + scripts/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled)."""
     import glob
     import re
-    # newest record by version number (natural order: r01_v10 after r01_v9)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")),
                    key=lambda f: [int(t) for t in re.findall(r"\d+", os.path.basename(f))])
     if not files:
         return None, None
     rec = json.load(open(files[-1])).get("classes", {}).get(cls)
     if rec is None:
-        return None, None
+        return None, os.path.relpath(files[-1], ROOT)
     return round(rec["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(state_dict, B=2, steps=2):
-    """Time the oracle's training step (oracle/train_step.py, torch CPU fp32) on a bounded sample."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(state_dict, B=16, img=256, timed=3):
+    """The oracle's training step (oracle/train_step.py, torch CPU fp32; pinned against the reference by the golden
+    fixtures) at the full cfg2 batch: set_num_threads(the CPUs this process may run on), 1 warm-up + `timed` steps,
+    img/s = B / median step (BASELINE.md 'CPU-baseline plan')."""
     from oracle.train_step import OracleTrainer
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
-    torch.set_num_threads(threads)
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    torch.set_num_threads(cores)
     P = {k: v.detach().cpu() for k, v in state_dict.items()}
-    ora = OracleTrainer(P, dict(enc_blk_nums=CFG["enc_blk_nums"], middle_blk_num=CFG["middle_blk_num"],
-                                dec_blk_nums=CFG["dec_blk_nums"]), w_l1=W_L1, w_ssim=W_SSIM, w_phys=W_PHYS)
+    ora = OracleTrainer(P, BLK, **WORKLOADS["cfg2"]["w"])
     g = torch.Generator().manual_seed(123)
-    lq = torch.rand(B, 3, IMG, IMG, generator=g)
-    gt = torch.rand(B, 3, IMG, IMG, generator=g)
+    lq = torch.rand(B, 3, img, img, generator=g)
+    gt = torch.rand(B, 3, img, img, generator=g)
     r = torch.ones(B, 1, 1, 1)
     ora.step(lq, gt, lq.clamp(0, 1), r)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    ts = []
+    for _ in range(timed):
+        t0 = time.perf_counter()
         ora.step(lq, gt, lq.clamp(0, 1), r)
-    dt = (time.perf_counter() - t0) / steps
-    return {"value": round(B / dt, 4), "unit": "img/s", "cores": threads, "kind": "port",
-            "sample": f"oracle train step (torch CPU fp32), cfg2 model, bs={B} {IMG}x{IMG}, {steps} timed steps "
-                      f"after 1 warm-up, {dt:.2f} s/step"}
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return {"value": round(B / med, 4), "unit": "img/s", "cores": cores, "kind": "port",
+            "sample": f"oracle train step (torch {torch.__version__} CPU fp32: fwd + L1/SSIM/Phys_srgb + bwd + clip + "
+                      f"AdamW), cfg2 model at the full bs={B} {img}x{img}, median of {timed} timed steps after 1 "
+                      f"warm-up ({', '.join(f'{t:.2f}' for t in ts)} s), torch.set_num_threads({cores}) = "
+                      f"len(sched_getaffinity); os.cpu_count() {os.cpu_count()}; CPU {_cpu_model()}"}
 
 
-def psnr_vs_cpu(net, dev):
+def psnr_vs_cpu(net, dev, img, active=False):
+    """GPU output vs the CPU oracle's on the same weights and input (1 image).  active: random layer scales."""
     from oracle.nafnet import nafnet as oracle_nafnet
+    backup = None
+    if active:
+        backup = net.flat.data.clone()
+        g = torch.Generator().manual_seed(7)
+        with torch.no_grad():
+            for k, e in net.entries.items():
+                if k.endswith("beta") or k.endswith("gamma"):
+                    net.flat.data[e.offset:e.offset + e.numel] = (0.2 * torch.randn(e.numel, generator=g)).to(dev)
     g = torch.Generator().manual_seed(321)
-    x = torch.rand(1, 3, IMG, IMG, generator=g)
+    x = torch.rand(1, 3, img, img, generator=g)
     with torch.no_grad():
         y = net(x.to(dev)).cpu()
         P = {k: v.cpu() for k, v in net.state_dict().items()}
-        yr = oracle_nafnet(P, x, CFG["enc_blk_nums"], CFG["middle_blk_num"], CFG["dec_blk_nums"])
+        yr = oracle_nafnet(P, x, **BLK)
+    if backup is not None:
+        net.flat.data.copy_(backup)
     mse = ((y.double() - yr.double()) ** 2).mean().item()
     psnr = float("inf") if mse <= 1e-30 else 10 * torch.log10(torch.tensor(1.0 / mse)).item()
-    return psnr, (y - yr).abs().max().item()
+    return (round(psnr, 2) if psnr != float("inf") else "inf"), (y - yr).abs().max().item()
+
+
+def make_trainer(dev, workload, precision, seed=0):
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    torch.manual_seed(seed)
+    net = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **CFG)
+    init_sd = {k: v.clone() for k, v in net.state_dict().items()}
+    net = net.to(dev)
+    net.precision = precision
+    return NBPTrainer(net, psf_mode="rgb", psf_spec="B2", **WORKLOADS[workload]["w"]), init_sd
+
+
+def batch(dev, B, img, rank):
+    g = torch.Generator(device=dev).manual_seed(0 + rank)
+    lq = torch.rand(B, 3, img, img, device=dev, generator=g)
+    gt = torch.rand(B, 3, img, img, device=dev, generator=g)
+    ratio = torch.ones(B, 1, 1, 1, device=dev)
+    return lq, gt, (lq * ratio).clamp(0, 1), ratio
+
+
+def short_run(dev, workload, precision, steps=5, warmup=3):
+    """img/s of a graph-replayed run (extra keys; the headline is the main run)."""
+    wl = WORKLOADS[workload]
+    tr, _ = make_trainer(dev, workload, precision)
+    b = batch(dev, wl["batch"], wl["img"], 0)
+    for _ in range(warmup):
+        tr.graph_step(*b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.graph_step(*b)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    out = {"value": round(wl["batch"] / dt, 2), "unit": "img/s", "ms_per_step": round(dt * 1e3, 3),
+           "precision": precision, "steps": steps, "warmup": warmup, "losses": tr.logs()}
+    del tr
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -117,14 +255,14 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="headline only: no extra modes / cfg3 / CPU baseline")
     ap.add_argument("--eager", action="store_true", help="time eager launches instead of HIP-graph replays")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
-                    help="bf16: bf16 MFMA operands + fp32 accumulation (the reference's AMP training); "
-                         "fp32: fp32 everywhere (parity mode)")
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "bf16", "fp32"],
+                    help="fp16 (default; the reference's AMP dtype) / bf16: 16-bit storage + MFMA operands, fp32 "
+                         "accumulation; fp32: fp32 everywhere (parity mode)")
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=0, help="per-GPU batch override (diagnostics; 0 = the workload's)")
     args = ap.parse_args()
-    global BATCH, IMG
     wl = WORKLOADS[args.workload]
     BATCH, IMG = (args.batch or wl["batch"]), wl["img"]
 
@@ -137,59 +275,26 @@ def main():
     dev = torch.device("cuda", local)
 
     from lowlight_image_enhancement_amd import _lib
-    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
-    from lowlight_image_enhancement_amd.train import NBPTrainer
 
-    torch.manual_seed(0)
-    net = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **CFG)
-    init_sd = {k: v.clone() for k, v in net.state_dict().items()}
-    net = net.to(dev)
-    net.precision = args.precision
-    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", **wl["w"])
-    g = torch.Generator(device=dev).manual_seed(0 + rank)
-    lq = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
-    gt = torch.rand(BATCH, 3, IMG, IMG, device=dev, generator=g)
-    ratio = torch.ones(BATCH, 1, 1, 1, device=dev)
-    short = (lq * ratio).clamp(0, 1)
+    tr, init_sd = make_trainer(dev, args.workload, args.precision)
+    net = tr.net
+    lq, gt, short, ratio = batch(dev, BATCH, IMG, rank)
 
     for _ in range(args.warmup):
         tr.step(lq, gt, short, ratio)
-    logs_warm = tr.logs()
+    tr.logs()
 
-    # live per-kernel timing (HIP events on the launch stream) for the timed steps; each record carries the
-    # launch's algorithmic flops and HBM bytes (operands read once, outputs written once)
-    def mk(name, fl):
+    # live per-launch timing (HIP events on the launch stream) over K eager steps; each record carries the launch's
+    # algorithmic FLOPs and HBM bytes (operands read once, outputs written once)
+    prof = {}
+
+    def mk(cls, cost):
         def cb(a, e0, e1):
-            prof[name].append((*fl(a), e0, e1))
+            prof.setdefault(cls, []).append((*cost(a), e0, e1))
         return cb
 
-    def gemm_bf16_cost(a):  # (A,lda,amode,ascale,rows,adt,Bw,ldb,C,ldc,cmode,cdt,M,N,K,gh,gw,cs,bias,R,rscale,pre)
-        M, N, K = a[12], a[13], a[14]
-        ab, cb = (2 if a[5] else 4), (2 if a[11] else 4)
-        by = M * K * ab + N * K * 2 + M * N * cb + (M * N * cb if a[19] is not None else 0) + \
-            (M * N * 4 if a[21] is not None else 0)
-        return 2.0 * M * N * K, by
-
-    def gemm_f32_cost(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
-        M, N, K = a[11], a[12], a[13]
-        by = 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0) + (M * N if a[20] is not None else 0))
-        return 2.0 * M * N * K, by
-
-    def wgrad_cost(a):  # (G,ldg,gm,X,ldx,xm,xs,rows,M,N,K,...,dtype)
-        M, N, K = a[8], a[9], a[10]
-        eb = 2 if a[-1] == 1 else 4
-        return 2.0 * M * N * K, M * (N + K) * eb + N * K * 4
-
-    def conv3x3_cost(a):  # (x,B,H,W,Cin,w,Cout,bias,mode,R,y,y_dtype): VGG implicit-GEMM conv, K = 9*Cin
-        M, N, K = a[1] * a[2] * a[3], a[6], 9 * a[4]
-        by = M * a[4] * 2 + N * K * 2 + M * N * (2 if a[11] else 4) + (M * N * 2 if a[9] is not None else 0)
-        return 2.0 * M * N * K, by
-
-    gemm_name = "gemm_f32" if args.precision == "fp32" else "gemm_bf16"
-    prof = {gemm_name: [], "wgrad_f32": [], "conv3x3_bf16": []}
-    _lib.PROFILE["conv3x3_bf16"] = mk("conv3x3_bf16", conv3x3_cost)
-    _lib.PROFILE[gemm_name] = mk(gemm_name, gemm_f32_cost if args.precision == "fp32" else gemm_bf16_cost)
-    _lib.PROFILE["wgrad_f32"] = mk("wgrad_f32", wgrad_cost)
+    for name, (cls, cost) in ENTRIES.items():
+        _lib.PROFILE[name] = mk(cls, cost)
     blk_events = []
     orig_fwd, orig_bwd = net._block_fwd, net._block_bwd
 
@@ -206,8 +311,6 @@ def main():
         return w
 
     net._block_fwd, net._block_bwd = timed(orig_fwd, "fwd"), timed(orig_bwd, "bwd")
-
-    # profiled pass: K eager steps with per-kernel HIP events on the launch stream (graph replays cannot carry them)
     step_events = []
     for _ in range(args.steps):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -244,17 +347,15 @@ def main():
     logs = tr.logs()
 
     classes = {}
-    for name, recs in prof.items():
-        if not recs:
-            continue
+    for cls, recs in prof.items():
         ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in recs)
-        classes[name] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), len(recs))
+        classes[cls] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), len(recs))
     dom = max(classes, key=lambda k: classes[k][0])
     ms, fl, by, nl = classes[dom]
-    peak_tf = FP32_PEAK_TFLOPS if args.precision == "fp32" else BF16_PEAK_TFLOPS
+    peak_tf = FP32_PEAK_TFLOPS if args.precision == "fp32" else MFMA16_PEAK_TFLOPS
     tflops = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     gbps = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-    # the binding roof is the one the kernel class is closer to (arithmetic intensity vs the ridge point)
+    # the binding roof is the one the class is closer to (arithmetic intensity vs the ridge point)
     if fl / max(by, 1) < peak_tf * 1e12 / (HBM_PEAK_GBPS * 1e9):
         roof = {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(gbps / HBM_PEAK_GBPS, 4)}
@@ -262,10 +363,14 @@ def main():
         roof = {"bound": "mfma", "achieved": round(tflops, 3), "peak": peak_tf, "unit": "TFLOP/s",
                 "frac": round(tflops / peak_tf, 4)}
     traffic, tsrc = _pmc_traffic(dom)
-    roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel": dom, "launches_per_step": nl // args.steps,
-                 "ms_per_step": round(ms / args.steps, 3), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
-                 "flop_intensity": round(fl / max(by, 1), 2), "tflops": round(tflops, 2),
-                 "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in classes.items()}})
+    roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel": dom, "rocprof_kernels": ROCPROF_KERNELS[dom],
+                 "launches_per_step": nl // args.steps, "ms_per_step": round(ms / args.steps, 3),
+                 "avg_launch_us": round(ms * 1e3 / nl, 2), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
+                 "algorithmic_flops_per_launch": round(fl / max(nl, 1)), "flop_intensity": round(fl / max(by, 1), 2),
+                 "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_tf, 4),
+                 "classes": {k: {"ms_per_step": round(v[0] / args.steps, 3), "launches_per_step": v[3] // args.steps,
+                                 "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1),
+                                 "TFLOPs": round(v[1] / (v[0] * 1e-3) / 1e12, 2)} for k, v in classes.items()}})
     blk_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in blk_events) / args.steps
     eager_step_ms = sum(e0.elapsed_time(e1) for e0, e1 in step_events) / args.steps
     per_level = {}
@@ -277,17 +382,17 @@ def main():
     for d in per_level.values():
         d["blocks_fwd"] //= args.steps
         d["fwd_ms"], d["bwd_ms"] = round(d["fwd_ms"], 3), round(d["bwd_ms"], 3)
-    blk_bytes = nafblock_bytes(net, BATCH, IMG, IMG)
+    esize = ESIZE[args.precision]
+    blk_bytes = nafblock_bytes(net, BATCH, IMG, IMG, esize)
     # The eager per-block events include host-dispatch stalls at the small levels (the GPU outruns the launches
     # there); the NAFBlock GPU time is the timed step minus the non-NAFBlock part of the eager step (boundary convs,
     # down/up, loss head, optimizer: few large kernels, not dispatch-bound).
-    step_ms_timed = elapsed / args.steps * 1e3
+    step_ms = elapsed / args.steps * 1e3
     nonblock_ms = max(eager_step_ms - blk_ms, 0.0)
-    blk_ms_gpu = max(step_ms_timed - nonblock_ms, 1e-6)
+    blk_ms_gpu = max(step_ms - nonblock_ms, 1e-6)
     blk_gbps = blk_bytes / (blk_ms_gpu * 1e-3) / 1e9
 
     if rank == 0:
-        step_ms = elapsed / args.steps * 1e3
         res = {
             "metric": METRIC if args.workload == "cfg2" else f"training images/sec ({args.workload})",
             "value": round(BATCH * world * args.steps / elapsed, 3),
@@ -301,11 +406,12 @@ def main():
             "vs_baseline": None,
             "dtype": {"bf16": "bf16", "fp16": "f16", "fp32": "f32"}[args.precision],
             "data": "synthetic (U[0,1) sRGB, expo_ratio 1, torch default init, seed 0+rank)",
-            "config": {"workload": wl["desc"],
-                       "global_batch": BATCH * world, "image": IMG, "parallelism": f"dp{world}",
+            "config": {"workload": wl["desc"], "global_batch": BATCH * world, "image": IMG,
+                       "parallelism": f"dp{world}", "precision": args.precision,
                        "launch": "hip-graph replay" if use_graph else "eager"},
             "roofline": roof,
-            "nafblock_roofline": {"bytes_per_step": blk_bytes, "ms_per_step": round(blk_ms_gpu, 3),
+            "nafblock_roofline": {"bytes_per_step": blk_bytes, "bytes_per_element": esize,
+                                  "ms_per_step": round(blk_ms_gpu, 3),
                                   "ms_method": "timed step - non-NAFBlock part of the eager step",
                                   "eager_blocks_ms_per_step": round(blk_ms, 3),
                                   "per_level_eager": per_level,
@@ -314,11 +420,16 @@ def main():
             "losses": logs,
         }
         if world == 1:
-            psnr, maxabs = psnr_vs_cpu(net, dev)
-            res["psnr_vs_cpu_ref_db"] = round(psnr, 2) if psnr != float("inf") else "inf"
-            res["max_abs_vs_cpu_ref"] = maxabs
-            if not args.no_cpu_baseline and args.workload == "cfg2":
-                res["cpu_baseline"] = cpu_baseline(init_sd)
+            res["psnr_vs_cpu_ref_db"], res["max_abs_vs_cpu_ref"] = psnr_vs_cpu(net, dev, IMG)
+            res["psnr_active_blocks_db"], res["max_abs_active_blocks"] = psnr_vs_cpu(net, dev, IMG, active=True)
+            if not args.quick and args.workload == "cfg2":
+                del tr, net
+                torch.cuda.empty_cache()
+                res["modes"] = {p: short_run(dev, "cfg2", p) for p in ("fp32", "bf16", "fp16") if p != args.precision}
+                res["cfg3"] = dict(short_run(dev, "cfg3", args.precision, steps=3, warmup=2),
+                                   workload=WORKLOADS["cfg3"]["desc"], global_batch=WORKLOADS["cfg3"]["batch"])
+                if not args.no_cpu_baseline:
+                    res["cpu_baseline"] = cpu_baseline(init_sd)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

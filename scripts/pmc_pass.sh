@@ -1,12 +1,21 @@
 #!/bin/bash
-# Two separate PMC passes (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950), kernel trace + stats only,
-# eager launches so every dispatch is attributed.  Output under gpurun_out/pmc_{fetch,write}/.
+# PMC passes over the bench (eager launches so every dispatch is attributed), kernel trace + stats only, each counter
+# group in its own run (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
+#   fetch: FETCH_SIZE   write: WRITE_SIZE   mfma: SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE
+# Output under gpurun_out/pmc_<pass>/; scripts/pmc_traffic.py turns them into profiles/<name>_pmc_traffic.json.
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d gpurun_out/pmc_fetch -o run \
-    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager > gpurun_out/pmc_fetch.log 2>&1
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats -d gpurun_out/pmc_write -o run \
-    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --eager > gpurun_out/pmc_write.log 2>&1
-ls -R gpurun_out/pmc_fetch | head -20
+PREC=${PREC:-fp16}
+BENCH="python bench.py --steps 3 --warmup 1 --quick --eager --precision $PREC"
+pass() {
+  local name=$1
+  shift
+  timeout -s KILL 300 rocprofv3 --pmc "$@" --kernel-trace --stats -d gpurun_out/pmc_$name -o run --output-format csv \
+      -- $BENCH > gpurun_out/pmc_$name.log 2>&1
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE
+ls gpurun_out/pmc_fetch gpurun_out/pmc_mfma | head
