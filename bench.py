@@ -149,6 +149,12 @@ def _pmc_traffic(cls):
     return round(rec["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
+def nproc() -> int:
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -161,10 +167,11 @@ def _cpu_model():
 
 def cpu_baseline(state_dict, B=16, img=256, timed=3):
     """The oracle's training step (oracle/train_step.py, torch CPU fp32; pinned against the reference by the golden
-    fixtures) at the full cfg2 batch: set_num_threads(the CPUs this process may run on), 1 warm-up + `timed` steps,
-    img/s = B / median step (BASELINE.md 'CPU-baseline plan')."""
+    fixtures) at the full cfg2 batch: set_num_threads(nproc), 1 warm-up + `timed` steps, img/s = B / median step
+    (BASELINE.md 'CPU-baseline plan').  nproc = the CPUs this process may run on, capped by OMP_NUM_THREADS (what
+    coreutils nproc reports: the GPU box exports OMP_NUM_THREADS=16, its per-GPU CPU share)."""
     from oracle.train_step import OracleTrainer
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = nproc()
     torch.set_num_threads(cores)
     P = {k: v.detach().cpu() for k, v in state_dict.items()}
     ora = OracleTrainer(P, BLK, **WORKLOADS["cfg2"]["w"])
@@ -174,16 +181,17 @@ def cpu_baseline(state_dict, B=16, img=256, timed=3):
     r = torch.ones(B, 1, 1, 1)
     ora.step(lq, gt, lq.clamp(0, 1), r)  # warm-up
     ts = []
-    for _ in range(timed):
+    for i in range(timed):
         t0 = time.perf_counter()
         ora.step(lq, gt, lq.clamp(0, 1), r)
         ts.append(time.perf_counter() - t0)
+        print(f"[bench] cpu baseline step {i + 1}/{timed}: {ts[-1]:.2f} s", file=sys.stderr, flush=True)
     med = statistics.median(ts)
     return {"value": round(B / med, 4), "unit": "img/s", "cores": cores, "kind": "port",
             "sample": f"oracle train step (torch {torch.__version__} CPU fp32: fwd + L1/SSIM/Phys_srgb + bwd + clip + "
                       f"AdamW), cfg2 model at the full bs={B} {img}x{img}, median of {timed} timed steps after 1 "
-                      f"warm-up ({', '.join(f'{t:.2f}' for t in ts)} s), torch.set_num_threads({cores}) = "
-                      f"len(sched_getaffinity); os.cpu_count() {os.cpu_count()}; CPU {_cpu_model()}"}
+                      f"warm-up ({', '.join(f'{t:.2f}' for t in ts)} s), torch.set_num_threads({cores}) = nproc "
+                      f"(os.cpu_count() {os.cpu_count()}); CPU {_cpu_model()}"}
 
 
 def psnr_vs_cpu(net, dev, img, active=False):
@@ -425,10 +433,13 @@ def main():
             if not args.quick and args.workload == "cfg2":
                 del tr, net
                 torch.cuda.empty_cache()
+                print("[bench] extra modes", file=sys.stderr, flush=True)
                 res["modes"] = {p: short_run(dev, "cfg2", p) for p in ("fp32", "bf16", "fp16") if p != args.precision}
+                print("[bench] cfg3 sample", file=sys.stderr, flush=True)
                 res["cfg3"] = dict(short_run(dev, "cfg3", args.precision, steps=3, warmup=2),
                                    workload=WORKLOADS["cfg3"]["desc"], global_batch=WORKLOADS["cfg3"]["batch"])
                 if not args.no_cpu_baseline:
+                    print("[bench] cpu baseline", file=sys.stderr, flush=True)
                     res["cpu_baseline"] = cpu_baseline(init_sd)
         print(json.dumps(res), flush=True)
     if world > 1:

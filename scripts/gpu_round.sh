@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 echo "cpus: os.cpu_count=$(python -c 'import os;print(os.cpu_count())') affinity=$(python -c 'import os;print(len(os.sched_getaffinity(0)))') nproc=$(nproc)" | tee gpurun_out/host.txt
 grep -m1 "model name" /proc/cpuinfo | tee -a gpurun_out/host.txt
-[[ ${STEPS:-bench,prof,pmc} == *bench* ]] && timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 && tail -c 600 gpurun_out/bench.log
+[[ ${STEPS:-bench,prof,pmc} == *bench* ]] && timeout -k 10 600 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err && tail -c 600 gpurun_out/bench.log
 if [[ ${STEPS:-bench,prof,pmc} == *prof* ]]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
       python bench.py --steps 10 --warmup 3 --quick > gpurun_out/prof_bench.log 2>&1
