@@ -299,6 +299,14 @@ int nbp_sobel_mag(const float* lab, int B, int H, int W, float* out, nbp_stream_
    transposed weights).  Cin, Cout multiples of 8; y bf16 (y_dtype 1) or fp32 (y_dtype 0, mode 1). */
 int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
                      const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s);
+/* General zero-padded KH x KW / stride conv over NHWC 16-bit maps (LPIPS(net='alex') trunk, lpips 0.1.4 /
+   torchvision alexnet features: 11x11/4 pad 2, 5x5 pad 2, 3x3 pad 1) as an implicit GEMM on the 16-bit MFMA kernel:
+   y [B][Ho][Wo][Cout] = (relu?)(sum_{ki,kj,c} x[b][oi*stride + ki - pad][oj*stride + kj - pad][c] w[n][ki*KW+kj][c]
+   + bias[n]), Ho = (H + 2 pad - KH) / stride + 1.  Cin, Cout multiples of 8; dtype 1 bf16 / 2 fp16 (x, w, y). */
+int nbp_conv2d_16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, int KH, int KW, int stride,
+                  int pad, const float* bias, int relu, void* y, int dtype, nbp_stream_t s);
+/* k x k max pool with stride, no padding (floor), NHWC 16-bit, forward (torchvision MaxPool2d(kernel_size=3, stride=2)). */
+int nbp_maxpool_k_fwd(const void* x, int B, int H, int W, int C, int k, int stride, void* y, int dtype, nbp_stream_t s);
 /* PerceptualLoss input (losses.py:56-66): NCHW fp32 sRGB -> NHWC bf16 [B][H][W][8] = (clamp01(x) - m) / s, c >= 3
    zero.  The input gradient maps d[B][H][W][8] fp32 back to NCHW (/ s, clamp mask). */
 int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float m1, float m2, float s0, float s1,

@@ -21,7 +21,7 @@ namespace {
 // C modes: plain, depth-to-space scatter, bias + ReLU, ReLU-mask by R (C = acc where R > 0, else 0), SimpleGate
 // forward (C = t with channel pairs (c, C+c) interleaved, and pre <- g = t[2c] * t[2c+1]) and SimpleGate backward
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
-enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3 };
+enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3, AM_CONV = 4 };
 enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7,
        CM_CHANDOT = 8, CM_SGBWD_RC = 9 };
 
@@ -52,6 +52,9 @@ struct GemmPB {
   const void* dres;
   float* slab_w;
   float* slab_b;
+  // AM_CONV (general KH x KW / stride / zero-pad implicit GEMM): gh x gw = the output map, ih x iw = the input map,
+  // k = (ki * kw + kj) * cs + c
+  int kh, kw, stride, pad, ih, iw;
 };
 
 __device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
@@ -170,7 +173,15 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       vec_t<H, 8> v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (AMODE == AM_IM2COL) {
+      if (AMODE == AM_CONV) {
+        if (m < M && k < K) {
+          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, oi = rem / p.gw, oj = rem - oi * p.gw;
+          const int t = k / p.cs, c = k - t * p.cs, ki = t / p.kw, kj = t - ki * p.kw;
+          const int ii = oi * p.stride + ki - p.pad, jj = oj * p.stride + kj - p.pad;
+          if (ii >= 0 && ii < p.ih && jj >= 0 && jj < p.iw)
+            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.ih + ii) * p.iw + jj) * p.cs + c, nullptr);
+        }
+      } else if (AMODE == AM_IM2COL) {
         if (m < M && k < K) {
           const int per = p.gh * p.gw, b = m / per, rem = m - b * per, i = rem / p.gw, j = rem - i * p.gw;
           const int t = k / p.cs, c = k - t * p.cs;
@@ -1157,6 +1168,37 @@ int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w,
     else dispatch<AM_IM2COL, CM_PLAIN, T16, float, T16>(p, st);
   }
   return check_launch("conv3x3_bf16");
+}
+
+int nbp_conv2d_16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, int KH, int KW, int stride,
+                  int pad, const float* bias, int relu, void* y, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+              "nbp_conv2d_16: bad args");
+  NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv2d_16: Cin and Cout must be multiples of 8 (%d, %d)", Cin, Cout);
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_conv2d_16: dtype 1 (bf16) or 2 (fp16)");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  NBP_REQUIRE(Ho > 0 && Wo > 0, "nbp_conv2d_16: empty output");
+  const long M = (long)B * Ho * Wo;
+  NBP_REQUIRE(M < (1L << 31), "nbp_conv2d_16: too many pixels");
+  GemmPB p{x, 0, nullptr, 1, w, (long)KH * KW * Cin, y, Cout, (int)M, Cout, KH * KW * Cin, Ho, Wo, Cin, bias, nullptr,
+           nullptr, nullptr};
+  p.kh = KH;
+  p.kw = KW;
+  p.stride = stride;
+  p.pad = pad;
+  p.ih = H;
+  p.iw = W;
+  hipStream_t st = S(s);
+  if (dtype == 2) {
+    using T16 = _Float16;
+    if (relu) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
+    else dispatch<AM_CONV, CM_PLAIN, T16, T16, T16>(p, st);
+  } else {
+    using T16 = __bf16;
+    if (relu) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
+    else dispatch<AM_CONV, CM_PLAIN, T16, T16, T16>(p, st);
+  }
+  return check_launch("conv2d_16");
 }
 
 }  // extern "C"

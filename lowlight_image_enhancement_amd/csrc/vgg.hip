@@ -4,6 +4,8 @@
 // Kernels: the input prologue (NCHW fp32 -> NHWC bf16 with the channel dim padded to 8), 2x2 max-pool with argmax
 // (first maximum in window order, as torch's max_pool2d) and its backward fused with the ReLU mask of the pool input,
 // the feature distance with its gradient (fused with the last ReLU's mask), and the input-gradient epilogue.
+#include <math.h>
+
 #include "nbp_common.h"
 
 using namespace nbp;
@@ -261,6 +263,33 @@ __global__ __launch_bounds__(256) void lpips_tap_bwd(const HT* __restrict__ a, c
   }
 }
 
+// k x k max pool, stride s, no padding (floor), NHWC 16-bit, forward only (torchvision AlexNet's MaxPool2d(3, 2))
+template <typename HT>
+__global__ __launch_bounds__(256) void maxpool_k_fwd_kernel(const HT* __restrict__ x, int H, int W, int C, int k, int st,
+                                                            int Ho, int Wo, long total8, HT* __restrict__ y) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
+    const int C8 = C / 8;
+    const int c8 = (int)(e % C8);
+    const long o = e / C8;
+    const int j = (int)(o % Wo), i = (int)((o / Wo) % Ho);
+    const long b = o / ((long)Wo * Ho);
+    float best[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) best[q] = -INFINITY;
+    for (int di = 0; di < k; ++di)
+      for (int dj = 0; dj < k; ++dj) {
+        const vec_t<HT, 8> v =
+            *reinterpret_cast<const vec_t<HT, 8>*>(x + ((b * H + i * st + di) * W + j * st + dj) * C + c8 * 8);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) best[q] = fmaxf(best[q], (float)v[q]);
+      }
+    vec_t<HT, 8> out;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) out[q] = (HT)best[q];
+    *reinterpret_cast<vec_t<HT, 8>*>(y + o * C + c8 * 8) = out;
+  }
+}
+
 inline int grid_for(long n) {
   long g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -295,6 +324,15 @@ int nbp_maxpool2_bwd(const void* dy, const unsigned char* idx, const void* post_
       reinterpret_cast<const HT*>(dy), idx, reinterpret_cast<const HT*>(post_in), H, W, C, total8,
       reinterpret_cast<HT*>(dx)));
   return check_launch("maxpool2_bwd");
+}
+
+int nbp_maxpool_k_fwd(const void* x, int B, int H, int W, int C, int k, int stride, void* y, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && B > 0 && k > 0 && stride > 0 && H >= k && W >= k && C % 8 == 0, "nbp_maxpool_k_fwd: bad args");
+  const int Ho = (H - k) / stride + 1, Wo = (W - k) / stride + 1;
+  const long total8 = (long)B * Ho * Wo * (C / 8);
+  NBP_DISPATCH_16(dtype, HT, maxpool_k_fwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(x), H, W, C, k, stride, Ho, Wo, total8, reinterpret_cast<HT*>(y)));
+  return check_launch("maxpool_k_fwd");
 }
 
 size_t nbp_feat_dist_workspace_doubles(long n) {

@@ -1,5 +1,6 @@
-"""LPIPS (lpips==0.1.4, `lpips.LPIPS(net='vgg')`) on MI355X — the HybridLossPlus LPIPS term (NewBP_model/losses.py:
-265-274, 342-346).
+"""LPIPS (lpips==0.1.4, `lpips.LPIPS(net='vgg' | 'alex')`) on MI355X — the HybridLossPlus LPIPS term (net='vgg',
+NewBP_model/losses.py:265-274, 342-346) and the validation metric's default backbone (net='alex',
+metrics/lpips_metric.py:43-57, basicsr/metrics/lowlight_metrics.py:223-226).
 
 Restated from the package's published algorithm (the package and its weights are absent here: parity unpinned):
 ScalingLayer (x - shift) / scale with shift (-.030, -.088, -.188), scale (.458, .448, .450) (inputs taken as [-1, 1];
@@ -8,7 +9,11 @@ normalize_tensor over channels, squared difference, the non-negative 1x1 'lin' h
 Output [N, 1, 1, 1] per image like lpips.  The VGG16 trunk is the implicit-GEMM bf16 MFMA stack of vgg.py; the tap
 distances and their gradients are nbp_lpips_tap_* kernels; the tap gradients join the VGG backward walk.
 
-Weights: pretrained VGG16 + 'lin' weights cannot be downloaded here.  `weights` takes an lpips-style state_dict
+net='alex' (torchvision alexnet.features taps relu1..relu5: conv 11x11/4 pad 2 -> pool 3/2 -> conv 5x5 pad 2 -> pool 3/2 ->
+3 x conv 3x3 pad 1) runs its strided convs as implicit GEMMs on the 16-bit MFMA kernel (nbp_conv2d_16) with 3x3/2 max
+pools (nbp_maxpool_k_fwd); it is forward-only (the metric): its gradient raises NotImplementedError.
+
+Weights: pretrained VGG16 / AlexNet + 'lin' weights cannot be downloaded here.  `weights` takes an lpips-style state_dict
 (`net.sliceK.N.*`, `linK.model.1.weight`) or a path (torch.load(weights_only=True)); None gives a deterministic
 synthetic model (kaiming VGG16, lin = |N(0, 0.1)|, seed 0).
 """
@@ -29,6 +34,58 @@ SHIFT = (-0.030, -0.088, -0.188)
 SCALE = (0.458, 0.448, 0.450)
 TAPS = (3, 8, 15, 22, 29)        # relu1_2, relu2_2, relu3_3, relu4_3, relu5_3 in vgg16.features
 TAP_CH = (64, 128, 256, 512, 512)
+# torchvision alexnet.features: (module index, cin, cout, kernel, stride, pad) convs, max pools 3/2 at 2 and 5
+ALEX_CONVS = ((0, 3, 64, 11, 4, 2), (3, 64, 192, 5, 1, 2), (6, 192, 384, 3, 1, 1), (8, 384, 256, 3, 1, 1),
+              (10, 256, 256, 3, 1, 1))
+ALEX_TAP_CH = (64, 192, 384, 256, 256)  # relu1 .. relu5 (module indices 1, 4, 7, 9, 11)
+
+
+def alex_synthetic_state_dict(seed: int = 0) -> Dict[str, torch.Tensor]:
+    """torch's default Conv2d init (kaiming-uniform a = sqrt(5): U(+-1/sqrt(fan_in)) weights and biases) from a fixed
+    generator -- torchvision's AlexNet keeps the default init."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for idx, cin, cout, k, _, _ in ALEX_CONVS:
+        bound = 1.0 / (cin * k * k) ** 0.5
+        sd[f"{idx}.weight"] = (torch.rand(cout, cin, k, k, generator=g) * 2 - 1) * bound
+        sd[f"{idx}.bias"] = (torch.rand(cout, generator=g) * 2 - 1) * bound
+    return sd
+
+
+class AlexStack:
+    """Frozen alexnet.features[:12] on device, forward only: returns the five post-ReLU taps (NHWC 16-bit)."""
+
+    def __init__(self, device, feats: Dict[str, torch.Tensor], dtype: int = 1):
+        self.device, self.dtype = torch.device(device), dtype
+        self.tdt = torch.float16 if dtype == 2 else torch.bfloat16
+        self.convs = []
+        for idx, cin, cout, k, st, pad in ALEX_CONVS:
+            w = feats[f"{idx}.weight"].float()
+            if tuple(w.shape) != (cout, cin, k, k):
+                raise ValueError(f"alexnet layer {idx}: weight shape {tuple(w.shape)} != {(cout, cin, k, k)}")
+            cp = _vgg._pad8(cin)
+            wp = torch.zeros(cout, cp, k, k)
+            wp[:, :cin] = w
+            self.convs.append(dict(w=wp.permute(0, 2, 3, 1).reshape(cout, k * k, cp).to(self.device, self.tdt).contiguous(),
+                                   b=feats[f"{idx}.bias"].float().to(self.device).contiguous(), cin=cp, cout=cout, k=k,
+                                   st=st, pad=pad))
+
+    def taps(self, x8: torch.Tensor):
+        B, H, W, _ = x8.shape
+        feat, h, w, out = x8, H, W, []
+        for i, L in enumerate(self.convs):
+            if i in (1, 2):  # MaxPool2d(3, 2) before conv 2 and conv 3
+                ho, wo = (h - 3) // 2 + 1, (w - 3) // 2 + 1
+                y = torch.empty(B, ho, wo, feat.shape[-1], device=x8.device, dtype=self.tdt)
+                call("maxpool_k_fwd", feat, B, h, w, feat.shape[-1], 3, 2, y, self.dtype)
+                feat, h, w = y, ho, wo
+            ho, wo = (h + 2 * L["pad"] - L["k"]) // L["st"] + 1, (w + 2 * L["pad"] - L["k"]) // L["st"] + 1
+            y = torch.empty(B, ho, wo, L["cout"], device=x8.device, dtype=self.tdt)
+            call("conv2d_16", feat, B, h, w, L["cin"], L["w"], L["cout"], L["k"], L["k"], L["st"], L["pad"], L["b"], 1,
+                 y, self.dtype)
+            out.append(y)
+            feat, h, w = y, ho, wo
+        return out
 
 
 def _split_state_dict(sd: Dict[str, torch.Tensor]):
@@ -104,14 +161,29 @@ class LPIPS(nn.Module):
 
     def __init__(self, net: str = "vgg", weights=None, version: str = "0.1", precision: str = "bf16", **_):
         super().__init__()
-        if net != "vgg":
-            raise NotImplementedError("LPIPS on MI355X implements net='vgg' (the HybridLossPlus term)")
+        if net not in ("vgg", "alex"):
+            raise NotImplementedError("LPIPS on MI355X implements net='vgg' (the HybridLossPlus term) and net='alex' "
+                                      "(the metric's default)")
+        self.net = net
         self._weights = weights
         self._parts = {}
         self.precision = precision  # the VGG16 trunk's 16-bit type: "bf16" or "fp16" (see PerceptualLoss)
 
     def parts(self, device):
         key = (str(device), self.precision)
+        if key not in self._parts and self.net == "alex":
+            if self._weights is None:
+                warnings.warn("LPIPS: pretrained AlexNet / lin weights are not available offline; using a deterministic "
+                              "synthetic model", RuntimeWarning)
+                feats = alex_synthetic_state_dict(0)
+                g = torch.Generator().manual_seed(0)
+                lins = {k: (torch.randn(c, generator=g) * 0.1).abs() for k, c in enumerate(ALEX_TAP_CH)}
+            else:
+                sd = torch.load(self._weights, map_location="cpu", weights_only=True) if isinstance(
+                    self._weights, str) else dict(self._weights)
+                feats, lins = _split_state_dict(sd)
+            stack = AlexStack(device, feats, dtype={"bf16": 1, "fp16": 2}[self.precision])
+            self._parts[key] = (stack, [lins[k].to(device).float().contiguous() for k in range(5)])
         if key not in self._parts:
             if self._weights is None:
                 warnings.warn("LPIPS: pretrained VGG16 / lin weights are not available offline; using a deterministic "
@@ -130,6 +202,8 @@ class LPIPS(nn.Module):
     def value_and_grad(self, in0, in1, up: torch.Tensor, out: torch.Tensor, clamp: bool = True) -> torch.Tensor:
         """Autograd-free form for the fused trainer: out[N] = LPIPS(clamp01(in0), clamp01(in1)) per image (the
         HybridLossPlus call on Bhat_srgb01 / B_srgb01), returns d(sum_n up[n] out[n]) / d in0 (through the clamp)."""
+        if self.net != "vgg":
+            raise NotImplementedError("the fused trainer's LPIPS term is net='vgg' (losses.py:268)")
         stack, lins = self.parts(in0.device)
         f0, tape, t0 = stack.forward(_vgg.prep_input(in0, SHIFT, SCALE, clamp=clamp, dtype=stack.dtype), save=True,
                                      taps=TAPS)
@@ -150,7 +224,31 @@ class LPIPS(nn.Module):
         call("add_relu_masked", d_last, grads.pop(last), t0[last], d_last.numel(), stack.dtype)
         return _vgg.input_grad(stack.backward(tape, d_last, tap_grads=grads), in0, SCALE, clamp=clamp)
 
+    def _alex_forward(self, in0, in1, normalize):
+        _lib.require_cuda(in0, in1)
+        if in0.shape != in1.shape or in0.dim() != 4 or in0.shape[1] != 3:
+            raise ValueError("LPIPS expects two [N,3,H,W] tensors of the same shape")
+        if torch.is_grad_enabled() and (in0.requires_grad or in1.requires_grad):
+            raise NotImplementedError("LPIPS(net='alex') on MI355X is forward-only (the validation metric); use "
+                                      "net='vgg' for a differentiable term")
+        x0, x1 = in0.detach().float(), in1.detach().float()
+        if normalize:
+            x0, x1 = 2 * x0 - 1, 2 * x1 - 1
+        stack, lins = self.parts(in0.device)
+        t0 = stack.taps(_vgg.prep_input(x0, SHIFT, SCALE, clamp=False, dtype=stack.dtype))
+        t1 = stack.taps(_vgg.prep_input(x1, SHIFT, SCALE, clamp=False, dtype=stack.dtype))
+        N = in0.shape[0]
+        out = torch.zeros(N, device=in0.device)
+        for k in range(5):
+            a, b = t0[k], t1[k]
+            HW = a.shape[1] * a.shape[2]
+            ws = torch.empty(query("lpips_tap_workspace_doubles", N, HW), dtype=torch.float64, device=a.device)
+            call("lpips_tap_fwd", a, b, lins[k], N, HW, a.shape[3], 1, ws, out, stack.dtype)
+        return out.view(N, 1, 1, 1)
+
     def forward(self, in0, in1, retPerLayer: bool = False, normalize: bool = False):
         if retPerLayer:
             raise NotImplementedError("retPerLayer is not supported on MI355X")
+        if self.net == "alex":
+            return self._alex_forward(in0, in1.to(in0.device), bool(normalize))
         return _LPIPSFn.apply(in0, in1.to(in0.device), self, bool(normalize))

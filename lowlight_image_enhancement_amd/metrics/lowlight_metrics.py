@@ -3,7 +3,7 @@ NAFNet_base/basicsr/metrics/lowlight_metrics.py:211-272): thin wrappers over met
 metrics.color_error exactly as the reference composes them (fp32 casts, clamp01 before ΔE00)."""
 from __future__ import annotations
 
-from typing import Literal
+from typing import Literal, Optional
 
 import torch
 
@@ -11,7 +11,7 @@ from .color_error import deltaE2000_summary, edge_deltaE2000
 from .psnr import calculate_psnr
 from .ssim import calculate_ssim
 
-__all__ = ["linear_psnr", "linear_ssim", "deltae2000_mean", "deltae2000_p95", "edge_deltae2000_mean"]
+__all__ = ["linear_psnr", "linear_ssim", "lpips_distance", "deltae2000_mean", "deltae2000_p95", "edge_deltae2000_mean"]
 
 
 def linear_psnr(pred: torch.Tensor, target: torch.Tensor, *, data_range: float = 1.0) -> float:
@@ -20,6 +20,13 @@ def linear_psnr(pred: torch.Tensor, target: torch.Tensor, *, data_range: float =
 
 def linear_ssim(pred: torch.Tensor, target: torch.Tensor, *, data_range: float = 1.0) -> float:
     return calculate_ssim(target.to(torch.float32), pred.to(torch.float32), data_range=data_range)
+
+
+def lpips_distance(pred: torch.Tensor, target: torch.Tensor, *, net: str = "vgg", device: Optional[str] = None) -> float:
+    """lowlight_metrics.py:223-226: LPIPSEvaluator(net, device)(target, pred)."""
+    from .lpips_metric import evaluator
+    dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
+    return evaluator(net, dev)(target.to(dev), pred.to(dev))
 
 
 def deltae2000_mean(pred: torch.Tensor, target: torch.Tensor, *,

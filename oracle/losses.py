@@ -271,4 +271,35 @@ def lpips_vgg(feats, lins, in0, in1):
     return val
 
 
+# torchvision alexnet.features (lpips net='alex' slices: relu1 | pool, conv, relu2 | pool, conv, relu3 | conv, relu4 |
+# conv, relu5): (module index, stride, pad) of each conv
+ALEX_CONVS = ((0, 4, 2), (3, 1, 2), (6, 1, 1), (8, 1, 1), (10, 1, 1))
+
+
+def lpips_alex(feats, lins, in0, in1):
+    """lpips.LPIPS(net='alex').forward(in0, in1) per image [N,1,1,1] (lpips 0.1.4 pretrained_networks.alexnet +
+    the same head as lpips_vgg)."""
+    shift = torch.tensor(LPIPS_SHIFT, dtype=in0.dtype).view(1, 3, 1, 1)
+    scale = torch.tensor(LPIPS_SCALE, dtype=in0.dtype).view(1, 3, 1, 1)
+
+    def taps(x):
+        h, out = (x - shift) / scale, []
+        for i, (idx, st, pad) in enumerate(ALEX_CONVS):
+            if i in (1, 2):
+                h = F.max_pool2d(h, 3, 2)
+            h = F.relu(F.conv2d(h, feats[f"{idx}.weight"].to(x.dtype), feats[f"{idx}.bias"].to(x.dtype), stride=st,
+                                padding=pad))
+            out.append(h)
+        return out
+
+    t0, t1 = taps(in0), taps(in1)
+    val = 0
+    for k in range(5):
+        u = t0[k] / (t0[k].pow(2).sum(1, keepdim=True).sqrt() + 1e-10)
+        v = t1[k] / (t1[k].pow(2).sum(1, keepdim=True).sqrt() + 1e-10)
+        val = val + ((u - v) ** 2 * lins[k].to(in0.dtype).view(1, -1, 1, 1)).sum(1, keepdim=True).mean((2, 3),
+                                                                                                     keepdim=True)
+    return val
+
+
 _ = math  # keep import for callers that use math constants

@@ -222,3 +222,49 @@ def test_trainer_cfg3_terms_match_autograd_composition(dev):
         assert abs(logs[k] - v.item()) <= 1e-5 * max(abs(v.item()), 1e-6) + 1e-7, (k, logs[k], v.item())
     ref = net.flat.grad
     assert ((fused - ref).norm() / ref.norm()).item() < 1e-4
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_lpips_alex_against_oracle(dev, precision):
+    """LPIPS(net='alex') (lpips 0.1.4 restated; parity unpinned: package and weights absent) vs the oracle's float64
+    restatement with the same synthetic AlexNet + lin weights: strided 11x11 / 5x5 convs on the implicit-GEMM MFMA
+    kernel, 3x3/2 max pools; per-image values within 2 %.  Forward-only: a gradient request raises."""
+    import oracle.losses as OL
+    from lowlight_image_enhancement_amd.lpips import ALEX_TAP_CH, LPIPS, alex_synthetic_state_dict
+    feats = alex_synthetic_state_dict(3)
+    g = torch.Generator().manual_seed(4)
+    lins = [(torch.randn(c, generator=g) * 0.1).abs() for c in ALEX_TAP_CH]
+    sd = {f"net.slice1.{k}": v for k, v in feats.items()}
+    sd.update({f"lin{k}.model.1.weight": w.view(1, -1, 1, 1) for k, w in enumerate(lins)})
+    m = LPIPS(net="alex", weights=sd, precision=precision)
+    a, b = torch.rand(2, 3, 96, 80, generator=g) * 2 - 1, torch.rand(2, 3, 96, 80, generator=g) * 2 - 1
+    with torch.no_grad():
+        out = m(a.to(dev), b.to(dev)).cpu()
+    ref = OL.lpips_alex({k: v.double() for k, v in feats.items()}, lins, a.double(), b.double())
+    assert out.shape == (2, 1, 1, 1)
+    assert ((out.double() - ref).abs() <= 2e-2 * ref.abs()).all(), (out.view(-1), ref.view(-1))
+    with pytest.raises(NotImplementedError):
+        m(a.to(dev).requires_grad_(True), b.to(dev))
+
+
+def test_lpips_distance_metric_wiring(dev):
+    """basicsr lowlight_metrics.lpips_distance (:223-226) -> LPIPSEvaluator (metrics/lpips_metric.py:34-117): the
+    [0,1] -> [-1,1] mapping and the (target, pred) argument order, for the config's net='vgg' and the default 'alex'."""
+    import oracle.losses as OL
+    from lowlight_image_enhancement_amd.lpips import ALEX_TAP_CH, TAP_CH, alex_synthetic_state_dict
+    from lowlight_image_enhancement_amd.metrics.lowlight_metrics import lpips_distance
+    from lowlight_image_enhancement_amd.vgg import VGG16_CFG, synthetic_state_dict
+    g = torch.Generator().manual_seed(5)
+    pred, tgt = torch.rand(1, 3, 64, 64, generator=g), torch.rand(1, 3, 64, 64, generator=g)
+    got_vgg = lpips_distance(pred.to(dev), tgt.to(dev), net="vgg")
+    got_alex = lpips_distance(pred.to(dev), tgt.to(dev), net="alex")
+    gl = torch.Generator().manual_seed(0)
+    lins_v = [(torch.randn(c, generator=gl) * 0.1).abs() for c in TAP_CH]
+    gl = torch.Generator().manual_seed(0)
+    lins_a = [(torch.randn(c, generator=gl) * 0.1).abs() for c in ALEX_TAP_CH]
+    fv = {k: v.double() for k, v in synthetic_state_dict(VGG16_CFG, 30, seed=0).items()}
+    fa = {k: v.double() for k, v in alex_synthetic_state_dict(0).items()}
+    p1, t1 = pred.double() * 2 - 1, tgt.double() * 2 - 1
+    ref_vgg = OL.lpips_vgg(fv, lins_v, p1, t1).mean().item()
+    ref_alex = OL.lpips_alex(fa, lins_a, p1, t1).mean().item()
+    assert abs(got_vgg - ref_vgg) <= 3e-2 * ref_vgg and abs(got_alex - ref_alex) <= 2e-2 * ref_alex
