@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the bench (eager launches so every dispatch is attributed), kernel trace + stats only, each counter
 # group in its own run (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
-#   fetch: FETCH_SIZE   write: WRITE_SIZE   mfma: SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE
+#   fetch: FETCH_SIZE   write: WRITE_SIZE   mfma: SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_{F16,BF16,F32}
 # Output under gpurun_out/pmc_<pass>/; scripts/pmc_traffic.py turns them into profiles/<name>_pmc_traffic.json.
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -17,5 +17,5 @@ pass() {
 }
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
-pass mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE
+pass mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32
 ls gpurun_out/pmc_fetch gpurun_out/pmc_mfma | head

@@ -1,8 +1,11 @@
 """HBM traffic and MFMA busy per launch from the PMC passes of scripts/pmc_pass.sh (MI355X_MICROARCH.md, HBM and PMC
 sections): bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 -- FETCH_SIZE / WRITE_SIZE are in KiB and gfx950's FETCH_SIZE
-reports half the bytes of wide coalesced reads; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs)
-(the counter counts MFMA-pipe cycles summed over SIMDs, 32 per v_mfma_f32_32x32x16; GRBM_GUI_ACTIVE = the dispatch's GPU
-cycles).  Writes profiles/<out>.json keyed by bench.py's kernel classes.
+reports half the bytes of wide coalesced reads; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (dispatch ns * 2.4 GHz * 1024
+SIMDs) (the counter sums MFMA-pipe cycles over the SIMDs, ~32 per v_mfma_f32_32x32x16 -- calibrated against the GEMM
+class's algorithmic MFMA count; 2.4 GHz is the peak clock, so this is a lower bound on utilisation; rocprofv3 reports
+GRBM_GUI_ACTIVE summed over the 8 XCDs, so it is not used as the denominator) and MFMA FLOP rate = (MOPS_F16 + MOPS_BF16
++ MOPS_F32) * 512 / dispatch ns vs the dense peak of the dtype.  Writes profiles/<out>.json keyed by bench.py's kernel
+classes.
 
     python scripts/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_mfma profiles/rNN_pmc_traffic.json
 """
@@ -18,25 +21,31 @@ CLASSES = {"gemm16": ("gemm_bf16_kernel", "gemm_skinny_kernel"), "wgrad": ("wgra
 SIMDS = 256 * 4
 
 
-def load(d, counter):
+def load(d, counter, with_ns=False):
     per = collections.defaultdict(list)
     path = f"{d}/run_counter_collection.csv"
     if not os.path.exists(path):
         return per
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            v = float(r["Counter_Value"])
+            per[r["Kernel_Name"]].append((v, int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) if with_ns else v)
     return per
+
+
+CLOCK_GHZ = 2.4
+PEAK = {"f16": 2.5e15, "bf16": 2.5e15, "f32": 157.3e12}
 
 
 def main(fetch_dir, write_dir, mfma_dir, out):
     f, w = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
-    mb, ga = load(mfma_dir, "SQ_VALU_MFMA_BUSY_CYCLES"), load(mfma_dir, "GRBM_GUI_ACTIVE")
-    bc = load(mfma_dir, "SQ_BUSY_CU_CYCLES")
-    res = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES "
-                     "GRBM_GUI_ACTIVE in separate passes (--kernel-trace --stats), bench.py --eager --quick --steps 3 "
-                     "--warmup 1; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch; mfma_busy = "
-                     "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * 1024 SIMDs)",
+    mb = load(mfma_dir, "SQ_VALU_MFMA_BUSY_CYCLES", with_ns=True)
+    mops = {t: load(mfma_dir, f"SQ_INSTS_VALU_MFMA_MOPS_{t.upper()}") for t in ("f16", "bf16", "f32")}
+    res = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_VALU_MFMA_BUSY_CYCLES "
+                     "SQ_INSTS_VALU_MFMA_MOPS_{F16,BF16,F32} in separate passes (--kernel-trace --stats), bench.py "
+                     "--eager --quick --steps 3 --warmup 1; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch; "
+                     f"mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (dispatch ns * {CLOCK_GHZ} GHz * 1024 SIMDs); "
+                     "mfma_flops = MOPS * 512",
            "classes": {}}
     for cls, pats in CLASSES.items():
         names = [k for k in f if any(p in k for p in pats)]
@@ -49,13 +58,16 @@ def main(fetch_dir, write_dir, mfma_dir, out):
                "traffic_bytes_per_launch": (2 * fetch + write) / n}
         mn = [k for k in mb if any(p in k for p in pats)]
         if mn:
-            busy = sum(sum(mb[k]) for k in mn)
-            gui = sum(sum(ga.get(k, [])) for k in mn)
-            rec.update({"mfma_busy_cycles_per_launch": busy / sum(len(mb[k]) for k in mn),
-                        "gpu_cycles_per_launch": gui / max(sum(len(ga.get(k, [])) for k in mn), 1),
-                        "busy_cu_cycles_per_launch": sum(sum(bc.get(k, [])) for k in mn) / max(
-                            sum(len(bc.get(k, [])) for k in mn), 1),
-                        "mfma_busy_frac": busy / (gui * SIMDS) if gui else None})
+            busy = sum(v for k in mn for v, _ in mb[k])
+            ns = sum(t for k in mn for _, t in mb[k])
+            nl = sum(len(mb[k]) for k in mn)
+            rec.update({"mfma_busy_cycles_per_launch": busy / nl, "dispatch_us_per_launch": ns / nl / 1e3,
+                        "mfma_busy_frac": busy / (ns * CLOCK_GHZ * SIMDS) if ns else None})
+            for t, per in mops.items():
+                fl = sum(sum(per.get(k, [])) for k in mn) * 512.0
+                if fl:
+                    rec[f"mfma_{t}_flops_per_launch"] = fl / nl
+                    rec[f"mfma_{t}_flops_frac"] = fl / (ns * 1e-9) / PEAK[t]
         res["classes"][cls] = rec
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res["classes"], indent=1))
