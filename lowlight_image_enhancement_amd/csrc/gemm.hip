@@ -393,10 +393,11 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
 // (16 MFMAs per wave between barrier pairs, 8x the old 64 x 64 tile's), next stage prefetched into registers.
 // Each operand tile lives in LDS as two 64-column panels with the conflict-free 96-element rows of
 // wgrad_bf16_kernel, read transposed by ds_read_b64_tr_b16.  Bias (column sums of G) from the loader's registers.
+constexpr int WIDE_LDS = 4 * 64 * 96;  // 16-bit elements: G panels 0, 1; X panels 2, 3 (64 rows x 96)
+
 template <int XMODE, typename H>
-__device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by, int bz) {
+__device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by, int bz, H* lds) {
   constexpr int RM = 64, LS = 96, PAN = RM * LS;
-  __shared__ __attribute__((aligned(16))) H lds[4 * PAN];  // G panels 0, 1; X panels 2, 3
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -544,25 +545,30 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
 
 template <int XMODE, typename H>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
-  wgrad_wide_tile<XMODE, H>(p, blockIdx.x, blockIdx.y, blockIdx.z);
+  __shared__ __attribute__((aligned(16))) H lds[WIDE_LDS];
+  wgrad_wide_tile<XMODE, H>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
-// Several independent wide weight gradients (plain X) in one launch: NAFBlock conv5 (U) and conv4 at the deep levels
-// run together (2 workgroups per CU instead of 1, one launch boundary fewer); each problem's tiles are exactly those
-// of its own launch (bitwise identical results).
-constexpr int WG_MAX = 4;
+// Many independent wide weight gradients in one launch (nbp_wgrad_group): all the 128-multiple weight gradients of a
+// U-Net level's NAFBlocks (conv5's U, conv4, conv3's U with the per-image SCA scale, conv1) are queued while the
+// level's backward runs and launched together, with the M-splits chosen for the whole group (few or no splits when
+// the group alone fills the chip: the slabs shrink and so do their reductions).
+constexpr int WG_MAX = 24;
 struct WGroup {
   WgradP p[WG_MAX];
   int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
+  unsigned char xscale[WG_MAX];
   int n;
 };
 template <typename H>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
+  __shared__ __attribute__((aligned(16))) H lds[WIDE_LDS];
   const int b = blockIdx.x;
   int i = 0;
   while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
   const int l = b - g.start[i], gx = g.gx[i], gy = g.gy[i];
-  wgrad_wide_tile<AM_PLAIN, H>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy));
+  if (g.xscale[i]) wgrad_wide_tile<AM_SCALE, H>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy), lds);
+  else wgrad_wide_tile<AM_PLAIN, H>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy), lds);
 }
 
 // Column sums of a [S][L] fp32 slab.  A lane sums VEC adjacent columns (float4 loads when VEC = 4) over the rows
@@ -928,7 +934,34 @@ thread_local bool g_wgroup = false;
 thread_local std::vector<WgradP> g_wqueue;
 thread_local int g_wqueue_dtype = 1;  // the 16-bit type of the queued problems (one per group)
 
+// NBP_WGROUP_TARGET: the workgroup count a group launch aims for when choosing the M-splits (A/B measurement)
+long wgroup_target() {
+  static const long v = [] {
+    const char* e = getenv("NBP_WGROUP_TARGET");
+    const long t = e ? atol(e) : 512L;
+    return t < 1 ? 512L : t;
+  }();
+  return v;
+}
+
+// Splits for the whole group: each problem keeps at most its standalone split count (its workspace) and at least
+// 256 rows per split; the group as a whole aims at ~wgroup_target() workgroups.  The reductions queued for the
+// problems' slabs are re-pointed at the chosen split counts.
 void wgroup_launch(hipStream_t st) {
+  long tiles = 0;
+  for (const WgradP& p : g_wqueue) tiles += (long)(p.N / 128) * (p.K / 128);
+  const long want = (wgroup_target() + tiles - 1) / (tiles > 0 ? tiles : 1);
+  for (WgradP& p : g_wqueue) {
+    const long s_max = cdiv(p.M, p.chunk);
+    long s = want < s_max ? want : s_max;
+    const long rows_cap = p.M / 256 > 1 ? p.M / 256 : 1;
+    if (s > rows_cap) s = rows_cap;
+    if (s < 1) s = 1;
+    p.chunk = cdiv(cdiv(p.M, (int)s), 64) * 64;
+    const int S_ = cdiv(p.M, p.chunk);
+    for (RDesc& d : g_pending)
+      if (d.slab == p.slab || (p.slab_b && d.slab == p.slab_b)) d.S = S_, d.ty = make_rdesc(d.slab, S_, d.L, d.out).ty;
+  }
   size_t i = 0;
   while (i < g_wqueue.size()) {
     WGroup g;
@@ -939,6 +972,7 @@ void wgroup_launch(hipStream_t st) {
       g.p[g.n] = p;
       g.gx[g.n] = p.N / 128;
       g.gy[g.n] = p.K / 128;
+      g.xscale[g.n] = p.x_scale != nullptr;
       g.start[g.n] = blocks;
       blocks += g.gx[g.n] * g.gy[g.n] * cdiv(p.M, p.chunk);
       ++g.n;
@@ -977,9 +1011,10 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
                       (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0));
     const dim3 wgrid(N / 128, K / 128, S_);
     // grouped only while the slab reductions are deferred (they must run after the queued launch)
-    if (wide && x_mode == AM_PLAIN && g_wgroup && g_defer) {  // nbp_wgrad_group(0, ...) launches
+    if (wide && g_wgroup && g_defer) {  // nbp_wgrad_group(0, ...) launches
       NBP_REQUIRE(g_wqueue.empty() || g_wqueue_dtype == dtype, "nbp_wgrad_f32: mixed dtypes in one group");
       g_wqueue_dtype = dtype;
+      if (x_mode != AM_SCALE) p.x_scale = nullptr;  // the group kernel selects the X mode by x_scale
       g_wqueue.push_back(p);
     } else NBP_DISPATCH_H(dtype, {
       if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);

@@ -106,8 +106,11 @@ class NAFNet(nn.Module):
         # the LayerNorm fusions at C = 256 too (64 x 256 tiles, one workgroup per CU): NBP_FUSE_LN256 = bwd (default:
         # +0.35 %), 1 (both), fwd (-0.4 %) or 0
         self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "bwd")
-        # conv5 (U) and conv4 weight gradients as one grouped launch at C >= 128 (NBP_GROUP_WGRAD=0: two launches)
+        # the wide (C >= 128) weight gradients of a whole U-Net level (conv5's U, conv4, conv3's U, conv1 of every
+        # NAFBlock of the level) queued during the level's backward and launched as ONE grouped launch at its end,
+        # with M-splits chosen for the group (NBP_GROUP_WGRAD=0: one launch per weight gradient)
         self.group_wgrad = os.environ.get("NBP_GROUP_WGRAD", "1") != "0"
+        self._grouping = False
         # level 0 (C = 32): the conv4 output t4 is not stored; the conv5 dgrad rebuilds it per tile on MFMA
         # (nbp_dgrad_sg_rc, bitwise equal) -- NBP_SG_RC=0 stores and re-reads it
         self.sg_rc = os.environ.get("NBP_SG_RC", "1") != "0"
@@ -477,11 +480,24 @@ class NAFNet(nn.Module):
         try:
             return self._walk_backward(tape, dout, dflat, need_dx, P, hook)
         finally:
+            if self._grouping:  # an error inside a grouped level: launch what is queued so the library state is reset
+                self._grouping = False
+                call("wgrad_group", 0)
             if self._side_used:
                 torch.cuda.current_stream().wait_stream(self._side_used)
                 self._side_used = None
             call("grad_reduce_flush", 1)
             self._keep = None
+
+    def _level_grouped(self, c: int) -> bool:
+        return self.dt != 0 and c % 128 == 0 and self.group_wgrad and not self.overlap_wgrad
+
+    def _close_level(self, pending: List[str], hook):
+        """Launch the level's queued weight gradients, then complete its stages (flush + DP hooks) in order."""
+        call("wgrad_group", 0)
+        self._grouping = False
+        for name in pending:
+            self._stage_done(name, hook)
 
     def _walk_backward(self, tape, dout, dflat, need_dx, P, hook):
         Wt = (P,)
@@ -491,10 +507,20 @@ class NAFNet(nn.Module):
         dfeat = None
         dskips: List[torch.Tensor] = []
         dx_img = None
+        level: Optional[List[str]] = None  # stages of the current grouped level, completed when it closes
+        level_c = 0
         for rec in reversed(tape):
             kind = rec[0]
             if kind == "weights":
                 continue
+            grouped = kind == "block" and self._level_grouped(rec[2][3])
+            if level is not None and not (grouped and rec[2][3] == level_c):
+                self._close_level(level, hook)
+                level = None
+            if grouped and level is None:
+                call("wgrad_group", 1)
+                self._grouping = True
+                level, level_c = [], rec[2][3]
             if kind == "ending":
                 feat, (B, Ci, H0, W0, Hp, Wp, w) = rec[1], rec[2]
                 dfeat = torch.empty(B, Hp, Wp, w, device=dout.device, dtype=self.adt)
@@ -506,7 +532,10 @@ class NAFNet(nn.Module):
             elif kind == "block":
                 pre, geo, S = rec[1], rec[2], rec[3]
                 dfeat = self._block_bwd(P, Wt, dflat, pre, geo, S, dfeat)
-                self._stage_done(pre[:-1], hook)
+                if level is not None:
+                    level.append(pre[:-1])
+                else:
+                    self._stage_done(pre[:-1], hook)
             elif kind == "up":
                 i, (B, h, w, chan), x = rec[1], rec[2], rec[3]
                 dskips.append(dfeat)  # d(skip) = d(up output): the skip add is an identity branch
@@ -539,6 +568,8 @@ class NAFNet(nn.Module):
                 call("intro_bwd", x, dfeat, self._slice(P, "intro.weight"), self._slice(dflat, "intro.weight"),
                      self._slice(dflat, "intro.bias"), dx_img, ws, B, Ci, H0, W0, Hp, Wp, w, self.dt)
                 self._stage_done("intro", hook)
+        if level is not None:
+            self._close_level(level, hook)
         if need_dx:
             # global residual x + inp (NAFNet_arch.py:153): d inp += d out
             call("add", dx_img, dout, dx_img, dx_img.numel(), 0)
@@ -578,6 +609,8 @@ class NAFNet(nn.Module):
         referenced until the stage flush, which joins the side stream first."""
         n_ws = query("wgrad_workspace_floats", M, N, K)
         ws = self._ws(n_ws, G.device)
+        if self._grouping and self._keep is not None:  # the launch is deferred to the level's end: keep the operands
+            self._keep.extend(t for t in (G, X, xscale) if t is not None)
         if not (self.overlap_wgrad and self._keep is not None):
             call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
                  n_ws, self.dt if dtype is None else dtype)
@@ -623,10 +656,7 @@ class NAFNet(nn.Module):
             self._mm(Wt, dout, c, AM_SCALE, self._slice(P, pre + "gamma"), M, pre + "conv5.weight", dg2, c, CM_PLAIN,
                      M, c, c, dgrad=True)
             call("sg_bwd", dg2, S["t4"], dt4, M, c, 1, dt)
-        # the two wide weight gradients that only need dout / dt4 run as one grouped launch (nbp_wgrad_group)
-        group = dt != 0 and c % 128 == 0 and self.group_wgrad and not self.overlap_wgrad
-        if group:
-            call("wgrad_group", 1)
+        # at C >= 128 the wide weight gradients below are queued into the level's grouped launch (_walk_backward)
         U5, V5 = F(c * c), F(c)
         self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
         call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
@@ -639,8 +669,6 @@ class NAFNet(nn.Module):
         dy = E(M, c)
         self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
-        if group:
-            call("wgrad_group", 0)
         if fuse_ln:
             self._dgrad_ln(Wt, dflat, P, pre, "conv4.weight", "norm2", dt4, S["y"].reshape(M, c), S["st2"], dout, dy,
                            M, c)
