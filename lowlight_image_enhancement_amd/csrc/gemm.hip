@@ -938,8 +938,8 @@ thread_local int g_wqueue_dtype = 1;  // the 16-bit type of the queued problems 
 long wgroup_target() {
   static const long v = [] {
     const char* e = getenv("NBP_WGROUP_TARGET");
-    const long t = e ? atol(e) : 512L;
-    return t < 1 ? 512L : t;
+    const long t = e ? atol(e) : 1024L;
+    return t < 1 ? 1024L : t;
   }();
   return v;
 }

@@ -490,12 +490,21 @@ class NAFNet(nn.Module):
             self._keep = None
 
     def _level_grouped(self, c: int) -> bool:
-        return self.dt != 0 and c % 128 == 0 and self.group_wgrad and not self.overlap_wgrad
+        return self.dt != 0 and c % 128 == 0 and self.group_wgrad and self.overlap_wgrad in (0, 3)
 
     def _close_level(self, pending: List[str], hook):
-        """Launch the level's queued weight gradients, then complete its stages (flush + DP hooks) in order."""
-        call("wgrad_group", 0)
+        """Launch the level's queued weight gradients, then complete its stages (flush + DP hooks) in order.
+        NBP_OVERLAP_WGRAD=3 (single process): the grouped launch runs on the side stream, overlapping the next
+        level's backward; one join + reduction flush at the end of the backward."""
         self._grouping = False
+        if self.overlap_wgrad == 3 and hook is None:
+            side = self._side(self.flat.device if self.flat.is_cuda else torch.device("cuda"))
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                call("wgrad_group", 0)
+            self._side_used = side
+            return
+        call("wgrad_group", 0)
         for name in pending:
             self._stage_done(name, hook)
 
@@ -583,7 +592,7 @@ class NAFNet(nn.Module):
         return st
 
     def _stage_done(self, name, hook):
-        if self.overlap_wgrad == 2 and hook is None:
+        if self.overlap_wgrad in (2, 3) and hook is None:
             return  # everything is joined and flushed once at the end of exec_backward
         # join the wgrad side stream, then the stage's queued gradient reductions run before anyone (the DP
         # all-reduce hook) reads its slice
@@ -611,7 +620,7 @@ class NAFNet(nn.Module):
         ws = self._ws(n_ws, G.device)
         if self._grouping and self._keep is not None:  # the launch is deferred to the level's end: keep the operands
             self._keep.extend(t for t in (G, X, xscale) if t is not None)
-        if not (self.overlap_wgrad and self._keep is not None):
+        if not (self.overlap_wgrad in (1, 2) and self._keep is not None):
             call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
                  n_ws, self.dt if dtype is None else dtype)
             return

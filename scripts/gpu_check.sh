@@ -18,7 +18,9 @@ run() {
 }
 STEPS=${STEPS:-smoke,pytest,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+KARGS=()
+[ -n "${PYTEST_K:-}" ] && KARGS=(-k "$PYTEST_K")
+[[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread "${KARGS[@]}"
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --steps 10 --warmup 3
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
