@@ -10,6 +10,8 @@ from lowlight_image_enhancement_amd._lib import call, query  # noqa: E402
 
 dev = torch.device("cuda:0")
 REPS = 200
+DT = int(os.environ.get("NBP_MICRO_DT", "1"))  # 1 bf16, 2 fp16
+TD = torch.float16 if DT == 2 else torch.bfloat16
 
 
 def timeit(fn):
@@ -39,22 +41,22 @@ rows = []
 for (M, N, K, mode) in [(4096, 1024, 512, 0), (4096, 512, 512, 0), (4096, 512, 512, 2), (4096, 512, 1024, 0),
                         (16384, 512, 256, 0), (16384, 256, 256, 0), (16384, 256, 512, 0), (65536, 256, 128, 0),
                         (65536, 128, 128, 0), (65536, 128, 256, 0)]:
-    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
-    Cc = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    A = torch.randn(M, K, device=dev).to(TD)
+    W = torch.randn(N, K, device=dev).to(TD)
+    Cc = torch.empty(M, N, device=dev, dtype=TD)
     bias = torch.randn(N, device=dev)
     sc = torch.rand(M // 256 + 1, K, device=dev)
-    us = timeit(lambda: call("gemm_bf16", A, K, mode, sc if mode == 2 else None, 256, 1, W, K, Cc, N, 0, 1, M, N, K,
+    us = timeit(lambda: call("gemm_bf16", A, K, mode, sc if mode == 2 else None, 256, DT, W, K, Cc, N, 0, DT, M, N, K,
                              0, 0, 0, bias, None, None, None))
     fl = 2.0 * M * N * K
     rows.append(f"gemm  M={M:6d} N={N:5d} K={K:5d} amode={mode}: {us:7.2f} us  {fl / us / 1e6:7.1f} TF")
 for (M, N, K) in [(4096, 1024, 512), (4096, 512, 512), (16384, 512, 256), (16384, 256, 256), (65536, 256, 128)]:
-    G = torch.randn(M, N, device=dev).to(torch.bfloat16)
-    X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    G = torch.randn(M, N, device=dev).to(TD)
+    X = torch.randn(M, K, device=dev).to(TD)
     dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
     n_ws = query("wgrad_workspace_floats", M, N, K)
     ws = torch.empty(n_ws, device=dev)
-    us = timeit(lambda: call("wgrad_f32", G, N, 0, X, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws, 1))
+    us = timeit(lambda: call("wgrad_f32", G, N, 0, X, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws, DT))
     rows.append(f"wgrad M={M:6d} N={N:5d} K={K:5d} (+reduce): {us:7.2f} us  {2.0 * M * N * K / us / 1e6:7.1f} TF")
 print(f"NBP_GEMM_MINBLK={os.environ.get('NBP_GEMM_MINBLK', '-')}")
 print("\n".join(rows))
@@ -63,8 +65,8 @@ print("\n".join(rows))
 ref = []
 for (M, N, K) in [(4096, 1024, 512), (4096, 512, 512), (16384, 512, 256), (16384, 256, 256), (65536, 256, 128),
                   (65536, 128, 128)]:
-    A = torch.randn(M, K, device=dev).to(torch.bfloat16)
-    W = torch.randn(N, K, device=dev).to(torch.bfloat16)
+    A = torch.randn(M, K, device=dev).to(TD)
+    W = torch.randn(N, K, device=dev).to(TD)
     us = timeit(lambda: torch.mm(A, W.t()))
     ref.append(f"torch.mm M={M:6d} N={N:5d} K={K:5d}: {us:7.2f} us  {2.0 * M * N * K / us / 1e6:7.1f} TF")
     # an empty-ish launch for the launch floor
