@@ -155,8 +155,8 @@ int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const f
 int nbp_grad_reduce_flush(int stop, nbp_stream_t s);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
-/* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC, C a power of two
- * (multiple of 16 bytes): writes nout = w * (x - mu) / den + b and stats[M][2] = {mu, den = sqrt(var + eps)}.
+/* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC, C any multiple of
+ * 16 bytes (8 16-bit / 4 fp32 channels) up to 256 such chunks: writes nout = w * (x - mu) / den + b and stats[M][2] = {mu, den = sqrt(var + eps)}.
  * The closed-form backward (:277-289) recomputes yhat from x and stats, adds the residual gradient dres and writes
  * per-block partials of dw / db into slab_w / slab_b ([nbp_ln_nhwc_grid(M, C, dtype)][C] each, fold with
  * nbp_reduce_slab). */

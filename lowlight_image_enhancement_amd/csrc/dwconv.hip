@@ -218,13 +218,14 @@ __global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ pool, 
 }
 
 // per-image channel reduction: slab[b][chunk][c] = sum_{p in chunk} x[p][c] * (y ? y[p][c] : 1).
-// grid (chunks, B, channel groups of CG = min(C, 64) channels): each block a pixel chunk x channel group.
+// grid (chunks, B, ceil(C / 64) channel groups of up to 64 channels): each block a pixel chunk x channel group.
 template <typename T>
 __global__ void img_chan_dot(const T* __restrict__ x, const T* __restrict__ y, float* __restrict__ slab, Geo geo) {
   extern __shared__ float red[];
-  const int C = geo.C, CG = C < 64 ? C : 64, Q = CG / 4;
+  // channel group blockIdx.z: 64 channels (the last group of a C that is not a multiple of 64: the rest)
+  const int C = geo.C, c0 = blockIdx.z * 64, CG = min(64, C - c0), Q = CG / 4;
   const int tid = threadIdx.x, q = tid % Q, pl = tid / Q, PPI = blockDim.x / Q;
-  const int b = blockIdx.y, chunk = blockIdx.x, c0 = blockIdx.z * CG;
+  const int b = blockIdx.y, chunk = blockIdx.x;
   const int HW = geo.H * geo.W;
   const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
   float4 acc = f4(0.f);
@@ -1063,10 +1064,9 @@ int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const flo
 
 int nbp_img_chan_dot(const void* x, const void* y, float* slab, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && slab && B > 0 && C % 4 == 0 && C / 4 <= 1024, "nbp_img_chan_dot: bad args");
-  NBP_REQUIRE(C <= 64 || C % 64 == 0, "nbp_img_chan_dot: C must be <= 64 or a multiple of 64");
   const int Q = C / 4, blk = block_for_quads(Q);
   Geo geo = make_geo(B, H, W, C, Q, blk, img_cap(B, H, W));  // chunk geometry shared with nbp_dw_chunks(.., 0)
-  const int groups = C <= 64 ? 1 : C / 64;
+  const int groups = (C + 63) / 64;
   NBP_DISPATCH_T(dtype, img_chan_dot<T><<<dim3(geo.chunks, B, groups), 256, 256 * 4 * sizeof(float), S(s)>>>(
                             (const T*)x, (const T*)y, slab, geo));
   return check_launch("img_chan_dot");

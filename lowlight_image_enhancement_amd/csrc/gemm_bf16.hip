@@ -129,161 +129,18 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
   }
 }
 
-// 4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32 MFMA tiles.  K-loop: BK-wide tiles, double-buffered
-// LDS (one barrier per K step; the next tile's global loads are in flight during the current tile's MFMAs).
-// Epilogue: the fp32 accumulators are staged through LDS (aliasing the operand buffers) so that bias / pre-activation /
-// residual R + rscale * v / the C store all move 8 consecutive columns (16 bytes of bf16) per thread.
-template <int BM, int BN, int BK, int AMODE, int CMODE, typename TA, typename TC, typename H>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
-  static_assert(sizeof(TA) == 4 || sizeof(TA) == sizeof(H), "A is fp32 or the operand type");
-  static_assert(sizeof(TC) == 4 || sizeof(TC) == sizeof(H), "C is fp32 or the operand type");
-  constexpr int LS = BK + 8;  // 80 / 144-byte LDS rows: conflict-free 16-byte fragment reads
+// Epilogue of the tiled kernels: the fp32 accumulators (4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32
+// MFMA tiles) are staged through LDS (smem, aliasing the operand buffers; the caller has finished every read of them)
+// so that bias / pre-activation / residual R + rscale * v / the C store all move 8 consecutive columns per thread.
+template <int BM, int BN, int CMODE, typename TC, typename H>
+__device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / 64][BN / 64], unsigned char* smem,
+                                              int m0, int n0) {
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int KC = BK / 8;  // 8-element chunks per tile row
-  constexpr int A_IT = BM * KC / 256, B_IT = BN * KC / 256;
-  constexpr int AB_BYTES = 2 * (BM + BN) * LS * 2;
   constexpr int CLS = BN + 4;  // fp32 C-tile row stride
-  constexpr int C_BYTES = BM * CLS * 4;
-  constexpr int SM_BYTES = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
-  H* As = reinterpret_cast<H*>(smem);       // [2][BM][LS]
-  H* Bs = As + 2 * BM * LS;                       // [2][BN][LS]
-  float* Cs = reinterpret_cast<float*>(smem);          // [BM][CLS] (after the K loop)
+  float* Cs = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int M = p.M, N = p.N, K = p.K;
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // two register sets: with BK = 64 the loads of K-tiles t+1 and t+2 are in flight while tile t is multiplied
-  vec_t<H, 8> ra0[A_IT], rb0[B_IT], ra1[A_IT], rb1[B_IT];
-  auto load_tiles = [&](int k0, vec_t<H, 8>* ra, vec_t<H, 8>* rb) {
-#pragma unroll
-    for (int it = 0; it < A_IT; ++it) {
-      const int idx = tid + it * 256;
-      const int r = idx / KC, kc = idx % KC;
-      const int m = m0 + r, k = k0 + kc * 8;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (AMODE == AM_CONV) {
-        if (m < M && k < K) {
-          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, oi = rem / p.gw, oj = rem - oi * p.gw;
-          const int t = k / p.cs, c = k - t * p.cs, ki = t / p.kw, kj = t - ki * p.kw;
-          const int ii = oi * p.stride + ki - p.pad, jj = oj * p.stride + kj - p.pad;
-          if (ii >= 0 && ii < p.ih && jj >= 0 && jj < p.iw)
-            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.ih + ii) * p.iw + jj) * p.cs + c, nullptr);
-        }
-      } else if (AMODE == AM_IM2COL) {
-        if (m < M && k < K) {
-          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, i = rem / p.gw, j = rem - i * p.gw;
-          const int t = k / p.cs, c = k - t * p.cs;
-          const int ii = i + t / 3 - 1, jj = j + t % 3 - 1;
-          if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
-            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.gh + ii) * p.gw + jj) * p.cs + c, nullptr);
-        }
-      } else if (m < M && k < K) {
-        long off;
-        if (AMODE == AM_S2D) off = s2d_off(m, k, p.gh, p.gw, p.cs);
-        else off = (long)m * p.lda + k;
-        const float* sc = AMODE == AM_SCALE ? p.a_scale + (long)(m / p.rows_per_img) * K + k : nullptr;
-        v = load8<TA, AMODE, H>(p.A, off, sc);
-      }
-      ra[it] = v;
-    }
-#pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int idx = tid + it * 256;
-      const int r = idx / KC, kc = idx % KC;
-      const int n = n0 + r, k = k0 + kc * 8;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (n < N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.B) + (long)n * p.ldb + k);
-      rb[it] = v;
-    }
-  };
-  auto store_tiles = [&](int buf, const vec_t<H, 8>* ra, const vec_t<H, 8>* rb) {
-    H* a = As + buf * BM * LS;
-    H* b = Bs + buf * BN * LS;
-#pragma unroll
-    for (int it = 0; it < A_IT; ++it) {
-      const int idx = tid + it * 256;
-      *reinterpret_cast<vec_t<H, 8>*>(a + (idx / KC) * LS + (idx % KC) * 8) = ra[it];
-    }
-#pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int idx = tid + it * 256;
-      *reinterpret_cast<vec_t<H, 8>*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
-    }
-  };
-  const int arow = wm * (BM / 2) + (lane & 31);
-  const int brow = wn * (BN / 2) + (lane & 31);
-  const int kh = (lane >> 5) * 8;
-  auto compute = [&](int buf) {
-    const H* a_s = As + buf * BM * LS;
-    const H* b_s = Bs + buf * BN * LS;
-#pragma unroll
-    for (int s = 0; s < BK; s += 16) {
-      vec_t<H, 8> a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (arow + i * 32) * LS + s + kh);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (brow + j * 32) * LS + s + kh);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
-    }
-  };
-
-  const int nk = (K + BK - 1) / BK;
-  if constexpr (BK == 32) {
-    // short K (one or two tiles): one register set, the next tile's loads in flight during the MFMAs
-    load_tiles(0, ra0, rb0);
-    store_tiles(0, ra0, rb0);
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < nk) load_tiles((t + 1) * BK, ra0, rb0);
-      compute(buf);
-      if (t + 1 < nk) store_tiles(buf ^ 1, ra0, rb0);
-      __syncthreads();
-    }
-  } else {
-    load_tiles(0, ra0, rb0);
-    store_tiles(0, ra0, rb0);
-    if (nk > 1) load_tiles(BK, ra1, rb1);
-    if (nk > 2) load_tiles(2 * BK, ra0, rb0);
-    __syncthreads();
-    // steady state, unrolled by two so each register set is addressed statically:
-    //   even step t: tile t in LDS buf 0, t+1 in set 1, t+2 in flight in set 0
-    //   odd step t+1: tile t+1 in LDS buf 1, t+2 in set 0, t+3 in flight in set 1
-    for (int t = 0; t < nk; t += 2) {
-      compute(0);
-      if (t + 1 < nk) {
-        store_tiles(1, ra1, rb1);
-        if (t + 3 < nk) load_tiles((t + 3) * BK, ra1, rb1);
-      }
-      __syncthreads();
-      if (t + 1 >= nk) break;
-      compute(1);
-      if (t + 2 < nk) {
-        store_tiles(0, ra0, rb0);
-        if (t + 4 < nk) load_tiles((t + 4) * BK, ra0, rb0);
-      }
-      __syncthreads();
-    }
-  }
-
-  // ---- epilogue through LDS
+  const int M = p.M, N = p.N;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -508,6 +365,325 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
       reinterpret_cast<float*>(p.pre)[((long)img * chunks + chunk) * N + n0 + tid] = t;
     }
   }
+}
+
+// Register-staged tiled kernel (any A type / mode): 4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32 MFMA
+// tiles.  K-loop: BK-wide tiles, double-buffered LDS (one barrier per K step; the next tile's global loads are in
+// flight during the current tile's MFMAs).  Epilogue: gemm_epilogue.
+template <int BM, int BN, int BK, int AMODE, int CMODE, typename TA, typename TC, typename H>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
+  static_assert(sizeof(TA) == 4 || sizeof(TA) == sizeof(H), "A is fp32 or the operand type");
+  static_assert(sizeof(TC) == 4 || sizeof(TC) == sizeof(H), "C is fp32 or the operand type");
+  constexpr int LS = BK + 8;  // 80 / 144-byte LDS rows: conflict-free 16-byte fragment reads
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int KC = BK / 8;  // 8-element chunks per tile row
+  constexpr int A_IT = BM * KC / 256, B_IT = BN * KC / 256;
+  constexpr int AB_BYTES = 2 * (BM + BN) * LS * 2;
+  constexpr int CLS = BN + 4;  // fp32 C-tile row stride
+  constexpr int C_BYTES = BM * CLS * 4;
+  constexpr int SM_BYTES = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
+  H* As = reinterpret_cast<H*>(smem);       // [2][BM][LS]
+  H* Bs = As + 2 * BM * LS;                       // [2][BN][LS]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int M = p.M, N = p.N, K = p.K;
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // two register sets: with BK = 64 the loads of K-tiles t+1 and t+2 are in flight while tile t is multiplied
+  vec_t<H, 8> ra0[A_IT], rb0[B_IT], ra1[A_IT], rb1[B_IT];
+  auto load_tiles = [&](int k0, vec_t<H, 8>* ra, vec_t<H, 8>* rb) {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx / KC, kc = idx % KC;
+      const int m = m0 + r, k = k0 + kc * 8;
+      vec_t<H, 8> v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
+      if (AMODE == AM_CONV) {
+        if (m < M && k < K) {
+          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, oi = rem / p.gw, oj = rem - oi * p.gw;
+          const int t = k / p.cs, c = k - t * p.cs, ki = t / p.kw, kj = t - ki * p.kw;
+          const int ii = oi * p.stride + ki - p.pad, jj = oj * p.stride + kj - p.pad;
+          if (ii >= 0 && ii < p.ih && jj >= 0 && jj < p.iw)
+            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.ih + ii) * p.iw + jj) * p.cs + c, nullptr);
+        }
+      } else if (AMODE == AM_IM2COL) {
+        if (m < M && k < K) {
+          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, i = rem / p.gw, j = rem - i * p.gw;
+          const int t = k / p.cs, c = k - t * p.cs;
+          const int ii = i + t / 3 - 1, jj = j + t % 3 - 1;
+          if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
+            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.gh + ii) * p.gw + jj) * p.cs + c, nullptr);
+        }
+      } else if (m < M && k < K) {
+        long off;
+        if (AMODE == AM_S2D) off = s2d_off(m, k, p.gh, p.gw, p.cs);
+        else off = (long)m * p.lda + k;
+        const float* sc = AMODE == AM_SCALE ? p.a_scale + (long)(m / p.rows_per_img) * K + k : nullptr;
+        v = load8<TA, AMODE, H>(p.A, off, sc);
+      }
+      ra[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int idx = tid + it * 256;
+      const int r = idx / KC, kc = idx % KC;
+      const int n = n0 + r, k = k0 + kc * 8;
+      vec_t<H, 8> v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
+      if (n < N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.B) + (long)n * p.ldb + k);
+      rb[it] = v;
+    }
+  };
+  auto store_tiles = [&](int buf, const vec_t<H, 8>* ra, const vec_t<H, 8>* rb) {
+    H* a = As + buf * BM * LS;
+    H* b = Bs + buf * BN * LS;
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int idx = tid + it * 256;
+      *reinterpret_cast<vec_t<H, 8>*>(a + (idx / KC) * LS + (idx % KC) * 8) = ra[it];
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int idx = tid + it * 256;
+      *reinterpret_cast<vec_t<H, 8>*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
+    }
+  };
+  const int arow = wm * (BM / 2) + (lane & 31);
+  const int brow = wn * (BN / 2) + (lane & 31);
+  const int kh = (lane >> 5) * 8;
+  auto compute = [&](int buf) {
+    const H* a_s = As + buf * BM * LS;
+    const H* b_s = Bs + buf * BN * LS;
+#pragma unroll
+    for (int s = 0; s < BK; s += 16) {
+      vec_t<H, 8> a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (arow + i * 32) * LS + s + kh);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (brow + j * 32) * LS + s + kh);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
+    }
+  };
+
+  const int nk = (K + BK - 1) / BK;
+  if constexpr (BK == 32) {
+    // short K (one or two tiles): one register set, the next tile's loads in flight during the MFMAs
+    load_tiles(0, ra0, rb0);
+    store_tiles(0, ra0, rb0);
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < nk) load_tiles((t + 1) * BK, ra0, rb0);
+      compute(buf);
+      if (t + 1 < nk) store_tiles(buf ^ 1, ra0, rb0);
+      __syncthreads();
+    }
+  } else {
+    load_tiles(0, ra0, rb0);
+    store_tiles(0, ra0, rb0);
+    if (nk > 1) load_tiles(BK, ra1, rb1);
+    if (nk > 2) load_tiles(2 * BK, ra0, rb0);
+    __syncthreads();
+    // steady state, unrolled by two so each register set is addressed statically:
+    //   even step t: tile t in LDS buf 0, t+1 in set 1, t+2 in flight in set 0
+    //   odd step t+1: tile t+1 in LDS buf 1, t+2 in set 0, t+3 in flight in set 1
+    for (int t = 0; t < nk; t += 2) {
+      compute(0);
+      if (t + 1 < nk) {
+        store_tiles(1, ra1, rb1);
+        if (t + 3 < nk) load_tiles((t + 3) * BK, ra1, rb1);
+      }
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      compute(1);
+      if (t + 2 < nk) {
+        store_tiles(0, ra0, rb0);
+        if (t + 4 < nk) load_tiles((t + 4) * BK, ra0, rb0);
+      }
+      __syncthreads();
+    }
+  }
+
+  gemm_epilogue<BM, BN, CMODE, TC, H>(p, acc, smem, m0, n0);
+}
+
+// ---------------------------------------------------------------- LDS-DMA tiled kernel (16-bit A)
+// Same tiles, fragment order and MFMA sequence as gemm_bf16_kernel (so the same accumulation order: results are
+// bitwise those of the register-staged kernel), but the operand tiles go global -> LDS with global_load_lds_dwordx4
+// (no VGPR staging, no ds_write pass) into an NS-deep ring: NS - 1 K-tiles are in flight while one is multiplied,
+// retired by a counted vmcnt and a raw s_barrier (a __syncthreads would drain the ring: vmcnt(0)).
+// Per stage: A [BM][64] then B [BN][64] of 128-byte rows, the 16-byte chunk c of row r at slot c ^ ((r >> 1) & 7)
+// (a glds instruction writes 1 KB lane-linearly, so the permutation is applied to each lane's SOURCE address; the
+// fragment reads, lanes 0..31 on rows r..r+31 at one chunk, then hit 16 distinct slots per ds_read_b128 lane group),
+// then for AM_SCALE the tile's 64 fp32 column scales (one 4-byte glds).  Out-of-range rows / columns / K tail and the
+// zero padding of AM_IM2COL read g_zero16.
+__device__ __attribute__((aligned(16))) unsigned char g_zero16[16];
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+
+// dest = lds_wave_base (wave-uniform) + lane * size
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)lds_wave_base, 4, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H>
+__global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int SC_BYTES = AMODE == AM_SCALE ? 256 : 0;
+  constexpr int ST_BYTES = A_BYTES + B_BYTES + SC_BYTES;
+  constexpr int GA = BM / 32, GB = BN / 32;  // 1-KB (8-row) glds instructions per wave per stage
+  constexpr int G = GA + GB + (AMODE == AM_SCALE ? 1 : 0);
+  constexpr int C_BYTES = BM * (BN + 4) * 4;
+  constexpr int SM_BYTES = NS * ST_BYTES > C_BYTES ? NS * ST_BYTES : C_BYTES;
+  static_assert(NS == 2 || NS == 3, "ring depth");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int M = p.M, N = p.N, K = p.K;
+  const H* A = reinterpret_cast<const H*>(p.A);
+  const H* B = reinterpret_cast<const H*>(p.B);
+  const int lr = lane >> 3, lc = lane & 7;
+
+  // this lane's source rows: instruction i covers tile rows (wave * GA + i) * 8 .. + 7, the lane row lr, chunk slot lc
+  int a_m[GA], a_kof[GA], a_b[GA], a_i[GA], a_j[GA];
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int r = (wave * GA + i) * 8 + lr;
+    a_m[i] = m0 + r;
+    a_kof[i] = 8 * (lc ^ ((r >> 1) & 7));
+    a_b[i] = a_i[i] = a_j[i] = 0;
+    if constexpr (AMODE == AM_S2D || AMODE == AM_IM2COL) {
+      const int per = p.gh * p.gw, m = a_m[i] < M ? a_m[i] : 0;
+      a_b[i] = m / per;
+      const int rem = m - a_b[i] * per;
+      a_i[i] = rem / p.gw;
+      a_j[i] = rem - a_i[i] * p.gw;
+    }
+  }
+  int b_n[GB], b_kof[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int r = (wave * GB + i) * 8 + lr;
+    b_n[i] = n0 + r;
+    b_kof[i] = 8 * (lc ^ ((r >> 1) & 7));
+  }
+  const float* sc_row = AMODE == AM_SCALE ? p.a_scale + (long)(m0 / p.rows_per_img) * K : nullptr;
+
+  const int nk = (K + BK - 1) / BK;
+  auto issue = [&](int t) {
+    unsigned char* st = smem + (t % NS) * ST_BYTES;
+    const int k0 = t * BK;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int k = k0 + a_kof[i];
+      const void* src = g_zero16;
+      if (a_m[i] < M && k < K) {
+        if constexpr (AMODE == AM_S2D) {
+          const int q = k / p.cs, c = k - q * p.cs;
+          src = A + ((long)(a_b[i] * 2 * p.gh + 2 * a_i[i] + (q >> 1)) * (2 * p.gw) + 2 * a_j[i] + (q & 1)) * p.cs + c;
+        } else if constexpr (AMODE == AM_IM2COL) {
+          const int t9 = k / p.cs, c = k - t9 * p.cs;
+          const int ii = a_i[i] + t9 / 3 - 1, jj = a_j[i] + t9 % 3 - 1;
+          if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
+            src = A + ((long)(a_b[i] * p.gh + ii) * p.gw + jj) * p.cs + c;
+        } else {
+          src = A + (long)a_m[i] * p.lda + k;
+        }
+      }
+      glds16(src, st + (wave * GA + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int k = k0 + b_kof[i];
+      const void* src = (b_n[i] < N && k < K) ? (const void*)(B + (long)b_n[i] * p.ldb + k) : (const void*)g_zero16;
+      glds16(src, st + A_BYTES + (wave * GB + i) * 1024);
+    }
+    if constexpr (AMODE == AM_SCALE) {  // every wave loads the same 64 scales (identical bytes, one instruction each)
+      const int k = k0 + lane;
+      glds4(k < K ? (const void*)(sc_row + k) : (const void*)g_zero16, st + A_BYTES + B_BYTES);
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int key = (lane >> 1) & 7;  // ((row >> 1) & 7) of every fragment row: rows are 32-aligned + (lane & 31)
+  auto compute = [&](int buf) {
+    const unsigned char* a_s = smem + buf * ST_BYTES;
+    const unsigned char* b_s = a_s + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int slot = ((2 * s + (lane >> 5)) ^ key) << 4;
+      vec_t<H, 8> a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (wm * (BM / 2) + i * 32 + (lane & 31)) * 128 + slot);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (wn * (BN / 2) + j * 32 + (lane & 31)) * 128 + slot);
+      if constexpr (AMODE == AM_SCALE) {
+        const float* scs = reinterpret_cast<const float*>(b_s + B_BYTES) + s * 16 + (lane >> 5) * 8;
+        const float4 s0 = ld4(scs), s1 = ld4(scs + 4);
+        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[i][e] = (H)((float)a[i][e] * sv[e]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
+    }
+  };
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    // retire K-tile t (this wave's DMAs), leaving the later tiles of the ring in flight; the barrier then makes every
+    // wave's part of tile t visible and frees the stage read at step t - 1 for tile t + NS - 1
+    if (NS == 3 && t + 1 < nk) wait_vm<G>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    compute(t % NS);
+  }
+  __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
+  gemm_epilogue<BM, BN, CMODE, TC, H>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
@@ -916,9 +1092,29 @@ __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long*
   }
 }
 
+// NBP_GLDS: 0 = register-staged tiles only, 2 / 3 = LDS-DMA ring depth for 16-bit A (A/B measurement; read per launch
+// so a test can compare both paths in one process).  Default 2: at the deep-level shapes (scripts/gemm_probe.py) the
+// 3-deep ring's extra LDS costs more in blocks per CU than the second tile in flight buys.
+int glds_depth() {
+  const char* e = getenv("NBP_GLDS");
+  return e ? atoi(e) : 2;
+}
+
 template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC, typename H>
 void launch(const GemmPB& p, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
+  if constexpr (sizeof(TA) == 2 && (AMODE == AM_PLAIN || AMODE == AM_SCALE || AMODE == AM_S2D || AMODE == AM_IM2COL)) {
+    const int ns = glds_depth();
+    // 16-byte aligned sources (lda, ldb, cs multiples of 8); a tile's rows in one image for the per-image scale
+    const bool ok = ns >= 2 && p.K > 32 && p.ldb % 8 == 0 &&
+                    (AMODE == AM_S2D || AMODE == AM_IM2COL ? p.cs % 8 == 0 : p.lda % 8 == 0) &&
+                    (AMODE != AM_SCALE || p.rows_per_img % BM == 0);
+    if (ok) {
+      if (ns == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      else gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      return;
+    }
+  }
   if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
   else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
 }

@@ -7,9 +7,10 @@ using namespace nbp;
 
 namespace {
 
-// NHWC kernels: a row (pixel) of C channels = G lanes x V chunks of 16 bytes (E = 8 bf16 / 4 fp32 elements);
-// each wave handles 2 x (64 / G) rows per iteration (two independent rows per lane group for load-level
-// parallelism).  The forward writes the affine output and per-row stats (mu, den = sqrt(var + eps)); the backward
+// NHWC kernels: a row (pixel) of C channels = C / E chunks of 16 bytes (E = 8 bf16 / 4 fp32 elements) spread over
+// G lanes x V chunks (G a power of two, G * V >= C / E: lanes past the last chunk hold zeros and store nothing, so any
+// multiple of E works); each wave handles 2 x (64 / G) rows per iteration (two independent rows per lane group for
+// load-level parallelism).  The forward writes the affine output and per-row stats (mu, den = sqrt(var + eps)); the backward
 // recomputes yhat = (x - mu) / den from the block input it keeps anyway, so yhat is never stored.
 template <typename T>
 __device__ __forceinline__ void ld_chunk(const T* p, float* f) {
@@ -37,19 +38,22 @@ __device__ __forceinline__ void st_chunk(T* p, const float* f) {
 template <int G, int V, typename T>
 __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, const float* __restrict__ w,
                                                    const float* __restrict__ b, T* __restrict__ nout,
-                                                   float2* __restrict__ stats, long M, float eps) {
-  constexpr int E = 16 / sizeof(T), C = G * V * E, RPW = 64 / G;
-  const int lane = threadIdx.x & 63, lg = lane % G;
+                                                   float2* __restrict__ stats, long M, int C, float eps) {
+  constexpr int E = 16 / sizeof(T), RPW = 64 / G;
+  const int lane = threadIdx.x & 63, lg = lane % G, nch = C / E;
   const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const long nwaves = (long)gridDim.x * (blockDim.x / 64);
+  bool cv[V];  // this lane's chunk j exists
   float wr[V][E], br[V][E];
 #pragma unroll
-  for (int j = 0; j < V; ++j)
+  for (int j = 0; j < V; ++j) {
+    cv[j] = j * G + lg < nch;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      wr[j][e] = w[(j * G + lg) * E + e];
-      br[j][e] = b[(j * G + lg) * E + e];
+      wr[j][e] = cv[j] ? w[(j * G + lg) * E + e] : 0.f;
+      br[j][e] = cv[j] ? b[(j * G + lg) * E + e] : 0.f;
     }
+  }
   for (long r0 = wave_global * 2 * RPW; r0 < M; r0 += nwaves * 2 * RPW) {
     long row[2];
     bool ok[2];
@@ -61,7 +65,7 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, cons
       ok[r] = row[r] < M;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        if (ok[r]) ld_chunk(x + row[r] * C + (j * G + lg) * E, v[r][j]);
+        if (ok[r] && cv[j]) ld_chunk(x + row[r] * C + (j * G + lg) * E, v[r][j]);
         else
 #pragma unroll
           for (int e = 0; e < E; ++e) v[r][j][e] = 0.f;
@@ -83,7 +87,7 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, cons
       for (int j = 0; j < V; ++j)
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          const float d = v[r][j][e] - mu[r];
+          const float d = cv[j] ? v[r][j][e] - mu[r] : 0.f;
           q[r] = fmaf(d, d, q[r]);
         }
     }
@@ -95,6 +99,7 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, cons
       const float dd = sqrtf(q[r] / (float)C + eps), inv = 1.f / dd;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
+        if (!cv[j]) continue;
         const int c = (j * G + lg) * E;
         float o[E];
 #pragma unroll
@@ -112,20 +117,24 @@ template <int G, int V, typename T>
 __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, const T* __restrict__ x,
                                                    const float2* __restrict__ stats, const float* __restrict__ w,
                                                    const T* __restrict__ dres, T* __restrict__ dx,
-                                                   float* __restrict__ slab_w, float* __restrict__ slab_b, long M) {
-  constexpr int E = 16 / sizeof(T), C = G * V * E, RPW = 64 / G;
-  __shared__ float red[4][2][C];
-  const int lane = threadIdx.x & 63, lg = lane % G, wv = threadIdx.x >> 6;
+                                                   float* __restrict__ slab_w, float* __restrict__ slab_b, long M,
+                                                   int C) {
+  constexpr int E = 16 / sizeof(T), RPW = 64 / G, CMAX = G * V * E;
+  __shared__ float red[4][2][CMAX];
+  const int lane = threadIdx.x & 63, lg = lane % G, wv = threadIdx.x >> 6, nch = C / E;
   const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + wv;
   const long nwaves = (long)gridDim.x * (blockDim.x / 64);
+  bool cv[V];
   float aw[V][E], ab[V][E], wr[V][E];
 #pragma unroll
-  for (int j = 0; j < V; ++j)
+  for (int j = 0; j < V; ++j) {
+    cv[j] = j * G + lg < nch;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       aw[j][e] = ab[j][e] = 0.f;
-      wr[j][e] = w[(j * G + lg) * E + e];
+      wr[j][e] = cv[j] ? w[(j * G + lg) * E + e] : 0.f;
     }
+  }
   for (long r0 = wave_global * 2 * RPW; r0 < M; r0 += nwaves * 2 * RPW) {
     long row[2];
     bool ok[2];
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const int c = (j * G + lg) * E;
-        if (ok[r]) {
+        if (ok[r] && cv[j]) {
           ld_chunk(dn + row[r] * C + c, d[r][j]);
           ld_chunk(x + row[r] * C + c, yh[r][j]);
         } else {
@@ -156,7 +165,7 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
       for (int j = 0; j < V; ++j) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          const float y = ok[r] ? (yh[r][j][e] - st[r].x) * rinv[r] : 0.f;
+          const float y = ok[r] && cv[j] ? (yh[r][j][e] - st[r].x) * rinv[r] : 0.f;
           yh[r][j][e] = y;
           const float g = d[r][j][e] * wr[j][e];
           sg[r] += g;
@@ -175,6 +184,7 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
       const float mg = sg[r] / (float)C, mgy = sgy[r] / (float)C, inv = rinv[r];
 #pragma unroll
       for (int j = 0; j < V; ++j) {
+        if (!cv[j]) continue;
         const int c = (j * G + lg) * E;
         float o[E], rr[E];
         if (dres) ld_chunk(dres + row[r] * C + c, rr);
@@ -197,7 +207,7 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
         aw[j][e] += __shfl_xor(aw[j][e], o, 64);
         ab[j][e] += __shfl_xor(ab[j][e], o, 64);
       }
-      if (lane < G) {
+      if (lane < G && cv[j]) {
         red[wv][0][(j * G + lg) * E + e] = aw[j][e];
         red[wv][1][(j * G + lg) * E + e] = ab[j][e];
       }
@@ -281,18 +291,23 @@ __global__ void ln_wb_nchw(const float* __restrict__ dy, const float* __restrict
   }
 }
 
+int ln_lanes(int chunks) {  // G: the power of two >= the chunk count, at most 64
+  int G = 1;
+  while (G < chunks && G < 64) G <<= 1;
+  return G;
+}
+
 int ln_grid(long M, int C, int dtype) {
-  const int chunks = C / (dtype != 0 ? 8 : 4);
-  const int G = chunks >= 64 ? 64 : chunks;
+  const int G = ln_lanes(C / (dtype != 0 ? 8 : 4));
   const long rows_per_block = 4L * 2 * (64 / G);
   long g = (M + rows_per_block - 1) / rows_per_block;
   if (g > 1024) g = 1024;
   return (int)(g < 1 ? 1 : g);
 }
 
-// (G, V) from the chunk count: G = min(64, C / E), V = C / E / G
+// (G, V) from the chunk count n = C / E: G = the power of two >= n (at most 64), V = ceil(n / 64) in {1, 2, 4}
 #define NBP_LN_DISPATCH(KERNEL, ...)                                                          \
-  switch (C / E) {                                                                            \
+  switch (C / E <= 64 ? ln_lanes(C / E) : (C / E <= 128 ? 128 : 256)) {                       \
     case 1: KERNEL<1, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
     case 2: KERNEL<2, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
     case 4: KERNEL<4, 1, T><<<g, 256, 0, st>>>(__VA_ARGS__); break;                           \
@@ -314,12 +329,12 @@ int nbp_ln_fwd_nhwc(const void* x, const float* w, const float* b, void* nout, f
                     int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && b && nout && stats && M > 0, "nbp_ln_fwd_nhwc: bad args");
   const int E = dtype != 0 ? 8 : 4;
-  NBP_REQUIRE(C >= E && C / E <= 256 && (C & (C - 1)) == 0, "nbp_ln_fwd_nhwc: C must be a power of two in [%d, %d]",
+  NBP_REQUIRE(C >= E && C / E <= 256 && C % E == 0, "nbp_ln_fwd_nhwc: C must be a multiple of %d in [%d, %d]", E,
               E, 256 * E);
   const int g = ln_grid(M, C, dtype);
   hipStream_t st = S(s);
   NBP_DISPATCH_T(dtype, {
-    NBP_LN_DISPATCH(ln_fwd_nhwc, (const T*)x, w, b, (T*)nout, reinterpret_cast<float2*>(stats), M, eps);
+    NBP_LN_DISPATCH(ln_fwd_nhwc, (const T*)x, w, b, (T*)nout, reinterpret_cast<float2*>(stats), M, C, eps);
   });
   return check_launch("ln_fwd_nhwc");
 }
@@ -329,13 +344,13 @@ int nbp_ln_bwd_nhwc(const void* dn, const void* x, const float* stats, const flo
                     float* slab_w, float* slab_b, long M, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dn && x && stats && w && dx && slab_w && slab_b && M > 0, "nbp_ln_bwd_nhwc: bad args");
   const int E = dtype != 0 ? 8 : 4;
-  NBP_REQUIRE(C >= E && C / E <= 256 && (C & (C - 1)) == 0, "nbp_ln_bwd_nhwc: C must be a power of two in [%d, %d]",
+  NBP_REQUIRE(C >= E && C / E <= 256 && C % E == 0, "nbp_ln_bwd_nhwc: C must be a multiple of %d in [%d, %d]", E,
               E, 256 * E);
   const int g = ln_grid(M, C, dtype);
   hipStream_t st = S(s);
   NBP_DISPATCH_T(dtype, {
     NBP_LN_DISPATCH(ln_bwd_nhwc, (const T*)dn, (const T*)x, reinterpret_cast<const float2*>(stats), w, (const T*)dres,
-                    (T*)dx, slab_w, slab_b, M);
+                    (T*)dx, slab_w, slab_b, M, C);
   });
   return check_launch("ln_bwd_nhwc");
 }

@@ -74,8 +74,9 @@ class NAFNet(nn.Module):
 
     def __init__(self, img_channel=3, width=16, middle_blk_num=1, enc_blk_nums=[], dec_blk_nums=[]):  # noqa: B006
         super().__init__()
-        if width % 8 or width & (width - 1):
-            raise ValueError("the MI355X NAFNet needs a power-of-two width >= 8 (channel-quad vector kernels)")
+        if width < 4 or width % 4:
+            raise ValueError("the MI355X NAFNet needs a width that is a multiple of 4 (16-byte channel vectors; the "
+                             "16-bit precision modes need a multiple of 8)")
         if len(dec_blk_nums) != len(enc_blk_nums):
             raise ValueError("enc_blk_nums and dec_blk_nums must have the same length (U-Net skips)")
         if img_channel > 4:
@@ -225,7 +226,11 @@ class NAFNet(nn.Module):
     @property
     def dt(self) -> int:
         """dtype code of the C-ABI: 0 fp32, 1 bf16, 2 fp16"""
-        return {"fp32": 0, "bf16": 1, "fp16": 2}[self.precision]
+        d = {"fp32": 0, "bf16": 1, "fp16": 2}[self.precision]
+        if d and self.width % 8:
+            raise ValueError(f"precision {self.precision!r} needs a width that is a multiple of 8 (16-byte vectors of "
+                             f"16-bit channels); width {self.width} runs in the fp32 mode")
+        return d
 
     def _mm(self, W, A, lda, amode, ascale, rows, wkey, C, ldc, cmode, M, N, K, gh=0, gw=0, cs=0, bias=None,
             R=None, rscale=None, pre=None, dgrad=False):

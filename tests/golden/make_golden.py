@@ -304,6 +304,17 @@ def gen_cfg_nets(R):
     _net_case(R, "nafnet_w64.npz", CFG4, 301, 2, 64, 64, "rgb", "B2", full=False)
 
 
+def gen_widths(R):
+    """Widths that are not powers of two (the reference accepts any width, NAFNet_arch.py:85-118): w24 / w40 (multiples
+    of 8: every precision mode) and w20 (a multiple of 4: the fp32 mode), small U-Nets, full per-tensor gradients."""
+    _net_case(R, "nafnet_w24.npz", dict(width=24, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]), 400, 2,
+              48, 40, "rgb", "B2")
+    _net_case(R, "nafnet_w40.npz", dict(width=40, enc_blk_nums=[1, 1, 1], middle_blk_num=2, dec_blk_nums=[1, 1, 1]),
+              401, 2, 64, 48, "mono", "P2", full=False)
+    _net_case(R, "nafnet_w20.npz", dict(width=20, enc_blk_nums=[1], middle_blk_num=1, dec_blk_nums=[1]), 402, 2, 32, 24,
+              "rgb", "B2")
+
+
 def gen_cfg5(R):
     """BASELINE configs[4]: phys_cons_raw with expo_ratio in {100, 250, 300} at 8 x 3 x 1024^2 (per-GPU slice of bs 32
     over 4 GPUs) + psnr_linear / ssim_linear at data_range 4095 on the unnormalised scale; fp16 inputs too (the metric
@@ -414,7 +425,7 @@ def main():
     R = load_reference(args.ref)
     R.ref = args.ref
     gens = dict(psf=gen_psf, phys_srgb=gen_phys_srgb, phys_cons=gen_phys_cons, layernorm=gen_layernorm,
-                nafblock=gen_nafblock, nets=gen_nets, cfg_nets=gen_cfg_nets, cfg5=gen_cfg5,
+                nafblock=gen_nafblock, nets=gen_nets, cfg_nets=gen_cfg_nets, widths=gen_widths, cfg5=gen_cfg5,
                 train_steps=gen_train_steps, color=gen_color, linear=gen_linear)
     for name, fn in gens.items():
         if not args.only or name in args.only.split(","):

@@ -1,0 +1,159 @@
+"""The LDS-DMA (global_load_lds) tiled GEMM against the register-staged tiled GEMM: same tiles, same fragment order and
+MFMA sequence, so every output must be bitwise identical (NBP_GLDS=0 selects the register-staged kernel, 2 / 3 the
+DMA ring depth; the knob is read per launch).  Covers every A mode the DMA path serves (plain, per-image scale,
+space-to-depth gather, 3x3 im2col with zero padding), the C modes of the deep-level GEMMs, ragged M / N, a K tail
+(K % 64 != 0), both 16-bit types, and the fused-LayerNorm entries.  Accuracy against float64 is covered by the
+existing GEMM tests, which run on the DMA path by default."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def run_modes(fn):
+    outs = {}
+    old = os.environ.get("NBP_GLDS")
+    try:
+        for ns in ("0", "2", "3"):
+            os.environ["NBP_GLDS"] = ns
+            outs[ns] = [t.clone() for t in fn()]
+            torch.cuda.synchronize()
+    finally:
+        if old is None:
+            os.environ.pop("NBP_GLDS", None)
+        else:
+            os.environ["NBP_GLDS"] = old
+    for ns in ("2", "3"):
+        for a, b in zip(outs["0"], outs[ns]):
+            assert torch.equal(a, b), f"NBP_GLDS={ns} differs from the register-staged kernel"
+
+
+DT = {1: torch.bfloat16, 2: torch.float16}
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 512), (4136, 1000, 520), (16384, 256, 256), (100, 136, 72),
+                                   (4096, 512, 1024)])
+def test_glds_plain_bias_residual(dev, dt, M, N, K):
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M + N + K + dt)
+    A = torch.randn(M, K, device=dev, generator=gen).to(DT[dt])
+    W = (torch.randn(N, K, device=dev, generator=gen) / K ** 0.5).to(DT[dt])
+    bias, sc = torch.randn(N, device=dev, generator=gen), torch.randn(N, device=dev, generator=gen)
+    R = torch.randn(M, N, device=dev, generator=gen).to(DT[dt])
+    C0, C1 = torch.empty(M, N, device=dev, dtype=DT[dt]), torch.empty(M, N, device=dev)
+
+    def fn():
+        call("gemm_bf16", A, K, 0, None, 1, dt, W, K, C0, N, 0, dt, M, N, K, 0, 0, 0, bias, R, sc, None)
+        call("gemm_bf16", A, K, 0, None, 1, dt, W, K, C1, N, 0, 0, M, N, K, 0, 0, 0, None, None, None, None)
+        return C0, C1
+    run_modes(fn)
+    ref = A.double() @ W.double().t()
+    assert (C1.double() - ref).abs().max().item() < 1e-3 * K ** 0.5
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("M,C,rows", [(4096, 512, 256), (16384, 256, 1024), (2048, 128, 128)])
+def test_glds_scale_simplegate(dev, dt, M, C, rows):
+    """conv4 with the SimpleGate epilogue and the SCA-scaled conv3 / conv5 dgrad with the SimpleGate adjoint."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(M + C + dt)
+    A = torch.randn(M, C, device=dev, generator=gen).to(DT[dt])
+    W = (torch.randn(2 * C, C, device=dev, generator=gen) / C ** 0.5).to(DT[dt])
+    b = torch.randn(2 * C, device=dev, generator=gen)
+    scale = torch.rand(M // rows, C, device=dev, generator=gen) + 0.5
+    Wd = (torch.randn(C, C, device=dev, generator=gen) / C ** 0.5).to(DT[dt])
+    t, g = torch.empty(M, 2 * C, device=dev, dtype=DT[dt]), torch.empty(M, C, device=dev, dtype=DT[dt])
+    dtt, y = torch.empty(M, 2 * C, device=dev, dtype=DT[dt]), torch.empty(M, C, device=dev, dtype=DT[dt])
+
+    def fn():
+        call("gemm_bf16", A, C, 0, None, 1, dt, W, C, t, 2 * C, 4, dt, M, 2 * C, C, 0, 0, 0, b, None, None, g)
+        call("gemm_bf16", A, C, 2, scale, rows, dt, Wd, C, dtt, 2 * C, 5, dt, M, C, C, 0, 0, 0, None, t, None, None)
+        call("gemm_bf16", A, C, 2, scale, rows, dt, Wd, C, y, C, 0, dt, M, C, C, 0, 0, 0, b[:C].contiguous(), None,
+             None, None)
+        return t, g, dtt, y
+    run_modes(fn)
+
+
+@pytest.mark.parametrize("B,gh,gw,cs", [(16, 16, 16, 256), (2, 32, 24, 64), (3, 5, 7, 128)])
+def test_glds_space_to_depth(dev, B, gh, gw, cs):
+    """down conv (2x2 / stride 2 as a space-to-depth GEMM, K = 4 cs) and the up conv's depth-to-space epilogue."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(B * gh + cs)
+    x = torch.randn(B, 2 * gh, 2 * gw, cs, device=dev, generator=gen).to(torch.bfloat16)
+    M, K, N = B * gh * gw, 4 * cs, 2 * cs
+    W = (torch.randn(N, K, device=dev, generator=gen) / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev, generator=gen)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    Wu = (torch.randn(4 * cs, N, device=dev, generator=gen) / N ** 0.5).to(torch.bfloat16)
+    up = torch.empty(B, 2 * gh, 2 * gw, cs, device=dev, dtype=torch.bfloat16)
+
+    def fn():
+        call("gemm_bf16", x, K, 1, None, 1, 1, W, K, y, N, 0, 1, M, N, K, gh, gw, cs, bias, None, None, None)
+        call("gemm_bf16", y, N, 0, None, 1, 1, Wu, N, up, N, 1, 1, M, 4 * cs, N, gh, gw, cs, None, None, None, None)
+        return y, up
+    run_modes(fn)
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(1, 64, 64, 64, 128), (2, 17, 23, 128, 64), (1, 32, 32, 256, 256)])
+def test_glds_conv3x3(dev, B, H, W, Cin, Cout):
+    """VGG 3x3 convolution (implicit GEMM, zero padding read from the zero page): bias + ReLU and the ReLU-mask form."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(B * H + Cin)
+    x = torch.randn(B, H, W, Cin, device=dev, generator=gen).to(torch.bfloat16)
+    w = (torch.randn(Cout, 9 * Cin, device=dev, generator=gen) / (9 * Cin) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, device=dev, generator=gen)
+    y, ym = (torch.empty(B, H, W, Cout, device=dev, dtype=torch.bfloat16) for _ in range(2))
+
+    def fn():
+        call("conv3x3_bf16", x, B, H, W, Cin, w, Cout, b, 0, None, y, 1, 1)
+        call("conv3x3_bf16", x, B, H, W, Cin, w, Cout, None, 2, y, ym, 1, 1)
+        return y, ym
+    run_modes(fn)
+
+
+@pytest.mark.parametrize("M,N,K,amode", [(4096, 256, 256, 2), (16384, 128, 256, 0), (333, 256, 512, 0)])
+def test_glds_fused_layernorm(dev, M, N, K, amode):
+    """conv3 / conv5 with the LayerNorm forward in the epilogue, and the conv1 / conv4 dgrad with the LN backward."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(M + N + K)
+    rows = 256 if amode == 2 else M
+    A = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=gen) / K ** 0.5).to(torch.bfloat16)
+    scale = torch.rand(M // rows, K, device=dev, generator=gen) + 0.5 if amode == 2 else None
+    bias, rs = torch.randn(N, device=dev, generator=gen), torch.randn(N, device=dev, generator=gen)
+    R = torch.randn(M, N, device=dev, generator=gen).to(torch.bfloat16)
+    lnw, lnb = torch.randn(N, device=dev, generator=gen), torch.randn(N, device=dev, generator=gen)
+    y, n, st = (torch.empty(M, N, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev,
+                dtype=torch.bfloat16), torch.empty(M, 2, device=dev))
+    Wt = (torch.randn(N, K, device=dev, generator=gen) / K ** 0.5).to(torch.bfloat16)
+    dres = torch.randn(M, N, device=dev, generator=gen).to(torch.bfloat16)
+    dx, dlnw, dlnb = torch.empty(M, N, device=dev, dtype=torch.bfloat16), torch.empty(N, device=dev), torch.empty(
+        N, device=dev)
+    n_ws = query("dgrad_ln_workspace_floats", M, N)
+    ws = torch.empty(n_ws, device=dev)
+
+    def fn():
+        call("gemm_res_ln", A, K, amode, scale, rows, W, K, y, M, N, K, bias, R, rs, lnw, lnb, n, st, 1e-6, 1)
+        call("dgrad_ln_bwd", A, K, Wt, K, M, N, K, y, st, lnw, dres, dx, dlnw, dlnb, ws, n_ws, 1)
+        return y, n, st, dx, dlnw, dlnb
+    run_modes(fn)
+
+
+@pytest.mark.parametrize("B,HW,C", [(16, 256, 512), (3, 1024, 256)])
+def test_glds_chandot(dev, B, HW, C):
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(B * HW + C)
+    M = B * HW
+    A = torch.randn(M, C, device=dev, generator=gen).to(torch.bfloat16)
+    Wt = (torch.randn(C, C, device=dev, generator=gen) / C ** 0.5).to(torch.bfloat16)
+    g = torch.randn(M, C, device=dev, generator=gen).to(torch.bfloat16)
+    d = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+    slab = torch.empty(B * (HW // 64) * C, device=dev)
+
+    def fn():
+        call("gemm_bf16", A, C, 0, None, HW, 1, Wt, C, d, C, 8, 1, M, C, C, 0, 0, 0, None, g, None, slab)
+        return d, slab
+    run_modes(fn)
