@@ -331,10 +331,18 @@ def main():
     _lib.PROFILE.clear()
     net._block_fwd, net._block_bwd = orig_fwd, orig_bwd
 
-    use_graph = world == 1 and not args.eager
+    # graph replay at every world size (N > 1: segments cut at the gradient buckets, all-reduces between them); a
+    # rank whose capture fails falls back to eager steps, which issue the same collective sequence
+    use_graph = not args.eager
     run = tr.graph_step if use_graph else tr.step
     if use_graph:
-        run(lq, gt, short, ratio)  # capture + one replay, untimed
+        try:
+            run(lq, gt, short, ratio)  # capture + one replay, untimed
+        except Exception as e:  # noqa: BLE001
+            print(f"[bench] rank {rank}: graph capture failed ({type(e).__name__}: {e}); eager steps", file=sys.stderr)
+            tr._graph = None
+            use_graph, run = False, tr.step
+            torch.cuda.synchronize()
         run(lq, gt, short, ratio)
 
     # timed region: exactly K steps between barriers + device syncs

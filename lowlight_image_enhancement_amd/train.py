@@ -106,6 +106,7 @@ class NBPTrainer:
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.bucket_elems = int(bucket_mb * 1024 * 1024 / 4)
         self._handles: List = []
+        self._cap: Optional[dict] = None  # segment capture state of the data-parallel graph step
         self._pending_lo: Optional[int] = None
         self._pending_hi = 0
         if self.world > 1:
@@ -122,10 +123,22 @@ class NBPTrainer:
     def _flush(self):
         if self._pending_lo is None or self._pending_hi <= self._pending_lo:
             return
-        h = dist.all_reduce(self.grad[self._pending_lo:self._pending_hi], op=dist.ReduceOp.SUM, group=self.pg,
-                            async_op=True)
-        self._handles.append(h)
+        lo, hi = self._pending_lo, self._pending_hi
         self._pending_lo = None
+        if self._cap is not None:  # capturing graph segments: cut here; the replay all-reduces between segments
+            self._cut_segment((lo, hi))
+            return
+        h = dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        self._handles.append(h)
+
+    def _cut_segment(self, bucket):
+        """End the graph segment being captured (its last kernels complete `bucket`'s gradient slice) and begin the
+        next one in the same memory pool."""
+        cap = self._cap
+        cap["g"].capture_end()
+        cap["segs"].append((cap["g"], bucket))
+        cap["g"] = torch.cuda.CUDAGraph()
+        cap["g"].capture_begin(pool=cap["pool"], capture_error_mode=cap["mode"])
 
     # ------------------------------------------------------------------ the step
     def loss_and_grad(self, lq, gt, short=None, expo_ratio=None):
@@ -176,9 +189,10 @@ class NBPTrainer:
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
         if self.world > 1:
             self._flush()
-            for h in self._handles:
-                h.wait()
-            self._handles.clear()
+            if self._cap is None:
+                for h in self._handles:
+                    h.wait()
+                self._handles.clear()
         return out
 
     def _ensure_up(self, B: int):
@@ -224,14 +238,17 @@ class NBPTrainer:
         self._optimizer(1.0 / self.world)
         return out
 
-    # ------------------------------------------------------------------ HIP-graph step (single process)
+    # ------------------------------------------------------------------ HIP-graph step
     def graph_step(self, lq, gt, short=None, expo_ratio=None):
-        """One training step replayed from a captured HIP graph: every kernel of step() (forward, loss head,
+        """One training step replayed from captured HIP graphs: every kernel of step() (forward, loss head,
         backward with its deferred reductions, clip, AdamW) recorded once and relaunched with no host work but the
         input copies and the lr upload.  Numerically identical to step().  The first call captures with these
-        tensors' shapes; later calls copy their inputs into the captured buffers."""
-        if self.world > 1:
-            raise RuntimeError("graph_step is single-process; use step() with torch.distributed")
+        tensors' shapes; later calls copy their inputs into the captured buffers.
+
+        Data parallel (world > 1): the step is captured as a chain of graph segments cut where the backward completes
+        a gradient bucket; the replay launches each segment and then that bucket's asynchronous all-reduce (eager
+        RCCL, outside any graph, so the collective overlaps the next segment exactly as in step()), waits for the
+        buckets, and replays the clip + AdamW graph."""
         ins = (lq, gt, short, expo_ratio)
         if getattr(self, "_graph", None) is None:
             self._capture(ins)
@@ -252,13 +269,25 @@ class NBPTrainer:
         ev = torch.cuda.Event()
         ev.record()
         self._lr_ev[slot] = ev
-        self._graph.replay()
+        if self.world == 1:
+            self._graph.replay()
+            return self._graph_out
+        for g, bucket in self._segs:
+            g.replay()
+            if bucket is not None:
+                lo, hi = bucket
+                self._handles.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg,
+                                                     async_op=True))
+        for hd in self._handles:
+            hd.wait()
+        self._handles.clear()
+        self._graph.replay()  # clip (with the 1/world average) + AdamW
         return self._graph_out
 
     def _graph_body(self):
         lq, gt, short, ratio = self._static
         out = self.loss_and_grad(lq, gt, short, ratio)
-        self._optimizer(1.0)
+        self._optimizer(1.0 / self.world)
         return out
 
     def _capture(self, ins):
@@ -278,9 +307,49 @@ class NBPTrainer:
         torch.cuda.current_stream().wait_stream(side)
         for dst, src in zip(state, saved):
             dst.copy_(src)
-        self._graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._graph):
-            self._graph_out = self._graph_body()
+        if self.world == 1:
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._graph_out = self._graph_body()
+            return
+        # data parallel: segments of fwd + bwd cut at every bucket flush (no collective inside any graph), then the
+        # optimizer graph, all in one private memory pool and captured on one side stream
+        torch.cuda.synchronize()
+        pool = torch.cuda.graph_pool_handle()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        # thread-local capture mode: the process group's watchdog thread may query events meanwhile
+        mode = "thread_local"
+        with torch.cuda.stream(cs):
+            self._cap = {"pool": pool, "segs": [], "g": torch.cuda.CUDAGraph(), "mode": mode}
+            live = False
+            try:
+                self._cap["g"].capture_begin(pool=pool, capture_error_mode=mode)
+                live = True
+                lq, gt, short, ratio = self._static
+                out = self.loss_and_grad(lq, gt, short, ratio)
+                live = False
+                self._cap["g"].capture_end()
+                self._cap["segs"].append((self._cap["g"], None))
+                segs = self._cap["segs"]
+                opt = torch.cuda.CUDAGraph()
+                opt.capture_begin(pool=pool, capture_error_mode=mode)
+                live = True
+                self._optimizer(1.0 / self.world)
+                live = False
+                opt.capture_end()
+            except BaseException:
+                if live:  # leave the stream out of capture mode before re-raising
+                    try:
+                        (opt if "opt" in locals() else self._cap["g"]).capture_end()
+                    except Exception:  # noqa: BLE001
+                        pass
+                raise
+            finally:
+                self._cap = None
+        torch.cuda.current_stream().wait_stream(cs)
+        torch.cuda.synchronize()
+        self._segs, self._graph, self._graph_out = segs, opt, out
 
     def logs(self, reduce: bool = True) -> Dict[str, float]:
         """Loss dict of the last step (host sync), averaged over ranks like reduce_loss_dict (base_model.py:335-360)."""

@@ -84,3 +84,49 @@ def test_two_ranks_different_batches_equal_one_process_on_the_concatenation():
         assert np.abs(p - pref)[well].max() < 5e-6, rank
         assert abs(logs["Total"] - lref["Total"]) <= 1e-5 * lref["Total"], rank
     assert np.array_equal(res[0][2], res[1][2])  # replicas stay identical
+
+
+def _graph_worker(rank, world, port, q):
+    """Per rank: 3 eager steps on one trainer and 3 graph_steps (segmented capture, all-reduces between the
+    replayed segments) on a second trainer with the same initial state and the same rank-seeded batches."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        res = []
+        for use_graph in (False, True):
+            tr = _trainer()
+            fn = tr.graph_step if use_graph else tr.step
+            for s in range(3):
+                lq, gt = _batch(rank + 10 * s)
+                fn(lq, gt, lq.clamp(0, 1), torch.ones(lq.shape[0], 1, 1, 1, device="cuda"))
+            torch.cuda.synchronize()
+            res.append((tr.net.flat.detach().cpu().numpy().copy(), tr.grad.cpu().numpy().copy(), tr.logs()["Total"],
+                        len(getattr(tr, "_segs", []) or [])))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_graph_step_equals_eager_step():
+    """The data-parallel HIP-graph step (segments cut at the gradient buckets, bucket all-reduces launched between
+    the replays) gives bitwise the parameters, gradients and losses of the eager data-parallel step."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_graph_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ((p_e, g_e, l_e, _), (p_g, g_g, l_g, nseg)) in res:
+        assert nseg > 2, nseg  # several buckets -> several segments
+        assert np.array_equal(p_e, p_g), rank
+        assert np.array_equal(g_e, g_g), rank
+        assert l_e == l_g, rank
+    assert np.array_equal(res[0][1][1][0], res[1][1][1][0])  # replicas identical
