@@ -57,7 +57,7 @@ FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
 MFMA16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA peak
 HBM_PEAK_GBPS = 8000.0
 ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
-ROCPROF_KERNELS = {"gemm16": ["gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
+ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
                    "wgrad": ["wgrad_bf16_kernel", "wgrad_bf16_wide", "wgrad_f32_kernel"],
                    "dw_bwd": ["dw_bwd_tiled"], "dw_fwd": ["dw_sg_pool_tiled"]}
 

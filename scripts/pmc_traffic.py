@@ -13,11 +13,18 @@ import collections
 import csv
 import json
 import os
+import re
 import sys
 
-CLASSES = {"gemm16": ("gemm_bf16_kernel", "gemm_skinny_kernel"), "wgrad": ("wgrad_",), "gemm_f32": ("gemm_f32_kernel",),
+CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"), "wgrad": ("wgrad_",), "gemm_f32": ("gemm_f32_kernel",),
            "dw_bwd": ("dw_bwd_tiled",), "dw_fwd": ("dw_sg_pool_tiled",), "ln_fwd": ("ln_fwd_nhwc",),
-           "ln_bwd": ("ln_bwd_nhwc",)}
+           "ln_bwd": ("ln_bwd_nhwc",),
+           # VGG / AlexNet implicit-GEMM convs (cfg3's perceptual + LPIPS trunks): the tiled kernels with A mode 3 / 4
+           "vgg_conv": (re.compile(r"gemm_(glds|bf16)_kernelILi\d+ELi\d+ELi\d+ELi[34]E"),)}
+
+
+def _match(name, pats):
+    return any(p.search(name) if hasattr(p, "search") else p in name for p in pats)
 SIMDS = 256 * 4
 
 
@@ -48,7 +55,7 @@ def main(fetch_dir, write_dir, mfma_dir, out):
                      "mfma_flops = MOPS * 512",
            "classes": {}}
     for cls, pats in CLASSES.items():
-        names = [k for k in f if any(p in k for p in pats)]
+        names = [k for k in f if _match(k, pats)]
         n = sum(len(f[k]) for k in names)
         if not n:
             continue
@@ -56,7 +63,7 @@ def main(fetch_dir, write_dir, mfma_dir, out):
         write = sum(sum(w.get(k, [])) for k in names) * 1024.0
         rec = {"launches": n, "fetch_size_bytes_raw": fetch / n, "write_bytes": write / n,
                "traffic_bytes_per_launch": (2 * fetch + write) / n}
-        mn = [k for k in mb if any(p in k for p in pats)]
+        mn = [k for k in mb if _match(k, pats)]
         if mn:
             busy = sum(v for k in mn for v, _ in mb[k])
             ns = sum(t for k in mn for _, t in mb[k])

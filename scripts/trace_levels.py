@@ -4,7 +4,7 @@
 
 A step is the window from an `intro_fwd` launch to the next `adamw` launch; the last complete window is used (the
 bench's timed HIP-graph replays come last).  The window is cut into segments at the U-Net level changes: the
-down/up GEMMs (space-to-depth A-mode 1 / depth-to-space C-mode 1 of gemm_bf16_kernel, in both directions).  For
+down/up GEMMs (space-to-depth A-mode 1 / depth-to-space C-mode 1 of the tiled GEMM kernels, in both directions).  For
 each segment: launches, busy time (sum of kernel durations), span (wall) and the gap share, plus its top kernels.
 """
 import collections
@@ -22,7 +22,7 @@ def short(n):
 
 
 def is_level_cut(name):
-    if "gemm_bf16_kernel" not in name and "gemm_f32_kernel" not in name:
+    if "gemm_bf16_kernel" not in name and "gemm_glds_kernel" not in name and "gemm_f32_kernel" not in name:
         return False
     a = [int(v) for v in re.findall(r"Li(\d+)E", name)]
     return len(a) >= 5 and (a[3] == 1 or a[4] == 1)
