@@ -166,36 +166,69 @@ __global__ __launch_bounds__(256) void add_relu_masked_kernel(HT* __restrict__ d
 // ---------------------------------------------------------------- LPIPS tap distance (lpips 0.1.4, net='vgg')
 // per pixel: u = a / (|a| + 1e-10), v = b / (|b| + 1e-10) over the C channels (normalize_tensor),
 // d = sum_c w_c (u_c - v_c)^2 (the 1x1 'lin' head); per image out[n] (+)= mean over pixels (spatial_average).
-template <typename HT>
+// LPIPS tap (lpips 0.1.4 pretrained_networks / lpips.py: normalize_tensor over channels, (u - v)^2, 1x1 `lin` conv,
+// spatial mean): a pixel's C channels are C / 8 chunks of 16 bytes spread over a group of G lanes (G a power of two,
+// V chunks per lane; lanes past the last chunk masked), so every load is a coalesced row piece and the feature
+// vectors are read from HBM once (kept in registers between the norm pass and the distance / gradient pass);
+// channel sums are group shuffles.  Groups stride over the pixels.
+template <int G, int V, typename HT>
+struct TapRow {
+  vec_t<HT, 8> a[V], b[V];
+  bool ok[V];
+};
+
+template <int G, int V, typename HT>
+__device__ __forceinline__ void tap_load(TapRow<G, V, HT>& r, const HT* pa, const HT* pb, int lg, int nch) {
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int ch = j * G + lg;
+    r.ok[j] = ch < nch;
+    if (r.ok[j]) {
+      r.a[j] = *reinterpret_cast<const vec_t<HT, 8>*>(pa + ch * 8);
+      r.b[j] = *reinterpret_cast<const vec_t<HT, 8>*>(pb + ch * 8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r.a[j][e] = r.b[j][e] = (HT)0.f;
+    }
+  }
+}
+
+template <int G, int V, typename HT>
 __global__ __launch_bounds__(256) void lpips_tap_fwd(const HT* __restrict__ a, const HT* __restrict__ b,
                                                      const float* __restrict__ w, long HW, int C, int chunks,
                                                      double* __restrict__ slab) {
   __shared__ double red[16];
-  const int n = blockIdx.y;
+  constexpr int GPB = 256 / G;  // pixel groups per block
+  const int n = blockIdx.y, lg = threadIdx.x % G, grp = threadIdx.x / G, nch = C / 8;
   const long per = (HW + chunks - 1) / chunks, q0 = (long)blockIdx.x * per, q1 = min(HW, q0 + per);
-  double acc = 0.0;
-  for (long q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
-    const HT* pa = a + ((long)n * HW + q) * C;
-    const HT* pb = b + ((long)n * HW + q) * C;
-    float sa = 0.f, sb = 0.f;
-    for (int c = 0; c < C; c += 8) {
-      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
+  float wr[V][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sa = fmaf((float)va[j], (float)va[j], sa);
-        sb = fmaf((float)vb[j], (float)vb[j], sb);
+  for (int j = 0; j < V; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wr[j][e] = j * G + lg < nch ? w[(j * G + lg) * 8 + e] : 0.f;
+  double acc = 0.0;
+  for (long q = q0 + grp; q < q1; q += GPB) {
+    TapRow<G, V, HT> r;
+    tap_load<G, V, HT>(r, a + ((long)n * HW + q) * C, b + ((long)n * HW + q) * C, lg, nch);
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sa = fmaf((float)r.a[j][e], (float)r.a[j][e], sa);
+        sb = fmaf((float)r.b[j][e], (float)r.b[j][e], sb);
       }
-    }
+    sa = group_sum<G>(sa);
+    sb = group_sum<G>(sb);
     const float ia = 1.f / (sqrtf(sa) + 1e-10f), ib = 1.f / (sqrtf(sb) + 1e-10f);
     float d = 0.f;
-    for (int c = 0; c < C; c += 8) {
-      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float t = (float)va[j] * ia - (float)vb[j] * ib;
-        d = fmaf(w[c + j] * t, t, d);
+    for (int j = 0; j < V; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = (float)r.a[j][e] * ia - (float)r.b[j][e] * ib;
+        d = fmaf(wr[j][e] * t, t, d);
       }
-    }
     acc += (double)d;
   }
   const double t = block_sum_d(acc, red);
@@ -213,52 +246,63 @@ __global__ void lpips_finalize(const double* __restrict__ slab, int N, int chunk
 
 // d a_k = up[n] / HW * (g_k / na - a_k (sum_c g_c a_c) / (na^2 |a|)),  g_c = 2 w_c (u_c - v_c), na = |a| + 1e-10.
 // A pixel whose feature vector is all zero gets zero gradient (torch's sqrt backward yields NaN there).
-template <typename HT>
+template <int G, int V, typename HT>
 __global__ __launch_bounds__(256) void lpips_tap_bwd(const HT* __restrict__ a, const HT* __restrict__ b,
                                                      const float* __restrict__ w, long HW, int C, long npix,
                                                      const float* __restrict__ up, HT* __restrict__ da) {
-  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+  constexpr int GPB = 256 / G;
+  const int lg = threadIdx.x % G, grp = threadIdx.x / G, nch = C / 8;
+  float wr[V][8];
+#pragma unroll
+  for (int j = 0; j < V; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wr[j][e] = j * G + lg < nch ? 2.f * w[(j * G + lg) * 8 + e] : 0.f;
+  for (long p = (long)blockIdx.x * GPB + grp; p < npix; p += (long)gridDim.x * GPB) {
     const long n = p / HW;
-    const HT* pa = a + p * C;
-    const HT* pb = b + p * C;
+    TapRow<G, V, HT> r;
+    tap_load<G, V, HT>(r, a + p * C, b + p * C, lg, nch);
     HT* pd = da + p * C;
     float sa = 0.f, sb = 0.f;
-    for (int c = 0; c < C; c += 8) {
-      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sa = fmaf((float)va[j], (float)va[j], sa);
-        sb = fmaf((float)vb[j], (float)vb[j], sb);
+    for (int j = 0; j < V; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sa = fmaf((float)r.a[j][e], (float)r.a[j][e], sa);
+        sb = fmaf((float)r.b[j][e], (float)r.b[j][e], sb);
       }
-    }
+    sa = group_sum<G>(sa);
+    sb = group_sum<G>(sb);
     if (sa == 0.f) {
       vec_t<HT, 8> z;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = (HT)0.f;
-      for (int c = 0; c < C; c += 8) *reinterpret_cast<vec_t<HT, 8>*>(pd + c) = z;
+      for (int e = 0; e < 8; ++e) z[e] = (HT)0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        if (r.ok[j]) *reinterpret_cast<vec_t<HT, 8>*>(pd + (j * G + lg) * 8) = z;
       continue;
     }
     const float ra = sqrtf(sa), na = ra + 1e-10f, ia = 1.f / na, ib = 1.f / (sqrtf(sb) + 1e-10f);
-    float G = 0.f;
-    for (int c = 0; c < C; c += 8) {
-      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
+    float gs = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float av = (float)va[j];
-        G = fmaf(2.f * w[c + j] * (av * ia - (float)vb[j] * ib), av, G);
+    for (int j = 0; j < V; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float av = (float)r.a[j][e];
+        gs = fmaf(wr[j][e] * (av * ia - (float)r.b[j][e] * ib), av, gs);
       }
-    }
-    const float s = up[n] / (float)HW, k2 = G / (na * na * ra);
-    for (int c = 0; c < C; c += 8) {
-      const vec_t<HT, 8> va = *reinterpret_cast<const vec_t<HT, 8>*>(pa + c), vb = *reinterpret_cast<const vec_t<HT, 8>*>(pb + c);
+    gs = group_sum<G>(gs);
+    const float sc = up[n] / (float)HW, k2 = gs / (na * na * ra);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      if (!r.ok[j]) continue;
       vec_t<HT, 8> o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float av = (float)va[j];
-        const float g = 2.f * w[c + j] * (av * ia - (float)vb[j] * ib);
-        o[j] = (HT)(s * (g * ia - av * k2));
+      for (int e = 0; e < 8; ++e) {
+        const float av = (float)r.a[j][e];
+        const float g = wr[j][e] * (av * ia - (float)r.b[j][e] * ib);
+        o[e] = (HT)(sc * (g * ia - av * k2));
       }
-      *reinterpret_cast<vec_t<HT, 8>*>(pd + c) = o;
+      *reinterpret_cast<vec_t<HT, 8>*>(pd + (j * G + lg) * 8) = o;
     }
   }
 }
@@ -374,6 +418,25 @@ int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, int dt
   return check_launch("add_relu_masked");
 }
 
+// lanes per pixel group: the power of two >= the 16-byte chunk count, at most 64 (then V = ceil(chunks / 64) <= 4)
+inline int tap_lanes(int nch) {
+  int G = 1;
+  while (G < nch && G < 64) G <<= 1;
+  return G;
+}
+#define NBP_TAP_DISPATCH(KERNEL, GRID, ...)                                                   \
+  switch (C / 8 <= 64 ? tap_lanes(C / 8) : (C / 8 <= 128 ? 128 : 256)) {                    \
+    case 1: KERNEL<1, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                   \
+    case 2: KERNEL<2, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                   \
+    case 4: KERNEL<4, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                   \
+    case 8: KERNEL<8, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                   \
+    case 16: KERNEL<16, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                 \
+    case 32: KERNEL<32, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                 \
+    case 64: KERNEL<64, 1, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                 \
+    case 128: KERNEL<64, 2, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                \
+    default: KERNEL<64, 4, HT><<<GRID, 256, 0, S(s)>>>(__VA_ARGS__); break;                 \
+  }
+
 inline int lpips_chunks(long HW, int N) {
   long c = (HW + 2047) / 2048, want = (1024 + N - 1) / N;
   if (c > want) c = want;
@@ -384,20 +447,31 @@ size_t nbp_lpips_tap_workspace_doubles(int N, long HW) { return (size_t)N * lpip
 
 int nbp_lpips_tap_fwd(const void* a, const void* b, const float* w, int N, long HW, int C, int accumulate, double* ws,
                       float* out, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(a && b && w && ws && out && N > 0 && N <= 65535 && HW > 0 && C % 8 == 0, "nbp_lpips_tap_fwd: bad args");
+  NBP_REQUIRE(a && b && w && ws && out && N > 0 && N <= 65535 && HW > 0 && C % 8 == 0 && C <= 2048,
+              "nbp_lpips_tap_fwd: bad args");
   const int chunks = lpips_chunks(HW, N);
-  NBP_DISPATCH_16(dtype, HT, lpips_tap_fwd<HT><<<dim3(chunks, N), 256, 0, S(s)>>>(
-      reinterpret_cast<const HT*>(a), reinterpret_cast<const HT*>(b), w, HW, C, chunks, ws));
+  NBP_DISPATCH_16(dtype, HT, {
+    const HT* pa = reinterpret_cast<const HT*>(a);
+    const HT* pb = reinterpret_cast<const HT*>(b);
+    const dim3 g(chunks, N);
+    NBP_TAP_DISPATCH(lpips_tap_fwd, g, pa, pb, w, HW, C, chunks, ws);
+  });
   lpips_finalize<<<cdiv(N, 256), 256, 0, S(s)>>>(ws, N, chunks, 1.0 / (double)HW, accumulate, out);
   return check_launch("lpips_tap_fwd");
 }
 
 int nbp_lpips_tap_bwd(const void* a, const void* b, const float* w, int N, long HW, int C, const float* up, void* da,
                       int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(a && b && w && up && da && N > 0 && HW > 0 && C % 8 == 0, "nbp_lpips_tap_bwd: bad args");
+  NBP_REQUIRE(a && b && w && up && da && N > 0 && HW > 0 && C % 8 == 0 && C <= 2048, "nbp_lpips_tap_bwd: bad args");
   const long npix = (long)N * HW;
-  NBP_DISPATCH_16(dtype, HT, lpips_tap_bwd<HT><<<grid_for(npix), 256, 0, S(s)>>>(
-      reinterpret_cast<const HT*>(a), reinterpret_cast<const HT*>(b), w, HW, C, npix, up, reinterpret_cast<HT*>(da)));
+  NBP_DISPATCH_16(dtype, HT, {
+    const HT* pa = reinterpret_cast<const HT*>(a);
+    const HT* pb = reinterpret_cast<const HT*>(b);
+    const long gpb = 256 / tap_lanes(C / 8);
+    long g = (npix + gpb - 1) / gpb;
+    if (g > 8192) g = 8192;
+    NBP_TAP_DISPATCH(lpips_tap_bwd, (unsigned)g, pa, pb, w, HW, C, npix, up, reinterpret_cast<HT*>(da));
+  });
   return check_launch("lpips_tap_bwd");
 }
 
