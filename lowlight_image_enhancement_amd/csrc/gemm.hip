@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <vector>
 
+#include <algorithm>
+
 #include "nbp_common.h"
 
 using namespace nbp;
@@ -543,32 +545,283 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
   }
 }
 
+// The same 128 x 128 tile with the operand panels staged by LDS-DMA into an NS-deep ring (NS - 1 stages in flight
+// across the barriers, counted vmcnt, raw s_barrier): the register-staged tile above issues a stage's loads one stage
+// ahead and its in-order vmcnt waits expose their latency every stage.  Panel image: 64 rows x 128 columns of 256 B,
+// the 16-byte chunk c of row r at slot c ^ (4 (r & 3)) (permuted on the DMA source address), which keeps the
+// ds_read_b64_tr_b16 fragment reads (4 rows x 8 column pieces per 32-lane group) conflict-free.  The per-image SCA
+// scale of the stage's 128 X columns is DMA'd with the stage (a stage never straddles two images); the bias column
+// sums of G are read back from the panel.  Same MFMA sequence per tile as wgrad_wide_tile (the bias sums are added
+// in another order).
+template <int NS, int XMODE>
+constexpr int wide_glds_stage_bytes() { return 2 * 64 * 256 + (XMODE == AM_SCALE ? 512 : 0); }
+template <int NS>
+constexpr int wide_glds_lds_bytes() {
+  return NS * wide_glds_stage_bytes<NS, AM_SCALE>() > 16 * 128 * 4 ? NS * wide_glds_stage_bytes<NS, AM_SCALE>()
+                                                                   : 16 * 128 * 4;
+}
+
+// asm helpers of wgrad_wide_tile_glds: the 8 ds_read_b64_tr_b16 of one 16-row K step (rows KS + 4 t + lane part),
+// fragment order [t * 4 + {Gi0, Gi1, Xi0, Xi1}]; a counted lgkmcnt wait that also ties the fragments to it (so no
+// consumer is scheduled above the wait); and the step's 2 x 2 MFMAs.
+template <int KS>
+__device__ __forceinline__ void wide_tr_reads(s16x4 (&f)[8], unsigned g0, unsigned g1, unsigned x0, unsigned x1) {
+#define NBP_TR(dst, addr, off) asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "n"(off))
+  NBP_TR(f[0], g0, KS * 256);
+  NBP_TR(f[1], g1, KS * 256);
+  NBP_TR(f[2], x0, KS * 256);
+  NBP_TR(f[3], x1, KS * 256);
+  NBP_TR(f[4], g0, (KS + 4) * 256);
+  NBP_TR(f[5], g1, (KS + 4) * 256);
+  NBP_TR(f[6], x0, (KS + 4) * 256);
+  NBP_TR(f[7], x1, (KS + 4) * 256);
+#undef NBP_TR
+}
+template <int N>
+__device__ __forceinline__ void wide_tr_wait(s16x4 (&f)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7])
+               : "n"(N));
+}
+template <typename H>
+__device__ __forceinline__ void wide_mfma(const s16x4 (&f)[8], floatx16 (&acc)[2][2], bool bias, floatx16 (&accb)[2]) {
+  vec_t<H, 8> a[2], b[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const vec_t<H, 4> a0 = __builtin_bit_cast(vec_t<H, 4>, f[i]), a1 = __builtin_bit_cast(vec_t<H, 4>, f[4 + i]);
+    const vec_t<H, 4> b0 = __builtin_bit_cast(vec_t<H, 4>, f[2 + i]), b1 = __builtin_bit_cast(vec_t<H, 4>, f[6 + i]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[i][e] = a0[e];
+      a[i][4 + e] = a1[e];
+      b[i][e] = b0[e];
+      b[i][4 + e] = b1[e];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
+  if (bias) {  // column sums of G: the same A fragments against a ones B fragment (every output column = the sum)
+    vec_t<H, 8> ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (H)1.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) accb[i] = mfma32x32x16(a[i], ones, accb[i]);
+  }
+}
+
+template <int XMODE, typename H, int NS>
+__device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int by, int bz, unsigned char* smem) {
+  constexpr int RM = 64, PAN = RM * 256, ST = wide_glds_stage_bytes<NS, XMODE>();
+  constexpr int GL = 8 + (XMODE == AM_SCALE ? 2 : 0);  // DMA instructions per wave per stage
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  const H* G = reinterpret_cast<const H*>(p.G);
+  const H* X = reinterpret_cast<const H*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = bx * 128, k0 = by * 128, s = bz;
+  const int mb = s * p.chunk;
+  const int me = min(p.M, mb + p.chunk);
+  const bool do_b = p.slab_b && by == 0;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  constexpr int NT_ = XMODE == AM_SCALE ? 2 : 1;
+  floatx16 tot[NT_][NT_];
+#pragma unroll
+  for (int i = 0; i < NT_; ++i)
+#pragma unroll
+    for (int j = 0; j < NT_; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tot[i][j][r] = 0.f;
+  // DMA geometry: instruction j of this wave fills panel rows (4 wave + j) * 4 + lane / 16, physical slot lane % 16
+  int drow[4], dcol[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    drow[j] = (wave * 4 + j) * 4 + (lane >> 4);
+    dcol[j] = 8 * ((lane & 15) ^ (4 * (drow[j] & 3)));
+  }
+  const int nst = mb < me ? (me - mb + RM - 1) / RM : 0;
+  // the zero page's address in registers (laundered through asm: otherwise it is re-loaded from the GOT, with an
+  // lgkmcnt(0) wait, at every use inside the loop)
+  const void* zp = g_zero16;
+  asm volatile("" : "+s"(zp));
+  auto issue = [&](int t) {
+    unsigned char* st = smem + (t % NS) * ST;
+    const int m0 = mb + t * RM;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + drow[j];
+      glds16(m < me ? (const void*)(G + (long)m * p.ldg + n0 + dcol[j]) : zp, st + (wave * 4 + j) * 1024);
+      glds16(m < me ? (const void*)(X + (long)m * p.ldx + k0 + dcol[j]) : zp, st + PAN + (wave * 4 + j) * 1024);
+    }
+    if constexpr (XMODE == AM_SCALE) {  // every wave DMAs the same 128 scales of the stage's image
+      const float* sc = p.x_scale + (long)(m0 / p.rows_per_img) * p.K + k0;
+      glds4(sc + lane, st + 2 * PAN);
+      glds4(sc + 64 + lane, st + 2 * PAN + 256);
+    }
+  };
+  // fragment reads: lane (grp, q, pp, h) reads row ks + 8h + 4t + q, logical column (wave half) + 32 i + fcol; in the
+  // panel image that is byte row * 256 + 16 ((col / 8) ^ 4q) + 2 (col % 8).  The lane part is folded into four base
+  // addresses (G / X, i = 0 / 1); the rows ks + 4t are immediate offsets.
+  const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
+  const int lx = 2 * (grp & 1) + (pp >> 1);  // chunk within the 4-chunk (32-column) group
+  unsigned abase[2][2];                      // [G / X][i], relative to the stage
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    abase[0][i] = (8 * h + q) * 256 + ((4 * ((2 * wn + i) ^ q) + lx) << 4) + (pp & 1) * 8;
+    abase[1][i] = PAN + (8 * h + q) * 256 + ((4 * ((2 * wk + i) ^ q) + lx) << 4) + (pp & 1) * 8;
+  }
+  const unsigned smem_lds = (unsigned)(size_t)(lds_void_t*)smem;
+  float cur_sc[2] = {0.f, 0.f};
+  int cur_img = -1;
+  auto fold = [&]() {
+#pragma unroll
+    for (int j = 0; j < NT_; ++j)
+#pragma unroll
+      for (int i = 0; i < NT_; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          tot[i][j][r] = fmaf(acc[i][j][r], cur_sc[j], tot[i][j][r]);
+          acc[i][j][r] = 0.f;
+        }
+  };
+  // bias (column sums of G) on the MFMA pipe: waves wk == 0 of the by == 0 tiles
+  const bool wb = do_b && wk == 0;
+  floatx16 accb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nst) issue(t);
+  for (int t = 0; t < nst; ++t) {
+    // retire stage t: the stages issued after it (at most NS - 2) stay in flight
+    if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
+    else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + NS - 1 < nst) issue(t + NS - 1);
+    if constexpr (XMODE == AM_SCALE) {
+      const int im = (mb + t * RM) / p.rows_per_img;
+      if (im != cur_img) {
+        if (cur_img >= 0) fold();
+        cur_img = im;
+        // (asm LDS reads: a plain load here would make the compiler drain the DMA ring first)
+        const unsigned sa = smem_lds + (t % NS) * ST + 2 * PAN + (wk * 64 + (lane & 31)) * 4;
+        asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(cur_sc[0]), "=&v"(cur_sc[1])
+                     : "v"(sa));
+      }
+    }
+    // the 8 tr-reads of K step ks + 16 are in flight while step ks is multiplied (asm: a builtin tr-read would make
+    // the compiler drain the DMA ring, vmcnt(0), before it)
+    const unsigned sb = smem_lds + (t % NS) * ST;
+    const unsigned ga0 = sb + abase[0][0], ga1 = sb + abase[0][1], xa0 = sb + abase[1][0], xa1 = sb + abase[1][1];
+    s16x4 fr[2][8];
+    wide_tr_reads<0>(fr[0], ga0, ga1, xa0, xa1);
+    wide_tr_reads<16>(fr[1], ga0, ga1, xa0, xa1);
+    wide_tr_wait<8>(fr[0]);
+    wide_mfma<H>(fr[0], acc, wb, accb);
+    wide_tr_reads<32>(fr[0], ga0, ga1, xa0, xa1);
+    wide_tr_wait<8>(fr[1]);
+    wide_mfma<H>(fr[1], acc, wb, accb);
+    wide_tr_reads<48>(fr[1], ga0, ga1, xa0, xa1);
+    wide_tr_wait<8>(fr[0]);
+    wide_mfma<H>(fr[0], acc, wb, accb);
+    wide_tr_wait<0>(fr[1]);
+    wide_mfma<H>(fr[1], acc, wb, accb);
+  }
+  if constexpr (XMODE == AM_SCALE)
+    if (cur_img >= 0) fold();
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int k = k0 + wk * 64 + j * 32 + (lane & 31);
+        float v;
+        if constexpr (XMODE == AM_SCALE) v = tot[i % NT_][j % NT_][r];
+        else v = acc[i][j][r];
+        p.slab[((long)s * p.N + n) * p.K + k] = v;
+      }
+  if (wb && (lane & 31) == 0)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        p.slab_b[(long)s * p.N + n0 + wn * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] = accb[i][r];
+}
+
 template <int XMODE, typename H>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide(WgradP p) {
   __shared__ __attribute__((aligned(16))) H lds[WIDE_LDS];
   wgrad_wide_tile<XMODE, H>(p, blockIdx.x, blockIdx.y, blockIdx.z, lds);
 }
 
+template <int XMODE, typename H, int NS>
+__global__ __launch_bounds__(256) void wgrad_bf16_wide_glds(WgradP p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[wide_glds_lds_bytes<NS>()];
+  wgrad_wide_tile_glds<XMODE, H, NS>(p, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
 // Many independent wide weight gradients in one launch (nbp_wgrad_group): all the 128-multiple weight gradients of a
 // U-Net level's NAFBlocks (conv5's U, conv4, conv3's U with the per-image SCA scale, conv1) are queued while the
 // level's backward runs and launched together, with the M-splits chosen for the whole group (few or no splits when
 // the group alone fills the chip: the slabs shrink and so do their reductions).
+// XCD binning (g.xcd_bins): workgroup b runs on XCD b % 8 (round-robin dispatch), so every problem is given to one
+// XCD bin and its tiles take the ids b = 8 * (xstart + l) + bin: all the workgroups that re-read a problem's G and X
+// row panels (its N/128 x K/128 tiles of one M range run concurrently) share one L2, and each panel comes from HBM
+// once instead of once per XCD.  Pure scheduling: every tile computes exactly what it computed before.
 constexpr int WG_MAX = 24;
 struct WGroup {
   WgradP p[WG_MAX];
   int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
-  unsigned char xscale[WG_MAX];
-  int n;
+  int xstart[WG_MAX], cnt[WG_MAX];
+  unsigned char xscale[WG_MAX], xcd[WG_MAX];
+  int n, xcd_bins;
 };
-template <typename H>
+template <typename H, int NS>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
-  __shared__ __attribute__((aligned(16))) H lds[WIDE_LDS];
+  constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS)>();
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
   const int b = blockIdx.x;
-  int i = 0;
-  while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
-  const int l = b - g.start[i], gx = g.gx[i], gy = g.gy[i];
-  if (g.xscale[i]) wgrad_wide_tile<AM_SCALE, H>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy), lds);
-  else wgrad_wide_tile<AM_PLAIN, H>(g.p[i], l % gx, (l / gx) % gy, l / (gx * gy), lds);
+  int i = 0, l;
+  if (g.xcd_bins) {
+    const int x = b & 7, j = b >> 3;
+    i = -1;
+    for (int q = 0; q < g.n; ++q)
+      if (g.xcd[q] == x && j >= g.xstart[q] && j < g.xstart[q] + g.cnt[q]) {
+        i = q;
+        break;
+      }
+    if (i < 0) return;  // this XCD's bin is shorter than the longest one
+    l = j - g.xstart[i];
+  } else {
+    while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
+    l = b - g.start[i];
+  }
+  const int gx = g.gx[i], gy = g.gy[i];
+  const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
+  if constexpr (NS == 0) {
+    H* lds = reinterpret_cast<H*>(smem);
+    if (g.xscale[i]) wgrad_wide_tile<AM_SCALE, H>(g.p[i], bx, by, bz, lds);
+    else wgrad_wide_tile<AM_PLAIN, H>(g.p[i], bx, by, bz, lds);
+  } else {
+    if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS>(g.p[i], bx, by, bz, smem);
+    else wgrad_wide_tile_glds<AM_PLAIN, H, NS>(g.p[i], bx, by, bz, smem);
+  }
 }
 
 // Column sums of a [S][L] fp32 slab.  A lane sums VEC adjacent columns (float4 loads when VEC = 4) over the rows
@@ -944,6 +1197,24 @@ long wgroup_target() {
   return v;
 }
 
+// NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
+// launch (A/B measurement; tests compare the paths in one process)
+int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged tiles, +0.5 % over depth 2 (A/B)
+  const char* e = getenv("NBP_WGRAD_GLDS");
+  const int v = e ? atoi(e) : 3;
+  return v >= 2 && v <= 4 ? v : 0;
+}
+
+// NBP_WGROUP_XCD=1: each problem's tiles on one XCD bin (its panels then come from HBM once: measured 815 -> 252 MB
+// per middle-level group, but no faster -- the tile loop is not bandwidth-bound -- and the bin imbalance costs 0.4 %)
+int wgroup_xcd() {
+  static const int v = [] {
+    const char* e = getenv("NBP_WGROUP_XCD");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
+
 // Splits for the whole group: each problem keeps at most its standalone split count (its workspace) and at least
 // 256 rows per split; the group as a whole aims at ~wgroup_target() workgroups.  The reductions queued for the
 // problems' slabs are re-pointed at the chosen split counts.
@@ -978,7 +1249,38 @@ void wgroup_launch(hipStream_t st) {
       ++g.n;
     }
     g.start[g.n] = blocks;
-    NBP_DISPATCH_H(g_wqueue_dtype, wgrad_bf16_wide_group<H><<<blocks, 256, 0, st>>>(g));
+    g.xcd_bins = wgroup_xcd();
+    if (g.xcd_bins) {  // longest-processing-time binning of the problems over the 8 XCDs (work = tiles x rows)
+      int order[WG_MAX];
+      long work[8] = {}, load[8] = {};
+      for (int q = 0; q < g.n; ++q) {
+        order[q] = q;
+        g.cnt[q] = g.start[q + 1] - g.start[q];
+      }
+      std::sort(order, order + g.n, [&](int a, int b) {
+        return (long)g.cnt[a] * g.p[a].chunk > (long)g.cnt[b] * g.p[b].chunk;
+      });
+      for (int t = 0; t < g.n; ++t) {
+        const int q = order[t];
+        int x = 0;
+        for (int y = 1; y < 8; ++y)
+          if (work[y] < work[x]) x = y;
+        g.xcd[q] = (unsigned char)x;
+        g.xstart[q] = (int)load[x];
+        load[x] += g.cnt[q];
+        work[x] += (long)g.cnt[q] * g.p[q].chunk;
+      }
+      long mx = 0;
+      for (int x = 0; x < 8; ++x) mx = load[x] > mx ? load[x] : mx;
+      blocks = (int)(8 * mx);
+    }
+    const int ns = wgrad_glds_depth();
+    NBP_DISPATCH_H(g_wqueue_dtype, {
+      if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
+      else if (ns == 3) wgrad_bf16_wide_group<H, 3><<<blocks, 256, 0, st>>>(g);
+      else if (ns == 2) wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
+      else wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
+    });
   }
   g_wqueue.clear();
 }
@@ -1017,7 +1319,14 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       if (x_mode != AM_SCALE) p.x_scale = nullptr;  // the group kernel selects the X mode by x_scale
       g_wqueue.push_back(p);
     } else NBP_DISPATCH_H(dtype, {
-      if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
+      const int ns = wgrad_glds_depth();
+      if (wide && ns == 4 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 4><<<wgrid, 256, 0, st>>>(p);
+      else if (wide && ns == 4) wgrad_bf16_wide_glds<AM_SCALE, H, 4><<<wgrid, 256, 0, st>>>(p);
+      else if (wide && ns == 2 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 2><<<wgrid, 256, 0, st>>>(p);
+      else if (wide && ns == 2) wgrad_bf16_wide_glds<AM_SCALE, H, 2><<<wgrid, 256, 0, st>>>(p);
+      else if (wide && ns == 3 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 3><<<wgrid, 256, 0, st>>>(p);
+      else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
+      else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)

@@ -531,24 +531,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 // (a glds instruction writes 1 KB lane-linearly, so the permutation is applied to each lane's SOURCE address; the
 // fragment reads, lanes 0..31 on rows r..r+31 at one chunk, then hit 16 distinct slots per ds_read_b128 lane group),
 // then for AM_SCALE the tile's 64 fp32 column scales (one 4-byte glds).  Out-of-range rows / columns / K tail and the
-// zero padding of AM_IM2COL read g_zero16.
-__device__ __attribute__((aligned(16))) unsigned char g_zero16[16];
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glob_void_t;
-
-// dest = lds_wave_base (wave-uniform) + lane * size
-__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
-}
-__device__ __forceinline__ void glds4(const void* src, unsigned char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)lds_wave_base, 4, 0, 0);
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
+// zero padding of AM_IM2COL read g_zero16 (LDS-DMA helpers: nbp_common.h).
 template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H>
 __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
   constexpr int BK = 64;
@@ -594,6 +577,9 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
     b_kof[i] = 8 * (lc ^ ((r >> 1) & 7));
   }
   const float* sc_row = AMODE == AM_SCALE ? p.a_scale + (long)(m0 / p.rows_per_img) * K : nullptr;
+  // the zero page's address in registers (laundered through asm: otherwise re-loaded from the GOT at every use)
+  const void* zp = g_zero16;
+  asm volatile("" : "+s"(zp));
 
   const int nk = (K + BK - 1) / BK;
   auto issue = [&](int t) {
@@ -602,7 +588,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int k = k0 + a_kof[i];
-      const void* src = g_zero16;
+      const void* src = zp;
       if (a_m[i] < M && k < K) {
         if constexpr (AMODE == AM_S2D) {
           const int q = k / p.cs, c = k - q * p.cs;
@@ -621,12 +607,12 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
 #pragma unroll
     for (int i = 0; i < GB; ++i) {
       const int k = k0 + b_kof[i];
-      const void* src = (b_n[i] < N && k < K) ? (const void*)(B + (long)b_n[i] * p.ldb + k) : (const void*)g_zero16;
+      const void* src = (b_n[i] < N && k < K) ? (const void*)(B + (long)b_n[i] * p.ldb + k) : zp;
       glds16(src, st + A_BYTES + (wave * GB + i) * 1024);
     }
     if constexpr (AMODE == AM_SCALE) {  // every wave loads the same 64 scales (identical bytes, one instruction each)
       const int k = k0 + lane;
-      glds4(k < K ? (const void*)(sc_row + k) : (const void*)g_zero16, st + A_BYTES + B_BYTES);
+      glds4(k < K ? (const void*)(sc_row + k) : zp, st + A_BYTES + B_BYTES);
     }
   };
 

@@ -149,6 +149,25 @@ __device__ __forceinline__ int xcd_remap(int L, int T) {
   return (L & 7) * (T8 >> 3) + (L >> 3);
 }
 
+// ---- LDS-DMA (global_load_lds): the LDS destination is wave-uniform base + lane * size; each lane's SOURCE address is
+// free, so swizzled LDS images are made by permuting the sources.  Out-of-range lanes read g_zero16 (per-TU zero page).
+namespace {
+__device__ __attribute__((aligned(16))) unsigned char g_zero16[16];
+}
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glob_void_t;
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void* src, unsigned char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glob_void_t*)src, (lds_void_t*)lds_wave_base, 4, 0, 0);
+}
+// counted wait on this wave's outstanding vector-memory operations (LDS-DMA included)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline hipStream_t S(nbp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -157,3 +157,41 @@ def test_glds_chandot(dev, B, HW, C):
         call("gemm_bf16", A, C, 0, None, HW, 1, Wt, C, d, C, 8, 1, M, C, C, 0, 0, 0, None, g, None, slab)
         return d, slab
     run_modes(fn)
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("M,N,K,rows", [(4096, 1024, 512, 256), (16384, 256, 512, 1024), (65536, 128, 256, 4096),
+                                        (3000, 256, 128, 0), (4160, 512, 512, 0)])
+def test_glds_wide_wgrad(dev, dt, M, N, K, rows):
+    """Wide weight gradient (N, K multiples of 128) with LDS-DMA panels vs the register-staged tile: dW bitwise (same
+    MFMA sequence and per-image scale fold), the bias column sums (MFMA against ones vs register sums: another
+    order) within fp32 rounding.  rows > 0: the per-image SCA column scale of X."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(M + N + K + dt)
+    G = torch.randn(M, N, device=dev, generator=gen).to(DT[dt])
+    X = torch.randn(M, K, device=dev, generator=gen).to(DT[dt])
+    sc = torch.rand(max(M // max(rows, 1), 1), K, device=dev, generator=gen) + 0.5 if rows else None
+    n_ws = query("wgrad_workspace_floats", M, N, K)
+    ws = torch.empty(n_ws, device=dev)
+    res = {}
+    old = os.environ.get("NBP_WGRAD_GLDS")
+    try:
+        for ns in ("0", "2", "3", "4"):
+            os.environ["NBP_WGRAD_GLDS"] = ns
+            dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+            call("wgrad_f32", G, N, 0, X, K, 2 if rows else 0, sc, rows if rows else 1, M, N, K, 0, 0, 0, 0, dW, db,
+                 ws, n_ws, dt)
+            torch.cuda.synchronize()
+            res[ns] = (dW, db)
+    finally:
+        if old is None:
+            os.environ.pop("NBP_WGRAD_GLDS", None)
+        else:
+            os.environ["NBP_WGRAD_GLDS"] = old
+    for ns in ("2", "3", "4"):
+        assert torch.equal(res[ns][0], res["0"][0]), ns
+        torch.testing.assert_close(res[ns][1], res["0"][1], rtol=1e-5, atol=1e-4 * M ** 0.5)
+    Xe = X.double() * (sc.double().repeat_interleave(rows, 0)[:M] if rows else 1.0)
+    ref = G.double().t() @ Xe
+    assert (res["2"][0].double() - ref).abs().max().item() <= 1e-4 * M ** 0.5
+    assert (res["2"][1].double() - G.double().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5
