@@ -132,20 +132,22 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
 // Epilogue of the tiled kernels: the fp32 accumulators (4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32
 // MFMA tiles) are staged through LDS (smem, aliasing the operand buffers; the caller has finished every read of them)
 // so that bias / pre-activation / residual R + rscale * v / the C store all move 8 consecutive columns per thread.
-template <int BM, int BN, int CMODE, typename TC, typename H>
-__device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / 64][BN / 64], unsigned char* smem,
-                                              int m0, int n0) {
-  constexpr int TM = BM / 64, TN = BN / 64;
+// WN = waves along N (2: 4 waves in 2 x 2; 4: 8 waves in 2 x 4, each (BM / 2) x (BN / 4)); NT = 64 * 2 * WN threads.
+template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2>
+__device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / 64][BN / (32 * WN)],
+                                              unsigned char* smem, int m0, int n0) {
+  constexpr int TM = BM / 64, TN = BN / (32 * WN), NT = 128 * WN;
+  static_assert(WN == 2 || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT), "cross-wave reductions assume 4 waves");
   constexpr int CLS = BN + 4;  // fp32 C-tile row stride
   float* Cs = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int M = p.M, N = p.N;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int col = wn * (BN / 2) + j * 32 + (lane & 31);
+      const int col = wn * (BN / WN) + j * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -161,7 +163,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
   float cd[8], cb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) cd[j] = cb[j] = 0.f;
-  for (int e = tid; e < BM * G8; e += 256) {
+  for (int e = tid; e < BM * G8; e += NT) {
     const int row = e / G8, c8 = (e % G8) * 8;
     const int grow = m0 + row, gcol = n0 + c8;
     if (grow >= M || gcol >= N) continue;
@@ -532,21 +534,23 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 // fragment reads, lanes 0..31 on rows r..r+31 at one chunk, then hit 16 distinct slots per ds_read_b128 lane group),
 // then for AM_SCALE the tile's 64 fp32 column scales (one 4-byte glds).  Out-of-range rows / columns / K tail and the
 // zero padding of AM_IM2COL read g_zero16 (LDS-DMA helpers: nbp_common.h).
-template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H>
-__global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
-  constexpr int BK = 64;
-  constexpr int TM = BM / 64, TN = BN / 64;
+template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H, int WN = 2>
+__global__ __launch_bounds__(128 * WN) void gemm_glds_kernel(GemmPB p) {
+  constexpr int BK = 64, NW = 2 * WN;  // waves: 2 along M x WN along N
+  constexpr int TM = BM / 64, TN = BN / (32 * WN);
+  static_assert(TN >= 1, "tile too narrow for the wave layout");
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int SC_BYTES = AMODE == AM_SCALE ? 256 : 0;
   constexpr int ST_BYTES = A_BYTES + B_BYTES + SC_BYTES;
-  constexpr int GA = BM / 32, GB = BN / 32;  // 1-KB (8-row) glds instructions per wave per stage
+  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // 1-KB (8-row) glds instructions per wave per stage
+  static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "DMA rows per wave");
   constexpr int G = GA + GB + (AMODE == AM_SCALE ? 1 : 0);
   constexpr int C_BYTES = BM * (BN + 4) * 4;
   constexpr int SM_BYTES = NS * ST_BYTES > C_BYTES ? NS * ST_BYTES : C_BYTES;
   static_assert(NS == 2 || NS == 3, "ring depth");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int M = p.M, N = p.N, K = p.K;
   const H* A = reinterpret_cast<const H*>(p.A);
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
         a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (wm * (BM / 2) + i * 32 + (lane & 31)) * 128 + slot);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (wn * (BN / 2) + j * 32 + (lane & 31)) * 128 + slot);
+        b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (wn * (BN / WN) + j * 32 + (lane & 31)) * 128 + slot);
       if constexpr (AMODE == AM_SCALE) {
         const float* scs = reinterpret_cast<const float*>(b_s + B_BYTES) + s * 16 + (lane >> 5) * 8;
         const float4 s0 = ld4(scs), s1 = ld4(scs + 4);
@@ -669,7 +673,7 @@ __global__ __launch_bounds__(256) void gemm_glds_kernel(GemmPB p) {
     compute(t % NS);
   }
   __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
-  gemm_epilogue<BM, BN, CMODE, TC, H>(p, acc, smem, m0, n0);
+  gemm_epilogue<BM, BN, CMODE, TC, H, WN>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
@@ -1086,6 +1090,13 @@ int glds_depth() {
   return e ? atoi(e) : 2;
 }
 
+// NBP_GEMM_WAVES: 8 (default: 2 x 4 waves, two per SIMD, on tiles with BN >= 128) or 4 (2 x 2) for the LDS-DMA
+// kernel (A/B, read per launch: 8 waves + 128 x 128 tiles from 512 workgroups = +2 % step over 4 waves + 1024)
+int gemm_waves() {
+  const char* e = getenv("NBP_GEMM_WAVES");
+  return e && atoi(e) == 4 ? 4 : 8;
+}
+
 template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC, typename H>
 void launch(const GemmPB& p, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
@@ -1096,6 +1107,13 @@ void launch(const GemmPB& p, hipStream_t st) {
                     (AMODE == AM_S2D || AMODE == AM_IM2COL ? p.cs % 8 == 0 : p.lda % 8 == 0) &&
                     (AMODE != AM_SCALE || p.rows_per_img % BM == 0);
     if (ok) {
+      if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
+        if (gemm_waves() == 8) {  // 2 x 4 waves of (BM / 2) x (BN / 4): two waves per SIMD
+          if (ns == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+          else gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+          return;
+        }
+      }
       if (ns == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       else gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       return;
@@ -1105,13 +1123,13 @@ void launch(const GemmPB& p, hipStream_t st) {
   else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
 }
 
-// largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 1024 blocks (4 per CU);
-// otherwise 64x64, the most blocks available.
+// largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 512 blocks (2 per CU; with the
+// 8-wave DMA tiles: 1024 with the register-staged 4-wave kernel measured best); otherwise 64x64, the most blocks.
 // NBP_GEMM_MINBLK overrides the block-count threshold (A/B measurement)
 long gemm_minblk() {
   static const long v = [] {
     const char* e = getenv("NBP_GEMM_MINBLK");
-    return e ? atol(e) : 1024L;
+    return e ? atol(e) : 512L;
   }();
   return v;
 }
@@ -1124,8 +1142,6 @@ void dispatch(const GemmPB& p, hipStream_t st) {
     auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
     const bool n128 = p.N > 64, m128 = p.M > 64;
     const long mb = gemm_minblk();
-    // (128 x 128 from 512 blocks won in isolation on M 16K-64K shapes, scripts/gemm_micro.py, but lost 0.3 ms/step in
-    // the training step: kept at >= 1024 blocks)
     if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC, H>(p, st);
     else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC, H>(p, st);
     else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC, H>(p, st);
