@@ -132,12 +132,13 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
 // Epilogue of the tiled kernels: the fp32 accumulators (4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32
 // MFMA tiles) are staged through LDS (smem, aliasing the operand buffers; the caller has finished every read of them)
 // so that bias / pre-activation / residual R + rscale * v / the C store all move 8 consecutive columns per thread.
-// WN = waves along N (2: 4 waves in 2 x 2; 4: 8 waves in 2 x 4, each (BM / 2) x (BN / 4)); NT = 64 * 2 * WN threads.
-template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2>
-__device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / 64][BN / (32 * WN)],
+// WM x WN waves (default 2 x 2), each (BM / WM) x (BN / WN) of 32 x 32 MFMA tiles; NT = 64 WM WN threads.
+template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2, int WM = 2>
+__device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / (32 * WM)][BN / (32 * WN)],
                                               unsigned char* smem, int m0, int n0) {
-  constexpr int TM = BM / 64, TN = BN / (32 * WN), NT = 128 * WN;
-  static_assert(WN == 2 || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT), "cross-wave reductions assume 4 waves");
+  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN), NT = 64 * WM * WN;
+  static_assert((WN == 2 && WM == 2) || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT),
+                "cross-wave reductions assume 2 x 2 waves");
   constexpr int CLS = BN + 4;  // fp32 C-tile row stride
   float* Cs = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -150,7 +151,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       const int col = wn * (BN / WN) + j * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         Cs[row * CLS + col] = acc[i][j][r];
       }
     }
@@ -534,11 +535,11 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 // fragment reads, lanes 0..31 on rows r..r+31 at one chunk, then hit 16 distinct slots per ds_read_b128 lane group),
 // then for AM_SCALE the tile's 64 fp32 column scales (one 4-byte glds).  Out-of-range rows / columns / K tail and the
 // zero padding of AM_IM2COL read g_zero16 (LDS-DMA helpers: nbp_common.h).
-template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H, int WN = 2>
-__global__ __launch_bounds__(128 * WN) void gemm_glds_kernel(GemmPB p) {
-  constexpr int BK = 64, NW = 2 * WN;  // waves: 2 along M x WN along N
-  constexpr int TM = BM / 64, TN = BN / (32 * WN);
-  static_assert(TN >= 1, "tile too narrow for the wave layout");
+template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H, int WN = 2, int WM = 2>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
+  constexpr int BK = 64, NW = WM * WN;  // waves: WM along M x WN along N
+  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
+  static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
   constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
   constexpr int SC_BYTES = AMODE == AM_SCALE ? 256 : 0;
   constexpr int ST_BYTES = A_BYTES + B_BYTES + SC_BYTES;
@@ -638,7 +639,7 @@ __global__ __launch_bounds__(128 * WN) void gemm_glds_kernel(GemmPB p) {
       vec_t<H, 8> a[TM], b[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (wm * (BM / 2) + i * 32 + (lane & 31)) * 128 + slot);
+        a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (wm * (BM / WM) + i * 32 + (lane & 31)) * 128 + slot);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (wn * (BN / WN) + j * 32 + (lane & 31)) * 128 + slot);
@@ -673,7 +674,7 @@ __global__ __launch_bounds__(128 * WN) void gemm_glds_kernel(GemmPB p) {
     compute(t % NS);
   }
   __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
-  gemm_epilogue<BM, BN, CMODE, TC, H, WN>(p, acc, smem, m0, n0);
+  gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
@@ -1134,8 +1135,39 @@ long gemm_minblk() {
   return v;
 }
 
+// NBP_CONV_TILE (A/B measurement, read per launch; default 0 = the generic tile choice): 256-row tiles for the 3x3
+// implicit-GEMM convs, bit 0: 256 x 64 on 4 waves (4 x 1, 64 x 64 each) when N <= 64, bit 1: 256 x 128 on 8 waves
+// (4 x 2) when N > 64.  Measured on cfg3: bit 0 neutral, bit 1 -1.5 % (one 135 KB workgroup per CU): with one barrier
+// per K step the 128 x 128 tile stays the better structure.
+int conv_tile() {
+  const char* e = getenv("NBP_CONV_TILE");
+  return e ? atoi(e) : 0;
+}
+
+template <int AMODE, int CMODE, typename TA, typename TC, typename H>
+bool launch_conv_big(const GemmPB& p, hipStream_t st) {
+  if constexpr (sizeof(TA) == 2 && AMODE == AM_IM2COL && CMODE != CM_LNBWD && CMODE != CM_CHANDOT &&
+                CMODE != CM_RESLN) {
+    const int ns = glds_depth();
+    const int ct = conv_tile();
+    if (!(ct & (p.N <= 64 ? 1 : 2)) || ns < 2 || p.K <= 32 || p.ldb % 8 || p.cs % 8 ||
+        (long)cdiv(p.M, 256) * cdiv(p.N, 128) < 256)
+      return false;
+    if (p.N <= 64) {
+      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 64));
+      gemm_glds_kernel<256, 64, 2, AMODE, CMODE, TC, H, 1, 4><<<grid, 256, 0, st>>>(p);
+    } else {
+      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 128));
+      gemm_glds_kernel<256, 128, 2, AMODE, CMODE, TC, H, 2, 4><<<grid, 512, 0, st>>>(p);
+    }
+    return true;
+  }
+  return false;
+}
+
 template <int AMODE, int CMODE, typename TA, typename TC, typename H>
 void dispatch(const GemmPB& p, hipStream_t st) {
+  if (launch_conv_big<AMODE, CMODE, TA, TC, H>(p, st)) return;
   if constexpr (CMODE == CM_CHANDOT) {  // its partial-sum layout is per 64-row tile
     launch<64, 64, AMODE, CMODE, TA, TC, H>(p, st);
   } else {

@@ -97,9 +97,11 @@ def test_glds_space_to_depth(dev, B, gh, gw, cs):
     run_modes(fn)
 
 
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [(1, 64, 64, 64, 128), (2, 17, 23, 128, 64), (1, 32, 32, 256, 256)])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(1, 64, 64, 64, 128), (2, 17, 23, 128, 64), (1, 32, 32, 256, 256),
+                                            (3, 130, 170, 64, 64), (4, 128, 128, 128, 128), (2, 96, 180, 64, 256)])
 def test_glds_conv3x3(dev, B, H, W, Cin, Cout):
-    """VGG 3x3 convolution (implicit GEMM, zero padding read from the zero page): bias + ReLU and the ReLU-mask form."""
+    """VGG 3x3 convolution (implicit GEMM, zero padding read from the zero page): bias + ReLU and the ReLU-mask form.
+    The large shapes (>= 256 row tiles) run the 256-row conv tiles (NBP_CONV_TILE=1) on the DMA path."""
     from lowlight_image_enhancement_amd._lib import call
     gen = torch.Generator(device=dev).manual_seed(B * H + Cin)
     x = torch.randn(B, H, W, Cin, device=dev, generator=gen).to(torch.bfloat16)
