@@ -548,7 +548,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
   constexpr int G = GA + GB + (AMODE == AM_SCALE ? 1 : 0);
   constexpr int C_BYTES = BM * (BN + 4) * 4;
   constexpr int SM_BYTES = NS * ST_BYTES > C_BYTES ? NS * ST_BYTES : C_BYTES;
-  static_assert(NS == 2 || NS == 3, "ring depth");
+  static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(SM_BYTES <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -665,7 +666,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
   for (int t = 0; t < nk; ++t) {
     // retire K-tile t (this wave's DMAs), leaving the later tiles of the ring in flight; the barrier then makes every
     // wave's part of tile t visible and frees the stage read at step t - 1 for tile t + NS - 1
-    if (NS == 3 && t + 1 < nk) wait_vm<G>();
+    if (NS >= 4 && t + 2 < nk) wait_vm<2 * G>();
+    else if (NS >= 3 && t + 1 < nk) wait_vm<G>();
     else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -1108,15 +1110,21 @@ void launch(const GemmPB& p, hipStream_t st) {
                     (AMODE == AM_S2D || AMODE == AM_IM2COL ? p.cs % 8 == 0 : p.lda % 8 == 0) &&
                     (AMODE != AM_SCALE || p.rows_per_img % BM == 0);
     if (ok) {
+      // the ring depth the tile's LDS allows (stage = (BM + BN) x 128 B + scales; the fp32 C staging must fit too)
+      constexpr int STB = (BM + BN) * 128 + (AMODE == AM_SCALE ? 256 : 0), CB = BM * (BN + 4) * 4;
+      constexpr int NMAX = 4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
+      const int nd = ns < NMAX ? ns : NMAX;
       if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
         if (gemm_waves() == 8) {  // 2 x 4 waves of (BM / 2) x (BN / 4): two waves per SIMD
-          if (ns == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          else gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+          if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+          else if (nd == 3) gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+          else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
           return;
         }
       }
-      if (ns == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
-      else gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      else if (nd == 3) gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       return;
     }
   }

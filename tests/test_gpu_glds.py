@@ -16,7 +16,7 @@ def run_modes(fn):
     outs = {}
     old = os.environ.get("NBP_GLDS")
     try:
-        for ns in ("0", "2", "3"):
+        for ns in ("0", "2", "3", "4"):
             os.environ["NBP_GLDS"] = ns
             outs[ns] = [t.clone() for t in fn()]
             torch.cuda.synchronize()
@@ -25,7 +25,7 @@ def run_modes(fn):
             os.environ.pop("NBP_GLDS", None)
         else:
             os.environ["NBP_GLDS"] = old
-    for ns in ("2", "3"):
+    for ns in ("2", "3", "4"):
         for a, b in zip(outs["0"], outs[ns]):
             assert torch.equal(a, b), f"NBP_GLDS={ns} differs from the register-staged kernel"
 
