@@ -104,9 +104,9 @@ class NAFNet(nn.Module):
         self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
         # LayerNorm backward in the conv4 / conv1 dgrad epilogue at C = 128 (NBP_FUSE_LN_BWD128=0: standalone ln_bwd)
         self.fuse_ln_bwd128 = os.environ.get("NBP_FUSE_LN_BWD128", "1") != "0"
-        # the LayerNorm fusions at C = 256 too (64 x 256 tiles, one workgroup per CU): NBP_FUSE_LN256 = bwd (default:
-        # +0.35 %), 1 (both), fwd (-0.4 %) or 0
-        self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "bwd")
+        # the LayerNorm fusions at C = 256 too (64 x 256 tiles): NBP_FUSE_LN256 = 1 (both, default: +1.1 % with the
+        # 8-wave LDS-DMA tiles; round 1 with register-staged tiles: fwd -0.4 %, bwd +0.35 %), bwd, fwd or 0
+        self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "1")
         # the wide (C >= 128) weight gradients of a whole U-Net level (conv5's U, conv4, conv3's U, conv1 of every
         # NAFBlock of the level) queued during the level's backward and launched as ONE grouped launch at its end,
         # with M-splits chosen for the group (NBP_GROUP_WGRAD=0: one launch per weight gradient)
