@@ -124,6 +124,16 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
  * (nbp_gemm_bf16 CM_SG with C = NULL). */
 int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,
                     void* C, int M, int N, int K, int dtype, nbp_stream_t s);
+/* nbp_dgrad_sg_rc plus the weight gradients that read the same operands (level 0: the reads of the separate
+ * nbp_wgrad_f32 launches for conv5's U / V and conv4's weight / bias disappear): U = A^T g [N][N] with g the SimpleGate
+ * output rebuilt from t (the forward's stored g, bit for bit), V = colsum A [N], dW2 = C^T A2 [2N][K] (C = the stored
+ * dt), db2 = colsum C [2N]; block partials in ws (nbp_dgrad_sg_rc_wg_workspace_floats), reduced like nbp_wgrad_f32's
+ * slabs (deferred with the stage).  N = K = 32.  Reference: NAFNet_arch.py:76-80 (conv4 / SimpleGate / conv5),
+ * whose weight gradients torch autograd computes in separate passes. */
+size_t nbp_dgrad_sg_rc_wg_workspace_floats(long M, int N);
+int nbp_dgrad_sg_rc_wg(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2,
+                       const float* b2, void* C, int M, int N, int K, float* U, float* V, float* dW2, float* db2,
+                       float* ws, size_t ws_floats, int dtype, nbp_stream_t s);
 /* per-step weight prep: out = h(flat); for each desc {offset, rows, cols, scale_offset} (int64, device)
  * out_t[offset..] = h(diag(s) . flat matrix)^T, h = bf16 (dtype 1) or fp16 (dtype 2), with s = flat[scale_offset..] (rows values), or no scaling when
  * scale_offset < 0 (the NAFBlock layer scales folded into the conv3 / conv5 dgrad operands). */

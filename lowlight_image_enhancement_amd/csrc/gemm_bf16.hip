@@ -720,15 +720,26 @@ struct SkinnyP {
   const H* A2;
   const H* W2;
   const float* b2;
+  // WGF (with CM_SGBWD_RC at N = K = 32): the weight gradients that read this kernel's operands, per-block partials
+  // U = dout^T g (g = the SimpleGate output rebuilt from t), V = colsum dout, dW2 = C^T A2 (C = the stored dt), db2 =
+  // colsum C into slab_u [grid][N N], slab_v [grid][N], slab_w2 [grid][2N K], slab_b2 [grid][2N]
+  float* slab_u;
+  float* slab_v;
+  float* slab_w2;
+  float* slab_b2;
 };
 
-template <int NT, int KS, int AMODE, int CMODE, typename H>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
+template <int NT, int KS, int AMODE, int CMODE, typename H, bool WGF = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGF ? 2 : 1)))
+void gemm_skinny_kernel(SkinnyP<H> p) {
   constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
   constexpr bool RC = CMODE == CM_SGBWD_RC;
+  static_assert(!WGF || (RC && NT == 1 && KS == 2), "weight-gradient fold: level-0 conv5 dgrad (N = K = 32)");
   constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : 8;  // bf16 row stride of the recomputed gate-input tile
   __shared__ float stage[4][32 * LDT];
   __shared__ __attribute__((aligned(16))) H stage2[4][32 * LDT2];
+  // WGF: the tile's dt (32 rows x 64, 192-byte rows: conflict-free ds_read_b64_tr_b16), later the block's reduction
+  __shared__ __attribute__((aligned(16))) H stage3[WGF ? 4 : 1][WGF ? 32 * 96 : 8];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   float* tileS = stage[threadIdx.x >> 6];
   H* tileT = stage2[threadIdx.x >> 6];
@@ -779,6 +790,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
   float bia[8], rsc[8], aw[8], ab[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { bia[j] = 0.f; rsc[j] = 1.f; aw[j] = ab[j] = 0.f; }
+  // WGF accumulators: dW2 (2 x 32 rows of dt channels x 32 n2 channels), U (32 x 32), V (this lane's 16 dout channels)
+  floatx16 accw[2], accu;
+  float vsum[KS][8];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) accw[0][i] = accw[1][i] = accu[i] = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) vsum[ks][e] = 0.f;
   if (CMODE == CM_RESLN) {  // aw / ab hold the LN weight / bias of this lane's 8 columns
     const float4 w0 = ld4(p.lnw + ccol), w1 = ld4(p.lnw + ccol + 4), b0 = ld4(p.lnb_f + ccol), b1 = ld4(p.lnb_f + ccol + 4);
     aw[0] = w0.x; aw[1] = w0.y; aw[2] = w0.z; aw[3] = w0.w; aw[4] = w1.x; aw[5] = w1.y; aw[6] = w1.z; aw[7] = w1.w;
@@ -859,6 +879,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<float4*>(tileS + r * LDT + t * 32 + 8 * g + 4 * h) =
             make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
+    // WGF: the SimpleGate outputs g = (t[2c] t[2c+1]) of this lane's channels, from the fp32 t exactly as the conv4
+    // forward's SimpleGate epilogue computed them (its stored g)
+    vec_t<H, 2> g2h[NT2][4];
     if constexpr (RC) {  // t = bf16(A2 W2^T + b2) exactly as the conv4 forward stored it (same MFMA sequence)
 #pragma unroll
       for (int t = 0; t < NT2; ++t) {
@@ -870,9 +893,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           vec_t<H, 4> o;
+          float v[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (H)(a2c[4 * g + q] + b2r[t][g][q]);
+          for (int q = 0; q < 4; ++q) {
+            v[q] = a2c[4 * g + q] + b2r[t][g][q];
+            o[q] = (H)v[q];
+          }
           *reinterpret_cast<vec_t<H, 4>*>(tileT + r * LDT2 + t * 32 + 8 * g + 4 * h) = o;
+          if constexpr (WGF) {
+            g2h[t][g][0] = (H)(v[0] * v[1]);
+            g2h[t][g][1] = (H)(v[2] * v[3]);
+          }
         }
       }
     }
@@ -880,7 +911,16 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
     const long m0 = tile * 32;
     for (int rr = lane / cpr; rr < 32; rr += rstep) {
       const long m = m0 + rr;
-      if (m >= M) break;
+      if (m >= M) {
+        if constexpr (WGF) {  // the fold's dt tile: zero rows past M (their n2 rows are zero, stale data could be NaN)
+          vec_t<H, 8> z;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) z[j] = (H)0.f;
+          *reinterpret_cast<vec_t<H, 8>*>(stage3[threadIdx.x >> 6] + rr * 96 + ccol) = z;
+          continue;
+        }
+        break;
+      }
       if (CMODE == CM_SGBWD || RC) {  // chunk = 4 gates (interleaved pairs): dg from the tile, t from R (or rebuilt)
         const float4 dg = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol / 2);
         const long off = m * p.ldc + ccol;
@@ -894,6 +934,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
           o[2 * j + 1] = (H)(d[j] * (float)tv[2 * j]);
         }
         *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
+        if constexpr (WGF) {
+          *reinterpret_cast<vec_t<H, 8>*>(stage3[threadIdx.x >> 6] + rr * 96 + ccol) = o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ab[j] += (float)o[j];  // db2 partial of this lane's 8 columns
+        }
         continue;
       }
       const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
@@ -968,11 +1013,116 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyP<H> p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
+    if constexpr (WGF) {
+      // stage dout (this GEMM's A) and n2 (A2) in the dead fp32 tile, g in the dead t tile (32-element rows), then
+      // accumulate U += dout^T g and dW2 += dt^T n2 over the tile's 32 rows with transposed fragment reads
+      H* sd = reinterpret_cast<H*>(tileS);
+      H* sn = sd + 32 * 32;
+      H* sg = tileT;
+      const H* st = stage3[threadIdx.x >> 6];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        *reinterpret_cast<vec_t<H, 8>*>(sd + r * 32 + ks * 16 + 8 * h) = a0[ks];
+        *reinterpret_cast<vec_t<H, 8>*>(sn + r * 32 + ks * 16 + 8 * h) = c0[ks];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vsum[ks][e] += (float)a0[ks][e];  // V partial (rows past M are zero-filled)
+      }
+#pragma unroll
+      for (int t = 0; t < NT2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<vec_t<H, 2>*>(sg + r * 32 + t * 16 + 4 * g + 2 * h) = g2h[t][g];
+      __builtin_amdgcn_wave_barrier();
+      const int grp = lane >> 4, gq = (lane & 15) >> 2, pp = lane & 3;
+      const int fcol = 16 * (grp & 1) + 4 * pp;
+#pragma unroll
+      for (int ks = 0; ks < 32; ks += 16) {
+        vec_t<H, 8> fa[2], fn, fu, fg;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int row = ks + 8 * h + 4 * tt + gq;
+          const vec_t<H, 4> a0v = ds_read_tr16<H>(st + row * 96 + fcol);
+          const vec_t<H, 4> a1v = ds_read_tr16<H>(st + row * 96 + 32 + fcol);
+          const vec_t<H, 4> nv = ds_read_tr16<H>(sn + row * 32 + fcol);
+          const vec_t<H, 4> uv = ds_read_tr16<H>(sd + row * 32 + fcol);
+          const vec_t<H, 4> gv = ds_read_tr16<H>(sg + row * 32 + fcol);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            fa[0][4 * tt + e] = a0v[e];
+            fa[1][4 * tt + e] = a1v[e];
+            fn[4 * tt + e] = nv[e];
+            fu[4 * tt + e] = uv[e];
+            fg[4 * tt + e] = gv[e];
+          }
+        }
+        accw[0] = mfma32x32x16(fa[0], fn, accw[0]);
+        accw[1] = mfma32x32x16(fa[1], fn, accw[1]);
+        accu = mfma32x32x16(fu, fg, accu);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) a0[ks] = a1[ks];
     if constexpr (RC)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) c0[ks] = c1[ks];
+  }
+  if constexpr (WGF) {
+    // block partials, waves combined in fixed order through stage3 (as fp32): [0, 2048) dW2 (row n = dt column, col k =
+    // n2 channel), [2048, 3072) U, [3072, 3136) db2, [3136, 3168) V
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = cpr; o < 64; o <<= 1) ab[j] += __shfl_xor(ab[j], o, 64);  // lanes sharing ccol
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) vsum[ks][e] += __shfl_xor(vsum[ks][e], o, 64);  // lanes sharing h
+    float* red = reinterpret_cast<float*>(&stage3[0][0]);
+    const int wv = threadIdx.x >> 6;
+    for (int w = 0; w < 4; ++w) {
+      __syncthreads();
+      if (wv == w) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr) {
+            const int n = i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h, k = r;
+            float* d = red + n * 32 + k;
+            *d = (w == 0 ? 0.f : *d) + accw[i][rr];
+          }
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int n = (rr & 3) + 8 * (rr >> 2) + 4 * h, k = r;
+          float* d = red + 2048 + n * 32 + k;
+          *d = (w == 0 ? 0.f : *d) + accu[rr];
+        }
+        if (lane < cpr)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float* d = red + 3072 + ccol + j;
+            *d = (w == 0 ? 0.f : *d) + ab[j];
+          }
+        if (r == 0)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float* d = red + 3136 + ks * 16 + 8 * h + e;
+              *d = (w == 0 ? 0.f : *d) + vsum[ks][e];
+            }
+      }
+    }
+    __syncthreads();
+    const long bb = blockIdx.x;
+    for (int i = threadIdx.x; i < 3168; i += blockDim.x) {
+      const float v = red[i];
+      if (i < 2048) p.slab_w2[bb * 2048 + i] = v;
+      else if (i < 3072) p.slab_u[bb * 1024 + i - 2048] = v;
+      else if (i < 3136) p.slab_b2[bb * 64 + i - 3072] = v;
+      else p.slab_v[bb * 32 + i - 3136] = v;
+    }
   }
   if constexpr (CMODE == CM_LNBWD) {  // LN weight / bias gradient partials: lanes sharing ccol, then the 4 waves
     constexpr int G = 4 * NT;
@@ -1359,6 +1509,39 @@ int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const voi
     gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC, H><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
   });
   return check_launch("dgrad_sg_rc");
+}
+
+size_t nbp_dgrad_sg_rc_wg_workspace_floats(long M, int N) {
+  return N == 32 ? (size_t)skinny_blocks(M) * (2048 + 1024 + 64 + 32) : 0;
+}
+
+int nbp_dgrad_sg_rc_wg(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2,
+                       const float* b2, void* C, int M, int N, int K, float* U, float* V, float* dW2, float* db2,
+                       float* ws, size_t ws_floats, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(A && Wt && A2 && W2 && b2 && C && U && V && dW2 && db2 && ws && M > 0,
+              "nbp_dgrad_sg_rc_wg: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_sg_rc_wg: 16-bit storage (dtype 1 bf16 / 2 fp16)");
+  NBP_REQUIRE(N == 32 && K == 32 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_sg_rc_wg: N = K = 32 (N=%d K=%d)", N, K);
+  const long nb = skinny_blocks(M);
+  NBP_REQUIRE(ws_floats >= nbp_dgrad_sg_rc_wg_workspace_floats(M, N), "nbp_dgrad_sg_rc_wg: workspace too small");
+  float* sw2 = ws;
+  float* su = sw2 + nb * 2048;
+  float* sb2 = su + nb * 1024;
+  float* sv = sb2 + nb * 64;
+  NBP_DISPATCH_H(dtype, {
+    SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, nullptr, 1, reinterpret_cast<const H*>(Wt), ldb,
+                 reinterpret_cast<H*>(C), 2L * N, M, N, K, nullptr, nullptr, nullptr, nullptr,
+                 nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
+                 reinterpret_cast<const H*>(A2), reinterpret_cast<const H*>(W2), b2, su, sv, sw2, sb2};
+    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC, H, true><<<dim3((unsigned)nb), 256, 0, S(s)>>>(p);
+  });
+  int rc = check_launch("dgrad_sg_rc_wg");
+  if (rc) return rc;
+  // the block partials reduce with the stage's deferred reductions (nbp_wgrad_f32's semantics)
+  if ((rc = nbp_reduce_slab(sw2, (int)nb, 2L * N * K, dW2, s))) return rc;
+  if ((rc = nbp_reduce_slab(sb2, (int)nb, 2L * N, db2, s))) return rc;
+  if ((rc = nbp_reduce_slab(su, (int)nb, (long)N * N, U, s))) return rc;
+  return nbp_reduce_slab(sv, (int)nb, N, V, s);
 }
 
 int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int ndesc, void* out_t, int dtype,

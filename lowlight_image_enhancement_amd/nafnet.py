@@ -117,6 +117,9 @@ class NAFNet(nn.Module):
         self.sg_rc = os.environ.get("NBP_SG_RC", "1") != "0"
         # the rebuild lives in the skinny GEMM path (NBP_SKINNY=0 turns that path off, and with it the t4 drop)
         self.sg_rc = self.sg_rc and os.environ.get("NBP_SKINNY", "1")[:1] != "0"
+        # ... and with it folds conv5's U / V and conv4's weight / bias gradients into the same pass over dout / n2 /
+        # dt (nbp_dgrad_sg_rc_wg) -- NBP_SG_RC_WG=0 leaves them to separate nbp_wgrad_f32 launches
+        self.sg_rc_wg = os.environ.get("NBP_SG_RC_WG", "1") != "0"
         self._ln_carry = None
         self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
         self._side_used: Optional[torch.cuda.Stream] = None
@@ -654,11 +657,20 @@ class NAFNet(nn.Module):
         # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
         dt4 = E(M, 2 * c)
         folded = len(Wt) == 3 and self.fold_ls  # gamma / beta already in the transposed bf16 weights
+        U5, V5 = F(c * c), F(c)
+        wg_folded = False
         if dt != 0:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises
             if S["t4"] is None:  # t4 = conv4(n2) rebuilt per tile inside the dgrad (level 0, folded layer scale)
                 assert folded and c == 32
-                call("dgrad_sg_rc", dout, c, self._slice(Wt[2], pre + "conv5.weight"), c, S["n2"],
-                     self._slice(Wt[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"), dt4, M, c, c, dt)
+                args = (dout, c, self._slice(Wt[2], pre + "conv5.weight"), c, S["n2"],
+                        self._slice(Wt[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"), dt4, M, c, c)
+                if self.sg_rc_wg:  # + U5 / V5 and conv4's dW / db from the same tiles
+                    n_ws = query("dgrad_sg_rc_wg_workspace_floats", M, c)
+                    call("dgrad_sg_rc_wg", *args, U5, V5, self._slice(dflat, pre + "conv4.weight"),
+                         self._slice(dflat, pre + "conv4.bias"), F(n_ws), n_ws, dt)
+                    wg_folded = True
+                else:
+                    call("dgrad_sg_rc", *args, dt)
             elif folded:
                 self._mm(Wt, dout, c, AM_PLAIN, None, 1, pre + "conv5.weight", dt4, 2 * c, CM_SGBWD, M, c, c,
                          R=S["t4"], dgrad=True)
@@ -671,8 +683,8 @@ class NAFNet(nn.Module):
                      M, c, c, dgrad=True)
             call("sg_bwd", dg2, S["t4"], dt4, M, c, 1, dt)
         # at C >= 128 the wide weight gradients below are queued into the level's grouped launch (_walk_backward)
-        U5, V5 = F(c * c), F(c)
-        self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
+        if not wg_folded:
+            self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
         call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
              self._slice(P, pre + "gamma"), self._slice(dflat, pre + "conv5.weight"),
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
@@ -681,8 +693,9 @@ class NAFNet(nn.Module):
         fuse_ln = dt != 0 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
                                (c == 256 and self.fuse_ln256 in ("1", "bwd")))
         dy = E(M, c)
-        self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
-                    self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
+        if not wg_folded:
+            self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
+                        self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
         if fuse_ln:
             self._dgrad_ln(Wt, dflat, P, pre, "conv4.weight", "norm2", dt4, S["y"].reshape(M, c), S["st2"], dout, dy,
                            M, c)

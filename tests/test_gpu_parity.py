@@ -767,6 +767,7 @@ def test_sg_recompute_network_bitwise(dev):
         net.flat.add_(torch.randn_like(net.flat) * 0.05)
     x = torch.rand(2, 3, 48, 80, device=dev)
     grads = []
+    net.sg_rc_wg = False  # the weight-gradient fold changes fp32 summation order (its own test below)
     for rc in (True, False):
         net.sg_rc = rc
         net.flat.grad = None
@@ -779,6 +780,71 @@ def test_sg_recompute_network_bitwise(dev):
     out_nt, _ = net.exec_forward(x, save=False)
     out_t, _ = net.exec_forward(x, save=True)
     assert torch.equal(out_nt, out_t)
+
+
+@pytest.mark.parametrize("M,dtype", [(32, 1), (2 * 37 * 41, 1), (64 * 96, 2), (5 * 32 + 7, 2)])
+def test_dgrad_sg_rc_weight_grad_fold(dev, M, dtype):
+    """nbp_dgrad_sg_rc_wg: dt4 bit for bit nbp_dgrad_sg_rc's, plus U = dout^T g, V = colsum dout, dW4 = dt4^T n2,
+    db4 = colsum dt4 (g = the forward's stored gate map, dt4 = the stored output) within fp32 summation order of
+    the separate nbp_wgrad_f32 launches and of a float64 reference."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    ht = torch.bfloat16 if dtype == 1 else torch.float16
+    gen = torch.Generator(device=dev).manual_seed(M + dtype)
+    c = 32
+    n2 = torch.randn(M, c, device=dev, generator=gen).to(ht)
+    W4 = (torch.randn(2 * c, c, device=dev, generator=gen) / c ** 0.5).to(ht)
+    b4 = torch.randn(2 * c, device=dev, generator=gen) * 0.1
+    g2 = torch.empty(M, c, device=dev, dtype=ht)
+    call("gemm_bf16", n2, c, 0, None, 1, dtype, W4, c, None, 2 * c, 4, dtype, M, 2 * c, c, 0, 0, 0, b4, None, None,
+         g2)
+    dout = torch.randn(M, c, device=dev, generator=gen).to(ht)
+    W5t = (torch.randn(c, c, device=dev, generator=gen) / c ** 0.5).to(ht)
+    d0, d1 = (torch.full((M, 2 * c), float("nan"), device=dev, dtype=ht) for _ in range(2))
+    call("dgrad_sg_rc", dout, c, W5t, c, n2, W4, b4, d0, M, c, c, dtype)
+    U, V, dW, db = (torch.full((n,), float("nan"), device=dev) for n in (c * c, c, 2 * c * c, 2 * c))
+    n_ws = query("dgrad_sg_rc_wg_workspace_floats", M, c)
+    ws = torch.full((n_ws,), float("nan"), device=dev)
+    call("dgrad_sg_rc_wg", dout, c, W5t, c, n2, W4, b4, d1, M, c, c, U, V, dW, db, ws, n_ws, dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(d0, d1)
+    # the separate launches the fold replaces
+    U0, V0, dW0, db0 = (torch.empty(n, device=dev) for n in (c * c, c, 2 * c * c, 2 * c))
+    for G, X, N, dw_, db_ in ((dout, g2, c, U0, V0), (d0, n2, 2 * c, dW0, db0)):
+        nw = query("wgrad_workspace_floats", M, N, c)
+        call("wgrad_f32", G, N, 0, X, c, 0, None, 1, M, N, c, 0, 0, 0, 0, dw_, db_, torch.empty(nw, device=dev), nw,
+             dtype)
+    ref = {"U": dout.double().t() @ g2.double(), "V": dout.double().sum(0), "dW": d0.double().t() @ n2.double(),
+           "db": d0.double().sum(0)}
+    for k, got, sep in (("U", U, U0), ("V", V, V0), ("dW", dW, dW0), ("db", db, db0)):
+        r = ref[k].reshape(-1).float()
+        scale = r.abs().max().item() + 1e-12
+        assert (got - r).abs().max().item() <= 2e-5 * scale * max(1.0, (M / 1024) ** 0.5), k
+        assert (got - sep).abs().max().item() <= 2e-5 * scale * max(1.0, (M / 1024) ** 0.5), k
+
+
+def test_sg_rc_weight_grad_fold_network(dev):
+    """Whole bf16 training backward with the level-0 weight gradients folded into the conv5 dgrad (default) vs the
+    separate launches: identical outputs, parameter gradients within fp32 summation order."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    torch.manual_seed(4)
+    net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[2, 1], middle_blk_num=1,
+                           dec_blk_nums=[1, 2]).to(dev)
+    net.precision = "bf16"
+    with torch.no_grad():
+        net.flat.add_(torch.randn_like(net.flat) * 0.05)
+    x = torch.rand(2, 3, 48, 80, device=dev)
+    grads = []
+    for wg in (True, False):
+        net.sg_rc_wg = wg
+        net.flat.grad = None
+        out = net(x)
+        out.square().mean().backward()
+        grads.append((out.detach().clone(), net.flat.grad.clone()))
+    net.sg_rc_wg = True
+    assert torch.equal(grads[0][0], grads[1][0])
+    for k, e in net.entries.items():
+        a, b = (g[1][e.offset:e.offset + e.numel] for g in grads)
+        assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-12, k
 
 
 @pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
