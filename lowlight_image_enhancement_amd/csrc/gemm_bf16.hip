@@ -1238,9 +1238,33 @@ __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long*
 // NBP_GLDS: 0 = register-staged tiles only, 2 / 3 = LDS-DMA ring depth for 16-bit A (A/B measurement; read per launch
 // so a test can compare both paths in one process).  Default 2: at the deep-level shapes (scripts/gemm_probe.py) the
 // 3-deep ring's extra LDS costs more in blocks per CU than the second tile in flight buys.
+// Unset (default): chosen per launch by glds_auto_depth.
 int glds_depth() {
   const char* e = getenv("NBP_GLDS");
-  return e ? atoi(e) : 2;
+  return e ? atoi(e) : -1;
+}
+
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// Auto ring depth: the deepest ring (<= 4, <= nmax) with which every CU still holds all the blocks the grid gives it
+// (LDS per block = max(depth x stage, fp32 C staging)).  The small-grid deep-level GEMMs (2 blocks per CU, 8 K-steps,
+// memory-latency bound) get 3 / 4 tiles in flight; large grids keep 2 and their blocks per CU.
+int glds_auto_depth(long blocks, int stage_bytes, int c_bytes, int nmax) {
+  const long per_cu = (blocks + cu_count() - 1) / cu_count();
+  for (int d = nmax; d > 2; --d) {
+    const long lds = (long)d * stage_bytes > c_bytes ? (long)d * stage_bytes : c_bytes;
+    if (per_cu * lds <= 160L * 1024) return d;
+  }
+  return 2;
 }
 
 // NBP_GEMM_WAVES: 8 (default: 2 x 4 waves, two per SIMD, on tiles with BN >= 128) or 4 (2 x 2) for the LDS-DMA
@@ -1254,7 +1278,8 @@ template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC, typena
 void launch(const GemmPB& p, hipStream_t st) {
   dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
   if constexpr (sizeof(TA) == 2 && (AMODE == AM_PLAIN || AMODE == AM_SCALE || AMODE == AM_S2D || AMODE == AM_IM2COL)) {
-    const int ns = glds_depth();
+    const int ns_env = glds_depth();
+    const int ns = ns_env < 0 ? 2 : ns_env;
     // 16-byte aligned sources (lda, ldb, cs multiples of 8); a tile's rows in one image for the per-image scale
     const bool ok = ns >= 2 && p.K > 32 && p.ldb % 8 == 0 &&
                     (AMODE == AM_S2D || AMODE == AM_IM2COL ? p.cs % 8 == 0 : p.lda % 8 == 0) &&
@@ -1263,7 +1288,7 @@ void launch(const GemmPB& p, hipStream_t st) {
       // the ring depth the tile's LDS allows (stage = (BM + BN) x 128 B + scales; the fp32 C staging must fit too)
       constexpr int STB = (BM + BN) * 128 + (AMODE == AM_SCALE ? 256 : 0), CB = BM * (BN + 4) * 4;
       constexpr int NMAX = 4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
-      const int nd = ns < NMAX ? ns : NMAX;
+      const int nd = ns_env < 0 ? glds_auto_depth((long)grid.x * grid.y, STB, CB, NMAX) : (ns < NMAX ? ns : NMAX);
       if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
         if (gemm_waves() == 8) {  // 2 x 4 waves of (BM / 2) x (BN / 4): two waves per SIMD
           if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
@@ -1308,7 +1333,7 @@ bool launch_conv_big(const GemmPB& p, hipStream_t st) {
                 CMODE != CM_RESLN) {
     const int ns = glds_depth();
     const int ct = conv_tile();
-    if (!(ct & (p.N <= 64 ? 1 : 2)) || ns < 2 || p.K <= 32 || p.ldb % 8 || p.cs % 8 ||
+    if (!(ct & (p.N <= 64 ? 1 : 2)) || (ns >= 0 && ns < 2) || p.K <= 32 || p.ldb % 8 || p.cs % 8 ||
         (long)cdiv(p.M, 256) * cdiv(p.N, 128) < 256)
       return false;
     if (p.N <= 64) {
