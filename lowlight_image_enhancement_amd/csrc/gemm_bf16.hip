@@ -55,6 +55,8 @@ struct GemmPB {
   // AM_CONV (general KH x KW / stride / zero-pad implicit GEMM): gh x gw = the output map, ih x iw = the input map,
   // k = (ki * kw + kj) * cs + c
   int kh, kw, stride, pad, ih, iw;
+  // AM_IM2COL: the K-tiles lie inside one tap (Cin % 64 == 0): the DMA issue takes the tap per stage
+  int tap_tile;
 };
 
 __device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
@@ -588,14 +590,29 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
   asm volatile("" : "+s"(zp));
 
   const int nk = (K + BK - 1) / BK;
+  // IM2COL with Cin a multiple of BK: a K-tile lies inside one tap, so the tap (and its pixel offset) is per stage, not
+  // per lane -- no per-lane integer division in the DMA issue
+  const bool tap_tile = AMODE == AM_IM2COL && p.tap_tile != 0;
   auto issue = [&](int t) {
     unsigned char* st = smem + (t % NS) * ST_BYTES;
     const int k0 = t * BK;
+    int tap_off = 0, tap_c0 = 0, tap_di = 0, tap_dj = 0;
+    if (AMODE == AM_IM2COL && tap_tile) {
+      const int t9 = k0 / p.cs;
+      tap_c0 = k0 - t9 * p.cs;
+      tap_di = t9 / 3 - 1;
+      tap_dj = t9 % 3 - 1;
+      tap_off = tap_di * p.gw + tap_dj;
+    }
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const int k = k0 + a_kof[i];
       const void* src = zp;
-      if (a_m[i] < M && k < K) {
+      if (AMODE == AM_IM2COL && tap_tile) {
+        const int ii = a_i[i] + tap_di, jj = a_j[i] + tap_dj;
+        if (a_m[i] < M && k < K && ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
+          src = A + ((long)a_m[i] + tap_off) * p.cs + tap_c0 + a_kof[i];
+      } else if (a_m[i] < M && k < K) {
         if constexpr (AMODE == AM_S2D) {
           const int q = k / p.cs, c = k - q * p.cs;
           src = A + ((long)(a_b[i] * 2 * p.gh + 2 * a_i[i] + (q >> 1)) * (2 * p.gw) + 2 * a_j[i] + (q & 1)) * p.cs + c;
@@ -1587,6 +1604,12 @@ int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int
 // epi: mode 0 bias + ReLU, 1 bias only, 2 ReLU-mask by R (y = acc where R > 0 else 0; no bias).  x, w, R and a
 // 16-bit y share the type `dtype` (1 bf16, 2 fp16); y is that type (y_dtype 1) or fp32 (y_dtype 0, mode 1 only).
 // Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
+// NBP_IM2COL_TAP=0: per-lane tap division in the 3x3 conv's DMA issue (A/B measurement; read per launch)
+static bool im2col_tap_tile() {
+  const char* e = getenv("NBP_IM2COL_TAP");
+  return !(e && e[0] == '0');
+}
+
 int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
                      const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0, "nbp_conv3x3_bf16: bad args");
@@ -1599,6 +1622,7 @@ int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w,
   NBP_REQUIRE(M < (1L << 31), "nbp_conv3x3_bf16: too many pixels");
   GemmPB p{x, 0, nullptr, 1, w, 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
            mode == 2 ? nullptr : bias, mode == 2 ? R : nullptr, nullptr, nullptr};
+  p.tap_tile = Cin % 64 == 0 && im2col_tap_tile();
   hipStream_t st = S(s);
   if (dtype == 2) {
     using T16 = _Float16;

@@ -16,8 +16,11 @@ def run_modes(fn):
     outs = {}
     old = os.environ.get("NBP_GLDS")
     try:
-        for ns in ("0", "2", "3", "4"):
-            os.environ["NBP_GLDS"] = ns
+        for ns in ("0", "2", "3", "4", "auto"):  # auto (unset): the depth chosen per launch from the grid
+            if ns == "auto":
+                os.environ.pop("NBP_GLDS", None)
+            else:
+                os.environ["NBP_GLDS"] = ns
             outs[ns] = [t.clone() for t in fn()]
             torch.cuda.synchronize()
     finally:
@@ -25,7 +28,7 @@ def run_modes(fn):
             os.environ.pop("NBP_GLDS", None)
         else:
             os.environ["NBP_GLDS"] = old
-    for ns in ("2", "3", "4"):
+    for ns in ("2", "3", "4", "auto"):
         for a, b in zip(outs["0"], outs[ns]):
             assert torch.equal(a, b), f"NBP_GLDS={ns} differs from the register-staged kernel"
 
@@ -114,6 +117,15 @@ def test_glds_conv3x3(dev, B, H, W, Cin, Cout):
         call("conv3x3_bf16", x, B, H, W, Cin, w, Cout, None, 2, y, ym, 1, 1)
         return y, ym
     run_modes(fn)
+    # the per-stage tap of the DMA issue (Cin % 64 == 0, default) vs the per-lane division
+    ref = [t.clone() for t in fn()]
+    os.environ["NBP_IM2COL_TAP"] = "0"
+    try:
+        alt = [t.clone() for t in fn()]
+    finally:
+        os.environ.pop("NBP_IM2COL_TAP", None)
+    for a, b_ in zip(ref, alt):
+        assert torch.equal(a, b_)
 
 
 @pytest.mark.parametrize("M,N,K,amode", [(4096, 256, 256, 2), (16384, 128, 256, 0), (333, 256, 512, 0)])
