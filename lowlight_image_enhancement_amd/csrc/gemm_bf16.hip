@@ -5,1409 +5,8 @@
 // (space-to-depth gather for the down conv / up-conv dgrad, per-image column scale for SCA, depth-to-space scatter
 // + residual for the up conv).  Weights come from a per-step bf16 copy of the flat parameter buffer; dgrads use
 // the transposed copy so every launch is NT.
-#include <hip/hip_bf16.h>
-#include <stdlib.h>
+#include "gemm16_impl.h"
 
-#include "nbp_common.h"
-
-using namespace nbp;
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-namespace {
-
-// A modes: plain rows, space-to-depth gather, per-(image, column) scale, and 3x3 neighbourhood gather (implicit GEMM
-// of a zero-padded 3x3 conv over an NHWC map: row m = pixel, k = tap * Cin + c with gh = H, gw = W, cs = Cin).
-// C modes: plain, depth-to-space scatter, bias + ReLU, ReLU-mask by R (C = acc where R > 0, else 0), SimpleGate
-// forward (C = t with channel pairs (c, C+c) interleaved, and pre <- g = t[2c] * t[2c+1]) and SimpleGate backward
-// (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
-enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3, AM_CONV = 4 };
-enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7,
-       CM_CHANDOT = 8, CM_SGBWD_RC = 9 };
-
-struct GemmPB {
-  const void* A;
-  long lda;
-  const float* a_scale;
-  int rows_per_img;
-  const void* B;  // 16-bit weights (the kernel's operand type H)
-  long ldb;
-  void* C;
-  long ldc;
-  int M, N, K;
-  int gh, gw, cs;
-  const float* bias;
-  const void* R;
-  const float* rscale;
-  void* pre;
-  // CM_RESLN (tiled, N == BN == 128): the LayerNorm2d forward of each stored C row in the epilogue
-  const float* lnw;
-  const float* lnb;
-  void* nout;
-  float2* stats;
-  float eps;
-  // CM_LNBWD (tiled, N == BN == 128): R = the LN input x, stats_in = (mu, den), lnw, dres; LN weight / bias gradient
-  // partials per 64-row tile into slab_w / slab_b [M / 64][N]
-  const float2* stats_in;
-  const void* dres;
-  float* slab_w;
-  float* slab_b;
-  // AM_CONV (general KH x KW / stride / zero-pad implicit GEMM): gh x gw = the output map, ih x iw = the input map,
-  // k = (ki * kw + kj) * cs + c
-  int kh, kw, stride, pad, ih, iw;
-  // AM_IM2COL: the K-tiles lie inside one tap (Cin % 64 == 0): the DMA issue takes the tap per stage
-  int tap_tile;
-};
-
-__device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
-  const int per = gh * gw;
-  const int b = m / per, rem = m - b * per;
-  const int i = rem / gw, j = rem - i * gw;
-  const int q = k / cs, c = k - q * cs;
-  const int kh = q >> 1, kw = q & 1;
-  return ((long)(b * 2 * gh + 2 * i + kh) * (2 * gw) + 2 * j + kw) * cs + c;
-}
-
-template <typename T>
-__device__ __forceinline__ float ldf(const void* p, long off) {
-  return (float)reinterpret_cast<const T*>(p)[off];
-}
-template <typename T>
-__device__ __forceinline__ void stf(void* p, long off, float v) {
-  reinterpret_cast<T*>(p)[off] = (T)v;
-}
-
-// 8 consecutive elements of A at element offset `off`, optionally scaled, as the 16-bit operand type H
-template <typename TA, int AMODE, typename H>
-__device__ __forceinline__ vec_t<H, 8> load8(const void* A, long off, const float* scale) {
-  vec_t<H, 8> r;
-  if constexpr (sizeof(TA) == 4) {
-    const float4 a = ld4(reinterpret_cast<const float*>(A) + off);
-    const float4 b = ld4(reinterpret_cast<const float*>(A) + off + 4);
-    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    if (AMODE == AM_SCALE) {
-      const float4 s0 = ld4(scale), s1 = ld4(scale + 4);
-      v[0] *= s0.x; v[1] *= s0.y; v[2] *= s0.z; v[3] *= s0.w;
-      v[4] *= s1.x; v[5] *= s1.y; v[6] *= s1.z; v[7] *= s1.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (H)v[j];
-  } else {
-    static_assert(sizeof(TA) == 2, "16-bit A is the operand type");
-    r = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(A) + off);
-    if (AMODE == AM_SCALE) {
-      const float4 s0 = ld4(scale), s1 = ld4(scale + 4);
-      const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) r[j] = (H)((float)r[j] * s[j]);
-    }
-  }
-  return r;
-}
-
-// 8 consecutive fp32 values <-> storage type (16 bytes of 16-bit / 32 bytes of fp32)
-template <typename T>
-__device__ __forceinline__ void ld8f(const void* base, long off, float* v) {
-  if constexpr (sizeof(T) == 4) {
-    const float4 a = ld4(reinterpret_cast<const float*>(base) + off), b = ld4(reinterpret_cast<const float*>(base) + off + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-  } else {
-    const vec_t<T, 8> r = *reinterpret_cast<const vec_t<T, 8>*>(reinterpret_cast<const T*>(base) + off);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)r[j];
-  }
-}
-template <typename T>
-__device__ __forceinline__ void st8f(void* base, long off, const float* v) {
-  if constexpr (sizeof(T) == 4) {
-    float* d = reinterpret_cast<float*>(base) + off;
-    st4(d, make_float4(v[0], v[1], v[2], v[3]));
-    st4(d + 4, make_float4(v[4], v[5], v[6], v[7]));
-  } else {
-    vec_t<T, 8> r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (T)v[j];
-    *reinterpret_cast<vec_t<T, 8>*>(reinterpret_cast<T*>(base) + off) = r;
-  }
-}
-
-// Epilogue of the tiled kernels: the fp32 accumulators (4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32
-// MFMA tiles) are staged through LDS (smem, aliasing the operand buffers; the caller has finished every read of them)
-// so that bias / pre-activation / residual R + rscale * v / the C store all move 8 consecutive columns per thread.
-// WM x WN waves (default 2 x 2), each (BM / WM) x (BN / WN) of 32 x 32 MFMA tiles; NT = 64 WM WN threads.
-template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2, int WM = 2>
-__device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / (32 * WM)][BN / (32 * WN)],
-                                              unsigned char* smem, int m0, int n0) {
-  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN), NT = 64 * WM * WN;
-  static_assert((WN == 2 && WM == 2) || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT),
-                "cross-wave reductions assume 2 x 2 waves");
-  constexpr int CLS = BN + 4;  // fp32 C-tile row stride
-  float* Cs = reinterpret_cast<float*>(smem);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int M = p.M, N = p.N;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * (BN / WN) + j * 32 + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * (BM / WM) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        Cs[row * CLS + col] = acc[i][j][r];
-      }
-    }
-  __syncthreads();
-  constexpr int G8 = BN / 8;
-  const bool vec = (N % 8 == 0) && (CMODE == CM_D2S || p.ldc % 8 == 0);
-  // CM_CHANDOT (SCA backward, NAFNet_arch.py:39-41): besides C, per-column partial sums over the tile's rows of
-  // C (bf16-rounded) * R (the SimpleGate output g) -> pre[image][tile within image][col] (fp32), the per-image channel
-  // dot img_chan_dot computes, without re-reading C.  The launcher guarantees BM | rows_per_img.
-  float cd[8], cb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) cd[j] = cb[j] = 0.f;
-  for (int e = tid; e < BM * G8; e += NT) {
-    const int row = e / G8, c8 = (e % G8) * 8;
-    const int grow = m0 + row, gcol = n0 + c8;
-    if (grow >= M || gcol >= N) continue;
-    float v[8];
-    const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
-    v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
-    if constexpr (CMODE == CM_LNBWD) {  // dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * lnw
-      static_assert(BN == 128 || BN == 256, "CM_LNBWD (tiled): full-row tiles");
-      const long off = (long)grow * N + gcol;
-      float xv[8], rv[8];
-      ld8f<TC>(p.R, off, xv);
-      ld8f<TC>(p.dres, off, rv);
-      const float2 st = p.stats_in[grow];
-      const float inv = 1.f / st.y;
-      const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4);
-      const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      float yh[8], sg = 0.f, sgy = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        yh[j] = (xv[j] - st.x) * inv;
-        const float gg = v[j] * lw[j];
-        sg += gg;
-        sgy = fmaf(gg, yh[j], sgy);
-        cd[j] = fmaf(v[j], yh[j], cd[j]);  // dlnw partial
-        cb[j] += v[j];                      // dlnb partial
-      }
-      sg = group_sum<G8>(sg);
-      sgy = group_sum<G8>(sgy);
-      const float mg = sg / (float)N, mgy = sgy / (float)N;
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[j] * lw[j] - yh[j] * mgy - mg) * inv + rv[j];
-      st8f<TC>(p.C, off, o);
-      continue;
-    }
-    if constexpr (CMODE == CM_CHANDOT) {
-      const long off = (long)grow * p.ldc + gcol;
-      float gv[8];
-      ld8f<TC>(p.R, off, gv);
-      vec_t<H, 8> o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = (H)v[j];
-        cd[j] = fmaf((float)o[j], gv[j], cd[j]);
-      }
-      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.C) + off) = o;
-      continue;
-    }
-    if (CMODE == CM_SGBWD) {
-      // 8 gate channels -> 16 interleaved (t, dt) values
-      const long off = (long)grow * p.ldc + 2 * gcol;
-      if (vec) {
-        float ta[8], tb[8], oa[8], ob[8];
-        ld8f<TC>(p.R, off, ta);
-        ld8f<TC>(p.R, off + 8, tb);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          oa[2 * j] = v[j] * ta[2 * j + 1];
-          oa[2 * j + 1] = v[j] * ta[2 * j];
-          ob[2 * j] = v[4 + j] * tb[2 * j + 1];
-          ob[2 * j + 1] = v[4 + j] * tb[2 * j];
-        }
-        st8f<TC>(p.C, off, oa);
-        st8f<TC>(p.C, off + 8, ob);
-      } else {
-        for (int j = 0; j < 8 && gcol + j < N; ++j) {
-          const float t0 = ldf<TC>(p.R, off + 2 * j), t1 = ldf<TC>(p.R, off + 2 * j + 1);
-          stf<TC>(p.C, off + 2 * j, v[j] * t1);
-          stf<TC>(p.C, off + 2 * j + 1, v[j] * t0);
-        }
-      }
-      continue;
-    }
-    if (vec) {
-      const long off = CMODE == CM_D2S ? s2d_off(grow, gcol, p.gh, p.gw, p.cs) : (long)grow * p.ldc + gcol;
-      if (p.bias) {
-        const float4 b0 = ld4(p.bias + gcol), b1 = ld4(p.bias + gcol + 4);
-        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-      }
-      if (CMODE == CM_RELU) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
-      } else if (CMODE == CM_MASK) {
-        float rv[8];
-        ld8f<TC>(p.R, off, rv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = rv[j] > 0.f ? v[j] : 0.f;
-      }
-      if (CMODE == CM_SG) {
-        float g[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) g[j] = v[2 * j] * v[2 * j + 1];
-        // 4 gate values (8 bytes of bf16 / 16 of fp32) at row grow, column gcol / 2 of the [M][N/2] map
-        if constexpr (sizeof(TC) == 4) {
-          st4(reinterpret_cast<float*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2, make_float4(g[0], g[1], g[2], g[3]));
-        } else {
-          vec_t<H, 4> o;
-          o[0] = (H)g[0]; o[1] = (H)g[1]; o[2] = (H)g[2]; o[3] = (H)g[3];
-          *reinterpret_cast<vec_t<H, 4>*>(reinterpret_cast<H*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2) = o;
-        }
-      } else if (p.pre) {
-        st8f<TC>(p.pre, off, v);
-      }
-      if (CMODE != CM_MASK && p.R) {
-        float rv[8];
-        ld8f<TC>(p.R, off, rv);
-        if (p.rscale) {
-          const float4 s0 = ld4(p.rscale + gcol), s1 = ld4(p.rscale + gcol + 4);
-          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = rv[j] + sc[j] * v[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = rv[j] + v[j];
-        }
-      }
-      st8f<TC>(p.C, off, v);
-      if constexpr (CMODE == CM_RESLN) {  // the row's G8 chunks are G8 consecutive lanes (BN = N): group sums
-        static_assert(BN == 128 || BN == 256, "CM_RESLN (tiled): full-row tiles");
-        float xv[8], sm = 0.f, q = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xv[j] = (float)(H)v[j];
-          sm += xv[j];
-        }
-        sm = group_sum<G8>(sm);
-        const float mu = sm / (float)N;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = xv[j] - mu;
-          q = fmaf(d, d, q);
-        }
-        q = group_sum<G8>(q);
-        const float dd = sqrtf(q / (float)N + p.eps), inv = 1.f / dd;
-        const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4), b0 = ld4(p.lnb + gcol), b1 = ld4(p.lnb + gcol + 4);
-        const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        const float lb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        float o[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaf(lw[j], (xv[j] - mu) * inv, lb[j]);
-        st8f<TC>(p.nout, (long)grow * N + gcol, o);
-        if (gcol == 0) p.stats[grow] = make_float2(mu, dd);
-      }
-    } else {
-      for (int j = 0; j < 8 && gcol + j < N; ++j) {
-        const int col = gcol + j;
-        const long off = CMODE == CM_D2S ? s2d_off(grow, col, p.gh, p.gw, p.cs) : (long)grow * p.ldc + col;
-        float x = v[j] + (p.bias ? p.bias[col] : 0.f);
-        if (CMODE == CM_RELU) x = fmaxf(x, 0.f);
-        if (CMODE == CM_MASK) x = ldf<TC>(p.R, off) > 0.f ? x : 0.f;
-        if (CMODE == CM_SG) {
-          v[j] = x;
-          if (j & 1) stf<TC>(p.pre, (long)grow * (p.ldc / 2) + col / 2, v[j - 1] * x);
-        } else if (p.pre) {
-          stf<TC>(p.pre, off, x);
-        }
-        if (CMODE != CM_MASK && p.R) x = ldf<TC>(p.R, off) + (p.rscale ? p.rscale[col] : 1.f) * x;
-        stf<TC>(p.C, off, x);
-      }
-    }
-  }
-  if constexpr (CMODE == CM_LNBWD) {  // threads sharing a column chunk: lanes G8 apart, then the 4 waves (fixed order)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int o = G8; o < 64; o <<= 1) {
-        cd[j] += __shfl_xor(cd[j], o, 64);
-        cb[j] += __shfl_xor(cb[j], o, 64);
-      }
-    __syncthreads();
-    if (lane < G8)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Cs[(wave * 2 + 0) * BN + lane * 8 + j] = cd[j];
-        Cs[(wave * 2 + 1) * BN + lane * 8 + j] = cb[j];
-      }
-    __syncthreads();
-    if (tid < BN) {
-      const float tw = ((Cs[0 * BN + tid] + Cs[2 * BN + tid]) + Cs[4 * BN + tid]) + Cs[6 * BN + tid];
-      const float tb = ((Cs[1 * BN + tid] + Cs[3 * BN + tid]) + Cs[5 * BN + tid]) + Cs[7 * BN + tid];
-      p.slab_w[(long)blockIdx.x * N + tid] = tw;
-      p.slab_b[(long)blockIdx.x * N + tid] = tb;
-    }
-  }
-  if constexpr (CMODE == CM_CHANDOT) {  // threads sharing a column chunk: lanes 8 apart, then the 4 waves (fixed order)
-    static_assert(G8 == 8 && BM == 64, "CM_CHANDOT: 64 x 64 tiles");
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      cd[j] += __shfl_xor(cd[j], 8, 64);
-      cd[j] += __shfl_xor(cd[j], 16, 64);
-      cd[j] += __shfl_xor(cd[j], 32, 64);
-    }
-    __syncthreads();
-    if (lane < 8)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Cs[wave * 64 + lane * 8 + j] = cd[j];
-    __syncthreads();
-    if (tid < 64 && n0 + tid < N) {
-      const int img = m0 / p.rows_per_img, chunk = (m0 - img * p.rows_per_img) / BM, chunks = p.rows_per_img / BM;
-      const float t = ((Cs[tid] + Cs[64 + tid]) + Cs[128 + tid]) + Cs[192 + tid];
-      reinterpret_cast<float*>(p.pre)[((long)img * chunks + chunk) * N + n0 + tid] = t;
-    }
-  }
-}
-
-// Register-staged tiled kernel (any A type / mode): 4 waves in a 2x2 arrangement, each (BM/2) x (BN/2) of 32x32 MFMA
-// tiles.  K-loop: BK-wide tiles, double-buffered LDS (one barrier per K step; the next tile's global loads are in
-// flight during the current tile's MFMAs).  Epilogue: gemm_epilogue.
-template <int BM, int BN, int BK, int AMODE, int CMODE, typename TA, typename TC, typename H>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
-  static_assert(sizeof(TA) == 4 || sizeof(TA) == sizeof(H), "A is fp32 or the operand type");
-  static_assert(sizeof(TC) == 4 || sizeof(TC) == sizeof(H), "C is fp32 or the operand type");
-  constexpr int LS = BK + 8;  // 80 / 144-byte LDS rows: conflict-free 16-byte fragment reads
-  constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int KC = BK / 8;  // 8-element chunks per tile row
-  constexpr int A_IT = BM * KC / 256, B_IT = BN * KC / 256;
-  constexpr int AB_BYTES = 2 * (BM + BN) * LS * 2;
-  constexpr int CLS = BN + 4;  // fp32 C-tile row stride
-  constexpr int C_BYTES = BM * CLS * 4;
-  constexpr int SM_BYTES = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
-  H* As = reinterpret_cast<H*>(smem);       // [2][BM][LS]
-  H* Bs = As + 2 * BM * LS;                       // [2][BN][LS]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int M = p.M, N = p.N, K = p.K;
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  // two register sets: with BK = 64 the loads of K-tiles t+1 and t+2 are in flight while tile t is multiplied
-  vec_t<H, 8> ra0[A_IT], rb0[B_IT], ra1[A_IT], rb1[B_IT];
-  auto load_tiles = [&](int k0, vec_t<H, 8>* ra, vec_t<H, 8>* rb) {
-#pragma unroll
-    for (int it = 0; it < A_IT; ++it) {
-      const int idx = tid + it * 256;
-      const int r = idx / KC, kc = idx % KC;
-      const int m = m0 + r, k = k0 + kc * 8;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (AMODE == AM_CONV) {
-        if (m < M && k < K) {
-          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, oi = rem / p.gw, oj = rem - oi * p.gw;
-          const int t = k / p.cs, c = k - t * p.cs, ki = t / p.kw, kj = t - ki * p.kw;
-          const int ii = oi * p.stride + ki - p.pad, jj = oj * p.stride + kj - p.pad;
-          if (ii >= 0 && ii < p.ih && jj >= 0 && jj < p.iw)
-            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.ih + ii) * p.iw + jj) * p.cs + c, nullptr);
-        }
-      } else if (AMODE == AM_IM2COL) {
-        if (m < M && k < K) {
-          const int per = p.gh * p.gw, b = m / per, rem = m - b * per, i = rem / p.gw, j = rem - i * p.gw;
-          const int t = k / p.cs, c = k - t * p.cs;
-          const int ii = i + t / 3 - 1, jj = j + t % 3 - 1;
-          if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
-            v = load8<TA, AM_PLAIN, H>(p.A, ((long)(b * p.gh + ii) * p.gw + jj) * p.cs + c, nullptr);
-        }
-      } else if (m < M && k < K) {
-        long off;
-        if (AMODE == AM_S2D) off = s2d_off(m, k, p.gh, p.gw, p.cs);
-        else off = (long)m * p.lda + k;
-        const float* sc = AMODE == AM_SCALE ? p.a_scale + (long)(m / p.rows_per_img) * K + k : nullptr;
-        v = load8<TA, AMODE, H>(p.A, off, sc);
-      }
-      ra[it] = v;
-    }
-#pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int idx = tid + it * 256;
-      const int r = idx / KC, kc = idx % KC;
-      const int n = n0 + r, k = k0 + kc * 8;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (n < N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.B) + (long)n * p.ldb + k);
-      rb[it] = v;
-    }
-  };
-  auto store_tiles = [&](int buf, const vec_t<H, 8>* ra, const vec_t<H, 8>* rb) {
-    H* a = As + buf * BM * LS;
-    H* b = Bs + buf * BN * LS;
-#pragma unroll
-    for (int it = 0; it < A_IT; ++it) {
-      const int idx = tid + it * 256;
-      *reinterpret_cast<vec_t<H, 8>*>(a + (idx / KC) * LS + (idx % KC) * 8) = ra[it];
-    }
-#pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int idx = tid + it * 256;
-      *reinterpret_cast<vec_t<H, 8>*>(b + (idx / KC) * LS + (idx % KC) * 8) = rb[it];
-    }
-  };
-  const int arow = wm * (BM / 2) + (lane & 31);
-  const int brow = wn * (BN / 2) + (lane & 31);
-  const int kh = (lane >> 5) * 8;
-  auto compute = [&](int buf) {
-    const H* a_s = As + buf * BM * LS;
-    const H* b_s = Bs + buf * BN * LS;
-#pragma unroll
-    for (int s = 0; s < BK; s += 16) {
-      vec_t<H, 8> a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (arow + i * 32) * LS + s + kh);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (brow + j * 32) * LS + s + kh);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
-    }
-  };
-
-  const int nk = (K + BK - 1) / BK;
-  if constexpr (BK == 32) {
-    // short K (one or two tiles): one register set, the next tile's loads in flight during the MFMAs
-    load_tiles(0, ra0, rb0);
-    store_tiles(0, ra0, rb0);
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < nk) load_tiles((t + 1) * BK, ra0, rb0);
-      compute(buf);
-      if (t + 1 < nk) store_tiles(buf ^ 1, ra0, rb0);
-      __syncthreads();
-    }
-  } else {
-    load_tiles(0, ra0, rb0);
-    store_tiles(0, ra0, rb0);
-    if (nk > 1) load_tiles(BK, ra1, rb1);
-    if (nk > 2) load_tiles(2 * BK, ra0, rb0);
-    __syncthreads();
-    // steady state, unrolled by two so each register set is addressed statically:
-    //   even step t: tile t in LDS buf 0, t+1 in set 1, t+2 in flight in set 0
-    //   odd step t+1: tile t+1 in LDS buf 1, t+2 in set 0, t+3 in flight in set 1
-    for (int t = 0; t < nk; t += 2) {
-      compute(0);
-      if (t + 1 < nk) {
-        store_tiles(1, ra1, rb1);
-        if (t + 3 < nk) load_tiles((t + 3) * BK, ra1, rb1);
-      }
-      __syncthreads();
-      if (t + 1 >= nk) break;
-      compute(1);
-      if (t + 2 < nk) {
-        store_tiles(0, ra0, rb0);
-        if (t + 4 < nk) load_tiles((t + 4) * BK, ra0, rb0);
-      }
-      __syncthreads();
-    }
-  }
-
-  gemm_epilogue<BM, BN, CMODE, TC, H>(p, acc, smem, m0, n0);
-}
-
-// ---------------------------------------------------------------- LDS-DMA tiled kernel (16-bit A)
-// Same tiles, fragment order and MFMA sequence as gemm_bf16_kernel (so the same accumulation order: results are
-// bitwise those of the register-staged kernel), but the operand tiles go global -> LDS with global_load_lds_dwordx4
-// (no VGPR staging, no ds_write pass) into an NS-deep ring: NS - 1 K-tiles are in flight while one is multiplied,
-// retired by a counted vmcnt and a raw s_barrier (a __syncthreads would drain the ring: vmcnt(0)).
-// Per stage: A [BM][64] then B [BN][64] of 128-byte rows, the 16-byte chunk c of row r at slot c ^ ((r >> 1) & 7)
-// (a glds instruction writes 1 KB lane-linearly, so the permutation is applied to each lane's SOURCE address; the
-// fragment reads, lanes 0..31 on rows r..r+31 at one chunk, then hit 16 distinct slots per ds_read_b128 lane group),
-// then for AM_SCALE the tile's 64 fp32 column scales (one 4-byte glds).  Out-of-range rows / columns / K tail and the
-// zero padding of AM_IM2COL read g_zero16 (LDS-DMA helpers: nbp_common.h).
-template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H, int WN = 2, int WM = 2>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
-  constexpr int BK = 64, NW = WM * WN;  // waves: WM along M x WN along N
-  constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
-  static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
-  constexpr int SC_BYTES = AMODE == AM_SCALE ? 256 : 0;
-  constexpr int ST_BYTES = A_BYTES + B_BYTES + SC_BYTES;
-  constexpr int GA = BM / (8 * NW), GB = BN / (8 * NW);  // 1-KB (8-row) glds instructions per wave per stage
-  static_assert(GA * 8 * NW == BM && GB * 8 * NW == BN, "DMA rows per wave");
-  constexpr int G = GA + GB + (AMODE == AM_SCALE ? 1 : 0);
-  constexpr int C_BYTES = BM * (BN + 4) * 4;
-  constexpr int SM_BYTES = NS * ST_BYTES > C_BYTES ? NS * ST_BYTES : C_BYTES;
-  static_assert(NS >= 2 && NS <= 4, "ring depth");
-  static_assert(SM_BYTES <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int M = p.M, N = p.N, K = p.K;
-  const H* A = reinterpret_cast<const H*>(p.A);
-  const H* B = reinterpret_cast<const H*>(p.B);
-  const int lr = lane >> 3, lc = lane & 7;
-
-  // this lane's source rows: instruction i covers tile rows (wave * GA + i) * 8 .. + 7, the lane row lr, chunk slot lc
-  int a_m[GA], a_kof[GA], a_b[GA], a_i[GA], a_j[GA];
-#pragma unroll
-  for (int i = 0; i < GA; ++i) {
-    const int r = (wave * GA + i) * 8 + lr;
-    a_m[i] = m0 + r;
-    a_kof[i] = 8 * (lc ^ ((r >> 1) & 7));
-    a_b[i] = a_i[i] = a_j[i] = 0;
-    if constexpr (AMODE == AM_S2D || AMODE == AM_IM2COL) {
-      const int per = p.gh * p.gw, m = a_m[i] < M ? a_m[i] : 0;
-      a_b[i] = m / per;
-      const int rem = m - a_b[i] * per;
-      a_i[i] = rem / p.gw;
-      a_j[i] = rem - a_i[i] * p.gw;
-    }
-  }
-  int b_n[GB], b_kof[GB];
-#pragma unroll
-  for (int i = 0; i < GB; ++i) {
-    const int r = (wave * GB + i) * 8 + lr;
-    b_n[i] = n0 + r;
-    b_kof[i] = 8 * (lc ^ ((r >> 1) & 7));
-  }
-  const float* sc_row = AMODE == AM_SCALE ? p.a_scale + (long)(m0 / p.rows_per_img) * K : nullptr;
-  // the zero page's address in registers (laundered through asm: otherwise re-loaded from the GOT at every use)
-  const void* zp = g_zero16;
-  asm volatile("" : "+s"(zp));
-
-  const int nk = (K + BK - 1) / BK;
-  // IM2COL with Cin a multiple of BK: a K-tile lies inside one tap, so the tap (and its pixel offset) is per stage, not
-  // per lane -- no per-lane integer division in the DMA issue
-  const bool tap_tile = AMODE == AM_IM2COL && p.tap_tile != 0;
-  auto issue = [&](int t) {
-    unsigned char* st = smem + (t % NS) * ST_BYTES;
-    const int k0 = t * BK;
-    int tap_off = 0, tap_c0 = 0, tap_di = 0, tap_dj = 0;
-    if (AMODE == AM_IM2COL && tap_tile) {
-      const int t9 = k0 / p.cs;
-      tap_c0 = k0 - t9 * p.cs;
-      tap_di = t9 / 3 - 1;
-      tap_dj = t9 % 3 - 1;
-      tap_off = tap_di * p.gw + tap_dj;
-    }
-#pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int k = k0 + a_kof[i];
-      const void* src = zp;
-      if (AMODE == AM_IM2COL && tap_tile) {
-        const int ii = a_i[i] + tap_di, jj = a_j[i] + tap_dj;
-        if (a_m[i] < M && k < K && ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
-          src = A + ((long)a_m[i] + tap_off) * p.cs + tap_c0 + a_kof[i];
-      } else if (a_m[i] < M && k < K) {
-        if constexpr (AMODE == AM_S2D) {
-          const int q = k / p.cs, c = k - q * p.cs;
-          src = A + ((long)(a_b[i] * 2 * p.gh + 2 * a_i[i] + (q >> 1)) * (2 * p.gw) + 2 * a_j[i] + (q & 1)) * p.cs + c;
-        } else if constexpr (AMODE == AM_IM2COL) {
-          const int t9 = k / p.cs, c = k - t9 * p.cs;
-          const int ii = a_i[i] + t9 / 3 - 1, jj = a_j[i] + t9 % 3 - 1;
-          if (ii >= 0 && ii < p.gh && jj >= 0 && jj < p.gw)
-            src = A + ((long)(a_b[i] * p.gh + ii) * p.gw + jj) * p.cs + c;
-        } else {
-          src = A + (long)a_m[i] * p.lda + k;
-        }
-      }
-      glds16(src, st + (wave * GA + i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < GB; ++i) {
-      const int k = k0 + b_kof[i];
-      const void* src = (b_n[i] < N && k < K) ? (const void*)(B + (long)b_n[i] * p.ldb + k) : zp;
-      glds16(src, st + A_BYTES + (wave * GB + i) * 1024);
-    }
-    if constexpr (AMODE == AM_SCALE) {  // every wave loads the same 64 scales (identical bytes, one instruction each)
-      const int k = k0 + lane;
-      glds4(k < K ? (const void*)(sc_row + k) : zp, st + A_BYTES + B_BYTES);
-    }
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int key = (lane >> 1) & 7;  // ((row >> 1) & 7) of every fragment row: rows are 32-aligned + (lane & 31)
-  auto compute = [&](int buf) {
-    const unsigned char* a_s = smem + buf * ST_BYTES;
-    const unsigned char* b_s = a_s + A_BYTES;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const int slot = ((2 * s + (lane >> 5)) ^ key) << 4;
-      vec_t<H, 8> a[TM], b[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        a[i] = *reinterpret_cast<const vec_t<H, 8>*>(a_s + (wm * (BM / WM) + i * 32 + (lane & 31)) * 128 + slot);
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        b[j] = *reinterpret_cast<const vec_t<H, 8>*>(b_s + (wn * (BN / WN) + j * 32 + (lane & 31)) * 128 + slot);
-      if constexpr (AMODE == AM_SCALE) {
-        const float* scs = reinterpret_cast<const float*>(b_s + B_BYTES) + s * 16 + (lane >> 5) * 8;
-        const float4 s0 = ld4(scs), s1 = ld4(scs + 4);
-        const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) a[i][e] = (H)((float)a[i][e] * sv[e]);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma32x32x16(a[i], b[j], acc[i][j]);
-    }
-  };
-
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) issue(t);
-  for (int t = 0; t < nk; ++t) {
-    // retire K-tile t (this wave's DMAs), leaving the later tiles of the ring in flight; the barrier then makes every
-    // wave's part of tile t visible and frees the stage read at step t - 1 for tile t + NS - 1
-    if (NS >= 4 && t + 2 < nk) wait_vm<2 * G>();
-    else if (NS >= 3 && t + 1 < nk) wait_vm<G>();
-    else wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + NS - 1 < nk) issue(t + NS - 1);
-    compute(t % NS);
-  }
-  __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
-  gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM>(p, acc, smem, m0, n0);
-}
-
-// ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
-// The transposed product C^T = W . A^T on 32x32x16 MFMA: the weight is the A-operand (kept in registers for the whole
-// launch: N, K <= 64), the pixel rows are the B-operand, loaded straight from global memory in fragment order (lane l
-// reads 16 bytes of row l & 31 — no LDS, no barriers).  Each wave streams 32-pixel tiles, prefetching the next tile's
-// fragments while the current one is multiplied; a lane ends up owning one pixel's channels (4 consecutive per
-// register group), so the epilogue (bias, layer-scale residual, SimpleGate forward / backward) runs in registers and
-// stores 8 / 16-byte pieces that complete whole rows in L2.
-template <typename H>
-struct SkinnyP {
-  const H* A;
-  long lda;
-  const float* a_scale;
-  int rows_per_img;
-  const H* W;
-  long ldw;
-  H* C;
-  long ldc;
-  int M, N, K;
-  const float* bias;
-  const H* R;
-  const float* rscale;
-  H* aux;
-  // CM_LNBWD (LayerNorm2d backward in the epilogue, arch_util.py:277-289): the GEMM output is dn; R = the LN input x,
-  // stats = (mu, sqrt(var + eps)) per row, lnw = the LN weight, dres = the residual-branch gradient added to dx;
-  // per-block partials of sum(dn * yhat) / sum(dn) go to slab_w / slab_b [grid][N]
-  const float2* stats;
-  const float* lnw;
-  const H* dres;
-  float* slab_w;
-  float* slab_b;
-  // CM_RESLN (bias + layer-scale residual, then the next LayerNorm2d forward, arch_util.py:266-275): C = the stored
-  // residual sum, nout = LN(C) with lnw / lnb_f, stats_out = (mu, sqrt(var + eps)) per row
-  const float* lnb_f;
-  H* nout;
-  float2* stats_out;
-  float eps;
-  // CM_SGBWD_RC (SimpleGate backward with the gate input recomputed): t = A2 W2^T + b2 (the conv4 forward, its
-  // output rows interleaved as stored, 2N columns) is rebuilt per tile on MFMA instead of being read from memory
-  const H* A2;
-  const H* W2;
-  const float* b2;
-  // WGF (with CM_SGBWD_RC at N = K = 32): the weight gradients that read this kernel's operands, per-block partials
-  // U = dout^T g (g = the SimpleGate output rebuilt from t), V = colsum dout, dW2 = C^T A2 (C = the stored dt), db2 =
-  // colsum C into slab_u [grid][N N], slab_v [grid][N], slab_w2 [grid][2N K], slab_b2 [grid][2N]
-  float* slab_u;
-  float* slab_v;
-  float* slab_w2;
-  float* slab_b2;
-};
-
-template <int NT, int KS, int AMODE, int CMODE, typename H, bool WGF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGF ? 2 : 1)))
-void gemm_skinny_kernel(SkinnyP<H> p) {
-  constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
-  constexpr bool RC = CMODE == CM_SGBWD_RC;
-  static_assert(!WGF || (RC && NT == 1 && KS == 2), "weight-gradient fold: level-0 conv5 dgrad (N = K = 32)");
-  constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : 8;  // bf16 row stride of the recomputed gate-input tile
-  __shared__ float stage[4][32 * LDT];
-  __shared__ __attribute__((aligned(16))) H stage2[4][32 * LDT2];
-  // WGF: the tile's dt (32 rows x 64, 192-byte rows: conflict-free ds_read_b64_tr_b16), later the block's reduction
-  __shared__ __attribute__((aligned(16))) H stage3[WGF ? 4 : 1][WGF ? 32 * 96 : 8];
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  float* tileS = stage[threadIdx.x >> 6];
-  H* tileT = stage2[threadIdx.x >> 6];
-  const int M = p.M, N = p.N, K = p.K;
-  // RC: the conv4 weight (2N rows, K = the conv4 input width = this GEMM's K) and bias in registers
-  constexpr int NT2 = RC ? 2 * NT : 1;
-  vec_t<H, 8> w2[NT2][KS];
-  float b2r[NT2][4][4];
-  if constexpr (RC) {
-#pragma unroll
-    for (int t = 0; t < NT2; ++t) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int n = t * 32 + r, k = ks * 16 + 8 * h;
-        vec_t<H, 8> v;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-        if (n < 2 * N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(p.W2 + (long)n * K + k);
-        w2[t][ks] = v;
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c = t * 32 + 8 * g + 4 * h + q;
-          b2r[t][g][q] = c < 2 * N ? p.b2[c] : 0.f;
-        }
-    }
-  }
-  vec_t<H, 8> w[NT][KS];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int n = t * 32 + r, k = ks * 16 + 8 * h;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (n < N && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(p.W + (long)n * p.ldw + k);
-      w[t][ks] = v;
-    }
-  // coalesced epilogue geometry: chunks of 8 output elements, row-major over the 32-row tile.  The output row holds
-  // N elements (2N for the SimpleGate backward), so a lane's chunk column is fixed across its chunks.
-  const int outw = (CMODE == CM_SGBWD || RC ? 2 : 1) * N;
-  const int cpr = outw / 8;                                    // chunks per row (divides 64: outw in {8..128})
-  const int ccol = (lane % cpr) * 8;                           // this lane's output column
-  const int rstep = 64 / cpr;                                  // rows advanced per pass
-  float bia[8], rsc[8], aw[8], ab[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { bia[j] = 0.f; rsc[j] = 1.f; aw[j] = ab[j] = 0.f; }
-  // WGF accumulators: dW2 (2 x 32 rows of dt channels x 32 n2 channels), U (32 x 32), V (this lane's 16 dout channels)
-  floatx16 accw[2], accu;
-  float vsum[KS][8];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) accw[0][i] = accw[1][i] = accu[i] = 0.f;
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) vsum[ks][e] = 0.f;
-  if (CMODE == CM_RESLN) {  // aw / ab hold the LN weight / bias of this lane's 8 columns
-    const float4 w0 = ld4(p.lnw + ccol), w1 = ld4(p.lnw + ccol + 4), b0 = ld4(p.lnb_f + ccol), b1 = ld4(p.lnb_f + ccol + 4);
-    aw[0] = w0.x; aw[1] = w0.y; aw[2] = w0.z; aw[3] = w0.w; aw[4] = w1.x; aw[5] = w1.y; aw[6] = w1.z; aw[7] = w1.w;
-    ab[0] = b0.x; ab[1] = b0.y; ab[2] = b0.z; ab[3] = b0.w; ab[4] = b1.x; ab[5] = b1.y; ab[6] = b1.z; ab[7] = b1.w;
-  }
-  if (CMODE == CM_LNBWD) {  // rsc holds the LN weight of this lane's 8 columns
-    const float4 s0 = ld4(p.lnw + ccol), s1 = ld4(p.lnw + ccol + 4);
-    rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
-  } else if (CMODE != CM_SGBWD && !RC) {
-    if (p.bias) {
-      const float4 b0 = ld4(p.bias + ccol), b1 = ld4(p.bias + ccol + 4);
-      bia[0] = b0.x; bia[1] = b0.y; bia[2] = b0.z; bia[3] = b0.w; bia[4] = b1.x; bia[5] = b1.y; bia[6] = b1.z; bia[7] = b1.w;
-    }
-    if (p.rscale) {
-      const float4 s0 = ld4(p.rscale + ccol), s1 = ld4(p.rscale + ccol + 4);
-      rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
-    }
-  }
-  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = (long)gridDim.x * 4;
-  const long ntiles = (M + 31) / 32;
-  auto load_a = [&](long tile, vec_t<H, 8>* a) {
-    const long m = tile * 32 + r;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int k = ks * 16 + 8 * h;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (m < M && k < K) {
-        v = *reinterpret_cast<const vec_t<H, 8>*>(p.A + m * p.lda + k);
-        if (AMODE == AM_SCALE) {
-          const float* sc = p.a_scale + (m / p.rows_per_img) * K + k;
-          const float4 s0 = ld4(sc), s1 = ld4(sc + 4);
-          const float f[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (H)((float)v[j] * f[j]);
-        }
-      }
-      a[ks] = v;
-    }
-  };
-  auto load_a2 = [&](long tile, vec_t<H, 8>* a) {  // RC: the conv4 input rows (plain, row stride K)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const long m = tile * 32 + r;
-      const int k = ks * 16 + 8 * h;
-      vec_t<H, 8> v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (H)0.f;
-      if (m < M && k < K) v = *reinterpret_cast<const vec_t<H, 8>*>(p.A2 + m * K + k);
-      a[ks] = v;
-    }
-  };
-  vec_t<H, 8> a0[KS], a1[KS], c0[RC ? KS : 1], c1[RC ? KS : 1];
-  long tile = wave;
-  if (tile < ntiles) {
-    load_a(tile, a0);
-    if constexpr (RC) load_a2(tile, c0);
-  }
-  for (; tile < ntiles; tile += nwaves) {
-    if (tile + nwaves < ntiles) {
-      load_a(tile + nwaves, a1);
-      if constexpr (RC) load_a2(tile + nwaves, c1);
-    }
-    floatx16 acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma32x32x16(w[t][ks], a0[ks], acc[t]);
-    // lane (r, h) owns pixel r, channels t*32 + 8g + 4h + {0..3}: stage as rows of the tile
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(tileS + r * LDT + t * 32 + 8 * g + 4 * h) =
-            make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]);
-    // WGF: the SimpleGate outputs g = (t[2c] t[2c+1]) of this lane's channels, from the fp32 t exactly as the conv4
-    // forward's SimpleGate epilogue computed them (its stored g)
-    vec_t<H, 2> g2h[NT2][4];
-    if constexpr (RC) {  // t = bf16(A2 W2^T + b2) exactly as the conv4 forward stored it (same MFMA sequence)
-#pragma unroll
-      for (int t = 0; t < NT2; ++t) {
-        floatx16 a2c;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) a2c[i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) a2c = mfma32x32x16(w2[t][ks], c0[ks], a2c);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          vec_t<H, 4> o;
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v[q] = a2c[4 * g + q] + b2r[t][g][q];
-            o[q] = (H)v[q];
-          }
-          *reinterpret_cast<vec_t<H, 4>*>(tileT + r * LDT2 + t * 32 + 8 * g + 4 * h) = o;
-          if constexpr (WGF) {
-            g2h[t][g][0] = (H)(v[0] * v[1]);
-            g2h[t][g][1] = (H)(v[2] * v[3]);
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const long m0 = tile * 32;
-    for (int rr = lane / cpr; rr < 32; rr += rstep) {
-      const long m = m0 + rr;
-      if (m >= M) {
-        if constexpr (WGF) {  // the fold's dt tile: zero rows past M (their n2 rows are zero, stale data could be NaN)
-          vec_t<H, 8> z;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) z[j] = (H)0.f;
-          *reinterpret_cast<vec_t<H, 8>*>(stage3[threadIdx.x >> 6] + rr * 96 + ccol) = z;
-          continue;
-        }
-        break;
-      }
-      if (CMODE == CM_SGBWD || RC) {  // chunk = 4 gates (interleaved pairs): dg from the tile, t from R (or rebuilt)
-        const float4 dg = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol / 2);
-        const long off = m * p.ldc + ccol;
-        const vec_t<H, 8> tv = RC ? *reinterpret_cast<const vec_t<H, 8>*>(tileT + rr * LDT2 + ccol)
-                             : *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
-        const float d[4] = {dg.x, dg.y, dg.z, dg.w};
-        vec_t<H, 8> o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          o[2 * j] = (H)(d[j] * (float)tv[2 * j + 1]);
-          o[2 * j + 1] = (H)(d[j] * (float)tv[2 * j]);
-        }
-        *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
-        if constexpr (WGF) {
-          *reinterpret_cast<vec_t<H, 8>*>(stage3[threadIdx.x >> 6] + rr * 96 + ccol) = o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ab[j] += (float)o[j];  // db2 partial of this lane's 8 columns
-        }
-        continue;
-      }
-      const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
-      const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
-      float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      if constexpr (CMODE == CM_LNBWD) {  // the row's cpr lanes are consecutive: shuffle sums within the group
-        constexpr int G = 4 * NT;
-        const long off = m * p.ldc + ccol;
-        const vec_t<H, 8> xv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
-        const vec_t<H, 8> rv = *reinterpret_cast<const vec_t<H, 8>*>(p.dres + off);
-        const float2 st = p.stats[m];
-        const float inv = 1.f / st.y;
-        float yh[8], sg = 0.f, sgy = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          yh[j] = ((float)xv[j] - st.x) * inv;
-          const float g = v[j] * rsc[j];
-          sg += g;
-          sgy = fmaf(g, yh[j], sgy);
-          aw[j] = fmaf(v[j], yh[j], aw[j]);
-          ab[j] += v[j];
-        }
-        sg = group_sum<G>(sg);
-        sgy = group_sum<G>(sgy);
-        const float mg = sg / (float)N, mgy = sgy / (float)N;
-        vec_t<H, 8> o;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (H)((v[j] * rsc[j] - yh[j] * mgy - mg) * inv + (float)rv[j]);
-        *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
-        continue;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += bia[j];
-      const long off = m * p.ldc + ccol;
-      if ((CMODE == CM_PLAIN || CMODE == CM_RESLN) && p.R) {
-        const vec_t<H, 8> rv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (float)rv[j] + rsc[j] * v[j];
-      }
-      vec_t<H, 8> o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (H)v[j];
-      if (CMODE != CM_SG || p.C) *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;  // SG: t may be dropped (recomputed)
-      if constexpr (CMODE == CM_RESLN) {  // LayerNorm2d of the stored (bf16) row, as ln_fwd_nhwc computes it
-        constexpr int G = 4 * NT;
-        float xv[8], sm = 0.f, q = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xv[j] = (float)o[j];
-          sm += xv[j];
-        }
-        sm = group_sum<G>(sm);
-        const float mu = sm / (float)N;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = xv[j] - mu;
-          q = fmaf(d, d, q);
-        }
-        q = group_sum<G>(q);
-        const float dd = sqrtf(q / (float)N + p.eps), inv = 1.f / dd;
-        vec_t<H, 8> nn;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) nn[j] = (H)fmaf(aw[j], (xv[j] - mu) * inv, ab[j]);
-        *reinterpret_cast<vec_t<H, 8>*>(p.nout + m * N + ccol) = nn;
-        if (ccol == 0) p.stats_out[m] = make_float2(mu, dd);
-      }
-      if (CMODE == CM_SG) {  // g[c] = t[2c] * t[2c+1]: 4 gates of this chunk
-        vec_t<H, 4> gv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) gv[j] = (H)(v[2 * j] * v[2 * j + 1]);
-        *reinterpret_cast<vec_t<H, 4>*>(p.aux + m * (p.ldc / 2) + ccol / 2) = gv;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    if constexpr (WGF) {
-      // stage dout (this GEMM's A) and n2 (A2) in the dead fp32 tile, g in the dead t tile (32-element rows), then
-      // accumulate U += dout^T g and dW2 += dt^T n2 over the tile's 32 rows with transposed fragment reads
-      H* sd = reinterpret_cast<H*>(tileS);
-      H* sn = sd + 32 * 32;
-      H* sg = tileT;
-      const H* st = stage3[threadIdx.x >> 6];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        *reinterpret_cast<vec_t<H, 8>*>(sd + r * 32 + ks * 16 + 8 * h) = a0[ks];
-        *reinterpret_cast<vec_t<H, 8>*>(sn + r * 32 + ks * 16 + 8 * h) = c0[ks];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) vsum[ks][e] += (float)a0[ks][e];  // V partial (rows past M are zero-filled)
-      }
-#pragma unroll
-      for (int t = 0; t < NT2; ++t)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<vec_t<H, 2>*>(sg + r * 32 + t * 16 + 4 * g + 2 * h) = g2h[t][g];
-      __builtin_amdgcn_wave_barrier();
-      const int grp = lane >> 4, gq = (lane & 15) >> 2, pp = lane & 3;
-      const int fcol = 16 * (grp & 1) + 4 * pp;
-#pragma unroll
-      for (int ks = 0; ks < 32; ks += 16) {
-        vec_t<H, 8> fa[2], fn, fu, fg;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          const int row = ks + 8 * h + 4 * tt + gq;
-          const vec_t<H, 4> a0v = ds_read_tr16<H>(st + row * 96 + fcol);
-          const vec_t<H, 4> a1v = ds_read_tr16<H>(st + row * 96 + 32 + fcol);
-          const vec_t<H, 4> nv = ds_read_tr16<H>(sn + row * 32 + fcol);
-          const vec_t<H, 4> uv = ds_read_tr16<H>(sd + row * 32 + fcol);
-          const vec_t<H, 4> gv = ds_read_tr16<H>(sg + row * 32 + fcol);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            fa[0][4 * tt + e] = a0v[e];
-            fa[1][4 * tt + e] = a1v[e];
-            fn[4 * tt + e] = nv[e];
-            fu[4 * tt + e] = uv[e];
-            fg[4 * tt + e] = gv[e];
-          }
-        }
-        accw[0] = mfma32x32x16(fa[0], fn, accw[0]);
-        accw[1] = mfma32x32x16(fa[1], fn, accw[1]);
-        accu = mfma32x32x16(fu, fg, accu);
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) a0[ks] = a1[ks];
-    if constexpr (RC)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) c0[ks] = c1[ks];
-  }
-  if constexpr (WGF) {
-    // block partials, waves combined in fixed order through stage3 (as fp32): [0, 2048) dW2 (row n = dt column, col k =
-    // n2 channel), [2048, 3072) U, [3072, 3136) db2, [3136, 3168) V
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int o = cpr; o < 64; o <<= 1) ab[j] += __shfl_xor(ab[j], o, 64);  // lanes sharing ccol
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) vsum[ks][e] += __shfl_xor(vsum[ks][e], o, 64);  // lanes sharing h
-    float* red = reinterpret_cast<float*>(&stage3[0][0]);
-    const int wv = threadIdx.x >> 6;
-    for (int w = 0; w < 4; ++w) {
-      __syncthreads();
-      if (wv == w) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int rr = 0; rr < 16; ++rr) {
-            const int n = i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h, k = r;
-            float* d = red + n * 32 + k;
-            *d = (w == 0 ? 0.f : *d) + accw[i][rr];
-          }
-#pragma unroll
-        for (int rr = 0; rr < 16; ++rr) {
-          const int n = (rr & 3) + 8 * (rr >> 2) + 4 * h, k = r;
-          float* d = red + 2048 + n * 32 + k;
-          *d = (w == 0 ? 0.f : *d) + accu[rr];
-        }
-        if (lane < cpr)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float* d = red + 3072 + ccol + j;
-            *d = (w == 0 ? 0.f : *d) + ab[j];
-          }
-        if (r == 0)
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              float* d = red + 3136 + ks * 16 + 8 * h + e;
-              *d = (w == 0 ? 0.f : *d) + vsum[ks][e];
-            }
-      }
-    }
-    __syncthreads();
-    const long bb = blockIdx.x;
-    for (int i = threadIdx.x; i < 3168; i += blockDim.x) {
-      const float v = red[i];
-      if (i < 2048) p.slab_w2[bb * 2048 + i] = v;
-      else if (i < 3072) p.slab_u[bb * 1024 + i - 2048] = v;
-      else if (i < 3136) p.slab_b2[bb * 64 + i - 3072] = v;
-      else p.slab_v[bb * 32 + i - 3136] = v;
-    }
-  }
-  if constexpr (CMODE == CM_LNBWD) {  // LN weight / bias gradient partials: lanes sharing ccol, then the 4 waves
-    constexpr int G = 4 * NT;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int o = G; o < 64; o <<= 1) {
-        aw[j] += __shfl_xor(aw[j], o, 64);
-        ab[j] += __shfl_xor(ab[j], o, 64);
-      }
-    __syncthreads();
-    float* red = &stage[0][0];  // [4 waves][2][N]
-    const int wv = threadIdx.x >> 6;
-    if (lane < G) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[(wv * 2 + 0) * N + ccol + j] = aw[j];
-        red[(wv * 2 + 1) * N + ccol + j] = ab[j];
-      }
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < N; c += blockDim.x) {
-      p.slab_w[(long)blockIdx.x * N + c] = ((red[0 * N + c] + red[2 * N + c]) + red[4 * N + c]) + red[6 * N + c];
-      p.slab_b[(long)blockIdx.x * N + c] = ((red[1 * N + c] + red[3 * N + c]) + red[5 * N + c]) + red[7 * N + c];
-    }
-  }
-}
-
-long skinny_blocks(long M) {
-  const long ntiles = (M + 31) / 32;
-  const long blocks = (ntiles + 3) / 4;
-  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs (NBP_SKINNY_BLOCKS overrides: A/B measurement)
-  static const long cap = [] {
-    const long v = getenv("NBP_SKINNY_BLOCKS") ? atol(getenv("NBP_SKINNY_BLOCKS")) : 1024L;
-    if (v < 1 || v > 8192) {
-      fprintf(stderr, "NBP_SKINNY_BLOCKS=%ld out of [1, 8192]: using 1024\n", v);
-      return 1024L;
-    }
-    return v;
-  }();
-  return blocks > cap ? cap : blocks;
-}
-
-// K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads)
-template <int AMODE, int CMODE, typename H>
-void launch_skinny(const SkinnyP<H>& p, hipStream_t st) {
-  const dim3 g((unsigned)skinny_blocks(p.M));
-  const int nt = (p.N + 31) / 32, ks = (p.K + 15) / 16;
-#define NBP_SKINNY(NT_, KS_) gemm_skinny_kernel<NT_, KS_, AMODE, CMODE, H><<<g, 256, 0, st>>>(p)
-  if (nt == 1) {
-    if (ks == 1) NBP_SKINNY(1, 1); else if (ks == 2) NBP_SKINNY(1, 2); else if (ks == 3) NBP_SKINNY(1, 3);
-    else if (ks == 4) NBP_SKINNY(1, 4); else NBP_SKINNY(1, 8);
-  } else {
-    if (ks == 1) NBP_SKINNY(2, 1); else if (ks == 2) NBP_SKINNY(2, 2); else if (ks == 3) NBP_SKINNY(2, 3);
-    else if (ks == 4) NBP_SKINNY(2, 4); else NBP_SKINNY(2, 8);
-  }
-#undef NBP_SKINNY
-}
-
-// whether the skinny path serves this call (bf16 in / out, N and K <= 64, supported modes, aligned rows)
-template <typename H>
-bool try_skinny(const void* A, long lda, int a_mode, const float* a_scale, int rows, const void* Bw, long ldb, void* C,
-                long ldc, int c_mode, int M, int N, int K, const float* bias, const void* R, const float* rscale,
-                void* pre, hipStream_t st) {
-  if (N > 64 || K > 128 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc % 8) return false;
-  const bool ok = (a_mode == AM_PLAIN && c_mode == CM_PLAIN && !pre) || (a_mode == AM_SCALE && c_mode == CM_PLAIN && !pre) ||
-                  (a_mode == AM_PLAIN && c_mode == CM_SG) || (a_mode == AM_SCALE && c_mode == CM_SGBWD) ||
-                  (a_mode == AM_PLAIN && c_mode == CM_SGBWD);
-  if (!ok) return false;
-  SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, a_scale, rows, reinterpret_cast<const H*>(Bw), ldb,
-            reinterpret_cast<H*>(C), ldc, M, N, K, bias, reinterpret_cast<const H*>(R), rscale,
-            reinterpret_cast<H*>(pre), nullptr, nullptr, nullptr, nullptr, nullptr};
-  if (c_mode == CM_SG) launch_skinny<AM_PLAIN, CM_SG, H>(p, st);
-  else if (c_mode == CM_SGBWD && a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_SGBWD, H>(p, st);
-  else if (c_mode == CM_SGBWD) launch_skinny<AM_PLAIN, CM_SGBWD, H>(p, st);
-  else if (a_mode == AM_SCALE) launch_skinny<AM_SCALE, CM_PLAIN, H>(p, st);
-  else launch_skinny<AM_PLAIN, CM_PLAIN, H>(p, st);
-  return true;
-}
-
-// fp32 flat parameters -> bf16 copy (all), plus transposed bf16 copies of the listed [rows][cols] matrices
-template <typename H>
-__global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, H* __restrict__ dst) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    dst[i] = (H)src[i];
-}
-
-// desc: [ndesc][4] int64 {offset, rows, cols, row-scale offset or -1}; block (x: tile index, y: matrix).  With a
-// row scale s (the layer scale beta / gamma of conv3 / conv5) the copy is (diag(s) W)^T.
-template <typename H>
-__global__ void transpose_bf16_kernel(const float* __restrict__ src, const long* __restrict__ desc,
-                                      H* __restrict__ dst_t) {
-  __shared__ float tile[32][33];
-  const long off = desc[blockIdx.y * 4], R = desc[blockIdx.y * 4 + 1], Cc = desc[blockIdx.y * 4 + 2];
-  const long soff = desc[blockIdx.y * 4 + 3];
-  const long tiles_c = (Cc + 31) / 32, ntiles = ((R + 31) / 32) * tiles_c;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const long r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
-    for (int rr = ty; rr < 32; rr += 8) {
-      const long r = r0 + rr, c = c0 + tx;
-      tile[rr][tx] = (r < R && c < Cc) ? src[off + r * Cc + c] * (soff >= 0 ? src[soff + r] : 1.f) : 0.f;
-    }
-    __syncthreads();
-    for (int cc = ty; cc < 32; cc += 8) {
-      const long c = c0 + cc, r = r0 + tx;
-      if (r < R && c < Cc) dst_t[off + c * R + r] = (H)tile[tx][cc];
-    }
-    __syncthreads();
-  }
-}
-
-// NBP_GLDS: 0 = register-staged tiles only, 2 / 3 = LDS-DMA ring depth for 16-bit A (A/B measurement; read per launch
-// so a test can compare both paths in one process).  Default 2: at the deep-level shapes (scripts/gemm_probe.py) the
-// 3-deep ring's extra LDS costs more in blocks per CU than the second tile in flight buys.
-// Unset (default): chosen per launch by glds_auto_depth.
-int glds_depth() {
-  const char* e = getenv("NBP_GLDS");
-  return e ? atoi(e) : -1;
-}
-
-int cu_count() {
-  static const int n = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || v <= 0)
-      v = 256;
-    return v;
-  }();
-  return n;
-}
-
-// Auto ring depth: the deepest ring (<= 4, <= nmax) with which every CU still holds all the blocks the grid gives it
-// (LDS per block = max(depth x stage, fp32 C staging)).  The small-grid deep-level GEMMs (2 blocks per CU, 8 K-steps,
-// memory-latency bound) get 3 / 4 tiles in flight; large grids keep 2 and their blocks per CU.
-int glds_auto_depth(long blocks, int stage_bytes, int c_bytes, int nmax) {
-  const long per_cu = (blocks + cu_count() - 1) / cu_count();
-  for (int d = nmax; d > 2; --d) {
-    const long lds = (long)d * stage_bytes > c_bytes ? (long)d * stage_bytes : c_bytes;
-    if (per_cu * lds <= 160L * 1024) return d;
-  }
-  return 2;
-}
-
-// NBP_GEMM_WAVES: 8 (default: 2 x 4 waves, two per SIMD, on tiles with BN >= 128) or 4 (2 x 2) for the LDS-DMA
-// kernel (A/B, read per launch: 8 waves + 128 x 128 tiles from 512 workgroups = +2 % step over 4 waves + 1024)
-int gemm_waves() {
-  const char* e = getenv("NBP_GEMM_WAVES");
-  return e && atoi(e) == 4 ? 4 : 8;
-}
-
-template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC, typename H>
-void launch(const GemmPB& p, hipStream_t st) {
-  dim3 grid(cdiv(p.M, BM), cdiv(p.N, BN));
-  if constexpr (sizeof(TA) == 2 && (AMODE == AM_PLAIN || AMODE == AM_SCALE || AMODE == AM_S2D || AMODE == AM_IM2COL)) {
-    const int ns_env = glds_depth();
-    const int ns = ns_env < 0 ? 2 : ns_env;
-    // 16-byte aligned sources (lda, ldb, cs multiples of 8); a tile's rows in one image for the per-image scale
-    const bool ok = ns >= 2 && p.K > 32 && p.ldb % 8 == 0 &&
-                    (AMODE == AM_S2D || AMODE == AM_IM2COL ? p.cs % 8 == 0 : p.lda % 8 == 0) &&
-                    (AMODE != AM_SCALE || p.rows_per_img % BM == 0);
-    if (ok) {
-      // the ring depth the tile's LDS allows (stage = (BM + BN) x 128 B + scales; the fp32 C staging must fit too)
-      constexpr int STB = (BM + BN) * 128 + (AMODE == AM_SCALE ? 256 : 0), CB = BM * (BN + 4) * 4;
-      constexpr int NMAX = 4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
-      const int nd = ns_env < 0 ? glds_auto_depth((long)grid.x * grid.y, STB, CB, NMAX) : (ns < NMAX ? ns : NMAX);
-      if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
-        if (gemm_waves() == 8) {  // 2 x 4 waves of (BM / 2) x (BN / 4): two waves per SIMD
-          if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          else if (nd == 3) gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          return;
-        }
-      }
-      if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
-      else if (nd == 3) gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
-      else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
-      return;
-    }
-  }
-  if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
-  else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
-}
-
-// largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 512 blocks (2 per CU; with the
-// 8-wave DMA tiles: 1024 with the register-staged 4-wave kernel measured best); otherwise 64x64, the most blocks.
-// NBP_GEMM_MINBLK overrides the block-count threshold (A/B measurement)
-long gemm_minblk() {
-  static const long v = [] {
-    const char* e = getenv("NBP_GEMM_MINBLK");
-    return e ? atol(e) : 512L;
-  }();
-  return v;
-}
-
-// NBP_CONV_TILE (A/B measurement, read per launch; default 0 = the generic tile choice): 256-row tiles for the 3x3
-// implicit-GEMM convs, bit 0: 256 x 64 on 4 waves (4 x 1, 64 x 64 each) when N <= 64, bit 1: 256 x 128 on 8 waves
-// (4 x 2) when N > 64.  Measured on cfg3: bit 0 neutral, bit 1 -1.5 % (one 135 KB workgroup per CU): with one barrier
-// per K step the 128 x 128 tile stays the better structure.
-int conv_tile() {
-  const char* e = getenv("NBP_CONV_TILE");
-  return e ? atoi(e) : 0;
-}
-
-template <int AMODE, int CMODE, typename TA, typename TC, typename H>
-bool launch_conv_big(const GemmPB& p, hipStream_t st) {
-  if constexpr (sizeof(TA) == 2 && AMODE == AM_IM2COL && CMODE != CM_LNBWD && CMODE != CM_CHANDOT &&
-                CMODE != CM_RESLN) {
-    const int ns = glds_depth();
-    const int ct = conv_tile();
-    if (!(ct & (p.N <= 64 ? 1 : 2)) || (ns >= 0 && ns < 2) || p.K <= 32 || p.ldb % 8 || p.cs % 8 ||
-        (long)cdiv(p.M, 256) * cdiv(p.N, 128) < 256)
-      return false;
-    if (p.N <= 64) {
-      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 64));
-      gemm_glds_kernel<256, 64, 2, AMODE, CMODE, TC, H, 1, 4><<<grid, 256, 0, st>>>(p);
-    } else {
-      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 128));
-      gemm_glds_kernel<256, 128, 2, AMODE, CMODE, TC, H, 2, 4><<<grid, 512, 0, st>>>(p);
-    }
-    return true;
-  }
-  return false;
-}
-
-template <int AMODE, int CMODE, typename TA, typename TC, typename H>
-void dispatch(const GemmPB& p, hipStream_t st) {
-  if (launch_conv_big<AMODE, CMODE, TA, TC, H>(p, st)) return;
-  if constexpr (CMODE == CM_CHANDOT) {  // its partial-sum layout is per 64-row tile
-    launch<64, 64, AMODE, CMODE, TA, TC, H>(p, st);
-  } else {
-    auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
-    const bool n128 = p.N > 64, m128 = p.M > 64;
-    const long mb = gemm_minblk();
-    if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC, H>(p, st);
-    else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC, H>(p, st);
-    else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC, H>(p, st);
-    else launch<64, 64, AMODE, CMODE, TA, TC, H>(p, st);
-  }
-}
-
-// NBP_SKINNY=0 disables the skinny path (A/B measurement)
-bool getenv_skinny() {
-  static const bool on = [] {
-    const char* v = getenv("NBP_SKINNY");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
-template <typename TA, typename TC, typename H>
-int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {
-  if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch<AM_PLAIN, CM_PLAIN, TA, TC, H>(p, st);
-  else if (a_mode == AM_SCALE && c_mode == CM_PLAIN) dispatch<AM_SCALE, CM_PLAIN, TA, TC, H>(p, st);
-  else if (a_mode == AM_S2D && c_mode == CM_PLAIN) dispatch<AM_S2D, CM_PLAIN, TA, TC, H>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_D2S) dispatch<AM_PLAIN, CM_D2S, TA, TC, H>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_SG) dispatch<AM_PLAIN, CM_SG, TA, TC, H>(p, st);
-  else if (a_mode == AM_SCALE && c_mode == CM_SGBWD) dispatch<AM_SCALE, CM_SGBWD, TA, TC, H>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_SGBWD) dispatch<AM_PLAIN, CM_SGBWD, TA, TC, H>(p, st);
-  else if (a_mode == AM_PLAIN && c_mode == CM_CHANDOT) dispatch<AM_PLAIN, CM_CHANDOT, TA, TC, H>(p, st);
-  else {
-    set_error("nbp_gemm_bf16: unsupported mode combination");
-    return NBP_ERR_ARG;
-  }
-  return NBP_OK;
-}
-
-}  // namespace
 
 extern "C" {
 
@@ -1597,78 +196,6 @@ int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int
       transpose_bf16_kernel<H><<<dim3(256, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<H*>(out_t));
   });
   return check_launch("weights_bf16");
-}
-
-// 3x3 zero-padded convolution over NHWC 16-bit maps as an implicit GEMM on the 16-bit MFMA kernel:
-//   y[b][i][j][n] = epi( sum_{t, c} x[b][i + t/3 - 1][j + t%3 - 1][c] * w[n][t][c] (+ bias[n]) )
-// epi: mode 0 bias + ReLU, 1 bias only, 2 ReLU-mask by R (y = acc where R > 0 else 0; no bias).  x, w, R and a
-// 16-bit y share the type `dtype` (1 bf16, 2 fp16); y is that type (y_dtype 1) or fp32 (y_dtype 0, mode 1 only).
-// Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
-// NBP_IM2COL_TAP=0: per-lane tap division in the 3x3 conv's DMA issue (A/B measurement; read per launch)
-static bool im2col_tap_tile() {
-  const char* e = getenv("NBP_IM2COL_TAP");
-  return !(e && e[0] == '0');
-}
-
-int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
-                     const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0, "nbp_conv3x3_bf16: bad args");
-  NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv3x3_bf16: Cin and Cout must be multiples of 8 (%d, %d)", Cin,
-              Cout);
-  NBP_REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || R) && (y_dtype == 1 || mode == 1),
-              "nbp_conv3x3_bf16: mode / R / y_dtype");
-  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_conv3x3_bf16: dtype 1 (bf16) or 2 (fp16)");
-  const long M = (long)B * H * W;
-  NBP_REQUIRE(M < (1L << 31), "nbp_conv3x3_bf16: too many pixels");
-  GemmPB p{x, 0, nullptr, 1, w, 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
-           mode == 2 ? nullptr : bias, mode == 2 ? R : nullptr, nullptr, nullptr};
-  p.tap_tile = Cin % 64 == 0 && im2col_tap_tile();
-  hipStream_t st = S(s);
-  if (dtype == 2) {
-    using T16 = _Float16;
-    if (mode == 0) dispatch<AM_IM2COL, CM_RELU, T16, T16, T16>(p, st);
-    else if (mode == 2) dispatch<AM_IM2COL, CM_MASK, T16, T16, T16>(p, st);
-    else if (y_dtype == 1) dispatch<AM_IM2COL, CM_PLAIN, T16, T16, T16>(p, st);
-    else dispatch<AM_IM2COL, CM_PLAIN, T16, float, T16>(p, st);
-  } else {
-    using T16 = __bf16;
-    if (mode == 0) dispatch<AM_IM2COL, CM_RELU, T16, T16, T16>(p, st);
-    else if (mode == 2) dispatch<AM_IM2COL, CM_MASK, T16, T16, T16>(p, st);
-    else if (y_dtype == 1) dispatch<AM_IM2COL, CM_PLAIN, T16, T16, T16>(p, st);
-    else dispatch<AM_IM2COL, CM_PLAIN, T16, float, T16>(p, st);
-  }
-  return check_launch("conv3x3_bf16");
-}
-
-int nbp_conv2d_16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, int KH, int KW, int stride,
-                  int pad, const float* bias, int relu, void* y, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
-              "nbp_conv2d_16: bad args");
-  NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv2d_16: Cin and Cout must be multiples of 8 (%d, %d)", Cin, Cout);
-  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_conv2d_16: dtype 1 (bf16) or 2 (fp16)");
-  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
-  NBP_REQUIRE(Ho > 0 && Wo > 0, "nbp_conv2d_16: empty output");
-  const long M = (long)B * Ho * Wo;
-  NBP_REQUIRE(M < (1L << 31), "nbp_conv2d_16: too many pixels");
-  GemmPB p{x, 0, nullptr, 1, w, (long)KH * KW * Cin, y, Cout, (int)M, Cout, KH * KW * Cin, Ho, Wo, Cin, bias, nullptr,
-           nullptr, nullptr};
-  p.kh = KH;
-  p.kw = KW;
-  p.stride = stride;
-  p.pad = pad;
-  p.ih = H;
-  p.iw = W;
-  hipStream_t st = S(s);
-  if (dtype == 2) {
-    using T16 = _Float16;
-    if (relu) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
-    else dispatch<AM_CONV, CM_PLAIN, T16, T16, T16>(p, st);
-  } else {
-    using T16 = __bf16;
-    if (relu) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
-    else dispatch<AM_CONV, CM_PLAIN, T16, T16, T16>(p, st);
-  }
-  return check_launch("conv2d_16");
 }
 
 }  // extern "C"

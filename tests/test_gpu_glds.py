@@ -101,10 +101,13 @@ def test_glds_space_to_depth(dev, B, gh, gw, cs):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(1, 64, 64, 64, 128), (2, 17, 23, 128, 64), (1, 32, 32, 256, 256),
-                                            (3, 130, 170, 64, 64), (4, 128, 128, 128, 128), (2, 96, 180, 64, 256)])
+                                            (3, 130, 170, 64, 64), (4, 128, 128, 128, 128), (2, 96, 180, 64, 256),
+                                            (4, 128, 128, 256, 256), (3, 100, 180, 64, 264)])
 def test_glds_conv3x3(dev, B, H, W, Cin, Cout):
     """VGG 3x3 convolution (implicit GEMM, zero padding read from the zero page): bias + ReLU and the ReLU-mask form.
-    The large shapes (>= 256 row tiles) run the 256-row conv tiles (NBP_CONV_TILE=1) on the DMA path."""
+    The last two shapes (N >= 256, >= 256 workgroups) run the 256 x 256 tiles with the two-pass epilogue (ragged M and
+    N in the last); the register-staged kernel (NBP_GLDS=0) keeps 128-row tiles, so every tile shape is compared
+    bitwise with it.  The XCD-contiguous tile order (NBP_CONV_MAP, default 1) must not change a bit either."""
     from lowlight_image_enhancement_amd._lib import call
     gen = torch.Generator(device=dev).manual_seed(B * H + Cin)
     x = torch.randn(B, H, W, Cin, device=dev, generator=gen).to(torch.bfloat16)
@@ -126,6 +129,14 @@ def test_glds_conv3x3(dev, B, H, W, Cin, Cout):
         os.environ.pop("NBP_IM2COL_TAP", None)
     for a, b_ in zip(ref, alt):
         assert torch.equal(a, b_)
+    for knob, val in (("NBP_CONV_MAP", "0"), ("NBP_CONV_TILE", "0")):
+        os.environ[knob] = val
+        try:
+            alt = [t.clone() for t in fn()]
+        finally:
+            os.environ.pop(knob, None)
+        for a, b_ in zip(ref, alt):
+            assert torch.equal(a, b_), knob
 
 
 @pytest.mark.parametrize("M,N,K,amode", [(4096, 256, 256, 2), (16384, 128, 256, 0), (333, 256, 512, 0)])
