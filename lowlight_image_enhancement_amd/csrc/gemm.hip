@@ -553,26 +553,29 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
 // scale of the stage's 128 X columns is DMA'd with the stage (a stage never straddles two images); the bias column
 // sums of G are read back from the panel.  Same MFMA sequence per tile as wgrad_wide_tile (the bias sums are added
 // in another order).
-template <int NS, int XMODE>
-constexpr int wide_glds_stage_bytes() { return 2 * 64 * 256 + (XMODE == AM_SCALE ? 512 : 0); }
-template <int NS>
+// WNW = 4 (wgrad_bf16_wide_group8): 256 x 128 output tiles on 8 waves (4 along N x 2 along K, each 64 x 64): the G
+// panel rows are 512 B (2 rows per DMA instruction), 1.33x the MFMA work per staged byte of the 128 x 128 tile and
+// two waves per SIMD.
+template <int NS, int XMODE, int WNW = 2>
+constexpr int wide_glds_stage_bytes() { return 64 * 128 * WNW + 64 * 256 + (XMODE == AM_SCALE ? 512 : 0); }
+template <int NS, int WNW = 2>
 constexpr int wide_glds_lds_bytes() {
-  return NS * wide_glds_stage_bytes<NS, AM_SCALE>() > 16 * 128 * 4 ? NS * wide_glds_stage_bytes<NS, AM_SCALE>()
-                                                                   : 16 * 128 * 4;
+  return NS * wide_glds_stage_bytes<NS, AM_SCALE, WNW>() > 16 * 128 * 4 ? NS * wide_glds_stage_bytes<NS, AM_SCALE, WNW>()
+                                                                        : 16 * 128 * 4;
 }
 
 // asm helpers of wgrad_wide_tile_glds: the 8 ds_read_b64_tr_b16 of one 16-row K step (rows KS + 4 t + lane part),
 // fragment order [t * 4 + {Gi0, Gi1, Xi0, Xi1}]; a counted lgkmcnt wait that also ties the fragments to it (so no
 // consumer is scheduled above the wait); and the step's 2 x 2 MFMAs.
-template <int KS>
+template <int KS, int GRB = 256>  // GRB: G panel row bytes
 __device__ __forceinline__ void wide_tr_reads(s16x4 (&f)[8], unsigned g0, unsigned g1, unsigned x0, unsigned x1) {
 #define NBP_TR(dst, addr, off) asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "n"(off))
-  NBP_TR(f[0], g0, KS * 256);
-  NBP_TR(f[1], g1, KS * 256);
+  NBP_TR(f[0], g0, KS * GRB);
+  NBP_TR(f[1], g1, KS * GRB);
   NBP_TR(f[2], x0, KS * 256);
   NBP_TR(f[3], x1, KS * 256);
-  NBP_TR(f[4], g0, (KS + 4) * 256);
-  NBP_TR(f[5], g1, (KS + 4) * 256);
+  NBP_TR(f[4], g0, (KS + 4) * GRB);
+  NBP_TR(f[5], g1, (KS + 4) * GRB);
   NBP_TR(f[6], x0, (KS + 4) * 256);
   NBP_TR(f[7], x1, (KS + 4) * 256);
 #undef NBP_TR
@@ -611,16 +614,20 @@ __device__ __forceinline__ void wide_mfma(const s16x4 (&f)[8], floatx16 (&acc)[2
   }
 }
 
-template <int XMODE, typename H, int NS>
+template <int XMODE, typename H, int NS, int WNW = 2>
 __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int by, int bz, unsigned char* smem) {
-  constexpr int RM = 64, PAN = RM * 256, ST = wide_glds_stage_bytes<NS, XMODE>();
-  constexpr int GL = 8 + (XMODE == AM_SCALE ? 2 : 0);  // DMA instructions per wave per stage
+  constexpr int NWV = 2 * WNW, TNB = 64 * WNW;  // waves; output tile columns (N)
+  constexpr int GRB = 2 * TNB, RM = 64, PAN = RM * GRB, ST = wide_glds_stage_bytes<NS, XMODE, WNW>();
+  constexpr int GRI = 1024 / GRB, GLPR = 64 / GRI;  // G rows per DMA instruction, lanes per G row
+  constexpr int IG = RM / (GRI * NWV), IX = RM / (4 * NWV);  // DMA instructions per wave per stage (G, X)
+  constexpr int GL = IG + IX + (XMODE == AM_SCALE ? 2 : 0);
   static_assert(NS >= 2 && NS <= 4, "ring depth");
+  static_assert(WNW == 2 || WNW == 4, "wave columns");
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
-  const int n0 = bx * 128, k0 = by * 128, s = bz;
+  const int n0 = bx * TNB, k0 = by * 128, s = bz;
   const int mb = s * p.chunk;
   const int me = min(p.M, mb + p.chunk);
   const bool do_b = p.slab_b && by == 0;
@@ -639,12 +646,18 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
     for (int j = 0; j < NT_; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) tot[i][j][r] = 0.f;
-  // DMA geometry: instruction j of this wave fills panel rows (4 wave + j) * 4 + lane / 16, physical slot lane % 16
-  int drow[4], dcol[4];
+  // DMA geometry: G instruction j of this wave fills panel rows (IG wave + j) * GRI + lane / GLPR, physical slot
+  // lane % GLPR; X instruction j rows (IX wave + j) * 4 + lane / 16, slot lane % 16; chunk c at slot c ^ 4 (r & 3)
+  int grow_[IG], gcol_[IG], xrow_[IX], xcol_[IX];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    drow[j] = (wave * 4 + j) * 4 + (lane >> 4);
-    dcol[j] = 8 * ((lane & 15) ^ (4 * (drow[j] & 3)));
+  for (int j = 0; j < IG; ++j) {
+    grow_[j] = (wave * IG + j) * GRI + lane / GLPR;
+    gcol_[j] = 8 * ((lane % GLPR) ^ (4 * (grow_[j] & 3)));
+  }
+#pragma unroll
+  for (int j = 0; j < IX; ++j) {
+    xrow_[j] = (wave * IX + j) * 4 + (lane >> 4);
+    xcol_[j] = 8 * ((lane & 15) ^ (4 * (xrow_[j] & 3)));
   }
   const int nst = mb < me ? (me - mb + RM - 1) / RM : 0;
   // the zero page's address in registers (laundered through asm: otherwise it is re-loaded from the GOT, with an
@@ -655,15 +668,20 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
     unsigned char* st = smem + (t % NS) * ST;
     const int m0 = mb + t * RM;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + drow[j];
-      glds16(m < me ? (const void*)(G + (long)m * p.ldg + n0 + dcol[j]) : zp, st + (wave * 4 + j) * 1024);
-      glds16(m < me ? (const void*)(X + (long)m * p.ldx + k0 + dcol[j]) : zp, st + PAN + (wave * 4 + j) * 1024);
+    for (int j = 0; j < (IG > IX ? IG : IX); ++j) {  // (IG == IX == 4 at WNW 2: the original G / X interleave)
+      if (j < IG) {
+        const int m = m0 + grow_[j];
+        glds16(m < me ? (const void*)(G + (long)m * p.ldg + n0 + gcol_[j]) : zp, st + (wave * IG + j) * 1024);
+      }
+      if (j < IX) {
+        const int m = m0 + xrow_[j];
+        glds16(m < me ? (const void*)(X + (long)m * p.ldx + k0 + xcol_[j]) : zp, st + PAN + (wave * IX + j) * 1024);
+      }
     }
     if constexpr (XMODE == AM_SCALE) {  // every wave DMAs the same 128 scales of the stage's image
       const float* sc = p.x_scale + (long)(m0 / p.rows_per_img) * p.K + k0;
-      glds4(sc + lane, st + 2 * PAN);
-      glds4(sc + 64 + lane, st + 2 * PAN + 256);
+      glds4(sc + lane, st + PAN + RM * 256);
+      glds4(sc + 64 + lane, st + PAN + RM * 256 + 256);
     }
   };
   // fragment reads: lane (grp, q, pp, h) reads row ks + 8h + 4t + q, logical column (wave half) + 32 i + fcol; in the
@@ -674,7 +692,7 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
   unsigned abase[2][2];                      // [G / X][i], relative to the stage
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    abase[0][i] = (8 * h + q) * 256 + ((4 * ((2 * wn + i) ^ q) + lx) << 4) + (pp & 1) * 8;
+    abase[0][i] = (8 * h + q) * GRB + ((4 * ((2 * wn + i) ^ q) + lx) << 4) + (pp & 1) * 8;
     abase[1][i] = PAN + (8 * h + q) * 256 + ((4 * ((2 * wk + i) ^ q) + lx) << 4) + (pp & 1) * 8;
   }
   const unsigned smem_lds = (unsigned)(size_t)(lds_void_t*)smem;
@@ -717,7 +735,7 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
         if (cur_img >= 0) fold();
         cur_img = im;
         // (asm LDS reads: a plain load here would make the compiler drain the DMA ring first)
-        const unsigned sa = smem_lds + (t % NS) * ST + 2 * PAN + (wk * 64 + (lane & 31)) * 4;
+        const unsigned sa = smem_lds + (t % NS) * ST + PAN + RM * 256 + (wk * 64 + (lane & 31)) * 4;
         asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128\n\ts_waitcnt lgkmcnt(0)"
                      : "=&v"(cur_sc[0]), "=&v"(cur_sc[1])
                      : "v"(sa));
@@ -728,14 +746,14 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
     const unsigned sb = smem_lds + (t % NS) * ST;
     const unsigned ga0 = sb + abase[0][0], ga1 = sb + abase[0][1], xa0 = sb + abase[1][0], xa1 = sb + abase[1][1];
     s16x4 fr[2][8];
-    wide_tr_reads<0>(fr[0], ga0, ga1, xa0, xa1);
-    wide_tr_reads<16>(fr[1], ga0, ga1, xa0, xa1);
+    wide_tr_reads<0, GRB>(fr[0], ga0, ga1, xa0, xa1);
+    wide_tr_reads<16, GRB>(fr[1], ga0, ga1, xa0, xa1);
     wide_tr_wait<8>(fr[0]);
     wide_mfma<H>(fr[0], acc, wb, accb);
-    wide_tr_reads<32>(fr[0], ga0, ga1, xa0, xa1);
+    wide_tr_reads<32, GRB>(fr[0], ga0, ga1, xa0, xa1);
     wide_tr_wait<8>(fr[1]);
     wide_mfma<H>(fr[1], acc, wb, accb);
-    wide_tr_reads<48>(fr[1], ga0, ga1, xa0, xa1);
+    wide_tr_reads<48, GRB>(fr[1], ga0, ga1, xa0, xa1);
     wide_tr_wait<8>(fr[0]);
     wide_mfma<H>(fr[0], acc, wb, accb);
     wide_tr_wait<0>(fr[1]);
@@ -792,6 +810,20 @@ struct WGroup {
   unsigned char xscale[WG_MAX], xcd[WG_MAX];
   int n, xcd_bins;
 };
+// the 8-wave 256 x 128 tiles (every problem's N a multiple of 256; no XCD binning, no register-staged variant)
+template <typename H, int NS>
+__global__ __launch_bounds__(512) void wgrad_bf16_wide_group8(WGroup g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[wide_glds_lds_bytes<NS, 4>()];
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
+  const int l = b - g.start[i];
+  const int gx = g.gx[i], gy = g.gy[i];
+  const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
+  if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS, 4>(g.p[i], bx, by, bz, smem);
+  else wgrad_wide_tile_glds<AM_PLAIN, H, NS, 4>(g.p[i], bx, by, bz, smem);
+}
+
 template <typename H, int NS>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
   constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS)>();
@@ -1218,10 +1250,26 @@ int wgroup_xcd() {
 // Splits for the whole group: each problem keeps at most its standalone split count (its workspace) and at least
 // 256 rows per split; the group as a whole aims at ~wgroup_target() workgroups.  The reductions queued for the
 // problems' slabs are re-pointed at the chosen split counts.
+// NBP_WGRAD8 (read per launch; A/B measurement): 1 = the 8-wave 256 x 128 tiles for groups whose every N is a
+// multiple of 256 (ring depth 2 or 3 from NBP_WGRAD_GLDS), aiming at NBP_WGROUP_TARGET8 workgroups (default 512)
+int wgrad8() {
+  const char* e = getenv("NBP_WGRAD8");
+  return e ? atoi(e) : 0;
+}
+long wgroup_target8() {
+  const char* e = getenv("NBP_WGROUP_TARGET8");
+  const long t = e ? atol(e) : 512;
+  return t < 1 ? 512L : t;
+}
+
 void wgroup_launch(hipStream_t st) {
+  const int ns = wgrad_glds_depth();
+  bool w8 = wgrad8() == 1 && (ns == 2 || ns == 3) && !wgroup_xcd();
+  for (const WgradP& p : g_wqueue) w8 = w8 && p.N % 256 == 0;
+  const int TNB = w8 ? 256 : 128;
   long tiles = 0;
-  for (const WgradP& p : g_wqueue) tiles += (long)(p.N / 128) * (p.K / 128);
-  const long want = (wgroup_target() + tiles - 1) / (tiles > 0 ? tiles : 1);
+  for (const WgradP& p : g_wqueue) tiles += (long)(p.N / TNB) * (p.K / 128);
+  const long want = ((w8 ? wgroup_target8() : wgroup_target()) + tiles - 1) / (tiles > 0 ? tiles : 1);
   for (WgradP& p : g_wqueue) {
     const long s_max = cdiv(p.M, p.chunk);
     long s = want < s_max ? want : s_max;
@@ -1241,7 +1289,7 @@ void wgroup_launch(hipStream_t st) {
     for (; i < g_wqueue.size() && g.n < WG_MAX; ++i) {
       const WgradP& p = g_wqueue[i];
       g.p[g.n] = p;
-      g.gx[g.n] = p.N / 128;
+      g.gx[g.n] = p.N / TNB;
       g.gy[g.n] = p.K / 128;
       g.xscale[g.n] = p.x_scale != nullptr;
       g.start[g.n] = blocks;
@@ -1249,7 +1297,7 @@ void wgroup_launch(hipStream_t st) {
       ++g.n;
     }
     g.start[g.n] = blocks;
-    g.xcd_bins = wgroup_xcd();
+    g.xcd_bins = w8 ? 0 : wgroup_xcd();
     if (g.xcd_bins) {  // longest-processing-time binning of the problems over the 8 XCDs (work = tiles x rows)
       int order[WG_MAX];
       long work[8] = {}, load[8] = {};
@@ -1274,9 +1322,10 @@ void wgroup_launch(hipStream_t st) {
       for (int x = 0; x < 8; ++x) mx = load[x] > mx ? load[x] : mx;
       blocks = (int)(8 * mx);
     }
-    const int ns = wgrad_glds_depth();
     NBP_DISPATCH_H(g_wqueue_dtype, {
-      if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
+      if (w8 && ns == 3) wgrad_bf16_wide_group8<H, 3><<<blocks, 512, 0, st>>>(g);
+      else if (w8) wgrad_bf16_wide_group8<H, 2><<<blocks, 512, 0, st>>>(g);
+      else if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
       else if (ns == 3) wgrad_bf16_wide_group<H, 3><<<blocks, 256, 0, st>>>(g);
       else if (ns == 2) wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
       else wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
