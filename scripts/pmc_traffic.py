@@ -20,7 +20,9 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            "dw_bwd": ("dw_bwd_tiled",), "dw_fwd": ("dw_sg_pool_tiled",), "ln_fwd": ("ln_fwd_nhwc",),
            "ln_bwd": ("ln_bwd_nhwc",),
            # VGG / AlexNet implicit-GEMM convs (cfg3's perceptual + LPIPS trunks): the tiled kernels with A mode 3 / 4
-           "vgg_conv": (re.compile(r"gemm_(glds|bf16)_kernelILi\d+ELi\d+ELi\d+ELi[34]E"),)}
+           "vgg_conv": (re.compile(r"gemm_(glds|bf16)_kernelILi\d+ELi\d+ELi\d+ELi[34]E"),),
+           # the 256 x 256 DMA tiles of the N >= 256 VGG layers (a subset of vgg_conv)
+           "vgg_conv_256": (re.compile(r"gemm_glds_kernelILi256ELi256ELi\d+ELi3E"),)}
 
 
 def _match(name, pats):
