@@ -98,6 +98,10 @@ class NAFNet(nn.Module):
         # when no per-stage hook needs the gradient slices early, i.e. single-GPU)
         self.overlap_wgrad = int(os.environ.get("NBP_OVERLAP_WGRAD", "0"))
         self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
+        # levels 0 / 1 (C in {32, 64}, 16-bit): conv1 + depthwise + SimpleGate + pool partials in one launch
+        # (nbp_c1_dw_sg_pool_fwd: t1 is not re-read from HBM by the depthwise pass), NBP_C1DW=1.  Off by default:
+        # measured slower (level 0 157 vs 32 + 93 us, level 1 127 vs 22 + 37 us, scripts/c1dw_micro.py; -2 % step)
+        self.c1dw = os.environ.get("NBP_C1DW", "0") == "1"
         # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64, 128} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
         # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
@@ -408,15 +412,24 @@ class NAFNet(nn.Module):
             call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), n1, st1,
                  M, c, LN_EPS, dt)
         t1 = E(M, 2 * c)
-        self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
-                 bias=self._slice(P, pre + "conv1.bias"))
-        chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
         # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec).  Off by default:
         # measured slower at cfg2 (L0 dw backward 138 -> 211 us vs 25 us saved in the forward; profiles/r01_v9)
         rec = self.dw_rec and query("dw_tiled", c, dt) == 1
-        t2, g, pool = (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
-        call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2, g,
-             pool, B, h, w, c, dt)
+        fused_rows = (query("c1_dw_slab_rows", h, w, c, dt) if (self.c1dw and not rec and dt != 0 and
+                                                                  len(self._W) == 3) else 0)
+        if fused_rows:
+            chunks = fused_rows
+            t2, g, pool = E(M, 2 * c), E(M, c), F(B * chunks * c)
+            call("c1_dw_sg_pool_fwd", n1, self._slice(self._W[1], pre + "conv1.weight"),
+                 self._slice(P, pre + "conv1.bias"), self._slice(P, pre + "conv2.weight"),
+                 self._slice(P, pre + "conv2.bias"), t1, t2, g, pool, B, h, w, c, dt)
+        else:
+            self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
+                     bias=self._slice(P, pre + "conv1.bias"))
+            chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
+            t2, g, pool = (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
+            call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2,
+                 g, pool, B, h, w, c, dt)
         mean, a = F(B, c), F(B, c)
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
              a, B, h * w, c)
