@@ -277,9 +277,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NBP_BENCH_REHEARSE=1 (one-GPU box only, never the measurement): every rank on cuda:0 over gloo, to exercise the
+    # N > 1 path (graph segments + bucket all-reduces, barriers, max-over-ranks timing) where RCCL needs one GPU per rank
+    rehearse = os.environ.get("NBP_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     from lowlight_image_enhancement_amd import _lib
@@ -424,7 +432,8 @@ def main():
             "data": "synthetic (U[0,1) sRGB, expo_ratio 1, torch default init, seed 0+rank)",
             "config": {"workload": wl["desc"], "global_batch": BATCH * world, "image": IMG,
                        "parallelism": f"dp{world}", "precision": args.precision,
-                       "launch": "hip-graph replay" if use_graph else "eager"},
+                       "launch": "hip-graph replay" if use_graph else "eager",
+                       **({"rehearsal": "gloo, every rank on cuda:0 (not a measurement)"} if rehearse else {})},
             "roofline": roof,
             "nafblock_roofline": {"bytes_per_step": blk_bytes, "bytes_per_element": esize,
                                   "ms_per_step": round(blk_ms_gpu, 3),
