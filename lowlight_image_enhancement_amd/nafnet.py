@@ -102,6 +102,11 @@ class NAFNet(nn.Module):
         # (nbp_c1_dw_sg_pool_fwd: t1 is not re-read from HBM by the depthwise pass), NBP_C1DW=1.  Off by default:
         # measured slower (level 0 157 vs 32 + 93 us, level 1 127 vs 22 + 37 us, scripts/c1dw_micro.py; -2 % step)
         self.c1dw = os.environ.get("NBP_C1DW", "0") == "1"
+        # the forward of the blocks at h * w <= NBP_SPLIT_HW as two half-batch chains on two streams (0: off, the
+        # default: measured -2.5 to -3 % at cfg2 for 256 / 1024 / 4096, profiles/r02_v6/ab_split_hw.txt -- the
+        # half-size deep-level launches do not overlap into a shorter critical path)
+        self.split_hw = int(os.environ.get("NBP_SPLIT_HW", "0"))
+        self._split_streams: Dict[torch.device, torch.cuda.Stream] = {}
         # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64, 128} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
         # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
@@ -396,7 +401,11 @@ class NAFNet(nn.Module):
     def _block_fwd(self, P, pre, x, B, h, w, c, tape, next_pre=None):
         """One NAFBlock forward (NAFNet_arch.py:60-80).  At C in {32, 64, 128} (bf16) the LayerNorms run in the epilogue
         of the GEMM producing their input (nbp_gemm_res_ln): norm2 in conv3's, the next block's norm1 (next_pre)
-        in conv5's; that block then takes (n1, st1) from self._ln_carry."""
+        in conv5's; that block then takes (n1, st1) from self._ln_carry.
+        Every op is separable by image (per-pixel rows, per-image depthwise / pool / SCA), so at the small deep-level
+        maps (h * w <= NBP_SPLIT_HW) the batch is issued as two half-batch chains on two streams (forked from and
+        joined back into the current stream; captured as two branches of the HIP graph): each half's latency-bound
+        launches overlap the other's.  Same kernels on the same rows: results are bitwise those of one chain."""
         M = B * h * w
         dev = x.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
@@ -405,71 +414,94 @@ class NAFNet(nn.Module):
         fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and (c in (32, 64, 128) or
                                                                            (c == 256 and self.fuse_ln256 in ("1", "fwd")))
         carry, self._ln_carry = self._ln_carry, None
-        if carry is not None and carry[0] is x:
-            n1, st1 = carry[1], carry[2]
-        else:
-            n1, st1 = E(M, c), F(M, 2)
-            call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"), n1, st1,
-                 M, c, LN_EPS, dt)
-        t1 = E(M, 2 * c)
+        have_n1 = carry is not None and carry[0] is x
+        n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
         # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec).  Off by default:
         # measured slower at cfg2 (L0 dw backward 138 -> 211 us vs 25 us saved in the forward; profiles/r01_v9)
         rec = self.dw_rec and query("dw_tiled", c, dt) == 1
         fused_rows = (query("c1_dw_slab_rows", h, w, c, dt) if (self.c1dw and not rec and dt != 0 and
                                                                   len(self._W) == 3) else 0)
-        if fused_rows:
-            chunks = fused_rows
-            t2, g, pool = E(M, 2 * c), E(M, c), F(B * chunks * c)
-            call("c1_dw_sg_pool_fwd", n1, self._slice(self._W[1], pre + "conv1.weight"),
-                 self._slice(P, pre + "conv1.bias"), self._slice(P, pre + "conv2.weight"),
-                 self._slice(P, pre + "conv2.bias"), t1, t2, g, pool, B, h, w, c, dt)
-        else:
-            self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c, c,
-                     bias=self._slice(P, pre + "conv1.bias"))
-            chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
-            t2, g, pool = (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
-            call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t2,
-                 g, pool, B, h, w, c, dt)
+        chunks = fused_rows or query("dw_fwd_slab_rows", B, h, w, c, dt)
+        t1, t2, g, pool = E(M, 2 * c), (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
         mean, a = F(B, c), F(B, c)
-        call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"), mean,
-             a, B, h * w, c)
-        y = E(M, c)
-        n2, st2 = E(M, c), F(M, 2)
-        if fuse_ln:
-            call("gemm_res_ln", g, c, AM_SCALE, a, h * w, self._slice(self._W[1], pre + "conv3.weight"), c, y, M, c, c,
-                 self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
-                 self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS, dt)
-        else:
-            self._mm(self._W, g, c, AM_SCALE, a, h * w, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
-                     bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
-            call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2,
-                 M, c, LN_EPS, dt)
+        y, n2, st2 = E(M, c), E(M, c), F(M, 2)
         # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
         # it (sg_rc) or there is no backward
         drop_t4 = dt != 0 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) == 3))
         t4, g2 = (None if drop_t4 else E(M, 2 * c)), E(M, c)
-        if dt != 0:  # SimpleGate in the GEMM epilogue
-            self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
-                     bias=self._slice(P, pre + "conv4.bias"), pre=g2)
-        else:
-            self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c, c,
-                     bias=self._slice(P, pre + "conv4.bias"))
-            call("sg_fwd", t4, g2, M, c, 1, dt)
         out = E(M, c)
-        if fuse_ln and next_pre is not None:
-            nn1, nst1 = E(M, c), F(M, 2)
-            call("gemm_res_ln", g2, c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c, out, M, c,
-                 c, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"),
-                 self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), nn1, nst1,
-                 LN_EPS, dt)
-            self._ln_carry = (out.view(B, h, w, c), nn1, nst1)
+        carry_next = fuse_ln and next_pre is not None
+        nn1, nst1 = (E(M, c), F(M, 2)) if carry_next else (None, None)
+        hw = h * w
+
+        def ops(b0, nb):  # the block's launches for images b0 .. b0 + nb - 1
+            r0, r1, m = b0 * hw, (b0 + nb) * hw, nb * hw
+            R = lambda t: None if t is None else t[r0:r1]  # noqa: E731  (pixel rows)
+            I = lambda t: t[b0:b0 + nb]  # noqa: E731  (images)
+            xs = x[b0:b0 + nb]
+            if not have_n1:
+                call("ln_fwd_nhwc", xs, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"),
+                     R(n1), R(st1), m, c, LN_EPS, dt)
+            pl = pool[b0 * chunks * c:(b0 + nb) * chunks * c]
+            if fused_rows:
+                call("c1_dw_sg_pool_fwd", R(n1), self._slice(self._W[1], pre + "conv1.weight"),
+                     self._slice(P, pre + "conv1.bias"), self._slice(P, pre + "conv2.weight"),
+                     self._slice(P, pre + "conv2.bias"), R(t1), R(t2), R(g), pl, nb, h, w, c, dt)
+            else:
+                self._mm(self._W, R(n1), c, AM_PLAIN, None, 1, pre + "conv1.weight", R(t1), 2 * c, CM_PLAIN, m, 2 * c,
+                         c, bias=self._slice(P, pre + "conv1.bias"))
+                call("dw_sg_pool_fwd", R(t1), self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"),
+                     R(t2), R(g), pl, nb, h, w, c, dt)
+            call("sca_fwd", pl, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"),
+                 I(mean), I(a), nb, hw, c)
+            if fuse_ln:
+                call("gemm_res_ln", R(g), c, AM_SCALE, I(a), hw, self._slice(self._W[1], pre + "conv3.weight"), c, R(y),
+                     m, c, c, self._slice(P, pre + "conv3.bias"), xs, self._slice(P, pre + "beta"),
+                     self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), R(n2), R(st2), LN_EPS,
+                     dt)
+            else:
+                self._mm(self._W, R(g), c, AM_SCALE, I(a), hw, pre + "conv3.weight", R(y), c, CM_PLAIN, m, c, c,
+                         bias=self._slice(P, pre + "conv3.bias"), R=xs, rscale=self._slice(P, pre + "beta"))
+                call("ln_fwd_nhwc", R(y), self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"),
+                     R(n2), R(st2), m, c, LN_EPS, dt)
+            if dt != 0:  # SimpleGate in the GEMM epilogue
+                self._mm(self._W, R(n2), c, AM_PLAIN, None, 1, pre + "conv4.weight", R(t4), 2 * c, CM_SG, m, 2 * c, c,
+                         bias=self._slice(P, pre + "conv4.bias"), pre=R(g2))
+            else:
+                self._mm(self._W, R(n2), c, AM_PLAIN, None, 1, pre + "conv4.weight", R(t4), 2 * c, CM_PLAIN, m, 2 * c,
+                         c, bias=self._slice(P, pre + "conv4.bias"))
+                call("sg_fwd", R(t4), R(g2), m, c, 1, dt)
+            if carry_next:
+                call("gemm_res_ln", R(g2), c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c,
+                     R(out), m, c, c, self._slice(P, pre + "conv5.bias"), R(y), self._slice(P, pre + "gamma"),
+                     self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), R(nn1),
+                     R(nst1), LN_EPS, dt)
+            else:
+                self._mm(self._W, R(g2), c, AM_PLAIN, None, 1, pre + "conv5.weight", R(out), c, CM_PLAIN, m, c, c,
+                         bias=self._slice(P, pre + "conv5.bias"), R=R(y), rscale=self._slice(P, pre + "gamma"))
+
+        if self.split_hw and hw <= self.split_hw and B % 2 == 0 and B >= 2:
+            cur = torch.cuda.current_stream(dev)
+            side = self._split_stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                ops(B // 2, B // 2)
+            ops(0, B // 2)
+            cur.wait_stream(side)
         else:
-            self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
-                     bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
+            ops(0, B)
+        if carry_next:
+            self._ln_carry = (out.view(B, h, w, c), nn1, nst1)
         if tape is not None:
             tape.append(("block", pre, (B, h, w, c), dict(x=x, n1=n1, st1=st1, t1=t1, t2=t2, g=g, mean=mean, a=a, y=y,
                                                            n2=n2, st2=st2, t4=t4, g2=g2)))
         return self._ln_carry[0] if self._ln_carry is not None else out.view(B, h, w, c)
+
+    def _split_stream(self, dev) -> torch.cuda.Stream:
+        st = self._split_streams.get(dev)
+        if st is None:
+            st = self._split_streams[dev] = torch.cuda.Stream(dev)
+        return st
 
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
         ho, wo = h // 2, w // 2
