@@ -596,19 +596,26 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   const int q = tid % NQ, x = tid / NQ;
   const int lc = 4 * q;
   const int gc = lc < HS ? cbase + lc : C + cbase + (lc - HS);
-  float wk[4][9];
+  // the 4 channels' taps as packed pairs {c, c+1}, {c+2, c+3}: every FMA below is a v_pk_fma_f32 on register pairs
+  // that already sit together (no per-FMA operand moves)
+  f2v wk[9][2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) wk[j][t] = p.wdw[(gc + j) * 9 + t];
+    for (int hh = 0; hh < 2; ++hh) wk[t][hh] = f2v{p.wdw[(gc + 2 * hh) * 9 + t], p.wdw[(gc + 2 * hh + 1) * 9 + t]};
   // ---- stage t1 (and dt2 when unfused): 4 chunks per pixel = 2 halves x 2 chunks.  Every load of the stage is
   // issued before the first LDS store (register batches): one memory latency per tile instead of one per pass.
   constexpr int TOT2 = LH * LW * 2, N2 = FUSED ? (TOT2 + NT - 1) / NT : 1;
   uint4 rd[N2], ra[REC ? 1 : N2], rb[REC ? 1 : N2];
+  // addressing: 64-bit element index of the staging frame's origin pixel once per tile, then 32-bit in-frame offsets
+  // from 24-bit multiplies (full-rate v_mul_u32_u24; the launcher bounds W * 2C < 2^24) -- no per-load 64-bit or
+  // 32 x 32 multiplies
+  const unsigned rs1 = (unsigned)W * C2, rsh = (unsigned)W * C;  // row strides (elements) of t1 / t2 / dt1 and dh
   {
     const T* t1 = reinterpret_cast<const T*>(p.t1);
     const T* dt2 = reinterpret_cast<const T*>(p.dt2);
     constexpr int TOT1 = LHX * LWX * 4, N1 = (TOT1 + NT - 1) / NT;
+    const long e1 = (img + (long)(y0 - 1 - XO) * W + (x0 - 1 - XO)) * C2 + cbase;
     uint4 vx[N1], vg[FUSED ? 1 : N1];
 #pragma unroll
     for (int it = 0; it < N1; ++it) {
@@ -616,9 +623,10 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       vx[it] = make_uint4(0, 0, 0, 0);
       if (!FUSED) vg[it] = make_uint4(0, 0, 0, 0);
       const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
-      const int gy = y0 - 1 - XO + pix / LWX, gx = x0 - 1 - XO + pix % LWX;
+      const int py = pix / LWX, px = pix % LWX;
+      const int gy = y0 - 1 - XO + py, gx = x0 - 1 - XO + px;
       if (i < TOT1 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const long go = (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E;
+        const long go = e1 + (long)(__umul24(py, rs1) + __umul24(px, C2) + hh * C + k * E);
         vx[it] = *reinterpret_cast<const uint4*>(t1 + go);
         if (!FUSED) vg[it] = *reinterpret_cast<const uint4*>(dt2 + go);
       }
@@ -626,20 +634,22 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
     if (FUSED) {
       const T* dh = reinterpret_cast<const T*>(p.dh);
       const T* t2 = reinterpret_cast<const T*>(p.t2);
+      const long o2 = img + (long)(y0 - 1) * W + (x0 - 1);
+      const long eh = o2 * C + cbase, e2 = o2 * C2 + cbase;
 #pragma unroll
       for (int it = 0; it < N2; ++it) {
         const int i = tid + it * NT;
         const int pix = i >> 1, k = i & 1;
-        const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+        const int py = pix / LW, px = pix % LW;
+        const int gy = y0 - 1 + py, gx = x0 - 1 + px;
         rd[it] = make_uint4(0, 0, 0, 0);
         if (!REC) ra[it] = rb[it] = make_uint4(0, 0, 0, 0);
         if (i < TOT2 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
-          const long m = img + (long)gy * W + gx;
-          const int c = cbase + k * E;
-          rd[it] = *reinterpret_cast<const uint4*>(dh + m * C + c);
+          rd[it] = *reinterpret_cast<const uint4*>(dh + eh + (long)(__umul24(py, rsh) + __umul24(px, C) + k * E));
           if (!REC) {
-            ra[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + c);
-            rb[it] = *reinterpret_cast<const uint4*>(t2 + m * C2 + C + c);
+            const long o = e2 + (long)(__umul24(py, rs1) + __umul24(px, C2) + k * E);
+            ra[it] = *reinterpret_cast<const uint4*>(t2 + o);
+            rb[it] = *reinterpret_cast<const uint4*>(t2 + o + C);
           }
         }
       }
@@ -661,14 +671,15 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
     const float4 bq = ld4(p.bdw + gc);
     for (int pix = x; pix < LH * LW; pix += DWT_TW) {
       const int row = pix / LW, col = pix % LW;
-      float4 a = bq;
+      f2v a0 = f2v{bq.x, bq.y}, a1 = f2v{bq.z, bq.w};
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const float4 v = ldq(SX(row + t / 3 - 1, col + t % 3 - 1) + lc);
-        a.x = fmaf(wk[0][t], v.x, a.x); a.y = fmaf(wk[1][t], v.y, a.y);
-        a.z = fmaf(wk[2][t], v.z, a.z); a.w = fmaf(wk[3][t], v.w, a.w);
+        f2v v0, v1;
+        ldq2(SX(row + t / 3 - 1, col + t % 3 - 1) + lc, v0, v1);
+        a0 = __builtin_elementwise_fma(wk[t][0], v0, a0);
+        a1 = __builtin_elementwise_fma(wk[t][1], v1, a1);
       }
-      stq(sg + pix * CSL + lc, a);
+      stq(sg + pix * CSL + lc, make_float4(a0.x, a0.y, a1.x, a1.y));
     }
   }
   if (FUSED) {
@@ -712,49 +723,56 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   }
   __syncthreads();
   // ---- compute: thread = (quad q, column x)
-  float4 aw[9], ab = f4(0.f);
+  f2v aw[9][2], ab[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
 #pragma unroll
-  for (int t = 0; t < 9; ++t) aw[t] = f4(0.f);
-  float4 gw[3][3], xw[3][3];
+  for (int t = 0; t < 9; ++t) aw[t][0] = aw[t][1] = f2v{0.f, 0.f};
+  f2v gw[3][3][2], xw[3][3][2];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    gw[1][j] = ldq(sg + (0 * LW + x + j) * CSL + lc);
-    gw[2][j] = ldq(sg + (1 * LW + x + j) * CSL + lc);
-    xw[1][j] = ldq(SX(0, x + j) + lc);
-    xw[2][j] = ldq(SX(1, x + j) + lc);
+    ldq2(sg + (0 * LW + x + j) * CSL + lc, gw[1][j][0], gw[1][j][1]);
+    ldq2(sg + (1 * LW + x + j) * CSL + lc, gw[2][j][0], gw[2][j][1]);
+    ldq2(SX(0, x + j) + lc, xw[1][j][0], xw[1][j][1]);
+    ldq2(SX(1, x + j) + lc, xw[2][j][0], xw[2][j][1]);
   }
-  T* dt1 = reinterpret_cast<T*>(p.dt1);
+  // this thread's dt1 column: one 64-bit base; row r at + r * rs1 (a scalar product: r is unrolled, rs1 uniform)
+  T* dtp = reinterpret_cast<T*>(p.dt1) + (img + (long)y0 * W + x0 + x) * C2 + gc;
   const bool col_ok = x0 + x < W;
 #pragma unroll
   for (int r = 0; r < TH; ++r) {
 #pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        gw[0][j][hh] = gw[1][j][hh]; gw[1][j][hh] = gw[2][j][hh];
+        xw[0][j][hh] = xw[1][j][hh]; xw[1][j][hh] = xw[2][j][hh];
+      }
+#pragma unroll
     for (int j = 0; j < 3; ++j) {
-      gw[0][j] = gw[1][j]; gw[1][j] = gw[2][j];
-      xw[0][j] = xw[1][j]; xw[1][j] = xw[2][j];
-      gw[2][j] = ldq(sg + ((r + 2) * LW + x + j) * CSL + lc);
-      xw[2][j] = ldq(SX(r + 2, x + j) + lc);
+      ldq2(sg + ((r + 2) * LW + x + j) * CSL + lc, gw[2][j][0], gw[2][j][1]);
+      ldq2(SX(r + 2, x + j) + lc, xw[2][j][0], xw[2][j][1]);
     }
-    float4 acc = f4(0.f);
-    const float4 gc4 = gw[1][1];
+    f2v acc[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
 #pragma unroll
     for (int dh = -1; dh <= 1; ++dh)
 #pragma unroll
       for (int dw = -1; dw <= 1; ++dw) {
         const int t = (dh + 1) * 3 + (dw + 1);
-        const float4 gv = gw[1 - dh][1 - dw];
-        acc.x = fmaf(wk[0][t], gv.x, acc.x); acc.y = fmaf(wk[1][t], gv.y, acc.y);
-        acc.z = fmaf(wk[2][t], gv.z, acc.z); acc.w = fmaf(wk[3][t], gv.w, acc.w);
-        aw[t] = fma4(gc4, xw[1 + dh][1 + dw], aw[t]);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          acc[hh] = __builtin_elementwise_fma(wk[t][hh], gw[1 - dh][1 - dw][hh], acc[hh]);
+          aw[t][hh] = __builtin_elementwise_fma(gw[1][1][hh], xw[1 + dh][1 + dw][hh], aw[t][hh]);
+        }
       }
-    ab += gc4;
-    if (col_ok && y0 + r < H) stq(dt1 + (img + (long)(y0 + r) * W + x0 + x) * C2 + gc, acc);
+    ab[0] += gw[1][1][0];
+    ab[1] += gw[1][1][1];
+    if (col_ok && y0 + r < H) stq(dtp + (unsigned)r * rs1, make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y));
   }
   // ---- reduce the 40 partials over the tile's columns: lanes of one quad differ in bits >= log2(NQ)
   float v[40];
 #pragma unroll
   for (int t = 0; t < 10; ++t) {
-    const float4 a4 = t < 9 ? aw[t] : ab;
-    v[4 * t] = a4.x; v[4 * t + 1] = a4.y; v[4 * t + 2] = a4.z; v[4 * t + 3] = a4.w;
+    const f2v a0 = t < 9 ? aw[t][0] : ab[0], a1 = t < 9 ? aw[t][1] : ab[1];
+    v[4 * t] = a0.x; v[4 * t + 1] = a0.y; v[4 * t + 2] = a1.x; v[4 * t + 3] = a1.y;
   }
 #pragma unroll
   for (int i = 0; i < 40; ++i)
@@ -818,18 +836,21 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   const int C = p.C, C2 = 2 * C, H = p.H, W = p.W;
   const long img = (long)b * H * W;
   const int cbase = slice * HS;
-  {  // all staging loads issued before the LDS stores (one memory latency per tile)
+  const unsigned rs1 = (unsigned)W * C2, rsg = (unsigned)W * C;  // row strides (elements), < 2^24 (launcher)
+  {  // all staging loads issued before the LDS stores (one memory latency per tile); 32-bit in-frame offsets
     const T* t1 = reinterpret_cast<const T*>(p.t1);
     constexpr int TOT = LH * LW * 4, N1 = (TOT + NT - 1) / NT;
+    const long e1 = (img + (long)(y0 - 1) * W + (x0 - 1)) * C2 + cbase;
     uint4 v[N1];
 #pragma unroll
     for (int it = 0; it < N1; ++it) {
       const int i = tid + it * NT;
       const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
-      const int gy = y0 - 1 + pix / LW, gx = x0 - 1 + pix % LW;
+      const int py = pix / LW, px = pix % LW;
+      const int gy = y0 - 1 + py, gx = x0 - 1 + px;
       v[it] = make_uint4(0, 0, 0, 0);
       if (i < TOT && gy >= 0 && gy < H && gx >= 0 && gx < W)
-        v[it] = *reinterpret_cast<const uint4*>(t1 + (img + (long)gy * W + gx) * C2 + hh * C + cbase + k * E);
+        v[it] = *reinterpret_cast<const uint4*>(t1 + e1 + (long)(__umul24(py, rs1) + __umul24(px, C2) + hh * C + k * E));
     }
 #pragma unroll
     for (int it = 0; it < N1; ++it) {
@@ -842,53 +863,65 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   const int qg = tid % NQG, x = tid / NQG;
   const int la = 4 * qg, lb = HS + 4 * qg;       // local channels (LDS)
   const int gca = cbase + 4 * qg, gcb = C + gca;  // global conv channels
-  float wa[4][9], wb[4][9];
+  // taps of the 4 gate channels (a) and their 4 partners (b) as packed pairs: the FMAs are v_pk_fma_f32 on pairs
+  f2v wa[9][2], wb[9][2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      wa[j][t] = p.wdw[(gca + j) * 9 + t];
-      wb[j][t] = p.wdw[(gcb + j) * 9 + t];
+    for (int hh = 0; hh < 2; ++hh) {
+      wa[t][hh] = f2v{p.wdw[(gca + 2 * hh) * 9 + t], p.wdw[(gca + 2 * hh + 1) * 9 + t]};
+      wb[t][hh] = f2v{p.wdw[(gcb + 2 * hh) * 9 + t], p.wdw[(gcb + 2 * hh + 1) * 9 + t]};
     }
   const float4 ba = ld4(p.bdw + gca), bb = ld4(p.bdw + gcb);
-  float4 xa[3][3], xb[3][3];
+  f2v xa[3][3][2], xb[3][3][2];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    xa[1][j] = ldq(sx + (0 * LW + x + j) * CSL + la);
-    xa[2][j] = ldq(sx + (1 * LW + x + j) * CSL + la);
-    xb[1][j] = ldq(sx + (0 * LW + x + j) * CSL + lb);
-    xb[2][j] = ldq(sx + (1 * LW + x + j) * CSL + lb);
+    ldq2(sx + (0 * LW + x + j) * CSL + la, xa[1][j][0], xa[1][j][1]);
+    ldq2(sx + (1 * LW + x + j) * CSL + la, xa[2][j][0], xa[2][j][1]);
+    ldq2(sx + (0 * LW + x + j) * CSL + lb, xb[1][j][0], xb[1][j][1]);
+    ldq2(sx + (1 * LW + x + j) * CSL + lb, xb[2][j][0], xb[2][j][1]);
   }
-  T* t2 = reinterpret_cast<T*>(p.t2);
-  T* g = reinterpret_cast<T*>(p.g);
+  // this thread's column of t2 / g: one 64-bit base each, then a row stride per row
+  const long m0 = img + (long)y0 * W + x0 + x;
+  T* t2p = p.t2 ? reinterpret_cast<T*>(p.t2) + m0 * C2 : nullptr;
+  T* gp = reinterpret_cast<T*>(p.g) + m0 * C;
   float4 pacc = f4(0.f);
   const bool col_ok = x0 + x < W;
 #pragma unroll
   for (int r = 0; r < TH; ++r) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      xa[0][j] = xa[1][j]; xa[1][j] = xa[2][j];
-      xb[0][j] = xb[1][j]; xb[1][j] = xb[2][j];
-      xa[2][j] = ldq(sx + ((r + 2) * LW + x + j) * CSL + la);
-      xb[2][j] = ldq(sx + ((r + 2) * LW + x + j) * CSL + lb);
-    }
-    float4 aa = ba, ab = bb;
+    for (int j = 0; j < 3; ++j)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const float4 va = xa[t / 3][t % 3], vb = xb[t / 3][t % 3];
-      aa.x = fmaf(wa[0][t], va.x, aa.x); aa.y = fmaf(wa[1][t], va.y, aa.y);
-      aa.z = fmaf(wa[2][t], va.z, aa.z); aa.w = fmaf(wa[3][t], va.w, aa.w);
-      ab.x = fmaf(wb[0][t], vb.x, ab.x); ab.y = fmaf(wb[1][t], vb.y, ab.y);
-      ab.z = fmaf(wb[2][t], vb.z, ab.z); ab.w = fmaf(wb[3][t], vb.w, ab.w);
-    }
-    if (col_ok && y0 + r < H) {
-      const long m = img + (long)(y0 + r) * W + x0 + x;
-      if (t2) {  // null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
-        stq(t2 + m * C2 + gca, aa);
-        stq(t2 + m * C2 + gcb, ab);
+      for (int hh = 0; hh < 2; ++hh) {
+        xa[0][j][hh] = xa[1][j][hh]; xa[1][j][hh] = xa[2][j][hh];
+        xb[0][j][hh] = xb[1][j][hh]; xb[1][j][hh] = xb[2][j][hh];
       }
-      const float4 gv = aa * ab;
-      stq(g + m * C + gca, gv);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      ldq2(sx + ((r + 2) * LW + x + j) * CSL + la, xa[2][j][0], xa[2][j][1]);
+      ldq2(sx + ((r + 2) * LW + x + j) * CSL + lb, xb[2][j][0], xb[2][j][1]);
+    }
+    f2v a2[2] = {f2v{ba.x, ba.y}, f2v{ba.z, ba.w}}, b2[2] = {f2v{bb.x, bb.y}, f2v{bb.z, bb.w}};
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        a2[hh] = __builtin_elementwise_fma(wa[t][hh], xa[t / 3][t % 3][hh], a2[hh]);
+        b2[hh] = __builtin_elementwise_fma(wb[t][hh], xb[t / 3][t % 3][hh], b2[hh]);
+      }
+    const float4 aa = make_float4(a2[0].x, a2[0].y, a2[1].x, a2[1].y);
+    const float4 ab = make_float4(b2[0].x, b2[0].y, b2[1].x, b2[1].y);
+    if (col_ok && y0 + r < H) {
+      if (t2p) {  // null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
+        T* q2 = t2p + (unsigned)r * rs1;
+        stq(q2 + gca, aa);
+        stq(q2 + gcb, ab);
+      }
+      float4 gv = aa * ab;
+      // the fp32 product is what is rounded to the storage type (as in the other SimpleGate kernels): kept opaque so
+      // the mul + convert is not folded into one mixed-precision FMA (one rounding instead of two: other bits)
+      asm volatile("" : "+v"(gv.x), "+v"(gv.y), "+v"(gv.z), "+v"(gv.w));
+      stq(gp + (unsigned)r * rsg + gca, gv);
       pacc += gv;
     }
   }
@@ -954,6 +987,7 @@ Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
 int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float* ds, const void* t2, const void* t1,
                     const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
                     int W, int C, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE((long)W * 2 * C < (1L << 24), "depthwise backward: W * 2C must be < 2^24 (24-bit tile offsets)");
   const int hs = dtype != 0 ? 16 : 8;
   const int tw = dw_bwd_tw(W);
   const bool rec = dh != nullptr && t2 == nullptr;  // fused, t2 recomputed from t1
@@ -1201,6 +1235,7 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
   NBP_REQUIRE(t2 || dw_tiled_ok(C, dtype), "nbp_dw_sg_pool_fwd: t2 may be NULL only on the tiled path (nbp_dw_tiled)");
   NBP_REQUIRE(C % 4 == 0 && C / 4 <= 1024, "nbp_dw_sg_pool_fwd: C");
   if (dw_tiled_ok(C, dtype)) {
+    NBP_REQUIRE((long)W * 2 * C < (1L << 24), "nbp_dw_sg_pool_fwd: W * 2C must be < 2^24 (24-bit tile offsets)");
     const int tw = dw_fwd_tw(W, dtype), hs = dtype != 0 ? 16 : 8;
     DwFwdP p{t1, wdw, bdw, t2, g, pool_slab, B, H, W, C, cdiv(W, tw), dw_fwd_tiles(H, W, dtype), C / hs};
     const long nblk = (long)B * p.tiles * p.slices;

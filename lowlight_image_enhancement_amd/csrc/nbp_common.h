@@ -42,6 +42,8 @@ __device__ __forceinline__ float4 fma4(float4 a, float4 b, float4 c) {
   return make_float4(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z), fmaf(a.w, b.w, c.w));
 }
 __device__ __forceinline__ float get(float4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+// packed fp32 pair (an adjacent VGPR pair: the operand of v_pk_fma_f32 / v_pk_add_f32)
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 // storage-type generic quad (4 consecutive channels) access: fp32 or 16-bit (bf16 / fp16) storage, fp32 math
 template <typename T>
@@ -52,6 +54,13 @@ __device__ __forceinline__ float4 ldq(const T* p) {
     const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(p);
     return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
   }
+}
+// the same quad as two packed pairs {c, c+1}, {c+2, c+3}
+template <typename T>
+__device__ __forceinline__ void ldq2(const T* p, f2v& lo, f2v& hi) {
+  const float4 v = ldq(p);
+  lo = f2v{v.x, v.y};
+  hi = f2v{v.z, v.w};
 }
 template <typename T>
 __device__ __forceinline__ void stq(T* p, float4 v) {

@@ -1,0 +1,31 @@
+"""Depthwise forward (dw_sg_pool) and fused SCA/SimpleGate/depthwise backward per level at cfg2 (B 16, fp16): GPU time
+per launch (HIP-graph replays) and the algorithmic HBM rate.  python scripts/dw_time.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from lowlight_image_enhancement_amd._lib import call, query  # noqa: E402
+from scripts.gemm_micro_util import timeit  # noqa: E402
+
+dev = torch.device("cuda:0")
+dt, td = 2, torch.float16
+out = []
+for (B, H, W, C) in [(16, 256, 256, 32), (16, 128, 128, 64), (16, 64, 64, 128), (16, 32, 32, 256)]:
+    M = B * H * W
+    g = torch.Generator(device=dev).manual_seed(0)
+    t1, t2 = (torch.randn(M, 2 * C, device=dev, generator=g).to(td) for _ in range(2))
+    dh, gg = torch.randn(M, C, device=dev, generator=g).to(td), torch.empty(M, C, device=dev, dtype=td)
+    a, ds = torch.rand(B, C, device=dev, generator=g), torch.randn(B, C, device=dev, generator=g)
+    wdw, bdw = torch.randn(2 * C, 9, device=dev, generator=g), torch.randn(2 * C, device=dev, generator=g)
+    dt1 = torch.empty(M, 2 * C, device=dev, dtype=td)
+    dW, db = torch.empty(2 * C, 9, device=dev), torch.empty(2 * C, device=dev)
+    ws = torch.empty(query("dw_bwd_workspace_floats", B, H, W, C), device=dev)
+    pool = torch.empty(B * query("dw_fwd_slab_rows", B, H, W, C, dt) * C, device=dev)
+    tf = timeit(lambda: call("dw_sg_pool_fwd", t1, wdw, bdw, t2, gg, pool, B, H, W, C, dt), reps=50)
+    tb = timeit(lambda: call("sca_sg_dw_bwd", dh, a, ds, t2, t1, wdw, dt1, dW, db, ws, B, H, W, C, dt), reps=50)
+    bf, bb = M * 2 * 5 * C, M * 2 * 7 * C  # fwd t1 in, t2 + g out; bwd dh + t2 + t1 in, dt1 out
+    out.append(f"{H}x{W}xC{C}: fwd {tf:7.1f} us ({bf / tf / 1e3:5.0f} GB/s) | bwd {tb:7.1f} us ({bb / tb / 1e3:5.0f} GB/s)"
+               " (bwd incl. its two slab reductions)")
+    print(out[-1], flush=True)
