@@ -190,7 +190,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
     const float4 c0 = ld4(Cs + row * CLS + c8), c1 = ld4(Cs + row * CLS + c8 + 4);
     v[0] = c0.x; v[1] = c0.y; v[2] = c0.z; v[3] = c0.w; v[4] = c1.x; v[5] = c1.y; v[6] = c1.z; v[7] = c1.w;
     if constexpr (CMODE == CM_LNBWD) {  // dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * lnw
-      static_assert(BN == 128 || BN == 256, "CM_LNBWD (tiled): full-row tiles");
+      static_assert(BN == 128 || BN == 256 || BN == 512, "CM_LNBWD (tiled): full-row tiles");
       const long off = (long)grow * N + gcol;
       float xv[8], rv[8];
       ld8f<TC>(p.R, off, xv);
@@ -301,7 +301,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       }
       st8f<TC>(p.C, off, v);
       if constexpr (CMODE == CM_RESLN) {  // the row's G8 chunks are G8 consecutive lanes (BN = N): group sums
-        static_assert(BN == 128 || BN == 256, "CM_RESLN (tiled): full-row tiles");
+        static_assert(BN == 128 || BN == 256 || BN == 512, "CM_RESLN (tiled): full-row tiles");
         float xv[8], sm = 0.f, q = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -361,11 +361,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
         Cs[(wave * 2 + 1) * BN + lane * 8 + j] = cb[j];
       }
     __syncthreads();
-    if (tid < BN) {
-      const float tw = ((Cs[0 * BN + tid] + Cs[2 * BN + tid]) + Cs[4 * BN + tid]) + Cs[6 * BN + tid];
-      const float tb = ((Cs[1 * BN + tid] + Cs[3 * BN + tid]) + Cs[5 * BN + tid]) + Cs[7 * BN + tid];
-      p.slab_w[(long)blockIdx.x * N + tid] = tw;
-      p.slab_b[(long)blockIdx.x * N + tid] = tb;
+    for (int c = tid; c < BN; c += NT) {  // (BN 512: two columns per thread)
+      const float tw = ((Cs[0 * BN + c] + Cs[2 * BN + c]) + Cs[4 * BN + c]) + Cs[6 * BN + c];
+      const float tb = ((Cs[1 * BN + c] + Cs[3 * BN + c]) + Cs[5 * BN + c]) + Cs[7 * BN + c];
+      p.slab_w[(long)blockIdx.x * N + c] = tw;
+      p.slab_b[(long)blockIdx.x * N + c] = tb;
     }
   }
   if constexpr (CMODE == CM_CHANDOT) {  // threads sharing a column chunk: lanes 8 apart, then the 4 waves (fixed order)
@@ -1346,19 +1346,21 @@ void launch(const GemmPB& p, hipStream_t st) {
       if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
         if (gemm_waves() == 8) {  // 2 x 4 waves of (BM / 2) x (BN / 4): two waves per SIMD
           if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          else if (nd == 3) gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+          else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
           else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
           return;
         }
       }
       if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
-      else if (nd == 3) gemm_glds_kernel<BM, BN, 3, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       return;
     }
   }
-  if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
-  else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
+  if constexpr (BN <= 256) {  // the register-staged tiles (a 64 x 512 one would not fit its double buffer in LDS)
+    if (p.K <= 32) gemm_bf16_kernel<BM, BN, 32, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
+    else gemm_bf16_kernel<BM, BN, 64, AMODE, CMODE, TA, TC, H><<<grid, 256, 0, st>>>(p);
+  }
 }
 
 // largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 512 blocks (2 per CU; with the

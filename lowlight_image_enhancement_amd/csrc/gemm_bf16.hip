@@ -60,7 +60,7 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
 }
 
 size_t nbp_dgrad_ln_workspace_floats(long M, int N) {
-  return (size_t)2 * (N == 128 || N == 256 ? (M + 63) / 64 : skinny_blocks(M)) * N;
+  return (size_t)2 * (N == 128 || N == 256 || N == 512 ? (M + 63) / 64 : skinny_blocks(M)) * N;
 }
 
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
@@ -70,22 +70,24 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_ln_bwd: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   float *slab_w, *slab_b;
   long nb;
-  if (N == 128 || N == 256) {  // 64 x N tiles of the tiled kernel: a whole row per tile
+  if (N == 128 || N == 256 || N == 512) {  // 64 x N tiles of the tiled kernel: a whole row per tile
     NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_ln_bwd: K, lda, ldb multiples of 8");
+    NBP_REQUIRE(N != 512 || (K > 32 && (glds_depth() < 0 || glds_depth() >= 2)), "nbp_dgrad_ln_bwd: N = 512 runs on the LDS-DMA tiles only");
     nb = (M + 63) / 64;
     NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
     GemmPB p{A, lda, nullptr, 1, Wt, ldb, dx, N, M, N, K, 0, 0, 0, nullptr, x,
              nullptr, nullptr, lnw, nullptr, nullptr, nullptr, 0.f, reinterpret_cast<const float2*>(stats), dres, ws,
              ws + nb * N};
     NBP_DISPATCH_H(dtype, {
-      if (N == 256) launch<64, 256, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
+      if (N == 512) launch<64, 512, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
+      else if (N == 256) launch<64, 256, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
       else launch<64, 128, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
     });
     slab_w = p.slab_w;
     slab_b = p.slab_b;
   } else {
     NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
-                "nbp_dgrad_ln_bwd: N must be 32, 64, 128 or 256, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
+                "nbp_dgrad_ln_bwd: N must be 32, 64, 128, 256 or 512, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
     nb = skinny_blocks(M);
     NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
     slab_w = ws;
@@ -111,12 +113,15 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
   NBP_REQUIRE(A && Bw && C && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args");
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_gemm_res_ln: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   NBP_REQUIRE(a_mode == AM_PLAIN || (a_mode == AM_SCALE && a_scale && rows_per_img > 0), "nbp_gemm_res_ln: a_mode");
-  if (N == 128 || N == 256) {  // 64 x N tiles of the tiled kernel: a whole row per tile
+  if (N == 128 || N == 256 || N == 512) {  // 64 x N tiles of the tiled kernel: a whole row per tile
     NBP_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "nbp_gemm_res_ln: K, lda, ldb multiples of 8");
+    NBP_REQUIRE(N != 512 || (K > 32 && (glds_depth() < 0 || glds_depth() >= 2)), "nbp_gemm_res_ln: N = 512 runs on the LDS-DMA tiles only");
     GemmPB p{A, lda, a_scale, rows_per_img, Bw, ldb, C, N, M, N, K, 0, 0, 0, bias,
              R, rscale, nullptr, lnw, lnb, nout, reinterpret_cast<float2*>(stats), eps};
     NBP_DISPATCH_H(dtype, {
-      if (N == 256 && a_mode == AM_SCALE) launch<64, 256, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
+      if (N == 512 && a_mode == AM_SCALE) launch<64, 512, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
+      else if (N == 512) launch<64, 512, AM_PLAIN, CM_RESLN, H, H, H>(p, S(s));
+      else if (N == 256 && a_mode == AM_SCALE) launch<64, 256, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
       else if (N == 256) launch<64, 256, AM_PLAIN, CM_RESLN, H, H, H>(p, S(s));
       else if (a_mode == AM_SCALE) launch<64, 128, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
       else launch<64, 128, AM_PLAIN, CM_RESLN, H, H, H>(p, S(s));
@@ -124,7 +129,7 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
     return check_launch("gemm_res_ln(tiled)");
   }
   NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
-              "nbp_gemm_res_ln: N must be 32, 64, 128 or 256, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
+              "nbp_gemm_res_ln: N must be 32, 64, 128, 256 or 512, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
   NBP_DISPATCH_H(dtype, {
     SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, a_scale, rows_per_img, reinterpret_cast<const H*>(Bw), ldb,
                  reinterpret_cast<H*>(C), N, M, N, K, bias, reinterpret_cast<const H*>(R), rscale, nullptr,

@@ -116,6 +116,10 @@ class NAFNet(nn.Module):
         # the LayerNorm fusions at C = 256 too (64 x 256 tiles): NBP_FUSE_LN256 = 1 (both, default: +1.1 % with the
         # 8-wave LDS-DMA tiles; round 1 with register-staged tiles: fwd -0.4 %, bwd +0.35 %), bwd, fwd or 0
         self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "1")
+        # ... and at C = 512 (the middle level: 64 x 512 tiles, one 144 KB workgroup per CU, 64 workgroups at bs 16):
+        # NBP_FUSE_LN512 = 1 (both), bwd, fwd or 0 (default: measured -7 % / -2 % / -5 % for 1 / fwd / bwd,
+        # profiles/r02_v6/ab_ln512.txt -- 64 workgroups leave 3/4 of the CUs idle for longer than the LN launch costs)
+        self.fuse_ln512 = os.environ.get("NBP_FUSE_LN512", "0")
         # the wide (C >= 128) weight gradients of a whole U-Net level (conv5's U, conv4, conv3's U, conv1 of every
         # NAFBlock of the level) queued during the level's backward and launched as ONE grouped launch at its end,
         # with M-splits chosen for the group (NBP_GROUP_WGRAD=0: one launch per weight gradient)
@@ -412,7 +416,8 @@ class NAFNet(nn.Module):
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
         fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and (c in (32, 64, 128) or
-                                                                           (c == 256 and self.fuse_ln256 in ("1", "fwd")))
+                                                                           (c == 256 and self.fuse_ln256 in ("1", "fwd")) or
+                                                                           (c == 512 and self.fuse_ln512 in ("1", "fwd")))
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
@@ -736,7 +741,8 @@ class NAFNet(nn.Module):
         # conv4 input gradient + norm2 backward + residual
         # LN backward in the dgrad's epilogue (dn never stored): skinny kernel at C 32 / 64, 64 x 128 tiles at 128
         fuse_ln = dt != 0 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
-                               (c == 256 and self.fuse_ln256 in ("1", "bwd")))
+                               (c == 256 and self.fuse_ln256 in ("1", "bwd")) or
+                               (c == 512 and self.fuse_ln512 in ("1", "bwd")))
         dy = E(M, c)
         if not wg_folded:
             self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,

@@ -55,7 +55,8 @@ def test_gemm_fp16_simplegate_epilogues(dev, M, C):
     assert (g.double() - gr).abs().max().item() <= 1e-3 * gr.abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("M,N,K", [(4096, 32, 64), (3000, 64, 128), (4096, 128, 256), (2048, 256, 512)])
+@pytest.mark.parametrize("M,N,K", [(4096, 32, 64), (3000, 64, 128), (4096, 128, 256), (2048, 256, 512),
+                                   (4096, 512, 1024)])
 def test_dgrad_ln_bwd_fp16(dev, M, N, K):
     """The dgrad + LayerNorm2d-backward fusion on fp16 storage vs float64 (arch_util.py:277-289)."""
     from lowlight_image_enhancement_amd._lib import call, query

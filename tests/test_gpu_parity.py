@@ -605,7 +605,8 @@ def test_gemm_bf16_skinny_path(dev, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 32, 64), (3000, 64, 128), (777, 32, 32), (4096, 128, 256), (3000, 128, 256),
-                                   (100, 128, 128), (4096, 256, 512), (333, 256, 256)])
+                                   (100, 128, 128), (4096, 256, 512), (333, 256, 256), (4096, 512, 1024),
+                                   (333, 512, 512)])
 def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
     """Fused 1x1-conv input gradient + LayerNorm2d backward + residual (skinny bf16 GEMM epilogue) vs float64 math on
     the same bf16 operands: dn = A W^T, dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * w."""
@@ -636,7 +637,8 @@ def test_dgrad_ln_bwd_against_float64(dev, M, N, K):
 
 @pytest.mark.parametrize("M,N,K,amode", [(4096, 32, 32, 2), (3001, 64, 64, 0), (777, 32, 64, 0), (65, 64, 128, 2),
                                          (4096, 128, 128, 2), (3001, 128, 256, 0), (100, 128, 128, 0),
-                                         (4096, 256, 256, 2), (333, 256, 512, 0)])
+                                         (4096, 256, 256, 2), (333, 256, 512, 0), (4096, 512, 512, 2),
+                                         (333, 512, 1024, 0)])
 def test_gemm_res_ln_equals_gemm_then_ln_fwd(dev, M, N, K, amode):
     """conv3 / conv5 with the LayerNorm2d forward in the epilogue (nbp_gemm_res_ln) equals the skinny GEMM with the
     residual followed by the standalone ln_fwd_nhwc, bit for bit (same stored bf16 row, same summation order)."""
