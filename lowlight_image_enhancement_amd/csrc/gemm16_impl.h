@@ -364,8 +364,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
     for (int c = tid; c < BN; c += NT) {  // (BN 512: two columns per thread)
       const float tw = ((Cs[0 * BN + c] + Cs[2 * BN + c]) + Cs[4 * BN + c]) + Cs[6 * BN + c];
       const float tb = ((Cs[1 * BN + c] + Cs[3 * BN + c]) + Cs[5 * BN + c]) + Cs[7 * BN + c];
-      p.slab_w[(long)blockIdx.x * N + c] = tw;
-      p.slab_b[(long)blockIdx.x * N + c] = tb;
+      p.slab_w[(long)(m0 / BM) * N + c] = tw;  // the tile's row block (not blockIdx: tile_map may permute it)
+      p.slab_b[(long)(m0 / BM) * N + c] = tb;
     }
   }
   if constexpr (CMODE == CM_CHANDOT) {  // threads sharing a column chunk: lanes 8 apart, then the 4 waves (fixed order)
@@ -1380,6 +1380,15 @@ long gemm_minblk() {
 // Measured (scripts/conv_micro.py, fp16, bs 8): bit 2 +34-39 % on the 128^2 x 256 and 64^2 x 512 VGG layers
 // (629 -> 842, 659 -> 913 TFLOP/s; bitwise equal: the same MFMA sequence per output element); bit 0 neutral and
 // bit 1 -1.5 % on cfg3 (one 135 KB workgroup per CU and only 1.5x the work per staged byte), so both stay off.
+// NBP_GEMM_MAP (read per launch; A/B measurement, default 0): GemmPB::tile_map for the NAFNet 1x1-conv GEMMs of
+// nbp_gemm_bf16 / nbp_gemm_res_ln / nbp_dgrad_ln_bwd -- each XCD then owns a contiguous run of row tiles, the rows the
+// depthwise tiles of the same images (xcd_remap, image-major) also run on, so a producer's output can be an L2 hit for
+// its consumer on the same XCD
+int gemm_tile_map() {
+  const char* e = getenv("NBP_GEMM_MAP");
+  return e ? atoi(e) : 0;
+}
+
 int conv_tile() {
   const char* e = getenv("NBP_CONV_TILE");
   return e ? atoi(e) : 4;
