@@ -947,9 +947,12 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
 
 // backward tile height: 16 rows; NBP_DW_BWD_TH=8 selects 8 at W <= 32 (measured neutral in the step: the shorter
 // row chain is offset by the doubled weight-gradient slab)
+// NBP_DW_BWD_TH_BIG=8: 8-row tiles at W > 32 too (43.5 KB of LDS instead of 78: three workgroups per CU; A/B knob)
 inline int dw_bwd_th(int W) {
   static const int small = getenv("NBP_DW_BWD_TH") ? atoi(getenv("NBP_DW_BWD_TH")) : 16;
-  return W <= 32 && small == 8 ? 8 : DWT_TH;  // the instantiated heights
+  static const int big = getenv("NBP_DW_BWD_TH_BIG") ? atoi(getenv("NBP_DW_BWD_TH_BIG")) : 16;
+  if (W > 32) return big == 8 ? 8 : DWT_TH;
+  return small == 8 ? 8 : DWT_TH;  // the instantiated heights
 }
 int dw_tiles(int H, int W, bool rec = false) {
   return cdiv(H, rec ? DWT_TH_REC : dw_bwd_th(W)) * cdiv(W, dw_bwd_tw(W));
