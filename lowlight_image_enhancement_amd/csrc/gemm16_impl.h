@@ -912,10 +912,31 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
     load_a(tile, a0);
     if constexpr (RC) load_a2(tile, c0);
   }
+  // CM_LNBWD: a row's cpr = 4 NT lanes are consecutive (N = 32 NT), so a lane's epilogue rows are lane / cpr + q * rstep
+  // for q < 2 NT; their x / dres chunks and LN statistics are loaded before the tile's MFMAs (the latency then overlaps
+  // the MFMAs and the LDS staging instead of following them)
+  // (NT = 1 only: at NT = 2 the 4 preloaded rows cost more registers than the overlap gains -- measured 40 -> 50 us at
+  // level 1, 69 -> 60 us at level 0)
+  constexpr bool PRE = CMODE == CM_LNBWD && NT == 1;
+  constexpr int NPL = PRE ? 2 * NT : 1;
   for (; tile < ntiles; tile += nwaves) {
     if (tile + nwaves < ntiles) {
       load_a(tile + nwaves, a1);
       if constexpr (RC) load_a2(tile + nwaves, c1);
+    }
+    vec_t<H, 8> xpre[NPL], rpre[NPL];
+    float2 spre[NPL];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) {
+        const long m = tile * 32 + lane / cpr + q * rstep;
+        if (m < M) {
+          const long off = m * p.ldc + ccol;
+          xpre[q] = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
+          rpre[q] = *reinterpret_cast<const vec_t<H, 8>*>(p.dres + off);
+          spre[q] = p.stats[m];
+        }
+      }
     }
     floatx16 acc[NT];
 #pragma unroll
@@ -963,7 +984,38 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
     }
     __builtin_amdgcn_wave_barrier();
     const long m0 = tile * 32;
-    for (int rr = lane / cpr; rr < 32; rr += rstep) {
+    if constexpr (PRE) {  // dx = (g - yhat mean(g yhat) - mean(g)) / den + dres, g = dn * lnw
+      constexpr int G = 4 * NT;
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) {
+        const int rr = lane / cpr + q * rstep;
+        const long m = m0 + rr;
+        if (m >= M) break;
+        const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
+        const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
+        const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+        const float2 st = spre[q];
+        const float inv = 1.f / st.y;
+        float yh[8], sg = 0.f, sgy = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          yh[j] = ((float)xpre[q][j] - st.x) * inv;
+          const float g = v[j] * rsc[j];
+          sg += g;
+          sgy = fmaf(g, yh[j], sgy);
+          aw[j] = fmaf(v[j], yh[j], aw[j]);
+          ab[j] += v[j];
+        }
+        sg = group_sum<G>(sg);
+        sgy = group_sum<G>(sgy);
+        const float mg = sg / (float)N, mgy = sgy / (float)N;
+        vec_t<H, 8> o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (H)((v[j] * rsc[j] - yh[j] * mgy - mg) * inv + (float)rpre[q][j]);
+        *reinterpret_cast<vec_t<H, 8>*>(p.C + m * p.ldc + ccol) = o;
+      }
+    }
+    for (int rr = lane / cpr; !PRE && rr < 32; rr += rstep) {
       const long m = m0 + rr;
       if (m >= M) {
         if constexpr (WGF) {  // the fold's dt tile: zero rows past M (their n2 rows are zero, stale data could be NaN)
@@ -998,7 +1050,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
       const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
       const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
       float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      if constexpr (CMODE == CM_LNBWD) {  // the row's cpr lanes are consecutive: shuffle sums within the group
+      if constexpr (CMODE == CM_LNBWD) {  // (NT > 1) the row's cpr lanes are consecutive: shuffle sums in the group
         constexpr int G = 4 * NT;
         const long off = m * p.ldc + ccol;
         const vec_t<H, 8> xv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
