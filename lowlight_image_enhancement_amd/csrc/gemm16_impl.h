@@ -916,7 +916,8 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   // for q < 2 NT; their x / dres chunks and LN statistics are loaded before the tile's MFMAs (the latency then overlaps
   // the MFMAs and the LDS staging instead of following them)
   // (NT = 1 only: at NT = 2 the 4 preloaded rows cost more registers than the overlap gains -- measured 40 -> 50 us at
-  // level 1, 69 -> 60 us at level 0)
+  // level 1, 69 -> 60 us at level 0; the same preload of the residual rows in the level-0 CM_RESLN epilogue measured
+  // 61 -> 79 us, not kept)
   constexpr bool PRE = CMODE == CM_LNBWD && NT == 1;
   constexpr int NPL = PRE ? 2 * NT : 1;
   for (; tile < ntiles; tile += nwaves) {

@@ -112,7 +112,7 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, int dtype,
                     nbp_stream_t s) {
-  NBP_REQUIRE(A && Bw && C && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args");
+  NBP_REQUIRE(A && Bw && C && R && lnw && lnb && nout && stats && M > 0, "nbp_gemm_res_ln: bad args (R: the residual)");
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_gemm_res_ln: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   NBP_REQUIRE(a_mode == AM_PLAIN || (a_mode == AM_SCALE && a_scale && rows_per_img > 0), "nbp_gemm_res_ln: a_mode");
   if (N == 128 || N == 256 || N == 512) {  // 64 x N tiles of the tiled kernel: a whole row per tile
