@@ -275,9 +275,11 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
 // address of row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.  Two reads give the
 // 8 consecutive-m values of one fragment.  Rows are padded to 96 elements (192 B) so the four rows x two groups of
 // a half-wave hit 64 distinct banks.
-template <int GMODE, int XMODE, typename H>
+// RM = 64 (NBP_WGRAD_RM=64): 64-row stages -- twice the loads in flight per stage and half the barrier pairs; the
+// MFMA and bias-sum order over the rows is unchanged (bitwise equal to RM = 32)
+template <int GMODE, int XMODE, typename H, int RM = 32>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
-  constexpr int RM = 32, TNW = 64, TKW = 64, LS = 96;
+  constexpr int TNW = 64, TKW = 64, LS = 96, NR = RM / 32;
   __shared__ __attribute__((aligned(16))) H Gs[RM * LS];
   __shared__ __attribute__((aligned(16))) H Xs[RM * LS];
   const H* G = reinterpret_cast<const H*>(p.G);
@@ -304,33 +306,39 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
       acc[r] = 0.f;
     }
   };
-  // loader: one 16-byte chunk of G and one of X per thread: row r = tid >> 3, 8 columns at (tid & 7) * 8
+  // loader: NR 16-byte chunks of G and of X per thread: rows tid >> 3 (+ 32 i), 8 columns at (tid & 7) * 8
   const int lr = tid >> 3, lc = (tid & 7) * 8;
-  vec_t<H, 8> rg, rx;
+  vec_t<H, 8> rg[NR], rx[NR];
   auto load = [&](int m0) {
-    const int m = m0 + lr;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rg[j] = rx[j] = (H)0.f;
-    if (m < me) {
-      const int n = n0 + lc, k = k0 + lc;
-      if (n < p.N) {
-        const long off = GMODE == AM_S2D ? s2d_off(m, n, p.gh, p.gw, p.cs_g) : (long)m * p.ldg + n;
-        rg = *reinterpret_cast<const vec_t<H, 8>*>(G + off);
-      }
-      if (k < p.K) {
-        const long off = XMODE == AM_S2D ? s2d_off(m, k, p.gh, p.gw, p.cs_x) : (long)m * p.ldx + k;
-        rx = *reinterpret_cast<const vec_t<H, 8>*>(X + off);
-        if (XMODE == AM_SCALE) {
-          const float* sc = p.x_scale + (long)(m / p.rows_per_img) * p.K + k;
+    for (int i = 0; i < NR; ++i) {
+      const int m = m0 + lr + 32 * i;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) rx[j] = (H)((float)rx[j] * sc[j]);
+      for (int j = 0; j < 8; ++j) rg[i][j] = rx[i][j] = (H)0.f;
+      if (m < me) {
+        const int n = n0 + lc, k = k0 + lc;
+        if (n < p.N) {
+          const long off = GMODE == AM_S2D ? s2d_off(m, n, p.gh, p.gw, p.cs_g) : (long)m * p.ldg + n;
+          rg[i] = *reinterpret_cast<const vec_t<H, 8>*>(G + off);
+        }
+        if (k < p.K) {
+          const long off = XMODE == AM_S2D ? s2d_off(m, k, p.gh, p.gw, p.cs_x) : (long)m * p.ldx + k;
+          rx[i] = *reinterpret_cast<const vec_t<H, 8>*>(X + off);
+          if (XMODE == AM_SCALE) {
+            const float* sc = p.x_scale + (long)(m / p.rows_per_img) * p.K + k;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rx[i][j] = (H)((float)rx[i][j] * sc[j]);
+          }
         }
       }
     }
   };
   auto store = [&]() {
-    *reinterpret_cast<vec_t<H, 8>*>(Gs + lr * LS + lc) = rg;
-    *reinterpret_cast<vec_t<H, 8>*>(Xs + lr * LS + lc) = rx;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      *reinterpret_cast<vec_t<H, 8>*>(Gs + (lr + 32 * i) * LS + lc) = rg[i];
+      *reinterpret_cast<vec_t<H, 8>*>(Xs + (lr + 32 * i) * LS + lc) = rx[i];
+    }
   };
   // tr-read addressing (see header comment)
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
@@ -1229,6 +1237,14 @@ long wgroup_target() {
   return v;
 }
 
+// NBP_WGRAD_RM (read per launch; 64 default or 32): row-stage height of the narrow (N or K <= 64) weight-gradient
+// tiles.  64 measured +0.3 % at cfg2 (1214.0 -> 1217.9 img/s over three A/B pairs, profiles/r02_v6/ab_wgrad_rm.txt),
+// bitwise equal (tests/test_gpu_glds.py::test_narrow_wgrad_stage_height)
+int wgrad_rm() {
+  const char* e = getenv("NBP_WGRAD_RM");
+  return e && atoi(e) == 32 ? 32 : 64;
+}
+
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
 // launch (A/B measurement; tests compare the paths in one process)
 int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged tiles, +0.5 % over depth 2 (A/B)
@@ -1377,7 +1393,11 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
       else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64)
+        wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() == 64)
+        wgrad_bf16_kernel<AM_PLAIN, 3, H, 64><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
         wgrad_bf16_kernel<AM_PLAIN, 3, H><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE) wgrad_bf16_kernel<AM_PLAIN, AM_SCALE, H><<<grid, 256, 0, st>>>(p);

@@ -273,3 +273,38 @@ def test_wgrad_group_8wave(dev, dt):
         Xe = X.double() * (sc.double().repeat_interleave(r, 0) if r else 1.0)
         assert (c.double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5
         assert (d.double() - G.double().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("M,N,K,rows", [(1048576, 64, 32, 65536), (262144, 128, 64, 0), (262144, 64, 64, 16384),
+                                        (5000, 64, 32, 0)])
+def test_narrow_wgrad_stage_height(dev, dt, M, N, K, rows):
+    """Narrow weight gradients (N or K <= 64: levels 0 / 1) with 64-row stages (NBP_WGRAD_RM=64) vs 32-row stages:
+    the MFMA and bias-sum order over the rows is the same, so dW and db are bitwise equal; rows > 0: the per-image SCA
+    column scale folded per image."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(M + N + K + dt)
+    G = torch.randn(M, N, device=dev, generator=gen).to(DT[dt])
+    X = torch.randn(M, K, device=dev, generator=gen).to(DT[dt])
+    sc = torch.rand(M // rows, K, device=dev, generator=gen) + 0.5 if rows else None
+    n_ws = query("wgrad_workspace_floats", M, N, K)
+    ws = torch.empty(n_ws, device=dev)
+    res = {}
+    old = os.environ.get("NBP_WGRAD_RM")
+    try:
+        for rm in ("32", "64"):
+            os.environ["NBP_WGRAD_RM"] = rm
+            dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+            call("wgrad_f32", G, N, 0, X, K, 2 if rows else 0, sc, rows if rows else 1, M, N, K, 0, 0, 0, 0, dW, db,
+                 ws, n_ws, dt)
+            torch.cuda.synchronize()
+            res[rm] = (dW, db)
+    finally:
+        if old is None:
+            os.environ.pop("NBP_WGRAD_RM", None)
+        else:
+            os.environ["NBP_WGRAD_RM"] = old
+    assert torch.equal(res["32"][0], res["64"][0]) and torch.equal(res["32"][1], res["64"][1])
+    if M <= 262144:
+        Xe = X.double() * (sc.double().repeat_interleave(rows, 0)[:M] if rows else 1.0)
+        assert (res["64"][0].double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5
