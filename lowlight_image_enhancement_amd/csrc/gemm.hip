@@ -1239,10 +1239,11 @@ long wgroup_target() {
 
 // NBP_WGRAD_RM (read per launch; 64 default or 32): row-stage height of the narrow (N or K <= 64) weight-gradient
 // tiles.  64 measured +0.3 % at cfg2 (1214.0 -> 1217.9 img/s over three A/B pairs, profiles/r02_v6/ab_wgrad_rm.txt),
-// bitwise equal (tests/test_gpu_glds.py::test_narrow_wgrad_stage_height)
+// bitwise equal (tests/test_gpu_glds.py::test_narrow_wgrad_stage_height); 128 (49 KB of LDS) -1.5 %
+// (profiles/r02_v6/ab_wgrad_rm128.txt)
 int wgrad_rm() {
   const char* e = getenv("NBP_WGRAD_RM");
-  return e && atoi(e) == 32 ? 32 : 64;
+  return e && atoi(e) == 32 ? 32 : (e && atoi(e) == 128 ? 128 : 64);
 }
 
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
@@ -1393,10 +1394,14 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
       else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 128)
+        wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 128><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 128 == 0 && wgrad_rm() == 128)
+        wgrad_bf16_kernel<AM_PLAIN, 3, H, 128><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() == 64)
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() >= 64)
         wgrad_bf16_kernel<AM_PLAIN, 3, H, 64><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
         wgrad_bf16_kernel<AM_PLAIN, 3, H><<<grid, 256, 0, st>>>(p);

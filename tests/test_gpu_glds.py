@@ -292,7 +292,7 @@ def test_narrow_wgrad_stage_height(dev, dt, M, N, K, rows):
     res = {}
     old = os.environ.get("NBP_WGRAD_RM")
     try:
-        for rm in ("32", "64"):
+        for rm in ("32", "64", "128"):
             os.environ["NBP_WGRAD_RM"] = rm
             dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
             call("wgrad_f32", G, N, 0, X, K, 2 if rows else 0, sc, rows if rows else 1, M, N, K, 0, 0, 0, 0, dW, db,
@@ -304,7 +304,8 @@ def test_narrow_wgrad_stage_height(dev, dt, M, N, K, rows):
             os.environ.pop("NBP_WGRAD_RM", None)
         else:
             os.environ["NBP_WGRAD_RM"] = old
-    assert torch.equal(res["32"][0], res["64"][0]) and torch.equal(res["32"][1], res["64"][1])
+    for rm in ("64", "128"):
+        assert torch.equal(res["32"][0], res[rm][0]) and torch.equal(res["32"][1], res[rm][1]), rm
     if M <= 262144:
         Xe = X.double() * (sc.double().repeat_interleave(rows, 0)[:M] if rows else 1.0)
         assert (res["64"][0].double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5
