@@ -277,11 +277,15 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
 // a half-wave hit 64 distinct banks.
 // RM = 64 (NBP_WGRAD_RM=64): 64-row stages -- twice the loads in flight per stage and half the barrier pairs; the
 // MFMA and bias-sum order over the rows is unchanged (bitwise equal to RM = 32)
-template <int GMODE, int XMODE, typename H, int RM = 32>
+// DB: two LDS stage buffers -- the next stage is stored into the other buffer while this one is multiplied, one
+// barrier per stage instead of two (same MFMA / bias-sum order: bitwise equal)
+template <int GMODE, int XMODE, typename H, int RM = 32, bool DB = false>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
-  constexpr int TNW = 64, TKW = 64, LS = 96, NR = RM / 32;
-  __shared__ __attribute__((aligned(16))) H Gs[RM * LS];
-  __shared__ __attribute__((aligned(16))) H Xs[RM * LS];
+  constexpr int TNW = 64, TKW = 64, LS = 96, NR = RM / 32, NB = DB ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) H Gsb[NB * RM * LS];
+  __shared__ __attribute__((aligned(16))) H Xsb[NB * RM * LS];
+  H* Gs = Gsb;
+  H* Xs = Xsb;
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -333,13 +337,14 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
       }
     }
   };
-  auto store = [&]() {
+  auto store_to = [&](H* gs, H* xs) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      *reinterpret_cast<vec_t<H, 8>*>(Gs + (lr + 32 * i) * LS + lc) = rg[i];
-      *reinterpret_cast<vec_t<H, 8>*>(Xs + (lr + 32 * i) * LS + lc) = rx[i];
+      *reinterpret_cast<vec_t<H, 8>*>(gs + (lr + 32 * i) * LS + lc) = rg[i];
+      *reinterpret_cast<vec_t<H, 8>*>(xs + (lr + 32 * i) * LS + lc) = rx[i];
     }
   };
+  auto store = [&]() { store_to(Gs, Xs); };
   // tr-read addressing (see header comment)
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
   const int gcol = wn * 32 + 16 * (grp & 1) + 4 * pp;
@@ -378,10 +383,21 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
 #pragma unroll 8
         for (int r = 0; r < RM; ++r) bsum += (float)Gs[r * LS + tid];
       }
-      __syncthreads();
-      if (more) {
-        store();
+      if constexpr (DB) {
+        if (more) {  // the other buffer was last read before the previous stage's barrier
+          H* gn = Gs == Gsb ? Gsb + RM * LS : Gsb;
+          H* xn = Xs == Xsb ? Xsb + RM * LS : Xsb;
+          store_to(gn, xn);
+          Gs = gn;
+          Xs = xn;
+        }
         __syncthreads();
+      } else {
+        __syncthreads();
+        if (more) {
+          store();
+          __syncthreads();
+        }
       }
     }
   }
@@ -1246,6 +1262,13 @@ int wgrad_rm() {
   return e && atoi(e) == 32 ? 32 : (e && atoi(e) == 128 ? 128 : 64);
 }
 
+// NBP_WGRAD_DB=1 (read per launch; A/B): double-buffered LDS stages for the 64-row narrow weight-gradient tiles
+// (bitwise equal; measured -1 %: 48 KB of LDS per workgroup, profiles/r02_v6/ab_wgrad_db.txt -- off)
+int wgrad_db() {
+  const char* e = getenv("NBP_WGRAD_DB");
+  return e && e[0] == '1';
+}
+
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
 // launch (A/B measurement; tests compare the paths in one process)
 int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged tiles, +0.5 % over depth 2 (A/B)
@@ -1396,8 +1419,12 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 128)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 128><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64 && wgrad_db())
+        wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64, true><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() == 64 && wgrad_db())
+        wgrad_bf16_kernel<AM_PLAIN, 3, H, 64, true><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 128 == 0 && wgrad_rm() == 128)
         wgrad_bf16_kernel<AM_PLAIN, 3, H, 128><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);

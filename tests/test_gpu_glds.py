@@ -292,19 +292,22 @@ def test_narrow_wgrad_stage_height(dev, dt, M, N, K, rows):
     res = {}
     old = os.environ.get("NBP_WGRAD_RM")
     try:
-        for rm in ("32", "64", "128"):
-            os.environ["NBP_WGRAD_RM"] = rm
+        for rm in ("32", "64", "128", "64db"):
+            os.environ["NBP_WGRAD_RM"] = rm[:2] if rm == "64db" else rm
+            if rm == "64db":
+                os.environ["NBP_WGRAD_DB"] = "1"
             dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
             call("wgrad_f32", G, N, 0, X, K, 2 if rows else 0, sc, rows if rows else 1, M, N, K, 0, 0, 0, 0, dW, db,
                  ws, n_ws, dt)
             torch.cuda.synchronize()
             res[rm] = (dW, db)
     finally:
+        os.environ.pop("NBP_WGRAD_DB", None)
         if old is None:
             os.environ.pop("NBP_WGRAD_RM", None)
         else:
             os.environ["NBP_WGRAD_RM"] = old
-    for rm in ("64", "128"):
+    for rm in ("64", "128", "64db"):
         assert torch.equal(res["32"][0], res[rm][0]) and torch.equal(res["32"][1], res[rm][1]), rm
     if M <= 262144:
         Xe = X.double() * (sc.double().repeat_interleave(rows, 0)[:M] if rows else 1.0)
