@@ -6,7 +6,7 @@ HybridLoss terms L1 + SSIM + Phys_srgb, global-norm clip 0.01 + AdamW.  One "ste
 (+ bucketed RCCL all-reduce when N > 1) + clip + AdamW, all HIP kernels.  Default precision fp16 (fp16 storage and
 MFMA operands, fp32 accumulation / statistics / parameters, dynamic loss scaling): the reference's AMP dtype.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp16|bf16|fp32] [--quick]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp16|bf16|fp32] [--workload cfg2|cfg3|cfg4] [--quick]
     (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...)
 
 Rank 0 prints ONE JSON line.
@@ -17,8 +17,9 @@ Rank 0 prints ONE JSON line.
   (nbp_dw_sg_pool_fwd); rocprof kernel names in ROCPROF_KERNELS.
 * `nafblock_roofline`: the north-star figure, NAFBlock fwd+bwd algorithmic bytes (5*B*C*H*W*s per block,
   s = the storage bytes per element of this precision) vs 8 TB/s.
-* `modes` / `cfg3` (rank 0, N = 1, unless --quick): the other precision modes on the same workload, and a bounded
-  BASELINE configs[2] sample (bs 8 x 512^2, all six HybridLossPlus terms, synthetic VGG / LPIPS weights).
+* `modes` / `cfg3` / `cfg4` (rank 0, N = 1, unless --quick): the other precision modes on the same workload, a bounded
+  BASELINE configs[2] sample (bs 8 x 512^2, all six HybridLossPlus terms, synthetic VGG / LPIPS weights), and the
+  configs[3] model (w64, bs 16 per GPU: the scaling config; `--workload cfg4` times it at any N).
 * `cpu_baseline`: the CPU oracle (oracle/, kind "port") at the full cfg2 batch on this box's host cores (median of 3
   timed steps after 1 warm-up), as BASELINE.md prescribes.
 * `psnr_vs_cpu_ref_db`: GPU vs CPU-oracle output on the same weights and input, at the reference's init (zero layer
@@ -43,15 +44,22 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "training images/sec at 256×256 bs=16 (1/2/4/8 GPU) + PSNR vs CPU ref"
 CFG = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
 BLK = {k: v for k, v in CFG.items() if k != "width"}
-# BASELINE.json configs[1] (the headline) and configs[2] (VGG19 perceptual + LPIPS + ΔE00, bs8 512²; weights from
-# configs/colab/sid_newbp_rgb.yml:78-96; LPIPS is the HybridLossPlus term's net='vgg', synthetic offline weights)
+# BASELINE.json configs[1] (the headline) and configs[2] (VGG19 perceptual + LPIPS(alex) + ΔE00, bs8 512² as
+# BASELINE.json names it; weights from configs/colab/sid_newbp_rgb.yml:78-96; synthetic offline VGG / AlexNet weights)
+CFG4 = dict(CFG, width=64)
 WORKLOADS = {
     "cfg2": dict(batch=16, img=256, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1),
                  desc="cfg2: NAFNet w32 enc[2,2,4,8] mid12 dec[2,2,2,2] (29.16M), rgb/B2 PSF, bs16/GPU 256x256, "
                       "L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW"),
-    "cfg3": dict(batch=8, img=512, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1, w_perc=0.02, w_lpips=0.05, w_deltaE=0.02),
+    "cfg3": dict(batch=8, img=512, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1, w_perc=0.02, w_lpips=0.05, w_deltaE=0.02,
+                                          lpips_net="alex"),
                  desc="cfg3: cfg2 model, rgb/B2 PSF, bs8/GPU 512x512, L1 + 0.05*SSIM + 0.1*Phys_srgb + 0.02*VGG19 perc "
-                      "+ 0.05*LPIPS(vgg) + 0.02*DeltaE00, clip 0.01 + AdamW (synthetic VGG/LPIPS weights)"),
+                      "+ 0.05*LPIPS(alex) + 0.02*DeltaE00, clip 0.01 + AdamW (synthetic VGG/LPIPS weights)"),
+    # BASELINE.json configs[3], the >= 6.5x scaling config: w64 (115.98M), bs 16 per GPU (128 global on 8), the
+    # stressed R > G > B PSF family (S2; the reference only describes it, newbp_layer.py here defines it)
+    "cfg4": dict(batch=16, img=256, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1), model=CFG4, psf="S2",
+                 desc="cfg4: NAFNet w64 enc[2,2,4,8] mid12 dec[2,2,2,2] (115.98M), rgb/S2 stressed PSF (R>G>B), "
+                      "bs16/GPU 256x256, L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW"),
 }
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
 MFMA16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA peak
@@ -221,12 +229,14 @@ def psnr_vs_cpu(net, dev, img, active=False):
 def make_trainer(dev, workload, precision, seed=0):
     from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
     from lowlight_image_enhancement_amd.train import NBPTrainer
+    wl = WORKLOADS[workload]
+    spec = wl.get("psf", "B2")
     torch.manual_seed(seed)
-    net = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **CFG)
+    net = create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec=spec, **wl.get("model", CFG))
     init_sd = {k: v.clone() for k, v in net.state_dict().items()}
     net = net.to(dev)
     net.precision = precision
-    return NBPTrainer(net, psf_mode="rgb", psf_spec="B2", **WORKLOADS[workload]["w"]), init_sd
+    return NBPTrainer(net, psf_mode="rgb", psf_spec=spec, **wl["w"]), init_sd
 
 
 def batch(dev, B, img, rank):
@@ -455,6 +465,11 @@ def main():
                 print("[bench] cfg3 sample", file=sys.stderr, flush=True)
                 res["cfg3"] = dict(short_run(dev, "cfg3", args.precision, steps=3, warmup=2),
                                    workload=WORKLOADS["cfg3"]["desc"], global_batch=WORKLOADS["cfg3"]["batch"])
+                print("[bench] cfg4 N=1 line", file=sys.stderr, flush=True)
+                res["cfg4"] = dict(short_run(dev, "cfg4", args.precision, steps=5, warmup=3),
+                                   workload=WORKLOADS["cfg4"]["desc"], global_batch=WORKLOADS["cfg4"]["batch"],
+                                   note="the >= 6.5x scaling config at N = 1 (python bench.py --workload cfg4 "
+                                        "--gpus N times it at N GPUs)")
                 if not args.no_cpu_baseline:
                     print("[bench] cpu baseline", file=sys.stderr, flush=True)
                     res["cpu_baseline"] = cpu_baseline(init_sd)

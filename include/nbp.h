@@ -63,6 +63,17 @@ int nbp_phys_l1_fwd(const float* bhat, const float* a, const float* ratio, int r
 /* d loss / d bhat = up[0]/numel * PSF^T(sign) (* 1[0 <= bhat <= 1] when clamp_bhat). */
 int nbp_phys_l1_bwd(const float* sign_map, const float* bhat, const float* k, int k_shared, const float* up, int N,
                     int C, int H, int W, int KH, int KW, int pad_mode, int clamp_bhat, float* gx, nbp_stream_t s);
+/* PhysicsConsistencyLoss, groups == 1 branch (NewBP_model/losses.py:182-191: a [Co,1,kh,kw] kernel with Co not in
+ * {1, C} expanded to [Co,C,kh,kw], or a full [Co,C,kh,kw] kernel): yhat = conv2d(ReplicationPad(bhat), k) [N,Co,H,W]
+ * against al = clamp?(a * ratio) [N,Ca,H,W] (ratio [N*Ca] or full), L1 mean over torch's channel broadcast
+ * Cb = max(Co, Ca) (Co == Ca, or one of them 1).  k: [Co][C][KH][KW] (the expansion done by the caller).
+ * ws: nbp_phys_l1_workspace_doubles(N, Cb, H, W); sign_map [N][Cb][H][W] for the backward. */
+int nbp_phys_full_fwd(const float* bhat, const float* a, const float* ratio, int ratio_full, const float* k, int N,
+                      int C, int Co, int Ca, int H, int W, int KH, int KW, int clamp_align, double* ws, float* loss,
+                      float* sign_map, nbp_stream_t s);
+/* d loss / d bhat = up[0] / (N*Cb*H*W) * (replicate-pad adjoint of conv2d)^T(sign). */
+int nbp_phys_full_bwd(const float* sign_map, const float* k, const float* up, int N, int C, int Co, int Ca, int H, int W,
+                      int KH, int KW, float* gx, nbp_stream_t s);
 /* _phys_cons_core (metrics/phys_consistency.py:193-255) for phys_cons_raw (:260) / phys_cons_srgb (:323):
  * full [Co][Ci][KH][KW] PSF (already prepared), pad 0/1/2, ratio_mode 0 [N] / 1 [N,1,H,W] / 2 [N,Co,H,W],
  * crop 'valid' (crop_valid=1) or 'same', clamp01 of the synthesised observation (sRGB), L1 or Charbonnier
@@ -299,6 +310,11 @@ int nbp_rgb_to_lab(const float* rgb, int B, int H, int W, float* lab, nbp_stream
 size_t nbp_psnr_workspace_doubles(int N, long L);
 int nbp_psnr(const float* pred, const float* tgt, int N, long L, double data_range, double eps, int diff_double,
              double* ws, double* mse, double* psnr, nbp_stream_t s);
+/* calculate_ssim input alignment (metrics/ssim.py): BT.601 luma of NCHW RGB (color_space='y', :119-131) -> [N,1,H,W],
+ * and F.interpolate(bilinear / bicubic, align_corners=False) of `planes` Hi x Wi planes to Ho x Wo (resize_policy
+ * 'resize', :144-152; torch's CPU source-index and weight formulas). */
+int nbp_luma_bt601(const float* x, int N, int H, int W, float* y, nbp_stream_t s);
+int nbp_resize_planes(const float* x, long planes, int Hi, int Wi, int Ho, int Wo, int cubic, float* y, nbp_stream_t s);
 /* Windowed SSIM per-plane means out [N*C] float64: ssim_linear (metrics/linear.py:218-324: clamp_var = 1, crop = 0,
    eps) or the torchmetrics-1.2.0 form behind calculate_ssim (metrics/ssim.py:341-377: clamp_var = 0, eps = 0,
    crop = 1: the k/2 border of the map is excluded).  win: the k normalised 1-D window weights (device);
@@ -317,14 +333,27 @@ int nbp_sobel_mag(const float* lab, int B, int H, int W, float* out, nbp_stream_
    transposed weights).  Cin, Cout multiples of 8; y bf16 (y_dtype 1) or fp32 (y_dtype 0, mode 1). */
 int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
                      const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s);
-/* General zero-padded KH x KW / stride conv over NHWC 16-bit maps (LPIPS(net='alex') trunk, lpips 0.1.4 /
-   torchvision alexnet features: 11x11/4 pad 2, 5x5 pad 2, 3x3 pad 1) as an implicit GEMM on the 16-bit MFMA kernel:
-   y [B][Ho][Wo][Cout] = (relu?)(sum_{ki,kj,c} x[b][oi*stride + ki - pad][oj*stride + kj - pad][c] w[n][ki*KW+kj][c]
-   + bias[n]), Ho = (H + 2 pad - KH) / stride + 1.  Cin, Cout multiples of 8; dtype 1 bf16 / 2 fp16 (x, w, y). */
+/* General zero-padded KH x KW / stride conv over NHWC maps (LPIPS(net='alex') trunk, lpips 0.1.4 /
+   torchvision alexnet.features: 11x11/4 pad 2, 5x5 pad 2, 3x3 pad 1), implicit GEMM on the MFMA kernels:
+   y [B][Ho][Wo][Cout] = epi(sum_{ki,kj,c} x[b][oi*stride + ki - pad][oj*stride + kj - pad][c] w[n][ki*KW+kj][c]),
+   Ho = (H + 2 pad - KH) / stride + 1; epi as nbp_conv3x3_bf16: mode 0 bias + ReLU, 1 bias (or none), 2 ReLU-mask by
+   R (y = acc where R > 0: the stride-1 input gradient with tap-flipped [Cin][tap][Cout] weights).  Cin, Cout multiples
+   of 8; dtype 0 fp32 / 1 bf16 / 2 fp16 (x, w, R, y). */
 int nbp_conv2d_16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, int KH, int KW, int stride,
-                  int pad, const float* bias, int relu, void* y, int dtype, nbp_stream_t s);
-/* k x k max pool with stride, no padding (floor), NHWC 16-bit, forward (torchvision MaxPool2d(kernel_size=3, stride=2)). */
-int nbp_maxpool_k_fwd(const void* x, int B, int H, int W, int C, int k, int stride, void* y, int dtype, nbp_stream_t s);
+                  int pad, const float* bias, int mode, const void* R, void* y, int dtype, nbp_stream_t s);
+/* k x k / stride max pool without padding (torchvision AlexNet's MaxPool2d(3, 2)), NHWC; idx (optional) = the window
+   position (row-major, first maximum as torch's max_pool2d) of each output for the backward. */
+int nbp_maxpool_k_fwd(const void* x, int B, int H, int W, int C, int k, int stride, void* y, unsigned char* idx,
+                      int dtype, nbp_stream_t s);
+/* dx [B][H][W][C] = (sum of dy over the windows whose argmax is this input) * (post_in > 0): the pool input is a
+   post-ReLU map, its ReLU mask rides along (as nbp_maxpool2_bwd). */
+int nbp_maxpool_k_bwd(const void* dy, const unsigned char* idx, const void* post_in, int B, int H, int W, int C, int k,
+                      int stride, void* dx, int dtype, nbp_stream_t s);
+/* Input gradient of LPIPS alex's first conv (11x11, stride 4, pad 2, Cin padded 3 -> 8), a direct transposed conv:
+   d8 [B][H][W][8] fp32 (channels 0..2; 3..7 zero) = sum over the output taps that read (i, j) of
+   dpre[b][oi][oj][n] * w[n][ki*11+kj][c].  dpre [B][Ho][Wo][Cout] in `dtype`; w fp32 [Cout][121][8]. */
+int nbp_alex_conv0_input_grad(const void* dpre, const float* w, int B, int H, int W, int Ho, int Wo, int Cout,
+                              float* d8, int dtype, nbp_stream_t s);
 /* PerceptualLoss input (losses.py:56-66): NCHW fp32 sRGB -> NHWC bf16 [B][H][W][8] = (clamp01(x) - m) / s, c >= 3
    zero.  The input gradient maps d[B][H][W][8] fp32 back to NCHW (/ s, clamp mask). */
 int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float m1, float m2, float s0, float s1,

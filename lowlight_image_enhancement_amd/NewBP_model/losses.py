@@ -6,7 +6,8 @@ forward and backward runs as HIP kernels (include/nbp.h): L1 / Charbonnier (nbp_
 (nbp_align_exposure), ΔE00 (nbp_de00_loss_*).  Scalars stay on the device; the upstream gradient is read from device
 memory.
 
-The VGG19 perceptual term runs as implicit-GEMM bf16 MFMA convs (vgg.py); LPIPS is lpips.py.
+The VGG19 perceptual term runs as implicit-GEMM MFMA convs (vgg.py: fp32 like the reference's trunk, or 16-bit
+operands under autocast / the trainer's 16-bit modes); LPIPS is lpips.py.
 """
 from __future__ import annotations
 
@@ -161,13 +162,13 @@ class _PerceptualFn(torch.autograd.Function):
     """mean/sum of (VGG(prep(gen)) - VGG(prep(tgt)))^2 (or |.|); d/d gen through the frozen stack (vgg.py)."""
 
     @staticmethod
-    def forward(ctx, gen, tgt, module):
+    def forward(ctx, gen, tgt, module, dt):
         _lib.require_cuda(gen, tgt)
         if gen.shape != tgt.shape:
             raise ValueError(f"PerceptualLoss: shape mismatch {tuple(gen.shape)} vs {tuple(tgt.shape)}")
         if ctx.needs_input_grad[1]:
             raise NotImplementedError("PerceptualLoss gradient w.r.t. the target is not implemented on MI355X")
-        stack = module.stack(gen.device)
+        stack = module.stack(gen.device, dt)
         want = ctx.needs_input_grad[0]
         with torch.no_grad():
             ft, _, _ = stack.forward(_vgg.prep_input(tgt.detach(), dtype=stack.dtype), save=False)
@@ -192,19 +193,20 @@ class _PerceptualFn(torch.autograd.Function):
              up.float().contiguous().view(1), d, ctx.stack.dtype)
         d8 = ctx.stack.backward(ctx.tape, d)
         ctx.tape = ctx.fg = ctx.ft = None
-        return _vgg.input_grad(d8, gen), None, None
+        return _vgg.input_grad(d8, gen), None, None, None
 
 
 class PerceptualLoss(nn.Module):
     """losses.py:32-69 — clamp01 -> ImageNet mean/std -> vgg19.features[:36] (through relu5_4) for both images ->
-    MSE (use_mse) or L1, reduction 'mean' / 'sum'.  The conv stack is implicit-GEMM bf16 MFMA (vgg.py).
+    MSE (use_mse) or L1, reduction 'mean' / 'sum'.  The conv stack is implicit-GEMM MFMA (vgg.py).
     `weights`: None (deterministic synthetic VGG19 — the ImageNet download is unavailable offline), a state_dict of
     vgg19 (`features.N.*` or `N.*` keys) or a checkpoint path (loaded with weights_only=True).  `precision`: the trunk's
-    16-bit type, "bf16" (default: no loss scaling needed) or "fp16" (the reference's autocast dtype; pair it with loss
-    scaling, as NBPTrainer does in its fp16 mode)."""
+    storage / operand type: "auto" (default: fp32 like the reference's `.float()` trunk, fp16 / bf16 inside an enabled
+    CUDA autocast region), or "fp32", "bf16", "fp16" explicitly (fp16 wants loss scaling, as NBPTrainer's fp16 mode
+    applies)."""
 
     def __init__(self, device: Union[str, torch.device] = "cuda", use_mse: bool = True, reduction: str = "mean",
-                 weights=None, precision: str = "bf16"):
+                 weights=None, precision: str = "auto"):
         super().__init__()
         if reduction not in ("mean", "sum"):
             raise NotImplementedError("PerceptualLoss on MI355X supports reduction 'mean' and 'sum'")
@@ -212,10 +214,13 @@ class PerceptualLoss(nn.Module):
         self.reduction = reduction
         self._weights = weights
         self._stacks = {}
+        _vgg.resolve_precision(precision)  # validates
         self.precision = precision
 
-    def stack(self, device) -> "_vgg.VGGStack":
-        dt = {"bf16": 1, "fp16": 2}[self.precision]
+    def stack(self, device, dt: Optional[int] = None) -> "_vgg.VGGStack":
+        """The trunk for `device` at C-ABI dtype `dt` (None: this module's precision)."""
+        if dt is None:
+            dt = _vgg.resolve_precision(self.precision)
         key = (str(device), dt)
         if key not in self._stacks:
             self._stacks[key] = _vgg.VGGStack(_vgg.VGG19_CFG, 36, device, self._weights, dtype=dt)
@@ -224,12 +229,12 @@ class PerceptualLoss(nn.Module):
     def forward(self, generated_img, target_img):
         if target_img.device != generated_img.device:
             target_img = target_img.to(generated_img.device)
-        return _PerceptualFn.apply(generated_img, target_img, self)
+        return _PerceptualFn.apply(generated_img, target_img, self, _vgg.resolve_precision(self.precision))
 
-    def value_and_grad(self, gen, tgt, up: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    def value_and_grad(self, gen, tgt, up: torch.Tensor, out: torch.Tensor, dt: Optional[int] = None) -> torch.Tensor:
         """Autograd-free form for the fused trainer (no host sync, HIP-graph capturable): writes the loss into
-        out[0] and returns up[0] * d loss / d gen (NCHW fp32)."""
-        stack = self.stack(gen.device)
+        out[0] and returns up[0] * d loss / d gen (NCHW fp32).  `dt`: trunk dtype override (None: `precision`)."""
+        stack = self.stack(gen.device, dt)
         ft, _, _ = stack.forward(_vgg.prep_input(tgt, dtype=stack.dtype), save=False)
         fg, tape, _ = stack.forward(_vgg.prep_input(gen, dtype=stack.dtype), save=True)
         n = fg.numel()
@@ -322,9 +327,44 @@ class SSIMLoss(nn.Module):
         return _SSIMLossFn.apply(gen_srgb01, tgt_srgb01, self.window_size, self.max_val, 1)
 
 
+class _PhysFullFn(torch.autograd.Function):
+    """groups == 1 physics L1: conv2d(ReplicationPad(bhat), k [Co,C,kh,kw]) vs clamp?(a * ratio) under F.l1_loss's
+    channel broadcast (nbp_phys_full_*)."""
+
+    @staticmethod
+    def forward(ctx, bhat, a, ratio_arr, ratio_full, k, clamp_align):
+        _lib.require_cuda(bhat, a, k)
+        if ctx.needs_input_grad[1]:
+            raise NotImplementedError("physics loss gradient w.r.t. the short exposure is not implemented")
+        bhat, a, kk = bhat.contiguous(), a.contiguous(), k.detach().contiguous()
+        N, C, H, W = bhat.shape
+        Co, Ca = kk.shape[0], a.shape[1]
+        Cb = max(Co, Ca)
+        ws = torch.empty(query("phys_l1_workspace_doubles", N, Cb, H, W), dtype=torch.float64, device=bhat.device)
+        loss = torch.empty((), device=bhat.device)
+        sign = torch.empty(N, Cb, H, W, device=bhat.device) if ctx.needs_input_grad[0] else None
+        call("phys_full_fwd", bhat, a, ratio_arr, ratio_full, kk, N, C, Co, Ca, H, W, kk.shape[-2], kk.shape[-1],
+             clamp_align, ws, loss, sign)
+        ctx.save_for_backward(sign, kk)
+        ctx.dims = (N, C, Co, Ca, H, W)
+        return loss
+
+    @staticmethod
+    def backward(ctx, up):
+        sign, kk = ctx.saved_tensors
+        N, C, Co, Ca, H, W = ctx.dims
+        g = torch.empty(N, C, H, W, device=sign.device)
+        call("phys_full_bwd", sign, kk, up.contiguous(), N, C, Co, Ca, H, W, kk.shape[-2], kk.shape[-1], g)
+        return g, None, None, None, None, None
+
+
 class PhysicsConsistencyLoss(nn.Module):
-    """losses.py:158-192: |K * ReplicationPad(Bhat_raw) - clamp(A_raw * ratio)|_1 with the UN-normalised K
-    (depthwise: K is [C,1,kh,kw] or the shared [1,1,kh,kw])."""
+    """losses.py:158-192: |K * ReplicationPad(Bhat_raw) - clamp(A_raw * ratio)|_1 with the UN-normalised K.
+    The reference's kernel forms, with its groups logic (:182-190): a shared [1,1,kh,kw] kernel is broadcast to every
+    channel and a [C,1,kh,kw] one is applied per channel (depthwise, nbp_phys_l1_*); any other [Co,1,kh,kw] kernel is
+    expanded to [Co,C,kh,kw] and a full [Co,C,kh,kw] kernel used as is (groups = 1, nbp_phys_full_*), the L1 taken over
+    F.l1_loss's broadcast of [N,Co,H,W] against A's channels.  Kernel / channel combinations the reference's conv2d
+    rejects raise RuntimeError as there."""
 
     def __init__(self, K_kernel: torch.Tensor, device: str = "cuda", clamp_align: bool = True):
         super().__init__()
@@ -339,12 +379,36 @@ class PhysicsConsistencyLoss(nn.Module):
             expo_ratio = expo_ratio.view(-1, 1, 1, 1)
         C = Bhat_raw.shape[1]
         k = self.K
-        if k.shape[1] != 1 or k.shape[0] not in (1, C):
-            raise NotImplementedError("PhysicsConsistencyLoss on MI355X implements the depthwise kernel forms "
-                                      "[C,1,kh,kw] and [1,1,kh,kw]")
+        kh, kw = k.shape[-2:]
+        if k.shape[0] == 1 and C > 1:  # shared kernel broadcast to every channel (:184-185)
+            if k.shape[1] != 1:
+                raise RuntimeError(f"PhysicsConsistencyLoss: kernel {tuple(k.shape)} cannot be expanded to "
+                                   f"{(C, 1, kh, kw)}")
+            k = k.expand(C, 1, kh, kw)
+        groups = C if k.shape[0] == C else 1  # :187
+        if groups == 1 and k.shape[1] == 1 and C != 1:  # :189-190
+            k = k.expand(k.shape[0], C, kh, kw)
+        if k.shape[1] != C // groups:  # what F.conv2d rejects
+            raise RuntimeError(f"PhysicsConsistencyLoss: conv2d weight {tuple(k.shape)} with groups={groups} does not "
+                               f"match {C} input channels")
+        if groups == C:  # depthwise (per-channel, or the broadcast shared kernel)
+            r, full = _ratio_array(expo_ratio, A_raw)
+            shared = int(self.K.shape[0] == 1 and C > 1)
+            kd = self.K if shared else k
+            return _PhysL1Fn.apply(Bhat_raw, A_raw, r, full, kd.to(Bhat_raw.dtype), shared, 1, 0, 0,
+                                   int(self.clamp_align))
+        Co, Ca = k.shape[0], A_raw.shape[1]
+        if A_raw.shape[0] != Bhat_raw.shape[0] or A_raw.shape[2:] != Bhat_raw.shape[2:] or not (
+                Co == Ca or Co == 1 or Ca == 1):
+            raise RuntimeError(f"PhysicsConsistencyLoss: conv output {(Bhat_raw.shape[0], Co, *Bhat_raw.shape[2:])} "
+                               f"does not broadcast with A {tuple(A_raw.shape)}")
+        if Co != Ca:  # F.l1_loss warns on a broadcast target (torch.nn.functional.l1_loss)
+            warnings.warn(f"Using a target size ({torch.Size([A_raw.shape[0], Ca, *A_raw.shape[2:]])}) that is "
+                          f"different to the input size ({torch.Size([Bhat_raw.shape[0], Co, *Bhat_raw.shape[2:]])}). "
+                          "This will likely lead to incorrect results due to broadcasting. Please ensure they have "
+                          "the same size.", UserWarning)
         r, full = _ratio_array(expo_ratio, A_raw)
-        return _PhysL1Fn.apply(Bhat_raw, A_raw, r, full, k.to(Bhat_raw.dtype), int(k.shape[0] == 1 and C > 1), 1,
-                               0, 0, int(self.clamp_align))
+        return _PhysFullFn.apply(Bhat_raw, A_raw.float(), r, full, k.float().contiguous(), int(self.clamp_align))
 
 
 def align_exposure_srgb(a_srgb: torch.Tensor, ratio) -> torch.Tensor:

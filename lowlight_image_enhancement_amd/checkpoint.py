@@ -164,4 +164,7 @@ def resume_training(trainer, resume_state) -> Dict:
         trainer.scaler.copy_(torch.tensor([amp["scale"], amp["growth_factor"], amp["backoff_factor"],
                                            float(amp["growth_interval"])]))
         trainer.ctl[1] = int(amp["_growth_tracker"])
+        # the current upstream gradients carry the old scale: re-derive them from the restored one (other batch
+        # sizes' buffers are refreshed when the trainer switches to them)
+        trainer._refresh_up()
     return resume_state

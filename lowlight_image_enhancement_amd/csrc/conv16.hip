@@ -1,4 +1,5 @@
-// 16-bit implicit-GEMM convolutions (VGG / LPIPS trunks) on the DMA GEMM kernel of gemm16_impl.h.
+// Implicit-GEMM convolutions of the VGG / LPIPS trunks: 16-bit on the DMA GEMM kernel of gemm16_impl.h, fp32 (the
+// parity mode, dtype 0) on the fp32 MFMA GEMM of gemm.hip (nbp::conv_f32).
 #include "gemm16_impl.h"
 
 extern "C" {
@@ -7,6 +8,7 @@ extern "C" {
 //   y[b][i][j][n] = epi( sum_{t, c} x[b][i + t/3 - 1][j + t%3 - 1][c] * w[n][t][c] (+ bias[n]) )
 // epi: mode 0 bias + ReLU, 1 bias only, 2 ReLU-mask by R (y = acc where R > 0 else 0; no bias).  x, w, R and a
 // 16-bit y share the type `dtype` (1 bf16, 2 fp16); y is that type (y_dtype 1) or fp32 (y_dtype 0, mode 1 only).
+// dtype 0: x, w, R, y all fp32 (y_dtype 0).
 // Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
 // NBP_IM2COL_TAP=0: per-lane tap division in the 3x3 conv's DMA issue (A/B measurement; read per launch)
 static bool im2col_tap_tile() {
@@ -27,9 +29,12 @@ int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w,
   NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0, "nbp_conv3x3_bf16: bad args");
   NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv3x3_bf16: Cin and Cout must be multiples of 8 (%d, %d)", Cin,
               Cout);
-  NBP_REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || R) && (y_dtype == 1 || mode == 1),
+  NBP_REQUIRE(dtype >= 0 && dtype <= 2, "nbp_conv3x3_bf16: dtype 0 (fp32), 1 (bf16) or 2 (fp16)");
+  NBP_REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || R) && (dtype == 0 ? y_dtype == 0 : (y_dtype == 1 || mode == 1)),
               "nbp_conv3x3_bf16: mode / R / y_dtype");
-  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_conv3x3_bf16: dtype 1 (bf16) or 2 (fp16)");
+  if (dtype == 0)
+    return conv_f32(static_cast<const float*>(x), B, H, W, Cin, static_cast<const float*>(w), Cout, 3, 3, 1, 1, bias,
+                    mode, static_cast<const float*>(R), static_cast<float*>(y), S(s));
   const long M = (long)B * H * W;
   NBP_REQUIRE(M < (1L << 31), "nbp_conv3x3_bf16: too many pixels");
   GemmPB p{x, 0, nullptr, 1, w, 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
@@ -54,17 +59,21 @@ int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w,
 }
 
 int nbp_conv2d_16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, int KH, int KW, int stride,
-                  int pad, const float* bias, int relu, void* y, int dtype, nbp_stream_t s) {
+                  int pad, const float* bias, int mode, const void* R, void* y, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
               "nbp_conv2d_16: bad args");
   NBP_REQUIRE(Cin % 8 == 0 && Cout % 8 == 0, "nbp_conv2d_16: Cin and Cout must be multiples of 8 (%d, %d)", Cin, Cout);
-  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_conv2d_16: dtype 1 (bf16) or 2 (fp16)");
+  NBP_REQUIRE(dtype >= 0 && dtype <= 2, "nbp_conv2d_16: dtype 0 (fp32), 1 (bf16) or 2 (fp16)");
+  NBP_REQUIRE(mode >= 0 && mode <= 2 && (mode != 2 || R), "nbp_conv2d_16: mode / R");
+  if (dtype == 0)
+    return conv_f32(static_cast<const float*>(x), B, H, W, Cin, static_cast<const float*>(w), Cout, KH, KW, stride, pad,
+                    bias, mode, static_cast<const float*>(R), static_cast<float*>(y), S(s));
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   NBP_REQUIRE(Ho > 0 && Wo > 0, "nbp_conv2d_16: empty output");
   const long M = (long)B * Ho * Wo;
   NBP_REQUIRE(M < (1L << 31), "nbp_conv2d_16: too many pixels");
-  GemmPB p{x, 0, nullptr, 1, w, (long)KH * KW * Cin, y, Cout, (int)M, Cout, KH * KW * Cin, Ho, Wo, Cin, bias, nullptr,
-           nullptr, nullptr};
+  GemmPB p{x, 0, nullptr, 1, w, (long)KH * KW * Cin, y, Cout, (int)M, Cout, KH * KW * Cin, Ho, Wo, Cin,
+           mode == 2 ? nullptr : bias, mode == 2 ? R : nullptr, nullptr, nullptr};
   p.kh = KH;
   p.kw = KW;
   p.stride = stride;
@@ -74,11 +83,13 @@ int nbp_conv2d_16(const void* x, int B, int H, int W, int Cin, const void* w, in
   hipStream_t st = S(s);
   if (dtype == 2) {
     using T16 = _Float16;
-    if (relu) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
+    if (mode == 0) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
+    else if (mode == 2) dispatch<AM_CONV, CM_MASK, T16, T16, T16>(p, st);
     else dispatch<AM_CONV, CM_PLAIN, T16, T16, T16>(p, st);
   } else {
     using T16 = __bf16;
-    if (relu) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
+    if (mode == 0) dispatch<AM_CONV, CM_RELU, T16, T16, T16>(p, st);
+    else if (mode == 2) dispatch<AM_CONV, CM_MASK, T16, T16, T16>(p, st);
     else dispatch<AM_CONV, CM_PLAIN, T16, T16, T16>(p, st);
   }
   return check_launch("conv2d_16");

@@ -14,8 +14,8 @@ using namespace nbp;
 
 namespace {
 
-enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2 };
-enum { CM_PLAIN = 0, CM_D2S = 1 };
+enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_CONV = 3 };
+enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3 };
 
 struct GemmP {
   const float* A;
@@ -32,6 +32,9 @@ struct GemmP {
   const float* R;
   const float* rscale;
   float* pre;
+  // AM_CONV (implicit-GEMM KH x KW / stride conv over an NHWC map, zero padded): input ih x iw x cin, output grid
+  // gh x gw (rows m = (b, oi, oj)), K index = (ki * kw + kj) * cin + c
+  int ih, iw, cin, kh, kw, stride, pad;
 };
 
 // offset of element (m, kq*4 .. +3) of a space-to-depth view of a 2x-resolution NHWC map
@@ -65,6 +68,19 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   float4 ra[A_IT], rb[B_IT];
+  // AM_CONV: each thread's A rows are fixed over the K loop: image origin and top-left input tap of its rows
+  long cbase[AM_CONV == AMODE ? A_IT : 1];
+  int ci0[AM_CONV == AMODE ? A_IT : 1], cj0[AM_CONV == AMODE ? A_IT : 1];
+  if (AMODE == AM_CONV) {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int m = m0 + ((tid + it * 256) >> 3);
+      const int per = p.gh * p.gw, b = m / per, rem = m - b * per, oi = rem / p.gw, oj = rem - oi * p.gw;
+      cbase[it] = (long)b * p.ih * p.iw * p.cin;
+      ci0[it] = oi * p.stride - p.pad;
+      cj0[it] = oj * p.stride - p.pad;
+    }
+  }
 
   auto load_tiles = [&](int k0) {
 #pragma unroll
@@ -74,7 +90,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
       const int m = m0 + r, k = k0 + kq * 4;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (m < M && k < K) {
-        if (AMODE == AM_S2D) v = ld4(p.A + s2d_off(m, k, p.gh, p.gw, p.cs));
+        if (AMODE == AM_CONV) {
+          const int tap = k / p.cin, c = k - tap * p.cin, ki = tap / p.kw, kj = tap - ki * p.kw;
+          const int ii = ci0[it] + ki, jj = cj0[it] + kj;
+          if (ii >= 0 && ii < p.ih && jj >= 0 && jj < p.iw)
+            v = ld4(p.A + cbase[it] + ((long)ii * p.iw + jj) * p.cin + c);
+        } else if (AMODE == AM_S2D) v = ld4(p.A + s2d_off(m, k, p.gh, p.gw, p.cs));
         else v = ld4(p.A + (long)m * p.lda + k);
         if (AMODE == AM_SCALE) v = v * ld4(p.a_scale + (long)(m / p.rows_per_img) * K + k);
       }
@@ -164,6 +185,14 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
         if (CMODE == CM_D2S) off = s2d_off(row, col, p.gh, p.gw, p.cs);
         else off = (long)row * p.ldc + col;
         float v = acc[i][j][r] + bcol;
+        if (CMODE == CM_RELU) {
+          p.C[off] = fmaxf(v, 0.f);
+          continue;
+        }
+        if (CMODE == CM_MASK) {  // y = acc where R > 0 (the previous post-ReLU map), no bias
+          p.C[off] = p.R[off] > 0.f ? acc[i][j][r] : 0.f;
+          continue;
+        }
         if (p.pre) p.pre[off] = v;
         if (p.R) v = p.R[off] + scol * v;
         p.C[off] = v;
@@ -1216,7 +1245,8 @@ int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int
   NBP_REQUIRE(a_mode != AM_S2D || K == 4 * cs, "nbp_gemm_f32: S2D needs K == 4*cs");
   NBP_REQUIRE(c_mode != CM_D2S || N == 4 * cs, "nbp_gemm_f32: D2S needs N == 4*cs");
   NBP_REQUIRE(a_mode == AM_S2D || lda % 4 == 0, "nbp_gemm_f32: lda alignment");
-  GemmP p{A, lda, a_scale, rows_per_img, B, ldb, C, ldc, M, N, K, gh, gw, cs, bias, R, rscale, pre};
+  GemmP p{A, lda, a_scale, rows_per_img, B, ldb, C, ldc, M, N, K, gh, gw, cs, bias, R, rscale, pre,
+          0, 0, 0, 0, 0, 0, 0};
   hipStream_t st = S(s);
   if (b_nk) {
     if (a_mode == AM_PLAIN && c_mode == CM_PLAIN) dispatch_tiles<true, AM_PLAIN, CM_PLAIN>(p, st);
@@ -1233,6 +1263,31 @@ int nbp_gemm_f32(const float* A, long lda, int a_mode, const float* a_scale, int
   }
   return check_launch("gemm_f32");
 }
+
+}  // extern "C"
+
+namespace nbp {
+// fp32 implicit-GEMM convolution (the parity mode of the VGG / LPIPS trunks: the reference's PerceptualLoss runs its
+// conv stack in fp32, NewBP_model/losses.py:63-69): y[b][oi][oj][n] = epi(sum_{ki,kj,c} x[b][oi*s+ki-p][oj*s+kj-p][c]
+// * w[n][ki*KW+kj][c] (+ bias[n])) on v_mfma_f32_32x32x2_f32 (exact products, fp32 accumulation).
+// mode 0 bias + ReLU, 1 bias (or none), 2 ReLU-mask by R (no bias).  Cin, Cout multiples of 4.
+int conv_f32(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH, int KW, int stride, int pad,
+             const float* bias, int mode, const float* R, float* y, hipStream_t st) {
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  NBP_REQUIRE(Ho > 0 && Wo > 0 && Cin % 4 == 0 && Cout % 4 == 0, "conv_f32: shape");
+  const long M = (long)B * Ho * Wo;
+  NBP_REQUIRE(M < (1L << 31), "conv_f32: too many pixels");
+  const int K = KH * KW * Cin;
+  GemmP p{x, 0, nullptr, 1, w, (long)K, y, Cout, (int)M, Cout, K, Ho, Wo, 0, mode == 2 ? nullptr : bias,
+          mode == 2 ? R : nullptr, nullptr, nullptr, H, W, Cin, KH, KW, stride, pad};
+  if (mode == 0) dispatch_tiles<true, AM_CONV, CM_RELU>(p, st);
+  else if (mode == 2) dispatch_tiles<true, AM_CONV, CM_MASK>(p, st);
+  else dispatch_tiles<true, AM_CONV, CM_PLAIN>(p, st);
+  return check_launch("conv_f32");
+}
+}  // namespace nbp
+
+extern "C" {
 
 size_t nbp_wgrad_workspace_floats(int M, int N, int K) {
   const int S_ = wgrad_splits(M, N, K);

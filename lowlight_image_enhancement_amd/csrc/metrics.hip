@@ -160,6 +160,68 @@ __global__ __launch_bounds__(256) void sobel_mag_kernel(const float* __restrict_
 
 }  // namespace
 
+// ---------------------------------------------------------------- calculate_ssim input alignment (metrics/ssim.py)
+// BT.601 luma (ssim.py:119-131): y = 0.2989 r + 0.5870 g + 0.1140 b, evaluated as torch does it (each product and
+// each sum rounded to fp32 on its own: no contraction), NCHW [N,3,H,W] -> [N,1,H,W]
+__global__ __launch_bounds__(256) void luma_bt601_kernel(const float* __restrict__ x, long HW, long npix,
+                                                         float* __restrict__ y) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+    const long b = p / HW, q = p - b * HW;
+    const float* xb = x + b * 3 * HW + q;
+    const float t = __fadd_rn(__fmul_rn(0.2989f, xb[0]), __fmul_rn(0.5870f, xb[HW]));
+    y[p] = __fadd_rn(t, __fmul_rn(0.1140f, xb[2 * HW]));
+  }
+}
+
+// F.interpolate(mode='bilinear' | 'bicubic', align_corners=False) of NCHW planes (ssim.py:144-152, resize_policy
+// 'resize'), torch's CPU formulas (aten UpSample.h): scale = in / out, src = scale * (dst + 0.5) - 0.5; bilinear clamps
+// src at 0, taps i0 = min(floor(src), in - 1), i1 = i0 + (i0 < in - 1), weights 1 - l, l; bicubic: taps floor(src) - 1
+// .. + 2 clamped to the border, Keys' kernel A = -0.75.
+__device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
+  const float A = -0.75f;
+  auto cc1 = [&](float x) { return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f; };        // |x| <= 1
+  auto cc2 = [&](float x) { return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A; };  // 1 < |x| < 2
+  c[0] = cc2(t + 1.f);
+  c[1] = cc1(t);
+  c[2] = cc1(1.f - t);
+  c[3] = cc2((1.f - t) + 1.f);
+}
+
+template <bool CUBIC>
+__global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x, int Hi, int Wi, int Ho, int Wo,
+                                                     long total, float sh, float sw, float* __restrict__ y) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int ow = (int)(e % Wo);
+    const long t = e / Wo;
+    const int oh = (int)(t % Ho);
+    const long plane = t / Ho;
+    const float* xp = x + plane * Hi * Wi;
+    const float rh = sh * (oh + 0.5f) - 0.5f, rw = sw * (ow + 0.5f) - 0.5f;
+    if (!CUBIC) {
+      const float fh = fmaxf(rh, 0.f), fw = fmaxf(rw, 0.f);
+      const int h0 = min((int)floorf(fh), Hi - 1), w0 = min((int)floorf(fw), Wi - 1);
+      const int h1 = h0 + (h0 < Hi - 1 ? 1 : 0), w1 = w0 + (w0 < Wi - 1 ? 1 : 0);
+      const float lh = fminf(fmaxf(fh - h0, 0.f), 1.f), lw = fminf(fmaxf(fw - w0, 0.f), 1.f);
+      const float top = (1.f - lw) * xp[(long)h0 * Wi + w0] + lw * xp[(long)h0 * Wi + w1];
+      const float bot = (1.f - lw) * xp[(long)h1 * Wi + w0] + lw * xp[(long)h1 * Wi + w1];
+      y[e] = (1.f - lh) * top + lh * bot;
+    } else {
+      const int h0 = (int)floorf(rh), w0 = (int)floorf(rw);
+      float ch[4], cw[4];
+      cubic_coeffs(rh - h0, ch);
+      cubic_coeffs(rw - w0, cw);
+      float acc = 0.f;
+      for (int i = 0; i < 4; ++i) {
+        const int hh = min(max(h0 - 1 + i, 0), Hi - 1);
+        float row = 0.f;
+        for (int j = 0; j < 4; ++j) row += cw[j] * xp[(long)hh * Wi + min(max(w0 - 1 + j, 0), Wi - 1)];
+        acc += ch[i] * row;
+      }
+      y[e] = acc;
+    }
+  }
+}
+
 extern "C" {
 
 int nbp_sobel_mag(const float* lab, int B, int H, int W, float* out, nbp_stream_t s) {
@@ -206,6 +268,25 @@ int nbp_ssim_linear(const float* pred, const float* tgt, int N, int C, int H, in
   const long r = k / 2, cnt = crop ? (long)(H - 2 * r) * (W - 2 * r) : HW;
   plane_mean_finalize<<<cdiv(P, 256), 256, 0, S(s)>>>(slab, P, chunks, 1.0 / (double)cnt, out);
   return check_launch("ssim_linear");
+}
+
+int nbp_luma_bt601(const float* x, int N, int H, int W, float* y, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && N > 0 && H > 0 && W > 0, "nbp_luma_bt601: bad args");
+  const long HW = (long)H * W, n = (long)N * HW;
+  long g = (n + 255) / 256;
+  luma_bt601_kernel<<<(int)(g > 8192 ? 8192 : g), 256, 0, S(s)>>>(x, HW, n, y);
+  return check_launch("luma_bt601");
+}
+
+int nbp_resize_planes(const float* x, long planes, int Hi, int Wi, int Ho, int Wo, int cubic, float* y, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && planes > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0, "nbp_resize_planes: bad args");
+  const long total = planes * Ho * Wo;
+  long g = (total + 255) / 256;
+  const int grid = (int)(g > 8192 ? 8192 : g);
+  const float sh = (float)Hi / (float)Ho, sw = (float)Wi / (float)Wo;
+  if (cubic) resize_kernel<true><<<grid, 256, 0, S(s)>>>(x, Hi, Wi, Ho, Wo, total, sh, sw, y);
+  else resize_kernel<false><<<grid, 256, 0, S(s)>>>(x, Hi, Wi, Ho, Wo, total, sh, sw, y);
+  return check_launch("resize_planes");
 }
 
 }  // extern "C"

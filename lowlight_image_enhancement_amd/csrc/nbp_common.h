@@ -21,6 +21,9 @@ namespace nbp {
 // ---------------------------------------------------------------- error plumbing (host)
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// fp32 implicit-GEMM KH x KW / stride conv over NHWC maps (gemm.hip): mode 0 bias + ReLU, 1 bias, 2 ReLU-mask by R
+int conv_f32(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH, int KW, int stride, int pad,
+             const float* bias, int mode, const float* R, float* y, hipStream_t st);
 
 #define NBP_REQUIRE(cond, ...)            \
   do {                                    \
@@ -117,6 +120,16 @@ __device__ __forceinline__ void sts1(T* p, float v) { *p = (T)v; }
     }                                                \
   } while (0)
 #define NBP_DISPATCH_H(dtype, ...) NBP_DISPATCH_16(dtype, H, __VA_ARGS__)
+// every storage type (0 fp32, 1 bf16, 2 fp16) as the type alias TN
+#define NBP_DISPATCH_ALL(dtype, TN, ...)             \
+  do {                                               \
+    if ((dtype) == 0) {                              \
+      using TN = float;                              \
+      __VA_ARGS__;                                   \
+    } else {                                         \
+      NBP_DISPATCH_16(dtype, TN, __VA_ARGS__);       \
+    }                                                \
+  } while (0)
 
 // sum over the 64 lanes of a wave
 __device__ __forceinline__ float wave_sum(float v) {

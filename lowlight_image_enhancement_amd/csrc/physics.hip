@@ -180,6 +180,78 @@ __global__ void phys_l1_bwd(const float* __restrict__ sign_map, const float* __r
   }
 }
 
+// ---------------------------------------------------------------- raw physics L1, groups = 1 (full / expanded PSF)
+// PhysicsConsistencyLoss's groups == 1 branch (NewBP_model/losses.py:182-191): a [Co][C][KH][KW] kernel (the caller
+// expands a [Co][1] one along C) over the replicate-padded prediction,
+//   yhat[n][co][h][w] = sum_{c,a,b} k[co][c][a][b] * bhat[n][c][clamp(h + a - KH/2)][clamp(w + b - KW/2)],
+// compared with al = clamp?(a * ratio) under torch's channel broadcast of F.l1_loss: Cb = max(Co, Ca) output
+// channels, yhat's channel min(cb, Co - 1) (Co == 1 broadcasts), al's min(cb, Ca - 1).  Partial sums of |d| per
+// block, sign(d) map [N][Cb][H][W].
+__global__ void phys_full_fwd(const float* __restrict__ bhat, const float* __restrict__ a, const float* __restrict__ ratio,
+                              int ratio_full, const float* __restrict__ k, int N, int C, int Co, int Ca, int H, int W,
+                              int KH, int KW, int clamp_align, double* __restrict__ partial,
+                              float* __restrict__ sign_map) {
+  __shared__ double red[16];
+  const int Cb = Co > Ca ? Co : Ca;
+  const int total = N * Cb * H * W;  // < 2^31 (host check)
+  double s = 0.0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W, h = hw % H;
+    const int plane = hw / H;
+    const int cb = plane % Cb, n = plane / Cb;
+    const int co = Co == 1 ? 0 : cb, ca = Ca == 1 ? 0 : cb;
+    float y = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float* xp = bhat + ((long)n * C + c) * H * W;
+      const float* kc = k + ((long)co * C + c) * KH * KW;
+      for (int aa = 0; aa < KH; ++aa) {
+        const int hh = clampi(h + aa - KH / 2, 0, H - 1);
+        for (int bb = 0; bb < KW; ++bb)
+          y = fmaf(kc[aa * KW + bb], xp[(long)hh * W + clampi(w + bb - KW / 2, 0, W - 1)], y);
+      }
+    }
+    const long ai = (((long)n * Ca + ca) * H + h) * W + w;
+    const float r = ratio_full ? ratio[ai] : ratio[n * Ca + ca];
+    float al = a[ai] * r;
+    if (clamp_align) al = clamp01(al);
+    const float d = y - al;
+    s += fabsf(d);
+    if (sign_map) sign_map[i] = fsign(d);
+  }
+  s = block_sum_d(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// gx[n][c][p] = up[0] * scale * sum_cb sum_{a,b} k[co(cb)][c][a][b] * sum_{q: clamp(q + off) == p} sign[n][cb][q]
+__global__ void phys_full_bwd(const float* __restrict__ sign_map, const float* __restrict__ k, const float* __restrict__ up,
+                              float scale, int N, int C, int Co, int Cb, int H, int W, int KH, int KW,
+                              float* __restrict__ gx) {
+  const int total = N * C * H * W;
+  const float g0 = up[0] * scale;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int w = i % W, hw = i / W, h = hw % H;
+    const int plane = hw / H;
+    const int c = plane % C, n = plane / C;
+    float acc = 0.f;
+    for (int cb = 0; cb < Cb; ++cb) {
+      const float* sp = sign_map + ((long)n * Cb + cb) * H * W;
+      const float* kc = k + ((long)(Co == 1 ? 0 : cb) * C + c) * KH * KW;
+      for (int aa = 0; aa < KH; ++aa) {
+        int qh0, qh1;
+        rep_range(h, aa - KH / 2, H, qh0, qh1);
+        for (int bb = 0; bb < KW; ++bb) {
+          int qw0, qw1;
+          rep_range(w, bb - KW / 2, W, qw0, qw1);
+          const float kv = kc[aa * KW + bb];
+          for (int qh = qh0; qh <= qh1; ++qh)
+            for (int qw = qw0; qw <= qw1; ++qw) acc = fmaf(kv, sp[(long)qh * W + qw], acc);
+        }
+      }
+    }
+    gx[i] = g0 * acc;
+  }
+}
+
 // fixed-order sum of block partials -> out[0] = scale * sum
 __global__ void finalize_sum(const double* __restrict__ partial, int n, double scale, float* __restrict__ out) {
   __shared__ double red[16];
@@ -361,6 +433,35 @@ int nbp_phys_l1_bwd(const float* sign_map, const float* bhat, const float* k, in
     phys_l1_bwd<1><<<grid_for(total), kBlk, 0, S(s)>>>(sign_map, bhat, k, k_shared, up, scale, N, C, H, W, KH, KW,
                                                         clamp_bhat, gx);
   return check_launch("phys_l1_bwd");
+}
+
+int nbp_phys_full_fwd(const float* bhat, const float* a, const float* ratio, int ratio_full, const float* k, int N,
+                      int C, int Co, int Ca, int H, int W, int KH, int KW, int clamp_align, double* ws, float* loss,
+                      float* sign_map, nbp_stream_t s) {
+  NBP_REQUIRE(bhat && a && ratio && k && ws && loss && N > 0 && C > 0 && Co > 0 && Ca > 0 && H > 0 && W > 0,
+              "nbp_phys_full_fwd: bad args");
+  NBP_REQUIRE((KH & 1) && (KW & 1), "nbp_phys_full_fwd: odd kernel sizes");
+  NBP_REQUIRE(Co == Ca || Co == 1 || Ca == 1, "nbp_phys_full_fwd: channels %d and %d do not broadcast", Co, Ca);
+  const int Cb = Co > Ca ? Co : Ca;
+  NBP_REQUIRE((long)N * (Cb > C ? Cb : C) * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
+  const long total = (long)N * Cb * H * W;
+  const int g = grid_for(total);
+  phys_full_fwd<<<g, kBlk, 0, S(s)>>>(bhat, a, ratio, ratio_full, k, N, C, Co, Ca, H, W, KH, KW, clamp_align, ws,
+                                       sign_map);
+  finalize_sum<<<1, 256, 0, S(s)>>>(ws, g, 1.0 / (double)total, loss);
+  return check_launch("phys_full_fwd");
+}
+
+int nbp_phys_full_bwd(const float* sign_map, const float* k, const float* up, int N, int C, int Co, int Ca, int H, int W,
+                      int KH, int KW, float* gx, nbp_stream_t s) {
+  NBP_REQUIRE(sign_map && k && up && gx && N > 0 && C > 0 && H > 0 && W > 0, "nbp_phys_full_bwd: bad args");
+  NBP_REQUIRE(Co == Ca || Co == 1 || Ca == 1, "nbp_phys_full_bwd: channels %d and %d do not broadcast", Co, Ca);
+  const int Cb = Co > Ca ? Co : Ca;
+  NBP_REQUIRE((long)N * (Cb > C ? Cb : C) * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
+  const long total = (long)N * C * H * W;
+  const float scale = (float)(1.0 / ((double)N * Cb * H * W));
+  phys_full_bwd<<<grid_for(total), kBlk, 0, S(s)>>>(sign_map, k, up, scale, N, C, Co, Cb, H, W, KH, KW, gx);
+  return check_launch("phys_full_bwd");
 }
 
 size_t nbp_phys_cons_workspace_doubles(int N, int H, int W) {

@@ -1,4 +1,5 @@
-// VGG feature-loss glue around the implicit-GEMM 3x3 convs (nbp_conv3x3_bf16), NHWC bf16 activations:
+// VGG feature-loss glue around the implicit-GEMM 3x3 convs (nbp_conv3x3_bf16), NHWC activations stored as
+// `dtype` (0 fp32: the parity mode, the reference's fp32 trunk; 1 bf16; 2 fp16):
 //   PerceptualLoss (NewBP_model/losses.py:32-69): (clamp01(x) - mean) / std -> vgg19.features[:36] -> MSE / L1;
 //   the LPIPS backbone taps reuse the same pieces.
 // Kernels: the input prologue (NCHW fp32 -> NHWC bf16 with the channel dim padded to 8), 2x2 max-pool with argmax
@@ -307,10 +308,12 @@ __global__ __launch_bounds__(256) void lpips_tap_bwd(const HT* __restrict__ a, c
   }
 }
 
-// k x k max pool, stride s, no padding (floor), NHWC 16-bit, forward only (torchvision AlexNet's MaxPool2d(3, 2))
+// k x k max pool, stride s, no padding (floor), NHWC (torchvision AlexNet's MaxPool2d(3, 2)); idx (optional): the
+// window position of the first maximum in row-major window order (NaN wins, as torch's max_pool2d)
 template <typename HT>
 __global__ __launch_bounds__(256) void maxpool_k_fwd_kernel(const HT* __restrict__ x, int H, int W, int C, int k, int st,
-                                                            int Ho, int Wo, long total8, HT* __restrict__ y) {
+                                                            int Ho, int Wo, long total8, HT* __restrict__ y,
+                                                            unsigned char* __restrict__ idx) {
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
     const int C8 = C / 8;
     const int c8 = (int)(e % C8);
@@ -318,19 +321,108 @@ __global__ __launch_bounds__(256) void maxpool_k_fwd_kernel(const HT* __restrict
     const int j = (int)(o % Wo), i = (int)((o / Wo) % Ho);
     const long b = o / ((long)Wo * Ho);
     float best[8];
+    int bi[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) best[q] = -INFINITY;
+    for (int q = 0; q < 8; ++q) {
+      best[q] = -INFINITY;
+      bi[q] = 0;
+    }
     for (int di = 0; di < k; ++di)
       for (int dj = 0; dj < k; ++dj) {
         const vec_t<HT, 8> v =
             *reinterpret_cast<const vec_t<HT, 8>*>(x + ((b * H + i * st + di) * W + j * st + dj) * C + c8 * 8);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) best[q] = fmaxf(best[q], (float)v[q]);
+        for (int q = 0; q < 8; ++q) {
+          const float f = (float)v[q];
+          if ((di == 0 && dj == 0) || f > best[q] || (f != f && best[q] == best[q])) {
+            best[q] = f;
+            bi[q] = di * k + dj;
+          }
+        }
       }
     vec_t<HT, 8> out;
 #pragma unroll
     for (int q = 0; q < 8; ++q) out[q] = (HT)best[q];
     *reinterpret_cast<vec_t<HT, 8>*>(y + o * C + c8 * 8) = out;
+    if (idx) {
+      unsigned long long packed = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) packed |= (unsigned long long)bi[q] << (8 * q);
+      *reinterpret_cast<unsigned long long*>(idx + o * C + c8 * 8) = packed;
+    }
+  }
+}
+
+// gather form of the overlapping-window backward: input (i, j) collects dy of every window (oi, oj) that covers it
+// and whose argmax is it; times the ReLU mask of the (post-ReLU) pool input
+template <typename HT>
+__global__ __launch_bounds__(256) void maxpool_k_bwd_kernel(const HT* __restrict__ dy, const unsigned char* __restrict__ idx,
+                                                            const HT* __restrict__ post_in, int H, int W, int C, int k,
+                                                            int st, int Ho, int Wo, long total8, HT* __restrict__ dx) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total8; e += (long)gridDim.x * blockDim.x) {
+    const int C8 = C / 8;
+    const int c8 = (int)(e % C8);
+    const long pix = e / C8;
+    const int j = (int)(pix % W), i = (int)((pix / W) % H);
+    const long b = pix / ((long)W * H);
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    const int oi0 = i - k + 1 > 0 ? (i - k + 1 + st - 1) / st : 0, oi1 = min(i / st, Ho - 1);
+    const int oj0 = j - k + 1 > 0 ? (j - k + 1 + st - 1) / st : 0, oj1 = min(j / st, Wo - 1);
+    for (int oi = oi0; oi <= oi1; ++oi)
+      for (int oj = oj0; oj <= oj1; ++oj) {
+        const long o = ((b * Ho + oi) * Wo + oj) * C + c8 * 8;
+        const int pos = (i - oi * st) * k + (j - oj * st);
+        const vec_t<HT, 8> g = *reinterpret_cast<const vec_t<HT, 8>*>(dy + o);
+        const unsigned long long packed = *reinterpret_cast<const unsigned long long*>(idx + o);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if ((int)((packed >> (8 * q)) & 0xff) == pos) acc[q] += (float)g[q];
+      }
+    const vec_t<HT, 8> pin = *reinterpret_cast<const vec_t<HT, 8>*>(post_in + pix * C + c8 * 8);
+    vec_t<HT, 8> out;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) out[q] = (HT)((float)pin[q] > 0.f ? acc[q] : 0.f);
+    *reinterpret_cast<vec_t<HT, 8>*>(dx + pix * C + c8 * 8) = out;
+  }
+}
+
+// LPIPS alex conv0 (11x11 / 4, pad 2) input gradient: a thread per input pixel gathers the <= 3 x 3 output taps of its
+// stride phase; the 3 image channels accumulate in fp32 (channels 3..7 of the padded input get zero)
+template <typename HT>
+__global__ __launch_bounds__(256) void alex_conv0_dgrad_kernel(const HT* __restrict__ dpre, const float* __restrict__ w,
+                                                               int H, int W, int Ho, int Wo, int Cout, long npix,
+                                                               float* __restrict__ d8) {
+  constexpr int K = 11, ST = 4, PAD = 2;
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(p % W), i = (int)((p / W) % H);
+    const long b = p / ((long)W * H);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int ki = (i + PAD) % ST; ki < K; ki += ST) {
+      const int oi = (i + PAD - ki) / ST;
+      if (oi < 0 || oi >= Ho) continue;
+      for (int kj = (j + PAD) % ST; kj < K; kj += ST) {
+        const int oj = (j + PAD - kj) / ST;
+        if (oj < 0 || oj >= Wo) continue;
+        const HT* g = dpre + ((b * Ho + oi) * Wo + oj) * Cout;
+        const float* wt = w + (ki * K + kj) * 8;
+        for (int n = 0; n < Cout; n += 8) {
+          const vec_t<HT, 8> gv = *reinterpret_cast<const vec_t<HT, 8>*>(g + n);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float gq = (float)gv[q];
+            const float* wq = wt + (long)(n + q) * K * K * 8;
+            a0 = fmaf(gq, wq[0], a0);
+            a1 = fmaf(gq, wq[1], a1);
+            a2 = fmaf(gq, wq[2], a2);
+          }
+        }
+      }
+    }
+    float4* o = reinterpret_cast<float4*>(d8 + p * 8);
+    o[0] = make_float4(a0, a1, a2, 0.f);
+    o[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -347,7 +439,7 @@ int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float
                  float s2, void* y, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && y && B > 0 && H > 0 && W > 0, "nbp_vgg_prep: bad args");
   const long HW = (long)H * W, n = B * HW;
-  NBP_DISPATCH_16(dtype, HT, vgg_prep_kernel<HT><<<grid_for(n), 256, 0, S(s)>>>(x, HW, n, clamp, m0, m1, m2, s0, s1, s2,
+  NBP_DISPATCH_ALL(dtype, HT, vgg_prep_kernel<HT><<<grid_for(n), 256, 0, S(s)>>>(x, HW, n, clamp, m0, m1, m2, s0, s1, s2,
                                                                               reinterpret_cast<HT*>(y)));
   return check_launch("vgg_prep");
 }
@@ -355,7 +447,7 @@ int nbp_vgg_prep(const float* x, int B, int H, int W, int clamp, float m0, float
 int nbp_maxpool2_fwd(const void* x, int B, int H, int W, int C, void* y, unsigned char* idx, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && y && idx && B > 0 && H >= 2 && W >= 2 && C % 8 == 0, "nbp_maxpool2_fwd: bad args");
   const long total8 = (long)B * (H / 2) * (W / 2) * (C / 8);
-  NBP_DISPATCH_16(dtype, HT, maxpool_fwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+  NBP_DISPATCH_ALL(dtype, HT, maxpool_fwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
       reinterpret_cast<const HT*>(x), H, W, C, total8, reinterpret_cast<HT*>(y), idx));
   return check_launch("maxpool2_fwd");
 }
@@ -364,19 +456,43 @@ int nbp_maxpool2_bwd(const void* dy, const unsigned char* idx, const void* post_
                      int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dy && idx && post_in && dx && B > 0 && H >= 2 && W >= 2 && C % 8 == 0, "nbp_maxpool2_bwd: bad args");
   const long total8 = (long)B * H * W * (C / 8);
-  NBP_DISPATCH_16(dtype, HT, maxpool_bwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+  NBP_DISPATCH_ALL(dtype, HT, maxpool_bwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
       reinterpret_cast<const HT*>(dy), idx, reinterpret_cast<const HT*>(post_in), H, W, C, total8,
       reinterpret_cast<HT*>(dx)));
   return check_launch("maxpool2_bwd");
 }
 
-int nbp_maxpool_k_fwd(const void* x, int B, int H, int W, int C, int k, int stride, void* y, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(x && y && B > 0 && k > 0 && stride > 0 && H >= k && W >= k && C % 8 == 0, "nbp_maxpool_k_fwd: bad args");
+int nbp_maxpool_k_fwd(const void* x, int B, int H, int W, int C, int k, int stride, void* y, unsigned char* idx,
+                      int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && B > 0 && k > 0 && k * k <= 256 && stride > 0 && H >= k && W >= k && C % 8 == 0,
+              "nbp_maxpool_k_fwd: bad args");
   const int Ho = (H - k) / stride + 1, Wo = (W - k) / stride + 1;
   const long total8 = (long)B * Ho * Wo * (C / 8);
-  NBP_DISPATCH_16(dtype, HT, maxpool_k_fwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
-      reinterpret_cast<const HT*>(x), H, W, C, k, stride, Ho, Wo, total8, reinterpret_cast<HT*>(y)));
+  NBP_DISPATCH_ALL(dtype, HT, maxpool_k_fwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(x), H, W, C, k, stride, Ho, Wo, total8, reinterpret_cast<HT*>(y), idx));
   return check_launch("maxpool_k_fwd");
+}
+
+int nbp_maxpool_k_bwd(const void* dy, const unsigned char* idx, const void* post_in, int B, int H, int W, int C, int k,
+                      int stride, void* dx, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dy && idx && post_in && dx && B > 0 && k > 0 && stride > 0 && H >= k && W >= k && C % 8 == 0,
+              "nbp_maxpool_k_bwd: bad args");
+  const int Ho = (H - k) / stride + 1, Wo = (W - k) / stride + 1;
+  const long total8 = (long)B * H * W * (C / 8);
+  NBP_DISPATCH_ALL(dtype, HT, maxpool_k_bwd_kernel<HT><<<grid_for(total8), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(dy), idx, reinterpret_cast<const HT*>(post_in), H, W, C, k, stride, Ho, Wo, total8,
+      reinterpret_cast<HT*>(dx)));
+  return check_launch("maxpool_k_bwd");
+}
+
+int nbp_alex_conv0_input_grad(const void* dpre, const float* w, int B, int H, int W, int Ho, int Wo, int Cout,
+                              float* d8, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dpre && w && d8 && B > 0 && H > 0 && W > 0 && Cout % 8 == 0, "nbp_alex_conv0_input_grad: bad args");
+  NBP_REQUIRE(Ho == (H + 4 - 11) / 4 + 1 && Wo == (W + 4 - 11) / 4 + 1, "nbp_alex_conv0_input_grad: output geometry");
+  const long npix = (long)B * H * W;
+  NBP_DISPATCH_ALL(dtype, HT, alex_conv0_dgrad_kernel<HT><<<grid_for(npix), 256, 0, S(s)>>>(
+      reinterpret_cast<const HT*>(dpre), w, H, W, Ho, Wo, Cout, npix, d8));
+  return check_launch("alex_conv0_input_grad");
 }
 
 size_t nbp_feat_dist_workspace_doubles(long n) {
@@ -388,7 +504,7 @@ int nbp_feat_dist_fwd(const void* a, const void* b, long n, int mode, double sca
                       int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && ws && out && n > 0 && (mode == 0 || mode == 1), "nbp_feat_dist_fwd: bad args");
   const int g = (int)nbp_feat_dist_workspace_doubles(n);
-  NBP_DISPATCH_16(dtype, HT, feat_dist_fwd<HT><<<g, 256, 0, S(s)>>>(reinterpret_cast<const HT*>(a),
+  NBP_DISPATCH_ALL(dtype, HT, feat_dist_fwd<HT><<<g, 256, 0, S(s)>>>(reinterpret_cast<const HT*>(a),
                                                                      reinterpret_cast<const HT*>(b), n, mode, ws));
   feat_dist_finalize<<<1, 64, 0, S(s)>>>(ws, g, scale, out);
   return check_launch("feat_dist_fwd");
@@ -397,7 +513,7 @@ int nbp_feat_dist_fwd(const void* a, const void* b, long n, int mode, double sca
 int nbp_feat_dist_bwd(const void* a, const void* b, long n, int mode, float scale, int relu_mask, const float* up,
                       void* da, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && up && da && n > 0 && (mode == 0 || mode == 1), "nbp_feat_dist_bwd: bad args");
-  NBP_DISPATCH_16(dtype, HT, feat_dist_bwd<HT><<<grid_for(n), 256, 0, S(s)>>>(
+  NBP_DISPATCH_ALL(dtype, HT, feat_dist_bwd<HT><<<grid_for(n), 256, 0, S(s)>>>(
       reinterpret_cast<const HT*>(a), reinterpret_cast<const HT*>(b), n, mode, scale, relu_mask, up,
       reinterpret_cast<HT*>(da)));
   return check_launch("feat_dist_bwd");
@@ -413,7 +529,7 @@ int nbp_vgg_input_grad(const float* d8, const float* x, int B, int H, int W, int
 
 int nbp_add_relu_masked(void* d, const void* g, const void* post, long n, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(d && g && post && n > 0, "nbp_add_relu_masked: bad args");
-  NBP_DISPATCH_16(dtype, HT, add_relu_masked_kernel<HT><<<grid_for(n), 256, 0, S(s)>>>(
+  NBP_DISPATCH_ALL(dtype, HT, add_relu_masked_kernel<HT><<<grid_for(n), 256, 0, S(s)>>>(
       reinterpret_cast<HT*>(d), reinterpret_cast<const HT*>(g), reinterpret_cast<const HT*>(post), n));
   return check_launch("add_relu_masked");
 }
@@ -450,7 +566,7 @@ int nbp_lpips_tap_fwd(const void* a, const void* b, const float* w, int N, long 
   NBP_REQUIRE(a && b && w && ws && out && N > 0 && N <= 65535 && HW > 0 && C % 8 == 0 && C <= 2048,
               "nbp_lpips_tap_fwd: bad args");
   const int chunks = lpips_chunks(HW, N);
-  NBP_DISPATCH_16(dtype, HT, {
+  NBP_DISPATCH_ALL(dtype, HT, {
     const HT* pa = reinterpret_cast<const HT*>(a);
     const HT* pb = reinterpret_cast<const HT*>(b);
     const dim3 g(chunks, N);
@@ -464,7 +580,7 @@ int nbp_lpips_tap_bwd(const void* a, const void* b, const float* w, int N, long 
                       int dtype, nbp_stream_t s) {
   NBP_REQUIRE(a && b && w && up && da && N > 0 && HW > 0 && C % 8 == 0 && C <= 2048, "nbp_lpips_tap_bwd: bad args");
   const long npix = (long)N * HW;
-  NBP_DISPATCH_16(dtype, HT, {
+  NBP_DISPATCH_ALL(dtype, HT, {
     const HT* pa = reinterpret_cast<const HT*>(a);
     const HT* pb = reinterpret_cast<const HT*>(b);
     const long gpb = 256 / tap_lanes(C / 8);

@@ -2,11 +2,16 @@
 
 LPIPSEvaluator(net='alex' | 'vgg', device)(img_true, img_pred) -> float: the reference's input handling (shape checks,
 [C,H,W] promoted to [1,C,H,W], [0,255] -> [0,1] when max > 1.5, [0,1] -> [-1,1] when the values lie in [0,1]) around
-the MI355X LPIPS (lpips.py; the default 'alex' backbone runs forward-only).  Parity unpinned: the lpips package and its
-pretrained weights are absent here; synthetic deterministic weights unless `weights` is given.
+the MI355X LPIPS (lpips.py).  Parity unpinned: the lpips package and its pretrained weights are absent here.
+
+Weights: `weights` (an lpips-style state_dict or a path), else the path in $NBP_LPIPS_WEIGHTS_ALEX / _VGG.  A metric
+computed with the deterministic synthetic model would not be comparable with the reference's pretrained-weight LPIPS,
+so without weights the evaluator raises -- unless `allow_synthetic=True` (or $NBP_LPIPS_ALLOW_SYNTHETIC=1) is given
+explicitly, and then `synthetic` is True on the evaluator.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -19,10 +24,19 @@ __all__ = ["LPIPSEvaluator"]
 class LPIPSEvaluator:
     """lpips_metric.py:34-117: callable average LPIPS distance over two image batches."""
 
-    def __init__(self, net: str = "alex", device=None, weights=None) -> None:
+    def __init__(self, net: str = "alex", device=None, weights=None, allow_synthetic: Optional[bool] = None) -> None:
         if device is None:
             device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
         self.device = torch.device(device)
+        if weights is None:
+            weights = os.environ.get(f"NBP_LPIPS_WEIGHTS_{net.upper()}") or None
+        if allow_synthetic is None:
+            allow_synthetic = os.environ.get("NBP_LPIPS_ALLOW_SYNTHETIC") == "1"
+        if weights is None and not allow_synthetic:
+            raise RuntimeError(f"LPIPS metric (net={net!r}): pretrained weights are required (pass weights=<lpips "
+                               f"state_dict or path> or set NBP_LPIPS_WEIGHTS_{net.upper()}); the offline synthetic "
+                               "model gives numbers not comparable with lpips 0.1.4 -- opt in with allow_synthetic=True")
+        self.synthetic = weights is None
         self.loss_fn = LPIPS(net=net, weights=weights)
         self.loss_fn.eval()
 

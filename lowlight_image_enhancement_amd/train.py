@@ -52,10 +52,11 @@ class NBPTrainer:
                  scheduler: Optional[TrueCosineAnnealingLR] = None, process_group=None, bucket_mb: float = 25.0,
                  w_deltaE: float = 0.0, w_perc: float = 0.0, w_lpips: float = 0.0, perceptual=None, lpips=None,
                  loss_scale: Optional[str] = "auto", init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
-                 backoff_factor: float = 0.5, growth_interval: int = 2000):
+                 backoff_factor: float = 0.5, growth_interval: int = 2000, lpips_net: str = "vgg"):
         """Loss terms and weights as HybridLossPlus (losses.py:223-372): L1 (raw), Perc (VGG19), LPIPS (vgg), ΔE00,
         SSIM, Phys_srgb; a zero weight skips the term.  `perceptual` / `lpips`: PerceptualLoss / LPIPS modules
-        (constructed with the synthetic offline weights when needed and not given).  `loss_scale`: "auto" (dynamic
+        (constructed with the synthetic offline weights when needed and not given; `lpips_net` picks the backbone of
+        a constructed LPIPS: 'vgg' as HybridLossPlus, or 'alex' as BASELINE.json cfg3 names it).  `loss_scale`: "auto" (dynamic
         GradScaler scaling when net.precision == "fp16"), "dynamic" or None; the GradScaler arguments are torch's
         defaults.  A step whose gradient is non-finite leaves parameters and moments untouched in every mode."""
         self.net = net
@@ -69,16 +70,13 @@ class NBPTrainer:
         # scale), {L1, SSIM, Phys, DeltaE, Perc} then one LPIPS entry per image (d(w * mean_n LPIPS_n) / d LPIPS_n)
         self.up_base: Optional[torch.Tensor] = None
         self.up: Optional[torch.Tensor] = None
+        self._ups: Dict[int, tuple] = {}  # batch size -> (up_base, up), never freed (graphs hold their addresses)
         if w_perc and perceptual is None:
             from .NewBP_model.losses import PerceptualLoss
             perceptual = PerceptualLoss(device=dev)
         if w_lpips and lpips is None:
             from .lpips import LPIPS
-            lpips = LPIPS(net="vgg")
-        if net.precision == "fp16":  # the VGG trunks follow the autocast dtype under the trainer's loss scaling
-            for m in (perceptual, lpips):
-                if m is not None:
-                    m.precision = "fp16"
+            lpips = LPIPS(net=lpips_net)
         self.perceptual, self.lpips = perceptual, lpips
         self.lpips_buf: Optional[torch.Tensor] = None
         self.lr, self.betas, self.wd, self.eps = lr, betas, weight_decay, eps
@@ -100,6 +98,11 @@ class NBPTrainer:
             loss_scale = "dynamic" if net.precision == "fp16" else None
         self.scaler = (torch.tensor([init_scale, growth_factor, backoff_factor, float(growth_interval)],
                                     dtype=torch.float32, device=dev) if loss_scale == "dynamic" else None)
+        # VGG / LPIPS trunk type for modules left at precision "auto" (the trainer's default ones): fp32 in the fp32
+        # parity mode (the reference's fp32 trunk); in the 16-bit modes the autocast counterpart -- fp16 only under a
+        # loss scale (its ~1/n feature gradients underflow fp16 otherwise), else bf16.  A module given an explicit
+        # precision keeps it; the trainer never changes a module's attributes.
+        self.vgg_dt = 0 if net.precision == "fp32" else (2 if net.precision == "fp16" and self.scaler is not None else 1)
         self.loss_buf = torch.zeros(6, device=dev)  # L1, SSIM, Phys, DeltaE, Perc, Total
         self.iter = 0  # iterations run (the scheduler's position; AdamW's own step count self.t excludes skips)
         self.pg = process_group
@@ -178,12 +181,13 @@ class NBPTrainer:
             call("de00_loss_bwd", out, gt, B, H, W, 1, 1e-6, self.up[3:4], tmp)
             call("add", d_out, tmp, d_out, n, 0)
         if wpe != 0.0:
-            g = self.perceptual.value_and_grad(out, gt, self.up[4:5], self.loss_buf[4:5])
+            g = self.perceptual.value_and_grad(out, gt, self.up[4:5], self.loss_buf[4:5], dt=self._trunk_dt(self.perceptual))
             call("add", d_out, g, d_out, n, 0)
         if wlp != 0.0:
             if self.lpips_buf is None or self.lpips_buf.numel() != B:
                 self.lpips_buf = torch.zeros(B, device=lq.device)
-            g = self.lpips.value_and_grad(out, gt, self.up[5:5 + B], self.lpips_buf, clamp=True)
+            g = self.lpips.value_and_grad(out, gt, self.up[5:5 + B], self.lpips_buf, clamp=True,
+                                          dt=self._trunk_dt(self.lpips))
             call("add", d_out, g, d_out, n, 0)
         hook = self._on_stage if self.world > 1 else None
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
@@ -195,15 +199,33 @@ class NBPTrainer:
                 self._handles.clear()
         return out
 
+    def _trunk_dt(self, module) -> Optional[int]:
+        return self.vgg_dt if getattr(module, "precision", "auto") == "auto" else None
+
     def _ensure_up(self, B: int):
-        """Upstream-gradient buffers for a batch of B images (re-made when B changes; the current loss scale is
-        kept)."""
+        """Select the upstream-gradient buffers of a batch of B images.  One pair (up_base, up) per batch size is kept
+        for the trainer's lifetime: a captured graph addresses its pair by device pointer, so a pair is never freed or
+        rebound.  Switching to another batch size refreshes that pair's up = up_base * S from the current loss scale
+        (a device op: the optimizer of the steps run at other sizes moved S)."""
         if self.up_base is not None and self.up_base.numel() == 5 + B:
             return
-        wl1, wss, wph = self.w
-        base = [wl1, wss, wph, self.w_extra["de"], self.w_extra["perc"]] + [self.w_extra["lpips"] / B] * B
-        self.up_base = torch.tensor(base, dtype=torch.float32, device=self.dev)
-        self.up = self.up_base * self.scaler[0] if self.scaler is not None else self.up_base.clone()
+        pair = self._ups.get(B)
+        if pair is None:
+            wl1, wss, wph = self.w
+            base = [wl1, wss, wph, self.w_extra["de"], self.w_extra["perc"]] + [self.w_extra["lpips"] / B] * B
+            up_base = torch.tensor(base, dtype=torch.float32, device=self.dev)
+            pair = self._ups[B] = (up_base, up_base.clone())
+        self.up_base, self.up = pair
+        self._refresh_up()
+
+    def _refresh_up(self):
+        """up = up_base * S (the loss scale on the device), or up_base without a scaler."""
+        if self.up is None:
+            return
+        if self.scaler is not None:
+            torch.mul(self.up_base, self.scaler[0], out=self.up)
+        else:
+            self.up.copy_(self.up_base)
 
     def _optimizer(self, grad_scale: float):
         """clip + finiteness verdict + GradScaler update (nbp_optim_prepare), then AdamW (nbp_adamw_apply)."""
@@ -256,8 +278,13 @@ class NBPTrainer:
             for dst, src in zip(self._static, ins):
                 if (dst is None) != (src is None):
                     raise ValueError("graph_step: inputs must keep the structure of the captured step")
+                if dst is not None and tuple(src.shape) != tuple(dst.shape):
+                    raise ValueError(f"graph_step: input shape {tuple(src.shape)} differs from the captured "
+                                     f"{tuple(dst.shape)}; use step() for other batch shapes")
+            for dst, src in zip(self._static, ins):
                 if dst is not None and src is not dst:
                     dst.copy_(src, non_blocking=True)
+            self._ensure_up(self._static[0].shape[0])  # eager steps at another batch size may have switched pairs
         self.iter += 1
         slot = self.iter % len(self._lr_host)
         ev = self._lr_ev[slot]
@@ -382,5 +409,10 @@ class NBPTrainer:
         if self.scaler is not None:
             out["loss_scale"] = float(st[6])
         if st[2] != 0:
+            if self.scaler is None:
+                # no GradScaler: the reference has no skip here (image_restoration_model.py:316-320); a non-finite
+                # gradient left the parameters untouched, and the run must not continue silently
+                raise RuntimeError("NBPTrainer: the last step's gradient was non-finite (step skipped; no loss scaler "
+                                   f"is active); grad_norm={float(st[0])}")
             out["skipped"] = 1.0
         return out

@@ -6,9 +6,10 @@ A frozen VGG `features` prefix (3x3 conv + ReLU, 2x2 max pool) runs over NHWC bf
   * the input gradient (weights are frozen: no weight gradients) is the same implicit GEMM over the gradient map with
     the tap-flipped, transposed weights; the ReLU masks ride in the epilogue (conv -> conv) or in the pool backward
     (conv -> pool -> conv); max pools keep their argmax.
-16-bit operands with fp32 accumulation: bf16 (default; no loss scaling needed) or fp16 (`dtype=2`, the reference's
-autocast dtype, used under the trainer's dynamic loss scaling -- its 11-bit significand keeps the deep input gradient
-far closer to fp32).
+Storage / operand type `dtype`: 0 fp32 (the reference's own trunk: PerceptualLoss feeds `x.float()` to the conv stack,
+NewBP_model/losses.py:63-69; implicit GEMM on the fp32 MFMA, exact products), 1 bf16 or 2 fp16 (16-bit MFMA operands,
+fp32 accumulation; fp16 is the reference's autocast dtype, used under the trainer's dynamic loss scaling -- its 11-bit
+significand keeps the deep input gradient far closer to fp32).
 
 Pretrained ImageNet weights (torchvision / lpips downloads) are not available offline: `weights=None` builds the
 architecture with a deterministic synthetic initialisation (kaiming-normal fan-out as torchvision, seed 0); pass a
@@ -64,6 +65,22 @@ def _pad8(c: int) -> int:
     return (c + 7) // 8 * 8
 
 
+TORCH_DTYPE = {0: torch.float32, 1: torch.bfloat16, 2: torch.float16}
+PRECISIONS = {"fp32": 0, "bf16": 1, "fp16": 2}
+
+
+def resolve_precision(precision: str) -> int:
+    """C-ABI dtype of a trunk precision.  "auto" follows torch.autocast as the reference's fp32 module does under
+    it (fp16 / bf16 conv operands inside an enabled CUDA autocast region, fp32 otherwise)."""
+    if precision == "auto":
+        if torch.is_autocast_enabled("cuda"):
+            return 2 if torch.get_autocast_dtype("cuda") == torch.float16 else 1
+        return 0
+    if precision not in PRECISIONS:
+        raise ValueError(f"VGG trunk precision must be 'auto', 'fp32', 'bf16' or 'fp16', got {precision!r}")
+    return PRECISIONS[precision]
+
+
 class VGGStack:
     """Frozen VGG features[:n_modules] on device.  forward() returns the final post-ReLU map (NHWC bf16) and,
     when asked, the post-ReLU maps at `taps` (torch module indices of ReLUs); backward() maps d(final pre-ReLU map)
@@ -71,11 +88,12 @@ class VGGStack:
 
     def __init__(self, cfg, n_modules: int, device, weights: Union[None, str, Dict[str, torch.Tensor]] = None,
                  seed: int = 0, dtype: int = 1):
-        if dtype not in (1, 2):
-            raise ValueError("VGGStack dtype: 1 (bf16) or 2 (fp16)")
+        if dtype not in (0, 1, 2):
+            raise ValueError("VGGStack dtype: 0 (fp32), 1 (bf16) or 2 (fp16)")
         self.cfg, self.n_modules, self.device = cfg, n_modules, torch.device(device)
         self.dtype = dtype
-        self.tdt = torch.float16 if dtype == 2 else torch.bfloat16
+        self.tdt = TORCH_DTYPE[dtype]
+        self.ydt = 0 if dtype == 0 else 1  # nbp_conv3x3_bf16's y_dtype for an activation-typed output
         if weights is None:
             warnings.warn("VGG: ImageNet weights are not available offline; using a deterministic synthetic "
                           "initialisation (pass weights=<state_dict or path> for real weights)", RuntimeWarning)
@@ -107,7 +125,8 @@ class VGGStack:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x8: torch.Tensor, save: bool, taps: Sequence[int] = ()):
-        """x8: [B][H][W][8] 16-bit prepared input (prep_input with this stack's dtype).  Returns (final post-ReLU map, tape, {tap index: post map})."""
+        """x8: [B][H][W][8] prepared input (prep_input with this stack's dtype).  Returns (final post-ReLU map, tape,
+        {tap index: post map})."""
         B, H, W, _ = x8.shape
         h, w, feat = H, W, x8
         tape: List = []
@@ -115,7 +134,8 @@ class VGGStack:
         for L in self.layers:
             if L["kind"] == "conv":
                 y = torch.empty(B, h, w, L["cout"], device=x8.device, dtype=self.tdt)
-                call("conv3x3_bf16", feat, B, h, w, L["cin"], L["wf"], L["cout"], L["bias"], 0, None, y, 1, self.dtype)
+                call("conv3x3_bf16", feat, B, h, w, L["cin"], L["wf"], L["cout"], L["bias"], 0, None, y, self.ydt,
+                     self.dtype)
                 if save:
                     tape.append(("conv", L, (B, h, w), y))
                 if L["idx"] + 1 in taps:
@@ -134,7 +154,7 @@ class VGGStack:
 
     # ------------------------------------------------------------------ input gradient
     def backward(self, tape, d_last_pre: torch.Tensor, tap_grads: Optional[Dict[int, torch.Tensor]] = None):
-        """d_last_pre: gradient w.r.t. the last conv's PRE-ReLU output (16-bit NHWC).  tap_grads: {relu index:
+        """d_last_pre: gradient w.r.t. the last conv's PRE-ReLU output (NHWC, the stack's type).  tap_grads: {relu index:
         gradient w.r.t. that post-ReLU map} added where the walk passes it.  Returns d(prepared input) fp32 [B,H,W,8]."""
         tap_grads = tap_grads or {}
         d = d_last_pre
@@ -152,7 +172,7 @@ class VGGStack:
             if prev[0] == "conv":  # conv -> ReLU -> conv: mask by the previous post map in the epilogue
                 post = prev[3]
                 dn = torch.empty(B, h, w, L["cin"], device=d.device, dtype=self.tdt)
-                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 2, post, dn, 1, self.dtype)
+                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 2, post, dn, self.ydt, self.dtype)
                 tg = tap_grads.get(prev[1]["idx"] + 1)
                 if tg is not None:  # + d(tap) * relu mask
                     call("add_relu_masked", dn, tg.to(self.tdt).contiguous(), post, dn.numel(), self.dtype)
@@ -160,7 +180,7 @@ class VGGStack:
             else:  # conv -> ReLU -> pool -> conv
                 (_, (Bp, hp, wp, C), idx, pool_in) = prev
                 dp = torch.empty(B, h, w, L["cin"], device=d.device, dtype=self.tdt)
-                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 1, None, dp, 1, self.dtype)
+                call("conv3x3_bf16", d, B, h, w, L["cout"], L["wt"], L["cin"], None, 1, None, dp, self.ydt, self.dtype)
                 dn = torch.empty(Bp, hp, wp, C, device=d.device, dtype=self.tdt)
                 call("maxpool2_bwd", dp, idx, pool_in, Bp, hp, wp, C, dn, self.dtype)
                 conv_before = tape[k - 2]
@@ -172,13 +192,13 @@ class VGGStack:
 
 
 def prep_input(x: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD, clamp: bool = True, dtype: int = 1) -> torch.Tensor:
-    """NCHW fp32 [B,3,H,W] -> NHWC 16-bit [B,H,W,8] of (clamp01(x) - mean) / std (nbp_vgg_prep)."""
+    """NCHW fp32 [B,3,H,W] -> NHWC [B,H,W,8] (the stack's type) of (clamp01(x) - mean) / std (nbp_vgg_prep)."""
     _lib.require_cuda(x)
     if x.dim() != 4 or x.shape[1] != 3:
         raise ValueError(f"VGG input must be [B,3,H,W], got {tuple(x.shape)}")
     x = x.float().contiguous()
     B, _, H, W = x.shape
-    y = torch.empty(B, H, W, 8, device=x.device, dtype=torch.float16 if dtype == 2 else torch.bfloat16)
+    y = torch.empty(B, H, W, 8, device=x.device, dtype=TORCH_DTYPE[dtype])
     call("vgg_prep", x, B, H, W, int(clamp), *[float(v) for v in mean], *[float(v) for v in std], y, dtype)
     return y
 

@@ -213,6 +213,26 @@ def ssim_linear(pred, target, data_range=1.0, kernel_size=11, sigma=1.5, k1=0.01
     return {"mean": pi.mean(0), "sum": pi.sum(0), "none": pi}[reduction]
 
 
+def luma_bt601(images):
+    """metrics/ssim.py:119-131 (_to_luma_bt601)."""
+    return 0.2989 * images[:, 0:1] + 0.5870 * images[:, 1:2] + 0.1140 * images[:, 2:3]
+
+
+def ssim_align_pair(target, prediction, policy, mode="bilinear"):
+    """metrics/ssim.py:134-167 (_align_pair): resize the prediction to the target's size, or centre-crop both."""
+    if policy is None:
+        return target, prediction
+    if policy == "resize":
+        return target, F.interpolate(prediction, size=target.shape[-2:], mode=mode, align_corners=False)
+    h, w = min(target.shape[-2], prediction.shape[-2]), min(target.shape[-1], prediction.shape[-1])
+
+    def crop(x):
+        top, left = max((x.shape[-2] - h) // 2, 0), max((x.shape[-1] - w) // 2, 0)
+        return x[:, :, top:top + h, left:left + w]
+
+    return crop(target), crop(prediction)
+
+
 # ---- torchvision==0.17.1 vgg19 / vgg16 `features` and lpips==0.1.4, restated (losses.py:32-69, 265-274) ----
 # Weights: torchvision's pretrained files are a download (unavailable offline), so the oracle takes the state_dict
 # the caller passes (the product's deterministic synthetic one in the tests) -- parity unpinned for real weights.

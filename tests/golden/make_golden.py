@@ -159,6 +159,79 @@ def gen_phys_srgb(R):
     save("phys_srgb.npz", **out)
 
 
+def gen_phys_raw_full(R):
+    """PhysicsConsistencyLoss (losses.py:158-192) in its groups == 1 branch: a [Co,1,kh,kw] kernel with Co not in
+    {1, C} (expanded along C) and full [Co,C,kh,kw] kernels, with F.l1_loss's channel broadcast against A; plus the
+    kernel forms the reference's conv2d rejects (recorded as raising)."""
+    import warnings
+    g = torch.Generator().manual_seed(21)
+    B, H, W = 2, 12, 10
+    ratio = torch.tensor([100.0, 250.0])
+    cases = {  # name: (C, kernel shape, A channels, clamp_align)
+        "c1_co2": (1, (2, 1, 3, 3), 1, True),
+        "c3_co4_a1": (3, (4, 1, 3, 3), 1, True),
+        "c3_co4_a4": (3, (4, 1, 3, 3), 4, False),
+        "full_c3_co2": (3, (2, 3, 3, 3), 2, False),
+        "full_c3_co2_a1": (3, (2, 3, 5, 3), 1, True),
+        "full_c4_co1_a4": (4, (1, 4, 3, 3), 4, True),
+        "full_c3_co3": (3, (3, 3, 3, 3), 3, True),
+    }
+    out = {"ratio": t2n(ratio), "cases": np.asarray(list(cases))}
+    for name, (C, ks, Ca, clamp) in cases.items():
+        bhat = torch.rand(B, C, H, W, generator=g)
+        k = torch.rand(*ks, generator=g) / (ks[1] * ks[2] * ks[3] / 2)
+        a = torch.rand(B, Ca, H, W, generator=g) / 250.0
+        out[f"{name}_bhat"], out[f"{name}_k"], out[f"{name}_a"] = t2n(bhat), t2n(k), t2n(a)
+        out[f"{name}_clamp"] = np.asarray(int(clamp))
+        crit = R.lo.PhysicsConsistencyLoss(k, device="cpu", clamp_align=clamp)
+        bi = bhat.clone().requires_grad_(True)
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                loss = crit(bi, a, ratio)
+            loss.backward()
+        except RuntimeError:
+            out[f"{name}_raises"] = np.asarray(1)
+            continue
+        out[f"{name}_raises"] = np.asarray(0)
+        out[f"{name}_loss"] = t2n(loss)
+        out[f"{name}_grad"] = t2n(bi.grad)
+    save("phys_raw_full.npz", **out)
+
+
+def gen_ssim_align(R):
+    """calculate_ssim's input alignment from the reference's own helpers (metrics/ssim.py:119-167): _to_luma_bt601 and
+    _align_pair ('center_crop', 'resize' bilinear / bicubic).  metrics/ssim.py imports torchmetrics at module level
+    (absent here): it is loaded with a stub `torchmetrics.image` whose SSIM class is never constructed -- only the two
+    helpers run."""
+    tm = types.ModuleType("torchmetrics")
+    tm.__path__ = []
+    tmi = types.ModuleType("torchmetrics.image")
+    tmi.StructuralSimilarityIndexMeasure = None
+    sys.modules["torchmetrics"], sys.modules["torchmetrics.image"] = tm, tmi
+    spec = importlib.util.spec_from_file_location("ref_metrics_ssim", os.path.join(R.ref, "metrics", "ssim.py"))
+    m = importlib.util.module_from_spec(spec)
+    sys.modules["ref_metrics_ssim"] = m  # dataclasses resolve the module by name
+    spec.loader.exec_module(m)
+    g = torch.Generator().manual_seed(22)
+    rgb = torch.rand(2, 3, 29, 33, generator=g)
+    out = {"rgb": t2n(rgb), "luma": t2n(m._to_luma_bt601(rgb))}
+    tgt = torch.rand(2, 3, 40, 36, generator=g)
+    pred = torch.rand(2, 3, 31, 45, generator=g)
+    out["tgt"], out["pred"] = t2n(tgt), t2n(pred)
+    ct, cp = m._align_pair(tgt, pred, "center_crop")
+    out["crop_t"], out["crop_p"] = t2n(ct), t2n(cp)
+    for mode in ("bilinear", "bicubic"):
+        _, rp = m._align_pair(tgt, pred, "resize", mode)
+        out[f"resize_{mode}"] = t2n(rp)
+    small = torch.rand(1, 3, 17, 13, generator=g)  # upsampling as well
+    out["small"] = t2n(small)
+    for mode in ("bilinear", "bicubic"):
+        _, rp = m._align_pair(tgt, small, "resize", mode)
+        out[f"up_{mode}"] = t2n(rp)
+    save("ssim_align.npz", **out)
+
+
 def gen_phys_cons(R):
     """phys_cons_raw / phys_cons_srgb (metrics/phys_consistency.py:193-368): the variant matrix."""
     import itertools
@@ -424,9 +497,10 @@ def main():
     torch.set_num_threads(8)
     R = load_reference(args.ref)
     R.ref = args.ref
-    gens = dict(psf=gen_psf, phys_srgb=gen_phys_srgb, phys_cons=gen_phys_cons, layernorm=gen_layernorm,
+    gens = dict(psf=gen_psf, phys_srgb=gen_phys_srgb, phys_raw_full=gen_phys_raw_full, phys_cons=gen_phys_cons, layernorm=gen_layernorm,
                 nafblock=gen_nafblock, nets=gen_nets, cfg_nets=gen_cfg_nets, widths=gen_widths, cfg5=gen_cfg5,
-                train_steps=gen_train_steps, color=gen_color, linear=gen_linear)
+                train_steps=gen_train_steps, color=gen_color, linear=gen_linear,
+                ssim_align=gen_ssim_align)
     for name, fn in gens.items():
         if not args.only or name in args.only.split(","):
             fn(R)

@@ -145,3 +145,44 @@ def test_resume_is_bitwise_continuation(dev, tmp_path):
     assert torch.equal(c.net.flat, a.net.flat)
     assert torch.equal(c.exp_avg, a.exp_avg) and torch.equal(c.exp_avg_sq, a.exp_avg_sq)
     assert np.isfinite(c.logs()["Total"])
+
+
+@pytest.mark.gpu
+def test_resume_into_a_trainer_that_has_stepped(dev, tmp_path):
+    """fp16 with dynamic loss scaling (growth every step): a trainer that already ran two steps (scale 2^18) resumes a
+    state saved at scale 2^17; its upstream gradients must follow the restored scale, so the next step equals an
+    uninterrupted run bit for bit (resume_training re-derives up = up_base * S)."""
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    g = golden("train_steps_cfg0.npz")
+    keys = list(create_newbp_net(in_channels=3, **CFG).state_dict().keys())
+    init = {k: torch.from_numpy(g["init:" + k]) for k in keys}
+
+    def trainer():
+        net = create_newbp_net(in_channels=3, **CFG)
+        net.load_state_dict(init)
+        net = net.to(dev)
+        net.precision = "fp16"
+        return NBPTrainer(net, psf_mode="rgb", psf_spec="B2", w_l1=1.0, w_phys=0.1, growth_interval=1)
+
+    batches = []
+    for s in range(2):
+        lq, gt = torch.from_numpy(g[f"s{s}:lq"]).to(dev), torch.from_numpy(g[f"s{s}:gt"]).to(dev)
+        r = torch.ones(lq.shape[0], 1, 1, 1, device=dev)
+        batches.append((lq, gt, (lq * r).clamp(0, 1), r))
+    a = trainer()
+    for b in batches:
+        a.step(*b)
+    bt = trainer()
+    bt.step(*batches[0])
+    ck.save_network(bt.net, str(tmp_path / "net_g_1.pth"))
+    ck.save_training_state(bt, 0, 1, str(tmp_path))
+    c = trainer()
+    c.step(*batches[1])
+    c.step(*batches[0])
+    assert float(c.scaler[0]) == 2.0 ** 18
+    ck.load_network(c.net, str(tmp_path / "net_g_1.pth"))
+    ck.resume_training(c, str(tmp_path / "1.state"))
+    assert float(c.scaler[0]) == 2.0 ** 17
+    c.step(*batches[1])
+    assert torch.equal(c.net.flat, a.net.flat)
+    assert torch.equal(c.exp_avg, a.exp_avg) and torch.equal(c.exp_avg_sq, a.exp_avg_sq)

@@ -177,9 +177,9 @@ def _synthetic_loss_weights():
 
 def test_cfg3_loss_head_512_against_oracle(dev):
     """cfg3: cfg2 model + every HybridLossPlus term (L1, VGG19 Perc, LPIPS(vgg), ΔE00, SSIM, Phys_srgb) at bs 1 x 512^2,
-    fp32 network mode, against the oracle with the same synthetic VGG weights.  The VGG trunks run bf16 MFMA: Perc /
-    LPIPS values within 3 %, the rest 1e-5; parameter gradient within 2 % (rel. norm; the VGG input gradient in bf16
-    is the inexact part)."""
+    fp32 network mode, against the oracle with the same synthetic VGG weights.  The fp32 mode runs the VGG / LPIPS
+    trunks in fp32 like the reference (NewBP_model/losses.py:63-69): every loss scalar within 1e-5 rel, per-tensor
+    parameter gradients within 1e-3 of the tensor's max (the cfg2 step's bound)."""
     from lowlight_image_enhancement_amd.NewBP_model.losses import PerceptualLoss
     from lowlight_image_enhancement_amd.lpips import LPIPS
     from lowlight_image_enhancement_amd.train import NBPTrainer
@@ -192,6 +192,7 @@ def test_cfg3_loss_head_512_against_oracle(dev):
     w = dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1, w_perc=0.02, w_lpips=0.05, w_deltaE=0.02)
     tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", perceptual=PerceptualLoss(device=dev, weights=v19),
                     lpips=LPIPS(net="vgg", weights=lp_sd), **w)
+    assert tr.vgg_dt == 0
     gen = torch.Generator().manual_seed(311)
     lq, gt = torch.rand(1, 3, 512, 512, generator=gen), torch.rand(1, 3, 512, 512, generator=gen)
     r = torch.ones(1, 1, 1, 1)
@@ -201,16 +202,48 @@ def test_cfg3_loss_head_512_against_oracle(dev):
                         vgg19_sd=v19, lpips_parts=(v16, lins))
     _, tot, ref_logs = ora.loss(lq, gt, lq, r)
     tot.backward()
-    for k in ("L1_raw", "SSIM", "Phys", "DeltaE"):
+    for k in ("L1_raw", "SSIM", "Phys", "DeltaE", "Perc", "LPIPS", "Total"):
         ref = float(ref_logs[k])
         assert abs(logs[k] - ref) <= 1e-5 * abs(ref), (k, logs[k], ref)
+    grads = _grads_ref_layout(net, tr.grad)
+    for k, p in ora.P.items():
+        scale = p.grad.abs().max().item()
+        err = (grads[k] - p.grad).abs().max().item()
+        assert err <= 1e-3 * scale + 1e-8, (k, err, scale)
+
+
+def test_cfg3_loss_head_fp16_trunk(dev):
+    """The fp16 mode's loss head (fp16 network and fp16 VGG / LPIPS trunks under the dynamic loss scale, the
+    reference's autocast counterpart) at a stated bound against the fp32 oracle: Perc / LPIPS within 3 %, the pixel
+    terms within 1e-2 (fp16 network output)."""
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PerceptualLoss
+    from lowlight_image_enhancement_amd.lpips import LPIPS
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    from oracle.train_step import OracleTrainer
+    torch.set_num_threads(16)
+    net, sd = _recipe_net(CFG2, 312, dev, "fp16")
+    v19, v16, lins = _synthetic_loss_weights()
+    lp_sd = {f"net.slice1.{k}": v for k, v in v16.items()}
+    lp_sd.update({f"lin{k}.model.1.weight": w.view(1, -1, 1, 1) for k, w in enumerate(lins)})
+    w = dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1, w_perc=0.02, w_lpips=0.05, w_deltaE=0.02)
+    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", perceptual=PerceptualLoss(device=dev, weights=v19),
+                    lpips=LPIPS(net="vgg", weights=lp_sd), **w)
+    assert tr.vgg_dt == 2
+    gen = torch.Generator().manual_seed(313)
+    lq, gt = torch.rand(1, 3, 256, 256, generator=gen), torch.rand(1, 3, 256, 256, generator=gen)
+    r = torch.ones(1, 1, 1, 1)
+    tr.loss_and_grad(lq.to(dev), gt.to(dev), lq.to(dev), r.to(dev))
+    logs = tr.logs()
+    ora = OracleTrainer(sd, BLK(CFG2), w_l1=1.0, w_ssim=0.05, w_phys=0.1, w_de=0.02, w_perc=0.02, w_lpips=0.05,
+                        vgg19_sd=v19, lpips_parts=(v16, lins))
+    with torch.no_grad():
+        _, _, ref_logs = ora.loss(lq, gt, lq, r)
+    for k in ("L1_raw", "SSIM", "Phys", "DeltaE"):
+        ref = float(ref_logs[k])
+        assert abs(logs[k] - ref) <= 1e-2 * abs(ref), (k, logs[k], ref)
     for k in ("Perc", "LPIPS"):
         ref = float(ref_logs[k])
         assert abs(logs[k] - ref) <= 3e-2 * abs(ref), (k, logs[k], ref)
-    grads = _grads_ref_layout(net, tr.grad)
-    num = sum(((grads[k] - p.grad) ** 2).sum().item() for k, p in ora.P.items())
-    den = sum((p.grad ** 2).sum().item() for p in ora.P.values())
-    assert (num / den) ** 0.5 < 2e-2, (num / den) ** 0.5
 
 
 # ---------------------------------------------------------------------------------------------- public loss classes
@@ -251,12 +284,11 @@ def test_hybrid_loss_plus_from_rgb_config(dev):
     wts = dict(L1_raw=1.0, Perc=0.02, DeltaE=0.02, Phys=0.1)
     ref_total = sum(wts[n] * v for n, v in terms.items())
     ref_total.backward()
-    for n, v in terms.items():
-        tol = 3e-2 if n == "Perc" else 1e-5
-        assert abs(logs[n].item() - v.item()) <= tol * abs(v.item()), (n, logs[n].item(), v.item())
-    assert abs(logs["Total"].item() - ref_total.item()) <= 1e-4 * ref_total.item()
+    for n, v in terms.items():  # the VGG trunk runs fp32 outside autocast, as the reference's does
+        assert abs(logs[n].item() - v.item()) <= 1e-5 * abs(v.item()), (n, logs[n].item(), v.item())
+    assert abs(logs["Total"].item() - ref_total.item()) <= 1e-5 * ref_total.item()
     a, b = o.grad.cpu().double().flatten(), orr.grad.double().flatten()
-    assert ((a - b).norm() / b.norm()).item() < 1e-2
+    assert ((a - b).norm() / b.norm()).item() < 1e-5
 
 
 def test_hybrid_loss_plus_zero_weight_terms_still_logged(dev):
@@ -289,10 +321,10 @@ def test_hybrid_loss_value_and_gradient(dev):
     rl1, rperc = OL.l1(xr, y), OL.perceptual_loss(v19, xr, y)
     (rl1 + 0.1 * rperc).backward()
     assert abs(l1.item() - rl1.item()) <= 1e-5 * rl1.item()
-    assert abs(perc.item() - rperc.item()) <= 3e-2 * rperc.item()
+    assert abs(perc.item() - rperc.item()) <= 1e-5 * rperc.item()
     assert abs(total.item() - (l1.item() + 0.1 * perc.item())) <= 1e-6
     a, b = xd.grad.cpu().double().flatten(), xr.grad.double().flatten()
-    assert ((a - b).norm() / b.norm()).item() < 1e-2
+    assert ((a - b).norm() / b.norm()).item() < 1e-5
 
 
 @pytest.mark.parametrize("kernel_type,spec", [("panchromatic", "P2"), ("rgb", "B2")])

@@ -75,6 +75,31 @@ def test_phys_raw_loss(dev):
             close(b.grad, g[f"raw_{name}_c{int(c)}_grad"], atol=1e-9, rtol=1e-5)
 
 
+def test_phys_raw_loss_groups1_branch(dev):
+    """PhysicsConsistencyLoss's groups == 1 branch (losses.py:182-191) vs the reference's outputs
+    (phys_raw_full.npz): a [Co,1,kh,kw] kernel with Co not in {1, C} expanded along C, full [Co,C,kh,kw] kernels
+    (5x3 too), the L1 under F.l1_loss's channel broadcast (A with 1 or Co channels); loss 1e-5 rel, gradient 1e-6.
+    Kernel forms the reference's conv2d rejects raise RuntimeError here too."""
+    import warnings
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PhysicsConsistencyLoss
+    g = golden("phys_raw_full.npz")
+    for name in g["cases"]:
+        name = str(name)
+        crit = PhysicsConsistencyLoss(T(g[f"{name}_k"]), device=dev, clamp_align=bool(g[f"{name}_clamp"]))
+        b = C(g[f"{name}_bhat"], dev).requires_grad_(True)
+        if int(g[f"{name}_raises"]):
+            with pytest.raises(RuntimeError):
+                crit(b, C(g[f"{name}_a"], dev), C(g["ratio"], dev))
+            continue
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            loss = crit(b, C(g[f"{name}_a"], dev), C(g["ratio"], dev))
+        loss.backward()
+        ref = float(g[f"{name}_loss"])
+        assert abs(loss.item() - ref) <= 1e-5 * abs(ref), (name, loss.item(), ref)
+        close(b.grad, g[f"{name}_grad"], atol=1e-6 * np.abs(g[f"{name}_grad"]).max(), rtol=1e-5)
+
+
 def test_phys_cons_variant_matrix(dev):
     from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_raw, phys_cons_srgb
     g = golden("phys_cons.npz")
@@ -545,6 +570,38 @@ def test_graph_step_bitwise_equals_eager(dev, precision):
         assert torch.equal(net_a.flat, net_b.flat), f"params differ at step {i}"
         assert torch.equal(trs[0].exp_avg_sq, trs[1].exp_avg_sq)
         assert trs[0].logs() == trs[1].logs()
+
+
+def test_graph_step_survives_eager_steps_at_other_batch_sizes(dev):
+    """A captured graph addresses the upstream-gradient buffers of its batch size: eager steps at another batch size
+    (a short last batch) must neither free them nor leave them at a stale loss scale.  fp16 with a growth interval of 1
+    moves the scale every step, so graph replays after eager B=1 steps equal an all-eager trainer bit for bit.  A
+    replay with a different input shape raises."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    cfg = dict(width=16, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1])
+    torch.manual_seed(0)
+    nets = [create_newbp_net(in_channels=3, kernel_type="rgb", kernel_spec="B2", **cfg) for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    trs = []
+    for net in nets:
+        net.to(dev)
+        net.precision = "fp16"
+        trs.append(NBPTrainer(net, w_l1=1.0, w_ssim=0.05, w_phys=0.1, growth_interval=1))
+    g = torch.Generator(device=dev).manual_seed(6)
+    big = tuple(torch.rand(2, 3, 48, 48, device=dev, generator=g) for _ in range(2))
+    small = tuple(torch.rand(1, 3, 48, 48, device=dev, generator=g) for _ in range(2))
+    ratio2, ratio1 = torch.ones(2, 1, 1, 1, device=dev), torch.ones(1, 1, 1, 1, device=dev)
+    plan = [(big, ratio2, True), (small, ratio1, False), (small, ratio1, False), (big, ratio2, True),
+            (big, ratio2, True)]
+    for i, ((lq, gt), r, graph) in enumerate(plan):
+        trs[0].step(lq, gt, lq.clamp(0, 1), r)
+        (trs[1].graph_step if graph else trs[1].step)(lq, gt, lq.clamp(0, 1), r)
+        assert torch.equal(nets[0].flat, nets[1].flat), f"params differ at step {i}"
+        assert torch.equal(trs[0].scaler, trs[1].scaler)
+    assert float(trs[1].scaler[0]) == 2.0 ** 16 * 2 ** 5  # grew every step: the buffers were kept in step with it
+    with pytest.raises(ValueError, match="captured"):
+        trs[1].graph_step(small[0], small[1], small[0].clamp(0, 1), ratio1)
 
 
 @pytest.mark.parametrize("M,C", [(1000, 32), (4096, 64), (300, 24)])

@@ -73,6 +73,36 @@ def test_phys_srgb_all_ratio_forms():
             close(b.grad, g[f"raw_{name}_c{int(c)}_grad"], atol=1e-9)
 
 
+def test_phys_raw_groups1_fixtures():
+    """The oracle's raw physics loss in the reference's groups == 1 branch (losses.py:182-191) vs the reference's
+    outputs: expanded [Co,1,kh,kw] and full [Co,C,kh,kw] kernels, F.l1_loss's channel broadcast, rejected forms."""
+    g = golden("phys_raw_full.npz")
+    for name in g["cases"]:
+        name = str(name)
+        b = T(g[f"{name}_bhat"]).clone().requires_grad_(True)
+        args = (T(g[f"{name}_a"]), T(g["ratio"]), T(g[f"{name}_k"]))
+        if int(g[f"{name}_raises"]):
+            with pytest.raises(RuntimeError):
+                P.phys_raw_loss(b, *args, clamp_align=bool(g[f"{name}_clamp"]))
+            continue
+        loss = P.phys_raw_loss(b, *args, clamp_align=bool(g[f"{name}_clamp"]))
+        loss.backward()
+        close(loss, g[f"{name}_loss"], atol=1e-6)
+        close(b.grad, g[f"{name}_grad"], atol=1e-9)
+
+
+def test_ssim_alignment_helpers_fixtures():
+    """The oracle's calculate_ssim input alignment vs the reference's own helpers (metrics/ssim.py:119-167)."""
+    import oracle.losses as OL
+    g = golden("ssim_align.npz")
+    assert torch.equal(OL.luma_bt601(T(g["rgb"])), T(g["luma"]))
+    ct, cp = OL.ssim_align_pair(T(g["tgt"]), T(g["pred"]), "center_crop")
+    assert torch.equal(ct, T(g["crop_t"])) and torch.equal(cp, T(g["crop_p"]))
+    for mode in ("bilinear", "bicubic"):
+        assert torch.equal(OL.ssim_align_pair(T(g["tgt"]), T(g["pred"]), "resize", mode)[1], T(g[f"resize_{mode}"]))
+        assert torch.equal(OL.ssim_align_pair(T(g["tgt"]), T(g["small"]), "resize", mode)[1], T(g[f"up_{mode}"]))
+
+
 def test_phys_cons_variant_matrix():
     g = golden("phys_cons.npz")
     cases = json.load(open(os.path.join(GOLDEN, "phys_cons_cases.json")))
