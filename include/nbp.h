@@ -200,14 +200,6 @@ int nbp_dw_chunks(int B, int H, int W, int C, int which);
 int nbp_dw_fwd_slab_rows(int B, int H, int W, int C, int dtype);
 int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
                        int H, int W, int C, int dtype, nbp_stream_t s);
-/* Levels 0 / 1 fused: conv1 (1x1, C -> 2C, w1 = the 16-bit per-step weight copy [2C][C], b1 fp32) -> depthwise
- * 3x3 -> SimpleGate -> pool partials in one launch (NAFNet_arch.py:60-66 + :38): writes t1 and t2 ([M][2C], the
- * backward's tape), g ([M][C]) and pool_slab [B][nbp_c1_dw_slab_rows][C]; t1 / t2 / g equal nbp_gemm_bf16 (conv1) +
- * nbp_dw_sg_pool_fwd, only the pool partials are summed over other tiles.  C in {32, 64}, dtype 1 / 2;
- * nbp_c1_dw_slab_rows returns 0 for a shape it does not serve. */
-int nbp_c1_dw_slab_rows(int H, int W, int C, int dtype);
-int nbp_c1_dw_sg_pool_fwd(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
-                          void* t2, void* g, float* pool_slab, int B, int H, int W, int C, int dtype, nbp_stream_t s);
 /* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s);

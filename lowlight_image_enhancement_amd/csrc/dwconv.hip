@@ -571,14 +571,14 @@ __device__ __forceinline__ void unpack16(uint4 r, float* f) {
 // REC (with FUSED): t2 is not read from HBM either - the forward never stored it.  t1 is staged with a two-pixel
 // halo, t2 = bias + conv(t1) is recomputed into LDS on the one-pixel halo (the forward's FMA order), and the SCA /
 // SimpleGate backward turns it into dt2 in place.  Shorter tiles (TH 12) keep two blocks per CU.
-template <typename T, bool FUSED, int DWT_TW, bool REC, int THS = DWT_TH>
+template <typename T, bool FUSED, int DWT_TW, bool REC>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
   constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
   constexpr int HS = CSL / 2;            // gate channels per slice
   constexpr int NQ = CSL / 4;            // channel quads per slice
   constexpr int NT = NQ * DWT_TW;        // threads
-  constexpr int TH = REC ? DWT_TH_REC : THS;
+  constexpr int TH = REC ? DWT_TH_REC : DWT_TH;
   constexpr int XO = REC ? 1 : 0;        // extra t1 halo
   constexpr int LW = DWT_TW + 2, LH = TH + 2;
   constexpr int LWX = LW + 2 * XO, LHX = LH + 2 * XO;
@@ -736,9 +736,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   }
   // this thread's dt1 column: one 64-bit base; row r at + r * rs1 (a scalar product: r is unrolled, rs1 uniform)
   T* dtp = reinterpret_cast<T*>(p.dt1) + (img + (long)y0 * W + x0 + x) * C2 + gc;
-  const bool col_ok = x0 + x < W;
-#pragma unroll
-  for (int r = 0; r < TH; ++r) {
+  auto one_row = [&](int r, bool store) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -765,7 +763,19 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       }
     ab[0] += gw[1][1][0];
     ab[1] += gw[1][1][1];
-    if (col_ok && y0 + r < H) stq(dtp + (unsigned)r * rs1, make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y));
+    if (store) stq(dtp + (unsigned)r * rs1, make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y));
+  };
+  // Interior tiles (every tile at the power-of-two levels) run branch-free: with the store under a per-row lane
+  // predicate the compiler sank each row's dt1 chain into the predicated block, serialising its two FMA chains with
+  // a hazard s_nop between dependent v_pk_fma_f32 -- a uniform split keeps the chains interleaved with the
+  // weight-gradient FMAs (same FMA order per value: bitwise unchanged).
+  if (y0 + TH <= H && x0 + DWT_TW <= W) {
+#pragma unroll
+    for (int r = 0; r < TH; ++r) one_row(r, true);
+  } else {
+    const bool col_ok = x0 + x < W;
+#pragma unroll
+    for (int r = 0; r < TH; ++r) one_row(r, col_ok && y0 + r < H);
   }
   // ---- reduce the 40 partials over the tile's columns: lanes of one quad differ in bits >= log2(NQ)
   float v[40];
@@ -886,9 +896,7 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   T* t2p = p.t2 ? reinterpret_cast<T*>(p.t2) + m0 * C2 : nullptr;
   T* gp = reinterpret_cast<T*>(p.g) + m0 * C;
   float4 pacc = f4(0.f);
-  const bool col_ok = x0 + x < W;
-#pragma unroll
-  for (int r = 0; r < TH; ++r) {
+  auto one_row = [&](int r, bool store, bool st2) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -911,8 +919,8 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
       }
     const float4 aa = make_float4(a2[0].x, a2[0].y, a2[1].x, a2[1].y);
     const float4 ab = make_float4(b2[0].x, b2[0].y, b2[1].x, b2[1].y);
-    if (col_ok && y0 + r < H) {
-      if (t2p) {  // null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
+    if (store) {
+      if (st2) {  // t2p null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
         T* q2 = t2p + (unsigned)r * rs1;
         stq(q2 + gca, aa);
         stq(q2 + gcb, ab);
@@ -924,6 +932,15 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
       stq(gp + (unsigned)r * rsg + gca, gv);
       pacc += gv;
     }
+  };
+  // interior tiles branch-free (see dw_bwd_tiled: a per-row lane predicate serialised each row's FMA chains)
+  if (y0 + TH <= H && x0 + TW <= W && t2p) {
+#pragma unroll
+    for (int r = 0; r < TH; ++r) one_row(r, true, true);
+  } else {
+    const bool col_ok = x0 + x < W;
+#pragma unroll
+    for (int r = 0; r < TH; ++r) one_row(r, col_ok && y0 + r < H, t2p != nullptr);
   }
   // reduce pacc over the tile's columns (lanes of one gate quad differ in bits >= log2(NQG)), then across waves
 #pragma unroll
@@ -945,17 +962,9 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   }
 }
 
-// backward tile height: 16 rows; NBP_DW_BWD_TH=8 selects 8 at W <= 32 (measured neutral in the step: the shorter
-// row chain is offset by the doubled weight-gradient slab)
-// NBP_DW_BWD_TH_BIG=8: 8-row tiles at W > 32 too (43.5 KB of LDS instead of 78: three workgroups per CU; A/B knob)
-inline int dw_bwd_th(int W) {
-  static const int small = getenv("NBP_DW_BWD_TH") ? atoi(getenv("NBP_DW_BWD_TH")) : 16;
-  static const int big = getenv("NBP_DW_BWD_TH_BIG") ? atoi(getenv("NBP_DW_BWD_TH_BIG")) : 16;
-  if (W > 32) return big == 8 ? 8 : DWT_TH;
-  return small == 8 ? 8 : DWT_TH;  // the instantiated heights
-}
+// backward tile height: 16 rows (8-row tiles were measured neutral at W <= 32 and at every width: DESIGN §5)
 int dw_tiles(int H, int W, bool rec = false) {
-  return cdiv(H, rec ? DWT_TH_REC : dw_bwd_th(W)) * cdiv(W, dw_bwd_tw(W));
+  return cdiv(H, rec ? DWT_TH_REC : DWT_TH) * cdiv(W, dw_bwd_tw(W));
 }
 bool dw_tiled_ok(int C, int dtype) { return C % (dtype != 0 ? 16 : 8) == 0; }
 
@@ -1004,17 +1013,10 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   const bool fused = dh != nullptr;
   NBP_DISPATCH_T(dtype, {
     constexpr int NQ = (64 / sizeof(T)) / 4;
-    const bool th8 = !rec && dw_bwd_th(W) == 8;
-    if (tw == 32 && th8) {
-      if (fused) dw_bwd_tiled<T, true, 32, false, 8><<<nblk, NQ * 32, 0, S(s)>>>(p);
-      else dw_bwd_tiled<T, false, 32, false, 8><<<nblk, NQ * 32, 0, S(s)>>>(p);
-    } else if (tw == 32) {
+    if (tw == 32) {
       if (rec) dw_bwd_tiled<T, true, 32, true><<<nblk, NQ * 32, 0, S(s)>>>(p);
       else if (fused) dw_bwd_tiled<T, true, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
       else dw_bwd_tiled<T, false, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
-    } else if (th8) {
-      if (fused) dw_bwd_tiled<T, true, 16, false, 8><<<nblk, NQ * 16, 0, S(s)>>>(p);
-      else dw_bwd_tiled<T, false, 16, false, 8><<<nblk, NQ * 16, 0, S(s)>>>(p);
     } else {
       if (rec) dw_bwd_tiled<T, true, 16, true><<<nblk, NQ * 16, 0, S(s)>>>(p);
       else if (fused) dw_bwd_tiled<T, true, 16, false><<<nblk, NQ * 16, 0, S(s)>>>(p);
@@ -1026,191 +1028,6 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   rc = nbp_reduce_slab(p.slab_w, (int)nrow, 2L * C * 9, dwdw, s);
   if (rc) return rc;
   return nbp_reduce_slab(p.slab_b, (int)nrow, 2L * C, dbdw, s);
-}
-
-// ---------------------------------------------------------------- conv1 -> depthwise 3x3 -> SimpleGate -> pool, fused
-// Levels 0 / 1 (C = 32 / 64, 16-bit): one workgroup per 8 x TW pixel tile holds ALL 2C conv1 channels of the tile and
-// its one-pixel halo in LDS (gate half and partner half in two planes, pixel stride C elements: the depthwise reads of
-// a wave then cover 256 consecutive bytes per 32-lane group, conflict-free).  Phase 1: t1 = n1 . W1^T + b1 on 32x32x16
-// MFMA over the halo frame's pixels in 32-pixel groups (W1 is the A operand held in registers, the pixels the B
-// operand loaded in fragment order: the skinny conv1's MFMA sequence and epilogue, so t1 is bitwise the unfused
-// conv1's at level 0); halo pixels outside the image are the depthwise conv's zero padding.  Phase 2: the tile's t1
-// is stored (the backward reads it) with 16-byte stores from LDS, and the depthwise conv + bias, SimpleGate and the
-// pool partial sums run as in dw_sg_pool_tiled (same FMA order: t2 and g bitwise).  What the fusion removes is the
-// depthwise kernel's re-read of t1 from HBM (2C elements per pixel plus its halo) and one launch per block.
-// Reference: NAFNet_arch.py:60-66 (conv1, conv2, SimpleGate, sca's pool).
-struct C1DwP {
-  const void* n1;    // [M][C]
-  const void* w1;    // [2C][C] (16-bit per-step copy)
-  const float* b1;   // [2C]
-  const float* wdw;  // [2C][9]
-  const float* bdw;  // [2C]
-  void* t1;          // [M][2C]
-  void* t2;          // [M][2C]
-  void* g;           // [M][C]
-  float* pool_slab;  // [B][tiles][C]
-  int B, H, W, tiles_x, tiles;
-};
-constexpr int C1DW_TH = 8;
-inline int c1dw_tw(int C) { return C == 32 ? 32 : 16; }
-
-template <typename T, int C, int TW>
-__global__ __launch_bounds__(256) void c1_dw_sg_pool(C1DwP p) {
-  constexpr int TH = C1DW_TH, C2 = 2 * C, NQG = C / 4, NT_ = NQG * TW;
-  static_assert(NT_ == 256, "one thread per (gate quad, column)");
-  constexpr int LW = TW + 2, LH = TH + 2, NPX = LH * LW;
-  constexpr int NJT = C2 / 32, KS = C / 16;  // conv1 MFMA tiles over the output channels, 16-wide K steps
-  __shared__ __attribute__((aligned(16))) T pa[NPX * C];  // t1 channels 0..C-1 (gate half)
-  __shared__ __attribute__((aligned(16))) T pb[NPX * C];  // t1 channels C..2C-1 (partner half)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int u = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring tiles (shared halo rows of n1) on one XCD
-  const int tile = u % p.tiles, b = u / p.tiles;
-  const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * TW;
-  const int H = p.H, W = p.W;
-  const long img = (long)b * H * W;
-  const T* n1 = reinterpret_cast<const T*>(p.n1);
-  {  // ---- phase 1: conv1 over the halo frame
-    const int r = lane & 31, h = lane >> 5;
-    vec_t<T, 8> w[NJT][KS];
-#pragma unroll
-    for (int t = 0; t < NJT; ++t)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        w[t][ks] = *reinterpret_cast<const vec_t<T, 8>*>(reinterpret_cast<const T*>(p.w1) + (long)(t * 32 + r) * C +
-                                                         ks * 16 + 8 * h);
-    constexpr int NG = (NPX + 31) / 32, NGW = (NG + 3) / 4;  // 32-pixel groups, per wave
-    // every n1 fragment of this wave's groups is loaded before the first MFMA (one memory latency per tile)
-    vec_t<T, 8> af[NGW][KS];
-    bool inbf[NGW];
-#pragma unroll
-    for (int q = 0; q < NGW; ++q) {
-      const int pg = (wave + 4 * q) * 32 + r;
-      const int ly = pg / LW, lx = pg - (pg / LW) * LW;
-      const int gy = y0 - 1 + ly, gx = x0 - 1 + lx;
-      inbf[q] = pg < NPX && gy >= 0 && gy < H && gx >= 0 && gx < W;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) af[q][ks][j] = (T)0.f;
-        if (inbf[q])
-          af[q][ks] = *reinterpret_cast<const vec_t<T, 8>*>(n1 + (img + (long)gy * W + gx) * C + ks * 16 + 8 * h);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NGW; ++q) {
-      const int gi = wave + 4 * q;
-      if (gi >= NG) break;
-      const int pg = gi * 32 + r;
-      const bool inb = inbf[q];
-      const vec_t<T, 8>* a = af[q];
-      floatx16 acc[NJT];
-#pragma unroll
-      for (int t = 0; t < NJT; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-        for (int t = 0; t < NJT; ++t) acc[t] = mfma32x32x16(w[t][ks], a[ks], acc[t]);
-      if (pg < NPX) {
-        // lane (r, h) owns pixel pg, channels t*32 + 8g + 4h + {0..3}
-#pragma unroll
-        for (int t = 0; t < NJT; ++t)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int j0 = t * 32 + 8 * g + 4 * h;
-            vec_t<T, 4> o;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = inb ? (T)(acc[t][4 * g + q] + p.b1[j0 + q]) : (T)0.f;
-            T* dst = (j0 < C ? pa + pg * C + j0 : pb + pg * C + (j0 - C));
-            *reinterpret_cast<vec_t<T, 4>*>(dst) = o;
-          }
-      }
-    }
-  }
-  __syncthreads();
-  {  // ---- phase 2a: the tile's t1 to HBM (16-byte chunks, C / 4 per pixel: gate half then partner half)
-    constexpr int CPP = C / 4, TOT = TH * TW * CPP;
-    T* t1 = reinterpret_cast<T*>(p.t1);
-#pragma unroll
-    for (int it = 0; it < TOT / NT_; ++it) {
-      const int i = tid + it * NT_;
-      const int px = i / CPP, cc = i - px * CPP;
-      const int ty = px / TW, tx = px - ty * TW;
-      if (y0 + ty < H && x0 + tx < W) {
-        const int lp = (ty + 1) * LW + tx + 1;
-        const uint4 v = cc < CPP / 2 ? *reinterpret_cast<const uint4*>(pa + lp * C + cc * 8)
-                                     : *reinterpret_cast<const uint4*>(pb + lp * C + (cc - CPP / 2) * 8);
-        *reinterpret_cast<uint4*>(t1 + (img + (long)(y0 + ty) * W + x0 + tx) * C2 + cc * 8) = v;
-      }
-    }
-  }
-  // ---- phase 2b: depthwise 3x3 + bias, SimpleGate, pool partials (dw_sg_pool_tiled's arithmetic)
-  const int qg = tid % NQG, x = tid / NQG;
-  const int gca = 4 * qg, gcb = C + gca;
-  float wa[4][9], wb[4][9];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      wa[j][t] = p.wdw[(gca + j) * 9 + t];
-      wb[j][t] = p.wdw[(gcb + j) * 9 + t];
-    }
-  const float4 ba = ld4(p.bdw + gca), bb = ld4(p.bdw + gcb);
-  float4 xa[3][3], xb[3][3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    xa[1][j] = ldq(pa + (0 * LW + x + j) * C + gca);
-    xa[2][j] = ldq(pa + (1 * LW + x + j) * C + gca);
-    xb[1][j] = ldq(pb + (0 * LW + x + j) * C + gca);
-    xb[2][j] = ldq(pb + (1 * LW + x + j) * C + gca);
-  }
-  T* t2 = reinterpret_cast<T*>(p.t2);
-  T* g = reinterpret_cast<T*>(p.g);
-  float4 pacc = f4(0.f);
-  const bool col_ok = x0 + x < W;
-#pragma unroll
-  for (int r = 0; r < TH; ++r) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      xa[0][j] = xa[1][j]; xa[1][j] = xa[2][j];
-      xb[0][j] = xb[1][j]; xb[1][j] = xb[2][j];
-      xa[2][j] = ldq(pa + ((r + 2) * LW + x + j) * C + gca);
-      xb[2][j] = ldq(pb + ((r + 2) * LW + x + j) * C + gca);
-    }
-    float4 aa = ba, ab = bb;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const float4 va = xa[t / 3][t % 3], vb = xb[t / 3][t % 3];
-      aa.x = fmaf(wa[0][t], va.x, aa.x); aa.y = fmaf(wa[1][t], va.y, aa.y);
-      aa.z = fmaf(wa[2][t], va.z, aa.z); aa.w = fmaf(wa[3][t], va.w, aa.w);
-      ab.x = fmaf(wb[0][t], vb.x, ab.x); ab.y = fmaf(wb[1][t], vb.y, ab.y);
-      ab.z = fmaf(wb[2][t], vb.z, ab.z); ab.w = fmaf(wb[3][t], vb.w, ab.w);
-    }
-    if (col_ok && y0 + r < H) {
-      const long m = img + (long)(y0 + r) * W + x0 + x;
-      stq(t2 + m * C2 + gca, aa);
-      stq(t2 + m * C2 + gcb, ab);
-      const float4 gv = aa * ab;
-      stq(g + m * C + gca, gv);
-      pacc += gv;
-    }
-  }
-#pragma unroll
-  for (int o = NQG; o < 64; o <<= 1) {
-    pacc.x += __shfl_xor(pacc.x, o, 64); pacc.y += __shfl_xor(pacc.y, o, 64);
-    pacc.z += __shfl_xor(pacc.z, o, 64); pacc.w += __shfl_xor(pacc.w, o, 64);
-  }
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(pa);
-  if (lane < NQG) st4(red + (wave * NQG + lane) * 4, pacc);
-  __syncthreads();
-  if (tid < C) {
-    float sum = 0.f;
-#pragma unroll
-    for (int w2 = 0; w2 < 4; ++w2) sum += red[w2 * C + tid];
-    p.pool_slab[((long)b * p.tiles + tile) * C + tid] = sum;
-  }
 }
 
 }  // namespace
@@ -1263,27 +1080,6 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
   NBP_DISPATCH_T(dtype, dw_sg_pool_fwd<T><<<grid, blk, blk * 4 * sizeof(float), S(s)>>>((const T*)t1, wdw, bdw, (T*)t2,
                                                                                        (T*)g, pool_slab, geo));
   return check_launch("dw_sg_pool_fwd");
-}
-
-int nbp_c1_dw_slab_rows(int H, int W, int C, int dtype) {
-  if (!((C == 32 || C == 64) && (dtype == 1 || dtype == 2) && H > 0 && W > 0)) return 0;
-  return cdiv(H, C1DW_TH) * cdiv(W, c1dw_tw(C));
-}
-
-int nbp_c1_dw_sg_pool_fwd(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
-                          void* t2, void* g, float* pool_slab, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(n1 && w1 && b1 && wdw && bdw && t1 && t2 && g && pool_slab && B > 0 && H > 0 && W > 0,
-              "nbp_c1_dw_sg_pool_fwd: bad args");
-  NBP_REQUIRE((C == 32 || C == 64) && (dtype == 1 || dtype == 2), "nbp_c1_dw_sg_pool_fwd: C in {32, 64}, 16-bit dtype");
-  const int tw = c1dw_tw(C);
-  C1DwP p{n1, w1, b1, wdw, bdw, t1, t2, g, pool_slab, B, H, W, cdiv(W, tw), nbp_c1_dw_slab_rows(H, W, C, dtype)};
-  const long nblk = (long)B * p.tiles;
-  NBP_REQUIRE(nblk < (1L << 31), "nbp_c1_dw_sg_pool_fwd: grid too large");
-  NBP_DISPATCH_16(dtype, T, {
-    if (C == 32) c1_dw_sg_pool<T, 32, 32><<<nblk, 256, 0, S(s)>>>(p);
-    else c1_dw_sg_pool<T, 64, 16><<<nblk, 256, 0, S(s)>>>(p);
-  });
-  return check_launch("c1_dw_sg_pool");
 }
 
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,

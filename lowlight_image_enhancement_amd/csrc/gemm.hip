@@ -306,15 +306,11 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
 // a half-wave hit 64 distinct banks.
 // RM = 64 (NBP_WGRAD_RM=64): 64-row stages -- twice the loads in flight per stage and half the barrier pairs; the
 // MFMA and bias-sum order over the rows is unchanged (bitwise equal to RM = 32)
-// DB: two LDS stage buffers -- the next stage is stored into the other buffer while this one is multiplied, one
-// barrier per stage instead of two (same MFMA / bias-sum order: bitwise equal)
-template <int GMODE, int XMODE, typename H, int RM = 32, bool DB = false>
+template <int GMODE, int XMODE, typename H, int RM = 32>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
-  constexpr int TNW = 64, TKW = 64, LS = 96, NR = RM / 32, NB = DB ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) H Gsb[NB * RM * LS];
-  __shared__ __attribute__((aligned(16))) H Xsb[NB * RM * LS];
-  H* Gs = Gsb;
-  H* Xs = Xsb;
+  constexpr int TNW = 64, TKW = 64, LS = 96, NR = RM / 32;
+  __shared__ __attribute__((aligned(16))) H Gs[RM * LS];
+  __shared__ __attribute__((aligned(16))) H Xs[RM * LS];
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -412,21 +408,10 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
 #pragma unroll 8
         for (int r = 0; r < RM; ++r) bsum += (float)Gs[r * LS + tid];
       }
-      if constexpr (DB) {
-        if (more) {  // the other buffer was last read before the previous stage's barrier
-          H* gn = Gs == Gsb ? Gsb + RM * LS : Gsb;
-          H* xn = Xs == Xsb ? Xsb + RM * LS : Xsb;
-          store_to(gn, xn);
-          Gs = gn;
-          Xs = xn;
-        }
+      __syncthreads();
+      if (more) {
+        store();
         __syncthreads();
-      } else {
-        __syncthreads();
-        if (more) {
-          store();
-          __syncthreads();
-        }
       }
     }
   }
@@ -606,9 +591,8 @@ __device__ __forceinline__ void wgrad_wide_tile(const WgradP& p, int bx, int by,
 // scale of the stage's 128 X columns is DMA'd with the stage (a stage never straddles two images); the bias column
 // sums of G are read back from the panel.  Same MFMA sequence per tile as wgrad_wide_tile (the bias sums are added
 // in another order).
-// WNW = 4 (wgrad_bf16_wide_group8): 256 x 128 output tiles on 8 waves (4 along N x 2 along K, each 64 x 64): the G
-// panel rows are 512 B (2 rows per DMA instruction), 1.33x the MFMA work per staged byte of the 128 x 128 tile and
-// two waves per SIMD.
+// WNW = 4: 256 x 128 output tiles on 8 waves (4 along N x 2 along K, each 64 x 64; the G panel rows are 512 B) --
+// measured slower in the grouped weight gradients, no longer instantiated.
 template <int NS, int XMODE, int WNW = 2>
 constexpr int wide_glds_stage_bytes() { return 64 * 128 * WNW + 64 * 256 + (XMODE == AM_SCALE ? 512 : 0); }
 template <int NS, int WNW = 2>
@@ -851,52 +835,22 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide_glds(WgradP p) {
 // U-Net level's NAFBlocks (conv5's U, conv4, conv3's U with the per-image SCA scale, conv1) are queued while the
 // level's backward runs and launched together, with the M-splits chosen for the whole group (few or no splits when
 // the group alone fills the chip: the slabs shrink and so do their reductions).
-// XCD binning (g.xcd_bins): workgroup b runs on XCD b % 8 (round-robin dispatch), so every problem is given to one
-// XCD bin and its tiles take the ids b = 8 * (xstart + l) + bin: all the workgroups that re-read a problem's G and X
-// row panels (its N/128 x K/128 tiles of one M range run concurrently) share one L2, and each panel comes from HBM
-// once instead of once per XCD.  Pure scheduling: every tile computes exactly what it computed before.
 constexpr int WG_MAX = 24;
 struct WGroup {
   WgradP p[WG_MAX];
   int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
-  int xstart[WG_MAX], cnt[WG_MAX];
-  unsigned char xscale[WG_MAX], xcd[WG_MAX];
-  int n, xcd_bins;
+  unsigned char xscale[WG_MAX];
+  int n;
 };
-// the 8-wave 256 x 128 tiles (every problem's N a multiple of 256; no XCD binning, no register-staged variant)
-template <typename H, int NS>
-__global__ __launch_bounds__(512) void wgrad_bf16_wide_group8(WGroup g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[wide_glds_lds_bytes<NS, 4>()];
-  const int b = blockIdx.x;
-  int i = 0;
-  while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
-  const int l = b - g.start[i];
-  const int gx = g.gx[i], gy = g.gy[i];
-  const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
-  if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS, 4>(g.p[i], bx, by, bz, smem);
-  else wgrad_wide_tile_glds<AM_PLAIN, H, NS, 4>(g.p[i], bx, by, bz, smem);
-}
 
 template <typename H, int NS>
 __global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
   constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS)>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
   const int b = blockIdx.x;
-  int i = 0, l;
-  if (g.xcd_bins) {
-    const int x = b & 7, j = b >> 3;
-    i = -1;
-    for (int q = 0; q < g.n; ++q)
-      if (g.xcd[q] == x && j >= g.xstart[q] && j < g.xstart[q] + g.cnt[q]) {
-        i = q;
-        break;
-      }
-    if (i < 0) return;  // this XCD's bin is shorter than the longest one
-    l = j - g.xstart[i];
-  } else {
-    while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
-    l = b - g.start[i];
-  }
+  int i = 0;
+  while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
+  const int l = b - g.start[i];
   const int gx = g.gx[i], gy = g.gy[i];
   const int bx = l % gx, by = (l / gx) % gy, bz = l / (gx * gy);
   if constexpr (NS == 0) {
@@ -1310,18 +1264,11 @@ long wgroup_target() {
 
 // NBP_WGRAD_RM (read per launch; 64 default or 32): row-stage height of the narrow (N or K <= 64) weight-gradient
 // tiles.  64 measured +0.3 % at cfg2 (1214.0 -> 1217.9 img/s over three A/B pairs, profiles/r02_v6/ab_wgrad_rm.txt),
-// bitwise equal (tests/test_gpu_glds.py::test_narrow_wgrad_stage_height); 128 (49 KB of LDS) -1.5 %
-// (profiles/r02_v6/ab_wgrad_rm128.txt)
+// bitwise equal (tests/test_gpu_glds.py::test_narrow_wgrad_stage_height); 128-row and double-buffered 64-row stages
+// were measured slower and removed
 int wgrad_rm() {
   const char* e = getenv("NBP_WGRAD_RM");
-  return e && atoi(e) == 32 ? 32 : (e && atoi(e) == 128 ? 128 : 64);
-}
-
-// NBP_WGRAD_DB=1 (read per launch; A/B): double-buffered LDS stages for the 64-row narrow weight-gradient tiles
-// (bitwise equal; measured -1 %: 48 KB of LDS per workgroup, profiles/r02_v6/ab_wgrad_db.txt -- off)
-int wgrad_db() {
-  const char* e = getenv("NBP_WGRAD_DB");
-  return e && e[0] == '1';
+  return e && atoi(e) == 32 ? 32 : 64;
 }
 
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
@@ -1332,39 +1279,15 @@ int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged til
   return v >= 2 && v <= 4 ? v : 0;
 }
 
-// NBP_WGROUP_XCD=1: each problem's tiles on one XCD bin (its panels then come from HBM once: measured 815 -> 252 MB
-// per middle-level group, but no faster -- the tile loop is not bandwidth-bound -- and the bin imbalance costs 0.4 %)
-int wgroup_xcd() {
-  static const int v = [] {
-    const char* e = getenv("NBP_WGROUP_XCD");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return v;
-}
-
 // Splits for the whole group: each problem keeps at most its standalone split count (its workspace) and at least
 // 256 rows per split; the group as a whole aims at ~wgroup_target() workgroups.  The reductions queued for the
 // problems' slabs are re-pointed at the chosen split counts.
-// NBP_WGRAD8 (read per launch; A/B measurement): 1 = the 8-wave 256 x 128 tiles for groups whose every N is a
-// multiple of 256 (ring depth 2 or 3 from NBP_WGRAD_GLDS), aiming at NBP_WGROUP_TARGET8 workgroups (default 512)
-int wgrad8() {
-  const char* e = getenv("NBP_WGRAD8");
-  return e ? atoi(e) : 0;
-}
-long wgroup_target8() {
-  const char* e = getenv("NBP_WGROUP_TARGET8");
-  const long t = e ? atol(e) : 512;
-  return t < 1 ? 512L : t;
-}
-
 void wgroup_launch(hipStream_t st) {
   const int ns = wgrad_glds_depth();
-  bool w8 = wgrad8() == 1 && (ns == 2 || ns == 3) && !wgroup_xcd();
-  for (const WgradP& p : g_wqueue) w8 = w8 && p.N % 256 == 0;
-  const int TNB = w8 ? 256 : 128;
+  constexpr int TNB = 128;
   long tiles = 0;
   for (const WgradP& p : g_wqueue) tiles += (long)(p.N / TNB) * (p.K / 128);
-  const long want = ((w8 ? wgroup_target8() : wgroup_target()) + tiles - 1) / (tiles > 0 ? tiles : 1);
+  const long want = (wgroup_target() + tiles - 1) / (tiles > 0 ? tiles : 1);
   for (WgradP& p : g_wqueue) {
     const long s_max = cdiv(p.M, p.chunk);
     long s = want < s_max ? want : s_max;
@@ -1392,35 +1315,8 @@ void wgroup_launch(hipStream_t st) {
       ++g.n;
     }
     g.start[g.n] = blocks;
-    g.xcd_bins = w8 ? 0 : wgroup_xcd();
-    if (g.xcd_bins) {  // longest-processing-time binning of the problems over the 8 XCDs (work = tiles x rows)
-      int order[WG_MAX];
-      long work[8] = {}, load[8] = {};
-      for (int q = 0; q < g.n; ++q) {
-        order[q] = q;
-        g.cnt[q] = g.start[q + 1] - g.start[q];
-      }
-      std::sort(order, order + g.n, [&](int a, int b) {
-        return (long)g.cnt[a] * g.p[a].chunk > (long)g.cnt[b] * g.p[b].chunk;
-      });
-      for (int t = 0; t < g.n; ++t) {
-        const int q = order[t];
-        int x = 0;
-        for (int y = 1; y < 8; ++y)
-          if (work[y] < work[x]) x = y;
-        g.xcd[q] = (unsigned char)x;
-        g.xstart[q] = (int)load[x];
-        load[x] += g.cnt[q];
-        work[x] += (long)g.cnt[q] * g.p[q].chunk;
-      }
-      long mx = 0;
-      for (int x = 0; x < 8; ++x) mx = load[x] > mx ? load[x] : mx;
-      blocks = (int)(8 * mx);
-    }
     NBP_DISPATCH_H(g_wqueue_dtype, {
-      if (w8 && ns == 3) wgrad_bf16_wide_group8<H, 3><<<blocks, 512, 0, st>>>(g);
-      else if (w8) wgrad_bf16_wide_group8<H, 2><<<blocks, 512, 0, st>>>(g);
-      else if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
+      if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
       else if (ns == 3) wgrad_bf16_wide_group<H, 3><<<blocks, 256, 0, st>>>(g);
       else if (ns == 2) wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
       else wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
@@ -1472,16 +1368,8 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
       else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 128)
-        wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 128><<<grid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64 && wgrad_db())
-        wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64, true><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() == 64 && wgrad_db())
-        wgrad_bf16_kernel<AM_PLAIN, 3, H, 64, true><<<grid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 128 == 0 && wgrad_rm() == 128)
-        wgrad_bf16_kernel<AM_PLAIN, 3, H, 128><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() >= 64)
         wgrad_bf16_kernel<AM_PLAIN, 3, H, 64><<<grid, 256, 0, st>>>(p);

@@ -1427,28 +1427,13 @@ long gemm_minblk() {
   return v;
 }
 
-// NBP_CONV_TILE (read per launch; default 4): 256-row tiles for the 3x3 implicit-GEMM convs, bit 0: 256 x 64 on 4
-// waves (4 x 1, 64 x 64 each) when N <= 64, bit 1: 256 x 128 on 8 waves (4 x 2) when N > 64, bit 2: 256 x 256 on 8
-// waves (2 x 4, 128 x 64 each; two-pass epilogue) when N >= 256 and the grid still has >= 256 workgroups.
-// Measured (scripts/conv_micro.py, fp16, bs 8): bit 2 +34-39 % on the 128^2 x 256 and 64^2 x 512 VGG layers
-// (629 -> 842, 659 -> 913 TFLOP/s; bitwise equal: the same MFMA sequence per output element); bit 0 neutral and
-// bit 1 -1.5 % on cfg3 (one 135 KB workgroup per CU and only 1.5x the work per staged byte), so both stay off.
-// NBP_GEMM_MAP (read per launch; A/B measurement, default 0): GemmPB::tile_map for the NAFNet 1x1-conv GEMMs of
-// nbp_gemm_bf16 / nbp_gemm_res_ln / nbp_dgrad_ln_bwd -- each XCD then owns a contiguous run of row tiles, the rows the
-// depthwise tiles of the same images (xcd_remap, image-major) also run on, so a producer's output can be an L2 hit for
-// its consumer on the same XCD
-int gemm_tile_map() {
-  const char* e = getenv("NBP_GEMM_MAP");
-  return e ? atoi(e) : 0;
-}
-
+// NBP_CONV_TILE (read per launch; default 4, 0 = off): 256 x 256 tiles on 8 waves (2 x 4, 128 x 64 each; two-pass
+// epilogue) for the 3x3 implicit-GEMM convs with N >= 256 while the grid still has >= 256 workgroups.  Measured
+// (scripts/conv_micro.py, fp16, bs 8): +34-39 % on the 128^2 x 256 and 64^2 x 512 VGG layers (629 -> 842, 659 -> 913
+// TFLOP/s; bitwise equal: the same MFMA sequence per output element).  The other 256-row shapes (256 x 64, 256 x 128,
+// 32-wide K-tiles) were measured neutral or slower and removed.
 int conv_tile() {
   const char* e = getenv("NBP_CONV_TILE");
-  return e ? atoi(e) : 4;
-}
-// NBP_CONV_NS (read per launch): ring depth of the 32-wide-K 256 x 256 conv tiles (4 or 5)
-int conv_ns() {
-  const char* e = getenv("NBP_CONV_NS");
   return e ? atoi(e) : 4;
 }
 
@@ -1457,34 +1442,13 @@ bool launch_conv_big(const GemmPB& p, hipStream_t st) {
   if constexpr (sizeof(TA) == 2 && AMODE == AM_IM2COL && CMODE != CM_LNBWD && CMODE != CM_CHANDOT &&
                 CMODE != CM_RESLN) {
     const int ns = glds_depth();
-    const int ct = conv_tile();
     if ((ns >= 0 && ns < 2) || p.K <= 32 || p.ldb % 8 || p.cs % 8) return false;
-    if ((ct & 4) && p.N >= 256 && (long)cdiv(p.M, 256) * cdiv(p.N, 256) >= 256) {
+    if ((conv_tile() & 4) && p.N >= 256 && (long)cdiv(p.M, 256) * cdiv(p.N, 256) >= 256) {
       // 256 x 256 tiles on 2 x 4 waves (128 x 64 each): twice the MFMA work per staged byte of the 128 x 128 tile
       const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 256));
-      if (ct & 8) {  // 32-wide K-tiles: 3 (NBP_CONV_NS=4) or 4 (=5) of them in flight instead of one 64-wide
-        if (conv_ns() == 5) gemm_glds_kernel<256, 256, 5, AMODE, CMODE, TC, H, 4, 2, 32><<<grid, 512, 0, st>>>(p);
-        else gemm_glds_kernel<256, 256, 4, AMODE, CMODE, TC, H, 4, 2, 32><<<grid, 512, 0, st>>>(p);
-      } else {
-        gemm_glds_kernel<256, 256, 2, AMODE, CMODE, TC, H, 4, 2><<<grid, 512, 0, st>>>(p);
-      }
+      gemm_glds_kernel<256, 256, 2, AMODE, CMODE, TC, H, 4, 2><<<grid, 512, 0, st>>>(p);
       return true;
     }
-    if ((ct & 16) && p.N > 64 && p.N <= 128 && (long)cdiv(p.M, 256) * cdiv(p.N, 128) >= 256) {
-      // 256 x 128 tiles, 32-wide K-tiles, 3-deep ring, two-pass epilogue: 72 KB, two workgroups per CU
-      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 128));
-      gemm_glds_kernel<256, 128, 3, AMODE, CMODE, TC, H, 2, 4, 32><<<grid, 512, 0, st>>>(p);
-      return true;
-    }
-    if (!(ct & (p.N <= 64 ? 1 : 2)) || (long)cdiv(p.M, 256) * cdiv(p.N, 128) < 256) return false;
-    if (p.N <= 64) {
-      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 64));
-      gemm_glds_kernel<256, 64, 2, AMODE, CMODE, TC, H, 1, 4><<<grid, 256, 0, st>>>(p);
-    } else {
-      const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 128));
-      gemm_glds_kernel<256, 128, 2, AMODE, CMODE, TC, H, 2, 4><<<grid, 512, 0, st>>>(p);
-    }
-    return true;
   }
   return false;
 }

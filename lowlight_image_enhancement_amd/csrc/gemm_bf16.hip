@@ -40,7 +40,6 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   NBP_REQUIRE(c_mode != CM_D2S || N == 4 * cs, "nbp_gemm_bf16: D2S needs N == 4*cs");
   NBP_REQUIRE(a_mode == AM_S2D || lda % 8 == 0, "nbp_gemm_bf16: lda alignment");
   GemmPB p{A, lda, a_scale, rows_per_img, Bw, ldb, C, ldc, M, N, K, gh, gw, cs, bias, R, rscale, pre};
-  p.tile_map = gemm_tile_map();
   hipStream_t st = S(s);
   int rc = NBP_OK;
   bool done = false;
@@ -79,7 +78,6 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
     GemmPB p{A, lda, nullptr, 1, Wt, ldb, dx, N, M, N, K, 0, 0, 0, nullptr, x,
              nullptr, nullptr, lnw, nullptr, nullptr, nullptr, 0.f, reinterpret_cast<const float2*>(stats), dres, ws,
              ws + nb * N};
-    p.tile_map = gemm_tile_map();
     NBP_DISPATCH_H(dtype, {
       if (N == 512) launch<64, 512, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
       else if (N == 256) launch<64, 256, AM_PLAIN, CM_LNBWD, H, H, H>(p, S(s));
@@ -120,7 +118,6 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
     NBP_REQUIRE(N != 512 || (K > 32 && (glds_depth() < 0 || glds_depth() >= 2)), "nbp_gemm_res_ln: N = 512 runs on the LDS-DMA tiles only");
     GemmPB p{A, lda, a_scale, rows_per_img, Bw, ldb, C, N, M, N, K, 0, 0, 0, bias,
              R, rscale, nullptr, lnw, lnb, nout, reinterpret_cast<float2*>(stats), eps};
-    p.tile_map = gemm_tile_map();
     NBP_DISPATCH_H(dtype, {
       if (N == 512 && a_mode == AM_SCALE) launch<64, 512, AM_SCALE, CM_RESLN, H, H, H>(p, S(s));
       else if (N == 512) launch<64, 512, AM_PLAIN, CM_RESLN, H, H, H>(p, S(s));

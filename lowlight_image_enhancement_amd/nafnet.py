@@ -92,21 +92,8 @@ class NAFNet(nn.Module):
         self._init_reference_like()
         self.grad_ready_hook: Optional[Callable[[Stage], None]] = None
         self._keep: Optional[List[torch.Tensor]] = None  # slabs awaiting a deferred gradient reduction
-        # weight gradients on a side stream (joined at each stage flush), NBP_OVERLAP_WGRAD=1.  Off by default:
-        # measured slower on MI355X at cfg2 (803.8 -> 759.6 img/s graph, 808.9 -> 791.8 eager; scripts/ab_overlap.sh)
-        # 2: side stream for the weight gradients and ONE join + reduction flush at the end of the backward (only
-        # when no per-stage hook needs the gradient slices early, i.e. single-GPU)
-        self.overlap_wgrad = int(os.environ.get("NBP_OVERLAP_WGRAD", "0"))
+        # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec)
         self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
-        # levels 0 / 1 (C in {32, 64}, 16-bit): conv1 + depthwise + SimpleGate + pool partials in one launch
-        # (nbp_c1_dw_sg_pool_fwd: t1 is not re-read from HBM by the depthwise pass), NBP_C1DW=1.  Off by default:
-        # measured slower (level 0 157 vs 32 + 93 us, level 1 127 vs 22 + 37 us, scripts/c1dw_micro.py; -2 % step)
-        self.c1dw = os.environ.get("NBP_C1DW", "0") == "1"
-        # the forward of the blocks at h * w <= NBP_SPLIT_HW as two half-batch chains on two streams (0: off, the
-        # default: measured -2.5 to -3 % at cfg2 for 256 / 1024 / 4096, profiles/r02_v6/ab_split_hw.txt -- the
-        # half-size deep-level launches do not overlap into a shorter critical path)
-        self.split_hw = int(os.environ.get("NBP_SPLIT_HW", "0"))
-        self._split_streams: Dict[torch.device, torch.cuda.Stream] = {}
         # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64, 128} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
         self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
         # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
@@ -116,10 +103,6 @@ class NAFNet(nn.Module):
         # the LayerNorm fusions at C = 256 too (64 x 256 tiles): NBP_FUSE_LN256 = 1 (both, default: +1.1 % with the
         # 8-wave LDS-DMA tiles; round 1 with register-staged tiles: fwd -0.4 %, bwd +0.35 %), bwd, fwd or 0
         self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "1")
-        # ... and at C = 512 (the middle level: 64 x 512 tiles, one 144 KB workgroup per CU, 64 workgroups at bs 16):
-        # NBP_FUSE_LN512 = 1 (both), bwd, fwd or 0 (default: measured -7 % / -2 % / -5 % for 1 / fwd / bwd,
-        # profiles/r02_v6/ab_ln512.txt -- 64 workgroups leave 3/4 of the CUs idle for longer than the LN launch costs)
-        self.fuse_ln512 = os.environ.get("NBP_FUSE_LN512", "0")
         # the wide (C >= 128) weight gradients of a whole U-Net level (conv5's U, conv4, conv3's U, conv1 of every
         # NAFBlock of the level) queued during the level's backward and launched as ONE grouped launch at its end,
         # with M-splits chosen for the group (NBP_GROUP_WGRAD=0: one launch per weight gradient)
@@ -134,8 +117,6 @@ class NAFNet(nn.Module):
         # dt (nbp_dgrad_sg_rc_wg) -- NBP_SG_RC_WG=0 leaves them to separate nbp_wgrad_f32 launches
         self.sg_rc_wg = os.environ.get("NBP_SG_RC_WG", "1") != "0"
         self._ln_carry = None
-        self._side_streams: Dict[torch.device, torch.cuda.Stream] = {}
-        self._side_used: Optional[torch.cuda.Stream] = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
         # image_restoration_model.py:255; the trainer adds GradScaler-style dynamic loss scaling for it).
@@ -405,28 +386,21 @@ class NAFNet(nn.Module):
     def _block_fwd(self, P, pre, x, B, h, w, c, tape, next_pre=None):
         """One NAFBlock forward (NAFNet_arch.py:60-80).  At C in {32, 64, 128} (bf16) the LayerNorms run in the epilogue
         of the GEMM producing their input (nbp_gemm_res_ln): norm2 in conv3's, the next block's norm1 (next_pre)
-        in conv5's; that block then takes (n1, st1) from self._ln_carry.
-        Every op is separable by image (per-pixel rows, per-image depthwise / pool / SCA), so at the small deep-level
-        maps (h * w <= NBP_SPLIT_HW) the batch is issued as two half-batch chains on two streams (forked from and
-        joined back into the current stream; captured as two branches of the HIP graph): each half's latency-bound
-        launches overlap the other's.  Same kernels on the same rows: results are bitwise those of one chain."""
+        in conv5's; that block then takes (n1, st1) from self._ln_carry."""
         M = B * h * w
         dev = x.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
         fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and (c in (32, 64, 128) or
-                                                                           (c == 256 and self.fuse_ln256 in ("1", "fwd")) or
-                                                                           (c == 512 and self.fuse_ln512 in ("1", "fwd")))
+                                                                           (c == 256 and self.fuse_ln256 in ("1", "fwd")))
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
         # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec).  Off by default:
         # measured slower at cfg2 (L0 dw backward 138 -> 211 us vs 25 us saved in the forward; profiles/r01_v9)
         rec = self.dw_rec and query("dw_tiled", c, dt) == 1
-        fused_rows = (query("c1_dw_slab_rows", h, w, c, dt) if (self.c1dw and not rec and dt != 0 and
-                                                                  len(self._W) == 3) else 0)
-        chunks = fused_rows or query("dw_fwd_slab_rows", B, h, w, c, dt)
+        chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
         t1, t2, g, pool = E(M, 2 * c), (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
         mean, a = F(B, c), F(B, c)
         y, n2, st2 = E(M, c), E(M, c), F(M, 2)
@@ -438,75 +412,47 @@ class NAFNet(nn.Module):
         carry_next = fuse_ln and next_pre is not None
         nn1, nst1 = (E(M, c), F(M, 2)) if carry_next else (None, None)
         hw = h * w
-
-        def ops(b0, nb):  # the block's launches for images b0 .. b0 + nb - 1
-            r0, r1, m = b0 * hw, (b0 + nb) * hw, nb * hw
-            R = lambda t: None if t is None else t[r0:r1]  # noqa: E731  (pixel rows)
-            I = lambda t: t[b0:b0 + nb]  # noqa: E731  (images)
-            xs = x[b0:b0 + nb]
-            if not have_n1:
-                call("ln_fwd_nhwc", xs, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"),
-                     R(n1), R(st1), m, c, LN_EPS, dt)
-            pl = pool[b0 * chunks * c:(b0 + nb) * chunks * c]
-            if fused_rows:
-                call("c1_dw_sg_pool_fwd", R(n1), self._slice(self._W[1], pre + "conv1.weight"),
-                     self._slice(P, pre + "conv1.bias"), self._slice(P, pre + "conv2.weight"),
-                     self._slice(P, pre + "conv2.bias"), R(t1), R(t2), R(g), pl, nb, h, w, c, dt)
-            else:
-                self._mm(self._W, R(n1), c, AM_PLAIN, None, 1, pre + "conv1.weight", R(t1), 2 * c, CM_PLAIN, m, 2 * c,
-                         c, bias=self._slice(P, pre + "conv1.bias"))
-                call("dw_sg_pool_fwd", R(t1), self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"),
-                     R(t2), R(g), pl, nb, h, w, c, dt)
-            call("sca_fwd", pl, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"),
-                 I(mean), I(a), nb, hw, c)
-            if fuse_ln:
-                call("gemm_res_ln", R(g), c, AM_SCALE, I(a), hw, self._slice(self._W[1], pre + "conv3.weight"), c, R(y),
-                     m, c, c, self._slice(P, pre + "conv3.bias"), xs, self._slice(P, pre + "beta"),
-                     self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), R(n2), R(st2), LN_EPS,
-                     dt)
-            else:
-                self._mm(self._W, R(g), c, AM_SCALE, I(a), hw, pre + "conv3.weight", R(y), c, CM_PLAIN, m, c, c,
-                         bias=self._slice(P, pre + "conv3.bias"), R=xs, rscale=self._slice(P, pre + "beta"))
-                call("ln_fwd_nhwc", R(y), self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"),
-                     R(n2), R(st2), m, c, LN_EPS, dt)
-            if dt != 0:  # SimpleGate in the GEMM epilogue
-                self._mm(self._W, R(n2), c, AM_PLAIN, None, 1, pre + "conv4.weight", R(t4), 2 * c, CM_SG, m, 2 * c, c,
-                         bias=self._slice(P, pre + "conv4.bias"), pre=R(g2))
-            else:
-                self._mm(self._W, R(n2), c, AM_PLAIN, None, 1, pre + "conv4.weight", R(t4), 2 * c, CM_PLAIN, m, 2 * c,
-                         c, bias=self._slice(P, pre + "conv4.bias"))
-                call("sg_fwd", R(t4), R(g2), m, c, 1, dt)
-            if carry_next:
-                call("gemm_res_ln", R(g2), c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c,
-                     R(out), m, c, c, self._slice(P, pre + "conv5.bias"), R(y), self._slice(P, pre + "gamma"),
-                     self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), R(nn1),
-                     R(nst1), LN_EPS, dt)
-            else:
-                self._mm(self._W, R(g2), c, AM_PLAIN, None, 1, pre + "conv5.weight", R(out), c, CM_PLAIN, m, c, c,
-                         bias=self._slice(P, pre + "conv5.bias"), R=R(y), rscale=self._slice(P, pre + "gamma"))
-
-        if self.split_hw and hw <= self.split_hw and B % 2 == 0 and B >= 2:
-            cur = torch.cuda.current_stream(dev)
-            side = self._split_stream(dev)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                ops(B // 2, B // 2)
-            ops(0, B // 2)
-            cur.wait_stream(side)
+        if not have_n1:
+            call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"),
+                 n1, st1, M, c, LN_EPS, dt)
+        self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c,
+                 c, bias=self._slice(P, pre + "conv1.bias"))
+        call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"),
+             t2, g, pool, B, h, w, c, dt)
+        call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"),
+             mean, a, B, hw, c)
+        if fuse_ln:
+            call("gemm_res_ln", g, c, AM_SCALE, a, hw, self._slice(self._W[1], pre + "conv3.weight"), c, y,
+                 M, c, c, self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
+                 self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS,
+                 dt)
         else:
-            ops(0, B)
+            self._mm(self._W, g, c, AM_SCALE, a, hw, pre + "conv3.weight", y, c, CM_PLAIN, M, c, c,
+                     bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
+            call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"),
+                 n2, st2, M, c, LN_EPS, dt)
+        if dt != 0:  # SimpleGate in the GEMM epilogue
+            self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
+                     bias=self._slice(P, pre + "conv4.bias"), pre=g2)
+        else:
+            self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c,
+                     c, bias=self._slice(P, pre + "conv4.bias"))
+            call("sg_fwd", t4, g2, M, c, 1, dt)
+        if carry_next:
+            call("gemm_res_ln", g2, c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c,
+                 out, M, c, c, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"),
+                 self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), nn1,
+                 nst1, LN_EPS, dt)
+        else:
+            self._mm(self._W, g2, c, AM_PLAIN, None, 1, pre + "conv5.weight", out, c, CM_PLAIN, M, c, c,
+                     bias=self._slice(P, pre + "conv5.bias"), R=y, rscale=self._slice(P, pre + "gamma"))
+
         if carry_next:
             self._ln_carry = (out.view(B, h, w, c), nn1, nst1)
         if tape is not None:
             tape.append(("block", pre, (B, h, w, c), dict(x=x, n1=n1, st1=st1, t1=t1, t2=t2, g=g, mean=mean, a=a, y=y,
                                                            n2=n2, st2=st2, t4=t4, g2=g2)))
         return self._ln_carry[0] if self._ln_carry is not None else out.view(B, h, w, c)
-
-    def _split_stream(self, dev) -> torch.cuda.Stream:
-        st = self._split_streams.get(dev)
-        if st is None:
-            st = self._split_streams[dev] = torch.cuda.Stream(dev)
-        return st
 
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
         ho, wo = h // 2, w // 2
@@ -541,27 +487,15 @@ class NAFNet(nn.Module):
             if self._grouping:  # an error inside a grouped level: launch what is queued so the library state is reset
                 self._grouping = False
                 call("wgrad_group", 0)
-            if self._side_used:
-                torch.cuda.current_stream().wait_stream(self._side_used)
-                self._side_used = None
             call("grad_reduce_flush", 1)
             self._keep = None
 
     def _level_grouped(self, c: int) -> bool:
-        return self.dt != 0 and c % 128 == 0 and self.group_wgrad and self.overlap_wgrad in (0, 3)
+        return self.dt != 0 and c % 128 == 0 and self.group_wgrad
 
     def _close_level(self, pending: List[str], hook):
-        """Launch the level's queued weight gradients, then complete its stages (flush + DP hooks) in order.
-        NBP_OVERLAP_WGRAD=3 (single process): the grouped launch runs on the side stream, overlapping the next
-        level's backward; one join + reduction flush at the end of the backward."""
+        """Launch the level's queued weight gradients, then complete its stages (flush + DP hooks) in order."""
         self._grouping = False
-        if self.overlap_wgrad == 3 and hook is None:
-            side = self._side(self.flat.device if self.flat.is_cuda else torch.device("cuda"))
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                call("wgrad_group", 0)
-            self._side_used = side
-            return
         call("wgrad_group", 0)
         for name in pending:
             self._stage_done(name, hook)
@@ -642,21 +576,8 @@ class NAFNet(nn.Module):
             call("add", dx_img, dout, dx_img, dx_img.numel(), 0)
         return dx_img
 
-    def _side(self, dev) -> torch.cuda.Stream:
-        """The wgrad side stream of this device (created lazily)."""
-        st = self._side_streams.get(dev)
-        if st is None:
-            st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
-        return st
-
     def _stage_done(self, name, hook):
-        if self.overlap_wgrad in (2, 3) and hook is None:
-            return  # everything is joined and flushed once at the end of exec_backward
-        # join the wgrad side stream, then the stage's queued gradient reductions run before anyone (the DP
-        # all-reduce hook) reads its slice
-        if self._side_used:
-            torch.cuda.current_stream().wait_stream(self._side_used)
-            self._side_used = None
+        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice
         call("grad_reduce_flush", 0)
         self._keep.clear()
         if hook is not None:
@@ -671,24 +592,13 @@ class NAFNet(nn.Module):
         return t
 
     def _wgrad(self, G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, dtype=None):
-        """Weight gradient.  Off the backward's critical path (its output only feeds the stage's deferred
-        reductions), so with overlap_wgrad it runs on a side stream forked from the current one; the inputs stay
-        referenced until the stage flush, which joins the side stream first."""
+        """Weight gradient (its output only feeds the stage's deferred reductions)."""
         n_ws = query("wgrad_workspace_floats", M, N, K)
         ws = self._ws(n_ws, G.device)
         if self._grouping and self._keep is not None:  # the launch is deferred to the level's end: keep the operands
             self._keep.extend(t for t in (G, X, xscale) if t is not None)
-        if not (self.overlap_wgrad in (1, 2) and self._keep is not None):
-            call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
-                 n_ws, self.dt if dtype is None else dtype)
-            return
-        side = self._side(G.device)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
-                 n_ws, self.dt if dtype is None else dtype)
-        self._keep.extend(t for t in (G, X, xscale) if t is not None)
-        self._side_used = side
+        call("wgrad_f32", G, ldg, gmode, X, ldx, xmode, xscale, rows, M, N, K, gh, gw, csg, csx, dW, db, ws,
+             n_ws, self.dt if dtype is None else dtype)
 
     def _reduce(self, slab, S, L, out):
         call("reduce_slab", slab, S, L, out)
@@ -741,8 +651,7 @@ class NAFNet(nn.Module):
         # conv4 input gradient + norm2 backward + residual
         # LN backward in the dgrad's epilogue (dn never stored): skinny kernel at C 32 / 64, 64 x 128 tiles at 128
         fuse_ln = dt != 0 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
-                               (c == 256 and self.fuse_ln256 in ("1", "bwd")) or
-                               (c == 512 and self.fuse_ln512 in ("1", "bwd")))
+                               (c == 256 and self.fuse_ln256 in ("1", "bwd")))
         dy = E(M, c)
         if not wg_folded:
             self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
