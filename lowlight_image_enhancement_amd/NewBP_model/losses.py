@@ -391,7 +391,7 @@ class PhysicsConsistencyLoss(nn.Module):
         if k.shape[1] != C // groups:  # what F.conv2d rejects
             raise RuntimeError(f"PhysicsConsistencyLoss: conv2d weight {tuple(k.shape)} with groups={groups} does not "
                                f"match {C} input channels")
-        if groups == C:  # depthwise (per-channel, or the broadcast shared kernel)
+        if groups == C and k.shape[0] == C and k.shape[1] == 1:  # depthwise (per-channel, or the broadcast shared one)
             r, full = _ratio_array(expo_ratio, A_raw)
             shared = int(self.K.shape[0] == 1 and C > 1)
             kd = self.K if shared else k

@@ -736,7 +736,9 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   }
   // this thread's dt1 column: one 64-bit base; row r at + r * rs1 (a scalar product: r is unrolled, rs1 uniform)
   T* dtp = reinterpret_cast<T*>(p.dt1) + (img + (long)y0 * W + x0 + x) * C2 + gc;
-  auto one_row = [&](int r, bool store) {
+  const bool col_ok = x0 + x < W;
+#pragma unroll
+  for (int r = 0; r < TH; ++r) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -763,19 +765,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       }
     ab[0] += gw[1][1][0];
     ab[1] += gw[1][1][1];
-    if (store) stq(dtp + (unsigned)r * rs1, make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y));
-  };
-  // Interior tiles (every tile at the power-of-two levels) run branch-free: with the store under a per-row lane
-  // predicate the compiler sank each row's dt1 chain into the predicated block, serialising its two FMA chains with
-  // a hazard s_nop between dependent v_pk_fma_f32 -- a uniform split keeps the chains interleaved with the
-  // weight-gradient FMAs (same FMA order per value: bitwise unchanged).
-  if (y0 + TH <= H && x0 + DWT_TW <= W) {
-#pragma unroll
-    for (int r = 0; r < TH; ++r) one_row(r, true);
-  } else {
-    const bool col_ok = x0 + x < W;
-#pragma unroll
-    for (int r = 0; r < TH; ++r) one_row(r, col_ok && y0 + r < H);
+    if (col_ok && y0 + r < H) stq(dtp + (unsigned)r * rs1, make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y));
   }
   // ---- reduce the 40 partials over the tile's columns: lanes of one quad differ in bits >= log2(NQ)
   float v[40];
@@ -896,7 +886,9 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
   T* t2p = p.t2 ? reinterpret_cast<T*>(p.t2) + m0 * C2 : nullptr;
   T* gp = reinterpret_cast<T*>(p.g) + m0 * C;
   float4 pacc = f4(0.f);
-  auto one_row = [&](int r, bool store, bool st2) {
+  const bool col_ok = x0 + x < W;
+#pragma unroll
+  for (int r = 0; r < TH; ++r) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -919,8 +911,8 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
       }
     const float4 aa = make_float4(a2[0].x, a2[0].y, a2[1].x, a2[1].y);
     const float4 ab = make_float4(b2[0].x, b2[0].y, b2[1].x, b2[1].y);
-    if (store) {
-      if (st2) {  // t2p null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
+    if (col_ok && y0 + r < H) {
+      if (t2p) {  // null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
         T* q2 = t2p + (unsigned)r * rs1;
         stq(q2 + gca, aa);
         stq(q2 + gcb, ab);
@@ -932,15 +924,6 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
       stq(gp + (unsigned)r * rsg + gca, gv);
       pacc += gv;
     }
-  };
-  // interior tiles branch-free (see dw_bwd_tiled: a per-row lane predicate serialised each row's FMA chains)
-  if (y0 + TH <= H && x0 + TW <= W && t2p) {
-#pragma unroll
-    for (int r = 0; r < TH; ++r) one_row(r, true, true);
-  } else {
-    const bool col_ok = x0 + x < W;
-#pragma unroll
-    for (int r = 0; r < TH; ++r) one_row(r, col_ok && y0 + r < H, t2p != nullptr);
   }
   // reduce pacc over the tile's columns (lanes of one gate quad differ in bits >= log2(NQG)), then across waves
 #pragma unroll

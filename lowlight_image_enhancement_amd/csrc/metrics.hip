@@ -165,11 +165,12 @@ __global__ __launch_bounds__(256) void sobel_mag_kernel(const float* __restrict_
 // each sum rounded to fp32 on its own: no contraction), NCHW [N,3,H,W] -> [N,1,H,W]
 __global__ __launch_bounds__(256) void luma_bt601_kernel(const float* __restrict__ x, long HW, long npix,
                                                          float* __restrict__ y) {
+#pragma clang fp contract(off)  // no FMA: torch rounds each product and each sum
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
     const long b = p / HW, q = p - b * HW;
     const float* xb = x + b * 3 * HW + q;
-    const float t = __fadd_rn(__fmul_rn(0.2989f, xb[0]), __fmul_rn(0.5870f, xb[HW]));
-    y[p] = __fadd_rn(t, __fmul_rn(0.1140f, xb[2 * HW]));
+    const float t = 0.2989f * xb[0] + 0.5870f * xb[HW];
+    y[p] = t + 0.1140f * xb[2 * HW];
   }
 }
 
@@ -190,6 +191,7 @@ __device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
 template <bool CUBIC>
 __global__ __launch_bounds__(256) void resize_kernel(const float* __restrict__ x, int Hi, int Wi, int Ho, int Wo,
                                                      long total, float sh, float sw, float* __restrict__ y) {
+#pragma clang fp contract(off)  // torch's CPU loops round every product and sum
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int ow = (int)(e % Wo);
     const long t = e / Wo;

@@ -22,4 +22,5 @@ KARGS=()
 [[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread "${KARGS[@]}"
 [[ $STEPS == *dw* ]] && run dw_time 300 python scripts/dw_time.py
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --quick --steps 20 --warmup 5
+[[ $STEPS == *barrier* ]] && run xcd_barrier 120 build/xcd_barrier_probe
 exit 0

@@ -120,7 +120,7 @@ def _graph_worker(rank, world, port, q, w64=False):
 def test_two_ranks_graph_step_equals_eager_step(w64):
     """The data-parallel HIP-graph step (segments cut at the gradient buckets, bucket all-reduces launched between
     the replays) gives bitwise the parameters, gradients and losses of the eager data-parallel step -- also for the
-    cfg4 scaling model (w64, fp16, the default 25 MB buckets: about 19 segments and all-reduces per step)."""
+    cfg4 scaling model (w64, fp16, the default 25 MB buckets: 17 segments and all-reduces per step)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -133,7 +133,7 @@ def test_two_ranks_graph_step_equals_eager_step(w64):
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, ((p_e, g_e, l_e, _), (p_g, g_g, l_g, nseg)) in res:
-        assert nseg >= (18 if w64 else 3), nseg  # several buckets -> several segments
+        assert nseg >= (15 if w64 else 3), nseg  # several buckets -> several segments
         assert np.array_equal(p_e, p_g), rank
         assert np.array_equal(g_e, g_g), rank
         assert l_e == l_g, rank
