@@ -143,18 +143,32 @@ ENTRIES = {"gemm_bf16": ("gemm16", cost_gemm16), "gemm_res_ln": ("gemm16", cost_
 
 
 def _pmc_traffic(cls):
-    """HBM bytes per launch of a kernel class from the newest committed PMC record (profiles/*pmc_traffic.json,
+    """HBM bytes per launch of a kernel class from the newest committed PMC record (profiles/[*/]*pmc_traffic.json,
     scripts/pmc_pass.sh + scripts/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled)."""
     import glob
     import re
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")),
-                   key=lambda f: [int(t) for t in re.findall(r"\d+", os.path.basename(f))])
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))
+                   + glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc_traffic.json")),
+                   key=lambda f: [int(t) for t in re.findall(r"\d+", os.path.relpath(f, os.path.join(ROOT, "profiles")))])
     if not files:
         return None, None
     rec = json.load(open(files[-1])).get("classes", {}).get(cls)
     if rec is None:
         return None, os.path.relpath(files[-1], ROOT)
     return round(rec["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+
+
+def _class_line(cls, v, steps, peak_tf):
+    """One kernel class of the profiled pass: its launches, average launch, algorithmic bytes / FLOPs per launch and
+    the fraction of the HBM and MFMA roofs they reach, with the PMC traffic per launch when a record holds the class."""
+    ms, fl, by, n = v
+    gbps = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    tfl = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+    traffic, _ = _pmc_traffic(cls)
+    return {"rocprof_kernels": ROCPROF_KERNELS[cls], "ms_per_step": round(ms / steps, 3), "launches_per_step": n // steps,
+            "avg_launch_us": round(ms * 1e3 / max(n, 1), 2), "algorithmic_bytes_per_launch": round(by / max(n, 1)),
+            "GBps": round(gbps, 1), "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4), "TFLOPs": round(tfl, 2),
+            "mfma_frac": round(tfl / peak_tf, 4), "traffic": traffic}
 
 
 def nproc() -> int:
@@ -402,9 +416,7 @@ def main():
                  "avg_launch_us": round(ms * 1e3 / nl, 2), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
                  "algorithmic_flops_per_launch": round(fl / max(nl, 1)), "flop_intensity": round(fl / max(by, 1), 2),
                  "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_tf, 4),
-                 "classes": {k: {"ms_per_step": round(v[0] / args.steps, 3), "launches_per_step": v[3] // args.steps,
-                                 "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1),
-                                 "TFLOPs": round(v[1] / (v[0] * 1e-3) / 1e12, 2)} for k, v in classes.items()}})
+                 "classes": {k: _class_line(k, v, args.steps, peak_tf) for k, v in classes.items()}})
     blk_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in blk_events) / args.steps
     eager_step_ms = sum(e0.elapsed_time(e1) for e0, e1 in step_events) / args.steps
     per_level = {}

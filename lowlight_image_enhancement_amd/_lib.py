@@ -15,7 +15,7 @@ from typing import Dict, List, Tuple
 import torch
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "_lib", "liblowlight_nbp.so")
+LIB_PATH = os.environ.get("NBP_LIB") or os.path.join(PKG, "_lib", "liblowlight_nbp.so")  # NBP_LIB: A/B builds
 HEADER = os.path.join(os.path.dirname(PKG), "include", "nbp.h")
 
 _C_TYPES = {
