@@ -765,6 +765,14 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       }
     ab[0] += gw[1][1][0];
     ab[1] += gw[1][1][1];
+    // the row's dt1 and weight-gradient FMAs are materialised here, in one block: left alone the compiler sinks dt1's
+    // two 9-FMA chains into the store's branch (dependent v_pk_fma_f32 back to back, an s_nop between each pair) and
+    // every row's dW FMAs past the loop (all rows' windows held raw in registers)
+    asm volatile("" : "+v"(acc[0]), "+v"(acc[1]));
+    asm volatile("" : "+v"(aw[0][0]), "+v"(aw[0][1]), "+v"(aw[1][0]), "+v"(aw[1][1]), "+v"(aw[2][0]), "+v"(aw[2][1]),
+                 "+v"(aw[3][0]), "+v"(aw[3][1]), "+v"(aw[4][0]), "+v"(aw[4][1]));
+    asm volatile("" : "+v"(aw[5][0]), "+v"(aw[5][1]), "+v"(aw[6][0]), "+v"(aw[6][1]), "+v"(aw[7][0]), "+v"(aw[7][1]),
+                 "+v"(aw[8][0]), "+v"(aw[8][1]), "+v"(ab[0]), "+v"(ab[1]));
     if (col_ok && y0 + r < H) stq(dtp + (unsigned)r * rs1, make_float4(acc[0].x, acc[0].y, acc[1].x, acc[1].y));
   }
   // ---- reduce the 40 partials over the tile's columns: lanes of one quad differ in bits >= log2(NQ)
@@ -774,17 +782,44 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
     const f2v a0 = t < 9 ? aw[t][0] : ab[0], a1 = t < 9 ? aw[t][1] : ab[1];
     v[4 * t] = a0.x; v[4 * t + 1] = a0.y; v[4 * t + 2] = a1.x; v[4 * t + 3] = a1.y;
   }
-#pragma unroll
-  for (int i = 0; i < 40; ++i)
-#pragma unroll
-    for (int o = NQ; o < 64; o <<= 1) v[i] += __shfl_xor(v[i], o, 64);
-  __syncthreads();  // tiles are dead: reuse sg as the cross-wave buffer
-  float* red = reinterpret_cast<float*>(sg);
   const int lane = tid & 63, wave = tid >> 6;
   constexpr int NW = NT / 64;
-  if (lane < NQ) {
+  float* red = reinterpret_cast<float*>(sg);
+  if constexpr (NQ == 8) {
+    // reduce-scatter over the 8 columns of a wave (lane bits 3..5): each step keeps half of the values and adds the
+    // partner's copy of that half (40 -> 20 -> 10 -> 5 values per lane; 35 shuffles instead of 120).  Every sum is
+    // own + partner over the same pairs as the butterfly, so the totals are bitwise those of the butterfly.
+    float v2[20], v3[10], v4[5];
+    const bool b3 = lane & 8, b4 = lane & 16, b5 = lane & 32;
 #pragma unroll
-    for (int i = 0; i < 40; ++i) red[(wave * NQ + lane) * 40 + i] = v[i];
+    for (int j = 0; j < 20; ++j) {
+      const float snd = b3 ? v[j] : v[j + 20], keep = b3 ? v[j + 20] : v[j];
+      v2[j] = keep + __shfl_xor(snd, 8, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const float snd = b4 ? v2[j] : v2[j + 10], keep = b4 ? v2[j + 10] : v2[j];
+      v3[j] = keep + __shfl_xor(snd, 16, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const float snd = b5 ? v3[j] : v3[j + 5], keep = b5 ? v3[j + 5] : v3[j];
+      v4[j] = keep + __shfl_xor(snd, 32, 64);
+    }
+    __syncthreads();  // tiles are dead: reuse sg as the cross-wave buffer
+    const int e0 = (b3 ? 20 : 0) + (b4 ? 10 : 0) + (b5 ? 5 : 0);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) red[(wave * NQ + (lane & 7)) * 40 + e0 + j] = v4[j];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 40; ++i)
+#pragma unroll
+      for (int o = NQ; o < 64; o <<= 1) v[i] += __shfl_xor(v[i], o, 64);
+    __syncthreads();  // tiles are dead: reuse sg as the cross-wave buffer
+    if (lane < NQ) {
+#pragma unroll
+      for (int i = 0; i < 40; ++i) red[(wave * NQ + lane) * 40 + i] = v[i];
+    }
   }
   __syncthreads();
   const long row = (long)b * p.tiles + tile;
