@@ -667,7 +667,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   }
   if (REC) {
     // t2 on the one-pixel-halo frame into sg: thread = (quad q, column), rows in steps (FMA order of the forward)
-    __syncthreads();
+    lds_barrier();
     const float4 bq = ld4(p.bdw + gc);
     for (int pix = x; pix < LH * LW; pix += DWT_TW) {
       const int row = pix / LW, col = pix % LW;
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
     }
   }
   if (FUSED) {
-    if (REC) __syncthreads();
+    if (REC) lds_barrier();
     // NT is even, so this thread's chunk k = tid & 1 (and its E channels) is the same in every pass: a and ds / HW once
     static_assert(NT % 2 == 0, "chunk parity per thread");
     float ak[E], sk[E];
@@ -716,12 +716,15 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
         const float dg = inside ? fmaf(d[j], ak[j], sk[j]) : 0.f;
         lo[j] = dg * tb[j];
         hi[j] = dg * ta[j];
+        // the fp32 products are what is rounded to the storage type (the SimpleGate convention of every kernel):
+        // left alone the compiler folds some of the mul + convert pairs into one fp16-output v_fma_mix
+        asm volatile("" : "+v"(lo[j]), "+v"(hi[j]));
       }
       st16f(sg + pix * CSL + k * E, lo);
       st16f(sg + pix * CSL + HS + k * E, hi);
     }
   }
-  __syncthreads();
+  lds_barrier();
   // ---- compute: thread = (quad q, column x)
   f2v aw[9][2], ab[2] = {f2v{0.f, 0.f}, f2v{0.f, 0.f}};
 #pragma unroll
@@ -806,7 +809,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       const float snd = b5 ? v3[j] : v3[j + 5], keep = b5 ? v3[j + 5] : v3[j];
       v4[j] = keep + __shfl_xor(snd, 32, 64);
     }
-    __syncthreads();  // tiles are dead: reuse sg as the cross-wave buffer
+    lds_barrier();  // tiles are dead: reuse sg as the cross-wave buffer
     const int e0 = (b3 ? 20 : 0) + (b4 ? 10 : 0) + (b5 ? 5 : 0);
 #pragma unroll
     for (int j = 0; j < 5; ++j) red[(wave * NQ + (lane & 7)) * 40 + e0 + j] = v4[j];
@@ -815,13 +818,13 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
     for (int i = 0; i < 40; ++i)
 #pragma unroll
       for (int o = NQ; o < 64; o <<= 1) v[i] += __shfl_xor(v[i], o, 64);
-    __syncthreads();  // tiles are dead: reuse sg as the cross-wave buffer
+    lds_barrier();  // tiles are dead: reuse sg as the cross-wave buffer
     if (lane < NQ) {
 #pragma unroll
       for (int i = 0; i < 40; ++i) red[(wave * NQ + lane) * 40 + i] = v[i];
     }
   }
-  __syncthreads();
+  lds_barrier();
   const long row = (long)b * p.tiles + tile;
   for (int i = tid; i < NQ * 40; i += NT) {
     const int qq = i / 40, e = i % 40, t = e >> 2, j = e & 3;
@@ -894,7 +897,7 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
       if (i < TOT) *reinterpret_cast<uint4*>(sx + pix * CSL + hh * HS + k * E) = v[it];
     }
   }
-  __syncthreads();
+  lds_barrier();
   const int qg = tid % NQG, x = tid / NQG;
   const int la = 4 * qg, lb = HS + 4 * qg;       // local channels (LDS)
   const int gca = cbase + 4 * qg, gcb = C + gca;  // global conv channels
@@ -966,12 +969,12 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
     pacc.x += __shfl_xor(pacc.x, o, 64); pacc.y += __shfl_xor(pacc.y, o, 64);
     pacc.z += __shfl_xor(pacc.z, o, 64); pacc.w += __shfl_xor(pacc.w, o, 64);
   }
-  __syncthreads();
+  lds_barrier();
   float* red = reinterpret_cast<float*>(sx);
   const int lane = tid & 63, wave = tid >> 6;
   constexpr int NW = (NT + 63) / 64;
   if (lane < NQG) st4(red + (wave * NQG + lane) * 4, pacc);
-  __syncthreads();
+  lds_barrier();
   if (tid < NQG * 4) {
     float sum = 0.f;
 #pragma unroll
@@ -1051,6 +1054,7 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
 }  // namespace
 
 extern "C" {
+
 
 // geometry helper for callers sizing the slabs: returns chunks per image for the forward pool / img_chan_dot
 int nbp_dw_chunks(int B, int H, int W, int C, int which) {

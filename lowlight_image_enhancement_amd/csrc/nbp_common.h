@@ -190,6 +190,14 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// workgroup barrier for LDS hand-offs: waits for this wave's LDS operations only.  __syncthreads' release fence is an
+// s_waitcnt vmcnt(0) as well, which exposes the latency of every global store the wave still has in flight.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 inline hipStream_t S(nbp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -1,5 +1,5 @@
 """Depthwise forward (dw_sg_pool) and fused SCA/SimpleGate/depthwise backward per level at cfg2 (B 16, fp16): GPU time
-per launch (HIP-graph replays) and the algorithmic HBM rate.  python scripts/dw_time.py"""
+per launch (HIP-graph replays) and the algorithmic HBM rate.  python scripts/dw_time.py [B,H,W,C ...]"""
 import os
 import sys
 
@@ -12,7 +12,10 @@ from scripts.gemm_micro_util import timeit  # noqa: E402
 dev = torch.device("cuda:0")
 dt, td = 2, torch.float16
 out = []
-for (B, H, W, C) in [(16, 256, 256, 32), (16, 128, 128, 64), (16, 64, 64, 128), (16, 32, 32, 256)]:
+SHAPES = [(16, 256, 256, 32), (16, 128, 128, 64), (16, 64, 64, 128), (16, 32, 32, 256)]
+if len(sys.argv) > 1:  # extra shapes: B,H,W,C ...
+    SHAPES = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
+for (B, H, W, C) in SHAPES:
     M = B * H * W
     g = torch.Generator(device=dev).manual_seed(0)
     t1, t2 = (torch.randn(M, 2 * C, device=dev, generator=g).to(td) for _ in range(2))
