@@ -279,27 +279,47 @@ __global__ __launch_bounds__(256) void ending_fwd_px(const T* __restrict__ feat,
   }
 }
 
-// ending input gradient on the padded grid (dy is zero off the crop)
+// ending input gradient on the padded grid (dy is zero off the crop).  Weights in LDS as [t][o][CF] rows (broadcast
+// ds_read_b128, not SGPR re-fetches), the lane's CF accumulators as packed channel pairs; per channel the FMAs run in
+// the order t, o of the scalar form.
 template <int CI, int CF, typename T>
 __global__ __launch_bounds__(256) void ending_bwd_x_px(const float* __restrict__ dy, const float* __restrict__ w,
                                                        T* __restrict__ dfeat, Img g) {
+  __shared__ __attribute__((aligned(16))) float wl[9 * CI * CF];  // [t][o][c] = w[o][c][t]
+  for (int i = threadIdx.x; i < 9 * CI * CF; i += blockDim.x) {
+    const int c = i % CF, o = (i / CF) % CI, t = i / (CF * CI);
+    wl[i] = w[(o * CF + c) * 9 + t];
+  }
+  __syncthreads();
   const int row = blockIdx.x, y = row % g.Hp, b = row / g.Hp;
   for (int x = threadIdx.x; x < g.Wp; x += blockDim.x) {
-    float acc[CF];
+    f2v acc[CF / 2];
 #pragma unroll
-    for (int c = 0; c < CF; ++c) acc[c] = 0.f;
-#pragma unroll
+    for (int c = 0; c < CF / 2; ++c) acc[c] = f2v{0.f, 0.f};
+#pragma unroll 1
     for (int t = 0; t < 9; ++t) {
       const int yo = y - (t / 3 - 1), xo = x - (t % 3 - 1);
       if (yo < 0 || yo >= g.H0 || xo < 0 || xo >= g.W0) continue;
 #pragma unroll
       for (int o = 0; o < CI; ++o) {
         const float d = dy[(((long)b * CI + o) * g.H0 + yo) * g.W0 + xo];
+        const f2v dd = f2v{d, d};
+        const float4* wr = reinterpret_cast<const float4*>(wl + (t * CI + o) * CF);
 #pragma unroll
-        for (int c = 0; c < CF; ++c) acc[c] = fmaf(w[(o * CF + c) * 9 + t], d, acc[c]);
+        for (int c4 = 0; c4 < CF / 4; ++c4) {
+          const float4 wq = wr[c4];
+          acc[2 * c4] = __builtin_elementwise_fma(f2v{wq.x, wq.y}, dd, acc[2 * c4]);
+          acc[2 * c4 + 1] = __builtin_elementwise_fma(f2v{wq.z, wq.w}, dd, acc[2 * c4 + 1]);
+        }
       }
     }
-    store_row<T, CF>(dfeat + ((long)row * g.Wp + x) * CF, acc);
+    float a[CF];
+#pragma unroll
+    for (int c = 0; c < CF / 2; ++c) {
+      a[2 * c] = acc[c].x;
+      a[2 * c + 1] = acc[c].y;
+    }
+    store_row<T, CF>(dfeat + ((long)row * g.Wp + x) * CF, a);
   }
 }
 
