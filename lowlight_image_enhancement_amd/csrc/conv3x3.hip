@@ -256,10 +256,9 @@ __global__ __launch_bounds__(256) void ending_fwd_px(const T* __restrict__ feat,
     float acc[CI];
 #pragma unroll
     for (int o = 0; o < CI; ++o) acc[o] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
+    auto tap = [&](int t) {
       const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-      if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) continue;
+      if (yy < 0 || yy >= g.Hp || xx < 0 || xx >= g.Wp) return;
       const T* fp = feat + (((long)b * g.Hp + yy) * g.Wp + xx) * CF;
 #pragma unroll
       for (int c = 0; c < CF; c += 8) {
@@ -270,6 +269,15 @@ __global__ __launch_bounds__(256) void ending_fwd_px(const T* __restrict__ feat,
 #pragma unroll
           for (int o = 0; o < CI; ++o) acc[o] = fmaf(w[(o * CF + c + j) * 9 + t], v[j], acc[o]);
       }
+    };
+    if constexpr (CF >= 64) {
+      // the tap loop stays rolled at 64 channels: unrolled, its 9 x 64 x CI FMAs with their scalar weight loads
+      // outgrow the instruction cache (300 us per launch at w64 against 56 at w32)
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t) tap(t);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) tap(t);
     }
 #pragma unroll
     for (int o = 0; o < CI; ++o) {
