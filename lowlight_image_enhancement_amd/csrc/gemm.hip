@@ -1011,6 +1011,16 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
 }
 
 void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vector<LDesc>& ls = {}) {
+  static const bool log = getenv("NBP_REDUCE_LOG") != nullptr;  // diagnostic: the flush's descriptors to stderr
+  if (log) {
+    long bytes = 0;
+    for (const RDesc& d : ds) bytes += (long)d.S * d.L * 4;
+    for (const LDesc& l : ls) bytes += (long)l.SU * l.N * l.K * 4 + (long)l.SV * l.N * 4;
+    fprintf(stderr, "[reduce] flush: %zu slabs + %zu layer-scale, %.2f MB:", ds.size(), ls.size(), bytes / 1e6);
+    for (const RDesc& d : ds) fprintf(stderr, " %dx%ld", d.S, d.L);
+    for (const LDesc& l : ls) fprintf(stderr, " U%dx%dx%d/V%d", l.SU, l.N, l.K, l.SV);
+    fprintf(stderr, "\n");
+  }
   size_t i = 0, j = 0;
   while (i < ds.size() || j < ls.size()) {
     RBatch rb;
@@ -1161,7 +1171,7 @@ void dispatch_tiles(const GemmP& p, hipStream_t st) {
 
 bool wide_wgrad(int N, int K) { return N % 128 == 0 && K % 128 == 0; }
 
-// split-M count: enough blocks to fill the chip (~2048), >= 256 rows per split, and fp32 slab bytes
+// split-M count: enough blocks to fill the chip (~1024), >= 256 rows per split, and fp32 slab bytes
 // (S * N * K * 4, written once and read once by the reduction) no larger than the operand bytes M * (N + K) * 2.
 int wgrad_splits(int M, int N, int K) {
   if (wide_wgrad(N, K)) {  // 128 x 128 tiles: ~256 workgroups (NBP_WIDE_TARGET), >= 256 rows per split
@@ -1172,8 +1182,11 @@ int wgrad_splits(int M, int N, int K) {
     if (s > maxs) s = maxs;
     return (int)(s > 1024 ? 1024 : s);
   }
+  // ~1024 blocks: at levels 0 / 1 the fp32 slabs of ~2048 blocks (up to 32 MB for a 32 KB gradient, 106 MB per
+  // stage flush at level 1: NBP_REDUCE_LOG) cost more to write and reduce than the extra blocks gain (A/B: 2048 ->
+  // 1024 +0.5 %, 512 +0.2 %, 256 -3.5 %)
   const long tiles = (long)cdiv(N, 64) * cdiv(K, 64);
-  long s = (2048 + tiles - 1) / tiles;
+  long s = (1024 + tiles - 1) / tiles;
   const long maxs = cdiv(M, 256);  // keep >= 256 rows per split
   if (s > maxs) s = maxs;
   const long slab_cap = (long)M * (N + K) / (2L * N * K);
