@@ -1192,7 +1192,7 @@ int wgrad_splits(int M, int N, int K) {
   const long slab_cap = (long)M * (N + K) / (2L * N * K);
   if (s > slab_cap) s = slab_cap;
   if (s < 1) s = 1;
-  if (s > 1024) s = 1024;
+  if (s > 1024) s = 1024;  // (a cap of 512 / 256 splits: -0.4 / -2.9 %)
   return (int)s;
 }
 
