@@ -186,14 +186,12 @@ __global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ pool, 
   extern __shared__ float sm[];  // [NB][C] then [256] partials
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int o = blockIdx.x * 4 + wv, b0 = blockIdx.y * NB, nb = min(NB, B - b0);
+  // the W row: unconditional loads of clamped (in-bounds) indices, entries past C unused by the dot below, so the
+  // loads stay in flight with the chunk-sum loads (a guarded / masked copy waited for them first)
   float w[16];
-  if (o < C) {
+  const long orow = (long)min(o, C - 1) * C;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int i = lane + 64 * j;
-      w[j] = i < C ? wsca[(long)o * C + i] : 0.f;
-    }
-  }
+  for (int j = 0; j < 16; ++j) w[j] = wsca[orow + min(lane + 64 * j, C - 1)];
   stage_chunk_sums(pool, chunks, C, b0, 0, C, nb * C, inv_hw, sm, sm + NB * C);
   __syncthreads();
   if (blockIdx.x == 0)

@@ -43,15 +43,19 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, cons
   const int lane = threadIdx.x & 63, lg = lane % G, nch = C / E;
   const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   const long nwaves = (long)gridDim.x * (blockDim.x / 64);
+  // Loads are branch-free: lanes past the last chunk / rows past M read the last chunk / row (in bounds) and mask the
+  // values to zero afterwards, so both rows' loads are in flight together (a guarded load waits inside its branch).
   bool cv[V];  // this lane's chunk j exists
+  int cc[V];   // its first channel (clamped)
   float wr[V][E], br[V][E];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     cv[j] = j * G + lg < nch;
+    cc[j] = (cv[j] ? j * G + lg : nch - 1) * E;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      wr[j][e] = cv[j] ? w[(j * G + lg) * E + e] : 0.f;
-      br[j][e] = cv[j] ? b[(j * G + lg) * E + e] : 0.f;
+      wr[j][e] = w[cc[j] + e];
+      br[j][e] = b[cc[j] + e];
     }
   }
   for (long r0 = wave_global * 2 * RPW; r0 < M; r0 += nwaves * 2 * RPW) {
@@ -63,20 +67,19 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, cons
     for (int r = 0; r < 2; ++r) {
       row[r] = r0 + r * RPW + lane / G;
       ok[r] = row[r] < M;
+      const long rl = ok[r] ? row[r] : M - 1;
 #pragma unroll
-      for (int j = 0; j < V; ++j) {
-        if (ok[r] && cv[j]) ld_chunk(x + row[r] * C + (j * G + lg) * E, v[r][j]);
-        else
-#pragma unroll
-          for (int e = 0; e < E; ++e) v[r][j][e] = 0.f;
-      }
+      for (int j = 0; j < V; ++j) ld_chunk(x + rl * C + cc[j], v[r][j]);
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int j = 0; j < V; ++j)
 #pragma unroll
-        for (int e = 0; e < E; ++e) s[r] += v[r][j][e];
+        for (int e = 0; e < E; ++e) {
+          v[r][j][e] = ok[r] && cv[j] ? v[r][j][e] : 0.f;
+          s[r] += v[r][j][e];
+        }
     s[0] = group_sum<G>(s[0]);
     s[1] = group_sum<G>(s[1]);
     float q[2] = {0.f, 0.f}, mu[2];
@@ -100,11 +103,13 @@ __global__ __launch_bounds__(256) void ln_fwd_nhwc(const T* __restrict__ x, cons
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         if (!cv[j]) continue;
-        const int c = (j * G + lg) * E;
         float o[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) o[e] = fmaf(wr[j][e], (v[r][j][e] - mu[r]) * inv, br[j][e]);
-        st_chunk(nout + row[r] * C + c, o);
+        for (int e = 0; e < E; ++e) {  // rounded to fp32 before the store conversion (no single-rounding fma_mix)
+          o[e] = fmaf(wr[j][e], (v[r][j][e] - mu[r]) * inv, br[j][e]);
+          asm volatile("" : "+v"(o[e]));
+        }
+        st_chunk(nout + row[r] * C + cc[j], o);
       }
       if (lg == 0) stats[row[r]] = make_float2(mu[r], dd);
     }
@@ -120,43 +125,58 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
                                                    float* __restrict__ slab_w, float* __restrict__ slab_b, long M,
                                                    int C) {
   constexpr int E = 16 / sizeof(T), RPW = 64 / G, CMAX = G * V * E;
+  constexpr bool PRE = V <= 2;  // dres loaded with dn / x (its chunks held raw; wider rows load it at the store)
   __shared__ float red[4][2][CMAX];
   const int lane = threadIdx.x & 63, lg = lane % G, wv = threadIdx.x >> 6, nch = C / E;
   const long wave_global = (long)blockIdx.x * (blockDim.x / 64) + wv;
   const long nwaves = (long)gridDim.x * (blockDim.x / 64);
-  bool cv[V];
-  float aw[V][E], ab[V][E], wr[V][E];
+  const T* rp = dres ? dres : dn;  // branch-free residual loads (ignored without dres)
+  bool cv[V];  // branch-free loads as in ln_fwd_nhwc: clamped chunk / row, values masked
+  int cc[V];
+  float aw[V][E], ab[V][E];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     cv[j] = j * G + lg < nch;
+    cc[j] = (cv[j] ? j * G + lg : nch - 1) * E;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       aw[j][e] = ab[j][e] = 0.f;
-      wr[j][e] = cv[j] ? w[(j * G + lg) * E + e] : 0.f;
     }
   }
   for (long r0 = wave_global * 2 * RPW; r0 < M; r0 += nwaves * 2 * RPW) {
-    long row[2];
+    long row[2], rl[2];
     bool ok[2];
-    float d[2][V][E], yh[2][V][E];
+    float d[2][V][E], yh[2][V][E], wr[V][E];
+    vec_t<T, E> rres[2][PRE ? V : 1];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {  // weights reloaded per row pair (cache hits), issued with the rows: a copy hoisted
+      int ci = cc[j];              // out of the loop waits for them before the first row loads
+      asm volatile("" : "+v"(ci));
+#pragma unroll
+      for (int e = 0; e < E; ++e) wr[j][e] = w[ci + e];  // (unmasked: g is masked below)
+    }
     float2 st[2];
     float sg[2] = {0.f, 0.f}, sgy[2] = {0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       row[r] = r0 + r * RPW + lane / G;
       ok[r] = row[r] < M;
-      st[r] = ok[r] ? stats[row[r]] : make_float2(0.f, 1.f);
+      rl[r] = ok[r] ? row[r] : M - 1;
+      st[r] = stats[rl[r]];
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        const int c = (j * G + lg) * E;
-        if (ok[r] && cv[j]) {
-          ld_chunk(dn + row[r] * C + c, d[r][j]);
-          ld_chunk(x + row[r] * C + c, yh[r][j]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < E; ++e) d[r][j][e] = yh[r][j][e] = 0.f;
-        }
+        ld_chunk(dn + rl[r] * C + cc[j], d[r][j]);
+        ld_chunk(x + rl[r] * C + cc[j], yh[r][j]);
+        if constexpr (PRE) rres[r][j] = *reinterpret_cast<const vec_t<T, E>*>(rp + rl[r] * C + cc[j]);
       }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (!ok[r]) st[r] = make_float2(0.f, 1.f);
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+#pragma unroll
+        for (int e = 0; e < E; ++e) d[r][j][e] = ok[r] && cv[j] ? d[r][j][e] : 0.f;
     }
     const float rinv[2] = {1.f / st[0].y, 1.f / st[1].y};
 #pragma unroll
@@ -167,8 +187,9 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
         for (int e = 0; e < E; ++e) {
           const float y = ok[r] && cv[j] ? (yh[r][j][e] - st[r].x) * rinv[r] : 0.f;
           yh[r][j][e] = y;
-          const float g = d[r][j][e] * wr[j][e];
-          sg[r] += g;
+          const float wm = cv[j] ? wr[j][e] : 0.f;
+          const float g = d[r][j][e] * wm;
+          sg[r] = fmaf(d[r][j][e], wm, sg[r]);  // (the contraction of sg += g the compiler chose, spelt out)
           sgy[r] = fmaf(g, y, sgy[r]);
           aw[j][e] = fmaf(d[r][j][e], y, aw[j][e]);
           ab[j][e] += d[r][j][e];
@@ -185,15 +206,19 @@ __global__ __launch_bounds__(256) void ln_bwd_nhwc(const T* __restrict__ dn, con
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         if (!cv[j]) continue;
-        const int c = (j * G + lg) * E;
         float o[E], rr[E];
-        if (dres) ld_chunk(dres + row[r] * C + c, rr);
+        if constexpr (PRE) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          o[e] = (d[r][j][e] * wr[j][e] - yh[r][j][e] * mgy - mg) * inv;
-          if (dres) o[e] += rr[e];
+          for (int e = 0; e < E; ++e) rr[e] = (float)rres[r][j][e];
+        } else {
+          ld_chunk(rp + row[r] * C + cc[j], rr);
         }
-        st_chunk(dx + row[r] * C + c, o);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {  // the contraction the compiler chose for (g - yhat * mgy - mg) * inv + dres, spelt out
+          const float t = fmaf(-yh[r][j][e], mgy, d[r][j][e] * wr[j][e]) - mg;
+          o[e] = dres ? fmaf(inv, t, rr[e]) : t * inv;
+        }
+        st_chunk(dx + row[r] * C + cc[j], o);
       }
     }
   }
