@@ -215,6 +215,37 @@ __global__ __launch_bounds__(256) void sca_gemv(const float* __restrict__ pool, 
   }
 }
 
+// sum over pixels p = p, p + step, ... < p1 of x[o(p)] * y[o(p)] (HASY) or x[o(p)], in ascending p: 8 pixels' loads
+// issued before their adds (a load per pixel waited for before the next one was issued, and y's inside its branch
+// after x's); the product is rounded before the add as before (no contraction into an fma)
+template <bool HASY, typename T>
+__device__ __forceinline__ void chan_dot_run(const T* __restrict__ x, const T* __restrict__ y, long base, int C, int p,
+                                             int p1, int step, float4& acc) {
+  auto prod = [&](float4 v, float4 w) {
+    float4 r = v * w;
+    asm volatile("" : "+v"(r.x), "+v"(r.y), "+v"(r.z), "+v"(r.w));
+    return r;
+  };
+  for (; p + 7 * step < p1; p += 8 * step) {
+    float4 v[8], w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ldq(x + base + (long)(p + u * step) * C);
+    if constexpr (HASY) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = ldq(y + base + (long)(p + u * step) * C);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = prod(v[u], w[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; p < p1; p += step) {
+    float4 v = ldq(x + base + (long)p * C);
+    if constexpr (HASY) v = prod(v, ldq(y + base + (long)p * C));
+    acc += v;
+  }
+}
+
 // per-image channel reduction: slab[b][chunk][c] = sum_{p in chunk} x[p][c] * (y ? y[p][c] : 1).
 // grid (chunks, B, ceil(C / 64) channel groups of up to 64 channels): each block a pixel chunk x channel group.
 template <typename T>
@@ -228,12 +259,9 @@ __global__ void img_chan_dot(const T* __restrict__ x, const T* __restrict__ y, f
   const int p0 = chunk * geo.chunk_px, p1 = min(HW, p0 + geo.chunk_px);
   float4 acc = f4(0.f);
   if (pl < PPI) {
-    for (int p = p0 + pl; p < p1; p += PPI) {
-      const long o = ((long)b * HW + p) * C + c0 + q * 4;
-      float4 v = ldq(x + o);
-      if (y) v = v * ldq(y + o);
-      acc += v;
-    }
+    const long base = (long)b * HW * C + c0 + q * 4;
+    if (y) chan_dot_run<true>(x, y, base, C, p0 + pl, p1, PPI, acc);
+    else chan_dot_run<false>(x, y, base, C, p0 + pl, p1, PPI, acc);
   }
   st4(red + tid * 4, acc);
   __syncthreads();
