@@ -7,7 +7,14 @@ HybridLoss terms L1 + SSIM + Phys_srgb, global-norm clip 0.01 + AdamW.  One "ste
 MFMA operands, fp32 accumulation / statistics / parameters, dynamic loss scaling): the reference's AMP dtype.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision fp16|bf16|fp32] [--workload cfg2|cfg3|cfg4] [--quick]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...)
+
+N > 1 runs one process per GPU.  Either under a launcher (python -m torch.distributed.run --nproc-per-node N
+--master-addr 127.0.0.1 bench.py --gpus N ...: WORLD_SIZE must equal N, else the bench exits non-zero), or stand-alone
+(`python bench.py --gpus N` with WORLD_SIZE unset): the bench then starts N local ranks itself, torchrun-style
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in each child's environment; the DDP launch
+contract of NAFNet_base/basicsr/train.py:54-63, utils/dist_util.py:28-40), before anything touches the GPU, and exits
+with the first failing rank's status.  Fewer visible GPUs than N is an error (NBP_BENCH_REHEARSE=1 excepted: every
+rank on cuda:0 over gloo, a rehearsal of the N > 1 path on a one-GPU box, tagged in the JSON line).
 
 Rank 0 prints ONE JSON line.
 * `roofline`: the dominant kernel class (by measured time among the classes below), timed live with HIP events on
@@ -66,8 +73,20 @@ MFMA16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA peak
 HBM_PEAK_GBPS = 8000.0
 ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
 ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
-                   "wgrad": ["wgrad_bf16_kernel", "wgrad_bf16_wide", "wgrad_f32_kernel"],
-                   "dw_bwd": ["dw_bwd_tiled"], "dw_fwd": ["dw_sg_pool_tiled"]}
+                   "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel"], "wgrad_group": ["wgrad_bf16_wide_group"],
+                   "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
+                   "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32, false>"],
+                   "dw_fwd": ["dw_sg_pool_tiled"]}
+# classes that are ONE kernel (one template instance in the step): the headline `roofline` is the one of them with the
+# most time per step (the dominant kernel); the multi-kernel classes are reported beside it
+SINGLE_KERNEL = ("dw_bwd_32", "wgrad_group", "reduce")
+UNIT_DEF = {
+    "dw_bwd_32": "SURVEY §8(d)-style per pixel: dh C + t2 2C + t1 2C read, dt1 2C written = 7*C*s bytes per pixel "
+                 "(s = storage bytes), x B*H*W pixels of the launch (levels 0-3: the 32-wide tile kernel)",
+    "wgrad_group": "per grouped launch: each queued problem's operands read once, M*(N+K)*s, + its fp32 dW (+db) "
+                   "written once; the split-M fp32 slabs the launch writes instead are `slab_bytes_per_step`",
+    "reduce": "per reduce_multi_kernel launch: the fp32 slabs read once + the reduced outputs written once",
+}
 
 
 def nafblock_bytes(net, B, H, W, esize):
@@ -116,9 +135,9 @@ def cost_sg_rc(a):  # (A,lda,Wt,ldb,A2,W2,b2,C,M,N,K,dt): dgrad + the rebuilt co
     return 2.0 * M * N * K + 4.0 * M * N * K, (2 * M * K + 3 * N * K + 2 * M * N) * 2
 
 
-def cost_wgrad(a):  # (G,ldg,gm,X,ldx,xm,xs,rows,M,N,K,gh,gw,csg,csx,dW,db,ws,n_ws,dtype)
+def cost_wgrad(a):  # (G,ldg,gm,X,ldx,xm,xs,rows,M,N,K,gh,gw,csg,csx,dW,db,ws,n_ws,dtype): operands once + fp32 dW/db
     M, N, K = a[8], a[9], a[10]
-    return 2.0 * M * N * K, M * (N + K) * _e(a[-1]) + N * K * 4
+    return 2.0 * M * N * K, M * (N + K) * _e(a[-1]) + N * K * 4 + (N * 4 if a[16] is not None else 0)
 
 
 def cost_dw_bwd(a):  # (dh,a,ds,t2,t1,wdw,dt1,dwdw,dbdw,ws,B,h,w,c,dt): dh C + t2 2C + t1 2C in, dt1 2C out
@@ -136,10 +155,61 @@ def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh
     return 2.0 * M * N * K, 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0))
 
 
-ENTRIES = {"gemm_bf16": ("gemm16", cost_gemm16), "gemm_res_ln": ("gemm16", cost_res_ln),
-           "dgrad_ln_bwd": ("gemm16", cost_dgrad_ln), "dgrad_sg_rc": ("gemm16", cost_sg_rc),
-           "gemm_f32": ("gemm_f32", cost_gemm_f32), "wgrad_f32": ("wgrad", cost_wgrad),
-           "sca_sg_dw_bwd": ("dw_bwd", cost_dw_bwd), "dw_sg_pool_fwd": ("dw_fwd", cost_dw_fwd)}
+def rec_plain(cls, cost):
+    """one C-ABI call = one kernel launch of `cls`"""
+    return lambda a: [(cls, *cost(a), 1, 0.0)]
+
+
+def rec_wgrad(a):
+    """nbp_wgrad_f32: a wide problem inside an open level group is only queued (no GPU work: not a launch of its
+    own; its bytes are counted in the group launch), the others launch one wgrad kernel writing S fp32 slabs."""
+    st = _lib_stats(0)
+    if st[0]:
+        return []
+    fl, by = cost_wgrad(a)
+    return [("wgrad_narrow", fl, by, 1, st[2])]
+
+
+def rec_wgroup(a):
+    """nbp_wgrad_group(0): the level's grouped launch(es): operands read once + fp32 dW / db written once per problem
+    (algorithmic); the fp32 split-M slabs the launch writes instead are reported as slab bytes (the reduce class
+    reads them back)."""
+    if a[0]:
+        return []
+    st = _lib_stats(2)
+    if not st[5]:
+        return []
+    return [("wgrad_group", st[1], st[2] + st[3], int(st[5]), st[4])]
+
+
+def rec_flush(a):
+    """nbp_grad_reduce_flush: the stage's deferred slab reductions (+ layer-scale post-ops): fp32 slabs read once,
+    outputs written once, per reduce_multi_kernel launch."""
+    st = _lib_stats(1)
+    if not st[3]:
+        return []
+    return [("reduce", 0.0, st[1] + st[2], int(st[3]), 0.0)]
+
+
+def rec_dw_bwd(a):
+    fl, by = cost_dw_bwd(a)
+    out = [("dw_bwd", fl, by, 1, 0.0)]
+    if a[12] >= 32:  # dw_bwd_tw(W): the 32-wide tile kernel dw_bwd_tiled<T, true, 32, false>
+        out.append(("dw_bwd_32", fl, by, 1, 0.0))
+    return out
+
+
+def _lib_stats(which):
+    from lowlight_image_enhancement_amd import _lib
+    return _lib.last_call_stats(which)
+
+
+# C-ABI entry -> records [(class, FLOPs, algorithmic bytes, kernel launches, fp32 slab bytes written)]
+ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_plain("gemm16", cost_res_ln),
+           "dgrad_ln_bwd": rec_plain("gemm16", cost_dgrad_ln), "dgrad_sg_rc": rec_plain("gemm16", cost_sg_rc),
+           "gemm_f32": rec_plain("gemm_f32", cost_gemm_f32), "wgrad_f32": rec_wgrad, "wgrad_group": rec_wgroup,
+           "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_dw_bwd,
+           "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd)}
 
 
 def _pmc_traffic(cls):
@@ -159,16 +229,26 @@ def _pmc_traffic(cls):
 
 
 def _class_line(cls, v, steps, peak_tf):
-    """One kernel class of the profiled pass: its launches, average launch, algorithmic bytes / FLOPs per launch and
-    the fraction of the HBM and MFMA roofs they reach, with the PMC traffic per launch when a record holds the class."""
-    ms, fl, by, n = v
+    """One kernel class of the profiled pass, per KERNEL launch (the unit of the PMC traffic record) and per step:
+    launches, average launch, algorithmic bytes / FLOPs, the fraction of the HBM and MFMA roofs they reach, the PMC
+    traffic and its ratio to the algorithmic bytes, and the fp32 split-M slab bytes the class writes (read back by
+    the `reduce` class)."""
+    ms, fl, by, nl, ncall, slab = v
     gbps = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     tfl = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     traffic, _ = _pmc_traffic(cls)
-    return {"rocprof_kernels": ROCPROF_KERNELS[cls], "ms_per_step": round(ms / steps, 3), "launches_per_step": n // steps,
-            "avg_launch_us": round(ms * 1e3 / max(n, 1), 2), "algorithmic_bytes_per_launch": round(by / max(n, 1)),
+    alg = by / max(nl, 1)
+    line = {"rocprof_kernels": ROCPROF_KERNELS[cls], "ms_per_step": round(ms / steps, 3),
+            "launches_per_step": round(nl / steps, 2), "c_abi_calls_per_step": round(ncall / steps, 2),
+            "avg_launch_us": round(ms * 1e3 / max(nl, 1), 2), "algorithmic_bytes_per_launch": round(alg),
+            "algorithmic_bytes_per_step": round(by / steps), "algorithmic_flops_per_launch": round(fl / max(nl, 1)),
             "GBps": round(gbps, 1), "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4), "TFLOPs": round(tfl, 2),
-            "mfma_frac": round(tfl / peak_tf, 4), "traffic": traffic}
+            "mfma_frac": round(tfl / peak_tf, 4), "traffic": traffic,
+            "traffic_per_step": None if traffic is None else round(traffic * nl / steps),
+            "traffic_over_algorithmic": None if traffic is None or alg <= 0 else round(traffic / alg, 3)}
+    if slab:
+        line["slab_bytes_per_step"] = round(slab / steps)
+    return line
 
 
 def nproc() -> int:
@@ -281,9 +361,68 @@ def short_run(dev, workload, precision, steps=5, warmup=3):
     return out
 
 
+def plan_launch(gpus, env, device_count, rehearse):
+    """How this invocation runs, from `--gpus` (None = not given) and the launcher environment:
+    ("run", world) = this process is one rank of `world` (a launcher set WORLD_SIZE, or N = 1);
+    ("spawn", N)   = start N local ranks (WORLD_SIZE unset, N > 1).
+    Raises SystemExit with a message when the request cannot be honoured: WORLD_SIZE != --gpus, N < 1, or fewer
+    visible GPUs than N (unless rehearsing on one GPU)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        world = int(ws)
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks; they must match")
+        return "run", world
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {n}")
+    if not rehearse and device_count < n:
+        raise SystemExit(f"bench.py: --gpus {n} requested but only {device_count} GPU(s) are visible")
+    return ("spawn", n) if n > 1 else ("run", 1)
+
+
+def rank_envs(n, base_env, port):
+    """The environment of each of n local ranks (torchrun's variables; MASTER_ADDR 127.0.0.1)."""
+    envs = []
+    for r in range(n):
+        e = dict(base_env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(n, argv):
+    """Start n copies of this script as local ranks (child processes: no exec, no GPU call in this parent), wait for
+    all, and return the first non-zero exit status (the others are then terminated by PID)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=e)
+             for e in rank_envs(n, os.environ, port)]
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc
+                print(f"[bench] rank {procs.index(p)} exited with status {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs = ranks (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -298,12 +437,15 @@ def main():
     wl = WORKLOADS[args.workload]
     BATCH, IMG = (args.batch or wl["batch"]), wl["img"]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # NBP_BENCH_REHEARSE=1 (one-GPU box only, never the measurement): every rank on cuda:0 over gloo, to exercise the
     # N > 1 path (graph segments + bucket all-reduces, barriers, max-over-ranks timing) where RCCL needs one GPU per rank
     rehearse = os.environ.get("NBP_BENCH_REHEARSE") == "1"
+    # device_count() does not initialise the GPU on this image: the parent of spawned ranks never touches it
+    how, world = plan_launch(args.gpus, os.environ, torch.cuda.device_count(), rehearse)
+    if how == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if rehearse:
         local = 0
     if world > 1:
@@ -328,13 +470,14 @@ def main():
     # algorithmic FLOPs and HBM bytes (operands read once, outputs written once)
     prof = {}
 
-    def mk(cls, cost):
+    def mk(records):
         def cb(a, e0, e1):
-            prof.setdefault(cls, []).append((*cost(a), e0, e1))
+            for cls, fl, by, nl, slab in records(a):
+                prof.setdefault(cls, []).append((fl, by, nl, slab, e0, e1))
         return cb
 
-    for name, (cls, cost) in ENTRIES.items():
-        _lib.PROFILE[name] = mk(cls, cost)
+    for name, records in ENTRIES.items():
+        _lib.PROFILE[name] = mk(records)
     blk_events = []
     orig_fwd, orig_bwd = net._block_fwd, net._block_bwd
 
@@ -396,10 +539,12 @@ def main():
 
     classes = {}
     for cls, recs in prof.items():
-        ms = sum(e0.elapsed_time(e1) for _, _, e0, e1 in recs)
-        classes[cls] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), len(recs))
-    dom = max(classes, key=lambda k: classes[k][0])
-    ms, fl, by, nl = classes[dom]
+        ms = sum(e0.elapsed_time(e1) for *_, e0, e1 in recs)
+        classes[cls] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), sum(r[2] for r in recs), len(recs),
+                        sum(r[3] for r in recs))
+    # the dominant KERNEL: the single-kernel line with the most time per step
+    dom = max((k for k in classes if k in SINGLE_KERNEL), key=lambda k: classes[k][0])
+    ms, fl, by, nl, _, _ = classes[dom]
     peak_tf = FP32_PEAK_TFLOPS if args.precision == "fp32" else MFMA16_PEAK_TFLOPS
     tflops = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     gbps = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -412,8 +557,11 @@ def main():
                 "frac": round(tflops / peak_tf, 4)}
     traffic, tsrc = _pmc_traffic(dom)
     roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel": dom, "rocprof_kernels": ROCPROF_KERNELS[dom],
-                 "launches_per_step": nl // args.steps, "ms_per_step": round(ms / args.steps, 3),
+                 "launches_per_step": round(nl / args.steps, 2), "ms_per_step": round(ms / args.steps, 3),
                  "avg_launch_us": round(ms * 1e3 / nl, 2), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
+                 "algorithmic_bytes_per_step": round(by / args.steps),
+                 "traffic_over_algorithmic": None if traffic is None else round(traffic / max(by / max(nl, 1), 1), 3),
+                 "algorithmic_bytes_definition": UNIT_DEF[dom],
                  "algorithmic_flops_per_launch": round(fl / max(nl, 1)), "flop_intensity": round(fl / max(by, 1), 2),
                  "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_tf, 4),
                  "classes": {k: _class_line(k, v, args.steps, peak_tf) for k, v in classes.items()}})
@@ -481,7 +629,7 @@ def main():
                 res["cfg4"] = dict(short_run(dev, "cfg4", args.precision, steps=5, warmup=3),
                                    workload=WORKLOADS["cfg4"]["desc"], global_batch=WORKLOADS["cfg4"]["batch"],
                                    note="the >= 6.5x scaling config at N = 1 (python bench.py --workload cfg4 "
-                                        "--gpus N times it at N GPUs)")
+                                        "--gpus N starts N local ranks and times it at N GPUs)")
                 if not args.no_cpu_baseline:
                     print("[bench] cpu baseline", file=sys.stderr, flush=True)
                     res["cpu_baseline"] = cpu_baseline(init_sd)

@@ -74,6 +74,11 @@ int nbp_phys_full_fwd(const float* bhat, const float* a, const float* ratio, int
 /* d loss / d bhat = up[0] / (N*Cb*H*W) * (replicate-pad adjoint of conv2d)^T(sign). */
 int nbp_phys_full_bwd(const float* sign_map, const float* k, const float* up, int N, int C, int Co, int Ca, int H, int W,
                       int KH, int KW, float* gx, nbp_stream_t s);
+/* Gradient w.r.t. the short exposure A of either physics L1 (the reference's modules are plain autograd, so A gets one):
+   ga = -up[0] / (N*Cb*H*W) * sum_{cb -> ca} sign_map * ratio * clamp masks (clamp_align: of a*ratio, clamp_a_in: of a),
+   sign_map [N][Cb][H][W] from the forward; Ca == Cb (depthwise losses) or Ca == 1 (broadcast). */
+int nbp_phys_a_bwd(const float* sign_map, const float* a, const float* ratio, int ratio_full, int N, int Ca, int Cb, int H,
+                   int W, int clamp_a_in, int clamp_align, const float* up, float* ga, nbp_stream_t s);
 /* _phys_cons_core (metrics/phys_consistency.py:193-255) for phys_cons_raw (:260) / phys_cons_srgb (:323):
  * full [Co][Ci][KH][KW] PSF (already prepared), pad 0/1/2, ratio_mode 0 [N] / 1 [N,1,H,W] / 2 [N,Co,H,W],
  * crop 'valid' (crop_valid=1) or 'same', clamp01 of the synthesised observation (sRGB), L1 or Charbonnier
@@ -174,6 +179,13 @@ int nbp_grad_reduce_defer(nbp_stream_t s);
 int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const float* b, const float* scale, float* dW,
                          float* db, float* dscale, int N, int K, nbp_stream_t s);
 int nbp_grad_reduce_flush(int stop, nbp_stream_t s);
+/* Measurement record of this thread's last call of a kind (host bookkeeping only, no GPU work; bench.py's per-launch
+ * roofline accounting).  which = 0: the last nbp_wgrad_f32 -> {queued into the open group (1) or
+ * launched (0), M-splits, fp32 slab bytes written, FLOPs 2MNK}; 1: the last nbp_grad_reduce_flush -> {slabs reduced,
+ * slab bytes read, bytes written, reduce_multi_kernel (+ post-op) launches}; 2: the last nbp_wgrad_group(0) -> {problems,
+ * FLOPs, operand bytes read once, fp32 dW / db bytes, fp32 slab bytes written at the group's M-splits, launches}.
+ * Copies min(n, record length) values to out (the rest zero). */
+int nbp_last_call_stats(int which, double* out, int n);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
 /* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC, C any multiple of
@@ -269,17 +281,22 @@ int nbp_pix_loss_fwd(const float* a, const float* b, long n, int mode, float eps
                      float* loss, nbp_stream_t s);
 int nbp_pix_loss_bwd(const float* a, const float* b, long n, int mode, float eps, int clamp_a, int clamp_b,
                      const float* up, float* ga, nbp_stream_t s);
-/* SSIMLoss (losses.py:146-155 -> kornia 0.6.12 ssim_loss, window 11, sigma 1.5, reflect pad). */
+/* SSIMLoss (losses.py:146-155 -> kornia 0.6.12 ssim_loss, window 11, sigma 1.5, reflect pad): the loss map
+ * clamp((1 - ssim) / 2, 0, 1) reduced by `reduction` 0 = 'mean' (loss[0]), 1 = 'sum' (loss[0]) or 2 = 'none' (lmap
+ * [N][C][H][W]; loss may be null).  want_grad keeps the gradient coefficients in ws for nbp_ssim_loss_bwd, which writes
+ * gx = d/dx: scaled by up[0] (mean / sum) or, with up_map (reduction 'none'), by the per-pixel upstream map.  The map
+ * is symmetric in (x, y): d/dy is the same pair of calls with x and y swapped. */
 size_t nbp_ssim_workspace_floats(long n);
 int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W, int window, float max_val,
-                      int clamp_in, int want_grad, float* ws, float* loss, nbp_stream_t s);
+                      int clamp_in, int want_grad, int reduction, float* ws, float* loss, float* lmap, nbp_stream_t s);
 int nbp_ssim_loss_bwd(const float* x, const float* y, int N, int C, int H, int W, int clamp_in, const float* up,
-                      float* ws, float* gx, nbp_stream_t s);
+                      const float* up_map, float* ws, float* gx, nbp_stream_t s);
 
 /* ------------------------------------------------------------------ colour difference (NCHW sRGB [B][3][H][W] fp32) */
 /* DeltaE00Loss (NewBP_model/losses.py:92-143): out[0] = mean over pixels of the loss-form CIEDE2000 between
    rgb_to_lab(clamp01 gen) and rgb_to_lab(clamp01 tgt) (kornia 0.6.12 conversion; clamp = 0 skips the clamps);
-   ws: nbp_de00_workspace_doubles(B*H*W) doubles.  The backward writes dgen = up[0] / (B*H*W) * d dE / d gen. */
+   ws: nbp_de00_workspace_doubles(B*H*W) doubles.  The backward writes dgen = up[0] / (B*H*W) * d dE / d gen; the
+   loss is symmetric in (gen, tgt), so d / d tgt is the backward with the two swapped. */
 size_t nbp_de00_workspace_doubles(long npix);
 int nbp_de00_loss_fwd(const float* gen, const float* tgt, int B, int H, int W, int clamp, float eps, double* ws,
                       float* out, nbp_stream_t s);
@@ -292,6 +309,10 @@ int nbp_de00_metric_map(const float* pred, const float* tgt, int B, int H, int W
    eps), 1 = the metric form (color_error.py:105-210, kL kC kH eps). */
 int nbp_de00_lab(const float* lab1, const float* lab2, int B, int H, int W, int form, float kL, float kC, float kH,
                  float eps, float* out, nbp_stream_t s);
+/* Gradient of the loss form on Lab inputs (DeltaE00Loss._ciede2000's autograd): d1 = g [B][H][W] * d dE / d lab1
+   (forward-mode AD per pixel).  The form is symmetric: d / d lab2 = the same call with lab1 and lab2 swapped. */
+int nbp_de00_lab_bwd(const float* lab1, const float* lab2, int B, int H, int W, float eps, const float* g, float* d1,
+                     nbp_stream_t s);
 /* kornia rgb_to_lab of NCHW sRGB into lab [B][3][H][W]. */
 int nbp_rgb_to_lab(const float* rgb, int B, int H, int W, float* lab, nbp_stream_t s);
 

@@ -75,31 +75,51 @@ def charbonnier_loss(a, b, eps=1e-12):
     return _PixLossFn.apply(a, b, 1, float(eps), False, False)
 
 
+_SSIM_REDUCTION = {"mean": 0, "sum": 1, "none": 2}
+
+
 class _SSIMLossFn(torch.autograd.Function):
+    """kornia 0.6.12 ssim_loss: clamp((1 - ssim(x, y)) / 2, 0, 1) reduced by 'mean' / 'sum' / 'none' (the map).  The
+    map is symmetric in (x, y), so d/dy is the kernel pair with the inputs swapped (a second forward, made only when
+    y needs a gradient)."""
+
     @staticmethod
-    def forward(ctx, x, y, window, max_val, clamp_in):
+    def forward(ctx, x, y, window, max_val, clamp_in, reduction):
         _lib.require_cuda(x, y)
         if x.shape != y.shape or x.dim() != 4:
             raise ValueError("SSIMLoss expects two [N,C,H,W] tensors of the same shape")
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("SSIM gradient w.r.t. the target is not implemented on the MI355X path")
         x, y = x.contiguous(), y.contiguous()
         N, C, H, W = x.shape
-        ws = torch.empty(query("ssim_workspace_floats", x.numel()), device=x.device)
-        loss = torch.empty((), device=x.device)
-        want = ctx.needs_input_grad[0]
-        call("ssim_loss_fwd", x, y, N, C, H, W, window, float(max_val), clamp_in, int(want), ws, loss)
-        ctx.save_for_backward(x, y, ws)
-        ctx.clamp_in = clamp_in
-        return loss
+        red = _SSIM_REDUCTION[reduction]
+        loss = torch.empty((), device=x.device) if red != 2 else None
+        lmap = torch.empty_like(x) if red == 2 else None
+        wsx = wsy = None
+        want_x, want_y = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        wsx = torch.empty(query("ssim_workspace_floats", x.numel()), device=x.device)
+        call("ssim_loss_fwd", x, y, N, C, H, W, window, float(max_val), clamp_in, int(want_x), red, wsx, loss, lmap)
+        if want_y:
+            wsy = torch.empty(query("ssim_workspace_floats", x.numel()), device=x.device)
+            tmp = torch.empty((), device=x.device) if red != 2 else torch.empty_like(x)
+            call("ssim_loss_fwd", y, x, N, C, H, W, window, float(max_val), clamp_in, 1, red, wsy,
+                 tmp if red != 2 else None, tmp if red == 2 else None)
+        ctx.save_for_backward(x, y, wsx, wsy)
+        ctx.clamp_in, ctx.red = clamp_in, red
+        return loss if red != 2 else lmap
 
     @staticmethod
     def backward(ctx, up):
-        x, y, ws = ctx.saved_tensors
+        x, y, wsx, wsy = ctx.saved_tensors
         N, C, H, W = x.shape
-        gx = torch.empty_like(x)
-        call("ssim_loss_bwd", x, y, N, C, H, W, ctx.clamp_in, up.contiguous(), ws, gx)
-        return gx, None, None, None, None
+        up = up.float().contiguous()
+        us, um = (None, up) if ctx.red == 2 else (up.view(1), None)
+        gx = gy = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            call("ssim_loss_bwd", x, y, N, C, H, W, ctx.clamp_in, us, um, wsx, gx)
+        if ctx.needs_input_grad[1]:
+            gy = torch.empty_like(y)
+            call("ssim_loss_bwd", y, x, N, C, H, W, ctx.clamp_in, us, um, wsy, gy)
+        return gx, gy, None, None, None, None
 
 
 def _ratio_array(ratio, ref: torch.Tensor) -> Tuple[torch.Tensor, int]:
@@ -132,29 +152,33 @@ class _PhysL1Fn(torch.autograd.Function):
         _lib.require_cuda(bhat, a, k)
         if bhat.shape != a.shape:
             raise ValueError(f"shape mismatch {tuple(bhat.shape)} vs {tuple(a.shape)}")
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("physics loss gradient w.r.t. the short exposure is not implemented")
         bhat, a = bhat.contiguous(), a.contiguous()
         N, C, H, W = bhat.shape
         kk = k.detach().contiguous()
         ws = torch.empty(query("phys_l1_workspace_doubles", N, C, H, W), dtype=torch.float64, device=bhat.device)
         loss = torch.empty((), device=bhat.device)
-        sign = torch.empty_like(bhat) if ctx.needs_input_grad[0] else None
+        sign = torch.empty_like(bhat) if (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]) else None
         call("phys_l1_fwd", bhat, a, ratio_arr, ratio_full, kk, k_shared, N, C, H, W, kk.shape[-2], kk.shape[-1],
              pad_mode, clamp_bhat, clamp_a_in, clamp_align, ws, loss, sign)
-        ctx.save_for_backward(sign, bhat, kk)
-        ctx.args = (k_shared, pad_mode, clamp_bhat)
+        ctx.save_for_backward(sign, bhat, kk, a, ratio_arr)
+        ctx.args = (k_shared, pad_mode, clamp_bhat, clamp_a_in, clamp_align, ratio_full)
         return loss
 
     @staticmethod
     def backward(ctx, up):
-        sign, bhat, kk = ctx.saved_tensors
-        k_shared, pad_mode, clamp_bhat = ctx.args
+        sign, bhat, kk, a, ratio_arr = ctx.saved_tensors
+        k_shared, pad_mode, clamp_bhat, clamp_a_in, clamp_align, ratio_full = ctx.args
         N, C, H, W = bhat.shape
-        g = torch.empty_like(bhat)
-        call("phys_l1_bwd", sign, bhat, kk, k_shared, up.contiguous(), N, C, H, W, kk.shape[-2], kk.shape[-1],
-             pad_mode, clamp_bhat, g)
-        return g, None, None, None, None, None, None, None, None, None
+        up = up.float().contiguous().view(1)
+        g = ga = None
+        if ctx.needs_input_grad[0]:
+            g = torch.empty_like(bhat)
+            call("phys_l1_bwd", sign, bhat, kk, k_shared, up, N, C, H, W, kk.shape[-2], kk.shape[-1], pad_mode,
+                 clamp_bhat, g)
+        if ctx.needs_input_grad[1]:  # the short exposure's gradient (plain autograd in the reference)
+            ga = torch.empty_like(a)
+            call("phys_a_bwd", sign, a, ratio_arr, ratio_full, N, C, C, H, W, clamp_a_in, clamp_align, up, ga)
+        return g, ga, None, None, None, None, None, None, None, None
 
 
 # ---------------------------------------------------------------- public classes (reference names)
@@ -166,12 +190,10 @@ class _PerceptualFn(torch.autograd.Function):
         _lib.require_cuda(gen, tgt)
         if gen.shape != tgt.shape:
             raise ValueError(f"PerceptualLoss: shape mismatch {tuple(gen.shape)} vs {tuple(tgt.shape)}")
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("PerceptualLoss gradient w.r.t. the target is not implemented on MI355X")
         stack = module.stack(gen.device, dt)
-        want = ctx.needs_input_grad[0]
+        want, want_t = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         with torch.no_grad():
-            ft, _, _ = stack.forward(_vgg.prep_input(tgt.detach(), dtype=stack.dtype), save=False)
+            ft, tape_t, _ = stack.forward(_vgg.prep_input(tgt.detach(), dtype=stack.dtype), save=want_t)
             fg, tape, _ = stack.forward(_vgg.prep_input(gen.detach(), dtype=stack.dtype), save=want)
         n = fg.numel()
         mode = 0 if module.use_mse else 1
@@ -179,21 +201,28 @@ class _PerceptualFn(torch.autograd.Function):
         ws = torch.empty(query("feat_dist_workspace_doubles", n), dtype=torch.float64, device=gen.device)
         out = torch.empty((), device=gen.device)
         call("feat_dist_fwd", fg, ft, n, mode, scale, ws, out, stack.dtype)
-        if want:
-            ctx.tape, ctx.fg, ctx.ft, ctx.stack = tape, fg, ft, stack
+        if want or want_t:
+            ctx.tape, ctx.tape_t, ctx.fg, ctx.ft, ctx.stack = tape, tape_t, fg, ft, stack
             ctx.mode, ctx.scale = mode, scale
-            ctx.save_for_backward(gen.detach())
+            ctx.save_for_backward(gen.detach(), tgt.detach())
         return out
 
     @staticmethod
     def backward(ctx, up):
-        (gen,) = ctx.saved_tensors
-        d = torch.empty_like(ctx.fg)
-        call("feat_dist_bwd", ctx.fg, ctx.ft, ctx.fg.numel(), ctx.mode, float(ctx.scale), 1,
-             up.float().contiguous().view(1), d, ctx.stack.dtype)
-        d8 = ctx.stack.backward(ctx.tape, d)
-        ctx.tape = ctx.fg = ctx.ft = None
-        return _vgg.input_grad(d8, gen), None, None, None
+        gen, tgt = ctx.saved_tensors
+        up = up.float().contiguous().view(1)
+        n = ctx.fg.numel()
+        dg = dt_ = None
+        if ctx.needs_input_grad[0]:
+            d = torch.empty_like(ctx.fg)
+            call("feat_dist_bwd", ctx.fg, ctx.ft, n, ctx.mode, float(ctx.scale), 1, up, d, ctx.stack.dtype)
+            dg = _vgg.input_grad(ctx.stack.backward(ctx.tape, d), gen)
+        if ctx.needs_input_grad[1]:  # MSE / L1 are symmetric: the distance gradient with the features swapped
+            d = torch.empty_like(ctx.ft)
+            call("feat_dist_bwd", ctx.ft, ctx.fg, n, ctx.mode, float(ctx.scale), 1, up, d, ctx.stack.dtype)
+            dt_ = _vgg.input_grad(ctx.stack.backward(ctx.tape_t, d), tgt)
+        ctx.tape = ctx.tape_t = ctx.fg = ctx.ft = None
+        return dg, dt_, None, None
 
 
 class PerceptualLoss(nn.Module):
@@ -276,8 +305,6 @@ class _DeltaE00Fn(torch.autograd.Function):
         _lib.require_cuda(gen, tgt)
         if gen.shape != tgt.shape or gen.dim() != 4 or gen.shape[1] != 3:
             raise ValueError("DeltaE00Loss expects two [N,3,H,W] sRGB tensors of the same shape")
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("DeltaE00 gradient w.r.t. the target is not implemented on the MI355X path")
         gen = gen.detach().float().contiguous()
         tgt = tgt.detach().float().contiguous()
         N, _, H, W = gen.shape
@@ -292,9 +319,47 @@ class _DeltaE00Fn(torch.autograd.Function):
     def backward(ctx, up):
         gen, tgt = ctx.saved_tensors
         N, _, H, W = gen.shape
-        g = torch.empty_like(gen)
-        call("de00_loss_bwd", gen, tgt, N, H, W, 1, ctx.eps, up.float().contiguous().view(1), g)
-        return g, None, None
+        up = up.float().contiguous().view(1)
+        g = gt = None
+        if ctx.needs_input_grad[0]:
+            g = torch.empty_like(gen)
+            call("de00_loss_bwd", gen, tgt, N, H, W, 1, ctx.eps, up, g)
+        if ctx.needs_input_grad[1]:  # the loss is symmetric in (gen, tgt): the same kernel with the two swapped
+            gt = torch.empty_like(tgt)
+            call("de00_loss_bwd", tgt, gen, N, H, W, 1, ctx.eps, up, gt)
+        return g, gt, None
+
+
+class _CIEDE2000LabFn(torch.autograd.Function):
+    """DeltaE00Loss._ciede2000 on Lab tensors [N,3,H,W] -> dE [N,H,W] (losses.py:98-136), both gradients by forward-mode
+    AD per pixel (nbp_de00_lab_bwd; the form is symmetric, so d/dLab2 swaps the inputs)."""
+
+    @staticmethod
+    def forward(ctx, lab1, lab2, eps):
+        _lib.require_cuda(lab1, lab2)
+        if lab1.shape != lab2.shape or lab1.dim() != 4 or lab1.shape[1] != 3:
+            raise ValueError("_ciede2000 expects two [N,3,H,W] Lab tensors of the same shape")
+        lab1, lab2 = lab1.detach().contiguous(), lab2.detach().contiguous()
+        N, _, H, W = lab1.shape
+        out = torch.empty(N, H, W, device=lab1.device)
+        call("de00_lab", lab1, lab2, N, H, W, 0, 1.0, 1.0, 1.0, float(eps), out)
+        ctx.save_for_backward(lab1, lab2)
+        ctx.eps = float(eps)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lab1, lab2 = ctx.saved_tensors
+        N, _, H, W = lab1.shape
+        g = g.float().contiguous()
+        d1 = d2 = None
+        if ctx.needs_input_grad[0]:
+            d1 = torch.empty_like(lab1)
+            call("de00_lab_bwd", lab1, lab2, N, H, W, ctx.eps, g, d1)
+        if ctx.needs_input_grad[1]:
+            d2 = torch.empty_like(lab2)
+            call("de00_lab_bwd", lab2, lab1, N, H, W, ctx.eps, g, d2)
+        return d1, d2, None
 
 
 class DeltaE00Loss(nn.Module):
@@ -307,24 +372,31 @@ class DeltaE00Loss(nn.Module):
 
     @staticmethod
     def _ciede2000(Lab1: torch.Tensor, Lab2: torch.Tensor, eps: float = 1e-6) -> torch.Tensor:
-        raise NotImplementedError("the Lab-domain helper is not exposed on the MI355X path; call forward() on sRGB")
+        """losses.py:98-136: the per-pixel loss-form CIEDE2000 of Lab [N,3,H,W] pairs -> [N,H,W] (differentiable in
+        both arguments); one HIP kernel each way (color.hip)."""
+        return _CIEDE2000LabFn.apply(Lab1.float(), Lab2.to(Lab1.device).float(), float(eps))
 
     def forward(self, gen_srgb01, tgt_srgb01):
         return _DeltaE00Fn.apply(gen_srgb01, tgt_srgb01, self.eps)
 
 
 class SSIMLoss(nn.Module):
-    """losses.py:146-155: kornia SSIMLoss(window_size=11, max_val=1) on clamp(0,1) inputs, mean reduction."""
+    """losses.py:146-155: kornia SSIMLoss(window_size=11, max_val=1, reduction) on clamp(0,1) inputs; reduction
+    'mean' / 'sum' -> a scalar, 'none' -> the [N,C,H,W] loss map (kornia 0.6.12 ssim_loss); gradients to both
+    inputs."""
 
     def __init__(self, window_size: int = 11, max_val: float = 1.0, reduction: str = "mean"):
         super().__init__()
-        if window_size != 11 or reduction != "mean":
-            raise NotImplementedError("SSIMLoss on MI355X implements window_size=11, reduction='mean'")
+        if window_size != 11:
+            raise NotImplementedError("SSIMLoss on MI355X implements window_size=11 (the reference's only use)")
+        if reduction not in _SSIM_REDUCTION:
+            raise ValueError(f"Invalid reduction mode: {reduction}")  # kornia's ssim_loss message
         self.window_size = window_size
         self.max_val = max_val
+        self.reduction = reduction
 
     def forward(self, gen_srgb01, tgt_srgb01):
-        return _SSIMLossFn.apply(gen_srgb01, tgt_srgb01, self.window_size, self.max_val, 1)
+        return _SSIMLossFn.apply(gen_srgb01, tgt_srgb01, self.window_size, self.max_val, 1, self.reduction)
 
 
 class _PhysFullFn(torch.autograd.Function):
@@ -334,28 +406,35 @@ class _PhysFullFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, bhat, a, ratio_arr, ratio_full, k, clamp_align):
         _lib.require_cuda(bhat, a, k)
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("physics loss gradient w.r.t. the short exposure is not implemented")
         bhat, a, kk = bhat.contiguous(), a.contiguous(), k.detach().contiguous()
         N, C, H, W = bhat.shape
         Co, Ca = kk.shape[0], a.shape[1]
         Cb = max(Co, Ca)
         ws = torch.empty(query("phys_l1_workspace_doubles", N, Cb, H, W), dtype=torch.float64, device=bhat.device)
         loss = torch.empty((), device=bhat.device)
-        sign = torch.empty(N, Cb, H, W, device=bhat.device) if ctx.needs_input_grad[0] else None
+        want = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        sign = torch.empty(N, Cb, H, W, device=bhat.device) if want else None
         call("phys_full_fwd", bhat, a, ratio_arr, ratio_full, kk, N, C, Co, Ca, H, W, kk.shape[-2], kk.shape[-1],
              clamp_align, ws, loss, sign)
-        ctx.save_for_backward(sign, kk)
+        ctx.save_for_backward(sign, kk, a, ratio_arr)
         ctx.dims = (N, C, Co, Ca, H, W)
+        ctx.args = (clamp_align, ratio_full)
         return loss
 
     @staticmethod
     def backward(ctx, up):
-        sign, kk = ctx.saved_tensors
+        sign, kk, a, ratio_arr = ctx.saved_tensors
         N, C, Co, Ca, H, W = ctx.dims
-        g = torch.empty(N, C, H, W, device=sign.device)
-        call("phys_full_bwd", sign, kk, up.contiguous(), N, C, Co, Ca, H, W, kk.shape[-2], kk.shape[-1], g)
-        return g, None, None, None, None, None
+        clamp_align, ratio_full = ctx.args
+        up = up.float().contiguous().view(1)
+        g = ga = None
+        if ctx.needs_input_grad[0]:
+            g = torch.empty(N, C, H, W, device=sign.device)
+            call("phys_full_bwd", sign, kk, up, N, C, Co, Ca, H, W, kk.shape[-2], kk.shape[-1], g)
+        if ctx.needs_input_grad[1]:
+            ga = torch.empty_like(a)
+            call("phys_a_bwd", sign, a, ratio_arr, ratio_full, N, Ca, max(Co, Ca), H, W, 0, clamp_align, up, ga)
+        return g, ga, None, None, None, None
 
 
 class PhysicsConsistencyLoss(nn.Module):

@@ -146,6 +146,16 @@ def host_call(name: str, *args) -> int:
     return rc
 
 
+def last_call_stats(which: int, n: int = 6) -> List[float]:
+    """nbp_last_call_stats: host-side record of this thread's last nbp_wgrad_f32 (0), nbp_grad_reduce_flush (1) or
+    nbp_wgrad_group end (2) call -- what it queued / launched and its algorithmic bytes (include/nbp.h)."""
+    buf = (ctypes.c_double * n)()
+    rc = lib().dll.nbp_last_call_stats(which, ctypes.cast(buf, ctypes.c_void_p), n)
+    if rc != 0:
+        raise NBPError(f"nbp_last_call_stats failed ({rc}): {lib().dll.nbp_last_error_string().decode()}")
+    return list(buf)
+
+
 def require_cuda(*tensors):
     for t in tensors:
         if t is not None and (not t.is_cuda or t.dtype != torch.float32):

@@ -260,6 +260,24 @@ __global__ __launch_bounds__(256) void de00_lab_kernel(const float* __restrict__
   }
 }
 
+// d/d lab1 of the loss-form CIEDE2000 on Lab inputs (DeltaE00Loss._ciede2000's autograd, losses.py:98-136): dual
+// numbers carry d/d(L1, a1, b1); d1 = g[p] * partials.  The formula is symmetric in its two arguments (every
+// difference enters squared or as the product dC' dH'), so the caller gets d/d lab2 by swapping the inputs.
+__global__ __launch_bounds__(256) void de00_lab_bwd_kernel(const float* __restrict__ lab1, const float* __restrict__ lab2,
+                                                           long HW, long npix, float eps, const float* __restrict__ g,
+                                                           float* __restrict__ d1) {
+  for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+    const long b = p / HW, q = p - b * HW;
+    const long o = b * 3 * HW + q;
+    const D3 L1{lab1[o], 1.f, 0.f, 0.f}, A1{lab1[o + HW], 0.f, 1.f, 0.f}, B1{lab1[o + 2 * HW], 0.f, 0.f, 1.f};
+    const D3 dE = ciede2000_loss(L1, A1, B1, mk(lab2[o]), mk(lab2[o + HW]), mk(lab2[o + 2 * HW]), eps);
+    const float gp = g[p];
+    d1[o] = gp * dE.d0;
+    d1[o + HW] = gp * dE.d1;
+    d1[o + 2 * HW] = gp * dE.d2;
+  }
+}
+
 // Lab of NCHW sRGB (kornia rgb_to_lab), for callers that need the L channel (edge_deltaE2000)
 __global__ __launch_bounds__(256) void rgb_to_lab_kernel(const float* __restrict__ rgb, long HW, long npix,
                                                          float* __restrict__ lab) {
@@ -317,6 +335,14 @@ int nbp_de00_lab(const float* lab1, const float* lab2, int B, int H, int W, int 
   const long HW = (long)H * W, npix = B * HW;
   de00_lab_kernel<<<grid_for(npix), 256, 0, S(s)>>>(lab1, lab2, HW, npix, form, kL, kC, kH, eps, out);
   return check_launch("de00_lab");
+}
+
+int nbp_de00_lab_bwd(const float* lab1, const float* lab2, int B, int H, int W, float eps, const float* g, float* d1,
+                     nbp_stream_t s) {
+  NBP_REQUIRE(lab1 && lab2 && g && d1 && B > 0 && H > 0 && W > 0, "nbp_de00_lab_bwd: bad args");
+  const long HW = (long)H * W, npix = B * HW;
+  de00_lab_bwd_kernel<<<grid_for(npix), 256, 0, S(s)>>>(lab1, lab2, HW, npix, eps, g, d1);
+  return check_launch("de00_lab_bwd");
 }
 
 int nbp_rgb_to_lab(const float* rgb, int B, int H, int W, float* lab, nbp_stream_t s) {

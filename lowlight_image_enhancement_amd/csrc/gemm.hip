@@ -1010,6 +1010,16 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
   }
 }
 
+// Measurement records of the last call of this thread (nbp_last_call_stats; bench.py's per-launch roofline accounting):
+// [0] = slabs + layer-scale rows reduced, [1] = slab bytes read, [2] = bytes written, [3] = reduce_multi_kernel launches
+thread_local double g_stats_flush[4];
+// the last nbp_wgrad_f32 call: [0] = queued into the open group (1) or launched (0), [1] = M-splits, [2] = fp32 slab
+// bytes written (at the standalone splits), [3] = FLOPs 2 M N K
+thread_local double g_stats_wgrad[4];
+// the last group launch: [0] = problems, [1] = FLOPs, [2] = operand bytes read once, [3] = fp32 dW / db bytes,
+// [4] = fp32 slab bytes written at the group's M-splits, [5] = kernel launches
+thread_local double g_stats_group[6];
+
 void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vector<LDesc>& ls = {}) {
   static const bool log = getenv("NBP_REDUCE_LOG") != nullptr;  // diagnostic: the flush's descriptors to stderr
   if (log) {
@@ -1020,6 +1030,14 @@ void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vecto
     for (const RDesc& d : ds) fprintf(stderr, " %dx%ld", d.S, d.L);
     for (const LDesc& l : ls) fprintf(stderr, " U%dx%dx%d/V%d", l.SU, l.N, l.K, l.SV);
     fprintf(stderr, "\n");
+  }
+  {  // measurement record of this flush (nbp_last_call_stats(1, ...))
+    double rd = 0, wr = 0;
+    for (const RDesc& d : ds) rd += (double)d.S * d.L * 4, wr += (double)d.L * 4;
+    for (const LDesc& l : ls) rd += (double)l.SU * l.N * l.K * 4 + (double)l.SV * l.N * 4, wr += (double)l.N * (l.K + 2) * 4;
+    g_stats_flush[0] += (double)(ds.size() + ls.size());
+    g_stats_flush[1] += rd;
+    g_stats_flush[2] += wr;
   }
   size_t i = 0, j = 0;
   while (i < ds.size() || j < ls.size()) {
@@ -1041,6 +1059,7 @@ void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vecto
       rb.l[rb.nl++] = d;
     }
     reduce_multi_kernel<<<(unsigned)(blocks + lblocks), 256, 0, st>>>(rb);
+    g_stats_flush[3] += 1;
   }
 }
 
@@ -1123,6 +1142,7 @@ bool getenv_ls_fuse() {
 }
 
 void flush_pending() {
+  for (double& v : g_stats_flush) v = 0;
   // a post-op whose U and V are both reductions of this flush becomes a layer-scale row descriptor of the same launch
   std::vector<LDesc> ls;
   std::vector<PDesc> post;
@@ -1148,6 +1168,7 @@ void flush_pending() {
   }
   launch_multi(g_pending, g_defer_stream, ls);
   g_pending.clear();
+  if (!post.empty()) g_stats_flush[3] += 1;
   launch_post(post, g_defer_stream);  // post-ops read reduction outputs: after every reduction of the flush
   g_post.clear();
 }
@@ -1296,6 +1317,7 @@ int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged til
 // 256 rows per split; the group as a whole aims at ~wgroup_target() workgroups.  The reductions queued for the
 // problems' slabs are re-pointed at the chosen split counts.
 void wgroup_launch(hipStream_t st) {
+  for (double& v : g_stats_group) v = 0;
   const int ns = wgrad_glds_depth();
   constexpr int TNB = 128;
   long tiles = 0;
@@ -1309,6 +1331,12 @@ void wgroup_launch(hipStream_t st) {
     if (s < 1) s = 1;
     p.chunk = cdiv(cdiv(p.M, (int)s), 64) * 64;
     const int S_ = cdiv(p.M, p.chunk);
+    const int es = g_wqueue_dtype != 0 ? 2 : 4;
+    g_stats_group[0] += 1;
+    g_stats_group[1] += 2.0 * p.M * p.N * p.K;
+    g_stats_group[2] += (double)p.M * (p.N + p.K) * es;
+    g_stats_group[3] += (double)p.N * p.K * 4 + (p.slab_b ? (double)p.N * 4 : 0.0);
+    g_stats_group[4] += (double)S_ * p.N * p.K * 4 + (p.slab_b ? (double)S_ * p.N * 4 : 0.0);
     for (RDesc& d : g_pending)
       if (d.slab == p.slab || (p.slab_b && d.slab == p.slab_b)) d.S = S_, d.ty = make_rdesc(d.slab, S_, d.L, d.out).ty;
   }
@@ -1334,6 +1362,7 @@ void wgroup_launch(hipStream_t st) {
       else if (ns == 2) wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
       else wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
     });
+    g_stats_group[5] += 1;
   }
   g_wqueue.clear();
 }
@@ -1357,6 +1386,10 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
   dim3 grid(cdiv(N, 64), cdiv(K, 64), S_);
   hipStream_t st = S(s);
   bool ok = true;
+  g_stats_wgrad[0] = 0;
+  g_stats_wgrad[1] = S_;
+  g_stats_wgrad[2] = (double)S_ * N * K * 4 + (db ? (double)S_ * N * 4 : 0.0);
+  g_stats_wgrad[3] = 2.0 * M * N * K;
   if (dtype != 0) {
     NBP_REQUIRE(N % 8 == 0 && K % 8 == 0 && (g_mode != AM_S2D || cs_g % 8 == 0) && (x_mode != AM_S2D || cs_x % 8 == 0),
                 "nbp_wgrad_f32(16-bit): N, K and S2D channel counts must be multiples of 8");
@@ -1371,6 +1404,7 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       g_wqueue_dtype = dtype;
       if (x_mode != AM_SCALE) p.x_scale = nullptr;  // the group kernel selects the X mode by x_scale
       g_wqueue.push_back(p);
+      g_stats_wgrad[0] = 1;
     } else NBP_DISPATCH_H(dtype, {
       const int ns = wgrad_glds_depth();
       if (wide && ns == 4 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 4><<<wgrid, 256, 0, st>>>(p);
@@ -1434,6 +1468,7 @@ int nbp_layer_scale_grad(const float* U, const float* V, const float* W, const f
 int nbp_wgrad_group(int begin, nbp_stream_t s) {
   NBP_REQUIRE(begin ? !g_wgroup : g_wgroup, "nbp_wgrad_group: unbalanced begin / end");
   g_wgroup = begin != 0;
+  for (double& v : g_stats_group) v = 0;
   if (!begin) wgroup_launch(S(s));
   return check_launch("wgrad_group");
 }
@@ -1446,8 +1481,17 @@ int nbp_grad_reduce_defer(nbp_stream_t s) {
   return NBP_OK;
 }
 
+int nbp_last_call_stats(int which, double* out, int n) {
+  NBP_REQUIRE(out && n > 0 && which >= 0 && which <= 2, "nbp_last_call_stats: bad args");
+  const double* src = which == 0 ? g_stats_wgrad : which == 1 ? g_stats_flush : g_stats_group;
+  const int len = which == 2 ? 6 : 4;
+  for (int i = 0; i < n; ++i) out[i] = i < len ? src[i] : 0.0;
+  return NBP_OK;
+}
+
 int nbp_grad_reduce_flush(int stop, nbp_stream_t s) {
   NBP_REQUIRE(!g_defer || g_defer_stream == S(s), "nbp_grad_reduce_flush: deferral is active on another stream");
+  for (double& v : g_stats_flush) v = 0;
   if (g_defer) flush_pending();
   if (stop) g_defer = false;
   return check_launch("grad_reduce_flush");

@@ -69,10 +69,13 @@ __global__ void finalize_mean(const double* __restrict__ partial, int n, double 
 // gradient-coefficient maps (the only global writes).  Every input pixel is read from HBM once (+halo).
 constexpr int SS_TH = 32, SS_TW = 64, SS_R = 5;
 
+// inv_n: the reduction's weight of one pixel in the coefficient maps (1/n for 'mean', 1 for 'sum' and 'none'; with
+// 'none' the backward multiplies each coefficient by that pixel's upstream gradient); lmap (optional): the clamped
+// per-pixel loss map (reduction 'none')
 __global__ __launch_bounds__(256) void ssim_fwd_tiled(const float* __restrict__ x, const float* __restrict__ y, int H,
                                                        int W, int clamp_in, Win win, float C1, float C2, float eps,
                                                        float inv_n, double* __restrict__ partial,
-                                                       float* __restrict__ coef, long n) {
+                                                       float* __restrict__ coef, float* __restrict__ lmap, long n) {
   constexpr int LH = SS_TH + 2 * SS_R, LW = SS_TW + 2 * SS_R;
   __shared__ float xs[LH][LW + 1], ys[LH][LW + 1];
   __shared__ float hm[5][LH][SS_TW + 1];
@@ -142,7 +145,9 @@ __global__ __launch_bounds__(256) void ssim_fwd_tiled(const float* __restrict__ 
     const float num = A1 * A2, D = B1 * B2 + eps;
     const float S = num / D;
     const float l = (1.f - S) / 2.f;
-    sacc += fminf(fmaxf(l, 0.f), 1.f);
+    const float lc = fminf(fmaxf(l, 0.f), 1.f);
+    sacc += lc;
+    if (lmap) lmap[(plane * H + gy) * W + gx] = lc;
     if (coef) {
       const float dS = (l >= 0.f && l <= 1.f) ? -0.5f * inv_n : 0.f;
       // dnum/dmx = 2 my (A2 - A1); dden/dmx = 2 mx (B2 - B1); dS/dE[x^2] = -S B1 / D; dS/dE[xy] = 2 A1 / D
@@ -175,10 +180,13 @@ __device__ __forceinline__ int refl_sources(int j, int n, int* qs) {
   return nq;
 }
 
+// up_map (optional, reduction 'none'): the per-pixel upstream gradient, applied to the coefficients as they are
+// staged (the adjoint filters are linear); otherwise the scalar up[0] scales the result
 __global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ coef, const float* __restrict__ x,
                                                        const float* __restrict__ y, int H, int W, Win win,
                                                        int clamp_in, const float* __restrict__ up,
-                                                       float* __restrict__ gx, long n) {
+                                                       const float* __restrict__ up_map, float* __restrict__ gx,
+                                                       long n) {
   constexpr int LH = SB_TH + 2 * SB_M, LW = SB_TW + 2 * SB_M;
   __shared__ float cs[3][LH][LW + 1];
   __shared__ float tv[3][SB_TH][LW + 1];
@@ -195,8 +203,9 @@ __global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ 
       const int gy = y0 - SB_M + r, gxx = x0 - SB_M + c;
       const bool in = e < LH * LW && gy >= 0 && gy < H && gxx >= 0 && gxx < W;
       const long o = pb + (long)gy * W + gxx;
+      const float um = in && up_map ? up_map[o] : 1.f;
 #pragma unroll
-      for (int m = 0; m < 3; ++m) v[u][m] = in ? coef[m * n + o] : 0.f;
+      for (int m = 0; m < 3; ++m) v[u][m] = in ? coef[m * n + o] * um : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -253,7 +262,7 @@ __global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ 
     tv[0][r][c] = a0; tv[1][r][c] = a1; tv[2][r][c] = a2;
   }
   __syncthreads();
-  const float g0 = up[0];
+  const float g0 = up_map ? 1.f : up[0];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int e = tid + k * 256;
@@ -340,8 +349,9 @@ int nbp_pix_loss_bwd(const float* a, const float* b, long n, int mode, float eps
 size_t nbp_ssim_workspace_floats(long n) { return (size_t)5 * n + 4; }
 
 int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W, int window, float max_val,
-                      int clamp_in, int want_grad, float* ws, float* loss, nbp_stream_t s) {
-  NBP_REQUIRE(x && y && ws && loss && N > 0 && C > 0, "nbp_ssim_loss_fwd: bad args");
+                      int clamp_in, int want_grad, int reduction, float* ws, float* loss, float* lmap, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && ws && N > 0 && C > 0 && reduction >= 0 && reduction <= 2, "nbp_ssim_loss_fwd: bad args");
+  NBP_REQUIRE(reduction == 2 ? lmap != nullptr : loss != nullptr, "nbp_ssim_loss_fwd: output missing for the reduction");
   NBP_REQUIRE(window == 11, "nbp_ssim_loss_fwd: only the 11-tap window (SSIMLoss default) is implemented");
   NBP_REQUIRE(H > 5 && W > 5, "nbp_ssim_loss_fwd: reflect padding needs H, W > 5");
   NBP_REQUIRE((long)N * C <= 65535, "nbp_ssim_loss_fwd: N*C <= 65535 planes");
@@ -352,21 +362,22 @@ int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W
   const dim3 g(cdiv(W, SS_TW), cdiv(H, SS_TH), (unsigned)planes);
   const int nb = (int)(g.x * g.y * g.z);
   const float C1 = (0.01f * max_val) * (0.01f * max_val), C2 = (0.03f * max_val) * (0.03f * max_val);
-  ssim_fwd_tiled<<<g, 256, 0, S(s)>>>(x, y, H, W, clamp_in, win, C1, C2, 1e-12f, (float)(1.0 / (double)n), partial,
-                                      want_grad ? coef : nullptr, n);
-  finalize_mean<<<1, 256, 0, S(s)>>>(partial, nb, 1.0 / (double)n, loss);
+  const float inv_n = reduction == 0 ? (float)(1.0 / (double)n) : 1.f;
+  ssim_fwd_tiled<<<g, 256, 0, S(s)>>>(x, y, H, W, clamp_in, win, C1, C2, 1e-12f, inv_n, partial,
+                                      want_grad ? coef : nullptr, reduction == 2 ? lmap : nullptr, n);
+  if (loss) finalize_mean<<<1, 256, 0, S(s)>>>(partial, nb, reduction == 0 ? 1.0 / (double)n : 1.0, loss);
   return check_launch("ssim_loss_fwd");
 }
 
 // requires the workspace of a forward call made with want_grad = 1 on the same inputs
 int nbp_ssim_loss_bwd(const float* x, const float* y, int N, int C, int H, int W, int clamp_in, const float* up,
-                      float* ws, float* gx, nbp_stream_t s) {
-  NBP_REQUIRE(x && y && ws && up && gx && N > 0 && C > 0 && H > 5 && W > 5, "nbp_ssim_loss_bwd: bad args");
+                      const float* up_map, float* ws, float* gx, nbp_stream_t s) {
+  NBP_REQUIRE(x && y && ws && (up || up_map) && gx && N > 0 && C > 0 && H > 5 && W > 5, "nbp_ssim_loss_bwd: bad args");
   NBP_REQUIRE((long)N * C <= 65535, "nbp_ssim_loss_bwd: N*C <= 65535 planes");
   const long planes = (long)N * C, n = planes * H * W;
   const Win win = make_window(11, 1.5f);
   const dim3 g(cdiv(W, SB_TW), cdiv(H, SB_TH), (unsigned)planes);
-  ssim_bwd_tiled<<<g, 256, 0, S(s)>>>(ws, x, y, H, W, win, clamp_in, up, gx, n);
+  ssim_bwd_tiled<<<g, 256, 0, S(s)>>>(ws, x, y, H, W, win, clamp_in, up, up_map, gx, n);
   return check_launch("ssim_loss_bwd");
 }
 

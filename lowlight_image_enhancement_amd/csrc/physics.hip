@@ -252,6 +252,34 @@ __global__ void phys_full_bwd(const float* __restrict__ sign_map, const float* _
   }
 }
 
+// grad wrt the short exposure A (the reference's losses are plain autograd, NewBP_model/losses.py:158-220):
+// al = clamp?(pre?(a) * r) enters d = yhat - al with a minus sign, so
+//   ga[n][ca][p] = -up[0] * scale * sum_{cb -> ca} sign[n][cb][p] * r * mask_align * mask_a
+// (torch's clamp backward passes the gradient where lo <= x <= hi; cb -> ca: F.l1_loss's channel broadcast, every cb
+// when Ca == 1, else cb == ca).  Depthwise losses: Cb = Ca = C.
+__global__ void phys_a_bwd(const float* __restrict__ sign_map, const float* __restrict__ a, const float* __restrict__ ratio,
+                           int ratio_full, int N, int Ca, int Cb, int H, int W, int clamp_a_in, int clamp_align,
+                           const float* __restrict__ up, float scale, float* __restrict__ ga) {
+  const int total = N * Ca * H * W;
+  const float g0 = -up[0] * scale;
+  const int HW = H * W;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int p = i % HW, plane = i / HW;
+    const int ca = plane % Ca, n = plane / Ca;
+    const float a0 = a[i];
+    const float av = clamp_a_in ? clamp01(a0) : a0;
+    const float r = ratio_full ? ratio[i] : ratio[plane];
+    const float al = av * r;
+    float m = (!clamp_align || (al >= 0.f && al <= 1.f)) ? r : 0.f;
+    if (clamp_a_in && !(a0 >= 0.f && a0 <= 1.f)) m = 0.f;
+    float acc = 0.f;
+    if (Ca == Cb) acc = sign_map[i];
+    else
+      for (int cb = 0; cb < Cb; ++cb) acc += sign_map[((long)n * Cb + cb) * HW + p];
+    ga[i] = g0 * acc * m;
+  }
+}
+
 // fixed-order sum of block partials -> out[0] = scale * sum
 __global__ void finalize_sum(const double* __restrict__ partial, int n, double scale, float* __restrict__ out) {
   __shared__ double red[16];
@@ -462,6 +490,19 @@ int nbp_phys_full_bwd(const float* sign_map, const float* k, const float* up, in
   const float scale = (float)(1.0 / ((double)N * Cb * H * W));
   phys_full_bwd<<<grid_for(total), kBlk, 0, S(s)>>>(sign_map, k, up, scale, N, C, Co, Cb, H, W, KH, KW, gx);
   return check_launch("phys_full_bwd");
+}
+
+int nbp_phys_a_bwd(const float* sign_map, const float* a, const float* ratio, int ratio_full, int N, int Ca, int Cb, int H,
+                   int W, int clamp_a_in, int clamp_align, const float* up, float* ga, nbp_stream_t s) {
+  NBP_REQUIRE(sign_map && a && ratio && up && ga && N > 0 && Ca > 0 && Cb > 0 && H > 0 && W > 0,
+              "nbp_phys_a_bwd: bad args");
+  NBP_REQUIRE(Ca == Cb || Ca == 1, "nbp_phys_a_bwd: A's %d channels do not broadcast to %d", Ca, Cb);
+  NBP_REQUIRE((long)N * Cb * H * W < (1L << 31), "physics kernels: N*C*H*W must be < 2^31");
+  const long total = (long)N * Ca * H * W;
+  const float scale = (float)(1.0 / ((double)N * Cb * H * W));
+  phys_a_bwd<<<grid_for(total), kBlk, 0, S(s)>>>(sign_map, a, ratio, ratio_full, N, Ca, Cb, H, W, clamp_a_in,
+                                                 clamp_align, up, scale, ga);
+  return check_launch("phys_a_bwd");
 }
 
 size_t nbp_phys_cons_workspace_doubles(int N, int H, int W) {

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const HT* __restrict__
   }
 }
 
-// din = scatter(dout at the argmax) * (post_in > 0)   (the pool input is a post-ReLU map)
+// din = scatter(dout at the argmax) * !(post_in <= 0)   (the pool input is a post-ReLU map; torch's threshold_backward
+// passes the gradient of a NaN)
 template <typename HT>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const HT* __restrict__ dy,
                                                           const unsigned char* __restrict__ idx,
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const HT* __restrict__
       const vec_t<HT, 8> pin = *reinterpret_cast<const vec_t<HT, 8>*>(post_in + pix * C + c8 * 8);
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if ((int)((packed >> (8 * k)) & 0xff) == pos && (float)pin[k] > 0.f) out[k] = g[k];
+        if ((int)((packed >> (8 * k)) & 0xff) == pos && !((float)pin[k] <= 0.f)) out[k] = g[k];  // relu bwd: NaN passes
     }
     *reinterpret_cast<vec_t<HT, 8>*>(dx + pix * C + c8 * 8) = out;
   }
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(256) void lpips_tap_bwd(const HT* __restrict__ a, c
 }
 
 // k x k max pool, stride s, no padding (floor), NHWC (torchvision AlexNet's MaxPool2d(3, 2)); idx (optional): the
-// window position of the first maximum in row-major window order (NaN wins, as torch's max_pool2d)
+// window position of the first maximum in row-major window order (a NaN replaces the running maximum, so the last NaN wins, as torch's max_pool2d)
 template <typename HT>
 __global__ __launch_bounds__(256) void maxpool_k_fwd_kernel(const HT* __restrict__ x, int H, int W, int C, int k, int st,
                                                             int Ho, int Wo, long total8, HT* __restrict__ y,
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(256) void maxpool_k_fwd_kernel(const HT* __restrict
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float f = (float)v[q];
-          if ((di == 0 && dj == 0) || f > best[q] || (f != f && best[q] == best[q])) {
+          if ((di == 0 && dj == 0) || f > best[q] || f != f) {  // torch: val > maxval || isnan(val): the last NaN wins
             best[q] = f;
             bi[q] = di * k + dj;
           }
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(256) void maxpool_k_bwd_kernel(const HT* __restrict
     const vec_t<HT, 8> pin = *reinterpret_cast<const vec_t<HT, 8>*>(post_in + pix * C + c8 * 8);
     vec_t<HT, 8> out;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) out[q] = (HT)((float)pin[q] > 0.f ? acc[q] : 0.f);
+    for (int q = 0; q < 8; ++q) out[q] = (HT)(!((float)pin[q] <= 0.f) ? acc[q] : 0.f);  // relu bwd: NaN passes
     *reinterpret_cast<vec_t<HT, 8>*>(dx + pix * C + c8 * 8) = out;
   }
 }

@@ -193,44 +193,46 @@ class _LPIPSFn(torch.autograd.Function):
         _lib.require_cuda(in0, in1)
         if in0.shape != in1.shape or in0.dim() != 4 or in0.shape[1] != 3:
             raise ValueError("LPIPS expects two [N,3,H,W] tensors of the same shape")
-        if ctx.needs_input_grad[1]:
-            raise NotImplementedError("LPIPS gradient w.r.t. the second input is not implemented on MI355X")
         x0 = in0.detach().float()
         x1 = in1.detach().float()
         if normalize:  # [0,1] -> [-1,1]
             x0, x1 = 2 * x0 - 1, 2 * x1 - 1
         stack, lins = module.parts(in0.device, dt)
-        want = ctx.needs_input_grad[0]
+        want0, want1 = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         with torch.no_grad():
             # the ScalingLayer is the prologue's (x - mean) / std with mean = shift, std = scale (no clamp)
-            t0, tape = _trunk_taps(stack, x0, want)
-            t1, _ = _trunk_taps(stack, x1, False)
+            t0, tape0 = _trunk_taps(stack, x0, want0)
+            t1, tape1 = _trunk_taps(stack, x1, want1)
         N = in0.shape[0]
         out = torch.zeros(N, device=in0.device)
         _tap_distances(stack, lins, t0, t1, out, False)
-        if want:
-            ctx.tape, ctx.t0, ctx.t1, ctx.stack, ctx.lins = tape, t0, t1, stack, lins
+        if want0 or want1:
+            ctx.tapes, ctx.t0, ctx.t1, ctx.stack, ctx.lins = (tape0, tape1), t0, t1, stack, lins
             ctx.normalize = normalize
-            ctx.save_for_backward(x0)
+            ctx.save_for_backward(x0, x1)
         return out.view(N, 1, 1, 1)
 
     @staticmethod
     def backward(ctx, up):
-        (x0,) = ctx.saved_tensors
+        x0, x1 = ctx.saved_tensors
         up = up.float().contiguous().view(-1)
-        grads = []
-        for k in range(5):
-            a, b = ctx.t0[k], ctx.t1[k]
-            g = torch.empty_like(a)
-            call("lpips_tap_bwd", a, b, ctx.lins[k], a.shape[0], a.shape[1] * a.shape[2], a.shape[3], up, g,
-                 ctx.stack.dtype)
-            grads.append(g)
-        d8 = _trunk_backward(ctx.stack, ctx.tape, grads)
-        dx = _vgg.input_grad(d8, x0, SCALE, clamp=False)
-        if ctx.normalize:
-            dx = dx * 2
-        ctx.tape = ctx.t0 = ctx.t1 = None
-        return dx, None, None, None, None
+        outs = [None, None]
+        # the tap distance sum_c w_c (a/|a| - b/|b|)^2 is symmetric: d/d in1 is the tap gradient with the maps swapped
+        for side, (mine, other, x) in enumerate(((ctx.t0, ctx.t1, x0), (ctx.t1, ctx.t0, x1))):
+            if not ctx.needs_input_grad[side]:
+                continue
+            grads = []
+            for k in range(5):
+                a, b = mine[k], other[k]
+                g = torch.empty_like(a)
+                call("lpips_tap_bwd", a, b, ctx.lins[k], a.shape[0], a.shape[1] * a.shape[2], a.shape[3], up, g,
+                     ctx.stack.dtype)
+                grads.append(g)
+            d8 = _trunk_backward(ctx.stack, ctx.tapes[side], grads)
+            dx = _vgg.input_grad(d8, x, SCALE, clamp=False)
+            outs[side] = dx * 2 if ctx.normalize else dx
+        ctx.tapes = ctx.t0 = ctx.t1 = None
+        return outs[0], outs[1], None, None, None
 
 
 class LPIPS(nn.Module):

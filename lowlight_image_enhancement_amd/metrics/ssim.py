@@ -105,8 +105,13 @@ def calculate_ssim(img_true: torch.Tensor, img_pred: torch.Tensor, data_range: f
     if t.shape[:2] != p.shape[:2]:
         raise ValueError("SSIM requires the same batch size and channel count for target and prediction. "
                          f"Got target={t.shape}, prediction={p.shape}.")
-    _lib.require_cuda(t, p)
-    t, p = _align_pair(t.float(), p.float(), resize_policy, resize_mode)
+    # the reference's _prepare_inputs (ssim.py:269-271) moves both to the evaluator's device as float32: CPU tensors
+    # are accepted and moved to the GPU the kernels run on (the first CUDA input's device, else the current one)
+    if not torch.cuda.is_available():
+        raise _lib.NBPError("calculate_ssim runs on the GPU (HIP kernels); no GPU is visible and there is no CPU path")
+    dev = t.device if t.is_cuda else (p.device if p.is_cuda else torch.device("cuda", torch.cuda.current_device()))
+    t, p = t.to(dev, torch.float32), p.to(dev, torch.float32)
+    t, p = _align_pair(t, p, resize_policy, resize_mode)
     if color_space == "y":
         if t.shape[1] == 3:
             t, p = _to_luma_bt601(t), _to_luma_bt601(p)

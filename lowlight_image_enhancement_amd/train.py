@@ -79,6 +79,8 @@ class NBPTrainer:
             lpips = LPIPS(net=lpips_net)
         self.perceptual, self.lpips = perceptual, lpips
         self.lpips_buf: Optional[torch.Tensor] = None
+        self._lpips_bufs: Dict[int, torch.Tensor] = {}  # batch size -> per-image LPIPS values, never freed (as _ups)
+        self._skipped_seen = 0  # ctl[2] (skipped steps) at the previous logs() call
         self.lr, self.betas, self.wd, self.eps = lr, betas, weight_decay, eps
         self.max_norm = max_norm if max_norm is not None else 0.0
         self.scheduler = scheduler
@@ -161,8 +163,8 @@ class NBPTrainer:
         call("pix_loss_bwd", out, gt, n, 0, 0.0, 0, 0, self.up[0:1], d_out)
         if wss != 0.0:
             ss_ws = torch.empty(query("ssim_workspace_floats", n), device=lq.device)
-            call("ssim_loss_fwd", out, gt, B, C, H, W, 11, 1.0, 1, 1, ss_ws, self.loss_buf[1:2])
-            call("ssim_loss_bwd", out, gt, B, C, H, W, 1, self.up[1:2], ss_ws, tmp)
+            call("ssim_loss_fwd", out, gt, B, C, H, W, 11, 1.0, 1, 1, 0, ss_ws, self.loss_buf[1:2], None)
+            call("ssim_loss_bwd", out, gt, B, C, H, W, 1, self.up[1:2], None, ss_ws, tmp)
             call("add", d_out, tmp, d_out, n, 0)
         if wph != 0.0 and short is not None:
             if expo_ratio is None:  # ones [B,1,1,1] when the batch has no ratio (image_restoration_model.py:281-287)
@@ -184,8 +186,6 @@ class NBPTrainer:
             g = self.perceptual.value_and_grad(out, gt, self.up[4:5], self.loss_buf[4:5], dt=self._trunk_dt(self.perceptual))
             call("add", d_out, g, d_out, n, 0)
         if wlp != 0.0:
-            if self.lpips_buf is None or self.lpips_buf.numel() != B:
-                self.lpips_buf = torch.zeros(B, device=lq.device)
             g = self.lpips.value_and_grad(out, gt, self.up[5:5 + B], self.lpips_buf, clamp=True,
                                           dt=self._trunk_dt(self.lpips))
             call("add", d_out, g, d_out, n, 0)
@@ -206,9 +206,15 @@ class NBPTrainer:
         """Select the upstream-gradient buffers of a batch of B images.  One pair (up_base, up) per batch size is kept
         for the trainer's lifetime: a captured graph addresses its pair by device pointer, so a pair is never freed or
         rebound.  Switching to another batch size refreshes that pair's up = up_base * S from the current loss scale
-        (a device op: the optimizer of the steps run at other sizes moved S)."""
+        (a device op: the optimizer of the steps run at other sizes moved S).  The per-image LPIPS value buffer is
+        kept per batch size the same way (a captured graph's LPIPS tap kernels write into it)."""
         if self.up_base is not None and self.up_base.numel() == 5 + B:
             return
+        if self.w_extra["lpips"]:
+            buf = self._lpips_bufs.get(B)
+            if buf is None:
+                buf = self._lpips_bufs[B] = torch.zeros(B, device=self.dev)
+            self.lpips_buf = buf
         pair = self._ups.get(B)
         if pair is None:
             wl1, wss, wph = self.w
@@ -390,6 +396,8 @@ class NBPTrainer:
             dist.all_reduce(buf, group=self.pg)
             buf /= self.world
         vals = buf.cpu()
+        skipped = int(self.ctl[2].item())
+        new_skips, self._skipped_seen = skipped - self._skipped_seen, skipped  # counted once, even when raising below
         if not torch.isfinite(vals).all():
             raise RuntimeError(f"HybridLossPlus detected non-finite values: {vals.tolist()}")
         out = {"L1_raw": float(vals[0])}
@@ -408,11 +416,12 @@ class NBPTrainer:
         out["grad_norm"] = float(st[0])
         if self.scaler is not None:
             out["loss_scale"] = float(st[6])
-        if st[2] != 0:
+        if st[2] != 0 or new_skips > 0:
             if self.scaler is None:
                 # no GradScaler: the reference has no skip here (image_restoration_model.py:316-320); a non-finite
-                # gradient left the parameters untouched, and the run must not continue silently
-                raise RuntimeError("NBPTrainer: the last step's gradient was non-finite (step skipped; no loss scaler "
-                                   f"is active); grad_norm={float(st[0])}")
-            out["skipped"] = 1.0
+                # gradient on ANY step since the previous logs() left the parameters untouched, and the run must not
+                # continue silently
+                raise RuntimeError(f"NBPTrainer: {max(new_skips, 1)} step(s) since the previous logs() had a non-finite "
+                                   f"gradient (skipped; no loss scaler is active); last grad_norm={float(st[0])}")
+            out["skipped"] = float(max(new_skips, 1))
         return out

@@ -16,8 +16,14 @@ import os
 import re
 import sys
 
-CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"), "wgrad": ("wgrad_",), "gemm_f32": ("gemm_f32_kernel",),
-           "dw_bwd": ("dw_bwd_tiled",), "dw_fwd": ("dw_sg_pool_tiled",), "ln_fwd": ("ln_fwd_nhwc",),
+CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"), "gemm_f32": ("gemm_f32_kernel",),
+           # weight gradients launched at once (N or K <= 64) / the grouped wide launches of a U-Net level, and the
+           # fp32 slab reductions (+ layer-scale post-ops) that fold their split-M partials: per KERNEL launch, the
+           # unit bench.py's algorithmic bytes use for these classes
+           "wgrad_narrow": ("wgrad_bf16_kernel", "wgrad_f32_kernel"), "wgrad_group": ("wgrad_bf16_wide",),
+           "reduce": ("reduce_multi_kernel", "layer_scale_grad_kernel"),
+           "dw_bwd": ("dw_bwd_tiled",), "dw_bwd_32": (re.compile(r"dw_bwd_tiledI\w+?Li32E"),),
+           "dw_fwd": ("dw_sg_pool_tiled",), "ln_fwd": ("ln_fwd_nhwc",),
            "ln_bwd": ("ln_bwd_nhwc",),
            # VGG / AlexNet implicit-GEMM convs (cfg3's perceptual + LPIPS trunks): the tiled kernels with A mode 3 / 4
            "vgg_conv": (re.compile(r"gemm_(glds|bf16)_kernelILi\d+ELi\d+ELi\d+ELi[34]E"),),

@@ -1,0 +1,69 @@
+"""bench.py --gpus N argument handling (CPU): N ranks are started (or required from the launcher) exactly as asked,
+never silently one.  The launch contract mirrors the reference's DDP launch
+(NAFNet_base/basicsr/train.py:54-63, utils/dist_util.py:28-40): one process per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT in the environment."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_plan_single_gpu_default():
+    assert bench.plan_launch(None, {}, 1, False) == ("run", 1)
+    assert bench.plan_launch(1, {}, 8, False) == ("run", 1)
+
+
+def test_plan_spawns_n_ranks_without_a_launcher():
+    assert bench.plan_launch(8, {}, 8, False) == ("spawn", 8)
+    assert bench.plan_launch(2, {}, 1, True) == ("spawn", 2)  # rehearsal: every rank on cuda:0
+
+
+def test_plan_under_a_launcher_must_match():
+    assert bench.plan_launch(4, {"WORLD_SIZE": "4"}, 8, False) == ("run", 4)
+    assert bench.plan_launch(None, {"WORLD_SIZE": "2"}, 8, False) == ("run", 2)
+    with pytest.raises(SystemExit, match="must match"):
+        bench.plan_launch(8, {"WORLD_SIZE": "1"}, 8, False)
+
+
+def test_plan_refuses_more_ranks_than_gpus():
+    with pytest.raises(SystemExit, match="only 1 GPU"):
+        bench.plan_launch(8, {}, 1, False)
+    with pytest.raises(SystemExit, match=">= 1"):
+        bench.plan_launch(0, {}, 8, False)
+
+
+def test_rank_envs_are_torchrun_style():
+    envs = bench.rank_envs(4, {"FOO": "1"}, 29555)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29555"
+        assert e["FOO"] == "1"
+
+
+def _run(args, env_extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_mismatched_world_size_exits_nonzero():
+    r = _run(["--gpus", "2"], {"WORLD_SIZE": "3"})
+    assert r.returncode != 0 and "must match" in r.stderr
+
+
+def test_spawned_ranks_report_their_failure():
+    """Stand-alone --gpus 2 (rehearsal, so the GPU count check passes here): the parent starts two ranks with
+    WORLD_SIZE=2; on this GPU-less container each rank fails at its first GPU call, and the parent exits non-zero
+    instead of timing one process."""
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--quick"], {"NBP_BENCH_REHEARSE": "1"})
+    assert r.returncode != 0
+    assert "exited with status" in r.stderr
+    assert '"n_gpus"' not in r.stdout

@@ -387,6 +387,22 @@ def test_nonfinite_step_is_skipped(dev, precision, graph):
     assert np.isfinite(tr.logs()["Total"])
 
 
+def test_skip_between_logs_is_reported_without_a_scaler(dev):
+    """without a loss scaler a skipped (non-finite-gradient) step anywhere between two logs() calls must
+    raise at the next logs(), not only when it was the last step (the clean step after it hides it from the per-step
+    verdict)."""
+    tr = _small_trainer(dev, "fp32")
+    tr.step(*_batch(dev, 1))
+    tr.logs()
+    tr.step(*_batch(dev, 2, nan=True))  # skipped
+    assert tr.skipped_steps == 1
+    tr.step(*_batch(dev, 3))  # clean: the last step alone would not show the skip
+    with pytest.raises(RuntimeError, match="non-finite"):
+        tr.logs()
+    tr.step(*_batch(dev, 4))
+    assert np.isfinite(tr.logs()["Total"])  # each skip is reported once
+
+
 def test_dynamic_loss_scale_is_exact_and_follows_gradscaler(dev):
     """Loss scaling by a power of two commutes with every (linear) backward op, so a dynamically scaled fp32 run
     equals the unscaled one bit for bit; the scale follows torch.amp.GradScaler.update (backoff 0.5 on a skipped

@@ -1,0 +1,205 @@
+"""GPU parity of the loss modules' public-API corners: the reference's loss modules are plain torch
+autograd (NewBP_model/losses.py), so every input gets a gradient and SSIMLoss honours kornia's reductions.
+
+* DeltaE00Loss._ciede2000 on Lab tensors (losses.py:98-136): values vs the reference's own outputs and the Sharma
+  pairs, d/dLab1 vs the reference's autograd (tests/golden/ciede2000.npz), d/dLab2 vs the oracle in float64;
+* SSIMLoss(reduction='mean' | 'sum' | 'none') (losses.py:146-155 -> kornia 0.6.12 ssim_loss) and its gradients to
+  both inputs vs the oracle restatement in float64 (kornia absent: parity unpinned);
+* the second-argument gradients of DeltaE00Loss, PerceptualLoss (VGG19, fp32 trunk), LPIPS (vgg and alex, fp32
+  trunks) and the physics losses' short-exposure (A-side) gradient vs the oracle in float64.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle.losses as OL
+import oracle.physics as OP
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _rel(a, b):
+    a, b = a.double().cpu().flatten(), b.double().cpu().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+# ------------------------------------------------------------------------------------------------ ΔE00 on Lab
+def test_ciede2000_lab_values_and_gradients(dev):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import DeltaE00Loss
+    d = np.load(os.path.join(GOLD, "ciede2000.npz"))
+    # Sharma pairs: the reference's loss form, bit-level close to its own outputs; within 1.5 of the gold values
+    # (the reference's tolerance, standard_tests/test_color_error.py:161-197; the loss form is non-standard)
+    l1, l2 = torch.from_numpy(d["lab1"]).to(dev), torch.from_numpy(d["lab2"]).to(dev)
+    got = DeltaE00Loss._ciede2000(l1, l2, 1e-6)
+    assert got.shape == (1, 1, 18)
+    np.testing.assert_allclose(got.cpu().numpy(), d["loss_sharma"], rtol=1e-5, atol=1e-5)
+    assert np.abs(got.cpu().numpy().ravel() - d["sharma_gold"]).max() < 1.5
+    # random Lab pairs: value and d/dLab1 of the mean vs the reference's autograd
+    r1 = torch.from_numpy(d["rl1"]).to(dev).requires_grad_(True)
+    r2 = torch.from_numpy(d["rl2"]).to(dev).requires_grad_(True)
+    v = DeltaE00Loss._ciede2000(r1, r2)
+    np.testing.assert_allclose(v.detach().cpu().numpy(), d["loss_rand"], rtol=1e-5, atol=1e-5)
+    v.mean().backward()
+    ref1 = torch.from_numpy(d["loss_rand_grad"])
+    assert _rel(r1.grad, ref1) < 1e-4, _rel(r1.grad, ref1)
+    # d/dLab2 (no reference fixture: the oracle's autograd in float64 on the same pair)
+    q1 = torch.from_numpy(d["rl1"]).double().requires_grad_(True)
+    q2 = torch.from_numpy(d["rl2"]).double().requires_grad_(True)
+    OL.ciede2000_loss_form(q1, q2, 1e-6).mean().backward()
+    assert _rel(r1.grad, q1.grad) < 1e-4
+    assert _rel(r2.grad, q2.grad) < 1e-4, _rel(r2.grad, q2.grad)
+    # a non-uniform upstream map
+    g = torch.Generator().manual_seed(3)
+    up = torch.rand(v.shape, generator=g)
+    r1.grad = r2.grad = None
+    DeltaE00Loss._ciede2000(r1, r2).backward(up.to(dev))
+    q1.grad = q2.grad = None
+    OL.ciede2000_loss_form(q1, q2, 1e-6).backward(up.double())
+    assert _rel(r1.grad, q1.grad) < 1e-4 and _rel(r2.grad, q2.grad) < 1e-4
+
+
+def test_deltae00_loss_gradient_to_both_inputs(dev):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import DeltaE00Loss
+    g = torch.Generator().manual_seed(5)
+    a = torch.rand(2, 3, 17, 23, generator=g) * 1.1 - 0.05  # some values outside [0, 1]: the clamp masks
+    b = torch.rand(2, 3, 17, 23, generator=g) * 1.1 - 0.05
+    x, y = a.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+    loss = DeltaE00Loss()(x, y)
+    loss.backward()
+    xr, yr = a.double().requires_grad_(True), b.double().requires_grad_(True)
+    lr = OL.deltae00_loss(xr, yr)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * lr.item()
+    assert _rel(x.grad, xr.grad) < 1e-4, _rel(x.grad, xr.grad)
+    assert _rel(y.grad, yr.grad) < 1e-4, _rel(y.grad, yr.grad)
+    out = (b < 0) | (b > 1)
+    assert torch.equal(y.grad.cpu()[out], torch.zeros(int(out.sum())))
+
+
+# ------------------------------------------------------------------------------------------------ SSIMLoss
+@pytest.mark.parametrize("reduction", ["mean", "sum", "none"])
+def test_ssim_loss_reductions_and_gradients(dev, reduction):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import SSIMLoss
+    g = torch.Generator().manual_seed(7)
+    a = torch.rand(2, 3, 37, 70, generator=g) * 1.1 - 0.05
+    b = torch.rand(2, 3, 37, 70, generator=g)
+    x, y = a.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+    out = SSIMLoss(reduction=reduction)(x, y)
+    xr, yr = a.double().requires_grad_(True), b.double().requires_grad_(True)
+    m = OL.ssim_map(xr.clamp(0, 1), yr.clamp(0, 1))
+    lmap = torch.clamp((1.0 - m) / 2, min=0, max=1)
+    ref = {"mean": lmap.mean(), "sum": lmap.sum(), "none": lmap}[reduction]
+    if reduction == "none":
+        assert out.shape == a.shape
+        assert (out.double().cpu() - ref.detach()).abs().max().item() < 2e-6
+        up = torch.rand(a.shape, generator=g)
+        out.backward(up.to(dev))
+        ref.backward(up.double())
+    else:
+        assert out.dim() == 0
+        assert abs(out.item() - ref.item()) <= 2e-6 * abs(ref.item())
+        out.backward()
+        ref.backward()
+    assert _rel(x.grad, xr.grad) < 1e-4, _rel(x.grad, xr.grad)
+    assert _rel(y.grad, yr.grad) < 1e-4, _rel(y.grad, yr.grad)
+    with pytest.raises(ValueError):
+        SSIMLoss(reduction="avg")
+
+
+# ------------------------------------------------------------------------------------------------ VGG / LPIPS
+def test_perceptual_loss_gradient_to_the_target(dev):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PerceptualLoss
+    from lowlight_image_enhancement_amd.vgg import VGG19_CFG, synthetic_state_dict
+    sd = synthetic_state_dict(VGG19_CFG, 36, seed=0)
+    sd = {k: (v + 0.01 if k.endswith("bias") else v) for k, v in sd.items()}
+    g = torch.Generator().manual_seed(2)
+    gen = torch.rand(2, 3, 64, 48, generator=g)
+    tgt = torch.rand(2, 3, 64, 48, generator=g) * 1.1 - 0.05
+    crit = PerceptualLoss(device=dev, weights=sd)  # fp32 trunk (the reference's)
+    x, y = gen.to(dev).requires_grad_(True), tgt.to(dev).requires_grad_(True)
+    crit(x, y).backward()
+    xr, yr = gen.double().requires_grad_(True), tgt.double().requires_grad_(True)
+    OL.perceptual_loss({k: v.double() for k, v in sd.items()}, xr, yr).backward()
+    assert _rel(x.grad, xr.grad) < 1e-4, _rel(x.grad, xr.grad)
+    assert _rel(y.grad, yr.grad) < 1e-4, _rel(y.grad, yr.grad)
+    # target only
+    y2 = tgt.to(dev).requires_grad_(True)
+    crit(gen.to(dev), y2).backward()
+    assert torch.equal(y2.grad, y.grad)
+
+
+@pytest.mark.parametrize("net", ["vgg", "alex"])
+def test_lpips_gradient_to_the_second_input(dev, net):
+    """fp32 trunks.  Bounds as for the first input (test_gpu_vgg.py): 1e-2 rel-norm for VGG16 (max-pool near-ties,
+    DESIGN §4), 1e-4 for AlexNet."""
+    from lowlight_image_enhancement_amd.lpips import ALEX_TAP_CH, LPIPS, TAP_CH, alex_synthetic_state_dict
+    from lowlight_image_enhancement_amd.vgg import VGG16_CFG, synthetic_state_dict
+    feats = synthetic_state_dict(VGG16_CFG, 30, seed=1) if net == "vgg" else alex_synthetic_state_dict(3)
+    g = torch.Generator().manual_seed(4)
+    lins = [(torch.randn(c, generator=g) * 0.1).abs() for c in (TAP_CH if net == "vgg" else ALEX_TAP_CH)]
+    sd = {f"net.slice1.{k}": v for k, v in feats.items()}
+    sd.update({f"lin{k}.model.1.weight": w.view(1, -1, 1, 1) for k, w in enumerate(lins)})
+    m = LPIPS(net=net, weights=sd, precision="fp32")
+    a, b = torch.rand(2, 3, 64, 64, generator=g) * 2 - 1, torch.rand(2, 3, 64, 64, generator=g) * 2 - 1
+    x, y = a.to(dev).requires_grad_(True), b.to(dev).requires_grad_(True)
+    up = torch.rand(2, 1, 1, 1, generator=g)
+    m(x, y).backward(up.to(dev))
+    f64 = {k: v.double() for k, v in feats.items()}
+    xr, yr = a.double().requires_grad_(True), b.double().requires_grad_(True)
+    fn = OL.lpips_vgg if net == "vgg" else OL.lpips_alex
+    fn(f64, lins, xr, yr).backward(up.double())
+    tol = 1e-2 if net == "vgg" else 1e-4
+    assert _rel(x.grad, xr.grad) < tol, _rel(x.grad, xr.grad)
+    assert _rel(y.grad, yr.grad) < tol, _rel(y.grad, yr.grad)
+
+
+# ------------------------------------------------------------------------------------------------ physics A-side
+@pytest.mark.parametrize("ratio_kind", ["scalar", "per_image", "full"])
+def test_phys_srgb_gradient_to_the_short_exposure(dev, ratio_kind):
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PhysicalConsistencyLossSRGB
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_crosstalk_psf
+    g = torch.Generator().manual_seed(11)
+    bhat = torch.rand(2, 3, 21, 19, generator=g)
+    a = torch.rand(2, 3, 21, 19, generator=g) * 0.6
+    ratio = {"scalar": 1.7, "per_image": torch.tensor([1.5, 2.5]),
+             "full": torch.rand(2, 3, 21, 19, generator=g) * 3}[ratio_kind]
+    psf = create_crosstalk_psf("rgb", "B2").to(dev)
+    x, y = bhat.to(dev).requires_grad_(True), a.to(dev).requires_grad_(True)
+    r_dev = ratio.to(dev) if torch.is_tensor(ratio) else ratio
+    loss = PhysicalConsistencyLossSRGB(psf)(x, y, r_dev)
+    loss.backward()
+    k = OP.normalize_psf(OP.build_psf_kernels("rgb", "B2")).double()
+    xr, yr = bhat.double().requires_grad_(True), a.double().requires_grad_(True)
+    r_ref = ratio.double() if torch.is_tensor(ratio) else ratio
+    lr = OP.phys_srgb_loss(xr, yr, r_ref, k)
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * lr.item()
+    assert _rel(x.grad, xr.grad) < 1e-5
+    assert _rel(y.grad, yr.grad) < 1e-5, _rel(y.grad, yr.grad)
+
+
+@pytest.mark.parametrize("kshape,a_ch", [((3, 1, 3, 3), 3), ((1, 1, 3, 3), 3), ((3, 3, 3, 3), 3), ((3, 3, 5, 5), 1)])
+def test_phys_raw_gradient_to_the_short_exposure(dev, kshape, a_ch):
+    """PhysicsConsistencyLoss: depthwise ([3,1] per channel, [1,1] shared) and groups = 1 ([3,3] full; against a
+    one-channel A, broadcast by F.l1_loss) kernels; the A-side gradient through clamp(A * ratio, 0, 1)."""
+    import warnings
+    from lowlight_image_enhancement_amd.NewBP_model.losses import PhysicsConsistencyLoss
+    g = torch.Generator().manual_seed(13)
+    bhat = torch.rand(2, 3, 16, 18, generator=g)
+    a = torch.rand(2, a_ch, 16, 18, generator=g) / 200
+    ratio = torch.tensor([100.0, 250.0])
+    k = torch.rand(*kshape, generator=g)
+    x, y = bhat.to(dev).requires_grad_(True), a.to(dev).requires_grad_(True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        loss = PhysicsConsistencyLoss(k, device=dev)(x, y, ratio.to(dev))
+        loss.backward()
+        xr, yr = bhat.double().requires_grad_(True), a.double().requires_grad_(True)
+        lr = OP.phys_raw_loss(xr, yr, ratio.double(), k.double())
+        lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * lr.item()
+    assert _rel(x.grad, xr.grad) < 1e-5
+    assert _rel(y.grad, yr.grad) < 1e-5, _rel(y.grad, yr.grad)

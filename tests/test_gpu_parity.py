@@ -572,11 +572,13 @@ def test_graph_step_bitwise_equals_eager(dev, precision):
         assert trs[0].logs() == trs[1].logs()
 
 
-def test_graph_step_survives_eager_steps_at_other_batch_sizes(dev):
+@pytest.mark.parametrize("w_lpips", [0.0, 0.05])
+def test_graph_step_survives_eager_steps_at_other_batch_sizes(dev, w_lpips):
     """A captured graph addresses the upstream-gradient buffers of its batch size: eager steps at another batch size
     (a short last batch) must neither free them nor leave them at a stale loss scale.  fp16 with a growth interval of 1
     moves the scale every step, so graph replays after eager B=1 steps equal an all-eager trainer bit for bit.  A
-    replay with a different input shape raises."""
+    replay with a different input shape raises.  With an LPIPS term the per-image LPIPS buffer the captured tap
+    kernels write is kept per batch size too: the logs of the two trainers agree after the mixed plan."""
     from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
     from lowlight_image_enhancement_amd.train import NBPTrainer
     cfg = dict(width=16, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1])
@@ -587,7 +589,7 @@ def test_graph_step_survives_eager_steps_at_other_batch_sizes(dev):
     for net in nets:
         net.to(dev)
         net.precision = "fp16"
-        trs.append(NBPTrainer(net, w_l1=1.0, w_ssim=0.05, w_phys=0.1, growth_interval=1))
+        trs.append(NBPTrainer(net, w_l1=1.0, w_ssim=0.05, w_phys=0.1, growth_interval=1, w_lpips=w_lpips))
     g = torch.Generator(device=dev).manual_seed(6)
     big = tuple(torch.rand(2, 3, 48, 48, device=dev, generator=g) for _ in range(2))
     small = tuple(torch.rand(1, 3, 48, 48, device=dev, generator=g) for _ in range(2))
@@ -600,6 +602,7 @@ def test_graph_step_survives_eager_steps_at_other_batch_sizes(dev):
         assert torch.equal(nets[0].flat, nets[1].flat), f"params differ at step {i}"
         assert torch.equal(trs[0].scaler, trs[1].scaler)
     assert float(trs[1].scaler[0]) == 2.0 ** 16 * 2 ** 5  # grew every step: the buffers were kept in step with it
+    assert trs[0].logs() == trs[1].logs()
     with pytest.raises(ValueError, match="captured"):
         trs[1].graph_step(small[0], small[1], small[0].clamp(0, 1), ratio1)
 

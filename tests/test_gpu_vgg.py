@@ -64,6 +64,40 @@ def test_maxpool_fwd_bwd(dev):
     assert torch.equal(dx.double(), ref)
 
 
+@pytest.mark.parametrize("k,st", [(2, 2), (3, 2)])
+def test_maxpool_nan_windows_route_like_torch(dev, k, st):
+    """torch's max_pool2d replaces the running maximum on every NaN (`val > maxval || isnan(val)`), so in
+    a window with several NaNs the LAST one (row-major) is the argmax and receives the gradient; torch's ReLU
+    backward (threshold_backward: `x <= 0 ? 0 : g`) passes a NaN position's gradient.  fp32 pools (the parity trunks)
+    vs float64 torch CPU on windows holding one, two and three NaNs."""
+    from lowlight_image_enhancement_amd._lib import call
+    B, H, W, C = 1, 7, 9, 8
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(B, H, W, C, generator=g)
+    for (i, j) in [(0, 1), (1, 0), (2, 3), (2, 4), (3, 3), (4, 6), (5, 7), (6, 8), (6, 6)]:
+        x[0, i, j, ::2] = float("nan")
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = Fn.max_pool2d(xr, k, st)
+    Ho, Wo = yr.shape[2], yr.shape[3]
+    dy = torch.randn(B, Ho, Wo, C, generator=g)
+    yr.backward(dy.double().permute(0, 3, 1, 2))
+    xd, dyd = x.to(dev), dy.to(dev)
+    y = torch.empty(B, Ho, Wo, C, device=dev)
+    idx = torch.empty(B, Ho, Wo, C, device=dev, dtype=torch.uint8)
+    dx = torch.empty_like(xd)
+    if k == 2:
+        call("maxpool2_fwd", xd, B, H, W, C, y, idx, 0)
+        call("maxpool2_bwd", dyd, idx, xd, B, H, W, C, dx, 0)
+    else:
+        call("maxpool_k_fwd", xd, B, H, W, C, k, st, y, idx, 0)
+        call("maxpool_k_bwd", dyd, idx, xd, B, H, W, C, k, st, dx, 0)
+    ref_y = yr.detach().permute(0, 2, 3, 1)
+    assert torch.equal(y.double().cpu().isnan(), ref_y.isnan())
+    assert torch.equal(torch.nan_to_num(y.double().cpu()), torch.nan_to_num(ref_y))
+    ref_dx = xr.grad.permute(0, 2, 3, 1)  # overlapping 3x3/2 windows: up to 4 dy summed (fp32 here, float64 there)
+    torch.testing.assert_close(dx.double().cpu(), ref_dx, atol=1e-6, rtol=1e-6)
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,st,pad", [(2, 13, 17, 16, 24, 3, 1, 1), (1, 64, 48, 8, 64, 3, 1, 1),
                                                     (2, 37, 29, 8, 64, 11, 4, 2), (1, 11, 9, 64, 192, 5, 1, 2)])
 def test_conv_fp32_modes(dev, B, H, W, Cin, Cout, k, st, pad):
