@@ -133,6 +133,14 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, int dtype,
                     nbp_stream_t s);
+/* The level-0 NAFBlock FFN half in one pass (NAFNet_arch.py:74-80; C = 32): out = y + gamma (.) (SG(n2 W4^T + b4)
+ * W5^T + b5) and, when nout is given, the next block's LayerNorm2d of out into nout / stats (as nbp_gemm_res_ln).  W4 /
+ * b4: conv4's bf16 weight and bias with the SimpleGate pairs interleaved (2C rows), W5: conv5's [C][C].  The gate map
+ * g2 = SG(t4) is formed in registers and never stored (the level-0 backward rebuilds it, nbp_dgrad_sg_rc_wg); out is
+ * bitwise the two-launch form's (nbp_gemm_bf16 CM_SG, then nbp_gemm_res_ln / CM_PLAIN with the residual). */
+int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5, const float* b5, const void* y,
+                 const float* gamma, const float* lnw, const float* lnb, void* out, void* nout, float* stats, int M,
+                 int C, float eps, int dtype, nbp_stream_t s);
 /* conv5 input gradient + SimpleGate backward with the gate input recomputed (bf16, N = K = C = 32: level 0, whose conv4
  * forward runs on the same skinny MFMA sequence): dg = A . Wt^T (the conv5 dgrad), t = A2 . W2^T + b2 rebuilt per tile (the conv4 forward: A2 = its input n2 [M][K],
  * W2 [2N][K] bf16 with SimpleGate pairs interleaved, b2 fp32), C[m][2c] = dg[c] t[2c+1], C[m][2c+1] = dg[c] t[2c]

@@ -26,7 +26,7 @@ namespace {
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3, AM_CONV = 4 };
 enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7,
-       CM_CHANDOT = 8, CM_SGBWD_RC = 9 };
+       CM_CHANDOT = 8, CM_SGBWD_RC = 9, CM_FFN = 10 };
 
 struct GemmPB {
   const void* A;
@@ -783,10 +783,20 @@ struct SkinnyP {
   float* slab_b2;
 };
 
+// CM_FFN (the level-0 NAFBlock FFN half, NAFNet_arch.py:74-80, N = K = 32): conv4 -> SimpleGate -> conv5 in one pass.
+// The conv4 weight / bias are held like CM_SGBWD_RC's (W2 / b2: 2N interleaved rows), A = n2; t = A W2^T + b2 is
+// formed on MFMA per 32-row tile exactly as the CM_SG kernel forms it, the gate g = t[2c] t[2c+1] (an fp32 product
+// rounded once to H, as CM_SG stores it) never leaves the registers: the two lanes of a pixel (l, l ^ 32) swap half of
+// their gates so each holds the 8 consecutive channels of a B-operand fragment, and conv5 (W = its weight) runs on
+// them.  The epilogue is CM_RESLN's (bias, layer-scale residual R + rscale v, the next LayerNorm when nout is given).
+// g2 (written and re-read by the two-launch form) is never stored: the level-0 backward rebuilds it from n2.
 template <int NT, int KS, int AMODE, int CMODE, typename H, bool WGF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WGF ? 2 : 1)))
 void gemm_skinny_kernel(SkinnyP<H> p) {
   constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
+  constexpr bool FFN = CMODE == CM_FFN;
+  static_assert(!FFN || (NT == 1 && KS == 2), "FFN fusion: the level-0 block (N = K = 32)");
+  constexpr bool RESLN = CMODE == CM_RESLN || FFN;
   constexpr bool RC = CMODE == CM_SGBWD_RC;
   static_assert(!WGF || (RC && NT == 1 && KS == 2), "weight-gradient fold: level-0 conv5 dgrad (N = K = 32)");
   constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : 8;  // bf16 row stride of the recomputed gate-input tile
@@ -798,11 +808,11 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   float* tileS = stage[threadIdx.x >> 6];
   H* tileT = stage2[threadIdx.x >> 6];
   const int M = p.M, N = p.N, K = p.K;
-  // RC: the conv4 weight (2N rows, K = the conv4 input width = this GEMM's K) and bias in registers
-  constexpr int NT2 = RC ? 2 * NT : 1;
+  // RC / FFN: the conv4 weight (2N rows, K = the conv4 input width = this GEMM's K) and bias in registers
+  constexpr int NT2 = RC || FFN ? 2 * NT : 1;
   vec_t<H, 8> w2[NT2][KS];
   float b2r[NT2][4][4];
-  if constexpr (RC) {
+  if constexpr (RC || FFN) {
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
 #pragma unroll
@@ -853,7 +863,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
     for (int e = 0; e < 8; ++e) vsum[ks][e] = 0.f;
-  if (CMODE == CM_RESLN) {  // aw / ab hold the LN weight / bias of this lane's 8 columns
+  if (RESLN && p.nout) {  // aw / ab hold the LN weight / bias of this lane's 8 columns
     const float4 w0 = ld4(p.lnw + ccol), w1 = ld4(p.lnw + ccol + 4), b0 = ld4(p.lnb_f + ccol), b1 = ld4(p.lnb_f + ccol + 4);
     aw[0] = w0.x; aw[1] = w0.y; aw[2] = w0.z; aw[3] = w0.w; aw[4] = w1.x; aw[5] = w1.y; aw[6] = w1.z; aw[7] = w1.w;
     ab[0] = b0.x; ab[1] = b0.y; ab[2] = b0.z; ab[3] = b0.w; ab[4] = b1.x; ab[5] = b1.y; ab[6] = b1.z; ab[7] = b1.w;
@@ -944,10 +954,46 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    if constexpr (FFN) {
+      // conv4: lane (r, h) gets pixel r's t channels 32 t2 + 8 g + 4 h + q (rows interleaved), i.e. the gates
+      // c = 16 t2 + 4 g + 2 h + {0, 1}
+      vec_t<H, 2> gp[NT2][4];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+      for (int t2 = 0; t2 < NT2; ++t2) {
+        floatx16 a2c;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mfma32x32x16(w[t][ks], a0[ks], acc[t]);
+        for (int i = 0; i < 16; ++i) a2c[i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a2c = mfma32x32x16(w2[t2][ks], a0[ks], a2c);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float pr0 = (a2c[4 * g] + b2r[t2][g][0]) * (a2c[4 * g + 1] + b2r[t2][g][1]);
+          float pr1 = (a2c[4 * g + 2] + b2r[t2][g][2]) * (a2c[4 * g + 3] + b2r[t2][g][3]);
+          asm volatile("" : "+v"(pr0), "+v"(pr1));  // an fp32 product, then one rounding (no fused mix-precision op)
+          gp[t2][g][0] = (H)pr0;
+          gp[t2][g][1] = (H)pr1;
+        }
+      }
+      // conv5's B fragment of K step ks = t2: lane h needs gates 16 t2 + 8 h + [0, 8); it holds g = 2h, 2h + 1 of
+      // them and its partner (lane ^ 32) the other two
+#pragma unroll
+      for (int t2 = 0; t2 < NT2; ++t2) {
+        const vec_t<H, 2> s0 = h ? gp[t2][0] : gp[t2][2], s1 = h ? gp[t2][1] : gp[t2][3];
+        const vec_t<H, 2> r0 = __builtin_bit_cast(vec_t<H, 2>, __shfl_xor(__builtin_bit_cast(int, s0), 32, 64));
+        const vec_t<H, 2> r1 = __builtin_bit_cast(vec_t<H, 2>, __shfl_xor(__builtin_bit_cast(int, s1), 32, 64));
+        const vec_t<H, 2> q0 = h ? r0 : gp[t2][0], q1 = h ? gp[t2][2] : r0;
+        const vec_t<H, 2> q2 = h ? r1 : gp[t2][1], q3 = h ? gp[t2][3] : r1;
+        vec_t<H, 8> bg;
+        bg[0] = q0[0]; bg[1] = q0[1]; bg[2] = q1[0]; bg[3] = q1[1];
+        bg[4] = q2[0]; bg[5] = q2[1]; bg[6] = q3[0]; bg[7] = q3[1];
+        acc[0] = mfma32x32x16(w[0][t2], bg, acc[0]);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma32x32x16(w[t][ks], a0[ks], acc[t]);
+    }
     // lane (r, h) owns pixel r, channels t*32 + 8g + 4h + {0..3}: stage as rows of the tile
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -977,8 +1023,10 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
           }
           *reinterpret_cast<vec_t<H, 4>*>(tileT + r * LDT2 + t * 32 + 8 * g + 4 * h) = o;
           if constexpr (WGF) {
-            g2h[t][g][0] = (H)(v[0] * v[1]);
-            g2h[t][g][1] = (H)(v[2] * v[3]);
+            float pr0 = v[0] * v[1], pr1 = v[2] * v[3];
+            asm volatile("" : "+v"(pr0), "+v"(pr1));  // the forward's gate: an fp32 product, then one rounding
+            g2h[t][g][0] = (H)pr0;
+            g2h[t][g][1] = (H)pr1;
           }
         }
       }
@@ -1080,7 +1128,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += bia[j];
       const long off = m * p.ldc + ccol;
-      if ((CMODE == CM_PLAIN || CMODE == CM_RESLN) && p.R) {
+      if ((CMODE == CM_PLAIN || RESLN) && p.R) {
         const vec_t<H, 8> rv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (float)rv[j] + rsc[j] * v[j];
@@ -1089,7 +1137,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (H)v[j];
       if (CMODE != CM_SG || p.C) *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;  // SG: t may be dropped (recomputed)
-      if constexpr (CMODE == CM_RESLN) {  // LayerNorm2d of the stored (bf16) row, as ln_fwd_nhwc computes it
+      if (RESLN && p.nout) {  // LayerNorm2d of the stored (bf16) row, as ln_fwd_nhwc computes it
         constexpr int G = 4 * NT;
         float xv[8], sm = 0.f, q = 0.f;
 #pragma unroll
@@ -1115,7 +1163,11 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
       if (CMODE == CM_SG) {  // g[c] = t[2c] * t[2c+1]: 4 gates of this chunk
         vec_t<H, 4> gv;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) gv[j] = (H)(v[2 * j] * v[2 * j + 1]);
+        for (int j = 0; j < 4; ++j) {
+          float pr = v[2 * j] * v[2 * j + 1];
+          asm volatile("" : "+v"(pr));  // an fp32 product, then one rounding (as CM_FFN forms the gate)
+          gv[j] = (H)pr;
+        }
         *reinterpret_cast<vec_t<H, 4>*>(p.aux + m * (p.ldc / 2) + ccol / 2) = gv;
       }
     }

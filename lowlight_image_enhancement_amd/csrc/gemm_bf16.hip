@@ -6,7 +6,7 @@
 // + residual for the up conv).  Weights come from a per-step bf16 copy of the flat parameter buffer; dgrads use
 // the transposed copy so every launch is NT.
 #include "gemm16_impl.h"
-
+#include "gemm16_entry.h"
 
 extern "C" {
 
@@ -39,21 +39,12 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   NBP_REQUIRE(a_mode != AM_S2D || K == 4 * cs, "nbp_gemm_bf16: S2D needs K == 4*cs");
   NBP_REQUIRE(c_mode != CM_D2S || N == 4 * cs, "nbp_gemm_bf16: D2S needs N == 4*cs");
   NBP_REQUIRE(a_mode == AM_S2D || lda % 8 == 0, "nbp_gemm_bf16: lda alignment");
-  GemmPB p{A, lda, a_scale, rows_per_img, Bw, ldb, C, ldc, M, N, K, gh, gw, cs, bias, R, rscale, pre};
-  hipStream_t st = S(s);
-  int rc = NBP_OK;
-  bool done = false;
-  NBP_DISPATCH_H(hd, {
-    if (h16 && getenv_skinny() &&
-        try_skinny<H>(A, lda, a_mode, a_scale, rows_per_img, Bw, ldb, C, ldc, c_mode, M, N, K, bias, R, rscale, pre, st))
-      done = true;
-    else if (!C) rc = NBP_ERR_ARG;
-    else if (a_dtype == 0 && c_dtype == 0) rc = dispatch_modes<float, float, H>(p, a_mode, c_mode, st);
-    else if (h16) rc = dispatch_modes<H, H, H>(p, a_mode, c_mode, st);
-    else if (a_dtype == 0) rc = dispatch_modes<float, H, H>(p, a_mode, c_mode, st);
-    else rc = dispatch_modes<H, float, H>(p, a_mode, c_mode, st);
-  });
-  if (done) return check_launch("gemm_bf16(skinny)");
+  // the tile dispatch of each 16-bit type lives in its own translation unit (gemm16_bf16.hip / gemm16_fp16.hip):
+  // the template instances of one type take minutes to compile, the two compile in parallel
+  const int rc = (hd == 2 ? nbp::gemm16_entry_fp16 : nbp::gemm16_entry_bf16)(
+      A, lda, a_mode, a_scale, rows_per_img, a_dtype, Bw, ldb, C, ldc, c_mode, c_dtype, M, N, K, gh, gw, cs, bias, R,
+      rscale, pre, S(s));
+  if (rc == 1) return check_launch("gemm_bf16(skinny)");
   NBP_REQUIRE(C, "nbp_gemm_bf16: C is null and the skinny path does not serve this shape");
   if (rc) return rc;
   return check_launch("gemm_bf16");
@@ -139,6 +130,23 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
     else launch_skinny<AM_PLAIN, CM_RESLN, H>(p, S(s));
   });
   return check_launch("gemm_res_ln");
+}
+
+int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5, const float* b5, const void* y,
+                 const float* gamma, const float* lnw, const float* lnb, void* out, void* nout, float* stats, int M,
+                 int C, float eps, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(n2 && W4 && b4 && W5 && b5 && y && gamma && out && M > 0, "nbp_gemm_ffn: bad args");
+  NBP_REQUIRE(!nout || (lnw && lnb && stats), "nbp_gemm_ffn: the next LayerNorm needs lnw, lnb, stats");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_gemm_ffn: 16-bit storage (dtype 1 bf16 / 2 fp16)");
+  NBP_REQUIRE(C == 32, "nbp_gemm_ffn: the fused FFN half serves C = 32 (C=%d)", C);
+  NBP_DISPATCH_H(dtype, {
+    SkinnyP<H> p{reinterpret_cast<const H*>(n2), C, nullptr, 1, reinterpret_cast<const H*>(W5), C,
+                 reinterpret_cast<H*>(out), C, M, C, C, b5, reinterpret_cast<const H*>(y), gamma, nullptr,
+                 nullptr, lnw, nullptr, nullptr, nullptr, lnb, reinterpret_cast<H*>(nout),
+                 reinterpret_cast<float2*>(stats), eps, nullptr, reinterpret_cast<const H*>(W4), b4};
+    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_FFN, H><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
+  });
+  return check_launch("gemm_ffn");
 }
 
 int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,

@@ -116,6 +116,9 @@ class NAFNet(nn.Module):
         # ... and with it folds conv5's U / V and conv4's weight / bias gradients into the same pass over dout / n2 /
         # dt (nbp_dgrad_sg_rc_wg) -- NBP_SG_RC_WG=0 leaves them to separate nbp_wgrad_f32 launches
         self.sg_rc_wg = os.environ.get("NBP_SG_RC_WG", "1") != "0"
+        # level 0 (C = 32) with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
+        # (nbp_gemm_ffn, bitwise the two launches), g2 never stored -- NBP_FFN=0: the two launches (A/B measurement)
+        self.fuse_ffn = os.environ.get("NBP_FFN", "1") != "0"
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
@@ -407,7 +410,9 @@ class NAFNet(nn.Module):
         # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
         # it (sg_rc) or there is no backward
         drop_t4 = dt != 0 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) == 3))
-        t4, g2 = (None if drop_t4 else E(M, 2 * c)), E(M, c)
+        # the fused FFN half (g2 never stored) wherever the backward rebuilds g2 too (nbp_dgrad_sg_rc_wg)
+        ffn = drop_t4 and self.fuse_ffn and len(self._W) == 3 and (tape is None or self.sg_rc_wg)
+        t4, g2 = (None if drop_t4 else E(M, 2 * c)), (None if ffn else E(M, c))
         out = E(M, c)
         carry_next = fuse_ln and next_pre is not None
         nn1, nst1 = (E(M, c), F(M, 2)) if carry_next else (None, None)
@@ -431,14 +436,22 @@ class NAFNet(nn.Module):
                      bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
             call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"),
                  n2, st2, M, c, LN_EPS, dt)
-        if dt != 0:  # SimpleGate in the GEMM epilogue
+        if ffn:
+            lnw, lnb = ((self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"))
+                        if carry_next else (None, None))
+            call("gemm_ffn", n2, self._slice(self._W[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"),
+                 self._slice(self._W[1], pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"), y,
+                 self._slice(P, pre + "gamma"), lnw, lnb, out, nn1, nst1, M, c, LN_EPS, dt)
+        elif dt != 0:  # SimpleGate in the GEMM epilogue
             self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_SG, M, 2 * c, c,
                      bias=self._slice(P, pre + "conv4.bias"), pre=g2)
         else:
             self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c,
                      c, bias=self._slice(P, pre + "conv4.bias"))
             call("sg_fwd", t4, g2, M, c, 1, dt)
-        if carry_next:
+        if ffn:
+            pass
+        elif carry_next:
             call("gemm_res_ln", g2, c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c,
                  out, M, c, c, self._slice(P, pre + "conv5.bias"), y, self._slice(P, pre + "gamma"),
                  self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"), nn1,
