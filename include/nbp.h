@@ -234,13 +234,9 @@ int nbp_sca_bwd(const float* da_slab, int chunks, const float* wsca, float* da, 
    the K = B nbp_wgrad_f32; NAFNet_arch.py:39-41,67). */
 int nbp_sca_bwd_fused(const float* da_slab, int chunks, const float* wsca, const float* mean, float* ds, float* dW,
                       float* db, int B, int C, nbp_stream_t s);
-/* 1 when the LDS-tiled depthwise kernels serve C channels at this dtype: then nbp_dw_sg_pool_fwd may be given
-   t2 = NULL (not stored) and the backward is nbp_sca_sg_dw_bwd_rec, which recomputes t2 from t1. */
+/* 1 when the LDS-tiled depthwise kernels serve C channels at this dtype (then nbp_dw_sg_pool_fwd may be given
+   t2 = NULL when no backward follows). */
 int nbp_dw_tiled(int C, int dtype);
-/* nbp_sca_sg_dw_bwd without a stored t2: t2 = conv2(t1) + bdw recomputed on the tile halo in LDS. */
-int nbp_sca_sg_dw_bwd_rec(const void* dh, const float* a, const float* ds, const void* t1, const float* wdw,
-                          const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C,
-                          int dtype, nbp_stream_t s);
 /* dg = dh*a + ds/HW, then SimpleGate backward into dt2 [M][2C]. */
 int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* t2, void* dt2, long M, int C, int HW,
                    int dtype, nbp_stream_t s);

@@ -10,20 +10,6 @@ extern "C" {
 // 16-bit y share the type `dtype` (1 bf16, 2 fp16); y is that type (y_dtype 1) or fp32 (y_dtype 0, mode 1 only).
 // dtype 0: x, w, R, y all fp32 (y_dtype 0).
 // Cin % 8 == 0 (pad the channel dimension), Cout % 8 == 0.
-// NBP_IM2COL_TAP=0: per-lane tap division in the 3x3 conv's DMA issue (A/B measurement; read per launch)
-static bool im2col_tap_tile() {
-  const char* e = getenv("NBP_IM2COL_TAP");
-  return !(e && e[0] == '0');
-}
-
-// NBP_CONV_MAP (read per launch; default 1): GemmPB::tile_map of the 3x3 convs.  XCD-contiguous M runs keep the
-// row overlaps of the taps between neighbouring tiles in one L2: +5-10 % on the 128 x 128 / 128 x 64 tiles of the
-// 64- and 128-channel VGG layers (scripts/conv_micro.py), neutral on the 256 x 256 tiles; bitwise equal.
-static int conv_tile_map() {
-  const char* e = getenv("NBP_CONV_MAP");
-  return e ? atoi(e) : 1;
-}
-
 int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w, int Cout, const float* bias, int mode,
                      const void* R, void* y, int y_dtype, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(x && w && y && B > 0 && H > 0 && W > 0, "nbp_conv3x3_bf16: bad args");
@@ -39,8 +25,8 @@ int nbp_conv3x3_bf16(const void* x, int B, int H, int W, int Cin, const void* w,
   NBP_REQUIRE(M < (1L << 31), "nbp_conv3x3_bf16: too many pixels");
   GemmPB p{x, 0, nullptr, 1, w, 9L * Cin, y, Cout, (int)M, Cout, 9 * Cin, H, W, Cin,
            mode == 2 ? nullptr : bias, mode == 2 ? R : nullptr, nullptr, nullptr};
-  p.tap_tile = Cin % 64 == 0 && im2col_tap_tile();
-  p.tile_map = conv_tile_map();
+  p.tap_tile = Cin % 64 == 0;  // a K-tile inside one tap: the tap is per stage, not a per-lane division
+  p.tile_map = 1;  // XCD-contiguous M runs: +5-10 % on the 128 x 128 / 128 x 64 VGG tiles
   hipStream_t st = S(s);
   if (dtype == 2) {
     using T16 = _Float16;

@@ -548,7 +548,7 @@ struct DwTileP {
   const void* t2;   // [M][2C]           (fused)
   const void* t1;   // [M][2C]
   const float* wdw; // [2C][9]
-  const float* bdw; // [2C]               (REC: the conv2 bias for the t2 recompute)
+  const float* bdw; // [2C]               (unused by the backward)
   void* dt1;        // [M][2C]
   float* slab_w;    // [rows][2C][9]
   float* slab_b;    // [rows][2C]
@@ -557,7 +557,6 @@ struct DwTileP {
 };
 
 constexpr int DWT_TH = 16;
-constexpr int DWT_TH_REC = 12;
 inline int dw_bwd_tw(int W) { return W >= 32 ? 32 : 16; }
 
 template <typename T>
@@ -594,24 +593,21 @@ __device__ __forceinline__ void unpack16(uint4 r, float* f) {
   }
 }
 
-// REC (with FUSED): t2 is not read from HBM either - the forward never stored it.  t1 is staged with a two-pixel
-// halo, t2 = bias + conv(t1) is recomputed into LDS on the one-pixel halo (the forward's FMA order), and the SCA /
-// SimpleGate backward turns it into dt2 in place.  Shorter tiles (TH 12) keep two blocks per CU.
-template <typename T, bool FUSED, int DWT_TW, bool REC>
+// (A variant that recomputed t2 from t1 in LDS instead of reading it, so that the forward need not store it, measured
+// neutral to slower and was removed in round 4.)
+template <typename T, bool FUSED, int DWT_TW>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
   constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
   constexpr int HS = CSL / 2;            // gate channels per slice
   constexpr int NQ = CSL / 4;            // channel quads per slice
   constexpr int NT = NQ * DWT_TW;        // threads
-  constexpr int TH = REC ? DWT_TH_REC : DWT_TH;
-  constexpr int XO = REC ? 1 : 0;        // extra t1 halo
+  constexpr int TH = DWT_TH;
   constexpr int LW = DWT_TW + 2, LH = TH + 2;
-  constexpr int LWX = LW + 2 * XO, LHX = LH + 2 * XO;
   __shared__ __attribute__((aligned(16))) T sg[LH * LW * CSL];
-  __shared__ __attribute__((aligned(16))) T sx[LHX * LWX * CSL];
+  __shared__ __attribute__((aligned(16))) T sx[LH * LW * CSL];
   // t1 at (row, col) of the one-pixel-halo frame
-  auto SX = [&](int row, int col) { return sx + ((row + XO) * LWX + col + XO) * CSL; };
+  auto SX = [&](int row, int col) { return sx + (row * LW + col) * CSL; };
   const int tid = threadIdx.x;
   const int u = xcd_remap(blockIdx.x, gridDim.x);  // the slices of one tile share an XCD (and its L2)
   const int slice = u % p.slices, tile = (u / p.slices) % p.tiles, b = u / (p.slices * p.tiles);
@@ -632,7 +628,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   // ---- stage t1 (and dt2 when unfused): 4 chunks per pixel = 2 halves x 2 chunks.  Every load of the stage is
   // issued before the first LDS store (register batches): one memory latency per tile instead of one per pass.
   constexpr int TOT2 = LH * LW * 2, N2 = FUSED ? (TOT2 + NT - 1) / NT : 1;
-  uint4 rd[N2], ra[REC ? 1 : N2], rb[REC ? 1 : N2];
+  uint4 rd[N2], ra[N2], rb[N2];
   // addressing: 64-bit element index of the staging frame's origin pixel once per tile, then 32-bit in-frame offsets
   // from 24-bit multiplies (full-rate v_mul_u32_u24; the launcher bounds W * 2C < 2^24) -- no per-load 64-bit or
   // 32 x 32 multiplies
@@ -640,8 +636,8 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
   {
     const T* t1 = reinterpret_cast<const T*>(p.t1);
     const T* dt2 = reinterpret_cast<const T*>(p.dt2);
-    constexpr int TOT1 = LHX * LWX * 4, N1 = (TOT1 + NT - 1) / NT;
-    const long e1 = (img + (long)(y0 - 1 - XO) * W + (x0 - 1 - XO)) * C2 + cbase;
+    constexpr int TOT1 = LH * LW * 4, N1 = (TOT1 + NT - 1) / NT;
+    const long e1 = (img + (long)(y0 - 1) * W + (x0 - 1)) * C2 + cbase;
     uint4 vx[N1], vg[FUSED ? 1 : N1];
 #pragma unroll
     for (int it = 0; it < N1; ++it) {
@@ -649,8 +645,8 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       vx[it] = make_uint4(0, 0, 0, 0);
       if (!FUSED) vg[it] = make_uint4(0, 0, 0, 0);
       const int pix = i >> 2, hh = (i >> 1) & 1, k = i & 1;
-      const int py = pix / LWX, px = pix % LWX;
-      const int gy = y0 - 1 - XO + py, gx = x0 - 1 - XO + px;
+      const int py = pix / LW, px = pix % LW;
+      const int gy = y0 - 1 + py, gx = x0 - 1 + px;
       if (i < TOT1 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
         const long go = e1 + (long)(__umul24(py, rs1) + __umul24(px, C2) + hh * C + k * E);
         vx[it] = *reinterpret_cast<const uint4*>(t1 + go);
@@ -668,15 +664,12 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
         const int pix = i >> 1, k = i & 1;
         const int py = pix / LW, px = pix % LW;
         const int gy = y0 - 1 + py, gx = x0 - 1 + px;
-        rd[it] = make_uint4(0, 0, 0, 0);
-        if (!REC) ra[it] = rb[it] = make_uint4(0, 0, 0, 0);
+        rd[it] = ra[it] = rb[it] = make_uint4(0, 0, 0, 0);
         if (i < TOT2 && gy >= 0 && gy < H && gx >= 0 && gx < W) {
           rd[it] = *reinterpret_cast<const uint4*>(dh + eh + (long)(__umul24(py, rsh) + __umul24(px, C) + k * E));
-          if (!REC) {
-            const long o = e2 + (long)(__umul24(py, rs1) + __umul24(px, C2) + k * E);
-            ra[it] = *reinterpret_cast<const uint4*>(t2 + o);
-            rb[it] = *reinterpret_cast<const uint4*>(t2 + o + C);
-          }
+          const long o = e2 + (long)(__umul24(py, rs1) + __umul24(px, C2) + k * E);
+          ra[it] = *reinterpret_cast<const uint4*>(t2 + o);
+          rb[it] = *reinterpret_cast<const uint4*>(t2 + o + C);
         }
       }
     }
@@ -691,25 +684,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       }
     }
   }
-  if (REC) {
-    // t2 on the one-pixel-halo frame into sg: thread = (quad q, column), rows in steps (FMA order of the forward)
-    lds_barrier();
-    const float4 bq = ld4(p.bdw + gc);
-    for (int pix = x; pix < LH * LW; pix += DWT_TW) {
-      const int row = pix / LW, col = pix % LW;
-      f2v a0 = f2v{bq.x, bq.y}, a1 = f2v{bq.z, bq.w};
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        f2v v0, v1;
-        ldq2(SX(row + t / 3 - 1, col + t % 3 - 1) + lc, v0, v1);
-        a0 = __builtin_elementwise_fma(wk[t][0], v0, a0);
-        a1 = __builtin_elementwise_fma(wk[t][1], v1, a1);
-      }
-      stq(sg + pix * CSL + lc, make_float4(a0.x, a0.y, a1.x, a1.y));
-    }
-  }
   if (FUSED) {
-    if (REC) lds_barrier();
     // NT is even, so this thread's chunk k = tid & 1 (and its E channels) is the same in every pass: a and ds / HW once
     static_assert(NT % 2 == 0, "chunk parity per thread");
     float ak[E], sk[E];
@@ -730,13 +705,8 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       const bool inside = gy >= 0 && gy < H && gx >= 0 && gx < W;
       float d[E], ta[E], tb[E], lo[E], hi[E];
       unpack16<T>(rd[it], d);
-      if (REC) {
-        ld16f(sg + pix * CSL + k * E, ta);
-        ld16f(sg + pix * CSL + HS + k * E, tb);
-      } else {
-        unpack16<T>(ra[it], ta);
-        unpack16<T>(rb[it], tb);
-      }
+      unpack16<T>(ra[it], ta);
+      unpack16<T>(rb[it], tb);
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         const float dg = inside ? fmaf(d[j], ak[j], sk[j]) : 0.f;
@@ -881,11 +851,8 @@ struct DwFwdP {
 // tile width: 64 / 32 / 16 columns by image width; fp32 (2 gate quads per slice) never below 32 (whole waves)
 inline int dw_fwd_tw(int W, int dtype) { return W >= 64 ? 64 : ((W >= 32 || dtype == 0) ? 32 : 16); }
 // tile height: 16 rows, 8 at the small deep-level images (W <= 32: 2x the blocks, half of each thread's serial
-// row chain; the extra halo rows are L2 hits).  NBP_DW_FWD_TH overrides the small-image height (A/B measurement).
-inline int dw_fwd_th(int W) {
-  static const int small = getenv("NBP_DW_FWD_TH") ? atoi(getenv("NBP_DW_FWD_TH")) : 8;
-  return W <= 32 && (small == 4 || small == 8) ? small : DWT_TH;  // the instantiated heights
-}
+// row chain; the extra halo rows are L2 hits)
+inline int dw_fwd_th(int W) { return W <= 32 ? 8 : DWT_TH; }
 int dw_fwd_tiles(int H, int W, int dtype) { return cdiv(H, dw_fwd_th(W)) * cdiv(W, dw_fwd_tw(W, dtype)); }
 
 template <typename T, int TW, int TH = DWT_TH>
@@ -976,7 +943,7 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
     const float4 aa = make_float4(a2[0].x, a2[0].y, a2[1].x, a2[1].y);
     const float4 ab = make_float4(b2[0].x, b2[0].y, b2[1].x, b2[1].y);
     if (col_ok && y0 + r < H) {
-      if (t2p) {  // null when the backward recomputes t2 (nbp_sca_sg_dw_bwd_rec)
+      if (t2p) {  // null: t2 not kept (no backward follows)
         T* q2 = t2p + (unsigned)r * rs1;
         stq(q2 + gca, aa);
         stq(q2 + gcb, ab);
@@ -1010,8 +977,8 @@ __global__ __launch_bounds__(256) void dw_sg_pool_tiled(DwFwdP p) {
 }
 
 // backward tile height: 16 rows (8-row tiles were measured neutral at W <= 32 and at every width: DESIGN §5)
-int dw_tiles(int H, int W, bool rec = false) {
-  return cdiv(H, rec ? DWT_TH_REC : DWT_TH) * cdiv(W, dw_bwd_tw(W));
+int dw_tiles(int H, int W) {
+  return cdiv(H, DWT_TH) * cdiv(W, dw_bwd_tw(W));
 }
 bool dw_tiled_ok(int C, int dtype) { return C % (dtype != 0 ? 16 : 8) == 0; }
 
@@ -1049,8 +1016,7 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   NBP_REQUIRE((long)W * 2 * C < (1L << 24), "depthwise backward: W * 2C must be < 2^24 (24-bit tile offsets)");
   const int hs = dtype != 0 ? 16 : 8;
   const int tw = dw_bwd_tw(W);
-  const bool rec = dh != nullptr && t2 == nullptr;  // fused, t2 recomputed from t1
-  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, bdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W, rec),
+  DwTileP p{dt2, dh, a, ds, t2, t1, wdw, bdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W),
             C / hs, 1.f / (float)(H * W)};
   const long nrow = (long)B * p.tiles;
   p.slab_w = ws;
@@ -1061,13 +1027,11 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   NBP_DISPATCH_T(dtype, {
     constexpr int NQ = (64 / sizeof(T)) / 4;
     if (tw == 32) {
-      if (rec) dw_bwd_tiled<T, true, 32, true><<<nblk, NQ * 32, 0, S(s)>>>(p);
-      else if (fused) dw_bwd_tiled<T, true, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
-      else dw_bwd_tiled<T, false, 32, false><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      if (fused) dw_bwd_tiled<T, true, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
     } else {
-      if (rec) dw_bwd_tiled<T, true, 16, true><<<nblk, NQ * 16, 0, S(s)>>>(p);
-      else if (fused) dw_bwd_tiled<T, true, 16, false><<<nblk, NQ * 16, 0, S(s)>>>(p);
-      else dw_bwd_tiled<T, false, 16, false><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      if (fused) dw_bwd_tiled<T, true, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      else dw_bwd_tiled<T, false, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
     }
   });
   int rc = check_launch("dw_bwd_tiled");
@@ -1113,10 +1077,8 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
       // whole waves only (the column reduction shuffles across all 64 lanes): fp32 uses TW >= 32
       const int th = dw_fwd_th(W);
       if (tw == 64) dw_sg_pool_tiled<T, 64><<<nblk, NQG * 64, 0, S(s)>>>(p);
-      else if ((tw == 32 || NQG * 16 < 64) && th == 4) dw_sg_pool_tiled<T, 32, 4><<<nblk, NQG * 32, 0, S(s)>>>(p);
       else if ((tw == 32 || NQG * 16 < 64) && th == 8) dw_sg_pool_tiled<T, 32, 8><<<nblk, NQG * 32, 0, S(s)>>>(p);
       else if (tw == 32 || NQG * 16 < 64) dw_sg_pool_tiled<T, 32><<<nblk, NQG * 32, 0, S(s)>>>(p);
-      else if (th == 4) dw_sg_pool_tiled<T, 16, 4><<<nblk, NQG * 16, 0, S(s)>>>(p);
       else if (th == 8) dw_sg_pool_tiled<T, 16, 8><<<nblk, NQG * 16, 0, S(s)>>>(p);
       else dw_sg_pool_tiled<T, 16><<<nblk, NQG * 16, 0, S(s)>>>(p);
     });
@@ -1205,8 +1167,7 @@ int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* 
 }
 
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
-  const size_t tr = dw_tiles(H, W, true), tp = dw_tiles(H, W, false);
-  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * (tr > tp ? tr : tp);
+  const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * dw_tiles(H, W);
   return (a > t ? a : t) * 2 * C * 10;
 }
 
@@ -1241,19 +1202,10 @@ int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const voi
   NBP_REQUIRE(dh && a && ds && t2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
               "nbp_sca_sg_dw_bwd: bad args");
   NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd: C must be a multiple of %d", dtype != 0 ? 16 : 8);
-  NBP_REQUIRE(t2, "nbp_sca_sg_dw_bwd: t2 required (nbp_sca_sg_dw_bwd_rec recomputes it)");
   return launch_dw_tiled(nullptr, dh, a, ds, t2, t1, wdw, nullptr, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
 }
 
 int nbp_dw_tiled(int C, int dtype) { return dw_tiled_ok(C, dtype) ? 1 : 0; }
 
-int nbp_sca_sg_dw_bwd_rec(const void* dh, const float* a, const float* ds, const void* t1, const float* wdw,
-                          const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C,
-                          int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(dh && a && ds && t1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
-              "nbp_sca_sg_dw_bwd_rec: bad args");
-  NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd_rec: C must be a multiple of %d", dtype != 0 ? 16 : 8);
-  return launch_dw_tiled(nullptr, dh, a, ds, nullptr, t1, wdw, bdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
-}
 
 }  // extern "C"

@@ -1132,15 +1132,6 @@ void grad_reduce(const float* slab, int S, long L, float* out, hipStream_t st) {
   launch_multi(std::vector<RDesc>{make_rdesc(slab, S, L, out)}, st);
 }
 
-// NBP_LS_FUSE=0 keeps the layer-scale post-op as its own launch after the reductions (A/B measurement)
-bool getenv_ls_fuse() {
-  static const bool on = [] {
-    const char* v = getenv("NBP_LS_FUSE");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 void flush_pending() {
   for (double& v : g_stats_flush) v = 0;
   // a post-op whose U and V are both reductions of this flush becomes a layer-scale row descriptor of the same launch
@@ -1152,7 +1143,7 @@ void flush_pending() {
       if (g_pending[i].out == p.U) iu = i;
       if (g_pending[i].out == p.V) iv = i;
     }
-    const bool ok = getenv_ls_fuse() && iu >= 0 && iv >= 0 && p.K % 4 == 0 && p.K <= 1024 &&
+    const bool ok = iu >= 0 && iv >= 0 && p.K % 4 == 0 && p.K <= 1024 &&
                     g_pending[iu].L == (long)p.N * p.K && g_pending[iv].L == p.N &&
                     (reinterpret_cast<uintptr_t>(g_pending[iu].slab) & 15) == 0 &&
                     (reinterpret_cast<uintptr_t>(p.W) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.dW) & 15) == 0;
@@ -1195,8 +1186,8 @@ bool wide_wgrad(int N, int K) { return N % 128 == 0 && K % 128 == 0; }
 // split-M count: enough blocks to fill the chip (~1024), >= 256 rows per split, and fp32 slab bytes
 // (S * N * K * 4, written once and read once by the reduction) no larger than the operand bytes M * (N + K) * 2.
 int wgrad_splits(int M, int N, int K) {
-  if (wide_wgrad(N, K)) {  // 128 x 128 tiles: ~256 workgroups (NBP_WIDE_TARGET), >= 256 rows per split
-    static const long target = getenv("NBP_WIDE_TARGET") ? atol(getenv("NBP_WIDE_TARGET")) : 256;
+  if (wide_wgrad(N, K)) {  // 128 x 128 tiles: ~256 workgroups, >= 256 rows per split
+    constexpr long target = 256;
     const long tiles = (long)(N / 128) * (K / 128);
     long s = (target + tiles - 1) / tiles;
     const long maxs = M / 256 > 1 ? M / 256 : 1;
@@ -1296,14 +1287,9 @@ long wgroup_target() {
   return v;
 }
 
-// NBP_WGRAD_RM (read per launch; 64 default or 32): row-stage height of the narrow (N or K <= 64) weight-gradient
-// tiles.  64 measured +0.3 % at cfg2 (1214.0 -> 1217.9 img/s over three A/B pairs, profiles/r02_v6/ab_wgrad_rm.txt),
-// bitwise equal (tests/test_gpu_glds.py::test_narrow_wgrad_stage_height); 128-row and double-buffered 64-row stages
-// were measured slower and removed
-int wgrad_rm() {
-  const char* e = getenv("NBP_WGRAD_RM");
-  return e && atoi(e) == 32 ? 32 : 64;
-}
+// Row-stage height of the narrow (N or K <= 64) weight-gradient tiles: 64 (measured +0.3 % at cfg2 over 32-row
+// stages, bitwise equal, profiles/r02_v6/ab_wgrad_rm.txt; 128-row and double-buffered 64-row stages were measured
+// slower).  32-row stages remain where a per-image scale block is not a multiple of 64 rows.
 
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
 // launch (A/B measurement; tests compare the paths in one process)
@@ -1415,10 +1401,9 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
       else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN && wgrad_rm() == 64)
+      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN) wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H><<<grid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0 && wgrad_rm() >= 64)
+      else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0)
         wgrad_bf16_kernel<AM_PLAIN, 3, H, 64><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 32 == 0)
         wgrad_bf16_kernel<AM_PLAIN, 3, H><<<grid, 256, 0, st>>>(p);

@@ -6,7 +6,7 @@ namespace nbp {
 int gemm16_entry_fp16(NBP_GEMM16_ENTRY_ARGS) {
   using H = _Float16;
   const bool h16 = a_dtype != 0 && c_dtype != 0;
-  if (h16 && getenv_skinny() &&
+  if (h16 &&
       try_skinny<H>(A, lda, a_mode, a_scale, rows_per_img, Bw, ldb, C, ldc, c_mode, M, N, K, bias, R, rscale, pre, st))
     return 1;
   if (!C) return NBP_ERR_ARG;

@@ -1313,15 +1313,8 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
 long skinny_blocks(long M) {
   const long ntiles = (M + 31) / 32;
   const long blocks = (ntiles + 3) / 4;
-  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs (NBP_SKINNY_BLOCKS overrides: A/B measurement)
-  static const long cap = [] {
-    const long v = getenv("NBP_SKINNY_BLOCKS") ? atol(getenv("NBP_SKINNY_BLOCKS")) : 1024L;
-    if (v < 1 || v > 8192) {
-      fprintf(stderr, "NBP_SKINNY_BLOCKS=%ld out of [1, 8192]: using 1024\n", v);
-      return 1024L;
-    }
-    return v;
-  }();
+  // 4 blocks (16 waves) resident per CU: one round over the 256 CUs (768 / 1536 / 2048 measured within +-0.5 %)
+  constexpr long cap = 1024;
   return blocks > cap ? cap : blocks;
 }
 
@@ -1394,13 +1387,12 @@ __global__ void transpose_bf16_kernel(const float* __restrict__ src, const long*
   }
 }
 
-// NBP_GLDS: 0 = register-staged tiles only, 2 / 3 = LDS-DMA ring depth for 16-bit A (A/B measurement; read per launch
-// so a test can compare both paths in one process).  Default 2: at the deep-level shapes (scripts/gemm_probe.py) the
-// 3-deep ring's extra LDS costs more in blocks per CU than the second tile in flight buys.
-// Unset (default): chosen per launch by glds_auto_depth.
+// NBP_GLDS=0 (read per launch): the register-staged tiles instead of the LDS-DMA ones -- the reference path of the
+// bitwise tests (tests/test_gpu_glds.py: same tiles, fragment order and MFMA sequence).  Unset: LDS-DMA, the ring
+// depth chosen per launch by glds_auto_depth.
 int glds_depth() {
   const char* e = getenv("NBP_GLDS");
-  return e ? atoi(e) : -1;
+  return e && e[0] == '0' ? 0 : -1;
 }
 
 int cu_count() {
@@ -1426,12 +1418,6 @@ int glds_auto_depth(long blocks, int stage_bytes, int c_bytes, int nmax) {
   return 2;
 }
 
-// NBP_GEMM_WAVES: 8 (default: 2 x 4 waves, two per SIMD, on tiles with BN >= 128) or 4 (2 x 2) for the LDS-DMA
-// kernel (A/B, read per launch: 8 waves + 128 x 128 tiles from 512 workgroups = +2 % step over 4 waves + 1024)
-int gemm_waves() {
-  const char* e = getenv("NBP_GEMM_WAVES");
-  return e && atoi(e) == 4 ? 4 : 8;
-}
 
 template <int BM, int BN, int AMODE, int CMODE, typename TA, typename TC, typename H>
 void launch(const GemmPB& p, hipStream_t st) {
@@ -1449,12 +1435,11 @@ void launch(const GemmPB& p, hipStream_t st) {
       constexpr int NMAX = 4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
       const int nd = ns_env < 0 ? glds_auto_depth((long)grid.x * grid.y, STB, CB, NMAX) : (ns < NMAX ? ns : NMAX);
       if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
-        if (gemm_waves() == 8) {  // 2 x 4 waves of (BM / 2) x (BN / 4): two waves per SIMD
-          if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-          return;
-        }
+        // 2 x 4 waves of (BM / 2) x (BN / 4), two per SIMD (+2 % step over 2 x 2 waves)
+        if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+        else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+        else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+        return;
       }
       if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
@@ -1470,24 +1455,13 @@ void launch(const GemmPB& p, hipStream_t st) {
 
 // largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 512 blocks (2 per CU; with the
 // 8-wave DMA tiles: 1024 with the register-staged 4-wave kernel measured best); otherwise 64x64, the most blocks.
-// NBP_GEMM_MINBLK overrides the block-count threshold (A/B measurement)
-long gemm_minblk() {
-  static const long v = [] {
-    const char* e = getenv("NBP_GEMM_MINBLK");
-    return e ? atol(e) : 512L;
-  }();
-  return v;
-}
+constexpr long GEMM_MINBLK = 512;
 
-// NBP_CONV_TILE (read per launch; default 4, 0 = off): 256 x 256 tiles on 8 waves (2 x 4, 128 x 64 each; two-pass
-// epilogue) for the 3x3 implicit-GEMM convs with N >= 256 while the grid still has >= 256 workgroups.  Measured
-// (scripts/conv_micro.py, fp16, bs 8): +34-39 % on the 128^2 x 256 and 64^2 x 512 VGG layers (629 -> 842, 659 -> 913
-// TFLOP/s; bitwise equal: the same MFMA sequence per output element).  The other 256-row shapes (256 x 64, 256 x 128,
-// 32-wide K-tiles) were measured neutral or slower and removed.
-int conv_tile() {
-  const char* e = getenv("NBP_CONV_TILE");
-  return e ? atoi(e) : 4;
-}
+// 256 x 256 tiles on 8 waves (2 x 4, 128 x 64 each; two-pass epilogue) for the 3x3 implicit-GEMM convs with N >= 256
+// while the grid still has >= 256 workgroups.  Measured (scripts/conv_micro.py, fp16, bs 8): +34-39 % on the 128^2 x
+// 256 and 64^2 x 512 VGG layers (629 -> 842, 659 -> 913 TFLOP/s; bitwise equal: the same MFMA sequence per output
+// element).  The other 256-row shapes (256 x 64, 256 x 128, 32-wide K-tiles) were measured neutral or slower
+//  and removed.
 
 template <int AMODE, int CMODE, typename TA, typename TC, typename H>
 bool launch_conv_big(const GemmPB& p, hipStream_t st) {
@@ -1495,7 +1469,7 @@ bool launch_conv_big(const GemmPB& p, hipStream_t st) {
                 CMODE != CM_RESLN) {
     const int ns = glds_depth();
     if ((ns >= 0 && ns < 2) || p.K <= 32 || p.ldb % 8 || p.cs % 8) return false;
-    if ((conv_tile() & 4) && p.N >= 256 && (long)cdiv(p.M, 256) * cdiv(p.N, 256) >= 256) {
+    if (p.N >= 256 && (long)cdiv(p.M, 256) * cdiv(p.N, 256) >= 256) {
       // 256 x 256 tiles on 2 x 4 waves (128 x 64 each): twice the MFMA work per staged byte of the 128 x 128 tile
       const dim3 grid(cdiv(p.M, 256), cdiv(p.N, 256));
       gemm_glds_kernel<256, 256, 2, AMODE, CMODE, TC, H, 4, 2><<<grid, 512, 0, st>>>(p);
@@ -1513,7 +1487,7 @@ void dispatch(const GemmPB& p, hipStream_t st) {
   } else {
     auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
     const bool n128 = p.N > 64, m128 = p.M > 64;
-    const long mb = gemm_minblk();
+    const long mb = GEMM_MINBLK;
     if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC, H>(p, st);
     else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC, H>(p, st);
     else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC, H>(p, st);
@@ -1521,14 +1495,6 @@ void dispatch(const GemmPB& p, hipStream_t st) {
   }
 }
 
-// NBP_SKINNY=0 disables the skinny path (A/B measurement)
-bool getenv_skinny() {
-  static const bool on = [] {
-    const char* v = getenv("NBP_SKINNY");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
 
 template <typename TA, typename TC, typename H>
 int dispatch_modes(const GemmPB& p, int a_mode, int c_mode, hipStream_t st) {

@@ -20,7 +20,7 @@ int nbp_gemm_bf16(const void* A, long lda, int a_mode, const float* a_scale, int
   const int hd = (a_dtype == 2 || c_dtype == 2) ? 2 : 1;
   const bool h16 = a_dtype != 0 && c_dtype != 0;
   // C may be null only for the skinny SimpleGate forward (the gate input is then recomputed by the backward)
-  NBP_REQUIRE(C || (c_mode == CM_SG && h16 && N <= 64 && K <= 128 && getenv_skinny()), "nbp_gemm_bf16: C is null");
+  NBP_REQUIRE(C || (c_mode == CM_SG && h16 && N <= 64 && K <= 128), "nbp_gemm_bf16: C is null");
   NBP_REQUIRE(K % 8 == 0 && N % 4 == 0 && ldb % 8 == 0, "nbp_gemm_bf16: K, ldb multiples of 8, N of 4 (K=%d N=%d)", K, N);
   NBP_REQUIRE(a_mode >= 0 && a_mode <= 2 && (c_mode == CM_PLAIN || c_mode == CM_D2S || c_mode == CM_SG ||
               c_mode == CM_SGBWD || c_mode == CM_CHANDOT), "nbp_gemm_bf16: mode");

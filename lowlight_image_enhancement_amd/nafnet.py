@@ -19,7 +19,6 @@ tensors the backward needs in a tape.
 from __future__ import annotations
 
 import math
-import os
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -92,42 +91,33 @@ class NAFNet(nn.Module):
         self._init_reference_like()
         self.grad_ready_hook: Optional[Callable[[Stage], None]] = None
         self._keep: Optional[List[torch.Tensor]] = None  # slabs awaiting a deferred gradient reduction
-        # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec)
-        self.dw_rec = os.environ.get("NBP_DW_REC", "0") == "1"
-        # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64, 128} (NBP_FUSE_LN_FWD=0: standalone ln_fwd)
-        self.fuse_ln_fwd = os.environ.get("NBP_FUSE_LN_FWD", "1") != "0"
-        # SCA channel dot in the conv3 dgrad epilogue at C > 64 (NBP_FUSE_CHANDOT=0: standalone img_chan_dot)
-        self.fuse_chandot = os.environ.get("NBP_FUSE_CHANDOT", "1") != "0"
-        # LayerNorm backward in the conv4 / conv1 dgrad epilogue at C = 128 (NBP_FUSE_LN_BWD128=0: standalone ln_bwd)
-        self.fuse_ln_bwd128 = os.environ.get("NBP_FUSE_LN_BWD128", "1") != "0"
-        # the LayerNorm fusions at C = 256 too (64 x 256 tiles): NBP_FUSE_LN256 = 1 (both, default: +1.1 % with the
-        # 8-wave LDS-DMA tiles; round 1 with register-staged tiles: fwd -0.4 %, bwd +0.35 %), bwd, fwd or 0
-        self.fuse_ln256 = os.environ.get("NBP_FUSE_LN256", "1")
+        # Fused / folded forms of the executor, all on (each measured faster; the environment knobs that
+        # toggled them for A/B runs were removed in round 4).  The attributes stay so that the GPU tests can compare
+        # a fused form bit for bit with its unfused one on the same network.
+        # LayerNorm forward in the conv3 / conv5 epilogues at C in {32, 64, 128, 256}
+        self.fuse_ln_fwd = True
         # the wide (C >= 128) weight gradients of a whole U-Net level (conv5's U, conv4, conv3's U, conv1 of every
         # NAFBlock of the level) queued during the level's backward and launched as ONE grouped launch at its end,
-        # with M-splits chosen for the group (NBP_GROUP_WGRAD=0: one launch per weight gradient)
-        self.group_wgrad = os.environ.get("NBP_GROUP_WGRAD", "1") != "0"
+        # with M-splits chosen for the group (False: one launch per weight gradient)
+        self.group_wgrad = True
         self._grouping = False
         # level 0 (C = 32): the conv4 output t4 is not stored; the conv5 dgrad rebuilds it per tile on MFMA
-        # (nbp_dgrad_sg_rc, bitwise equal) -- NBP_SG_RC=0 stores and re-reads it
-        self.sg_rc = os.environ.get("NBP_SG_RC", "1") != "0"
-        # the rebuild lives in the skinny GEMM path (NBP_SKINNY=0 turns that path off, and with it the t4 drop)
-        self.sg_rc = self.sg_rc and os.environ.get("NBP_SKINNY", "1")[:1] != "0"
-        # ... and with it folds conv5's U / V and conv4's weight / bias gradients into the same pass over dout / n2 /
-        # dt (nbp_dgrad_sg_rc_wg) -- NBP_SG_RC_WG=0 leaves them to separate nbp_wgrad_f32 launches
-        self.sg_rc_wg = os.environ.get("NBP_SG_RC_WG", "1") != "0"
-        # level 0 (C = 32) with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
-        # (nbp_gemm_ffn, bitwise the two launches), g2 never stored -- NBP_FFN=0: the two launches (A/B measurement)
-        self.fuse_ffn = os.environ.get("NBP_FFN", "1") != "0"
+        # (nbp_dgrad_sg_rc, bitwise equal) ...
+        self.sg_rc = True
+        # ... and folds conv5's U / V and conv4's weight / bias gradients into the same pass over dout / n2 / dt
+        # (nbp_dgrad_sg_rc_wg; False: separate nbp_wgrad_f32 launches)
+        self.sg_rc_wg = True
+        # level 0 with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
+        # (nbp_gemm_ffn, bitwise the two launches), g2 never stored
+        self.fuse_ffn = __import__("os").environ.get("NBP_FFN", "1") != "0"  # TEMP: A/B of the fusion (round 4)
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
         # image_restoration_model.py:255; the trainer adds GradScaler-style dynamic loss scaling for it).
         self.precision = "fp32"
-        # bf16 mode: the layer scales beta / gamma are folded into the transposed conv3 / conv5 weight copies (the
+        # 16-bit modes: the layer scales beta / gamma are folded into the transposed conv3 / conv5 weight copies (the
         # dgrad operands: dh = (beta (.) dy) W3 = dy (diag(beta) W3)), so those dgrads read A unscaled
-        # (NBP_FOLD_LS=0: A-column scale in the GEMM instead)
-        self.fold_ls = os.environ.get("NBP_FOLD_LS", "1") != "0"
+        self.fold_ls = True
 
         def _scale_off(k):
             if not self.fold_ls:
@@ -395,16 +385,12 @@ class NAFNet(nn.Module):
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
-        fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and (c in (32, 64, 128) or
-                                                                           (c == 256 and self.fuse_ln256 in ("1", "fwd")))
+        fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and c in (32, 64, 128, 256)
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
-        # NBP_DW_REC=1: t2 not stored, the backward recomputes it from t1 (nbp_sca_sg_dw_bwd_rec).  Off by default:
-        # measured slower at cfg2 (L0 dw backward 138 -> 211 us vs 25 us saved in the forward; profiles/r01_v9)
-        rec = self.dw_rec and query("dw_tiled", c, dt) == 1
         chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
-        t1, t2, g, pool = E(M, 2 * c), (None if rec else E(M, 2 * c)), E(M, c), F(B * chunks * c)
+        t1, t2, g, pool = E(M, 2 * c), E(M, 2 * c), E(M, c), F(B * chunks * c)
         mean, a = F(B, c), F(B, c)
         y, n2, st2 = E(M, c), E(M, c), F(M, 2)
         # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
@@ -663,8 +649,7 @@ class NAFNet(nn.Module):
              self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
         # conv4 input gradient + norm2 backward + residual
         # LN backward in the dgrad's epilogue (dn never stored): skinny kernel at C 32 / 64, 64 x 128 tiles at 128
-        fuse_ln = dt != 0 and (c in (32, 64) or (c == 128 and self.fuse_ln_bwd128) or
-                               (c == 256 and self.fuse_ln256 in ("1", "bwd")))
+        fuse_ln = dt != 0 and c in (32, 64, 128, 256)
         dy = E(M, c)
         if not wg_folded:
             self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
@@ -686,7 +671,7 @@ class NAFNet(nn.Module):
         dh = E(M, c)
         # tiled-GEMM levels (C > 64): the SCA channel dot sum_p dh (.) g rides in the dgrad epilogue (CM_CHANDOT,
         # per-64-row-tile partials); levels 0/1 (skinny GEMM) keep img_chan_dot
-        chandot = folded and c > 64 and HW % 64 == 0 and self.fuse_chandot
+        chandot = folded and c > 64 and HW % 64 == 0
         if chandot:
             chunks = HW // 64
             da_slab = F(B * chunks * c)
@@ -716,11 +701,7 @@ class NAFNet(nn.Module):
         ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
         dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
                    self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        if S["t2"] is None:
-            call("sca_sg_dw_bwd_rec", dh, S["a"], ds, S["t1"], self._slice(P, pre + "conv2.weight"),
-                 self._slice(P, pre + "conv2.bias"), dt1, self._slice(dflat, pre + "conv2.weight"),
-                 self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        elif c % (16 if dt != 0 else 8) == 0:
+        if c % (16 if dt != 0 else 8) == 0:
             call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
         else:
             dt2 = E(M, 2 * c)

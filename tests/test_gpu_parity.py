@@ -909,40 +909,6 @@ def test_sg_rc_weight_grad_fold_network(dev):
         assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-12, k
 
 
-@pytest.mark.parametrize("B,H,W,C,dtype", [(2, 37, 45, 16, 0), (2, 33, 70, 32, 1), (3, 16, 16, 64, 1)])
-def test_dw_bwd_t2_recompute_matches_stored(dev, B, H, W, C, dtype):
-    """The fused SCA/SimpleGate/depthwise backward that recomputes t2 = conv2(t1) + b in LDS (the forward then stores
-    no t2) equals the variant that reads the stored t2: bitwise-level in fp32, bf16-rounding level in bf16."""
-    from lowlight_image_enhancement_amd._lib import call, query
-    dt = torch.float32 if dtype == 0 else torch.bfloat16
-    gen = torch.Generator(device=dev).manual_seed(B * H + W * C)
-    M = B * H * W
-    t1 = torch.randn(M, 2 * C, device=dev, generator=gen).to(dt)
-    wdw = torch.randn(2 * C, 9, device=dev, generator=gen) * 0.3
-    bdw = torch.randn(2 * C, device=dev, generator=gen)
-    rows = query("dw_fwd_slab_rows", B, H, W, C, dtype)
-    t2 = torch.empty(M, 2 * C, device=dev, dtype=dt)
-    g = torch.empty(M, C, device=dev, dtype=dt)
-    pool = torch.empty(B * rows * C, device=dev)
-    call("dw_sg_pool_fwd", t1, wdw, bdw, t2, g, pool, B, H, W, C, dtype)
-    dh = torch.randn(M, C, device=dev, generator=gen).to(dt)
-    a = torch.rand(B, C, device=dev, generator=gen)
-    ds = torch.randn(B, C, device=dev, generator=gen)
-    outs = []
-    for rec in (False, True):
-        dt1 = torch.empty(M, 2 * C, device=dev, dtype=dt)
-        dW, db = torch.empty(2 * C, 9, device=dev), torch.empty(2 * C, device=dev)
-        ws = torch.empty(query("dw_bwd_workspace_floats", B, H, W, C), device=dev)
-        if rec:
-            call("sca_sg_dw_bwd_rec", dh, a, ds, t1, wdw, bdw, dt1, dW, db, ws, B, H, W, C, dtype)
-        else:
-            call("sca_sg_dw_bwd", dh, a, ds, t2, t1, wdw, dt1, dW, db, ws, B, H, W, C, dtype)
-        outs.append((dt1.float(), dW, db))
-    tol = dict(atol=1e-5, rtol=1e-5) if dtype == 0 else dict(atol=3e-2, rtol=2e-2)
-    for x, y in zip(outs[0], outs[1]):
-        close(y, x.cpu().numpy(), **tol)
-
-
 @pytest.mark.parametrize("dt", [0, 1, 2])
 @pytest.mark.parametrize("C", [8, 24, 40, 96, 160, 320, 512, 768, 2048])
 def test_ln_nhwc_any_channel_count(dev, dt, C):
