@@ -651,9 +651,15 @@ __device__ __forceinline__ void wide_mfma(const s16x4 (&f)[8], floatx16 (&acc)[2
   }
 }
 
-template <int XMODE, typename H, int NS, int WNW = 2>
+// LW (loader waves): 8 waves -- waves 4..7 only issue the stage DMAs (the geometry of waves 0..3 above), waves 0..3
+// only read fragments and multiply (the same MFMA sequence per output element: bitwise equal to LW = false).  Every
+// wave of the 4-wave tile issued 8 1-KB DMA pieces per 64-row stage beside its 16 MFMAs; in one instruction stream
+// the piece issue (60-185 cycles each among MFMAs, MI355X_MICROARCH.md 'LDS-DMA piece issue cost') and the MFMAs
+// serialise.  Split, the loaders' issue overlaps the consumers' MFMAs on the same SIMDs.
+template <int XMODE, typename H, int NS, int WNW = 2, bool LW = false>
 __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int by, int bz, unsigned char* smem) {
-  constexpr int NWV = 2 * WNW, TNB = 64 * WNW;  // waves; output tile columns (N)
+  static_assert(!LW || WNW == 2, "loader waves: the 4-wave 128 x 128 tile");
+  constexpr int NWV = 2 * WNW, TNB = 64 * WNW;  // (compute) waves; output tile columns (N)
   constexpr int GRB = 2 * TNB, RM = 64, PAN = RM * GRB, ST = wide_glds_stage_bytes<NS, XMODE, WNW>();
   constexpr int GRI = 1024 / GRB, GLPR = 64 / GRI;  // G rows per DMA instruction, lanes per G row
   constexpr int IG = RM / (GRI * NWV), IX = RM / (4 * NWV);  // DMA instructions per wave per stage (G, X)
@@ -662,7 +668,10 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
   static_assert(WNW == 2 || WNW == 4, "wave columns");
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
+  // LW: the loader waves take the DMA geometry of compute waves 0..3; loads / computes are each wave's roles
+  const bool loads = !LW || wave_id >= NWV, computes = !LW || wave_id < NWV;
+  const int wave = LW ? (wave_id & (NWV - 1)) : wave_id;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = bx * TNB, k0 = by * 128, s = bz;
   const int mb = s * p.chunk;
@@ -747,25 +756,30 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
         }
   };
   // bias (column sums of G) on the MFMA pipe: waves wk == 0 of the by == 0 tiles
-  const bool wb = do_b && wk == 0;
+  const bool wb = do_b && wk == 0 && computes;
   floatx16 accb[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
 
+  if (loads) {
 #pragma unroll
-  for (int t = 0; t < NS - 1; ++t)
-    if (t < nst) issue(t);
+    for (int t = 0; t < NS - 1; ++t)
+      if (t < nst) issue(t);
+  }
   for (int t = 0; t < nst; ++t) {
     // retire stage t: the stages issued after it (at most NS - 2) stay in flight
-    if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
-    else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
-    else wait_vm<0>();
+    if (loads) {
+      if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
+      else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
+      else wait_vm<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + NS - 1 < nst) issue(t + NS - 1);
+    if (loads && t + NS - 1 < nst) issue(t + NS - 1);
+    if (!computes) continue;
     if constexpr (XMODE == AM_SCALE) {
       const int im = (mb + t * RM) / p.rows_per_img;
       if (im != cur_img) {
@@ -796,6 +810,7 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
     wide_tr_wait<0>(fr[1]);
     wide_mfma<H>(fr[1], acc, wb, accb);
   }
+  if (!computes) return;
   if constexpr (XMODE == AM_SCALE)
     if (cur_img >= 0) fold();
 #pragma unroll
@@ -843,8 +858,9 @@ struct WGroup {
   int n;
 };
 
-template <typename H, int NS>
-__global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
+// NT = 512: the loader / consumer split (wgrad_wide_tile_glds LW)
+template <typename H, int NS, int NT = 256>
+__global__ __launch_bounds__(NT) void wgrad_bf16_wide_group(WGroup g) {
   constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS)>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
   const int b = blockIdx.x;
@@ -858,8 +874,9 @@ __global__ __launch_bounds__(256) void wgrad_bf16_wide_group(WGroup g) {
     if (g.xscale[i]) wgrad_wide_tile<AM_SCALE, H>(g.p[i], bx, by, bz, lds);
     else wgrad_wide_tile<AM_PLAIN, H>(g.p[i], bx, by, bz, lds);
   } else {
-    if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS>(g.p[i], bx, by, bz, smem);
-    else wgrad_wide_tile_glds<AM_PLAIN, H, NS>(g.p[i], bx, by, bz, smem);
+    constexpr bool LW = NT == 512;
+    if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS, 2, LW>(g.p[i], bx, by, bz, smem);
+    else wgrad_wide_tile_glds<AM_PLAIN, H, NS, 2, LW>(g.p[i], bx, by, bz, smem);
   }
 }
 
@@ -1294,9 +1311,10 @@ long wgroup_target() {
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
 // launch (A/B measurement; tests compare the paths in one process)
 int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged tiles, +0.5 % over depth 2 (A/B)
+  // 43 / 44 (round 4): the loader / consumer split (8 waves) with a 3- / 4-deep ring, in the grouped launch only
   const char* e = getenv("NBP_WGRAD_GLDS");
   const int v = e ? atoi(e) : 3;
-  return v >= 2 && v <= 4 ? v : 0;
+  return (v >= 2 && v <= 4) || v == 43 || v == 44 ? v : 0;
 }
 
 // Splits for the whole group: each problem keeps at most its standalone split count (its workspace) and at least
@@ -1343,7 +1361,9 @@ void wgroup_launch(hipStream_t st) {
     }
     g.start[g.n] = blocks;
     NBP_DISPATCH_H(g_wqueue_dtype, {
-      if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
+      if (ns == 44) wgrad_bf16_wide_group<H, 4, 512><<<blocks, 512, 0, st>>>(g);
+      else if (ns == 43) wgrad_bf16_wide_group<H, 3, 512><<<blocks, 512, 0, st>>>(g);
+      else if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
       else if (ns == 3) wgrad_bf16_wide_group<H, 3><<<blocks, 256, 0, st>>>(g);
       else if (ns == 2) wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
       else wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
@@ -1392,7 +1412,7 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       g_wqueue.push_back(p);
       g_stats_wgrad[0] = 1;
     } else NBP_DISPATCH_H(dtype, {
-      const int ns = wgrad_glds_depth();
+      const int ns = wgrad_glds_depth() % 10;  // (the loader-split variants are grouped-launch only)
       if (wide && ns == 4 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 4><<<wgrid, 256, 0, st>>>(p);
       else if (wide && ns == 4) wgrad_bf16_wide_glds<AM_SCALE, H, 4><<<wgrid, 256, 0, st>>>(p);
       else if (wide && ns == 2 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 2><<<wgrid, 256, 0, st>>>(p);

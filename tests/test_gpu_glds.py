@@ -230,3 +230,59 @@ def test_narrow_wgrad_vs_float64(dev, dt, M, N, K, rows):
     Xe = X.double() * (sc.double().repeat_interleave(rows, 0)[:M] if rows else 1.0)
     assert (dW.double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5
     assert (db.double() - G.double().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("C,HW", [(512, 256), (256, 1024), (128, 4096)])
+def test_wgrad_group_variants_bitwise(dev, dt, C, HW):
+    """The grouped wide weight gradients of one U-Net level (nbp_wgrad_group: conv1 / conv4 dW [2C x C], conv3 U with
+    the per-image SCA scale and conv5 U [C x C], two blocks) on every tile variant -- the register-staged tile
+    (NBP_WGRAD_GLDS=0), the 4-wave LDS-DMA rings (3, 4) and the loader / consumer split (43, 44: waves 4..7 issue the
+    DMA, 0..3 multiply) -- give bitwise equal dW (the same MFMA sequence per element); the bias column sums within fp32
+    rounding; dW against float64."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    gen = torch.Generator(device=dev).manual_seed(C + HW + dt)
+    B = 16 if C == 512 else 4
+    M = B * HW
+    probs = []
+    for _ in range(2):
+        for (n, k, scaled, bias) in ((2 * C, C, False, True), (C, C, True, False), (2 * C, C, False, True),
+                                     (C, C, False, False)):
+            G = torch.randn(M, n, device=dev, generator=gen).to(DT[dt])
+            X = torch.randn(M, k, device=dev, generator=gen).to(DT[dt])
+            xs = torch.rand(B, k, device=dev, generator=gen) + 0.5 if scaled else None
+            probs.append((G, X, xs, n, k, bias))
+    res = {}
+    old = os.environ.get("NBP_WGRAD_GLDS")
+    try:
+        for ns in ("0", "3", "4", "43", "44"):
+            os.environ["NBP_WGRAD_GLDS"] = ns
+            outs = []
+            call("grad_reduce_defer")
+            call("wgrad_group", 1)
+            for G, X, xs, n, k, bias in probs:
+                n_ws = query("wgrad_workspace_floats", M, n, k)
+                dW, db = torch.empty(n, k, device=dev), (torch.empty(n, device=dev) if bias else None)
+                ws = torch.empty(n_ws, device=dev)
+                call("wgrad_f32", G, n, 0, X, k, 2 if xs is not None else 0, xs, HW, M, n, k, 0, 0, 0, 0, dW, db, ws,
+                     n_ws, dt)
+                outs.append((dW, db, ws))
+            call("wgrad_group", 0)
+            call("grad_reduce_flush", 1)
+            torch.cuda.synchronize()
+            res[ns] = [(a, b) for a, b, _ in outs]
+    finally:
+        if old is None:
+            os.environ.pop("NBP_WGRAD_GLDS", None)
+        else:
+            os.environ["NBP_WGRAD_GLDS"] = old
+    for ns in ("3", "4", "43", "44"):
+        for (a, ab), (r, rb) in zip(res[ns], res["0"]):
+            assert torch.equal(a, r), ns
+            if rb is not None:
+                torch.testing.assert_close(ab, rb, rtol=1e-5, atol=1e-4 * M ** 0.5)
+    for (G, X, xs, n, k, bias), (dW, db) in zip(probs, res["44"]):
+        Xe = X.double() * (xs.double().repeat_interleave(HW, 0) if xs is not None else 1.0)
+        assert (dW.double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5
+        if bias:
+            assert (db.double() - G.double().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5
