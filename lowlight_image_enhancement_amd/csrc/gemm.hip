@@ -663,7 +663,7 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
   constexpr int GRB = 2 * TNB, RM = 64, PAN = RM * GRB, ST = wide_glds_stage_bytes<NS, XMODE, WNW>();
   constexpr int GRI = 1024 / GRB, GLPR = 64 / GRI;  // G rows per DMA instruction, lanes per G row
   constexpr int IG = RM / (GRI * NWV), IX = RM / (4 * NWV);  // DMA instructions per wave per stage (G, X)
-  constexpr int GL = IG + IX + (XMODE == AM_SCALE ? 2 : 0);
+  constexpr int GL = IG + IX + (XMODE == AM_SCALE && !LW ? 2 : 0);
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   static_assert(WNW == 2 || WNW == 4, "wave columns");
   const H* G = reinterpret_cast<const H*>(p.G);
@@ -710,22 +710,39 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
   // lgkmcnt(0) wait, at every use inside the loop)
   const void* zp = g_zero16;
   asm volatile("" : "+s"(zp));
+  // running source pointers and rows of this lane's pieces (issue() is called for t = 0, 1, 2, ... in order): one
+  // 64-bit add per piece and stage instead of a 64-bit multiply, and a select of the zero page past the chunk's end
+  const H* gsrc[IG];
+  const H* xsrc[IX];
+  int grw[IG], xrw[IX];
+#pragma unroll
+  for (int j = 0; j < IG; ++j) {
+    grw[j] = mb + grow_[j];
+    gsrc[j] = G + (long)grw[j] * p.ldg + n0 + gcol_[j];
+  }
+#pragma unroll
+  for (int j = 0; j < IX; ++j) {
+    xrw[j] = mb + xrow_[j];
+    xsrc[j] = X + (long)xrw[j] * p.ldx + k0 + xcol_[j];
+  }
+  const long gstep = (long)RM * p.ldg, xstep = (long)RM * p.ldx;
   auto issue = [&](int t) {
     unsigned char* st = smem + (t % NS) * ST;
-    const int m0 = mb + t * RM;
 #pragma unroll
     for (int j = 0; j < (IG > IX ? IG : IX); ++j) {  // (IG == IX == 4 at WNW 2: the original G / X interleave)
       if (j < IG) {
-        const int m = m0 + grow_[j];
-        glds16(m < me ? (const void*)(G + (long)m * p.ldg + n0 + gcol_[j]) : zp, st + (wave * IG + j) * 1024);
+        glds16(grw[j] < me ? (const void*)gsrc[j] : zp, st + (wave * IG + j) * 1024);
+        grw[j] += RM;
+        gsrc[j] += gstep;
       }
       if (j < IX) {
-        const int m = m0 + xrow_[j];
-        glds16(m < me ? (const void*)(X + (long)m * p.ldx + k0 + xcol_[j]) : zp, st + PAN + (wave * IX + j) * 1024);
+        glds16(xrw[j] < me ? (const void*)xsrc[j] : zp, st + PAN + (wave * IX + j) * 1024);
+        xrw[j] += RM;
+        xsrc[j] += xstep;
       }
     }
-    if constexpr (XMODE == AM_SCALE) {  // every wave DMAs the same 128 scales of the stage's image
-      const float* sc = p.x_scale + (long)(m0 / p.rows_per_img) * p.K + k0;
+    if constexpr (XMODE == AM_SCALE && !LW) {  // every wave DMAs the same 128 scales of the stage's image
+      const float* sc = p.x_scale + (long)((mb + t * RM) / p.rows_per_img) * p.K + k0;
       glds4(sc + lane, st + PAN + RM * 256);
       glds4(sc + 64 + lane, st + PAN + RM * 256 + 256);
     }
@@ -743,7 +760,6 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
   }
   const unsigned smem_lds = (unsigned)(size_t)(lds_void_t*)smem;
   float cur_sc[2] = {0.f, 0.f};
-  int cur_img = -1;
   auto fold = [&]() {
 #pragma unroll
     for (int j = 0; j < NT_; ++j)
@@ -768,51 +784,62 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
     for (int t = 0; t < NS - 1; ++t)
       if (t < nst) issue(t);
   }
-  for (int t = 0; t < nst; ++t) {
-    // retire stage t: the stages issued after it (at most NS - 2) stay in flight
-    if (loads) {
-      if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
-      else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
-      else wait_vm<0>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (loads && t + NS - 1 < nst) issue(t + NS - 1);
-    if (!computes) continue;
+  // the stages of one image form an inner loop with no fold inside it (a conditional fold in the stage loop made the
+  // compiler move all 64 accumulators between AGPRs and VGPRs every stage); AM_PLAIN: one segment
+  for (int t = 0; t < nst;) {
+    int tend = nst;
     if constexpr (XMODE == AM_SCALE) {
       const int im = (mb + t * RM) / p.rows_per_img;
-      if (im != cur_img) {
-        if (cur_img >= 0) fold();
-        cur_img = im;
-        // (asm LDS reads: a plain load here would make the compiler drain the DMA ring first)
-        const unsigned sa = smem_lds + (t % NS) * ST + PAN + RM * 256 + (wk * 64 + (lane & 31)) * 4;
-        asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(cur_sc[0]), "=&v"(cur_sc[1])
-                     : "v"(sa));
+      tend = min(nst, ((im + 1) * p.rows_per_img - mb + RM - 1) / RM);
+      if (LW && computes) {  // the consumers have no DMA in flight: a plain load of the image's 128 scales
+        const float* sc = p.x_scale + (long)im * p.K + k0 + wk * 64 + (lane & 31);
+        cur_sc[0] = sc[0];
+        cur_sc[1] = sc[32];
       }
     }
-    // the 8 tr-reads of K step ks + 16 are in flight while step ks is multiplied (asm: a builtin tr-read would make
-    // the compiler drain the DMA ring, vmcnt(0), before it)
-    const unsigned sb = smem_lds + (t % NS) * ST;
-    const unsigned ga0 = sb + abase[0][0], ga1 = sb + abase[0][1], xa0 = sb + abase[1][0], xa1 = sb + abase[1][1];
-    s16x4 fr[2][8];
-    wide_tr_reads<0, GRB>(fr[0], ga0, ga1, xa0, xa1);
-    wide_tr_reads<16, GRB>(fr[1], ga0, ga1, xa0, xa1);
-    wide_tr_wait<8>(fr[0]);
-    wide_mfma<H>(fr[0], acc, wb, accb);
-    wide_tr_reads<32, GRB>(fr[0], ga0, ga1, xa0, xa1);
-    wide_tr_wait<8>(fr[1]);
-    wide_mfma<H>(fr[1], acc, wb, accb);
-    wide_tr_reads<48, GRB>(fr[1], ga0, ga1, xa0, xa1);
-    wide_tr_wait<8>(fr[0]);
-    wide_mfma<H>(fr[0], acc, wb, accb);
-    wide_tr_wait<0>(fr[1]);
-    wide_mfma<H>(fr[1], acc, wb, accb);
+    const int tseg = t;
+    for (; t < tend; ++t) {
+      // retire stage t: the stages issued after it (at most NS - 2) stay in flight
+      if (loads) {
+        if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
+        else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
+        else wait_vm<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (loads && t + NS - 1 < nst) issue(t + NS - 1);
+      if (!computes) continue;
+      if constexpr (XMODE == AM_SCALE && !LW) {
+        if (t == tseg) {  // (asm LDS reads: a plain load here would make the compiler drain the DMA ring first)
+          const unsigned sa = smem_lds + (t % NS) * ST + PAN + RM * 256 + (wk * 64 + (lane & 31)) * 4;
+          asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128\n\ts_waitcnt lgkmcnt(0)"
+                       : "=&v"(cur_sc[0]), "=&v"(cur_sc[1])
+                       : "v"(sa));
+        }
+      }
+      // the 8 tr-reads of K step ks + 16 are in flight while step ks is multiplied (asm: a builtin tr-read would make
+      // the compiler drain the DMA ring, vmcnt(0), before it)
+      const unsigned sb = smem_lds + (t % NS) * ST;
+      const unsigned ga0 = sb + abase[0][0], ga1 = sb + abase[0][1], xa0 = sb + abase[1][0], xa1 = sb + abase[1][1];
+      s16x4 fr[2][8];
+      wide_tr_reads<0, GRB>(fr[0], ga0, ga1, xa0, xa1);
+      wide_tr_reads<16, GRB>(fr[1], ga0, ga1, xa0, xa1);
+      wide_tr_wait<8>(fr[0]);
+      wide_mfma<H>(fr[0], acc, wb, accb);
+      wide_tr_reads<32, GRB>(fr[0], ga0, ga1, xa0, xa1);
+      wide_tr_wait<8>(fr[1]);
+      wide_mfma<H>(fr[1], acc, wb, accb);
+      wide_tr_reads<48, GRB>(fr[1], ga0, ga1, xa0, xa1);
+      wide_tr_wait<8>(fr[0]);
+      wide_mfma<H>(fr[0], acc, wb, accb);
+      wide_tr_wait<0>(fr[1]);
+      wide_mfma<H>(fr[1], acc, wb, accb);
+    }
+    if constexpr (XMODE == AM_SCALE)
+      if (computes) fold();
   }
   if (!computes) return;
-  if constexpr (XMODE == AM_SCALE)
-    if (cur_img >= 0) fold();
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -855,7 +882,7 @@ struct WGroup {
   WgradP p[WG_MAX];
   int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
   unsigned char xscale[WG_MAX];
-  int n;
+  int n, remap;
 };
 
 // NT = 512: the loader / consumer split (wgrad_wide_tile_glds LW)
@@ -863,7 +890,8 @@ template <typename H, int NS, int NT = 256>
 __global__ __launch_bounds__(NT) void wgrad_bf16_wide_group(WGroup g) {
   constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS)>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
-  const int b = blockIdx.x;
+  // remap: consecutive tiles (the N tiles of one K tile and split, which share the X rows) on one XCD and its L2
+  const int b = g.remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   int i = 0;
   while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
   const int l = b - g.start[i];
@@ -1304,6 +1332,15 @@ long wgroup_target() {
   return v;
 }
 
+// NBP_WGROUP_XCD (A/B, round 4): 0 = tiles in launch order, 1 = consecutive tiles on one XCD
+int wgroup_xcd() {
+  static const int v = [] {
+    const char* e = getenv("NBP_WGROUP_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // Row-stage height of the narrow (N or K <= 64) weight-gradient tiles: 64 (measured +0.3 % at cfg2 over 32-row
 // stages, bitwise equal, profiles/r02_v6/ab_wgrad_rm.txt; 128-row and double-buffered 64-row stages were measured
 // slower).  32-row stages remain where a per-image scale block is not a multiple of 64 rows.
@@ -1348,6 +1385,7 @@ void wgroup_launch(hipStream_t st) {
   while (i < g_wqueue.size()) {
     WGroup g;
     g.n = 0;
+    g.remap = wgroup_xcd();
     int blocks = 0;
     for (; i < g_wqueue.size() && g.n < WG_MAX; ++i) {
       const WgradP& p = g_wqueue[i];

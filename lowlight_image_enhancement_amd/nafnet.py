@@ -108,8 +108,8 @@ class NAFNet(nn.Module):
         # (nbp_dgrad_sg_rc_wg; False: separate nbp_wgrad_f32 launches)
         self.sg_rc_wg = True
         # level 0 with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
-        # (nbp_gemm_ffn, bitwise the two launches), g2 never stored
-        self.fuse_ffn = __import__("os").environ.get("NBP_FFN", "1") != "0"  # TEMP: A/B of the fusion (round 4)
+        # (nbp_gemm_ffn, bitwise the two launches, +0.1 % step), g2 never stored
+        self.fuse_ffn = True
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
