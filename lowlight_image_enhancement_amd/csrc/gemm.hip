@@ -3,6 +3,7 @@
 //   as a GEMM over a space-to-depth gather), the 1x1 up conv + PixelShuffle(2) (:117-122, as a GEMM whose
 //   epilogue scatters depth-to-space and adds the skip, :148-149), and their dgrad / wgrad.
 // v_mfma_f32_32x32x2_f32: exact fp32 products, fp32 accumulation (one rounding per fma).
+#include <type_traits>
 #include <cstdint>
 #include <vector>
 
@@ -658,20 +659,21 @@ __device__ __forceinline__ void wide_mfma(const s16x4 (&f)[8], floatx16 (&acc)[2
 // serialise.  Split, the loaders' issue overlaps the consumers' MFMAs on the same SIMDs.
 template <int XMODE, typename H, int NS, int WNW = 2, bool LW = false>
 __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int by, int bz, unsigned char* smem) {
-  static_assert(!LW || WNW == 2, "loader waves: the 4-wave 128 x 128 tile");
   constexpr int NWV = 2 * WNW, TNB = 64 * WNW;  // (compute) waves; output tile columns (N)
+  constexpr int NDW = LW ? 4 : NWV;              // waves that issue the stage DMAs
   constexpr int GRB = 2 * TNB, RM = 64, PAN = RM * GRB, ST = wide_glds_stage_bytes<NS, XMODE, WNW>();
   constexpr int GRI = 1024 / GRB, GLPR = 64 / GRI;  // G rows per DMA instruction, lanes per G row
-  constexpr int IG = RM / (GRI * NWV), IX = RM / (4 * NWV);  // DMA instructions per wave per stage (G, X)
+  constexpr int IG = RM / (GRI * NDW), IX = RM / (4 * NDW);  // DMA instructions per wave per stage (G, X)
   constexpr int GL = IG + IX + (XMODE == AM_SCALE && !LW ? 2 : 0);
   static_assert(NS >= 2 && NS <= 4, "ring depth");
   static_assert(WNW == 2 || WNW == 4, "wave columns");
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
   const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
-  // LW: the loader waves take the DMA geometry of compute waves 0..3; loads / computes are each wave's roles
+  // LW: waves NWV .. NWV + 3 load (DMA geometry index dwave), waves 0 .. NWV - 1 compute
   const bool loads = !LW || wave_id >= NWV, computes = !LW || wave_id < NWV;
-  const int wave = LW ? (wave_id & (NWV - 1)) : wave_id;
+  const int dwave = LW ? (wave_id >= NWV ? wave_id - NWV : 0) : wave_id;
+  const int wave = wave_id;
   const int wn = wave >> 1, wk = wave & 1;
   const int n0 = bx * TNB, k0 = by * 128, s = bz;
   const int mb = s * p.chunk;
@@ -697,12 +699,12 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
   int grow_[IG], gcol_[IG], xrow_[IX], xcol_[IX];
 #pragma unroll
   for (int j = 0; j < IG; ++j) {
-    grow_[j] = (wave * IG + j) * GRI + lane / GLPR;
+    grow_[j] = (dwave * IG + j) * GRI + lane / GLPR;
     gcol_[j] = 8 * ((lane % GLPR) ^ (4 * (grow_[j] & 3)));
   }
 #pragma unroll
   for (int j = 0; j < IX; ++j) {
-    xrow_[j] = (wave * IX + j) * 4 + (lane >> 4);
+    xrow_[j] = (dwave * IX + j) * 4 + (lane >> 4);
     xcol_[j] = 8 * ((lane & 15) ^ (4 * (xrow_[j] & 3)));
   }
   const int nst = mb < me ? (me - mb + RM - 1) / RM : 0;
@@ -731,12 +733,12 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
 #pragma unroll
     for (int j = 0; j < (IG > IX ? IG : IX); ++j) {  // (IG == IX == 4 at WNW 2: the original G / X interleave)
       if (j < IG) {
-        glds16(grw[j] < me ? (const void*)gsrc[j] : zp, st + (wave * IG + j) * 1024);
+        glds16(grw[j] < me ? (const void*)gsrc[j] : zp, st + (dwave * IG + j) * 1024);
         grw[j] += RM;
         gsrc[j] += gstep;
       }
       if (j < IX) {
-        glds16(xrw[j] < me ? (const void*)xsrc[j] : zp, st + PAN + (wave * IX + j) * 1024);
+        glds16(xrw[j] < me ? (const void*)xsrc[j] : zp, st + PAN + (dwave * IX + j) * 1024);
         xrw[j] += RM;
         xsrc[j] += xstep;
       }
@@ -759,6 +761,9 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
     abase[1][i] = PAN + (8 * h + q) * 256 + ((4 * ((2 * wk + i) ^ q) + lx) << 4) + (pp & 1) * 8;
   }
   const unsigned smem_lds = (unsigned)(size_t)(lds_void_t*)smem;
+  // fragment sets: K steps 0 / 2 -> fa, 1 -> fc, 3 -> fb (the last K step multiplied under the next stage's first
+  // reads)
+  s16x4 fa[8], fb[8], fc[8];
   float cur_sc[2] = {0.f, 0.f};
   auto fold = [&]() {
 #pragma unroll
@@ -779,66 +784,76 @@ __device__ __forceinline__ void wgrad_wide_tile_glds(const WgradP p, int bx, int
 #pragma unroll
     for (int r = 0; r < 16; ++r) accb[i][r] = 0.f;
 
-  if (loads) {
-#pragma unroll
-    for (int t = 0; t < NS - 1; ++t)
-      if (t < nst) issue(t);
-  }
-  // the stages of one image form an inner loop with no fold inside it (a conditional fold in the stage loop made the
-  // compiler move all 64 accumulators between AGPRs and VGPRs every stage); AM_PLAIN: one segment
-  for (int t = 0; t < nst;) {
-    int tend = nst;
-    if constexpr (XMODE == AM_SCALE) {
-      const int im = (mb + t * RM) / p.rows_per_img;
-      tend = min(nst, ((im + 1) * p.rows_per_img - mb + RM - 1) / RM);
-      if (LW && computes) {  // the consumers have no DMA in flight: a plain load of the image's 128 scales
-        const float* sc = p.x_scale + (long)im * p.K + k0 + wk * 64 + (lane & 31);
-        cur_sc[0] = sc[0];
-        cur_sc[1] = sc[32];
-      }
+  // the stage loop per role (R: 0 = load and compute, 1 = load only, 2 = compute only): with loader waves the roles
+  // are separate loops with the same barriers, so neither role's loop-carried registers are live in the other's
+  auto run = [&](auto role) {
+    constexpr int R = decltype(role)::value;
+    constexpr bool RL = R != 2, RC = R != 1;
+    if (RL) {
+  #pragma unroll
+      for (int t = 0; t < NS - 1; ++t)
+        if (t < nst) issue(t);
     }
-    const int tseg = t;
-    for (; t < tend; ++t) {
-      // retire stage t: the stages issued after it (at most NS - 2) stay in flight
-      if (loads) {
-        if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
-        else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
-        else wait_vm<0>();
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (loads && t + NS - 1 < nst) issue(t + NS - 1);
-      if (!computes) continue;
-      if constexpr (XMODE == AM_SCALE && !LW) {
-        if (t == tseg) {  // (asm LDS reads: a plain load here would make the compiler drain the DMA ring first)
-          const unsigned sa = smem_lds + (t % NS) * ST + PAN + RM * 256 + (wk * 64 + (lane & 31)) * 4;
-          asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128\n\ts_waitcnt lgkmcnt(0)"
-                       : "=&v"(cur_sc[0]), "=&v"(cur_sc[1])
-                       : "v"(sa));
+    // the stages of one image form an inner loop with no fold inside it (a conditional fold in the stage loop made the
+    // compiler move all 64 accumulators between AGPRs and VGPRs every stage); AM_PLAIN: one segment
+    for (int t = 0; t < nst;) {
+      int tend = nst;
+      if constexpr (XMODE == AM_SCALE) {
+        const int im = (mb + t * RM) / p.rows_per_img;
+        tend = min(nst, ((im + 1) * p.rows_per_img - mb + RM - 1) / RM);
+        if (LW && RC) {  // the consumers have no DMA in flight: a plain load of the image's 128 scales
+          const float* sc = p.x_scale + (long)im * p.K + k0 + wk * 64 + (lane & 31);
+          cur_sc[0] = sc[0];
+          cur_sc[1] = sc[32];
         }
       }
-      // the 8 tr-reads of K step ks + 16 are in flight while step ks is multiplied (asm: a builtin tr-read would make
-      // the compiler drain the DMA ring, vmcnt(0), before it)
-      const unsigned sb = smem_lds + (t % NS) * ST;
-      const unsigned ga0 = sb + abase[0][0], ga1 = sb + abase[0][1], xa0 = sb + abase[1][0], xa1 = sb + abase[1][1];
-      s16x4 fr[2][8];
-      wide_tr_reads<0, GRB>(fr[0], ga0, ga1, xa0, xa1);
-      wide_tr_reads<16, GRB>(fr[1], ga0, ga1, xa0, xa1);
-      wide_tr_wait<8>(fr[0]);
-      wide_mfma<H>(fr[0], acc, wb, accb);
-      wide_tr_reads<32, GRB>(fr[0], ga0, ga1, xa0, xa1);
-      wide_tr_wait<8>(fr[1]);
-      wide_mfma<H>(fr[1], acc, wb, accb);
-      wide_tr_reads<48, GRB>(fr[1], ga0, ga1, xa0, xa1);
-      wide_tr_wait<8>(fr[0]);
-      wide_mfma<H>(fr[0], acc, wb, accb);
-      wide_tr_wait<0>(fr[1]);
-      wide_mfma<H>(fr[1], acc, wb, accb);
+      const int tseg = t;
+      for (; t < tend; ++t) {
+        // retire stage t: the stages issued after it (at most NS - 2) stay in flight
+        if (RL) {
+          if (NS >= 4 && t + 2 < nst) wait_vm<2 * GL>();
+          else if (NS >= 3 && t + 1 < nst) wait_vm<GL>();
+          else wait_vm<0>();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (RL && t + NS - 1 < nst) issue(t + NS - 1);
+        if (!RC) continue;
+        if constexpr (XMODE == AM_SCALE && !LW) {
+          if (t == tseg) {  // (asm LDS reads: a plain load here would make the compiler drain the DMA ring first)
+            const unsigned sa = smem_lds + (t % NS) * ST + PAN + RM * 256 + (wk * 64 + (lane & 31)) * 4;
+            asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %2 offset:128\n\ts_waitcnt lgkmcnt(0)"
+                         : "=&v"(cur_sc[0]), "=&v"(cur_sc[1])
+                         : "v"(sa));
+          }
+        }
+        // the 8 tr-reads of K step ks + 16 are in flight while step ks is multiplied (asm: a builtin tr-read would make
+        // the compiler drain the DMA ring, vmcnt(0), before it).  The stage's last K step (set fb) is multiplied after the
+        // next stage's barrier, under that stage's first fragment reads (the same MFMA order per accumulator)
+        const unsigned sb = smem_lds + (t % NS) * ST;
+        const unsigned ga0 = sb + abase[0][0], ga1 = sb + abase[0][1], xa0 = sb + abase[1][0], xa1 = sb + abase[1][1];
+        wide_tr_reads<0, GRB>(fa, ga0, ga1, xa0, xa1);
+        wide_tr_reads<16, GRB>(fc, ga0, ga1, xa0, xa1);
+        if (t != tseg) wide_mfma<H>(fb, acc, wb, accb);
+        wide_tr_wait<8>(fa);
+        wide_mfma<H>(fa, acc, wb, accb);
+        wide_tr_reads<32, GRB>(fa, ga0, ga1, xa0, xa1);
+        wide_tr_wait<8>(fc);
+        wide_mfma<H>(fc, acc, wb, accb);
+        wide_tr_reads<48, GRB>(fb, ga0, ga1, xa0, xa1);
+        wide_tr_wait<8>(fa);
+        wide_mfma<H>(fa, acc, wb, accb);
+        wide_tr_wait<0>(fb);  // (every read of the slot done before the next barrier frees it)
+      }
+      if (RC && tend > tseg) wide_mfma<H>(fb, acc, wb, accb);
+      if constexpr (XMODE == AM_SCALE)
+        if (RC) fold();
     }
-    if constexpr (XMODE == AM_SCALE)
-      if (computes) fold();
-  }
+  };
+  if constexpr (!LW) run(std::integral_constant<int, 0>{});
+  else if (loads) run(std::integral_constant<int, 1>{});
+  else run(std::integral_constant<int, 2>{});
   if (!computes) return;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -885,10 +900,11 @@ struct WGroup {
   int n, remap;
 };
 
-// NT = 512: the loader / consumer split (wgrad_wide_tile_glds LW)
-template <typename H, int NS, int NT = 256>
+// NT = 64 (2 WNW + 4): the loader / consumer split (wgrad_wide_tile_glds LW).  WNW = 4 (256-column tiles): plain
+// problems only (the per-image scale's fold registers do not fit beside 12 waves)
+template <typename H, int NS, int NT = 256, int WNW = 2>
 __global__ __launch_bounds__(NT) void wgrad_bf16_wide_group(WGroup g) {
-  constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS)>();
+  constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS), WNW>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
   // remap: consecutive tiles (the N tiles of one K tile and split, which share the X rows) on one XCD and its L2
   const int b = g.remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -902,9 +918,13 @@ __global__ __launch_bounds__(NT) void wgrad_bf16_wide_group(WGroup g) {
     if (g.xscale[i]) wgrad_wide_tile<AM_SCALE, H>(g.p[i], bx, by, bz, lds);
     else wgrad_wide_tile<AM_PLAIN, H>(g.p[i], bx, by, bz, lds);
   } else {
-    constexpr bool LW = NT == 512;
-    if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS, 2, LW>(g.p[i], bx, by, bz, smem);
-    else wgrad_wide_tile_glds<AM_PLAIN, H, NS, 2, LW>(g.p[i], bx, by, bz, smem);
+    constexpr bool LW = NT == 64 * (2 * WNW + 4);
+    if constexpr (WNW == 4) {
+      wgrad_wide_tile_glds<AM_PLAIN, H, NS, 4, LW>(g.p[i], bx, by, bz, smem);
+    } else {
+      if (g.xscale[i]) wgrad_wide_tile_glds<AM_SCALE, H, NS, 2, LW>(g.p[i], bx, by, bz, smem);
+      else wgrad_wide_tile_glds<AM_PLAIN, H, NS, 2, LW>(g.p[i], bx, by, bz, smem);
+    }
   }
 }
 
@@ -1322,14 +1342,29 @@ thread_local bool g_wgroup = false;
 thread_local std::vector<WgradP> g_wqueue;
 thread_local int g_wqueue_dtype = 1;  // the 16-bit type of the queued problems (one per group)
 
-// NBP_WGROUP_TARGET: the workgroup count a group launch aims for when choosing the M-splits (A/B measurement)
-long wgroup_target() {
-  static const long v = [] {
-    const char* e = getenv("NBP_WGROUP_TARGET");
-    const long t = e ? atol(e) : 1024L;
-    return t < 1 ? 1024L : t;
+// M-splits of a group launch kind with `tiles` output tiles (one resident workgroup per CU): the split count S
+// minimising rounds x (1 / S + per-workgroup overhead) + slab cost, rounds = ceil(tiles S / CUs) -- i.e. the fewest
+// splits that still fill the last round (middle level: the 256-column tiles unsplit in one round, the 128-column
+// scale tiles in two halves).
+int wgroup_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
   }();
-  return v;
+  return n;
+}
+long wgroup_splits(long tiles, long cap) {
+  const long cus = wgroup_cus();
+  long best = 1;
+  double best_c = 1e30;
+  for (long sp = 1; sp <= cap && sp <= 64; ++sp) {
+    const double c = (double)((tiles * sp + cus - 1) / cus) * (1.0 / sp + 0.07) + 0.02 * sp;
+    if (c < best_c - 1e-9) best_c = c, best = sp;
+  }
+  return best;
 }
 
 // NBP_WGROUP_XCD (A/B, round 4): 0 = tiles in launch order, 1 = consecutive tiles on one XCD
@@ -1347,26 +1382,41 @@ int wgroup_xcd() {
 
 // NBP_WGRAD_GLDS: LDS-DMA ring depth of the wide weight-gradient tiles (2 or 3; 0 = register-staged tiles), read per
 // launch (A/B measurement; tests compare the paths in one process)
-int wgrad_glds_depth() {  // default 3: +1.6 % step over the register-staged tiles, +0.5 % over depth 2 (A/B)
-  // 43 / 44 (round 4): the loader / consumer split (8 waves) with a 3- / 4-deep ring, in the grouped launch only
+int wgrad_glds_depth() {  // 3: +1.6 % step over the register-staged tiles, +0.5 % over depth 2 (A/B)
+  // 43 / 44 (round 4): the loader / consumer split (8 waves) with a 3- / 4-deep ring, in the grouped launch only;
+  // 83 (default): 43 plus the 256-column tiles where they fill one round (wgroup_launch)
   const char* e = getenv("NBP_WGRAD_GLDS");
-  const int v = e ? atoi(e) : 3;
-  return (v >= 2 && v <= 4) || v == 43 || v == 44 ? v : 0;
+  const int v = e ? atoi(e) : 83;
+  return (v >= 2 && v <= 4) || v == 43 || v == 44 || v == 83 || v == 84 ? v : 0;
 }
 
-// Splits for the whole group: each problem keeps at most its standalone split count (its workspace) and at least
-// 256 rows per split; the group as a whole aims at ~wgroup_target() workgroups.  The reductions queued for the
+// Splits per launch kind of the group (wgroup_splits): each problem keeps at most its standalone split count (its
+// workspace) and at least 256 rows per split.  The reductions queued for the
 // problems' slabs are re-pointed at the chosen split counts.
 void wgroup_launch(hipStream_t st) {
   for (double& v : g_stats_group) v = 0;
   const int ns = wgrad_glds_depth();
-  constexpr int TNB = 128;
-  long tiles = 0;
-  for (const WgradP& p : g_wqueue) tiles += (long)(p.N / TNB) * (p.K / 128);
-  const long want = (wgroup_target() + tiles - 1) / (tiles > 0 ? tiles : 1);
+  // 83 / 84: plain problems with N % 256 == 0 on 256 x 128 tiles (8 compute + 4 loader waves), the rest as 43 / 44
+  // -- where those tiles fill the chip in ONE unsplit round (the middle level: 240 tiles); elsewhere the split 256-
+  // column tiles measured slower than the 128-column ones (32 x 32 level 119 -> 130 us, 64 x 64 119 -> 240 us)
+  bool w4 = ns == 83 || ns == 84;
+  auto plain256 = [](const WgradP& p) { return p.x_scale == nullptr && p.N % 256 == 0; };
+  if (w4) {
+    long t4 = 0;
+    for (const WgradP& p : g_wqueue)
+      if (plain256(p)) t4 += (long)(p.N / 256) * (p.K / 128);
+    w4 = t4 > wgroup_cus() / 2 && t4 <= wgroup_cus();
+  }
+  auto wide4 = [&](const WgradP& p) { return w4 && plain256(p); };
+  long tiles[2] = {0, 0};  // per launch kind: 128- / 256-column tiles
+  for (const WgradP& p : g_wqueue) tiles[wide4(p)] += (long)(p.N / (wide4(p) ? 256 : 128)) * (p.K / 128);
+  long want[2] = {1, 1};  // kind 1 unsplit; the 128-column tiles packed by wgroup_splits
+  if (tiles[0]) want[0] = wgroup_splits(tiles[0], 64);
+  if (const char* e = getenv("NBP_WGROUP_SPLITS"))  // (test hook: equal splits for the bitwise variant comparison)
+    if (atoi(e) > 0) want[0] = want[1] = atoi(e);
   for (WgradP& p : g_wqueue) {
-    const long s_max = cdiv(p.M, p.chunk);
-    long s = want < s_max ? want : s_max;
+    const long s_max = cdiv(p.M, p.chunk);  // (the problem's workspace holds its standalone split count)
+    long s = want[wide4(p)] < s_max ? want[wide4(p)] : s_max;
     const long rows_cap = p.M / 256 > 1 ? p.M / 256 : 1;
     if (s > rows_cap) s = rows_cap;
     if (s < 1) s = 1;
@@ -1381,32 +1431,47 @@ void wgroup_launch(hipStream_t st) {
     for (RDesc& d : g_pending)
       if (d.slab == p.slab || (p.slab_b && d.slab == p.slab_b)) d.S = S_, d.ty = make_rdesc(d.slab, S_, d.L, d.out).ty;
   }
-  size_t i = 0;
-  while (i < g_wqueue.size()) {
-    WGroup g;
-    g.n = 0;
-    g.remap = wgroup_xcd();
-    int blocks = 0;
-    for (; i < g_wqueue.size() && g.n < WG_MAX; ++i) {
-      const WgradP& p = g_wqueue[i];
-      g.p[g.n] = p;
-      g.gx[g.n] = p.N / TNB;
-      g.gy[g.n] = p.K / 128;
-      g.xscale[g.n] = p.x_scale != nullptr;
+  for (int kind = 1; kind >= 0; --kind) {
+    if (!tiles[kind]) continue;
+    const int TNB = kind ? 256 : 128;
+    size_t i = 0;
+    while (i < g_wqueue.size()) {
+      WGroup g;
+      g.n = 0;
+      g.remap = wgroup_xcd();
+      int blocks = 0;
+      for (; i < g_wqueue.size() && g.n < WG_MAX; ++i) {
+        const WgradP& p = g_wqueue[i];
+        if ((int)wide4(p) != kind) continue;
+        g.p[g.n] = p;
+        g.gx[g.n] = p.N / TNB;
+        g.gy[g.n] = p.K / 128;
+        g.xscale[g.n] = p.x_scale != nullptr;
+        g.start[g.n] = blocks;
+        blocks += g.gx[g.n] * g.gy[g.n] * cdiv(p.M, p.chunk);
+        ++g.n;
+      }
+      if (!g.n) break;
       g.start[g.n] = blocks;
-      blocks += g.gx[g.n] * g.gy[g.n] * cdiv(p.M, p.chunk);
-      ++g.n;
+      NBP_DISPATCH_H(g_wqueue_dtype, {
+        if (kind) {  // (a 4-deep ring of 48-KB stages would not fit in LDS)
+          wgrad_bf16_wide_group<H, 3, 768, 4><<<blocks, 768, 0, st>>>(g);
+        } else if (ns == 44 || ns == 84) {
+          wgrad_bf16_wide_group<H, 4, 512><<<blocks, 512, 0, st>>>(g);
+        } else if (ns == 43 || ns == 83) {
+          wgrad_bf16_wide_group<H, 3, 512><<<blocks, 512, 0, st>>>(g);
+        } else if (ns == 4) {
+          wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
+        } else if (ns == 3) {
+          wgrad_bf16_wide_group<H, 3><<<blocks, 256, 0, st>>>(g);
+        } else if (ns == 2) {
+          wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
+        } else {
+          wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
+        }
+      });
+      g_stats_group[5] += 1;
     }
-    g.start[g.n] = blocks;
-    NBP_DISPATCH_H(g_wqueue_dtype, {
-      if (ns == 44) wgrad_bf16_wide_group<H, 4, 512><<<blocks, 512, 0, st>>>(g);
-      else if (ns == 43) wgrad_bf16_wide_group<H, 3, 512><<<blocks, 512, 0, st>>>(g);
-      else if (ns == 4) wgrad_bf16_wide_group<H, 4><<<blocks, 256, 0, st>>>(g);
-      else if (ns == 3) wgrad_bf16_wide_group<H, 3><<<blocks, 256, 0, st>>>(g);
-      else if (ns == 2) wgrad_bf16_wide_group<H, 2><<<blocks, 256, 0, st>>>(g);
-      else wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
-    });
-    g_stats_group[5] += 1;
   }
   g_wqueue.clear();
 }

@@ -12,25 +12,30 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def run_modes(fn, modes=("0", "auto")):
+def run_modes(fn, modes=("0", "auto", "lw1", "lw2")):
+    """fn's outputs bitwise equal under NBP_GLDS=0 (register-staged tiles), auto (LDS-DMA ring) and lw1 / lw2 (the
+    ring with loader waves, NBP_GEMM_LW=1; 2 also takes 128 x 128 tiles from 128 blocks)."""
     outs = {}
-    old = os.environ.get("NBP_GLDS")
+    old = {k: os.environ.get(k) for k in ("NBP_GLDS", "NBP_GEMM_LW")}
     try:
         for ns in modes:  # auto (unset): the depth chosen per launch from the grid
-            if ns == "auto":
-                os.environ.pop("NBP_GLDS", None)
-            else:
+            os.environ.pop("NBP_GLDS", None)
+            os.environ.pop("NBP_GEMM_LW", None)
+            if ns.startswith("lw"):
+                os.environ["NBP_GEMM_LW"] = ns[2:]
+            elif ns != "auto":
                 os.environ["NBP_GLDS"] = ns
             outs[ns] = [t.clone() for t in fn()]
             torch.cuda.synchronize()
     finally:
-        if old is None:
-            os.environ.pop("NBP_GLDS", None)
-        else:
-            os.environ["NBP_GLDS"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     for ns in modes[1:]:
         for a, b in zip(outs[modes[0]], outs[ns]):
-            assert torch.equal(a, b), f"NBP_GLDS={ns} differs from NBP_GLDS={modes[0]}"
+            assert torch.equal(a, b), f"mode {ns} differs from mode {modes[0]}"
 
 
 DT = {1: torch.bfloat16, 2: torch.float16}
@@ -237,9 +242,10 @@ def test_narrow_wgrad_vs_float64(dev, dt, M, N, K, rows):
 def test_wgrad_group_variants_bitwise(dev, dt, C, HW):
     """The grouped wide weight gradients of one U-Net level (nbp_wgrad_group: conv1 / conv4 dW [2C x C], conv3 U with
     the per-image SCA scale and conv5 U [C x C], two blocks) on every tile variant -- the register-staged tile
-    (NBP_WGRAD_GLDS=0), the 4-wave LDS-DMA rings (3, 4) and the loader / consumer split (43, 44: waves 4..7 issue the
-    DMA, 0..3 multiply) -- give bitwise equal dW (the same MFMA sequence per element); the bias column sums within fp32
-    rounding; dW against float64."""
+    (NBP_WGRAD_GLDS=0), the 4-wave LDS-DMA rings (3, 4), the loader / consumer split (43, 44: waves 4..7 issue the
+    DMA, 0..3 multiply) and the 256-column tiles of the plain problems (83: 8 compute + 4 loader waves) -- give bitwise
+    equal dW at equal M-splits (the same MFMA sequence per element); the bias column sums within fp32 rounding; dW
+    against float64 also under the default split policy."""
     from lowlight_image_enhancement_amd._lib import call, query
     gen = torch.Generator(device=dev).manual_seed(C + HW + dt)
     B = 16 if C == 512 else 4
@@ -253,10 +259,16 @@ def test_wgrad_group_variants_bitwise(dev, dt, C, HW):
             xs = torch.rand(B, k, device=dev, generator=gen) + 0.5 if scaled else None
             probs.append((G, X, xs, n, k, bias))
     res = {}
-    old = os.environ.get("NBP_WGRAD_GLDS")
+    old = {k: os.environ.get(k) for k in ("NBP_WGRAD_GLDS", "NBP_WGROUP_SPLITS")}
+    # (variant, NBP_WGRAD_GLDS, forced splits): equal splits for the bitwise comparison, then the default split policy
+    runs = [(v, v, "2") for v in ("0", "3", "4", "43", "44", "83")] + [("43auto", "43", None), ("83auto", "83", None)]
     try:
-        for ns in ("0", "3", "4", "43", "44"):
+        for name, ns, splits in runs:
             os.environ["NBP_WGRAD_GLDS"] = ns
+            if splits is None:
+                os.environ.pop("NBP_WGROUP_SPLITS", None)
+            else:
+                os.environ["NBP_WGROUP_SPLITS"] = splits
             outs = []
             call("grad_reduce_defer")
             call("wgrad_group", 1)
@@ -270,19 +282,23 @@ def test_wgrad_group_variants_bitwise(dev, dt, C, HW):
             call("wgrad_group", 0)
             call("grad_reduce_flush", 1)
             torch.cuda.synchronize()
-            res[ns] = [(a, b) for a, b, _ in outs]
+            res[name] = [(a, b) for a, b, _ in outs]
     finally:
-        if old is None:
-            os.environ.pop("NBP_WGRAD_GLDS", None)
-        else:
-            os.environ["NBP_WGRAD_GLDS"] = old
-    for ns in ("3", "4", "43", "44"):
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for ns in ("3", "4", "43", "44", "83"):
         for (a, ab), (r, rb) in zip(res[ns], res["0"]):
             assert torch.equal(a, r), ns
             if rb is not None:
                 torch.testing.assert_close(ab, rb, rtol=1e-5, atol=1e-4 * M ** 0.5)
-    for (G, X, xs, n, k, bias), (dW, db) in zip(probs, res["44"]):
-        Xe = X.double() * (xs.double().repeat_interleave(HW, 0) if xs is not None else 1.0)
-        assert (dW.double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5
-        if bias:
-            assert (db.double() - G.double().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5
+    for name in ("44", "43auto", "83auto"):
+        for (G, X, xs, n, k, bias), (dW, db) in zip(probs, res[name]):
+            Xe = X.double() * (xs.double().repeat_interleave(HW, 0) if xs is not None else 1.0)
+            assert (dW.double() - G.double().t() @ Xe).abs().max().item() <= 1e-4 * M ** 0.5, name
+            if bias:
+                assert (db.double() - G.double().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5, name
+
+
