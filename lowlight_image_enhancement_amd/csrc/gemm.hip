@@ -1393,9 +1393,7 @@ int wgrad_glds_depth() {  // 3: +1.6 % step over the register-staged tiles, +0.5
 // Splits per launch kind of the group (wgroup_splits): each problem keeps at most its standalone split count (its
 // workspace) and at least 256 rows per split.  The reductions queued for the
 // problems' slabs are re-pointed at the chosen split counts.
-void wgroup_launch(hipStream_t st) {
-  for (double& v : g_stats_group) v = 0;
-  const int ns = wgrad_glds_depth();
+void wgroup_launch_chunk(hipStream_t st, int ns, int q0, int q1) {
   // 83 / 84: plain problems with N % 256 == 0 on 256 x 128 tiles (8 compute + 4 loader waves), the rest as 43 / 44
   // -- where those tiles fill the chip in ONE unsplit round (the middle level: 240 tiles); elsewhere the split 256-
   // column tiles measured slower than the 128-column ones (32 x 32 level 119 -> 130 us, 64 x 64 119 -> 240 us)
@@ -1403,18 +1401,22 @@ void wgroup_launch(hipStream_t st) {
   auto plain256 = [](const WgradP& p) { return p.x_scale == nullptr && p.N % 256 == 0; };
   if (w4) {
     long t4 = 0;
-    for (const WgradP& p : g_wqueue)
-      if (plain256(p)) t4 += (long)(p.N / 256) * (p.K / 128);
+    for (int q = q0; q < q1; ++q)
+      if (plain256(g_wqueue[q])) t4 += (long)(g_wqueue[q].N / 256) * (g_wqueue[q].K / 128);
     w4 = t4 > wgroup_cus() / 2 && t4 <= wgroup_cus();
   }
   auto wide4 = [&](const WgradP& p) { return w4 && plain256(p); };
   long tiles[2] = {0, 0};  // per launch kind: 128- / 256-column tiles
-  for (const WgradP& p : g_wqueue) tiles[wide4(p)] += (long)(p.N / (wide4(p) ? 256 : 128)) * (p.K / 128);
+  for (int q = q0; q < q1; ++q) {
+    const WgradP& p = g_wqueue[q];
+    tiles[wide4(p)] += (long)(p.N / (wide4(p) ? 256 : 128)) * (p.K / 128);
+  }
   long want[2] = {1, 1};  // kind 1 unsplit; the 128-column tiles packed by wgroup_splits
   if (tiles[0]) want[0] = wgroup_splits(tiles[0], 64);
   if (const char* e = getenv("NBP_WGROUP_SPLITS"))  // (test hook: equal splits for the bitwise variant comparison)
     if (atoi(e) > 0) want[0] = want[1] = atoi(e);
-  for (WgradP& p : g_wqueue) {
+  for (int q = q0; q < q1; ++q) {
+    WgradP& p = g_wqueue[q];
     const long s_max = cdiv(p.M, p.chunk);  // (the problem's workspace holds its standalone split count)
     long s = want[wide4(p)] < s_max ? want[wide4(p)] : s_max;
     const long rows_cap = p.M / 256 > 1 ? p.M / 256 : 1;
@@ -1434,14 +1436,13 @@ void wgroup_launch(hipStream_t st) {
   for (int kind = 1; kind >= 0; --kind) {
     if (!tiles[kind]) continue;
     const int TNB = kind ? 256 : 128;
-    size_t i = 0;
-    while (i < g_wqueue.size()) {
+    {
       WGroup g;
       g.n = 0;
       g.remap = wgroup_xcd();
       int blocks = 0;
-      for (; i < g_wqueue.size() && g.n < WG_MAX; ++i) {
-        const WgradP& p = g_wqueue[i];
+      for (int q = q0; q < q1; ++q) {
+        const WgradP& p = g_wqueue[q];
         if ((int)wide4(p) != kind) continue;
         g.p[g.n] = p;
         g.gx[g.n] = p.N / TNB;
@@ -1451,7 +1452,7 @@ void wgroup_launch(hipStream_t st) {
         blocks += g.gx[g.n] * g.gy[g.n] * cdiv(p.M, p.chunk);
         ++g.n;
       }
-      if (!g.n) break;
+      if (!g.n) continue;
       g.start[g.n] = blocks;
       NBP_DISPATCH_H(g_wqueue_dtype, {
         if (kind) {  // (a 4-deep ring of 48-KB stages would not fit in LDS)
@@ -1473,8 +1474,17 @@ void wgroup_launch(hipStream_t st) {
       g_stats_group[5] += 1;
     }
   }
+}
+void wgroup_launch(hipStream_t st) {
+  for (double& v : g_stats_group) v = 0;
+  const int ns = wgrad_glds_depth();
+  // the queue (a whole U-Net level) in balanced chunks of <= WG_MAX problems, each chunk one launch per tile kind
+  const int nq = (int)g_wqueue.size(), nch = (nq + WG_MAX - 1) / WG_MAX;
+  for (int c = 0; c < nch; ++c)
+    wgroup_launch_chunk(st, ns, (int)((long)nq * c / nch), (int)((long)nq * (c + 1) / nch));
   g_wqueue.clear();
 }
+
 
 int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, int x_mode, const float* x_scale,
                   int rows_per_img, int M, int N, int K, int gh, int gw, int cs_g, int cs_x, float* dW, float* db,
