@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(WgradP p) {
 // address of row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.  Two reads give the
 // 8 consecutive-m values of one fragment.  Rows are padded to 96 elements (192 B) so the four rows x two groups of
 // a half-wave hit 64 distinct banks.
-// RM = 64 (NBP_WGRAD_RM=64): 64-row stages -- twice the loads in flight per stage and half the barrier pairs; the
+// RM = 64: 64-row stages -- twice the loads in flight per stage and half the barrier pairs; the
 // MFMA and bias-sum order over the rows is unchanged (bitwise equal to RM = 32)
 template <int GMODE, int XMODE, typename H, int RM = 32>
 __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
@@ -897,7 +897,7 @@ struct WGroup {
   WgradP p[WG_MAX];
   int gx[WG_MAX], gy[WG_MAX], start[WG_MAX + 1];
   unsigned char xscale[WG_MAX];
-  int n, remap;
+  int n;
 };
 
 // NT = 64 (2 WNW + 4): the loader / consumer split (wgrad_wide_tile_glds LW).  WNW = 4 (256-column tiles): plain
@@ -906,8 +906,9 @@ template <typename H, int NS, int NT = 256, int WNW = 2>
 __global__ __launch_bounds__(NT) void wgrad_bf16_wide_group(WGroup g) {
   constexpr int SM = NS == 0 ? WIDE_LDS * (int)sizeof(H) : wide_glds_lds_bytes<(NS == 0 ? 2 : NS), WNW>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
-  // remap: consecutive tiles (the N tiles of one K tile and split, which share the X rows) on one XCD and its L2
-  const int b = g.remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  // consecutive tiles (the N tiles of one K tile and split, which share the X rows) on one XCD and its L2: middle-level
+  // group 201.7 -> 188.3 us, 32 x 32 level 183.0 -> 166.6 us (profiles/r04/ab_wgrad_group_variants.txt)
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
   int i = 0;
   while (i + 1 < g.n && g.start[i + 1] <= b) ++i;
   const int l = b - g.start[i];
@@ -1367,15 +1368,6 @@ long wgroup_splits(long tiles, long cap) {
   return best;
 }
 
-// NBP_WGROUP_XCD (A/B, round 4): 0 = tiles in launch order, 1 = consecutive tiles on one XCD
-int wgroup_xcd() {
-  static const int v = [] {
-    const char* e = getenv("NBP_WGROUP_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
 // Row-stage height of the narrow (N or K <= 64) weight-gradient tiles: 64 (measured +0.3 % at cfg2 over 32-row
 // stages, bitwise equal, profiles/r02_v6/ab_wgrad_rm.txt; 128-row and double-buffered 64-row stages were measured
 // slower).  32-row stages remain where a per-image scale block is not a multiple of 64 rows.
@@ -1439,7 +1431,6 @@ void wgroup_launch_chunk(hipStream_t st, int ns, int q0, int q1) {
     {
       WGroup g;
       g.n = 0;
-      g.remap = wgroup_xcd();
       int blocks = 0;
       for (int q = q0; q < q1; ++q) {
         const WgradP& p = g_wqueue[q];

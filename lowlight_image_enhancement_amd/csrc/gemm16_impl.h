@@ -146,8 +146,7 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
 // staged and stored in pass q, one pass after the other through the same LDS rows.
 template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2, int WM = 2, int PASSES = 1>
 __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / (32 * WM)][BN / (32 * WN)],
-                                              unsigned char* smem, int m0, int n0, bool active = true) {
-  // active = false: a loader wave of the LW tiles (gemm_glds_kernel): it only joins the barriers
+                                              unsigned char* smem, int m0, int n0) {
   constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN), NT = 64 * WM * WN;
   static_assert((WN == 2 && WM == 2) || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT),
                 "cross-wave reductions assume 2 x 2 waves");
@@ -169,7 +168,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
   for (int j = 0; j < 8; ++j) cd[j] = cb[j] = 0.f;
   for (int pass = 0; pass < PASSES; ++pass) {
   if (pass) __syncthreads();  // the previous pass's rows are stored: the LDS rows are free
-  if (active && (PASSES == 1 || wm / (WM / PASSES) == pass)) {
+  if (PASSES == 1 || wm / (WM / PASSES) == pass) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -183,7 +182,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       }
   }
   __syncthreads();
-  for (int e = active ? tid : PR * G8; e < PR * G8; e += NT) {
+  for (int e = tid; e < PR * G8; e += NT) {
     const int row = e / G8, c8 = (e % G8) * 8;
     const int grow = m0 + pass * PR + row, gcol = n0 + c8;
     if (grow >= M || gcol >= N) continue;
@@ -558,15 +557,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmPB p) {
 // BK = 32 (plain / im2col A): 64-byte rows, chunk c of row r at slot c ^ ((r >> 2) & 3) (again 16 distinct slots per
 // ds_read_b128 lane group); half the bytes per stage, so twice the ring depth fits in the same LDS -- the 256 x 256
 // tiles keep 3-4 K-tiles in flight instead of one.  The MFMA sequence per output element does not depend on BK.
-//
-// LW (loader waves): WM x WN more waves that only issue the stage DMAs (the DMA geometry of the compute waves above);
-// the compute waves only read fragments and multiply (the same MFMA sequence: bitwise equal).  The loaders join every
-// barrier, the epilogue's too (as inactive threads).
-template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H, int WN = 2, int WM = 2, int BK = 64,
-          bool LW = false>
-__global__ __launch_bounds__(64 * WM * WN * (LW ? 2 : 1)) void gemm_glds_kernel(GemmPB p) {
-  constexpr int NW = WM * WN;  // (compute) waves: WM along M x WN along N
-  static_assert(!LW || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT), "LW: the cross-wave epilogue reductions");
+template <int BM, int BN, int NS, int AMODE, int CMODE, typename TC, typename H, int WN = 2, int WM = 2, int BK = 64>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
+  constexpr int NW = WM * WN;  // waves: WM along M x WN along N
   constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN);
   static_assert(TM >= 1 && TN >= 1, "tile too small for the wave layout");
   static_assert(BK == 64 || (BK == 32 && AMODE != AM_SCALE), "K-tile width");
@@ -587,9 +580,7 @@ __global__ __launch_bounds__(64 * WM * WN * (LW ? 2 : 1)) void gemm_glds_kernel(
   static_assert(NS >= 2 && NS <= 5, "ring depth");
   static_assert(SM_BYTES <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave_id = tid >> 6;
-  const bool loads = !LW || wave_id >= NW, computes = !LW || wave_id < NW;
-  const int wave = LW ? wave_id % NW : wave_id;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   // slot permutation key of row r
   auto swz = [](int r) { return BK == 64 ? (r >> 1) & 7 : (r >> 2) & 3; };
@@ -722,28 +713,24 @@ __global__ __launch_bounds__(64 * WM * WN * (LW ? 2 : 1)) void gemm_glds_kernel(
     }
   };
 
-  if (loads) {
 #pragma unroll
-    for (int t = 0; t < NS - 1; ++t)
-      if (t < nk) issue(t);
-  }
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
   for (int t = 0; t < nk; ++t) {
     // retire K-tile t (this wave's DMAs), leaving the later tiles of the ring in flight; the barrier then makes every
     // wave's part of tile t visible and frees the stage read at step t - 1 for tile t + NS - 1
-    if (loads) {
-      if (NS >= 5 && t + 3 < nk) wait_vm<3 * G>();
-      else if (NS >= 4 && t + 2 < nk) wait_vm<2 * G>();
-      else if (NS >= 3 && t + 1 < nk) wait_vm<G>();
-      else wait_vm<0>();
-    }
+    if (NS >= 5 && t + 3 < nk) wait_vm<3 * G>();
+    else if (NS >= 4 && t + 2 < nk) wait_vm<2 * G>();
+    else if (NS >= 3 && t + 1 < nk) wait_vm<G>();
+    else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (loads && t + NS - 1 < nk) issue(t + NS - 1);
-    if (computes) compute(t % NS);
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    compute(t % NS);
   }
   __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
-  gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM, EPP>(p, acc, smem, m0, n0, computes);
+  gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM, EPP>(p, acc, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
@@ -1422,12 +1409,6 @@ int cu_count() {
 // Auto ring depth: the deepest ring (<= 4, <= nmax) with which every CU still holds all the blocks the grid gives it
 // (LDS per block = max(depth x stage, fp32 C staging)).  The small-grid deep-level GEMMs (2 blocks per CU, 8 K-steps,
 // memory-latency bound) get 3 / 4 tiles in flight; large grids keep 2 and their blocks per CU.
-// NBP_GEMM_LW (A/B, round 4): 1 = every LDS-DMA tile with loader waves; 2 = also 128 x 128 tiles from 128 blocks
-int gemm_lw() {  // (read per launch, like NBP_GLDS: the bitwise test switches it in one process)
-  const char* e = getenv("NBP_GEMM_LW");
-  return e ? atoi(e) : 0;
-}
-
 int glds_auto_depth(long blocks, int stage_bytes, int c_bytes, int nmax) {
   const long per_cu = (blocks + cu_count() - 1) / cu_count();
   for (int d = nmax; d > 2; --d) {
@@ -1453,15 +1434,6 @@ void launch(const GemmPB& p, hipStream_t st) {
       constexpr int STB = (BM + BN) * 128 + (AMODE == AM_SCALE ? 256 : 0), CB = BM * (BN + 4) * 4;
       constexpr int NMAX = 4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
       const int nd = ns_env < 0 ? glds_auto_depth((long)grid.x * grid.y, STB, CB, NMAX) : (ns < NMAX ? ns : NMAX);
-      if constexpr (CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
-        if (gemm_lw()) {  // 2 x 2 compute waves + 2 x 2 loader waves
-          if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 2, 2, 64, true><<<grid, 512, 0, st>>>(p);
-          else if (nd == 3)
-            gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H, 2, 2, 64, true><<<grid, 512, 0, st>>>(p);
-          else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 2, 2, 64, true><<<grid, 512, 0, st>>>(p);
-          return;
-        }
-      }
       if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
         // 2 x 4 waves of (BM / 2) x (BN / 4), two per SIMD (+2 % step over 2 x 2 waves)
         if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
@@ -1516,8 +1488,7 @@ void dispatch(const GemmPB& p, hipStream_t st) {
     auto blocks = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
     const bool n128 = p.N > 64, m128 = p.M > 64;
     const long mb = GEMM_MINBLK;
-    if (m128 && n128 && (blocks(128, 128) >= mb || (gemm_lw() == 2 && blocks(128, 128) >= 128)))
-      launch<128, 128, AMODE, CMODE, TA, TC, H>(p, st);
+    if (m128 && n128 && blocks(128, 128) >= mb) launch<128, 128, AMODE, CMODE, TA, TC, H>(p, st);
     else if (m128 && blocks(128, 64) >= mb) launch<128, 64, AMODE, CMODE, TA, TC, H>(p, st);
     else if (n128 && blocks(64, 128) >= mb) launch<64, 128, AMODE, CMODE, TA, TC, H>(p, st);
     else launch<64, 64, AMODE, CMODE, TA, TC, H>(p, st);

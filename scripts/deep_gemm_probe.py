@@ -1,5 +1,5 @@
 """The deep-level 1x1-conv GEMM shapes (16x16 x C512 and 32x32 x C256 levels at bs 16: M = 4096 / 16384) on the
-16-bit DMA GEMM, GPU time per launch (HIP-graph replays).  Run once per NBP_GEMM_LW / NBP_GLDS value to compare the
+16-bit DMA GEMM, GPU time per launch (HIP-graph replays).  Run once per NBP_GLDS value to compare the
 tile forms: python scripts/deep_gemm_probe.py"""
 import os
 import sys
@@ -13,7 +13,7 @@ from scripts.gemm_micro_util import timeit  # noqa: E402
 dev = torch.device("cuda:0")
 TD = torch.float16
 tot = 0.0
-out = [f"NBP_GEMM_LW={os.environ.get('NBP_GEMM_LW', '-')} NBP_GLDS={os.environ.get('NBP_GLDS', '-')}"]
+out = [f"NBP_GLDS={os.environ.get('NBP_GLDS', '-')}"]
 for M, C in ((4096, 512), (16384, 256)):
     for N, K in ((2 * C, C), (C, C), (C, 2 * C)):
         A = torch.randn(M, K, device=dev).to(TD)

@@ -12,30 +12,25 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def run_modes(fn, modes=("0", "auto", "lw1", "lw2")):
-    """fn's outputs bitwise equal under NBP_GLDS=0 (register-staged tiles), auto (LDS-DMA ring) and lw1 / lw2 (the
-    ring with loader waves, NBP_GEMM_LW=1; 2 also takes 128 x 128 tiles from 128 blocks)."""
+def run_modes(fn, modes=("0", "auto")):
     outs = {}
-    old = {k: os.environ.get(k) for k in ("NBP_GLDS", "NBP_GEMM_LW")}
+    old = os.environ.get("NBP_GLDS")
     try:
         for ns in modes:  # auto (unset): the depth chosen per launch from the grid
-            os.environ.pop("NBP_GLDS", None)
-            os.environ.pop("NBP_GEMM_LW", None)
-            if ns.startswith("lw"):
-                os.environ["NBP_GEMM_LW"] = ns[2:]
-            elif ns != "auto":
+            if ns == "auto":
+                os.environ.pop("NBP_GLDS", None)
+            else:
                 os.environ["NBP_GLDS"] = ns
             outs[ns] = [t.clone() for t in fn()]
             torch.cuda.synchronize()
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        if old is None:
+            os.environ.pop("NBP_GLDS", None)
+        else:
+            os.environ["NBP_GLDS"] = old
     for ns in modes[1:]:
         for a, b in zip(outs[modes[0]], outs[ns]):
-            assert torch.equal(a, b), f"mode {ns} differs from mode {modes[0]}"
+            assert torch.equal(a, b), f"NBP_GLDS={ns} differs from NBP_GLDS={modes[0]}"
 
 
 DT = {1: torch.bfloat16, 2: torch.float16}
