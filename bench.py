@@ -76,7 +76,7 @@ ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skin
                    "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel"], "wgrad_group": ["wgrad_bf16_wide_group"],
                    "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
                    "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32, false>"],
-                   "dw_fwd": ["dw_sg_pool_tiled"]}
+                   "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"]}
 # classes that are ONE kernel (one template instance in the step): the headline `roofline` is the one of them with the
 # most time per step (the dominant kernel); the multi-kernel classes are reported beside it
 SINGLE_KERNEL = ("dw_bwd_32", "wgrad_group", "reduce")
@@ -150,6 +150,24 @@ def cost_dw_fwd(a):  # (t1,w,b,t2,g,pool,B,h,w,c,dt): t1 2C in, t2 2C + g C out
     return 2.0 * M * 2 * c * 9, (2 + (2 if a[3] is not None else 0) + 1) * M * c * _e(a[10])
 
 
+def cost_ffn(a):  # (n2,W4,b4,W5,b5,y,gamma,lnw,lnb,out,nout,stats,M,C,eps,dt): n2 + y in, out (+ nout + stats) out
+    M, C = a[12], a[13]
+    by = (3 * M * C + 3 * C * C + (M * C if a[10] is not None else 0)) * 2 + (8 * M if a[11] is not None else 0)
+    return 2.0 * M * 2 * C * C + 2.0 * M * C * C, by
+
+
+def cost_sg_rc_wg(a):  # cost_sg_rc + the folded weight gradients U = dout^T g, dW4 = dt4^T n2 (fp32 partial slabs)
+    fl, by = cost_sg_rc(a)
+    M, N, K = a[8], a[9], a[10]
+    return fl + 2.0 * M * N * N + 2.0 * M * 2 * N * K, by
+
+
+def cost_c1dw(a):  # (n1,w1,b1,wdw,bdw,t1,t2,g,pool,B,h,w,c,dt): n1 C in, t1 2C (+ t2 2C) + g C out, conv1 weight
+    M, c = a[9] * a[10] * a[11], a[12]
+    by = (M * c + 2 * M * c + (2 * M * c if a[6] is not None else 0) + M * c + 2 * c * c) * _e(a[13])
+    return 2.0 * M * 2 * c * c + 2.0 * M * 2 * c * 9, by
+
+
 def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
     M, N, K = a[11], a[12], a[13]
     return 2.0 * M * N * K, 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0))
@@ -209,7 +227,8 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "dgrad_ln_bwd": rec_plain("gemm16", cost_dgrad_ln), "dgrad_sg_rc": rec_plain("gemm16", cost_sg_rc),
            "gemm_f32": rec_plain("gemm_f32", cost_gemm_f32), "wgrad_f32": rec_wgrad, "wgrad_group": rec_wgroup,
            "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_dw_bwd,
-           "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd)}
+           "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd), "gemm_ffn": rec_plain("gemm16", cost_ffn),
+           "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw)}
 
 
 def _pmc_traffic(cls):

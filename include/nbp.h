@@ -220,6 +220,14 @@ int nbp_dw_chunks(int B, int H, int W, int C, int which);
 int nbp_dw_fwd_slab_rows(int B, int H, int W, int C, int dtype);
 int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void* t2, void* g, float* pool_slab, int B,
                        int H, int W, int C, int dtype, nbp_stream_t s);
+/* The deep levels' conv1 -> conv2 depthwise -> SimpleGate -> pool in one launch (NAFNet_arch.py:59-68, whole-image
+ * tiles, 16-bit storage): t1 = n1 W1^T + b1 [B*H*W][2C] (the tape), t2 (NULL: not kept), g [B*H*W][C] and the pool
+ * sums pool[B][C] (a one-row pool_slab: nbp_sca_fwd with chunks = 1).  t1 / t2 / g bitwise those of nbp_gemm_bf16 +
+ * nbp_dw_sg_pool_fwd; pool up to fp32 summation order.  nbp_c1dw_supported(H, W, C, dtype) is 1 for the shape served
+ * (16 x 16 at C 512). */
+int nbp_c1dw_supported(int H, int W, int C, int dtype);
+int nbp_c1_dw_sg_pool(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
+                      void* t2, void* g, float* pool, int B, int H, int W, int C, int dtype, nbp_stream_t s);
 /* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s);

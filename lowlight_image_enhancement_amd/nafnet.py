@@ -110,6 +110,9 @@ class NAFNet(nn.Module):
         # level 0 with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
         # (nbp_gemm_ffn, bitwise the two launches, +0.1 % step), g2 never stored
         self.fuse_ffn = True
+        # the middle level (16 x 16 at C 512): conv1 -> depthwise -> SimpleGate -> pool as one whole-image launch
+        # (nbp_c1_dw_sg_pool; t1 / t2 / g bitwise, the pool up to fp32 summation order)
+        self.fuse_c1dw = True
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
@@ -389,7 +392,8 @@ class NAFNet(nn.Module):
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
-        chunks = query("dw_fwd_slab_rows", B, h, w, c, dt)
+        c1dw = self.fuse_c1dw and dt != 0 and len(self._W) == 3 and query("c1dw_supported", h, w, c, dt) == 1
+        chunks = 1 if c1dw else query("dw_fwd_slab_rows", B, h, w, c, dt)
         t1, t2, g, pool = E(M, 2 * c), E(M, 2 * c), E(M, c), F(B * chunks * c)
         mean, a = F(B, c), F(B, c)
         y, n2, st2 = E(M, c), E(M, c), F(M, 2)
@@ -406,10 +410,15 @@ class NAFNet(nn.Module):
         if not have_n1:
             call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"),
                  n1, st1, M, c, LN_EPS, dt)
-        self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c,
-                 c, bias=self._slice(P, pre + "conv1.bias"))
-        call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"),
-             t2, g, pool, B, h, w, c, dt)
+        if c1dw:
+            call("c1_dw_sg_pool", n1, self._slice(self._W[1], pre + "conv1.weight"), self._slice(P, pre + "conv1.bias"),
+                 self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t1, t2, g, pool, B, h, w,
+                 c, dt)
+        else:
+            self._mm(self._W, n1, c, AM_PLAIN, None, 1, pre + "conv1.weight", t1, 2 * c, CM_PLAIN, M, 2 * c,
+                     c, bias=self._slice(P, pre + "conv1.bias"))
+            call("dw_sg_pool_fwd", t1, self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"),
+                 t2, g, pool, B, h, w, c, dt)
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"),
              mean, a, B, hw, c)
         if fuse_ln:
@@ -576,7 +585,8 @@ class NAFNet(nn.Module):
         return dx_img
 
     def _stage_done(self, name, hook):
-        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice
+        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice (one flush
+        # at the end of a hook-less backward measured neutral)
         call("grad_reduce_flush", 0)
         self._keep.clear()
         if hook is not None:
