@@ -144,9 +144,18 @@ __device__ __forceinline__ void st8f(void* base, long off, const float* v) {
 // WM x WN waves (default 2 x 2), each (BM / WM) x (BN / WN) of 32 x 32 MFMA tiles; NT = 64 WM WN threads.
 // PASSES > 1 (tiles whose fp32 image would not fit in LDS): the rows of wave-row group q (WM / PASSES wave rows) are
 // staged and stored in pass q, one pass after the other through the same LDS rows.
-template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2, int WM = 2, int PASSES = 1>
+// CM_LNBWD chunk inputs loaded before the K loop (gemm_glds_kernel, 16-bit C): the x / dres chunks and the row
+// statistics of each of the thread's NPRE epilogue chunks (their latency then overlaps the K loop)
+template <int NPRE>
+struct LnPre {
+  uint4 x[NPRE], r[NPRE];
+  float2 st[NPRE];
+};
+
+template <int BM, int BN, int CMODE, typename TC, typename H, int WN = 2, int WM = 2, int PASSES = 1, int NPRE = 0>
 __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[BM / (32 * WM)][BN / (32 * WN)],
-                                              unsigned char* smem, int m0, int n0) {
+                                              unsigned char* smem, int m0, int n0,
+                                              const LnPre<(NPRE > 0 ? NPRE : 1)>* pre = nullptr) {
   constexpr int TM = BM / (32 * WM), TN = BN / (32 * WN), NT = 64 * WM * WN;
   static_assert((WN == 2 && WM == 2) || (CMODE != CM_LNBWD && CMODE != CM_CHANDOT),
                 "cross-wave reductions assume 2 x 2 waves");
@@ -182,7 +191,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       }
   }
   __syncthreads();
-  for (int e = tid; e < PR * G8; e += NT) {
+  constexpr int NIT = (PR * G8 + NT - 1) / NT;
+  static_assert(NPRE == 0 || (CMODE == CM_LNBWD && NPRE == NIT && PASSES == 1), "preloaded LN-backward chunks");
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * NT;
+    if (e >= PR * G8) break;
     const int row = e / G8, c8 = (e % G8) * 8;
     const int grow = m0 + pass * PR + row, gcol = n0 + c8;
     if (grow >= M || gcol >= N) continue;
@@ -193,9 +207,21 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       static_assert(BN == 128 || BN == 256 || BN == 512, "CM_LNBWD (tiled): full-row tiles");
       const long off = (long)grow * N + gcol;
       float xv[8], rv[8];
-      ld8f<TC>(p.R, off, xv);
-      ld8f<TC>(p.dres, off, rv);
-      const float2 st = p.stats_in[grow];
+      float2 st;
+      if constexpr (NPRE > 0) {
+        const vec_t<TC, 8> xr = __builtin_bit_cast(vec_t<TC, 8>, pre->x[it]);
+        const vec_t<TC, 8> rr = __builtin_bit_cast(vec_t<TC, 8>, pre->r[it]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xv[j] = (float)xr[j];
+          rv[j] = (float)rr[j];
+        }
+        st = pre->st[it];
+      } else {
+        ld8f<TC>(p.R, off, xv);
+        ld8f<TC>(p.dres, off, rv);
+        st = p.stats_in[grow];
+      }
       const float inv = 1.f / st.y;
       const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4);
       const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
@@ -292,8 +318,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
         if (p.rscale) {
           const float4 s0 = ld4(p.rscale + gcol), s1 = ld4(p.rscale + gcol + 4);
           const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          // one fused multiply-add, spelt out (what the compiler contracted r + s * v to; left implicit, a change of
+          // the code around it -- a residual preload tried in round 4 -- un-fused it and changed the stored bits)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = rv[j] + sc[j] * v[j];
+          for (int j = 0; j < 8; ++j) v[j] = fmaf(sc[j], v[j], rv[j]);
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = rv[j] + v[j];
@@ -713,6 +741,29 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
     }
   };
 
+  // CM_LNBWD (16-bit C): the epilogue's x / dres chunks and row statistics loaded now, under the K loop.  Issued before
+  // the ring's prologue DMAs: the first counted retire then also covers them, and they complete first.  64 x 256 tiles
+  // (the 32 x 32 level's conv1 / conv4 dgrads): 22.3 -> 20.0 us per launch in the step trace; the same preload of the
+  // residual chunk in the CM_PLAIN / CM_RESLN epilogues measured neutral in the step (1236 vs 1236 img/s) and was
+  // not kept
+  constexpr bool LPRE = CMODE == CM_LNBWD && sizeof(TC) == 2 && EPP == 1;
+  constexpr int NPRE = LPRE ? (BM * (BN / 8) + 64 * NW - 1) / (64 * NW) : 0;
+  LnPre<(NPRE > 0 ? NPRE : 1)> lpre;
+  if constexpr (LPRE) {
+#pragma unroll
+    for (int it = 0; it < NPRE; ++it) {
+      const int e = tid + it * 64 * NW, row = e / (BN / 8), c8 = (e % (BN / 8)) * 8;
+      const int grow = m0 + row, gcol = n0 + c8;
+      lpre.x[it] = lpre.r[it] = make_uint4(0, 0, 0, 0);
+      lpre.st[it] = make_float2(0.f, 1.f);
+      if (e < BM * (BN / 8) && grow < M && gcol < N) {
+        const long off = (long)grow * N + gcol;
+        lpre.x[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const TC*>(p.R) + off);
+        lpre.r[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const TC*>(p.dres) + off);
+        lpre.st[it] = p.stats_in[grow];
+      }
+    }
+  }
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
@@ -730,7 +781,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
     compute(t % NS);
   }
   __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
-  gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM, EPP>(p, acc, smem, m0, n0);
+  gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM, EPP, NPRE>(p, acc, smem, m0, n0, &lpre);
 }
 
 // ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
