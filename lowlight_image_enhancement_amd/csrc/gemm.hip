@@ -1417,11 +1417,36 @@ void wgroup_launch_chunk(hipStream_t st, int ns, int q0, int q1) {
     p.chunk = cdiv(cdiv(p.M, (int)s), 64) * 64;
     const int S_ = cdiv(p.M, p.chunk);
     const int es = g_wqueue_dtype != 0 ? 2 : 4;
+    bool direct = false;
+    if (S_ == 1) {
+      // one split: the tile writes the weight (and bias) gradient itself and its queued reductions -- copies -- are
+      // dropped; not for the layer-scale problems (their U / V are reduced straight from the slabs by the flush)
+      auto ls = [](const float* out) {
+        for (const PDesc& q : g_post)
+          if (q.U == out || q.V == out) return true;
+        return false;
+      };
+      int iw = -1, ib = -1;
+      for (int r = 0; r < (int)g_pending.size(); ++r) {
+        if (g_pending[r].slab == p.slab) iw = r;
+        if (p.slab_b && g_pending[r].slab == p.slab_b) ib = r;
+      }
+      if (iw >= 0 && !ls(g_pending[iw].out) && (!p.slab_b || (ib >= 0 && !ls(g_pending[ib].out)))) {
+        float* ow = g_pending[iw].out;
+        float* ob = p.slab_b ? g_pending[ib].out : nullptr;
+        if (ib > iw) g_pending.erase(g_pending.begin() + ib);
+        g_pending.erase(g_pending.begin() + iw);
+        if (ib >= 0 && ib < iw) g_pending.erase(g_pending.begin() + ib);
+        p.slab = ow;
+        p.slab_b = ob;
+        direct = true;
+      }
+    }
     g_stats_group[0] += 1;
     g_stats_group[1] += 2.0 * p.M * p.N * p.K;
     g_stats_group[2] += (double)p.M * (p.N + p.K) * es;
     g_stats_group[3] += (double)p.N * p.K * 4 + (p.slab_b ? (double)p.N * 4 : 0.0);
-    g_stats_group[4] += (double)S_ * p.N * p.K * 4 + (p.slab_b ? (double)S_ * p.N * 4 : 0.0);
+    if (!direct) g_stats_group[4] += (double)S_ * p.N * p.K * 4 + (p.slab_b ? (double)S_ * p.N * 4 : 0.0);
     for (RDesc& d : g_pending)
       if (d.slab == p.slab || (p.slab_b && d.slab == p.slab_b)) d.S = S_, d.ty = make_rdesc(d.slab, S_, d.L, d.out).ty;
   }
