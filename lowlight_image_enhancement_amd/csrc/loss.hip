@@ -68,6 +68,10 @@ __global__ void finalize_mean(const double* __restrict__ partial, int n, double 
 // runs LDS -> LDS, the vertical pass LDS -> registers, then the SSIM map, the per-block loss partial and the three
 // gradient-coefficient maps (the only global writes).  Every input pixel is read from HBM once (+halo).
 constexpr int SS_TH = 32, SS_TW = 64, SS_R = 5;
+// Both passes are register-blocked by 4 along their filter direction: a thread reads the 14 staged values four
+// outputs need once and runs each output's 11-tap chain in the original tap order (so every coefficient is bitwise the
+// unblocked kernel's); the horizontal passes read LDS as float4 (row pitch 76, a multiple of 4).
+constexpr int SS_P = SS_TW + 2 * SS_R + 2;
 
 // inv_n: the reduction's weight of one pixel in the coefficient maps (1/n for 'mean', 1 for 'sum' and 'none'; with
 // 'none' the backward multiplies each coefficient by that pixel's upstream gradient); lmap (optional): the clamped
@@ -77,87 +81,136 @@ __global__ __launch_bounds__(256) void ssim_fwd_tiled(const float* __restrict__ 
                                                        float inv_n, double* __restrict__ partial,
                                                        float* __restrict__ coef, float* __restrict__ lmap, long n) {
   constexpr int LH = SS_TH + 2 * SS_R, LW = SS_TW + 2 * SS_R;
-  __shared__ float xs[LH][LW + 1], ys[LH][LW + 1];
-  __shared__ float hm[5][LH][SS_TW + 1];
+  // hm (the horizontal pass) overwrites xs / ys once every task holds its outputs in registers: 54 KB of LDS per
+  // tile, three tiles per CU
+  static_assert(5 * SS_TW >= 2 * SS_P, "hm must cover xs / ys");
+  __shared__ __attribute__((aligned(16))) float sbuf[5 * LH * SS_TW];
+  auto xs = reinterpret_cast<float (*)[SS_P]>(sbuf);
+  auto ys = reinterpret_cast<float (*)[SS_P]>(sbuf + LH * SS_P);
+  auto hm = reinterpret_cast<float (*)[LH][SS_TW]>(sbuf);
   __shared__ double red[16];
   const int tid = threadIdx.x;
   const int x0 = blockIdx.x * SS_TW, y0 = blockIdx.y * SS_TH;
   const long plane = blockIdx.z;
   const float* xp = x + plane * H * W;
   const float* yp = y + plane * H * W;
-  // staging in batches of 4 positions per thread: all 8 loads issued before the LDS stores
-  for (int e0 = tid; e0 < LH * LW; e0 += 4 * 256) {
-    float xv[4], yv[4];
+  // staging: every load of the thread's NB positions issued before the first LDS store
+  constexpr int NB = (LH * LW + 255) / 256;
+  float xv[NB], yv[NB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256;
-      const int r = e / LW, c = e % LW;
-      const int gy = y0 - SS_R + r, gx = x0 - SS_R + c;
-      xv[u] = yv[u] = 0.f;
-      if (e < LH * LW && gy < H + SS_R && gx < W + SS_R) {  // positions further out feed no valid output
-        const long o = (long)refl(gy, H) * W + refl(gx, W);
-        xv[u] = xp[o];
-        yv[u] = yp[o];
+  for (int u = 0; u < NB; ++u) {
+    const int e = tid + u * 256;
+    const int r = e / LW, c = e % LW;
+    const int gy = y0 - SS_R + r, gx = x0 - SS_R + c;
+    xv[u] = yv[u] = 0.f;
+    if (e < LH * LW && gy < H + SS_R && gx < W + SS_R) {  // positions further out feed no valid output
+      const long o = (long)refl(gy, H) * W + refl(gx, W);
+      xv[u] = xp[o];
+      yv[u] = yp[o];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int e = tid + u * 256;
+    if (e >= LH * LW) break;
+    const int r = e / LW, c = e % LW;
+    xs[r][c] = clamp_in ? clamp01(xv[u]) : xv[u];
+    ys[r][c] = clamp_in ? clamp01(yv[u]) : yv[u];
+  }
+  __syncthreads();
+  // horizontal 11-tap pass of {x, y, x^2, y^2, xy}: one row, four consecutive output columns per task
+  constexpr int HT = LH * (SS_TW / 4), HIT = (HT + 255) / 256;
+  float o[HIT][5][4];
+#pragma unroll
+  for (int it = 0; it < HIT; ++it) {
+    const int e = tid + it * 256;
+    if (e >= HT) break;
+    const int r = e >> 4, c0 = (e & 15) * 4;
+    float xw[16], yw[16];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const float4 a = *reinterpret_cast<const float4*>(&xs[r][c0 + 4 * s4]);
+      const float4 b = *reinterpret_cast<const float4*>(&ys[r][c0 + 4 * s4]);
+      xw[4 * s4] = a.x; xw[4 * s4 + 1] = a.y; xw[4 * s4 + 2] = a.z; xw[4 * s4 + 3] = a.w;
+      yw[4 * s4] = b.x; yw[4 * s4 + 1] = b.y; yw[4 * s4 + 2] = b.z; yw[4 * s4 + 3] = b.w;
+    }
+    float xx[14], yy[14], xy[14];  // the products once per staged value, not once per tap
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      xx[i] = xw[i] * xw[i];
+      yy[i] = yw[i] * yw[i];
+      xy[i] = xw[i] * yw[i];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 11; ++t) {
+        const float k = win.k[t];
+        s0 = fmaf(k, xw[q + t], s0);
+        s1 = fmaf(k, yw[q + t], s1);
+        s2 = fmaf(k, xx[q + t], s2);
+        s3 = fmaf(k, yy[q + t], s3);
+        s4 = fmaf(k, xy[q + t], s4);
       }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256;
-      if (e >= LH * LW) break;
-      const int r = e / LW, c = e % LW;
-      xs[r][c] = clamp_in ? clamp01(xv[u]) : xv[u];
-      ys[r][c] = clamp_in ? clamp01(yv[u]) : yv[u];
+      o[it][0][q] = s0; o[it][1][q] = s1; o[it][2][q] = s2; o[it][3][q] = s3; o[it][4][q] = s4;
     }
   }
   __syncthreads();
-  for (int e = tid; e < LH * SS_TW; e += 256) {
-    const int r = e / SS_TW, c = e % SS_TW;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
 #pragma unroll
-    for (int t = 0; t < 11; ++t) {
-      const float xv = xs[r][c + t], yv = ys[r][c + t], k = win.k[t];
-      s0 = fmaf(k, xv, s0);
-      s1 = fmaf(k, yv, s1);
-      s2 = fmaf(k, xv * xv, s2);
-      s3 = fmaf(k, yv * yv, s3);
-      s4 = fmaf(k, xv * yv, s4);
-    }
-    hm[0][r][c] = s0; hm[1][r][c] = s1; hm[2][r][c] = s2; hm[3][r][c] = s3; hm[4][r][c] = s4;
+  for (int it = 0; it < HIT; ++it) {
+    const int e = tid + it * 256;
+    if (e >= HT) break;
+    const int r = e >> 4, c0 = (e & 15) * 4;
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+      *reinterpret_cast<float4*>(&hm[m][r][c0]) = make_float4(o[it][m][0], o[it][m][1], o[it][m][2], o[it][m][3]);
   }
   __syncthreads();
+  // vertical pass + SSIM map: one column, four consecutive output rows per task
   double sacc = 0.0;
-  for (int e = tid; e < SS_TH * SS_TW; e += 256) {
-    const int r = e / SS_TW, c = e % SS_TW;
-    const int gy = y0 + r, gx = x0 + c;
-    if (gy >= H || gx >= W) continue;
-    float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int e = tid; e < (SS_TH / 4) * SS_TW; e += 256) {
+    const int r0 = (e / SS_TW) * 4, c = e % SS_TW;
+    const int gx = x0 + c;
+    if (gx >= W || y0 + r0 >= H) continue;
+    float h[5][14];
 #pragma unroll
-    for (int t = 0; t < 11; ++t) {
-      const float k = win.k[t];
+    for (int m = 0; m < 5; ++m)
 #pragma unroll
-      for (int m = 0; m < 5; ++m) v[m] = fmaf(k, hm[m][r + t][c], v[m]);
-    }
-    const float mx = v[0], my = v[1];
-    const float mx2 = mx * mx, my2 = my * my, mxy = mx * my;
-    const float sxx = v[2] - mx2, syy = v[3] - my2, sxy = v[4] - mxy;
-    const float A1 = 2.f * mxy + C1, A2 = 2.f * sxy + C2;
-    const float B1 = mx2 + my2 + C1, B2 = sxx + syy + C2;
-    const float num = A1 * A2, D = B1 * B2 + eps;
-    const float S = num / D;
-    const float l = (1.f - S) / 2.f;
-    const float lc = fminf(fmaxf(l, 0.f), 1.f);
-    sacc += lc;
-    if (lmap) lmap[(plane * H + gy) * W + gx] = lc;
-    if (coef) {
-      const float dS = (l >= 0.f && l <= 1.f) ? -0.5f * inv_n : 0.f;
-      // dnum/dmx = 2 my (A2 - A1); dden/dmx = 2 mx (B2 - B1); dS/dE[x^2] = -S B1 / D; dS/dE[xy] = 2 A1 / D
-      const float dmx = (2.f * my * (A2 - A1) - S * 2.f * mx * (B2 - B1)) / D;
-      const float dxx = -S * B1 / D;
-      const float dxy = 2.f * A1 / D;
+      for (int i = 0; i < 14; ++i) h[m][i] = hm[m][r0 + i][c];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int gy = y0 + r0 + q;
+      if (gy >= H) break;
+      float v[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 11; ++t) {
+        const float k = win.k[t];
+#pragma unroll
+        for (int m = 0; m < 5; ++m) v[m] = fmaf(k, h[m][q + t], v[m]);
+      }
+      const float mx = v[0], my = v[1];
+      const float mx2 = mx * mx, my2 = my * my, mxy = mx * my;
+      const float sxx = v[2] - mx2, syy = v[3] - my2, sxy = v[4] - mxy;
+      const float A1 = 2.f * mxy + C1, A2 = 2.f * sxy + C2;
+      const float B1 = mx2 + my2 + C1, B2 = sxx + syy + C2;
+      const float num = A1 * A2, D = B1 * B2 + eps;
+      const float S = num / D;
+      const float l = (1.f - S) / 2.f;
+      const float lc = fminf(fmaxf(l, 0.f), 1.f);
+      sacc += lc;
       const long o = (plane * H + gy) * W + gx;
-      coef[o] = dS * dmx;
-      coef[n + o] = dS * dxx;
-      coef[2 * n + o] = dS * dxy;
+      if (lmap) lmap[o] = lc;
+      if (coef) {
+        const float dS = (l >= 0.f && l <= 1.f) ? -0.5f * inv_n : 0.f;
+        // dnum/dmx = 2 my (A2 - A1); dden/dmx = 2 mx (B2 - B1); dS/dE[x^2] = -S B1 / D; dS/dE[xy] = 2 A1 / D
+        const float dmx = (2.f * my * (A2 - A1) - S * 2.f * mx * (B2 - B1)) / D;
+        const float dxx = -S * B1 / D;
+        const float dxy = 2.f * A1 / D;
+        coef[o] = dS * dmx;
+        coef[n + o] = dS * dxx;
+        coef[2 * n + o] = dS * dxy;
+      }
     }
   }
   sacc = block_sum_d(sacc, red);
@@ -169,8 +222,10 @@ __global__ __launch_bounds__(256) void ssim_fwd_tiled(const float* __restrict__ 
 // adjoint into LDS and the horizontal adjoint from LDS; 1-D adjoint of reflect padding: output j gathers
 // q in {j, -j (1 <= j <= 5), 2(n-1) - j (n-6 <= j <= n-2)}, taps q - t + 5 inside [0, n).  The reflected sources
 // stay inside the margin: -j only occurs in the first tile (TH > 5) and reads rows [0, 5 - j]; 2(n-1) - j reads
-// rows [n-5, n) with j >= y0.
+// rows [n-5, n) with j >= y0.  Interior groups of 4 rows (columns) run register-blocked; a group touching the
+// reflected border runs the per-output gather.
 constexpr int SB_TH = 32, SB_TW = 64, SB_M = 5;
+constexpr int SB_P = SB_TW + 2 * SB_M + 2;
 
 __device__ __forceinline__ int refl_sources(int j, int n, int* qs) {
   int nq = 0;
@@ -178,6 +233,28 @@ __device__ __forceinline__ int refl_sources(int j, int n, int* qs) {
   if (j >= 1 && j <= 5) qs[nq++] = -j;
   if (j <= n - 2 && j >= n - 6) qs[nq++] = 2 * (n - 1) - j;
   return nq;
+}
+
+// The reflected sources' taps of output j (after its direct window, in refl_sources order): only the lanes of the
+// five outputs next to each border run any; the direct window itself is the interior formula, the staged values
+// outside the image being zero.  lo: the source position of LDS index 0; NP: the LDS stride of one position; MS: of
+// one map.
+template <int NP, int MS>
+__device__ __forceinline__ void refl_extra(int j, int n, int lo, const Win& win, const float* __restrict__ base,
+                                           float& a0, float& a1, float& a2) {
+  int qs[3];
+  const int nq = refl_sources(j, n, qs);
+  for (int u = 1; u < nq; ++u) {
+    for (int t = 0; t < 11; ++t) {
+      const int rr = qs[u] - t + 5;
+      if (rr < 0 || rr >= n) continue;
+      const int l = (rr - lo) * NP;
+      const float k = win.k[t];
+      a0 = fmaf(k, base[l], a0);
+      a1 = fmaf(k, base[l + MS], a1);
+      a2 = fmaf(k, base[l + 2 * MS], a2);
+    }
+  }
 }
 
 // up_map (optional, reduction 'none'): the per-pixel upstream gradient, applied to the coefficients as they are
@@ -188,120 +265,150 @@ __global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ 
                                                        const float* __restrict__ up_map, float* __restrict__ gx,
                                                        long n) {
   constexpr int LH = SB_TH + 2 * SB_M, LW = SB_TW + 2 * SB_M;
-  __shared__ float cs[3][LH][LW + 1];
-  __shared__ float tv[3][SB_TH][LW + 1];
+  // tv (the vertical adjoint) overwrites cs once every task holds its outputs in registers: 38 KB of LDS per tile,
+  // four tiles per CU
+  __shared__ __attribute__((aligned(16))) float sbuf[3 * LH * SB_P];
+  auto cs = reinterpret_cast<float (*)[LH][SB_P]>(sbuf);
+  auto tv = reinterpret_cast<float (*)[SB_TH][SB_P]>(sbuf);
   const int tid = threadIdx.x;
   const int x0 = blockIdx.x * SB_TW, y0 = blockIdx.y * SB_TH;
   const long plane = blockIdx.z;
   const long pb = plane * H * W;
-  for (int e0 = tid; e0 < LH * LW; e0 += 4 * 256) {  // 12 loads in flight per thread, then the LDS stores
-    float v[4][3];
+  // every coefficient load of the thread's NB positions issued before the first LDS store
+  constexpr int NB = (LH * LW + 255) / 256;
+  float v[NB][3];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256;
-      const int r = e / LW, c = e % LW;
-      const int gy = y0 - SB_M + r, gxx = x0 - SB_M + c;
-      const bool in = e < LH * LW && gy >= 0 && gy < H && gxx >= 0 && gxx < W;
-      const long o = pb + (long)gy * W + gxx;
-      const float um = in && up_map ? up_map[o] : 1.f;
+  for (int u = 0; u < NB; ++u) {
+    const int e = tid + u * 256;
+    const int r = e / LW, c = e % LW;
+    const int gy = y0 - SB_M + r, gxx = x0 - SB_M + c;
+    const bool in = e < LH * LW && gy >= 0 && gy < H && gxx >= 0 && gxx < W;
+    const long o = pb + (long)gy * W + gxx;
+    const float um = in && up_map ? up_map[o] : 1.f;
 #pragma unroll
-      for (int m = 0; m < 3; ++m) v[u][m] = in ? coef[m * n + o] * um : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256;
-      if (e >= LH * LW) break;
-      const int r = e / LW, c = e % LW;
-#pragma unroll
-      for (int m = 0; m < 3; ++m) cs[m][r][c] = v[u][m];
-    }
+    for (int m = 0; m < 3; ++m) v[u][m] = in ? coef[m * n + o] * um : 0.f;
   }
-  // this thread's output pixels of x / y, loaded now so their latency overlaps the two adjoint passes
-  constexpr int PER = SB_TH * SB_TW / 256;
-  float xo[PER], yo[PER];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int e = tid + u * 256;
+    if (e >= LH * LW) break;
+    const int r = e / LW, c = e % LW;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) cs[m][r][c] = v[u][m];
+  }
+  // this thread's output pixels of x / y (two tasks of one row x four columns), loaded now so their latency overlaps
+  // the two adjoint passes
+  constexpr int PER = SB_TH * SB_TW / (4 * 256);
+  const bool vec = (W & 3) == 0;
+  float xo[PER][4], yo[PER][4];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int e = tid + k * 256, r = e / SB_TW, c = e % SB_TW;
-    const int j = y0 + r, i = x0 + c;
-    const long o = pb + (long)j * W + i;
-    const bool ok = j < H && i < W;
-    xo[k] = ok ? x[o] : 0.f;
-    yo[k] = ok ? y[o] : 0.f;
+    const int e = tid + k * 256, r = e >> 4, c0 = (e & 15) * 4;
+    const int j = y0 + r, i0 = x0 + c0;
+    const long o = pb + (long)j * W + i0;
+    if (j < H && vec && i0 + 3 < W) {
+      const float4 a = *reinterpret_cast<const float4*>(x + o);
+      const float4 b = *reinterpret_cast<const float4*>(y + o);
+      xo[k][0] = a.x; xo[k][1] = a.y; xo[k][2] = a.z; xo[k][3] = a.w;
+      yo[k][0] = b.x; yo[k][1] = b.y; yo[k][2] = b.z; yo[k][3] = b.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = j < H && i0 + q < W;
+        xo[k][q] = ok ? x[o + q] : 0.f;
+        yo[k][q] = ok ? y[o + q] : 0.f;
+      }
+    }
   }
   __syncthreads();
-  // vertical adjoint for the tile's rows and every staged column
-  for (int e = tid; e < SB_TH * LW; e += 256) {
-    const int r = e / LW, c = e % LW;
-    const int j = y0 + r;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    if (j >= 6 && j <= H - 7) {  // interior row: the plain 11-tap window, no reflected sources
-      const int lb = j - (y0 - SB_M) + 5;
+  // vertical adjoint for the tile's rows and every staged column: one column, four consecutive rows per task
+  constexpr int VT = (SB_TH / 4) * LW, VIT = (VT + 255) / 256;
+  float tvo[VIT][3][4];
+#pragma unroll
+  for (int it = 0; it < VIT; ++it) {
+    const int e = tid + it * 256;
+    if (e >= VT) break;
+    const int r0 = (e / LW) * 4, c = e % LW;
+    const int j0 = y0 + r0;
+    float w[3][14];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int i = 0; i < 14; ++i) w[m][i] = cs[m][r0 + i][c];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float a[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < 11; ++t) {
         const float k = win.k[t];
-        a0 = fmaf(k, cs[0][lb - t][c], a0);
-        a1 = fmaf(k, cs[1][lb - t][c], a1);
-        a2 = fmaf(k, cs[2][lb - t][c], a2);
-      }
-    } else if (j < H) {
-      int qs[3];
-      const int nq = refl_sources(j, H, qs);
-      for (int u = 0; u < nq; ++u) {
 #pragma unroll
-        for (int t = 0; t < 11; ++t) {
-          const int rr = qs[u] - t + 5;
-          if (rr < 0 || rr >= H) continue;
-          const int lr = rr - (y0 - SB_M);  // inside [0, LH) by the margin
-          const float k = win.k[t];
-          a0 = fmaf(k, cs[0][lr][c], a0);
-          a1 = fmaf(k, cs[1][lr][c], a1);
-          a2 = fmaf(k, cs[2][lr][c], a2);
-        }
+        for (int m = 0; m < 3; ++m) a[m] = fmaf(k, w[m][q + 10 - t], a[m]);
       }
+      const int j = j0 + q;
+      if ((j < 6 || j > H - 7) && j < H)
+        refl_extra<SB_P, LH * SB_P>(j, H, y0 - SB_M, win, &cs[0][0][c], a[0], a[1], a[2]);
+#pragma unroll
+      for (int m = 0; m < 3; ++m) tvo[it][m][q] = a[m];
     }
-    tv[0][r][c] = a0; tv[1][r][c] = a1; tv[2][r][c] = a2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < VIT; ++it) {
+    const int e = tid + it * 256;
+    if (e >= VT) break;
+    const int r0 = (e / LW) * 4, c = e % LW;
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tv[m][r0 + q][c] = tvo[it][m][q];
   }
   __syncthreads();
   const float g0 = up_map ? 1.f : up[0];
+  // horizontal adjoint + the pixel gradient: one row, four consecutive columns per task
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int e = tid + k * 256;
-    const int r = e / SB_TW, c = e % SB_TW;
-    const int j = y0 + r, i = x0 + c;
-    if (j >= H || i >= W) continue;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    if (i >= 6 && i <= W - 7) {  // interior column
-      const int lb = i - (x0 - SB_M) + 5;
+    const int e = tid + k * 256, r = e >> 4, c0 = (e & 15) * 4;
+    const int j = y0 + r, i0 = x0 + c0;
+    if (j >= H || i0 >= W) continue;
+    float w[3][16];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const float4 f = *reinterpret_cast<const float4*>(&tv[m][r][c0 + 4 * s4]);
+        w[m][4 * s4] = f.x; w[m][4 * s4 + 1] = f.y; w[m][4 * s4 + 2] = f.z; w[m][4 * s4 + 3] = f.w;
+      }
+    float a[3][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[0][q] = a[1][q] = a[2][q] = 0.f;
 #pragma unroll
       for (int t = 0; t < 11; ++t) {
-        const float k = win.k[t];
-        a0 = fmaf(k, tv[0][r][lb - t], a0);
-        a1 = fmaf(k, tv[1][r][lb - t], a1);
-        a2 = fmaf(k, tv[2][r][lb - t], a2);
+        const float kk = win.k[t];
+#pragma unroll
+        for (int m = 0; m < 3; ++m) a[m][q] = fmaf(kk, w[m][q + 10 - t], a[m][q]);
       }
+      const int i = i0 + q;
+      if ((i < 6 || i > W - 7) && i < W) refl_extra<1, SB_TH * SB_P>(i, W, x0 - SB_M, win, &tv[0][r][0], a[0][q], a[1][q], a[2][q]);
+    }
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float xr = xo[k][q];
+      float xv = xr, yv = yo[k][q];
+      if (clamp_in) { xv = clamp01(xv); yv = clamp01(yv); }
+      float gq = a[0][q] + 2.f * xv * a[1][q] + yv * a[2][q];
+      if (clamp_in && !(xr >= 0.f && xr <= 1.f)) gq = 0.f;
+      g[q] = g0 * gq;
+    }
+    const long o = pb + (long)j * W + i0;
+    if (vec && i0 + 3 < W) {
+      *reinterpret_cast<float4*>(gx + o) = make_float4(g[0], g[1], g[2], g[3]);
     } else {
-    int qs[3];
-    const int nq = refl_sources(i, W, qs);
-    for (int u = 0; u < nq; ++u) {
 #pragma unroll
-      for (int t = 0; t < 11; ++t) {
-        const int cc = qs[u] - t + 5;
-        if (cc < 0 || cc >= W) continue;
-        const int lc = cc - (x0 - SB_M);
-        const float k = win.k[t];
-        a0 = fmaf(k, tv[0][r][lc], a0);
-        a1 = fmaf(k, tv[1][r][lc], a1);
-        a2 = fmaf(k, tv[2][r][lc], a2);
-      }
+      for (int q = 0; q < 4; ++q)
+        if (i0 + q < W) gx[o + q] = g[q];
     }
-    }
-    const long o = pb + (long)j * W + i;
-    const float xr = xo[k];
-    float xv = xr, yv = yo[k];
-    if (clamp_in) { xv = clamp01(xv); yv = clamp01(yv); }
-    float g = a0 + 2.f * xv * a1 + yv * a2;
-    if (clamp_in && !(xr >= 0.f && xr <= 1.f)) g = 0.f;
-    gx[o] = g0 * g;
   }
 }
 
