@@ -412,6 +412,153 @@ __global__ __launch_bounds__(256) void bconv_wgrad(const float* __restrict__ src
   }
 }
 
+// Same contraction, operands staged through LDS: per (feature row, chunk of XC pixels) the block's 32 feature
+// channels (16-byte coalesced loads, XC * 64 B) and the three source rows around the feature row (CI planes, XC + 2
+// columns with zero padding) -- the gather above issues one 64-lane scattered load per MFMA operand.  The next
+// chunk's operands are loaded into registers while the MFMAs consume the current one.  Each wave runs the same
+// pixel-pair sequence (i = wave, wave + 4, ...) as the gather kernel, so every slab is bitwise the same.  Needs Cf a
+// multiple of 16 / sizeof(T).
+template <int MODE, int CI, typename T>
+__global__ __launch_bounds__(256, 4) void bconv_wgrad_lds(const float* __restrict__ src, const T* __restrict__ nhwc,
+                                                       float* __restrict__ slab_w, float* __restrict__ slab_b, Img g) {
+  constexpr int XC = 512 / sizeof(T);           // pixels per chunk: 16 KB of feature operand
+  constexpr int PPX = 32 * sizeof(T) / 16;      // 16-byte pieces per pixel
+  constexpr int EPP = 16 / sizeof(T);           // elements per piece
+  constexpr int BW = XC + 2;                    // staged source columns (x0 - 1 .. x0 + XC)
+  static_assert((XC / 2) % 4 == 0, "each wave keeps its pair residue across chunks");
+  // the operand tiles and the final cross-wave reduction share one LDS buffer (26 KB)
+  // bs rows: CI * 3 source rows, then a row of ones (the bias column's operand) and a row of zeros (columns past NK)
+  constexpr int AS_B = XC * 32 * (int)sizeof(T), BS_B = (CI * 3 + 2) * BW * 4, RED_B = 4 * 32 * 33 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[(AS_B + BS_B > RED_B) ? AS_B + BS_B : RED_B];
+  __shared__ float bred[4][64];
+  auto as = reinterpret_cast<T (*)[32]>(smem);
+  auto bs = reinterpret_cast<float (*)[3][BW]>(smem + AS_B);
+  auto red = reinterpret_cast<float (*)[32][33]>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5;
+  const int m0 = blockIdx.y * 32;
+  const int n = blockIdx.z * 32 + (lane & 31);
+  constexpr int NK = 9 * CI;
+  const int nc = n / 9, nt = n % 9, ndy = nt / 3 - 1, ndx = nt % 3 - 1;
+  // this lane's source tap relative to the chunk's staged rows / columns
+  const int ky = MODE == 0 ? ndy + 1 : 1 - ndy, kx = MODE == 0 ? ndx + 1 : 1 - ndx;
+  const bool ntap = n < NK, nbias = MODE == 0 && n == NK;
+  const int bc = ntap ? nc : 0;
+  // full chunks: this lane's operand addresses advance by a pair per MFMA with no per-pixel test
+  const float* bsx = &bs[0][0][0];
+  const float* bp = bsx + (ntap ? (nc * 3 + ky) * BW + kx : (nbias ? CI * 3 : CI * 3 + 1) * BW + 1) + half;
+  const T* ap = &as[half][lane & 31];
+  const float bm = (MODE == 1 && ntap && nt == 4) ? 1.f : 0.f;
+  for (int j = tid; j < 2 * BW; j += 256) (&bs[0][0][0])[CI * 3 * BW + j] = j < BW ? 1.f : 0.f;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float bacc = 0.f;
+  const int rows = g.B * g.Hp;
+  constexpr int KA = XC * PPX / 256, NBS = (CI * 3 * BW + 255) / 256;
+  uint4 va[KA];
+  float sv[NBS];
+  auto load = [&](int row, int x0) {
+    const int y = row % g.Hp, b = row / g.Hp;
+    const T* arow = nhwc + (long)row * g.Wp * g.Cf;
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      const int q = tid + k * 256, px = q / PPX, part = q % PPX;
+      const int x = x0 + px, c = m0 + part * EPP;
+      va[k] = make_uint4(0u, 0u, 0u, 0u);
+      if (x < g.Wp && c < g.Cf) va[k] = *reinterpret_cast<const uint4*>(arow + (long)x * g.Cf + c);
+    }
+#pragma unroll
+    for (int u = 0; u < NBS; ++u) {
+      const int e = tid + u * 256;
+      const int c = e / (3 * BW), k = (e / BW) % 3, j = e % BW;
+      const int yy = y + k - 1, xx = x0 - 1 + j;
+      sv[u] = 0.f;
+      if (e < CI * 3 * BW && yy >= 0 && yy < g.H0 && xx >= 0 && xx < g.W0)
+        sv[u] = src[(((long)b * CI + c) * g.H0 + yy) * g.W0 + xx];
+    }
+  };
+  int row = blockIdx.x, x0 = 0;
+  if (row < rows) load(row, 0);
+  while (row < rows) {
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      const int q = tid + k * 256;
+      *reinterpret_cast<uint4*>(&as[q / PPX][(q % PPX) * EPP]) = va[k];
+    }
+#pragma unroll
+    for (int u = 0; u < NBS; ++u) {
+      const int e = tid + u * 256;
+      if (e < CI * 3 * BW) (&bs[0][0][0])[e] = sv[u];
+    }
+    __syncthreads();
+    int nrow = row, nx0 = x0 + XC;
+    if (nx0 >= g.Wp) { nx0 = 0; nrow += gridDim.x; }
+    if (nrow < rows) load(nrow, nx0);
+    // U pairs' operands read before their MFMAs; pairs past the chunk read pair 0 and contribute zeros.  Pixels past
+    // the grid have a zero feature operand (staged so), which zeroes their products whatever the source tap holds.
+    const int np = min(XC, g.Wp - x0 + 1) >> 1;  // pixel pairs of this chunk (the last may hold one pixel)
+    constexpr int U = 8;
+    if (np == XC / 2) {
+      for (int i0 = wave; i0 < XC / 2; i0 += 4 * U) {
+        float av[U], bv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = i0 + 4 * u;
+          av[u] = (float)ap[i * 64];
+          bv[u] = bp[2 * i];
+          if (MODE == 1) bacc = fmaf(bm, bv[u], bacc);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+      }
+    } else {
+      // the row's last, partial chunk: one pair per step (the same MFMA sequence)
+      for (int i = wave; i < np; i += 4) {
+        const int xl = 2 * i + half;
+        const bool xval = x0 + xl < g.Wp;
+        const float av = (float)as[xl][lane & 31];
+        const float bt = bs[bc][ky][xl + kx];
+        const float bv = ntap ? bt : ((nbias && xval) ? 1.f : 0.f);
+        if (MODE == 1 && nt == 4) bacc += (ntap && xval) ? bt : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    row = nrow;
+    x0 = nx0;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[wave][8 * (r >> 2) + 4 * half + (r & 3)][lane & 31] = acc[r];
+  if (MODE == 1) bred[wave][lane] = bacc;
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * 32; e += 256) {
+    const int mi = e >> 5, ni = e & 31;
+    const int mm = blockIdx.y * 32 + mi, nn = blockIdx.z * 32 + ni;
+    const float v = ((red[0][mi][ni] + red[1][mi][ni]) + red[2][mi][ni]) + red[3][mi][ni];
+    if (mm >= g.Cf) continue;
+    if (MODE == 0) {
+      if (nn < NK) slab_w[((long)blockIdx.x * g.Cf + mm) * NK + nn] = v;
+      else if (nn == NK) slab_b[(long)blockIdx.x * g.Cf + mm] = v;
+    } else if (nn < NK) {
+      slab_w[(long)blockIdx.x * CI * g.Cf * 9 + ((long)(nn / 9) * g.Cf + mm) * 9 + nn % 9] = v;
+    }
+  }
+  if (MODE == 1 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < CI) {
+    const int l = threadIdx.x * 9 + 4;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += bred[w][l] + bred[w][l + 32];
+    slab_b[(long)blockIdx.x * CI + threadIdx.x] = s;
+  }
+}
+
+// NBP_BCONV_GATHER=1 (read per launch): the gather kernel -- the reference of the bitwise test
+bool bconv_lds(int Cf, int esize) {
+  const char* e = getenv("NBP_BCONV_GATHER");
+  if (e && e[0] == '1') return false;
+  return Cf % (16 / esize) == 0;
+}
+
 #define NBP_DISPATCH_CF(cf, ok, ...)                     \
   switch (cf) {                                          \
     case 8: { constexpr int CF = 8; __VA_ARGS__; } break;  \
@@ -466,8 +613,12 @@ int nbp_intro_bwd(const float* img, const void* dout, const float* w, float* dw,
   float* slab_w = ws;
   float* slab_b = ws + (long)nb * Cf * Cimg * 9;
   const dim3 grid(nb, cdiv(Cf, 32), cdiv(Cimg * 9 + 1, 32));
-  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, bconv_wgrad<0, CI, T><<<grid, 256, 0, S(s)>>>(
-                                                  img, (const T*)dout, slab_w, slab_b, g)));
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, {
+    if (bconv_lds(Cf, (int)sizeof(T)))
+      bconv_wgrad_lds<0, CI, T><<<grid, 256, 0, S(s)>>>(img, (const T*)dout, slab_w, slab_b, g);
+    else
+      bconv_wgrad<0, CI, T><<<grid, 256, 0, S(s)>>>(img, (const T*)dout, slab_w, slab_b, g);
+  }));
   int rc = check_launch("intro_bwd_w");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, nb, (long)Cf * Cimg * 9, dw, s);
@@ -521,8 +672,12 @@ int nbp_ending_bwd(const float* dy, const void* feat, const float* w, void* dfea
   float* slab_w = ws;
   float* slab_b = ws + (long)nb * Cimg * Cf * 9;
   const dim3 grid(nb, cdiv(Cf, 32), cdiv(Cimg * 9, 32));
-  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, bconv_wgrad<1, CI, T><<<grid, 256, 0, S(s)>>>(
-                                                  dy, (const T*)feat, slab_w, slab_b, g)));
+  NBP_DISPATCH_T(dtype, NBP_DISPATCH_CI(Cimg, {
+    if (bconv_lds(Cf, (int)sizeof(T)))
+      bconv_wgrad_lds<1, CI, T><<<grid, 256, 0, S(s)>>>(dy, (const T*)feat, slab_w, slab_b, g);
+    else
+      bconv_wgrad<1, CI, T><<<grid, 256, 0, S(s)>>>(dy, (const T*)feat, slab_w, slab_b, g);
+  }));
   int rc = check_launch("ending_bwd_w");
   if (rc) return rc;
   rc = nbp_reduce_slab(slab_w, nb, (long)Cimg * Cf * 9, dw, s);

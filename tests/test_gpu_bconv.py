@@ -59,3 +59,18 @@ def test_boundary_conv_gradients_against_float64(dev, shape, dtype):
                                                                                      ref_db_e)):
         err = (a.double() - r).abs().max().item()
         assert err <= 1e-5 * r.abs().max().item() + 1e-6, (name, err)
+
+
+@pytest.mark.parametrize("dtype", [0, 1, 2], ids=["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("shape", SHAPES, ids=["x".join(map(str, s)) for s in SHAPES])
+def test_boundary_conv_lds_staging_bitwise(dev, shape, dtype, monkeypatch):
+    """The LDS-staged weight-gradient kernel runs each wave's pixel-pair sequence of the gather kernel: every slab, so
+    dW / db, is bitwise the gather kernel's (NBP_BCONV_GATHER=1, read per launch)."""
+    B, CI, H0, W0, Hp, Wp, Cf = shape
+    if dtype and Cf % 8:
+        pytest.skip("16-bit widths are multiples of 8")
+    _, staged = _run(dev, B, CI, H0, W0, Hp, Wp, Cf, dtype)
+    monkeypatch.setenv("NBP_BCONV_GATHER", "1")
+    _, gather = _run(dev, B, CI, H0, W0, Hp, Wp, Cf, dtype)
+    for name, a, r in zip(("dw_intro", "db_intro", "dw_ending", "db_ending"), staged, gather):
+        assert torch.equal(a.view(torch.int32), r.view(torch.int32)), name
