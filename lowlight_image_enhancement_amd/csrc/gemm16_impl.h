@@ -1406,33 +1406,71 @@ bool try_skinny(const void* A, long lda, int a_mode, const float* a_scale, int r
   return true;
 }
 
-// fp32 flat parameters -> bf16 copy (all), plus transposed bf16 copies of the listed [rows][cols] matrices
+// fp32 flat parameters -> 16-bit copy (all; eight elements per thread, 16-byte stores), plus transposed 16-bit copies
+// of the listed [rows][cols] matrices
 template <typename H>
-__global__ void cvt_bf16_kernel(const float* __restrict__ src, long n, H* __restrict__ dst) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    dst[i] = (H)src[i];
+__global__ __launch_bounds__(256) void cvt_bf16_kernel(const float* __restrict__ src, long n, H* __restrict__ dst) {
+  const long n8 = n / 8, stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const float4 a = ld4(src + 8 * i), b = ld4(src + 8 * i + 4);
+    vec_t<H, 8> v;
+    v[0] = (H)a.x; v[1] = (H)a.y; v[2] = (H)a.z; v[3] = (H)a.w;
+    v[4] = (H)b.x; v[5] = (H)b.y; v[6] = (H)b.z; v[7] = (H)b.w;
+    *reinterpret_cast<vec_t<H, 8>*>(dst + 8 * i) = v;
+  }
+  for (long i = 8 * n8 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = (H)src[i];
 }
 
 // desc: [ndesc][4] int64 {offset, rows, cols, row-scale offset or -1}; block (x: tile index, y: matrix).  With a
-// row scale s (the layer scale beta / gamma of conv3 / conv5) the copy is (diag(s) W)^T.
+// row scale s (the layer scale beta / gamma of conv3 / conv5) the copy is (diag(s) W)^T.  64 x 64 tiles: float4 row
+// reads (cols a multiple of 4), transposed rows leave as 4-element (8-byte) stores (rows a multiple of 4).
 template <typename H>
-__global__ void transpose_bf16_kernel(const float* __restrict__ src, const long* __restrict__ desc,
-                                      H* __restrict__ dst_t) {
-  __shared__ float tile[32][33];
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const float* __restrict__ src, const long* __restrict__ desc,
+                                                             H* __restrict__ dst_t) {
+  __shared__ float tile[64][65];
   const long off = desc[blockIdx.y * 4], R = desc[blockIdx.y * 4 + 1], Cc = desc[blockIdx.y * 4 + 2];
   const long soff = desc[blockIdx.y * 4 + 3];
-  const long tiles_c = (Cc + 31) / 32, ntiles = ((R + 31) / 32) * tiles_c;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const long tiles_c = (Cc + 63) / 64, ntiles = ((R + 63) / 64) * tiles_c;
+  const int tid = threadIdx.x;
+  const bool vec = (Cc & 3) == 0 && (R & 3) == 0 && (off & 3) == 0;
   for (long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const long r0 = (t / tiles_c) * 32, c0 = (t % tiles_c) * 32;
-    for (int rr = ty; rr < 32; rr += 8) {
-      const long r = r0 + rr, c = c0 + tx;
-      tile[rr][tx] = (r < R && c < Cc) ? src[off + r * Cc + c] * (soff >= 0 ? src[soff + r] : 1.f) : 0.f;
+    const long r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rr = (tid >> 4) + 16 * k, cc = (tid & 15) * 4;
+      const long r = r0 + rr, c = c0 + cc;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (r < R) {
+        const float sc = soff >= 0 ? src[soff + r] : 1.f;
+        if (vec && c + 3 < Cc) {
+          const float4 q = ld4(src + off + r * Cc + c);
+          v[0] = q.x * sc; v[1] = q.y * sc; v[2] = q.z * sc; v[3] = q.w * sc;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c + j < Cc) v[j] = src[off + r * Cc + c + j] * sc;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tile[rr][cc + j] = v[j];
     }
     __syncthreads();
-    for (int cc = ty; cc < 32; cc += 8) {
-      const long c = c0 + cc, r = r0 + tx;
-      if (r < R && c < Cc) dst_t[off + c * R + r] = (H)tile[tx][cc];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int q = tid + 256 * k, ci = q >> 4, rq = (q & 15) * 4;
+      const long c = c0 + ci, r = r0 + rq;
+      if (c >= Cc || r >= R) continue;
+      H* d = dst_t + off + c * R + r;
+      if (vec) {
+        vec_t<H, 4> o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (H)tile[rq + j][ci];
+        *reinterpret_cast<vec_t<H, 4>*>(d) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (r + j < R) d[j] = (H)tile[rq + j][ci];
+      }
     }
     __syncthreads();
   }

@@ -202,11 +202,12 @@ int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int
                      nbp_stream_t s) {
   NBP_REQUIRE(flat && out && n > 0 && (ndesc == 0 || (desc && out_t)) && ndesc <= 65535, "nbp_weights_bf16: bad args");
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_weights_bf16: dtype 1 (bf16) or 2 (fp16)");
-  long g = (n + 255) / 256;
+  long g = (n / 8 + 255) / 256;
   NBP_DISPATCH_H(dtype, {
-    cvt_bf16_kernel<H><<<(int)(g > 4096 ? 4096 : g), 256, 0, S(s)>>>(flat, n, reinterpret_cast<H*>(out));
+    cvt_bf16_kernel<H><<<(int)(g > 4096 ? 4096 : (g < 1 ? 1 : g)), 256, 0, S(s)>>>(flat, n, reinterpret_cast<H*>(out));
+    // 64 tile-strided workgroups per matrix: the largest GEMM weight (1024 x 512) has 128 tiles
     if (ndesc > 0)
-      transpose_bf16_kernel<H><<<dim3(256, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<H*>(out_t));
+      transpose_bf16_kernel<H><<<dim3(64, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<H*>(out_t));
   });
   return check_launch("weights_bf16");
 }
