@@ -236,9 +236,12 @@ def _pmc_traffic(cls):
     scripts/pmc_pass.sh + scripts/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled)."""
     import glob
     import re
+    def newest(f):  # round number first, a round's "final" record after its numbered ones (r04_final > r04_v1)
+        rel = os.path.relpath(f, os.path.join(ROOT, "profiles"))
+        nums = [int(t) for t in re.findall(r"\d+", rel)]
+        return (nums[:1], "final" in rel, nums)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))
-                   + glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc_traffic.json")),
-                   key=lambda f: [int(t) for t in re.findall(r"\d+", os.path.relpath(f, os.path.join(ROOT, "profiles")))])
+                   + glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc_traffic.json")), key=newest)
     if not files:
         return None, None
     rec = json.load(open(files[-1])).get("classes", {}).get(cls)
