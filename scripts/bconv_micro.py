@@ -24,3 +24,7 @@ for gather in ("1", "0"):
     ti = timeit(lambda: call("intro_bwd", img, dout, w, dw_i, db_i, None, ws, B, CI, H, W, H, W, Cf, dt))
     te = timeit(lambda: call("ending_bwd", dy, feat, we, dfeat, dw_e, db_e, ws, B, CI, H, W, H, W, Cf, dt))
     print(f"{'gather' if gather == '1' else 'lds   '}: intro_bwd {ti:6.1f} us, ending_bwd {te:6.1f} us", flush=True)
+out, bias_i, bias_e = torch.empty_like(img), torch.randn(Cf, device=dev), torch.randn(CI, device=dev)
+tf = timeit(lambda: call("intro_fwd", img, w, bias_i, dfeat, B, CI, H, W, H, W, Cf, dt))
+te = timeit(lambda: call("ending_fwd", feat, we, bias_e, img, out, B, CI, H, W, H, W, Cf, dt))
+print(f"intro_fwd {tf:6.1f} us, ending_fwd {te:6.1f} us", flush=True)
