@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void ssim_fwd_tiled(const float* __restrict__ 
 // stay inside the margin: -j only occurs in the first tile (TH > 5) and reads rows [0, 5 - j]; 2(n-1) - j reads
 // rows [n-5, n) with j >= y0.  Interior groups of 4 rows (columns) run register-blocked; a group touching the
 // reflected border runs the per-output gather.
-constexpr int SB_TH = 32, SB_TW = 64, SB_M = 5;
+constexpr int SB_TH = 16, SB_TW = 64, SB_M = 5;
 constexpr int SB_P = SB_TW + 2 * SB_M + 2;
 
 __device__ __forceinline__ int refl_sources(int j, int n, int* qs) {
@@ -265,8 +265,9 @@ __global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ 
                                                        const float* __restrict__ up_map, float* __restrict__ gx,
                                                        long n) {
   constexpr int LH = SB_TH + 2 * SB_M, LW = SB_TW + 2 * SB_M;
-  // tv (the vertical adjoint) overwrites cs once every task holds its outputs in registers: 38 KB of LDS per tile,
-  // four tiles per CU
+  // tv (the vertical adjoint) overwrites cs once every task holds its outputs in registers: 24 KB of LDS per 16-row
+  // tile, six tiles per CU (16-row tiles: 52.5 -> 40.2 us at cfg2 against 32-row ones, whose 1.5 rounds of 4 tiles per
+  // CU left half the chip idle in the second)
   __shared__ __attribute__((aligned(16))) float sbuf[3 * LH * SB_P];
   auto cs = reinterpret_cast<float (*)[LH][SB_P]>(sbuf);
   auto tv = reinterpret_cast<float (*)[SB_TH][SB_P]>(sbuf);
