@@ -67,6 +67,13 @@ WORKLOADS = {
     "cfg4": dict(batch=16, img=256, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1), model=CFG4, psf="S2",
                  desc="cfg4: NAFNet w64 enc[2,2,4,8] mid12 dec[2,2,2,2] (115.98M), rgb/S2 stressed PSF (R>G>B), "
                       "bs16/GPU 256x256, L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + AdamW"),
+    # BASELINE.json configs[4], the RAW / linear-domain path: 4 x MI355X bs 32 at 1024^2 = 8 images per GPU, fp16
+    # compute; phys_cons_raw (metrics/phys_consistency.py:260-320) with expo_ratio in {100, 250, 300} and fp32
+    # accumulation evaluated on each step's output
+    "cfg5": dict(batch=8, img=1024, w=dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1), raw_ratios=(100.0, 250.0, 300.0),
+                 desc="cfg5: cfg2 model, rgb/B2 PSF, bs8/GPU 1024x1024, L1 + 0.05*SSIM + 0.1*Phys_srgb, clip 0.01 + "
+                      "AdamW; phys_cons_raw(out, short, psf, expo_ratio in {100,250,300}) on the fp16-cast output "
+                      "(fp32 accumulation)"),
 }
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak
 MFMA16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA peak
@@ -75,7 +82,7 @@ ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
 ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
                    "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel"], "wgrad_group": ["wgrad_bf16_wide_group"],
                    "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
-                   "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32, false>"],
+                   "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32>"],
                    "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"]}
 # classes that are ONE kernel (one template instance in the step): the headline `roofline` is the one of them with the
 # most time per step (the dominant kernel); the multi-kernel classes are reported beside it
@@ -212,7 +219,7 @@ def rec_flush(a):
 def rec_dw_bwd(a):
     fl, by = cost_dw_bwd(a)
     out = [("dw_bwd", fl, by, 1, 0.0)]
-    if a[12] >= 32:  # dw_bwd_tw(W): the 32-wide tile kernel dw_bwd_tiled<T, true, 32, false>
+    if a[12] >= 32:  # dw_bwd_tw(W): the 32-wide tile kernel dw_bwd_tiled<T, true, 32>
         out.append(("dw_bwd_32", fl, by, 1, 0.0))
     return out
 
@@ -363,6 +370,26 @@ def batch(dev, B, img, rank):
     return lq, gt, (lq * ratio).clamp(0, 1), ratio
 
 
+def raw_metric(tr, b, ratios):
+    """cfg5's linear-domain metric on the trainer's last output: phys_cons_raw(pred, short, psf, expo_ratio) with the
+    images' ratios cycling through `ratios`, fp16 inputs (the metric accumulates in fp32, phys_consistency.py:302-303),
+    mean and per-image values."""
+    from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_raw
+    out = tr._graph_out if getattr(tr, "_graph", None) is not None else None
+    if out is None:
+        out = tr.net(b[0])
+    B = out.shape[0]
+    r = torch.tensor([ratios[i % len(ratios)] for i in range(B)], device=out.device)
+    pred, obs = out.detach().clamp_min(0).half(), b[2].half()
+    k = tr.kernel  # [3, 1, 3, 3] depthwise crosstalk PSF -> the metric's [C_out, C_in, 3, 3] form (diagonal)
+    psf = torch.zeros(k.shape[0], k.shape[0], k.shape[2], k.shape[3], device=k.device)
+    for c in range(k.shape[0]):
+        psf[c, c] = k[c, 0]
+    per = phys_cons_raw(pred, obs, psf, r, reduction="none")
+    return {"mean": round(float(per.mean()), 6), "per_image": [round(float(v), 6) for v in per.flatten()],
+            "expo_ratio": [float(v) for v in r.tolist()], "inputs": "fp16 (output clamp_min 0, short)"}
+
+
 def short_run(dev, workload, precision, steps=5, warmup=3):
     """img/s of a graph-replayed run (extra keys; the headline is the main run)."""
     wl = WORKLOADS[workload]
@@ -378,6 +405,8 @@ def short_run(dev, workload, precision, steps=5, warmup=3):
     dt = (time.perf_counter() - t0) / steps
     out = {"value": round(wl["batch"] / dt, 2), "unit": "img/s", "ms_per_step": round(dt * 1e3, 3),
            "precision": precision, "steps": steps, "warmup": warmup, "losses": tr.logs()}
+    if "raw_ratios" in wl:
+        out["phys_cons_raw"] = raw_metric(tr, b, wl["raw_ratios"])
     del tr
     torch.cuda.empty_cache()
     return out
@@ -517,6 +546,7 @@ def main():
 
     net._block_fwd, net._block_bwd = timed(orig_fwd, "fwd"), timed(orig_bwd, "bwd")
     step_events = []
+    tr.comm_probe = world > 1  # the eager steps' exposed all-reduce time (not NAFBlock time, not the rest either)
     for _ in range(args.steps):
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
@@ -527,6 +557,8 @@ def main():
     torch.cuda.synchronize()
     _lib.PROFILE.clear()
     net._block_fwd, net._block_bwd = orig_fwd, orig_bwd
+    eager_comm = tr.comm_stats() if world > 1 else None
+    tr.comm_probe, tr.comm_events = False, []
 
     # graph replay at every world size (N > 1: segments cut at the gradient buckets, all-reduces between them); a
     # rank whose capture fails falls back to eager steps, which issue the same collective sequence
@@ -557,6 +589,18 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    comm = None
+    if world > 1:
+        # after the timed region: a few probed steps of the same kind (events on the compute stream around the bucket
+        # waits, after the last backward segment) -> the all-reduce time the backward left exposed
+        tr.comm_probe = True
+        for _ in range(min(args.steps, 5)):
+            run(lq, gt, short, ratio)
+        comm = tr.comm_stats()
+        tr.comm_probe, tr.comm_events = False, []
+        comm["allreduce_exposed_ms_eager"] = eager_comm["allreduce_exposed_ms"]
+        comm["note"] = ("exposed = compute-stream time from the end of the last backward kernel to the completion of "
+                        "every bucket all-reduce (graph replays; _eager: the profiled eager steps); rank 0's view")
     logs = tr.logs()
 
     classes = {}
@@ -604,8 +648,12 @@ def main():
     # there); the NAFBlock GPU time is the timed step minus the non-NAFBlock part of the eager step (boundary convs,
     # down/up, loss head, optimizer: few large kernels, not dispatch-bound).
     step_ms = elapsed / args.steps * 1e3
-    nonblock_ms = max(eager_step_ms - blk_ms, 0.0)
-    blk_ms_gpu = max(step_ms - nonblock_ms, 1e-6)
+    # N > 1: the exposed all-reduce time is neither NAFBlock nor the rest of the step: it leaves the eager
+    # non-block part and the timed step alike
+    exp_eager = (eager_comm or {}).get("allreduce_exposed_ms") or 0.0
+    exp_graph = (comm or {}).get("allreduce_exposed_ms") or 0.0
+    nonblock_ms = max(eager_step_ms - blk_ms - exp_eager, 0.0)
+    blk_ms_gpu = max(step_ms - exp_graph - nonblock_ms, 1e-6)
     blk_gbps = blk_bytes / (blk_ms_gpu * 1e-3) / 1e9
 
     if rank == 0:
@@ -629,13 +677,18 @@ def main():
             "roofline": roof,
             "nafblock_roofline": {"bytes_per_step": blk_bytes, "bytes_per_element": esize,
                                   "ms_per_step": round(blk_ms_gpu, 3),
-                                  "ms_method": "timed step - non-NAFBlock part of the eager step",
+                                  "ms_method": "timed step - non-NAFBlock part of the eager step" + (
+                                      " (both net of their exposed all-reduce time)" if world > 1 else ""),
                                   "eager_blocks_ms_per_step": round(blk_ms, 3),
                                   "per_level_eager": per_level,
                                   "achieved_GBps": round(blk_gbps, 1), "peak_GBps": HBM_PEAK_GBPS,
                                   "frac": round(blk_gbps / HBM_PEAK_GBPS, 4)},
             "losses": logs,
         }
+        if comm is not None:
+            res["comm"] = comm
+        if "raw_ratios" in wl:
+            res["phys_cons_raw"] = raw_metric(tr, (lq, gt, short, ratio), wl["raw_ratios"])
         if world == 1:
             res["psnr_vs_cpu_ref_db"], res["max_abs_vs_cpu_ref"] = psnr_vs_cpu(net, dev, IMG)
             res["psnr_active_blocks_db"], res["max_abs_active_blocks"] = psnr_vs_cpu(net, dev, IMG, active=True)
@@ -652,6 +705,11 @@ def main():
                                    workload=WORKLOADS["cfg4"]["desc"], global_batch=WORKLOADS["cfg4"]["batch"],
                                    note="the >= 6.5x scaling config at N = 1 (python bench.py --workload cfg4 "
                                         "--gpus N starts N local ranks and times it at N GPUs)")
+                print("[bench] cfg5 N=1 line", file=sys.stderr, flush=True)
+                res["cfg5"] = dict(short_run(dev, "cfg5", args.precision, steps=3, warmup=2),
+                                   workload=WORKLOADS["cfg5"]["desc"], global_batch=WORKLOADS["cfg5"]["batch"],
+                                   note="BASELINE configs[4] per GPU (4 x 8 = bs 32 globally); python bench.py "
+                                        "--workload cfg5 --gpus 4 times it at 4 GPUs")
                 if not args.no_cpu_baseline:
                     print("[bench] cpu baseline", file=sys.stderr, flush=True)
                     res["cpu_baseline"] = cpu_baseline(init_sd)

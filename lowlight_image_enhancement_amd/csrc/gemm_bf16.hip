@@ -202,6 +202,8 @@ int nbp_weights_bf16(const float* flat, long n, void* out, const long* desc, int
                      nbp_stream_t s) {
   NBP_REQUIRE(flat && out && n > 0 && (ndesc == 0 || (desc && out_t)) && ndesc <= 65535, "nbp_weights_bf16: bad args");
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_weights_bf16: dtype 1 (bf16) or 2 (fp16)");
+  NBP_REQUIRE((((uintptr_t)flat | (uintptr_t)out) & 15) == 0 && (ndesc == 0 || ((uintptr_t)out_t & 15) == 0),
+              "nbp_weights_bf16: flat / out / out_t must be 16-byte aligned (vector loads and stores)");
   long g = (n / 8 + 255) / 256;
   NBP_DISPATCH_H(dtype, {
     cvt_bf16_kernel<H><<<(int)(g > 4096 ? 4096 : (g < 1 ? 1 : g)), 256, 0, S(s)>>>(flat, n, reinterpret_cast<H*>(out));

@@ -300,7 +300,9 @@ __global__ __launch_bounds__(256) void ssim_bwd_tiled(const float* __restrict__ 
   // this thread's output pixels of x / y (two tasks of one row x four columns), loaded now so their latency overlaps
   // the two adjoint passes
   constexpr int PER = SB_TH * SB_TW / (4 * 256);
-  const bool vec = (W & 3) == 0;
+  // float4 paths only for 16-byte aligned rows: W a multiple of 4 AND 16-byte aligned bases (a public C-ABI entry may
+  // receive a view with an odd element offset)
+  const bool vec = (W & 3) == 0 && (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gx) & 15) == 0;
   float xo[PER][4], yo[PER][4];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {

@@ -114,6 +114,12 @@ class NBPTrainer:
         self._cap: Optional[dict] = None  # segment capture state of the data-parallel graph step
         self._pending_lo: Optional[int] = None
         self._pending_hi = 0
+        # communication accounting (the N > 1 bench line): buckets and bytes all-reduced by the last step, and, while
+        # comm_probe is set, a pair of events per step on the compute stream -- after the last backward kernel (the
+        # last graph segment) and after the waits for every bucket's all-reduce: the all-reduce time left exposed
+        self.comm_buckets: List[tuple] = []
+        self.comm_probe = False
+        self.comm_events: List[tuple] = []
         if self.world > 1:
             dist.broadcast(net.flat.data, src=0, group=process_group)
 
@@ -133,8 +139,37 @@ class NBPTrainer:
         if self._cap is not None:  # capturing graph segments: cut here; the replay all-reduces between segments
             self._cut_segment((lo, hi))
             return
+        self.comm_buckets.append((lo, hi))
         h = dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         self._handles.append(h)
+
+    def _wait_buckets(self):
+        """Wait (on the current stream) for every bucket all-reduce issued this step; with comm_probe set, events
+        bracket the wait: their distance is the all-reduce time the backward did not hide."""
+        e0 = None
+        if self.comm_probe:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        for h in self._handles:
+            h.wait()
+        self._handles.clear()
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.comm_events.append((e0, e1))
+
+    def comm_stats(self) -> Dict[str, float]:
+        """Buckets and gradient bytes all-reduced per step (the last step's), and the mean exposed all-reduce time of
+        the probed steps (ms; None when none was probed).  Reference contract: the DDP gradient all-reduce
+        (base_model.py:72-78, basicsr/train.py:54-63)."""
+        if self.comm_events:
+            torch.cuda.synchronize()
+        exp =[a.elapsed_time(b) for a, b in self.comm_events]
+        return {"buckets_per_step": len(self.comm_buckets),
+                "bytes_allreduced_per_step": int(sum(hi - lo for lo, hi in self.comm_buckets) * 4),
+                "bucket_mb": round(self.bucket_elems * 4 / 2 ** 20, 3),
+                "allreduce_exposed_ms": round(sum(exp) / len(exp), 4) if exp else None,
+                "probed_steps": len(exp)}
 
     def _cut_segment(self, bucket):
         """End the graph segment being captured (its last kernels complete `bucket`'s gradient slice) and begin the
@@ -190,13 +225,13 @@ class NBPTrainer:
                                           dt=self._trunk_dt(self.lpips))
             call("add", d_out, g, d_out, n, 0)
         hook = self._on_stage if self.world > 1 else None
+        if self.world > 1 and self._cap is None:
+            self.comm_buckets = []
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
         if self.world > 1:
             self._flush()
             if self._cap is None:
-                for h in self._handles:
-                    h.wait()
-                self._handles.clear()
+                self._wait_buckets()
         return out
 
     def _trunk_dt(self, module) -> Optional[int]:
@@ -305,15 +340,15 @@ class NBPTrainer:
         if self.world == 1:
             self._graph.replay()
             return self._graph_out
+        self.comm_buckets = []
         for g, bucket in self._segs:
             g.replay()
             if bucket is not None:
                 lo, hi = bucket
+                self.comm_buckets.append(bucket)
                 self._handles.append(dist.all_reduce(self.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.pg,
                                                      async_op=True))
-        for hd in self._handles:
-            hd.wait()
-        self._handles.clear()
+        self._wait_buckets()
         self._graph.replay()  # clip (with the 1/world average) + AdamW
         return self._graph_out
 

@@ -67,3 +67,20 @@ def test_spawned_ranks_report_their_failure():
     assert r.returncode != 0
     assert "exited with status" in r.stderr
     assert '"n_gpus"' not in r.stdout
+
+
+@pytest.mark.gpu
+def test_rehearsal_line_carries_the_comm_fields():
+    """The N > 1 bench line, rehearsed on the one-GPU box: two ranks on cuda:0 over gloo run the
+    graph segments and bucket all-reduces; rank 0's JSON line reports the buckets and bytes all-reduced per step, the
+    exposed all-reduce time of graph replays and of the eager steps, and the NAFBlock figure net of that time."""
+    import json
+    r = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--quick"], {"NBP_BENCH_REHEARSE": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["rehearsal"]
+    c = line["comm"]
+    assert c["buckets_per_step"] >= 1 and c["bytes_allreduced_per_step"] == 4 * 29159715
+    assert c["allreduce_exposed_ms"] is not None and c["allreduce_exposed_ms"] >= 0
+    assert c["allreduce_exposed_ms_eager"] is not None and c["probed_steps"] >= 1
+    assert "exposed all-reduce" in line["nafblock_roofline"]["ms_method"]

@@ -164,6 +164,45 @@ def test_cfg5_phys_cons_raw_1024(dev, dtype):
                                g["ssim4095_none"], atol=2e-6)
 
 
+def test_cfg5_training_step_1024_against_oracle(dev):
+    """configs[4]'s per-GPU step at one 1024 x 1024 image: the cfg2 model (active layer scales), one fused training step
+    (L1 + 0.05 SSIM + 0.1 Phys_srgb, clip, AdamW) in the fp32 parity mode against the oracle (output 1e-4 max-abs,
+    losses 1e-5 rel, per-tensor gradients 1e-3), then phys_cons_raw (phys_consistency.py:260-320) on the restored
+    image against the oracle's metric on the oracle's output, for each expo_ratio in {100, 250, 300}, fp32 and fp16
+    inputs (fp32 accumulation).  bench.py's `cfg5` line times the same step at 8 images per GPU in fp16."""
+    from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_raw
+    from lowlight_image_enhancement_amd.train import NBPTrainer
+    from oracle.physics import phys_cons
+    from oracle.train_step import OracleTrainer
+    torch.set_num_threads(16)
+    net, sd = _recipe_net(CFG2, 55, dev)
+    g = torch.Generator().manual_seed(5)
+    lq, gt = torch.rand(1, 3, 1024, 1024, generator=g), torch.rand(1, 3, 1024, 1024, generator=g)
+    r = torch.ones(1, 1, 1, 1)
+    w = dict(w_l1=1.0, w_ssim=0.05, w_phys=0.1)
+    tr = NBPTrainer(net, psf_mode="rgb", psf_spec="B2", **w)
+    out = tr.step(lq.to(dev), gt.to(dev), lq.clamp(0, 1).to(dev), r.to(dev)).detach()
+    logs = tr.logs()
+    ora = OracleTrainer(sd, BLK(CFG2), **w)
+    ref_out, ref_logs = ora.step(lq, gt, lq.clamp(0, 1), r)
+    ref_out = ref_out.detach()
+    assert (out.cpu() - ref_out).abs().max().item() <= 1e-4
+    for k in ("L1_raw", "SSIM", "Phys", "Total"):
+        ref = float(ref_logs[k])
+        assert abs(logs[k] - ref) <= 1e-5 * abs(ref), (k, logs[k], ref)
+    grads = _grads_ref_layout(net, tr.grad)
+    for k, p in ora.P.items():
+        scale = p.grad.abs().max().item()
+        assert (grads[k] - p.grad).abs().max().item() <= 1e-3 * scale + 1e-8, k
+    psf = T(golden("cfg5_raw.npz")["psf"])  # the reference's [C_out, C_in, 3, 3] PSF of the cfg5 fixture
+    for ratio in (100.0, 250.0, 300.0):
+        rr = torch.full((1,), ratio)
+        for dt in (torch.float32, torch.float16):
+            got = phys_cons_raw(out.clamp_min(0).to(dt), lq.to(dev, dt), psf.to(dev), rr.to(dev))
+            ref = phys_cons(ref_out.clamp_min(0).to(dt), lq.to(dt), psf, rr, clamp01=False)
+            assert abs(float(got) - float(ref)) <= 1e-5 * abs(float(ref)), (ratio, dt, float(got), float(ref))
+
+
 # ---------------------------------------------------------------------------------------------- configs[2]: cfg3
 def _synthetic_loss_weights():
     from lowlight_image_enhancement_amd.lpips import TAP_CH

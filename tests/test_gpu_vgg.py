@@ -260,12 +260,73 @@ def test_lpips_against_float64_torch(dev, precision):
     assert out.shape == (2, 1, 1, 1)
     ga, gb = x.grad.double().cpu().flatten(), xr.grad.flatten()
     if precision == "auto":
-        # fp32: values within 1e-5.  The input gradient is 3.5e-3 off float64 (1e-7 per tap in isolation,
-        # scripts/diag_lpips_tap.py): on this input one 2x2 max-pool window at relu1_2 holds a near-tie that the fp32
-        # forward resolves the other way (scripts/diag_vgg_masks.py: 1 argmax disagreement, 0 ReLU flips), and the
-        # relu5_3 tap's gradient reaches the input through it -- ill-conditioning of the max pool, bounded at 1e-2
+        # fp32: values within 1e-5.  The input gradient against the plain float64 autograd is 3.5e-3 off: a 2x2 max-pool
+        # window whose two largest inputs differ by less than the fp32 forward's accumulation noise routes the whole
+        # gradient to either input, and the fp32 forward resolved such a near-tie the other way (scripts/diag_vgg_masks.py)
+        # -- ill-conditioning of the max pool, not a kernel error.  So the float64 reference below takes the GPU's
+        # routing at exactly those windows (top-2 gap <= TIE_REL * |max|, i.e. ~84 fp32 ulp) and its own argmax
+        # everywhere else; every GPU / float64 argmax disagreement must be such a near-tie (counted), and the input
+        # gradient then holds at 1e-4.
         assert ((out.double().cpu() - r).abs() <= 1e-5 * r.abs()).all(), (out.view(-1), r.view(-1))
         assert ((ga - gb).norm() / gb.norm()).item() < 1e-2, ((ga - gb).norm() / gb.norm()).item()
+        from lowlight_image_enhancement_amd import vgg as _vgg
+        stack, _ = m.parts(dev)
+        _, tape, _ = stack.forward(_vgg.prep_input(a.to(dev), SHIFT, SCALE, clamp=False, dtype=stack.dtype), save=True)
+        gpu_pool_in = [rec[3].float().permute(0, 3, 1, 2).cpu().double() for rec in tape if rec[0] == "pool"]
+        stats = {"disagree": 0, "ties": 0, "windows": 0}
+
+        def windows(h):
+            B, C, H, W = h.shape
+            return h.reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(B, C, H // 2, W // 2, 4)
+
+        def routed_ref(x0):
+            shift = torch.tensor(SHIFT, dtype=torch.float64).view(1, 3, 1, 1)
+            scale = torch.tensor(SCALE, dtype=torch.float64).view(1, 3, 1, 1)
+            h, res, k = (x0 - shift) / scale, {}, 0
+            for kind, idx, _, _ in _layers(VGG16_CFG, 30):
+                if kind == "pool":
+                    win = windows(h)
+                    v = win.detach()
+                    top2 = v.topk(2, dim=-1).values
+                    tie = (top2[..., 0] - top2[..., 1]) <= TIE_REL * top2[..., 0].abs()
+                    gidx = windows(gpu_pool_in[k]).argmax(-1)  # the GPU kernel's first-max argmax on its fp32 input
+                    ridx = v.argmax(-1)
+                    dis = gidx != ridx
+                    assert not (dis & ~tie).any(), f"pool {k}: argmax disagreement outside a near-tie"
+                    stats["disagree"] += int(dis.sum())
+                    stats["ties"] += int((tie & (top2[..., 0] > 0)).sum())
+                    stats["windows"] += tie.numel()
+                    h = win.gather(-1, torch.where(tie, gidx, ridx).unsqueeze(-1)).squeeze(-1)
+                    k += 1
+                else:
+                    h = Fn.relu(Fn.conv2d(h, feats[f"{idx}.weight"].double(), feats[f"{idx}.bias"].double(), padding=1))
+                    if idx + 1 in TAPS:
+                        res[idx + 1] = h
+            return res
+
+        TIE_REL = 1e-5
+        xq = a.double().requires_grad_(True)
+        # the second input's taps need no routing (no gradient flows there)
+        shift = torch.tensor(SHIFT, dtype=torch.float64).view(1, 3, 1, 1)
+        scale = torch.tensor(SCALE, dtype=torch.float64).view(1, 3, 1, 1)
+        with torch.no_grad():
+            h1, t1 = (b.double() - shift) / scale, {}
+            for kind, idx, _, _ in _layers(VGG16_CFG, 30):
+                h1 = Fn.max_pool2d(h1, 2) if kind == "pool" else Fn.relu(
+                    Fn.conv2d(h1, feats[f"{idx}.weight"].double(), feats[f"{idx}.bias"].double(), padding=1))
+                if kind != "pool" and idx + 1 in TAPS:
+                    t1[idx + 1] = h1
+        t0, val = routed_ref(xq), 0
+        for k, tap in enumerate(TAPS):
+            u = t0[tap] / (t0[tap].pow(2).sum(1, keepdim=True).sqrt() + 1e-10)
+            v = t1[tap] / (t1[tap].pow(2).sum(1, keepdim=True).sqrt() + 1e-10)
+            val = val + ((u - v) ** 2 * lins[k].double().view(1, -1, 1, 1)).sum(1, keepdim=True).mean((2, 3), keepdim=True)
+        val.mean().backward()
+        gq = xq.grad.flatten()
+        rel = ((ga - gq).norm() / gq.norm()).item()
+        assert stats["disagree"] <= 8, stats  # a handful of near-ties on this input (measured: see the GPU log)
+        assert rel < 1e-4, (rel, stats)
+        print(f"lpips near-ties: {stats}, input-gradient rel-norm on the GPU's routing {rel:.2e}")
     else:
         assert ((out.double().cpu() - r).abs() <= 3e-2 * r.abs()).all(), (out.view(-1), r.view(-1))
         assert torch.dot(ga, gb).item() / (ga.norm() * gb.norm()).item() > 0.9

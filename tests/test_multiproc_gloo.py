@@ -47,6 +47,10 @@ def _worker(rank, world, port, bucket_mb, q):
             h.wait()
         n_buckets = len(tr._handles)
         tr._handles.clear()
+        # the bench's N > 1 communication fields: buckets and bytes of this step, no probe (no exposed time)
+        cs = tr.comm_stats()
+        assert cs["buckets_per_step"] == n_buckets and cs["allreduce_exposed_ms"] is None
+        assert cs["bytes_allreduced_per_step"] == 4 * (net.stages["intro"].hi - net.stages["ending"].lo)
         expect = torch.arange(net.numel, dtype=torch.float32) * sum(r + 1 for r in range(world))
         ok_sum = torch.equal(tr.grad, expect)
         tr.loss_buf.copy_(torch.tensor([1.0 + rank, 2.0, 3.0 * (rank + 1), 0.0, 0.0, 0.0]))
