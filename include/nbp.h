@@ -228,6 +228,24 @@ int nbp_dw_sg_pool_fwd(const void* t1, const float* wdw, const float* bdw, void*
 int nbp_c1dw_supported(int H, int W, int C, int dtype);
 int nbp_c1_dw_sg_pool(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
                       void* t2, void* g, float* pool, int B, int H, int W, int C, int dtype, nbp_stream_t s);
+/* Levels 0 / 1 (C 32 / 64, 16-bit) with the 2C-wide tape kept on chip (NAFNet_arch.py:59-68: conv1 -> conv2 (dw 3x3)
+ * -> SimpleGate -> the SCA's pool).  nbp_c1dw_fwd_tile: g = SG(dw3x3(conv1(n1))) and per-tile pool partials
+ * pool_slab[B][nbp_c1dw_tile_rows(H, W, C)][C] (the `chunks` of nbp_sca_fwd); t1 / t2 are written only when given
+ * (NULL: the backward rebuilds them).  w1: the 16-bit conv1 weight [2C][C].  t1, t2, g bitwise equal the skinny conv1
+ * + nbp_dw_sg_pool_fwd; pool equal up to fp32 summation order.
+ * nbp_c1dw_bwd_tile: replaces nbp_sca_sg_dw_bwd given n1 instead of t1 / t2 (rebuilt on chip, bitwise the forward's):
+ * dt1 = dw3x3^T(dt2), dt2 = (dg t2[C:], dg t2[:C]), dg = dh a + ds / HW; dwdw / dbdw as nbp_sca_sg_dw_bwd (per-tile
+ * slabs in ws, nbp_c1dw_bwd_workspace_floats, reduced with nbp_reduce_slab: deferred when deferral is on).  dt1 bitwise
+ * equal to nbp_sca_sg_dw_bwd on the stored tape; dwdw / dbdw up to fp32 summation order.
+ * nbp_c1dw_tile_supported(H, W, C, dtype) is 1 for the shapes served. */
+int nbp_c1dw_tile_supported(int H, int W, int C, int dtype);
+int nbp_c1dw_tile_rows(int H, int W, int C);
+int nbp_c1dw_fwd_tile(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
+                      void* t2, void* g, float* pool_slab, int B, int H, int W, int C, int dtype, nbp_stream_t s);
+size_t nbp_c1dw_bwd_workspace_floats(int B, int H, int W, int C);
+int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
+                      const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
+                      int W, int C, int dtype, nbp_stream_t s);
 /* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s);

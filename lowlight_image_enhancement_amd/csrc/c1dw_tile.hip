@@ -1,0 +1,620 @@
+// Levels 0 / 1 of the NAFBlock spatial branch with the 2C-wide tape kept on chip (VERDICT r4 item 1;
+// NAFNet_arch.py:59-68: conv1 (1x1, C -> 2C), conv2 (depthwise 3x3, zero pad 1), SimpleGate, the SCA's pool).
+//
+// Forward (c1dw_fwd_tile): a workgroup owns a TH x TW pixel tile of one image x one slice of 32 gate channels and their
+// 32 SimpleGate partners.  It walks the tile's rows with a 4-slot LDS ring of conv1 output rows (TW + 2 pixels, the
+// one-pixel halo, 64 fp32 channels each): per step the MFMA phase forms the next t1 row from the n1 row (32x32x16
+// MFMA, the conv1 weight slice as the A operand in registers, the pixels as the B operand loaded in fragment order,
+// the n1 rows of the next steps in flight), rounds it to the storage type and widens it into the ring (zeros outside
+// the image: the depthwise conv's padding); after one barrier the depthwise phase convolves the middle rows of the ring,
+// forms the gate and the pool partials.  t1 and t2 never reach HBM (the backward rebuilds them from n1); per pixel the
+// launch reads n1 (C) and writes g (C) instead of conv1's t1 (2C out) + the depthwise pass (2C in, 2C + C out).
+//
+// Backward (c1dw_bwd_tile): the mirror.  Per output row of dt1 the walk rebuilds t1 on a two-pixel halo (MFMA from n1),
+// t2 on a one-pixel halo (depthwise forward), forms dt2 = (dg t2[C:], dg t2[:C]) with dg = dh a + ds / HW (the SCA and
+// SimpleGate backward) into a 3-slot dt2 ring, accumulates the depthwise weight / bias gradients of the tile's own dt2
+// pixels, and convolves the dt2 ring into dt1 (stored: the conv1 input / weight gradients read it).  Per pixel: dh (C)
+// and n1 (C) in, dt1 (2C) out, instead of dh + t2 (2C) + t1 (2C) in and dt1 (2C) out.
+//
+// Bitwise contract (the GPU tests pin it against the two-launch path): t1 is the skinny conv1's MFMA sequence per
+// element (K ascending in steps of 16 on one accumulator, + bias, one rounding), t2 the tiled depthwise kernel's (bias,
+// then taps 0..8 by fused multiply-add), the gate the same opaque fp32 product rounded once, dt2 the products of the
+// rounded t2 with dg rounded once, dt1 taps 0..8 from zero.  The pool and the depthwise weight gradients are per-tile
+// partial sums in an order of their own (equal to the two-launch values up to fp32 summation order).
+#include <type_traits>
+
+#include "nbp_common.h"
+
+namespace nbp {
+namespace {
+
+constexpr int CT_TH = 16;  // tile rows
+
+struct C1TileP {
+  const void* n1;     // [B][H][W][C]: the block's norm1 output (conv1 input)
+  const void* w1;     // [2C][C] 16-bit forward copy of conv1.weight (rows 0..C-1 gate, C..2C-1 partners)
+  const float* b1;    // [2C]
+  const float* wdw;   // [2C][9] conv2.weight
+  const float* bdw;   // [2C]    conv2.bias
+  // forward
+  void* t1;           // [M][2C] optional out (null: not kept)
+  void* t2;           // [M][2C] optional out (null: not kept)
+  void* g;            // [M][C] out
+  float* pool;        // [B][tiles][C] out: per-tile pool partial sums of the fp32 gate products
+  // backward
+  const void* dh;     // [M][C] gradient of the SCA-scaled gate h = g * a
+  const float* a;     // [B][C] SCA scale
+  const float* ds;    // [B][C] gradient of the pooled mean (d pool sum = ds / HW)
+  void* dt1;          // [M][2C] out
+  float* slab_w;      // [B * tiles][2C][9] out: per-tile depthwise weight-gradient partials
+  float* slab_b;      // [B * tiles][2C]    out: per-tile depthwise bias-gradient partials
+  int B, H, W, tiles_x, tiles;
+  float inv_hw;
+};
+
+// Thread map of the depthwise phases (both kernels): lane l of wave w owns the channel quad Q16 = (l & 7) + 8 (l >> 5)
+// of the slice (quads 0..7: gate channels, 8..15: their SimpleGate partners, so a gate quad and its partner sit in
+// lanes l and l ^ 32 and meet by one shuffle) and PXT adjacent tile columns starting at PXT (4 w + ((l >> 3) & 3)).
+// t1 ring rows: LW pixels x 64 fp32 channels (16 quads, 256 B: every pixel starts on bank 0); quad q of pixel px is
+// stored at q ^ (((px / PXT) & 1) << 3), so the four column groups a 16-lane ds_read_b128 group spans hit 16
+// distinct 4-bank quarters.
+template <int PXT>
+__device__ __forceinline__ int qkey(int px) { return ((px / PXT) & 1) << 3; }
+
+// the slice's conv1 weight rows (A operand: n = t * 32 + r, t 0 gate rows slice * 32 + r, 1 partner rows C + ...) in
+// registers, and the bias of this lane's output channels t*32 + 8g + 4hh + q
+template <typename T, int C>
+struct Conv1Rows {
+  static constexpr int KS = C / 16;
+  vec_t<T, 8> w[2][KS];
+  float bias[2][4][4];
+
+  __device__ __forceinline__ void load_weights(const C1TileP& p, int slice, int r, int hh) {
+    const T* w1 = reinterpret_cast<const T*>(p.w1);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int n = (t == 0 ? 0 : C) + slice * 32 + r;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) w[t][ks] = *reinterpret_cast<const vec_t<T, 8>*>(w1 + (long)n * C + ks * 16 + 8 * hh);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 b = ld4(p.b1 + (t == 0 ? 0 : C) + slice * 32 + 8 * g + 4 * hh);
+        bias[t][g][0] = b.x; bias[t][g][1] = b.y; bias[t][g][2] = b.z; bias[t][g][3] = b.w;
+      }
+    }
+  }
+};
+
+// the B-operand fragments of one pixel chunk of one image row (zeros outside the image)
+template <typename T, int KS>
+__device__ __forceinline__ void load_n1(const T* __restrict__ n1, long img, int W, int H, int yy, int gx, bool lane_ok,
+                                        int hh, vec_t<T, 8>* f) {
+  const bool ok = lane_ok && yy >= 0 && yy < H && gx >= 0 && gx < W;
+  const T* src = n1 + ((img + (long)(ok ? yy : 0) * W + (ok ? gx : 0)) * (KS * 16)) + 8 * hh;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    vec_t<T, 8> v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (T)0.f;
+    if (ok) v = *reinterpret_cast<const vec_t<T, 8>*>(src + ks * 16);
+    f[ks] = v;
+  }
+}
+
+// the depthwise taps of quad q16 of the slice as packed pairs, and its bias
+struct DwQuad {
+  f2v w[9][2];
+  float4 b;
+  __device__ __forceinline__ void load(const float* wdw, const float* bdw, int ch) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) w[t][j] = f2v{wdw[(ch + 2 * j) * 9 + t], wdw[(ch + 2 * j + 1) * 9 + t]};
+    b = ld4(bdw + ch);
+  }
+};
+
+__device__ __forceinline__ float4 f4of(const f2v* v) { return make_float4(v[0].x, v[0].y, v[1].x, v[1].y); }
+__device__ __forceinline__ float4 shfl32(float4 v) {
+  return make_float4(__shfl_xor(v.x, 32, 64), __shfl_xor(v.y, 32, 64), __shfl_xor(v.z, 32, 64), __shfl_xor(v.w, 32, 64));
+}
+
+template <typename T, int C, int TW>
+__global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
+  constexpr int TH = CT_TH, LW = TW + 2, KS = C / 16, NSL = C / 32;
+  constexpr int NCHK = (LW + 31) / 32;  // 32-pixel MFMA chunks per ring row
+  constexpr int PXT = TW / 16;          // depthwise pixels per thread (adjacent columns)
+  constexpr int ROWF = LW * 64;         // floats per ring row
+  constexpr int PF = 2;                 // n1 rows in flight beyond the one being multiplied
+  static_assert(NCHK <= 4 && (PXT == 2 || PXT == 4), "tile width 32 or 64");
+  __shared__ __attribute__((aligned(16))) float ring[4 * ROWF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
+  // the slices of one tile, then neighbouring tiles, on one XCD (they share n1 lines: L2 hits)
+  const int u = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = u % NSL, tile = (u / NSL) % p.tiles, b = u / (NSL * p.tiles);
+  const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * TW;
+  const int H = p.H, W = p.W;
+  const long img = (long)b * H * W;
+  const T* n1 = reinterpret_cast<const T*>(p.n1);
+  const bool mfma_wave = wave < NCHK;
+  const int gxm = x0 - 1 + wave * 32 + r;  // this lane's MFMA pixel (ring pixel wave * 32 + r)
+  const bool lane_ok = wave * 32 + r < LW;
+  Conv1Rows<T, C> cw;
+  vec_t<T, 8> fq[PF + 1][KS];  // n1 fragments of the next image rows (register ring, static indices)
+  if (mfma_wave) {
+    cw.load_weights(p, slice, r, hh);
+#pragma unroll
+    for (int k = 0; k <= PF; ++k) load_n1<T, KS>(n1, img, W, H, y0 - 1 + k, gxm, lane_ok, hh, fq[k]);
+  }
+  const int q16 = (lane & 7) + 8 * hh, xl = PXT * (4 * wave + ((lane >> 3) & 3));
+  const bool gate = hh == 0;
+  const int ch = (gate ? 0 : C) + slice * 32 + 4 * (lane & 7);  // this lane's conv channels
+  DwQuad dw;
+  dw.load(p.wdw, p.bdw, ch);
+  T* t1o = reinterpret_cast<T*>(p.t1);
+  T* t2o = reinterpret_cast<T*>(p.t2);
+  T* go = reinterpret_cast<T*>(p.g);
+
+  // MFMA phase of ring row k (image row y0 - 1 + k): multiply fq[0], shift the register ring, issue the row PF + 1
+  // ahead.  The epilogue widens the rounded t1 into the ring (zero outside the image) and, when t1 is kept, stores the
+  // tile's own pixels.
+  auto mfma_row = [&](int k) {
+    const int yy = y0 - 1 + k;
+    const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
+    const bool st = t1o && valid && yy >= y0 && yy < y0 + TH && gxm >= x0 && gxm < x0 + TW;
+    floatx16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = mfma32x32x16(cw.w[t][ks], fq[0][ks], acc[t]);
+    const int px = wave * 32 + r;
+    if (px < LW) {
+      float* slot = ring + (k & 3) * ROWF;
+      const int key = qkey<PXT>(px);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          vec_t<T, 4> o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (T)(acc[t][4 * g + q] + cw.bias[t][g][q]);
+          const float4 v = valid ? make_float4((float)o[0], (float)o[1], (float)o[2], (float)o[3]) : f4(0.f);
+          *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = v;
+          if (st)
+            *reinterpret_cast<vec_t<T, 4>*>(t1o + (img + (long)yy * W + gxm) * 2 * C + (t == 0 ? 0 : C) + slice * 32 +
+                                            8 * g + 4 * hh) = o;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) fq[j][ks] = fq[j + 1][ks];
+    load_n1<T, KS>(n1, img, W, H, yy + PF + 1, gxm, lane_ok, hh, fq[PF]);
+  };
+
+  if (mfma_wave) {
+    mfma_row(0);
+    mfma_row(1);
+  }
+  float4 pacc = f4(0.f);
+#pragma unroll 1
+  for (int rr = 0; rr < TH; ++rr) {
+    if (mfma_wave) mfma_row(rr + 2);
+    lds_barrier();
+    const int y = y0 + rr;
+    if (y >= H) continue;  // uniform; every iteration still passes its barrier
+    // t2 of this lane's quad at its PXT columns: rows y - 1, y, y + 1 = ring rows rr, rr + 1, rr + 2
+    f2v a2[PXT][2];
+#pragma unroll
+    for (int j = 0; j < PXT; ++j) {
+      a2[j][0] = f2v{dw.b.x, dw.b.y};
+      a2[j][1] = f2v{dw.b.z, dw.b.w};
+    }
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float* row = ring + ((rr + dy) & 3) * ROWF;
+      f2v xw[PXT + 2][2];
+#pragma unroll
+      for (int c = 0; c < PXT + 2; ++c) {
+        const int px = xl + c;
+        const float4 v = *reinterpret_cast<const float4*>(row + (px * 16 + (q16 ^ qkey<PXT>(px))) * 4);
+        xw[c][0] = f2v{v.x, v.y};
+        xw[c][1] = f2v{v.z, v.w};
+      }
+#pragma unroll
+      for (int j = 0; j < PXT; ++j)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) a2[j][e] = __builtin_elementwise_fma(dw.w[dy * 3 + dx][e], xw[j + dx][e], a2[j][e]);
+    }
+#pragma unroll
+    for (int j = 0; j < PXT; ++j) {
+      const int gx = x0 + xl + j;
+      const float4 mine = f4of(a2[j]);
+      const float4 other = shfl32(mine);  // the partner quad's t2 (lane ^ 32)
+      if (gx >= W) continue;
+      const long m = img + (long)y * W + gx;
+      if (t2o) stq(t2o + m * 2 * C + ch, mine);
+      if (gate) {
+        float4 gv = mine * other;
+        // the fp32 product is what is rounded to the storage type (the SimpleGate convention of every kernel)
+        asm volatile("" : "+v"(gv.x), "+v"(gv.y), "+v"(gv.z), "+v"(gv.w));
+        stq(go + m * C + ch, gv);
+        pacc += gv;
+      }
+    }
+  }
+  // pool partial of the tile: the gate lanes of one quad (lane bits 3..4), then the 4 waves in order
+#pragma unroll
+  for (int o = 8; o < 32; o <<= 1) {
+    pacc.x += __shfl_xor(pacc.x, o, 64); pacc.y += __shfl_xor(pacc.y, o, 64);
+    pacc.z += __shfl_xor(pacc.z, o, 64); pacc.w += __shfl_xor(pacc.w, o, 64);
+  }
+  lds_barrier();  // the ring is dead
+  if (lane < 8) st4(ring + (wave * 8 + lane) * 4, pacc);
+  lds_barrier();
+  if (tid < 32) {
+    const int q = tid >> 2, e = tid & 3;
+    const float s = ((ring[(0 * 8 + q) * 4 + e] + ring[(1 * 8 + q) * 4 + e]) + ring[(2 * 8 + q) * 4 + e]) +
+                    ring[(3 * 8 + q) * 4 + e];
+    p.pool[((long)b * p.tiles + tile) * C + slice * 32 + tid] = s;
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// Geometry: a TH x TW (TW 32) tile of dt1 x one 32-gate-channel slice.  Per step i (0 .. TH + 1), dt2 row yd = y0 - 1 + i:
+//   MFMA : t1 row yd + 1 (ring row k = i + 2; ring row k = image row y0 - 2 + k) over pixels x0 - 2 .. x0 + TW + 1
+//   [barrier]
+//   dt2  : t2 = depthwise(t1 rows yd - 1 .. yd + 1) over pixels x0 - 1 .. x0 + TW, rounded; dg = dh a + ds / HW;
+//          dt2 = (dg t2[partner], dg t2[gate]) rounded into dt2 ring row i % 3; for the tile's own pixels (rows y0 ..
+//          y0 + TH - 1, columns x0 .. x0 + TW - 1) dW2 += dt2 * window, db2 += dt2
+//   [barrier]
+//   dt1  : (i >= 2) dt1 row yd - 1 = sum_t w[t] dt2(p - off_t) from dt2 rows yd - 2 .. yd
+// Both rings have 3 rows: with two barriers per step no row is overwritten while a wave may still read it.  The conv1
+// weight slice and bias live in LDS (read per chunk), the n1 rows of the next steps in registers of the two MFMA waves.
+// dt2 ring rows: TW + 2 pixels x 64 16-bit channels (gate half, partner half) on an 80-dword pitch, so the four pixels
+// 2 apart that a 32-lane ds_read_b64 group spans start on banks 0 / 16 / 32 / 48.
+template <typename T, int C>
+__global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
+  constexpr int TH = CT_TH, TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
+  constexpr int ROWF = LT * 64;          // floats per t1 ring row
+  constexpr int DP = 80;                 // T elements per dt2 ring pixel (64 + pad)
+  constexpr int ROWD = LD * DP;          // T elements per dt2 ring row
+  constexpr int PF = C == 32 ? 2 : 1;    // n1 / dh rows in flight beyond the current one (C 64: registers)
+  constexpr int RPB = 256 / (C * 2);     // weight rows per 256-byte LDS bank row (the swizzle key's divisor)
+  constexpr int NC = 2 * KS;             // 16-byte chunks per weight row
+  __shared__ __attribute__((aligned(16))) float t1r[3 * ROWF];
+  __shared__ __attribute__((aligned(16))) T dt2r[3 * ROWD];
+  __shared__ __attribute__((aligned(16))) T w1s[64 * C];
+  __shared__ __attribute__((aligned(16))) float b1s[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int u = xcd_remap(blockIdx.x, gridDim.x);
+  const int slice = u % NSL, tile = (u / NSL) % p.tiles, b = u / (NSL * p.tiles);
+  const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * TW;
+  const int H = p.H, W = p.W;
+  const long img = (long)b * H * W;
+  const T* n1 = reinterpret_cast<const T*>(p.n1);
+  const T* dh = reinterpret_cast<const T*>(p.dh);
+  // ---- the slice's conv1 weight rows (n = t * 32 + rr) and bias into LDS; chunk c of row n at c ^ key(n)
+  {
+    const T* w1 = reinterpret_cast<const T*>(p.w1);
+    for (int i = tid; i < 64 * NC; i += 256) {
+      const int n = i / NC, c = i % NC;
+      const int grow = (n < 32 ? 0 : C) + slice * 32 + (n & 31);
+      const uint4 v = *reinterpret_cast<const uint4*>(w1 + (long)grow * C + 8 * c);
+      *reinterpret_cast<uint4*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1)))) = v;
+    }
+    if (tid < 64) b1s[tid] = p.b1[(tid < 32 ? 0 : C) + slice * 32 + (tid & 31)];
+  }
+  // ---- MFMA lanes: waves 0 and 1, chunk = wave (t1 ring pixel wave * 32 + r = image column x0 - 2 + ...)
+  const bool mfma_wave = wave < 2;
+  const int gxm = x0 - 2 + wave * 32 + r;
+  const bool lane_ok = wave * 32 + r < LT;
+  vec_t<T, 8> fq[PF + 1][KS];
+  if (mfma_wave)
+#pragma unroll
+    for (int k = 0; k <= PF; ++k) load_n1<T, KS>(n1, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
+  // ---- depthwise lanes: quad q16 at tile columns xl, xl + 1 (dt2 ring pixels xl + 1, xl + 2); the 32 lanes of
+  // column group 0 of waves 0 / 1 also own the halo pixel of the dt2 rows (ring pixel 0 / TW + 1)
+  const int q16 = (lane & 7) + 8 * hh, xl = PXT * (4 * wave + ((lane >> 3) & 3));
+  const bool gate = hh == 0;
+  const int ch = (gate ? 0 : C) + slice * 32 + 4 * (lane & 7);  // conv channels of this lane
+  const int gch = slice * 32 + 4 * (lane & 7);                 // their gate channels (dg, dh)
+  const bool has_halo = wave < 2 && ((lane >> 3) & 3) == 0;
+  const int dph = wave == 0 ? 0 : TW + 1;
+  DwQuad dw;
+  dw.load(p.wdw, p.bdw, ch);
+  const float4 ak = ld4(p.a + (long)b * C + gch);
+  const float4 sk = ld4(p.ds + (long)b * C + gch) * f4(p.inv_hw);
+  auto load_dh = [&](int yy, int gx) {
+    vec_t<T, 4> v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (T)0.f;
+    if (yy >= 0 && yy < H && gx >= 0 && gx < W) v = *reinterpret_cast<const vec_t<T, 4>*>(dh + (img + (long)yy * W + gx) * C + gch);
+    return v;
+  };
+  vec_t<T, 4> dq[PF + 1][PXT], dqh[PF + 1];
+#pragma unroll
+  for (int k = 0; k <= PF; ++k) {
+#pragma unroll
+    for (int j = 0; j < PXT; ++j) dq[k][j] = load_dh(y0 - 1 + k, x0 + xl + j);
+    dqh[k] = load_dh(has_halo ? y0 - 1 + k : -1, x0 - 1 + dph);
+  }
+  f2v aw[9][2], db[2];  // this lane's depthwise weight / bias gradient partials
+#pragma unroll
+  for (int t = 0; t < 9; ++t) aw[t][0] = aw[t][1] = f2v{0.f, 0.f};
+  db[0] = db[1] = f2v{0.f, 0.f};
+  lds_barrier();  // weight slice and bias in LDS
+
+  // MFMA phase of t1 ring row k (image row y0 - 2 + k)
+  auto mfma_row = [&](int k) {
+    const int yy = y0 - 2 + k;
+    const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
+    floatx16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int n = t * 32 + r, c = 2 * ks + hh;
+        const vec_t<T, 8> wf = *reinterpret_cast<const vec_t<T, 8>*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1))));
+        acc[t] = mfma32x32x16(wf, fq[0][ks], acc[t]);
+      }
+    const int px = wave * 32 + r;
+    if (px < LT) {
+      float* slot = t1r + (k % 3) * ROWF;
+      const int key = qkey<PXT>(px);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
+          const float bq[4] = {bv.x, bv.y, bv.z, bv.w};
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = valid ? (float)(T)(acc[t][4 * g + q] + bq[q]) : 0.f;
+          *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) fq[j][ks] = fq[j + 1][ks];
+    load_n1<T, KS>(n1, img, W, H, yy + PF + 1, gxm, lane_ok, hh, fq[PF]);
+  };
+
+  // dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row yd, from t1
+  // ring rows k0 .. k0 + 2; `own`: accumulate the depthwise weight / bias gradients
+  auto dt2_px = [&](auto np_c, int dp0, int k0, int yd, const vec_t<T, 4>* dv, T* drow, bool own_row) {
+    constexpr int NP = decltype(np_c)::value;
+    f2v a2[NP][2];
+    f2v xw[3][NP + 2][2];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      a2[j][0] = f2v{dw.b.x, dw.b.y};
+      a2[j][1] = f2v{dw.b.z, dw.b.w};
+    }
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float* row = t1r + ((k0 + dy) % 3) * ROWF;
+#pragma unroll
+      for (int c = 0; c < NP + 2; ++c) {
+        const int px = dp0 + c;  // t1 ring pixel (image column x0 - 2 + px)
+        const float4 v = *reinterpret_cast<const float4*>(row + (px * 16 + (q16 ^ qkey<PXT>(px))) * 4);
+        xw[dy][c][0] = f2v{v.x, v.y};
+        xw[dy][c][1] = f2v{v.z, v.w};
+      }
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) a2[j][e] = __builtin_elementwise_fma(dw.w[dy * 3 + dx][e], xw[dy][j + dx][e], a2[j][e]);
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int dp = dp0 + j, gx = x0 - 1 + dp;
+      const bool inside = yd >= 0 && yd < H && gx >= 0 && gx < W;
+      const float4 tm = f4of(a2[j]);
+      const float4 mine = make_float4((float)(T)tm.x, (float)(T)tm.y, (float)(T)tm.z, (float)(T)tm.w);  // t2 rounded
+      const float4 other = shfl32(mine);  // the partner quad's rounded t2
+      const float oth[4] = {other.x, other.y, other.z, other.w};
+      const float av[4] = {ak.x, ak.y, ak.z, ak.w}, sv[4] = {sk.x, sk.y, sk.z, sk.w};
+      vec_t<T, 4> d2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dg = fmaf((float)dv[j][e], av[e], sv[e]);
+        float pr = dg * oth[e];
+        asm volatile("" : "+v"(pr));  // the fp32 product is what is rounded (the fused depthwise backward's convention)
+        d2[e] = inside ? (T)pr : (T)0.f;
+      }
+      *reinterpret_cast<vec_t<T, 4>*>(drow + dp * DP + 4 * q16) = d2;
+      if (own_row && gx >= x0 && gx < W) {
+        const f2v l0 = f2v{(float)d2[0], (float)d2[1]}, l1 = f2v{(float)d2[2], (float)d2[3]};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
+          aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
+        }
+        db[0] += l0;
+        db[1] += l1;
+      }
+    }
+  };
+
+  T* dt1o = reinterpret_cast<T*>(p.dt1);
+  if (mfma_wave) {
+    mfma_row(0);
+    mfma_row(1);
+  }
+#pragma unroll 1
+  for (int i = 0; i < TH + 2; ++i) {
+    const int yd = y0 - 1 + i;
+    if (mfma_wave) mfma_row(i + 2);
+    lds_barrier();
+    {
+      T* drow = dt2r + (i % 3) * ROWD;
+      const bool own_row = i >= 1 && i <= TH && yd < H;
+      dt2_px(std::integral_constant<int, PXT>{}, xl + 1, i, yd, dq[0], drow, own_row);
+      if (has_halo) dt2_px(std::integral_constant<int, 1>{}, dph, i, yd, &dqh[0], drow, false);
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+#pragma unroll
+        for (int j = 0; j < PXT; ++j) dq[k][j] = dq[k + 1][j];
+        dqh[k] = dqh[k + 1];
+      }
+#pragma unroll
+      for (int j = 0; j < PXT; ++j) dq[PF][j] = load_dh(yd + PF + 1, x0 + xl + j);
+      dqh[PF] = load_dh(has_halo ? yd + PF + 1 : -1, x0 - 1 + dph);
+    }
+    lds_barrier();
+    const int yo = yd - 1;
+    if (i >= 2 && yo < H) {
+      // dt1(p) = sum_t w[t] dt2(p - off_t): tap t = (dhh, dww) reads dt2 row yo - dhh (ring row i - 1 - dhh) at ring
+      // pixel xl + j + 1 - dww
+      f2v acc[PXT][2];
+#pragma unroll
+      for (int j = 0; j < PXT; ++j) acc[j][0] = acc[j][1] = f2v{0.f, 0.f};
+#pragma unroll
+      for (int dhh = -1; dhh <= 1; ++dhh) {
+        const T* drow = dt2r + ((i - 1 - dhh) % 3) * ROWD;
+        f2v gw[PXT + 2][2];
+#pragma unroll
+        for (int c = 0; c < PXT + 2; ++c) {
+          const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(drow + (xl + c) * DP + 4 * q16);
+          gw[c][0] = f2v{(float)v[0], (float)v[1]};
+          gw[c][1] = f2v{(float)v[2], (float)v[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < PXT; ++j)
+#pragma unroll
+          for (int dww = -1; dww <= 1; ++dww) {
+            const int t = (dhh + 1) * 3 + (dww + 1);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) acc[j][e] = __builtin_elementwise_fma(dw.w[t][e], gw[j + 1 - dww][e], acc[j][e]);
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < PXT; ++j) {
+        const int gx = x0 + xl + j;
+        if (gx < W) stq(dt1o + (img + (long)yo * W + gx) * 2 * C + ch, f4of(acc[j]));
+      }
+    }
+  }
+  // ---- the tile's depthwise weight / bias gradients: 40 values per lane, summed over the lanes of one quad (lane bits
+  // 3..4: a reduce-scatter, 40 -> 20 -> 10 values per lane), then over the 4 waves in order
+  float v[40];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    v[4 * t + 0] = aw[t][0].x; v[4 * t + 1] = aw[t][0].y; v[4 * t + 2] = aw[t][1].x; v[4 * t + 3] = aw[t][1].y;
+  }
+  v[36] = db[0].x; v[37] = db[0].y; v[38] = db[1].x; v[39] = db[1].y;
+  float v2[20], v3[10];
+  const bool b3 = lane & 8, b4 = lane & 16;
+#pragma unroll
+  for (int j = 0; j < 20; ++j) {
+    const float snd = b3 ? v[j] : v[j + 20], keep = b3 ? v[j + 20] : v[j];
+    v2[j] = keep + __shfl_xor(snd, 8, 64);
+  }
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const float snd = b4 ? v2[j] : v2[j + 10], keep = b4 ? v2[j + 10] : v2[j];
+    v3[j] = keep + __shfl_xor(snd, 16, 64);
+  }
+  lds_barrier();  // the t1 ring is dead: the cross-wave buffer [wave][q16][40]
+  float* red = t1r;
+  const int e0 = (b3 ? 20 : 0) + (b4 ? 10 : 0);
+#pragma unroll
+  for (int j = 0; j < 10; ++j) red[(wave * 16 + q16) * 40 + e0 + j] = v3[j];
+  lds_barrier();
+  const long row = (long)b * p.tiles + tile;
+  for (int i = tid; i < 16 * 40; i += 256) {
+    const int qq = i / 40, e = i % 40;
+    const float s = ((red[(0 * 16 + qq) * 40 + e] + red[(1 * 16 + qq) * 40 + e]) + red[(2 * 16 + qq) * 40 + e]) +
+                    red[(3 * 16 + qq) * 40 + e];
+    const int c4 = ((qq < 8) ? 0 : C) + slice * 32 + 4 * (qq & 7);
+    if (e < 36) p.slab_w[(row * 2 * C + c4 + (e & 3)) * 9 + (e >> 2)] = s;
+    else p.slab_b[row * 2 * C + c4 + (e - 36)] = s;
+  }
+}
+
+}  // namespace
+}  // namespace nbp
+
+using namespace nbp;
+
+namespace {
+int tile_w(int C) { return C == 32 ? 64 : 32; }
+}  // namespace
+
+extern "C" {
+
+int nbp_c1dw_tile_supported(int H, int W, int C, int dtype) {
+  if (dtype != 1 && dtype != 2) return 0;
+  if (C != 32 && C != 64) return 0;
+  return H > 0 && W > 0 && (long)W * 2 * C < (1L << 24) ? 1 : 0;
+}
+
+int nbp_c1dw_tile_rows(int H, int W, int C) {
+  if (C != 32 && C != 64) return 0;
+  return cdiv(H, CT_TH) * cdiv(W, tile_w(C));
+}
+
+int nbp_c1dw_fwd_tile(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
+                      void* t2, void* g, float* pool_slab, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(n1 && w1 && b1 && wdw && bdw && g && pool_slab && B > 0, "nbp_c1dw_fwd_tile: null pointer");
+  NBP_REQUIRE(nbp_c1dw_tile_supported(H, W, C, dtype), "nbp_c1dw_fwd_tile: unsupported shape (H %d W %d C %d dtype %d)",
+              H, W, C, dtype);
+  const int tw = tile_w(C);
+  C1TileP p{};
+  p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.t1 = t1; p.t2 = t2; p.g = g; p.pool = pool_slab;
+  p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, tw); p.tiles = nbp_c1dw_tile_rows(H, W, C);
+  const long nblk = (long)B * p.tiles * (C / 32);
+  NBP_REQUIRE(nblk < (1L << 31), "nbp_c1dw_fwd_tile: grid too large");
+  NBP_DISPATCH_H(dtype, {
+    if (C == 32) c1dw_fwd_tile<H, 32, 64><<<nblk, 256, 0, S(s)>>>(p);
+    else c1dw_fwd_tile<H, 64, 32><<<nblk, 256, 0, S(s)>>>(p);
+  });
+  return check_launch("c1dw_fwd_tile");
+}
+
+size_t nbp_c1dw_bwd_workspace_floats(int B, int H, int W, int C) {
+  return (size_t)B * cdiv(H, CT_TH) * cdiv(W, 32) * 2 * C * 10;
+}
+
+int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
+                      const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
+                      int W, int C, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dh && a && ds && n1 && w1 && b1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0,
+              "nbp_c1dw_bwd_tile: null pointer");
+  NBP_REQUIRE(nbp_c1dw_tile_supported(H, W, C, dtype), "nbp_c1dw_bwd_tile: unsupported shape (H %d W %d C %d dtype %d)",
+              H, W, C, dtype);
+  C1TileP p{};
+  p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.dh = dh; p.a = a; p.ds = ds; p.dt1 = dt1;
+  p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, 32); p.tiles = cdiv(H, CT_TH) * p.tiles_x;
+  p.inv_hw = 1.f / (float)((long)H * W);
+  const long nrow = (long)B * p.tiles;
+  p.slab_w = ws;
+  p.slab_b = ws + nrow * 2 * C * 9;
+  const long nblk = nrow * (C / 32);
+  NBP_REQUIRE(nblk < (1L << 31), "nbp_c1dw_bwd_tile: grid too large");
+  NBP_DISPATCH_H(dtype, {
+    if (C == 32) c1dw_bwd_tile<H, 32><<<nblk, 256, 0, S(s)>>>(p);
+    else c1dw_bwd_tile<H, 64><<<nblk, 256, 0, S(s)>>>(p);
+  });
+  int rc = check_launch("c1dw_bwd_tile");
+  if (rc) return rc;
+  rc = nbp_reduce_slab(p.slab_w, (int)nrow, 2L * C * 9, dwdw, s);
+  if (rc) return rc;
+  return nbp_reduce_slab(p.slab_b, (int)nrow, 2L * C, dbdw, s);
+}
+
+}  // extern "C"

@@ -113,6 +113,10 @@ class NAFNet(nn.Module):
         # the middle level (16 x 16 at C 512): conv1 -> depthwise -> SimpleGate -> pool as one whole-image launch
         # (nbp_c1_dw_sg_pool; t1 / t2 / g bitwise, the pool up to fp32 summation order)
         self.fuse_c1dw = True
+        # levels 0 / 1 (C 32 / 64, 16-bit): conv1 -> depthwise -> SimpleGate -> pool as one row-walking tile launch that
+        # keeps t1 / t2 on chip (nbp_c1dw_fwd_tile), and the mirror backward that rebuilds them from n1
+        # (nbp_c1dw_bwd_tile): the 2C-wide tape never reaches HBM
+        self.fuse_c1dw_tile = True
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
@@ -392,9 +396,16 @@ class NAFNet(nn.Module):
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
-        c1dw = self.fuse_c1dw and dt != 0 and len(self._W) == 3 and query("c1dw_supported", h, w, c, dt) == 1
-        chunks = 1 if c1dw else query("dw_fwd_slab_rows", B, h, w, c, dt)
-        t1, t2, g, pool = E(M, 2 * c), E(M, 2 * c), E(M, c), F(B * chunks * c)
+        tile = (self.fuse_c1dw_tile and dt != 0 and len(self._W) == 3
+                and query("c1dw_tile_supported", h, w, c, dt) == 1)
+        c1dw = (not tile and self.fuse_c1dw and dt != 0 and len(self._W) == 3
+                and query("c1dw_supported", h, w, c, dt) == 1)
+        chunks = (query("c1dw_tile_rows", h, w, c) if tile else
+                  (1 if c1dw else query("dw_fwd_slab_rows", B, h, w, c, dt)))
+        # the tile path keeps no t1 / t2 (the backward rebuilds them from n1); t2 is dropped anyway without a tape
+        t1 = None if tile else E(M, 2 * c)
+        t2 = None if tile else E(M, 2 * c)
+        g, pool = E(M, c), F(B * chunks * c)
         mean, a = F(B, c), F(B, c)
         y, n2, st2 = E(M, c), E(M, c), F(M, 2)
         # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
@@ -410,7 +421,11 @@ class NAFNet(nn.Module):
         if not have_n1:
             call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"),
                  n1, st1, M, c, LN_EPS, dt)
-        if c1dw:
+        if tile:
+            call("c1dw_fwd_tile", n1, self._slice(self._W[1], pre + "conv1.weight"), self._slice(P, pre + "conv1.bias"),
+                 self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), None, None, g, pool, B, h, w,
+                 c, dt)
+        elif c1dw:
             call("c1_dw_sg_pool", n1, self._slice(self._W[1], pre + "conv1.weight"), self._slice(P, pre + "conv1.bias"),
                  self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), t1, t2, g, pool, B, h, w,
                  c, dt)
@@ -708,12 +723,19 @@ class NAFNet(nn.Module):
              self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
         # SimpleGate + depthwise conv2 (fused when the channel slicing allows: dt2 stays in LDS)
         dt1 = E(M, 2 * c)
-        ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
-        dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
-                   self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        if c % (16 if dt != 0 else 8) == 0:
-            call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
+        if S["t1"] is None:  # levels 0 / 1 tile path: t1 / t2 rebuilt from n1 on chip (nbp_c1dw_bwd_tile)
+            ws = F(query("c1dw_bwd_workspace_floats", B, h, w, c))
+            call("c1dw_bwd_tile", dh, S["a"], ds, S["n1"], self._slice(Wt[1], pre + "conv1.weight"),
+                 self._slice(P, pre + "conv1.bias"), self._slice(P, pre + "conv2.weight"),
+                 self._slice(P, pre + "conv2.bias"), dt1, self._slice(dflat, pre + "conv2.weight"),
+                 self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
         else:
+            ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
+            dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
+                       self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
+        if S["t1"] is not None and c % (16 if dt != 0 else 8) == 0:
+            call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
+        elif S["t1"] is not None:
             dt2 = E(M, 2 * c)
             call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW, dt)
             call("dw_bwd", dt2, *dw_args)
