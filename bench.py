@@ -83,16 +83,20 @@ ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skin
                    "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel"], "wgrad_group": ["wgrad_bf16_wide_group"],
                    "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
                    "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32>"],
-                   "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"]}
+                   "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"],
+                   "c1dw_tile_fwd": ["c1dw_fwd_tile"], "c1dw_tile_bwd": ["c1dw_bwd_tile"],
+                   "c1dw_bwd_L0": ["c1dw_bwd_tile<T, 32>"]}
 # classes that are ONE kernel (one template instance in the step): the headline `roofline` is the one of them with the
 # most time per step (the dominant kernel); the multi-kernel classes are reported beside it
-SINGLE_KERNEL = ("dw_bwd_32", "wgrad_group", "reduce")
+SINGLE_KERNEL = ("dw_bwd_32", "wgrad_group", "reduce", "c1dw_bwd_L0")
 UNIT_DEF = {
     "dw_bwd_32": "SURVEY §8(d)-style per pixel: dh C + t2 2C + t1 2C read, dt1 2C written = 7*C*s bytes per pixel "
                  "(s = storage bytes), x B*H*W pixels of the launch (levels 0-3: the 32-wide tile kernel)",
     "wgrad_group": "per grouped launch: each queued problem's operands read once, M*(N+K)*s, + its fp32 dW (+db) "
                    "written once; the split-M fp32 slabs the launch writes instead are `slab_bytes_per_step`",
     "reduce": "per reduce_multi_kernel launch: the fp32 slabs read once + the reduced outputs written once",
+    "c1dw_bwd_L0": "per pixel: dh C + n1 C read, dt1 2C written = 4*C*s bytes (s = storage bytes; t1 / t2 rebuilt on "
+                   "chip, never read), x B*H*W pixels of the launch (level 0: C 32 at 256^2)",
 }
 
 
@@ -175,6 +179,25 @@ def cost_c1dw(a):  # (n1,w1,b1,wdw,bdw,t1,t2,g,pool,B,h,w,c,dt): n1 C in, t1 2C 
     return 2.0 * M * 2 * c * c + 2.0 * M * 2 * c * 9, by
 
 
+def cost_c1dw_fwd_tile(a):  # (n1,w1,b1,wdw,bdw,t1,t2,g,pool,B,h,w,c,dt): n1 C in, g C out (+ t1 / t2 2C when kept)
+    M, c = a[9] * a[10] * a[11], a[12]
+    by = (2 * M * c + (2 * M * c if a[5] is not None else 0) + (2 * M * c if a[6] is not None else 0) + 2 * c * c) * _e(a[13])
+    return 2.0 * M * 2 * c * c + 2.0 * M * 2 * c * 9, by
+
+
+def cost_c1dw_bwd_tile(a):  # (dh,a,ds,n1,w1,b1,wdw,bdw,dt1,dwdw,dbdw,ws,B,h,w,c,dt): dh C + n1 C in, dt1 2C out
+    M, c = a[12] * a[13] * a[14], a[15]
+    return 2.0 * M * 2 * c * c + 3 * 2.0 * M * 2 * c * 9, (4 * M * c + 2 * c * c) * _e(a[16])
+
+
+def rec_c1dw_bwd(a):
+    fl, by = cost_c1dw_bwd_tile(a)
+    out = [("c1dw_tile_bwd", fl, by, 1, 0.0)]
+    if a[15] == 32:  # the level-0 instance c1dw_bwd_tile<T, 32>
+        out.append(("c1dw_bwd_L0", fl, by, 1, 0.0))
+    return out
+
+
 def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
     M, N, K = a[11], a[12], a[13]
     return 2.0 * M * N * K, 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0))
@@ -235,7 +258,8 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "gemm_f32": rec_plain("gemm_f32", cost_gemm_f32), "wgrad_f32": rec_wgrad, "wgrad_group": rec_wgroup,
            "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_dw_bwd,
            "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd), "gemm_ffn": rec_plain("gemm16", cost_ffn),
-           "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw)}
+           "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
+           "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile), "c1dw_bwd_tile": rec_c1dw_bwd}
 
 
 def _pmc_traffic(cls):

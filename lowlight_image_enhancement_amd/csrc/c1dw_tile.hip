@@ -58,8 +58,40 @@ struct C1TileP {
 // t1 ring rows: LW pixels x 64 fp32 channels (16 quads, 256 B: every pixel starts on bank 0); quad q of pixel px is
 // stored at q ^ (((px / PXT) & 1) << 3), so the four column groups a 16-lane ds_read_b128 group spans hit 16
 // distinct 4-bank quarters.
+//
+// Memory operations: every global load / store goes through a buffer descriptor of its tensor, with the byte offset
+// replaced by OOB (past every descriptor's range) where the pixel lies outside the image: the hardware then returns
+// zeros / drops the store.  No memory operation sits behind a data-dependent branch, so the compiler's vmcnt
+// accounting stays exact and the rows prefetched into the register rings (static slots: the row loops are unrolled by
+// the ring depth, no register copies of in-flight loads) stay in flight across the steps.
 template <int PXT>
 __device__ __forceinline__ int qkey(int px) { return ((px / PXT) & 1) << 3; }
+
+constexpr int OOB = 0x7fffff00;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ vec_t<T, 8> bload8(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(vec_t<T, 8>, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+template <typename T>
+__device__ __forceinline__ vec_t<T, 4> bload4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(vec_t<T, 4>, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <typename T>
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  vec_t<T, 4> o;
+  o[0] = (T)v.x; o[1] = (T)v.y; o[2] = (T)v.z; o[3] = (T)v.w;
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), r, off, 0, 0);
+}
+template <typename T>
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, int off, vec_t<T, 4> o) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), r, off, 0, 0);
+}
 
 // the slice's conv1 weight rows (A operand: n = t * 32 + r, t 0 gate rows slice * 32 + r, 1 partner rows C + ...) in
 // registers, and the bias of this lane's output channels t*32 + 8g + 4hh + q
@@ -85,23 +117,17 @@ struct Conv1Rows {
   }
 };
 
-// the B-operand fragments of one pixel chunk of one image row (zeros outside the image)
+// the B-operand fragments of one pixel chunk of one image row (zeros outside the image: OOB offsets)
 template <typename T, int KS>
-__device__ __forceinline__ void load_n1(const T* __restrict__ n1, long img, int W, int H, int yy, int gx, bool lane_ok,
+__device__ __forceinline__ void load_n1(__amdgpu_buffer_rsrc_t rn, long img, int W, int H, int yy, int gx, bool lane_ok,
                                         int hh, vec_t<T, 8>* f) {
   const bool ok = lane_ok && yy >= 0 && yy < H && gx >= 0 && gx < W;
-  const T* src = n1 + ((img + (long)(ok ? yy : 0) * W + (ok ? gx : 0)) * (KS * 16)) + 8 * hh;
+  const int off = ok ? (int)((img + (long)yy * W + gx) * (KS * 32)) + 16 * hh : OOB;
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    vec_t<T, 8> v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (T)0.f;
-    if (ok) v = *reinterpret_cast<const vec_t<T, 8>*>(src + ks * 16);
-    f[ks] = v;
-  }
+  for (int ks = 0; ks < KS; ++ks) f[ks] = bload8<T>(rn, off + 32 * ks);
 }
 
-// the depthwise taps of quad q16 of the slice as packed pairs, and its bias
+// the depthwise taps of one channel quad as packed pairs, and its bias
 struct DwQuad {
   f2v w[9][2];
   float4 b;
@@ -119,14 +145,17 @@ __device__ __forceinline__ float4 shfl32(float4 v) {
   return make_float4(__shfl_xor(v.x, 32, 64), __shfl_xor(v.y, 32, 64), __shfl_xor(v.z, 32, 64), __shfl_xor(v.w, 32, 64));
 }
 
-template <typename T, int C, int TW>
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+template <typename T, int C, int TW, bool KEEP>
 __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
   constexpr int TH = CT_TH, LW = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int NCHK = (LW + 31) / 32;  // 32-pixel MFMA chunks per ring row
   constexpr int PXT = TW / 16;          // depthwise pixels per thread (adjacent columns)
   constexpr int ROWF = LW * 64;         // floats per ring row
-  constexpr int PF = 2;                 // n1 rows in flight beyond the one being multiplied
-  static_assert(NCHK <= 4 && (PXT == 2 || PXT == 4), "tile width 32 or 64");
+  constexpr int NR = 4;                 // n1 register-ring slots = the row loop's unroll (3 rows in flight)
+  static_assert(NCHK <= 4 && (PXT == 2 || PXT == 4) && TH % NR == 0, "tile geometry");
   __shared__ __attribute__((aligned(16))) float ring[4 * ROWF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
   // the slices of one tile, then neighbouring tiles, on one XCD (they share n1 lines: L2 hits)
@@ -134,34 +163,31 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
   const int slice = u % NSL, tile = (u / NSL) % p.tiles, b = u / (NSL * p.tiles);
   const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * TW;
   const int H = p.H, W = p.W;
-  const long img = (long)b * H * W;
-  const T* n1 = reinterpret_cast<const T*>(p.n1);
+  const long img = (long)b * H * W, M = (long)p.B * H * W;
+  const __amdgpu_buffer_rsrc_t rn = rsrc(p.n1, M * C * 2), rg = rsrc(p.g, M * C * 2);
+  const __amdgpu_buffer_rsrc_t r1 = rsrc(p.t1, KEEP ? M * C * 4 : 0), r2 = rsrc(p.t2, KEEP ? M * C * 4 : 0);
   const bool mfma_wave = wave < NCHK;
   const int gxm = x0 - 1 + wave * 32 + r;  // this lane's MFMA pixel (ring pixel wave * 32 + r)
   const bool lane_ok = wave * 32 + r < LW;
   Conv1Rows<T, C> cw;
-  vec_t<T, 8> fq[PF + 1][KS];  // n1 fragments of the next image rows (register ring, static indices)
+  vec_t<T, 8> fq[NR][KS];  // n1 fragments of image row y0 - 1 + k in slot k % NR
   if (mfma_wave) {
     cw.load_weights(p, slice, r, hh);
 #pragma unroll
-    for (int k = 0; k <= PF; ++k) load_n1<T, KS>(n1, img, W, H, y0 - 1 + k, gxm, lane_ok, hh, fq[k]);
+    for (int k = 0; k < NR; ++k) load_n1<T, KS>(rn, img, W, H, y0 - 1 + k, gxm, lane_ok, hh, fq[k]);
   }
   const int q16 = (lane & 7) + 8 * hh, xl = PXT * (4 * wave + ((lane >> 3) & 3));
   const bool gate = hh == 0;
   const int ch = (gate ? 0 : C) + slice * 32 + 4 * (lane & 7);  // this lane's conv channels
   DwQuad dw;
   dw.load(p.wdw, p.bdw, ch);
-  T* t1o = reinterpret_cast<T*>(p.t1);
-  T* t2o = reinterpret_cast<T*>(p.t2);
-  T* go = reinterpret_cast<T*>(p.g);
 
-  // MFMA phase of ring row k (image row y0 - 1 + k): multiply fq[0], shift the register ring, issue the row PF + 1
-  // ahead.  The epilogue widens the rounded t1 into the ring (zero outside the image) and, when t1 is kept, stores the
-  // tile's own pixels.
-  auto mfma_row = [&](int k) {
+  // MFMA phase of ring row k (image row y0 - 1 + k) from register slot S = k % NR, which then takes image row k + NR - 1.
+  // The epilogue widens the rounded t1 into the ring (zero outside the image); KEEP also stores the tile's own pixels.
+  auto mfma_row = [&](auto slot_c, int k) {
+    constexpr int S = decltype(slot_c)::value;
     const int yy = y0 - 1 + k;
     const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
-    const bool st = t1o && valid && yy >= y0 && yy < y0 + TH && gxm >= x0 && gxm < x0 + TW;
     floatx16 acc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -170,8 +196,11 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = mfma32x32x16(cw.w[t][ks], fq[0][ks], acc[t]);
+      for (int t = 0; t < 2; ++t) acc[t] = mfma32x32x16(cw.w[t][ks], fq[S][ks], acc[t]);
+    load_n1<T, KS>(rn, img, W, H, yy + NR, gxm, lane_ok, hh, fq[S]);
     const int px = wave * 32 + r;
+    const bool own = valid && yy >= y0 && yy < y0 + TH && gxm >= x0 && gxm < x0 + TW;
+    const int o1 = own ? (int)((img + (long)yy * W + gxm) * (4 * C)) : OOB;
     if (px < LW) {
       float* slot = ring + (k & 3) * ROWF;
       const int key = qkey<PXT>(px);
@@ -184,30 +213,27 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
           for (int q = 0; q < 4; ++q) o[q] = (T)(acc[t][4 * g + q] + cw.bias[t][g][q]);
           const float4 v = valid ? make_float4((float)o[0], (float)o[1], (float)o[2], (float)o[3]) : f4(0.f);
           *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = v;
-          if (st)
-            *reinterpret_cast<vec_t<T, 4>*>(t1o + (img + (long)yy * W + gxm) * 2 * C + (t == 0 ? 0 : C) + slice * 32 +
-                                            8 * g + 4 * hh) = o;
         }
     }
+    if constexpr (KEEP) {
 #pragma unroll
-    for (int j = 0; j < PF; ++j)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) fq[j][ks] = fq[j + 1][ks];
-    load_n1<T, KS>(n1, img, W, H, yy + PF + 1, gxm, lane_ok, hh, fq[PF]);
+        for (int g = 0; g < 4; ++g) {
+          vec_t<T, 4> o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = (T)(acc[t][4 * g + q] + cw.bias[t][g][q]);
+          bstore4<T>(r1, o1 + 2 * ((t == 0 ? 0 : C) + slice * 32 + 8 * g + 4 * hh), o);
+        }
+    }
   };
 
-  if (mfma_wave) {
-    mfma_row(0);
-    mfma_row(1);
-  }
   float4 pacc = f4(0.f);
-#pragma unroll 1
-  for (int rr = 0; rr < TH; ++rr) {
-    if (mfma_wave) mfma_row(rr + 2);
+  // one output row: MFMA of ring row rr + 2 (slot S), barrier, depthwise of image row y0 + rr from ring rows rr .. rr + 2
+  auto step = [&](auto slot_c, int rr) {
+    if (mfma_wave) mfma_row(slot_c, rr + 2);
     lds_barrier();
     const int y = y0 + rr;
-    if (y >= H) continue;  // uniform; every iteration still passes its barrier
-    // t2 of this lane's quad at its PXT columns: rows y - 1, y, y + 1 = ring rows rr, rr + 1, rr + 2
     f2v a2[PXT][2];
 #pragma unroll
     for (int j = 0; j < PXT; ++j) {
@@ -235,19 +261,29 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 #pragma unroll
     for (int j = 0; j < PXT; ++j) {
       const int gx = x0 + xl + j;
+      const bool ok = y < H && gx < W;
       const float4 mine = f4of(a2[j]);
       const float4 other = shfl32(mine);  // the partner quad's t2 (lane ^ 32)
-      if (gx >= W) continue;
       const long m = img + (long)y * W + gx;
-      if (t2o) stq(t2o + m * 2 * C + ch, mine);
-      if (gate) {
-        float4 gv = mine * other;
-        // the fp32 product is what is rounded to the storage type (the SimpleGate convention of every kernel)
-        asm volatile("" : "+v"(gv.x), "+v"(gv.y), "+v"(gv.z), "+v"(gv.w));
-        stq(go + m * C + ch, gv);
-        pacc += gv;
-      }
+      if constexpr (KEEP) bstore4<T>(r2, ok ? (int)(m * 4 * C) + 2 * ch : OOB, mine);
+      float4 gv = mine * other;
+      // the fp32 product is what is rounded to the storage type (the SimpleGate convention of every kernel)
+      asm volatile("" : "+v"(gv.x), "+v"(gv.y), "+v"(gv.z), "+v"(gv.w));
+      bstore4<T>(rg, ok && gate ? (int)(m * 2 * C) + 2 * ch : OOB, gv);
+      if (ok) pacc += gv;
     }
+  };
+
+  if (mfma_wave) {
+    mfma_row(IC<0>{}, 0);
+    mfma_row(IC<1>{}, 1);
+  }
+#pragma unroll 1
+  for (int rr = 0; rr < TH; rr += NR) {  // ring row rr + 2 lives in register slot (rr + 2) % NR
+    step(IC<2>{}, rr);
+    step(IC<3>{}, rr + 1);
+    step(IC<0>{}, rr + 2);
+    step(IC<1>{}, rr + 3);
   }
   // pool partial of the tile: the gate lanes of one quad (lane bits 3..4), then the 4 waves in order
 #pragma unroll
@@ -276,18 +312,20 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 //   [barrier]
 //   dt1  : (i >= 2) dt1 row yd - 1 = sum_t w[t] dt2(p - off_t) from dt2 rows yd - 2 .. yd
 // Both rings have 3 rows: with two barriers per step no row is overwritten while a wave may still read it.  The conv1
-// weight slice and bias live in LDS (read per chunk), the n1 rows of the next steps in registers of the two MFMA waves.
-// dt2 ring rows: TW + 2 pixels x 64 16-bit channels (gate half, partner half) on an 80-dword pitch, so the four pixels
-// 2 apart that a 32-lane ds_read_b64 group spans start on banks 0 / 16 / 32 / 48.
+// weight slice and bias live in LDS (read per chunk); the n1 rows (MFMA waves) and dh rows of the next steps in 3-slot
+// register rings (the step loop unrolled by 3).
+// dt2 ring rows: TW + 2 pixels x 64 16-bit channels (gate half, partner half) on an 80-element pitch, so the four
+// pixels 2 apart that a 32-lane ds_read_b64 group spans start on banks 0 / 16 / 32 / 48.
 template <typename T, int C>
 __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   constexpr int TH = CT_TH, TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int ROWF = LT * 64;          // floats per t1 ring row
   constexpr int DP = 80;                 // T elements per dt2 ring pixel (64 + pad)
   constexpr int ROWD = LD * DP;          // T elements per dt2 ring row
-  constexpr int PF = C == 32 ? 2 : 1;    // n1 / dh rows in flight beyond the current one (C 64: registers)
+  constexpr int NR = 3;                  // register-ring slots (n1, dh) = the step loop's unroll
   constexpr int RPB = 256 / (C * 2);     // weight rows per 256-byte LDS bank row (the swizzle key's divisor)
   constexpr int NC = 2 * KS;             // 16-byte chunks per weight row
+  static_assert((TH + 2) % NR == 0, "step loop unroll");
   __shared__ __attribute__((aligned(16))) float t1r[3 * ROWF];
   __shared__ __attribute__((aligned(16))) T dt2r[3 * ROWD];
   __shared__ __attribute__((aligned(16))) T w1s[64 * C];
@@ -297,9 +335,8 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   const int slice = u % NSL, tile = (u / NSL) % p.tiles, b = u / (NSL * p.tiles);
   const int y0 = (tile / p.tiles_x) * TH, x0 = (tile % p.tiles_x) * TW;
   const int H = p.H, W = p.W;
-  const long img = (long)b * H * W;
-  const T* n1 = reinterpret_cast<const T*>(p.n1);
-  const T* dh = reinterpret_cast<const T*>(p.dh);
+  const long img = (long)b * H * W, M = (long)p.B * H * W;
+  const __amdgpu_buffer_rsrc_t rn = rsrc(p.n1, M * C * 2), rh = rsrc(p.dh, M * C * 2), ro = rsrc(p.dt1, M * C * 4);
   // ---- the slice's conv1 weight rows (n = t * 32 + rr) and bias into LDS; chunk c of row n at c ^ key(n)
   {
     const T* w1 = reinterpret_cast<const T*>(p.w1);
@@ -315,10 +352,10 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   const bool mfma_wave = wave < 2;
   const int gxm = x0 - 2 + wave * 32 + r;
   const bool lane_ok = wave * 32 + r < LT;
-  vec_t<T, 8> fq[PF + 1][KS];
+  vec_t<T, 8> fq[NR][KS];  // n1 fragments of image row y0 - 2 + k in slot k % NR
   if (mfma_wave)
 #pragma unroll
-    for (int k = 0; k <= PF; ++k) load_n1<T, KS>(n1, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
+    for (int k = 0; k < NR; ++k) load_n1<T, KS>(rn, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
   // ---- depthwise lanes: quad q16 at tile columns xl, xl + 1 (dt2 ring pixels xl + 1, xl + 2); the 32 lanes of
   // column group 0 of waves 0 / 1 also own the halo pixel of the dt2 rows (ring pixel 0 / TW + 1)
   const int q16 = (lane & 7) + 8 * hh, xl = PXT * (4 * wave + ((lane >> 3) & 3));
@@ -331,19 +368,15 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   dw.load(p.wdw, p.bdw, ch);
   const float4 ak = ld4(p.a + (long)b * C + gch);
   const float4 sk = ld4(p.ds + (long)b * C + gch) * f4(p.inv_hw);
-  auto load_dh = [&](int yy, int gx) {
-    vec_t<T, 4> v;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = (T)0.f;
-    if (yy >= 0 && yy < H && gx >= 0 && gx < W) v = *reinterpret_cast<const vec_t<T, 4>*>(dh + (img + (long)yy * W + gx) * C + gch);
-    return v;
+  auto dh_off = [&](int yy, int gx, bool lane_has) {
+    return lane_has && yy >= 0 && yy < H && gx >= 0 && gx < W ? (int)((img + (long)yy * W + gx) * (2 * C)) + 2 * gch : OOB;
   };
-  vec_t<T, 4> dq[PF + 1][PXT], dqh[PF + 1];
+  vec_t<T, 4> dq[NR][PXT], dqh[NR];  // dh of dt2 row y0 - 1 + i in slot i % NR
 #pragma unroll
-  for (int k = 0; k <= PF; ++k) {
+  for (int k = 0; k < NR; ++k) {
 #pragma unroll
-    for (int j = 0; j < PXT; ++j) dq[k][j] = load_dh(y0 - 1 + k, x0 + xl + j);
-    dqh[k] = load_dh(has_halo ? y0 - 1 + k : -1, x0 - 1 + dph);
+    for (int j = 0; j < PXT; ++j) dq[k][j] = bload4<T>(rh, dh_off(y0 - 1 + k, x0 + xl + j, true));
+    dqh[k] = bload4<T>(rh, dh_off(y0 - 1 + k, x0 - 1 + dph, has_halo));
   }
   f2v aw[9][2], db[2];  // this lane's depthwise weight / bias gradient partials
 #pragma unroll
@@ -351,8 +384,9 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   db[0] = db[1] = f2v{0.f, 0.f};
   lds_barrier();  // weight slice and bias in LDS
 
-  // MFMA phase of t1 ring row k (image row y0 - 2 + k)
-  auto mfma_row = [&](int k) {
+  // MFMA phase of t1 ring row k (image row y0 - 2 + k) from register slot S = k % NR, which then takes row k + NR
+  auto mfma_row = [&](auto slot_c, int k) {
+    constexpr int S = decltype(slot_c)::value;
     const int yy = y0 - 2 + k;
     const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
     floatx16 acc[2];
@@ -366,8 +400,9 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       for (int t = 0; t < 2; ++t) {
         const int n = t * 32 + r, c = 2 * ks + hh;
         const vec_t<T, 8> wf = *reinterpret_cast<const vec_t<T, 8>*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1))));
-        acc[t] = mfma32x32x16(wf, fq[0][ks], acc[t]);
+        acc[t] = mfma32x32x16(wf, fq[S][ks], acc[t]);
       }
+    load_n1<T, KS>(rn, img, W, H, yy + NR, gxm, lane_ok, hh, fq[S]);
     const int px = wave * 32 + r;
     if (px < LT) {
       float* slot = t1r + (k % 3) * ROWF;
@@ -384,15 +419,10 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
           *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = make_float4(v[0], v[1], v[2], v[3]);
         }
     }
-#pragma unroll
-    for (int j = 0; j < PF; ++j)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) fq[j][ks] = fq[j + 1][ks];
-    load_n1<T, KS>(n1, img, W, H, yy + PF + 1, gxm, lane_ok, hh, fq[PF]);
   };
 
   // dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row yd, from t1
-  // ring rows k0 .. k0 + 2; `own`: accumulate the depthwise weight / bias gradients
+  // ring rows k0 .. k0 + 2; own_row: accumulate the depthwise weight / bias gradients of the tile's own pixels
   auto dt2_px = [&](auto np_c, int dp0, int k0, int yd, const vec_t<T, 4>* dv, T* drow, bool own_row) {
     constexpr int NP = decltype(np_c)::value;
     f2v a2[NP][2];
@@ -437,47 +467,33 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
         d2[e] = inside ? (T)pr : (T)0.f;
       }
       *reinterpret_cast<vec_t<T, 4>*>(drow + dp * DP + 4 * q16) = d2;
-      if (own_row && gx >= x0 && gx < W) {
-        const f2v l0 = f2v{(float)d2[0], (float)d2[1]}, l1 = f2v{(float)d2[2], (float)d2[3]};
+      const float own = own_row && gx >= x0 && gx < W ? 1.f : 0.f;  // multiply, not branch: no divergence in the FMAs
+      const f2v l0 = f2v{(float)d2[0], (float)d2[1]} * own, l1 = f2v{(float)d2[2], (float)d2[3]} * own;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
-          aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
-        }
-        db[0] += l0;
-        db[1] += l1;
+      for (int t = 0; t < 9; ++t) {
+        aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
+        aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
       }
+      db[0] += l0;
+      db[1] += l1;
     }
   };
 
-  T* dt1o = reinterpret_cast<T*>(p.dt1);
-  if (mfma_wave) {
-    mfma_row(0);
-    mfma_row(1);
-  }
-#pragma unroll 1
-  for (int i = 0; i < TH + 2; ++i) {
+  auto step = [&](auto slot_c, int i) {
+    constexpr int S = decltype(slot_c)::value;  // = i % NR: the register slots of dt2 row i and of t1 ring row i + 2
     const int yd = y0 - 1 + i;
-    if (mfma_wave) mfma_row(i + 2);
+    if (mfma_wave) mfma_row(IC<(S + 2) % NR>{}, i + 2);
     lds_barrier();
-    {
-      T* drow = dt2r + (i % 3) * ROWD;
-      const bool own_row = i >= 1 && i <= TH && yd < H;
-      dt2_px(std::integral_constant<int, PXT>{}, xl + 1, i, yd, dq[0], drow, own_row);
-      if (has_halo) dt2_px(std::integral_constant<int, 1>{}, dph, i, yd, &dqh[0], drow, false);
+    T* drow = dt2r + S * ROWD;  // ring row i % 3 (NR = 3)
+    const bool own_row = i >= 1 && i <= TH && yd < H;
+    dt2_px(IC<PXT>{}, xl + 1, i, yd, dq[S], drow, own_row);
+    if (has_halo) dt2_px(IC<1>{}, dph, i, yd, &dqh[S], drow, false);
 #pragma unroll
-      for (int k = 0; k < PF; ++k) {
-#pragma unroll
-        for (int j = 0; j < PXT; ++j) dq[k][j] = dq[k + 1][j];
-        dqh[k] = dqh[k + 1];
-      }
-#pragma unroll
-      for (int j = 0; j < PXT; ++j) dq[PF][j] = load_dh(yd + PF + 1, x0 + xl + j);
-      dqh[PF] = load_dh(has_halo ? yd + PF + 1 : -1, x0 - 1 + dph);
-    }
+    for (int j = 0; j < PXT; ++j) dq[S][j] = bload4<T>(rh, dh_off(yd + NR, x0 + xl + j, true));
+    dqh[S] = bload4<T>(rh, dh_off(yd + NR, x0 - 1 + dph, has_halo));
     lds_barrier();
-    const int yo = yd - 1;
-    if (i >= 2 && yo < H) {
+    if (i >= 2) {
+      const int yo = yd - 1;
       // dt1(p) = sum_t w[t] dt2(p - off_t): tap t = (dhh, dww) reads dt2 row yo - dhh (ring row i - 1 - dhh) at ring
       // pixel xl + j + 1 - dww
       f2v acc[PXT][2];
@@ -485,11 +501,11 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       for (int j = 0; j < PXT; ++j) acc[j][0] = acc[j][1] = f2v{0.f, 0.f};
 #pragma unroll
       for (int dhh = -1; dhh <= 1; ++dhh) {
-        const T* drow = dt2r + ((i - 1 - dhh) % 3) * ROWD;
+        const T* dr = dt2r + ((S + 2 - dhh) % 3) * ROWD;  // ring row (i - 1 - dhh) % 3
         f2v gw[PXT + 2][2];
 #pragma unroll
         for (int c = 0; c < PXT + 2; ++c) {
-          const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(drow + (xl + c) * DP + 4 * q16);
+          const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(dr + (xl + c) * DP + 4 * q16);
           gw[c][0] = f2v{(float)v[0], (float)v[1]};
           gw[c][1] = f2v{(float)v[2], (float)v[3]};
         }
@@ -505,9 +521,20 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
 #pragma unroll
       for (int j = 0; j < PXT; ++j) {
         const int gx = x0 + xl + j;
-        if (gx < W) stq(dt1o + (img + (long)yo * W + gx) * 2 * C + ch, f4of(acc[j]));
+        bstore4<T>(ro, yo < H && gx < W ? (int)((img + (long)yo * W + gx) * (4 * C)) + 2 * ch : OOB, f4of(acc[j]));
       }
     }
+  };
+
+  if (mfma_wave) {
+    mfma_row(IC<0>{}, 0);
+    mfma_row(IC<1>{}, 1);
+  }
+#pragma unroll 1
+  for (int i = 0; i < TH + 2; i += NR) {
+    step(IC<0>{}, i);
+    step(IC<1>{}, i + 1);
+    step(IC<2>{}, i + 2);
   }
   // ---- the tile's depthwise weight / bias gradients: 40 values per lane, summed over the lanes of one quad (lane bits
   // 3..4: a reduce-scatter, 40 -> 20 -> 10 values per lane), then over the 4 waves in order
@@ -560,7 +587,7 @@ extern "C" {
 int nbp_c1dw_tile_supported(int H, int W, int C, int dtype) {
   if (dtype != 1 && dtype != 2) return 0;
   if (C != 32 && C != 64) return 0;
-  return H > 0 && W > 0 && (long)W * 2 * C < (1L << 24) ? 1 : 0;
+  return H > 0 && W > 0 ? 1 : 0;
 }
 
 int nbp_c1dw_tile_rows(int H, int W, int C) {
@@ -573,15 +600,23 @@ int nbp_c1dw_fwd_tile(const void* n1, const void* w1, const float* b1, const flo
   NBP_REQUIRE(n1 && w1 && b1 && wdw && bdw && g && pool_slab && B > 0, "nbp_c1dw_fwd_tile: null pointer");
   NBP_REQUIRE(nbp_c1dw_tile_supported(H, W, C, dtype), "nbp_c1dw_fwd_tile: unsupported shape (H %d W %d C %d dtype %d)",
               H, W, C, dtype);
+  NBP_REQUIRE((long)B * H * W * C * 4 < (1L << 31), "nbp_c1dw_fwd_tile: B*H*W*2C*2 must be < 2^31 (buffer offsets)");
   const int tw = tile_w(C);
   C1TileP p{};
   p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.t1 = t1; p.t2 = t2; p.g = g; p.pool = pool_slab;
   p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, tw); p.tiles = nbp_c1dw_tile_rows(H, W, C);
   const long nblk = (long)B * p.tiles * (C / 32);
   NBP_REQUIRE(nblk < (1L << 31), "nbp_c1dw_fwd_tile: grid too large");
+  NBP_REQUIRE((t1 == nullptr) == (t2 == nullptr), "nbp_c1dw_fwd_tile: t1 and t2 are kept together or not at all");
+  const bool keep = t1 != nullptr;
   NBP_DISPATCH_H(dtype, {
-    if (C == 32) c1dw_fwd_tile<H, 32, 64><<<nblk, 256, 0, S(s)>>>(p);
-    else c1dw_fwd_tile<H, 64, 32><<<nblk, 256, 0, S(s)>>>(p);
+    if (C == 32) {
+      if (keep) c1dw_fwd_tile<H, 32, 64, true><<<nblk, 256, 0, S(s)>>>(p);
+      else c1dw_fwd_tile<H, 32, 64, false><<<nblk, 256, 0, S(s)>>>(p);
+    } else {
+      if (keep) c1dw_fwd_tile<H, 64, 32, true><<<nblk, 256, 0, S(s)>>>(p);
+      else c1dw_fwd_tile<H, 64, 32, false><<<nblk, 256, 0, S(s)>>>(p);
+    }
   });
   return check_launch("c1dw_fwd_tile");
 }
@@ -597,6 +632,7 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
               "nbp_c1dw_bwd_tile: null pointer");
   NBP_REQUIRE(nbp_c1dw_tile_supported(H, W, C, dtype), "nbp_c1dw_bwd_tile: unsupported shape (H %d W %d C %d dtype %d)",
               H, W, C, dtype);
+  NBP_REQUIRE((long)B * H * W * C * 4 < (1L << 31), "nbp_c1dw_bwd_tile: B*H*W*2C*2 must be < 2^31 (buffer offsets)");
   C1TileP p{};
   p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.dh = dh; p.a = a; p.ds = ds; p.dt1 = dt1;
   p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, 32); p.tiles = cdiv(H, CT_TH) * p.tiles_x;

@@ -24,6 +24,8 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            "reduce": ("reduce_multi_kernel", "layer_scale_grad_kernel"),
            "dw_bwd": ("dw_bwd_tiled",), "dw_bwd_32": (re.compile(r"dw_bwd_tiledI\w+?Li32E"),),
            "dw_fwd": ("dw_sg_pool_tiled",), "c1dw": ("c1_dw_sg_pool_img",), "ln_fwd": ("ln_fwd_nhwc",),
+           "c1dw_tile_fwd": ("c1dw_fwd_tile",), "c1dw_tile_bwd": ("c1dw_bwd_tile",),
+           "c1dw_bwd_L0": (re.compile(r"c1dw_bwd_tileI\w+?Li32E"),),
            "ln_bwd": ("ln_bwd_nhwc",),
            # VGG / AlexNet implicit-GEMM convs (cfg3's perceptual + LPIPS trunks): the tiled kernels with A mode 3 / 4
            "vgg_conv": (re.compile(r"gemm_(glds|bf16)_kernelILi\d+ELi\d+ELi\d+ELi[34]E"),),
