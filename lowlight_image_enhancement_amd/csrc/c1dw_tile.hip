@@ -141,8 +141,14 @@ struct DwQuad {
 };
 
 __device__ __forceinline__ float4 f4of(const f2v* v) { return make_float4(v[0].x, v[0].y, v[1].x, v[1].y); }
-__device__ __forceinline__ float4 shfl32(float4 v) {
-  return make_float4(__shfl_xor(v.x, 32, 64), __shfl_xor(v.y, 32, 64), __shfl_xor(v.z, 32, 64), __shfl_xor(v.w, 32, 64));
+// the value of lane l ^ 32 (the partner quad's) by one v_permlane32_swap per element: lanes 0..31 read the swapped
+// source copy (the upper half's values), lanes 32..63 the swapped destination copy (the lower half's)
+__device__ __forceinline__ float swap32(float v, bool upper) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(upper ? r[0] : r[1]);
+}
+__device__ __forceinline__ float4 swap32(float4 v, bool upper) {
+  return make_float4(swap32(v.x, upper), swap32(v.y, upper), swap32(v.z, upper), swap32(v.w, upper));
 }
 
 template <int V>
@@ -231,6 +237,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
   float4 pacc = f4(0.f);
   // one output row: MFMA of ring row rr + 2 (slot S), barrier, depthwise of image row y0 + rr from ring rows rr .. rr + 2
   auto step = [&](auto slot_c, int rr) {
+    __builtin_amdgcn_sched_barrier(0);  // no scheduling across steps
     if (mfma_wave) mfma_row(slot_c, rr + 2);
     lds_barrier();
     const int y = y0 + rr;
@@ -263,7 +270,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
       const int gx = x0 + xl + j;
       const bool ok = y < H && gx < W;
       const float4 mine = f4of(a2[j]);
-      const float4 other = shfl32(mine);  // the partner quad's t2 (lane ^ 32)
+      const float4 other = swap32(mine, false);  // the partner quad's t2 (lane ^ 32; consumed by the gate lanes only)
       const long m = img + (long)y * W + gx;
       if constexpr (KEEP) bstore4<T>(r2, ok ? (int)(m * 4 * C) + 2 * ch : OOB, mine);
       float4 gv = mine * other;
@@ -314,20 +321,19 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 // Both rings have 3 rows: with two barriers per step no row is overwritten while a wave may still read it.  The conv1
 // weight slice and bias live in LDS (read per chunk); the n1 rows (MFMA waves) and dh rows of the next steps in 3-slot
 // register rings (the step loop unrolled by 3).
-// dt2 ring rows: TW + 2 pixels x 64 16-bit channels (gate half, partner half) on an 80-element pitch, so the four
-// pixels 2 apart that a 32-lane ds_read_b64 group spans start on banks 0 / 16 / 32 / 48.
+// dt2 ring rows: TW + 2 pixels x 64 fp32 channels (the rounded dt2 widened once), quads keyed like the t1 ring's.
 template <typename T, int C>
 __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   constexpr int TH = CT_TH, TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int ROWF = LT * 64;          // floats per t1 ring row
-  constexpr int DP = 80;                 // T elements per dt2 ring pixel (64 + pad)
-  constexpr int ROWD = LD * DP;          // T elements per dt2 ring row
-  constexpr int NR = 3;                  // register-ring slots (n1, dh) = the step loop's unroll
+  constexpr int ROWD = LD * 64;          // floats per dt2 ring row
+  constexpr int NR = 3;                  // dh register-ring slots (= the rings' row count)
+  constexpr int NRF = 3;                 // n1 register-ring slots; the step loop unrolls by 3
   constexpr int RPB = 256 / (C * 2);     // weight rows per 256-byte LDS bank row (the swizzle key's divisor)
   constexpr int NC = 2 * KS;             // 16-byte chunks per weight row
-  static_assert((TH + 2) % NR == 0, "step loop unroll");
+  static_assert((TH + 2) % 3 == 0, "step loop unroll");
   __shared__ __attribute__((aligned(16))) float t1r[3 * ROWF];
-  __shared__ __attribute__((aligned(16))) T dt2r[3 * ROWD];
+  __shared__ __attribute__((aligned(16))) float dt2r[3 * ROWD];
   __shared__ __attribute__((aligned(16))) T w1s[64 * C];
   __shared__ __attribute__((aligned(16))) float b1s[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -352,18 +358,18 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   const bool mfma_wave = wave < 2;
   const int gxm = x0 - 2 + wave * 32 + r;
   const bool lane_ok = wave * 32 + r < LT;
-  vec_t<T, 8> fq[NR][KS];  // n1 fragments of image row y0 - 2 + k in slot k % NR
+  vec_t<T, 8> fq[NRF][KS];  // n1 fragments of image row y0 - 2 + k in slot k % NRF
   if (mfma_wave)
 #pragma unroll
-    for (int k = 0; k < NR; ++k) load_n1<T, KS>(rn, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
+    for (int k = 0; k < NRF; ++k) load_n1<T, KS>(rn, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
   // ---- depthwise lanes: quad q16 at tile columns xl, xl + 1 (dt2 ring pixels xl + 1, xl + 2); the 32 lanes of
-  // column group 0 of waves 0 / 1 also own the halo pixel of the dt2 rows (ring pixel 0 / TW + 1)
+  // column group 0 of waves 2 / 3 (no MFMA phase) also own the halo pixel of the dt2 rows (ring pixel 0 / TW + 1)
   const int q16 = (lane & 7) + 8 * hh, xl = PXT * (4 * wave + ((lane >> 3) & 3));
   const bool gate = hh == 0;
   const int ch = (gate ? 0 : C) + slice * 32 + 4 * (lane & 7);  // conv channels of this lane
   const int gch = slice * 32 + 4 * (lane & 7);                 // their gate channels (dg, dh)
-  const bool has_halo = wave < 2 && ((lane >> 3) & 3) == 0;
-  const int dph = wave == 0 ? 0 : TW + 1;
+  const bool has_halo = wave >= 2 && ((lane >> 3) & 3) == 0;
+  const int dph = wave == 2 ? 0 : TW + 1;
   DwQuad dw;
   dw.load(p.wdw, p.bdw, ch);
   const float4 ak = ld4(p.a + (long)b * C + gch);
@@ -384,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   db[0] = db[1] = f2v{0.f, 0.f};
   lds_barrier();  // weight slice and bias in LDS
 
-  // MFMA phase of t1 ring row k (image row y0 - 2 + k) from register slot S = k % NR, which then takes row k + NR
+  // MFMA phase of t1 ring row k (image row y0 - 2 + k) from register slot S = k % NRF, which then takes row k + NRF
   auto mfma_row = [&](auto slot_c, int k) {
     constexpr int S = decltype(slot_c)::value;
     const int yy = y0 - 2 + k;
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
         const vec_t<T, 8> wf = *reinterpret_cast<const vec_t<T, 8>*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1))));
         acc[t] = mfma32x32x16(wf, fq[S][ks], acc[t]);
       }
-    load_n1<T, KS>(rn, img, W, H, yy + NR, gxm, lane_ok, hh, fq[S]);
+    load_n1<T, KS>(rn, img, W, H, yy + NRF, gxm, lane_ok, hh, fq[S]);
     const int px = wave * 32 + r;
     if (px < LT) {
       float* slot = t1r + (k % 3) * ROWF;
@@ -423,8 +429,9 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
 
   // dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row yd, from t1
   // ring rows k0 .. k0 + 2; own_row: accumulate the depthwise weight / bias gradients of the tile's own pixels
-  auto dt2_px = [&](auto np_c, int dp0, int k0, int yd, const vec_t<T, 4>* dv, T* drow, bool own_row) {
+  auto dt2_px = [&](auto np_c, auto own_c, int dp0, int k0, int yd, const vec_t<T, 4>* dv, float* drow, bool own_row) {
     constexpr int NP = decltype(np_c)::value;
+    constexpr bool OWN = decltype(own_c)::value;  // false: halo pixels (no weight-gradient work)
     f2v a2[NP][2];
     f2v xw[3][NP + 2][2];
 #pragma unroll
@@ -455,7 +462,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       const bool inside = yd >= 0 && yd < H && gx >= 0 && gx < W;
       const float4 tm = f4of(a2[j]);
       const float4 mine = make_float4((float)(T)tm.x, (float)(T)tm.y, (float)(T)tm.z, (float)(T)tm.w);  // t2 rounded
-      const float4 other = shfl32(mine);  // the partner quad's rounded t2
+      const float4 other = swap32(mine, hh);  // the partner quad's rounded t2 (lane ^ 32)
       const float oth[4] = {other.x, other.y, other.z, other.w};
       const float av[4] = {ak.x, ak.y, ak.z, ak.w}, sv[4] = {sk.x, sk.y, sk.z, sk.w};
       vec_t<T, 4> d2;
@@ -466,28 +473,34 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
         asm volatile("" : "+v"(pr));  // the fp32 product is what is rounded (the fused depthwise backward's convention)
         d2[e] = inside ? (T)pr : (T)0.f;
       }
-      *reinterpret_cast<vec_t<T, 4>*>(drow + dp * DP + 4 * q16) = d2;
-      const float own = own_row && gx >= x0 && gx < W ? 1.f : 0.f;  // multiply, not branch: no divergence in the FMAs
-      const f2v l0 = f2v{(float)d2[0], (float)d2[1]} * own, l1 = f2v{(float)d2[2], (float)d2[3]} * own;
+      const float4 dw4 = make_float4((float)d2[0], (float)d2[1], (float)d2[2], (float)d2[3]);
+      *reinterpret_cast<float4*>(drow + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4) = dw4;
+      if constexpr (OWN) {
+        const float own = own_row && gx >= x0 && gx < W ? 1.f : 0.f;  // multiply, not branch: no divergence
+        const f2v l0 = f2v{dw4.x, dw4.y} * own, l1 = f2v{dw4.z, dw4.w} * own;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
-        aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
+        for (int t = 0; t < 9; ++t) {
+          aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
+          aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
+        }
+        db[0] += l0;
+        db[1] += l1;
       }
-      db[0] += l0;
-      db[1] += l1;
     }
   };
 
-  auto step = [&](auto slot_c, int i) {
-    constexpr int S = decltype(slot_c)::value;  // = i % NR: the register slots of dt2 row i and of t1 ring row i + 2
+  auto step = [&](auto j_c, int i) {
+    constexpr int J = decltype(j_c)::value;    // i = 3 m + J
+    constexpr int S = J % NR;                  // = i % 3: dt2 ring row and dh register slot of dt2 row i
+    constexpr int F = (J + 2) % NRF;           // = (i + 2) % NRF: n1 register slot of t1 ring row i + 2
     const int yd = y0 - 1 + i;
-    if (mfma_wave) mfma_row(IC<(S + 2) % NR>{}, i + 2);
+    __builtin_amdgcn_sched_barrier(0);  // no scheduling across steps (it hoists later steps' loads: register spills)
+    if (mfma_wave) mfma_row(IC<F>{}, i + 2);
     lds_barrier();
-    T* drow = dt2r + S * ROWD;  // ring row i % 3 (NR = 3)
+    float* drow = dt2r + S * ROWD;  // ring row i % 3 (NR = 3)
     const bool own_row = i >= 1 && i <= TH && yd < H;
-    dt2_px(IC<PXT>{}, xl + 1, i, yd, dq[S], drow, own_row);
-    if (has_halo) dt2_px(IC<1>{}, dph, i, yd, &dqh[S], drow, false);
+    dt2_px(IC<PXT>{}, std::true_type{}, xl + 1, i, yd, dq[S], drow, own_row);
+    if (has_halo) dt2_px(IC<1>{}, std::true_type{}, dph, i, yd, &dqh[S], drow, false);  // own_row false: no dW
 #pragma unroll
     for (int j = 0; j < PXT; ++j) dq[S][j] = bload4<T>(rh, dh_off(yd + NR, x0 + xl + j, true));
     dqh[S] = bload4<T>(rh, dh_off(yd + NR, x0 - 1 + dph, has_halo));
@@ -501,13 +514,14 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       for (int j = 0; j < PXT; ++j) acc[j][0] = acc[j][1] = f2v{0.f, 0.f};
 #pragma unroll
       for (int dhh = -1; dhh <= 1; ++dhh) {
-        const T* dr = dt2r + ((S + 2 - dhh) % 3) * ROWD;  // ring row (i - 1 - dhh) % 3
+        const float* dr = dt2r + ((S + 2 - dhh) % 3) * ROWD;  // ring row (i - 1 - dhh) % 3
         f2v gw[PXT + 2][2];
 #pragma unroll
         for (int c = 0; c < PXT + 2; ++c) {
-          const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(dr + (xl + c) * DP + 4 * q16);
-          gw[c][0] = f2v{(float)v[0], (float)v[1]};
-          gw[c][1] = f2v{(float)v[2], (float)v[3]};
+          const int dp = xl + c;
+          const float4 v = *reinterpret_cast<const float4*>(dr + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4);
+          gw[c][0] = f2v{v.x, v.y};
+          gw[c][1] = f2v{v.z, v.w};
         }
 #pragma unroll
         for (int j = 0; j < PXT; ++j)
@@ -531,7 +545,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     mfma_row(IC<1>{}, 1);
   }
 #pragma unroll 1
-  for (int i = 0; i < TH + 2; i += NR) {
+  for (int i = 0; i < TH + 2; i += 3) {
     step(IC<0>{}, i);
     step(IC<1>{}, i + 1);
     step(IC<2>{}, i + 2);
