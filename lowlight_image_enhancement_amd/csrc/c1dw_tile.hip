@@ -56,8 +56,9 @@ struct C1TileP {
 // of the slice (quads 0..7: gate channels, 8..15: their SimpleGate partners, so a gate quad and its partner sit in
 // lanes l and l ^ 32 and meet by one shuffle) and PXT adjacent tile columns starting at PXT (4 w + ((l >> 3) & 3)).
 // t1 ring rows: LW pixels x 64 fp32 channels (16 quads, 256 B: every pixel starts on bank 0); quad q of pixel px is
-// stored at q ^ (((px / PXT) & 1) << 3), so the four column groups a 16-lane ds_read_b128 group spans hit 16
-// distinct 4-bank quarters.
+// stored at q ^ key(px), a linear XOR key of the pixel's low bits chosen (by exhaustive search over the lane groups of
+// ds_read_b128 and ds_write_b128) so that the 16 lanes of a depthwise-phase read (4 column groups PXT apart x 4 quads)
+// and the 8 lanes of an MFMA-epilogue write (8 consecutive pixels, one quad) all hit distinct 4-bank quarters.
 //
 // Memory operations: every global load / store goes through a buffer descriptor of its tensor, with the byte offset
 // replaced by OOB (past every descriptor's range) where the pixel lies outside the image: the hardware then returns
@@ -65,7 +66,10 @@ struct C1TileP {
 // accounting stays exact and the rows prefetched into the register rings (static slots: the row loops are unrolled by
 // the ring depth, no register copies of in-flight loads) stay in flight across the steps.
 template <int PXT>
-__device__ __forceinline__ int qkey(int px) { return ((px / PXT) & 1) << 3; }
+__device__ __forceinline__ int qkey(int px) {
+  if constexpr (PXT == 2) return (px & 1) | ((px & 2) << 2) | ((px & 4) >> 1);  // px bits 0,1,2 -> key bits 0,3,1
+  else return (px & 3) | ((px & 4) << 1);                                      // px bits 0,1,2 -> key bits 0,1,3
+}
 
 constexpr int OOB = 0x7fffff00;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
