@@ -383,6 +383,9 @@ def make_trainer(dev, workload, precision, seed=0):
     init_sd = {k: v.clone() for k, v in net.state_dict().items()}
     net = net.to(dev)
     net.precision = precision
+    tc = os.environ.get("NBP_C1DW_TILE_C")  # A/B experiments only: the levels (channel counts) on the tile path
+    if tc is not None:
+        net.c1dw_tile_channels = tuple(int(c) for c in tc.split(",") if c)
     return NBPTrainer(net, psf_mode="rgb", psf_spec=spec, **wl["w"]), init_sd
 
 

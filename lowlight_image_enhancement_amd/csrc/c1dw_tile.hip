@@ -314,30 +314,35 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 }
 
 // ---------------------------------------------------------------- backward
-// Geometry: a TH x TW (TW 32) tile of dt1 x one 32-gate-channel slice.  Per step i (0 .. TH + 1), dt2 row yd = y0 - 1 + i:
-//   MFMA : t1 row yd + 1 (ring row k = i + 2; ring row k = image row y0 - 2 + k) over pixels x0 - 2 .. x0 + TW + 1
+// Geometry: a TH x TW (TW 32) tile of dt1 x one 32-gate-channel slice; t1 ring rows k = image row y0 - 2 + k (k 0 ..
+// TH + 3, pixels x0 - 2 .. x0 + TW + 1), dt2 rows i = image row y0 - 1 + i (i 0 .. TH + 1, pixels x0 - 1 .. x0 + TW).
+// One barrier per step j:
+//   A  (MFMA waves) t1 row k = j + 3 into t1 ring slot k % 5 (one step ahead of its first reader)
+//   B  dt1 of dt2-row o = j - 3 (1 <= o <= TH: image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1 (ring slots % 4),
+//      stored
 //   [barrier]
-//   dt2  : t2 = depthwise(t1 rows yd - 1 .. yd + 1) over pixels x0 - 1 .. x0 + TW, rounded; dg = dh a + ds / HW;
-//          dt2 = (dg t2[partner], dg t2[gate]) rounded into dt2 ring row i % 3; for the tile's own pixels (rows y0 ..
-//          y0 + TH - 1, columns x0 .. x0 + TW - 1) dW2 += dt2 * window, db2 += dt2
-//   [barrier]
-//   dt1  : (i >= 2) dt1 row yd - 1 = sum_t w[t] dt2(p - off_t) from dt2 rows yd - 2 .. yd
-// Both rings have 3 rows: with two barriers per step no row is overwritten while a wave may still read it.  The conv1
-// weight slice and bias live in LDS (read per chunk); the n1 rows (MFMA waves) and dh rows of the next steps in 3-slot
-// register rings (the step loop unrolled by 3).
-// dt2 ring rows: TW + 2 pixels x 64 fp32 channels (the rounded dt2 widened once), quads keyed like the t1 ring's.
+//   C  dt2 row i = j (i <= TH + 1): t2 = depthwise(t1 rows i .. i + 2) rounded; dg = dh a + ds / HW; dt2 = (dg
+//      t2[partner], dg t2[gate]) rounded into dt2 ring slot i % 4; for the tile's own pixels dW2 += dt2 * window,
+//      db2 += dt2
+// Reads of a row happen only after the barrier that follows its write; a slot is rewritten only after the barrier
+// that follows its last read (5 t1 slots: rows j - 1 .. j + 2 may still be read by slower waves while row j + 3 is
+// written; 4 dt2 slots: rows o - 1 .. o + 1 = j - 4 .. j - 2 are read before the barrier, row j written after it).
+// t1 ring: fp32 (the rounded t1 widened once), quads keyed as the forward's.  dt2 ring: the rounded 16-bit dt2, 80
+// elements (160 B) per pixel, so the four pixels 2 apart that a 32-lane ds_read_b64 group spans start on banks 0 /
+// 16 / 32 / 48.  The conv1 weight slice and bias live in LDS; the n1 rows (MFMA waves) and the dh rows of the next
+// steps in register rings with static slots (the step loop unrolled by the ring depth U: 3 at C 32, 2 at C 64).
 template <typename T, int C>
 __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   constexpr int TH = CT_TH, TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int ROWF = LT * 64;          // floats per t1 ring row
-  constexpr int ROWD = LD * 64;          // floats per dt2 ring row
-  constexpr int NR = 3;                  // dh register-ring slots (= the rings' row count)
-  constexpr int NRF = 3;                 // n1 register-ring slots; the step loop unrolls by 3
+  constexpr int DP = 80;                 // T elements per dt2 ring pixel (64 + pad)
+  constexpr int ROWD = LD * DP;          // T elements per dt2 ring row
+  constexpr int U = C == 32 ? 3 : 2;     // register-ring slots (n1, dh) = the step loop's unroll
+  constexpr int NS = TH + 4;             // steps (the last dt1 row at j = TH + 3)
   constexpr int RPB = 256 / (C * 2);     // weight rows per 256-byte LDS bank row (the swizzle key's divisor)
   constexpr int NC = 2 * KS;             // 16-byte chunks per weight row
-  static_assert((TH + 2) % 3 == 0, "step loop unroll");
-  __shared__ __attribute__((aligned(16))) float t1r[3 * ROWF];
-  __shared__ __attribute__((aligned(16))) float dt2r[3 * ROWD];
+  __shared__ __attribute__((aligned(16))) float t1r[5 * ROWF];
+  __shared__ __attribute__((aligned(16))) T dt2r[4 * ROWD];
   __shared__ __attribute__((aligned(16))) T w1s[64 * C];
   __shared__ __attribute__((aligned(16))) float b1s[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -362,10 +367,10 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   const bool mfma_wave = wave < 2;
   const int gxm = x0 - 2 + wave * 32 + r;
   const bool lane_ok = wave * 32 + r < LT;
-  vec_t<T, 8> fq[NRF][KS];  // n1 fragments of image row y0 - 2 + k in slot k % NRF
+  vec_t<T, 8> fq[U][KS];  // n1 fragments of t1 ring row k in slot k % U
   if (mfma_wave)
 #pragma unroll
-    for (int k = 0; k < NRF; ++k) load_n1<T, KS>(rn, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
+    for (int k = 0; k < U; ++k) load_n1<T, KS>(rn, img, W, H, y0 - 2 + k, gxm, lane_ok, hh, fq[k]);
   // ---- depthwise lanes: quad q16 at tile columns xl, xl + 1 (dt2 ring pixels xl + 1, xl + 2); the 32 lanes of
   // column group 0 of waves 2 / 3 (no MFMA phase) also own the halo pixel of the dt2 rows (ring pixel 0 / TW + 1)
   const int q16 = (lane & 7) + 8 * hh, xl = PXT * (4 * wave + ((lane >> 3) & 3));
@@ -381,9 +386,9 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   auto dh_off = [&](int yy, int gx, bool lane_has) {
     return lane_has && yy >= 0 && yy < H && gx >= 0 && gx < W ? (int)((img + (long)yy * W + gx) * (2 * C)) + 2 * gch : OOB;
   };
-  vec_t<T, 4> dq[NR][PXT], dqh[NR];  // dh of dt2 row y0 - 1 + i in slot i % NR
+  vec_t<T, 4> dq[U][PXT], dqh[U];  // dh of dt2 row i in slot i % U
 #pragma unroll
-  for (int k = 0; k < NR; ++k) {
+  for (int k = 0; k < U; ++k) {
 #pragma unroll
     for (int j = 0; j < PXT; ++j) dq[k][j] = bload4<T>(rh, dh_off(y0 - 1 + k, x0 + xl + j, true));
     dqh[k] = bload4<T>(rh, dh_off(y0 - 1 + k, x0 - 1 + dph, has_halo));
@@ -394,48 +399,50 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   db[0] = db[1] = f2v{0.f, 0.f};
   lds_barrier();  // weight slice and bias in LDS
 
-  // MFMA phase of t1 ring row k (image row y0 - 2 + k) from register slot S = k % NRF, which then takes row k + NRF
+  // A: t1 ring row k (image row y0 - 2 + k) from register slot S = k % U, which then takes row k + U
   auto mfma_row = [&](auto slot_c, int k) {
     constexpr int S = decltype(slot_c)::value;
     const int yy = y0 - 2 + k;
-    const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
-    floatx16 acc[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int n = t * 32 + r, c = 2 * ks + hh;
-        const vec_t<T, 8> wf = *reinterpret_cast<const vec_t<T, 8>*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1))));
-        acc[t] = mfma32x32x16(wf, fq[S][ks], acc[t]);
-      }
-    load_n1<T, KS>(rn, img, W, H, yy + NRF, gxm, lane_ok, hh, fq[S]);
-    const int px = wave * 32 + r;
-    if (px < LT) {
-      float* slot = t1r + (k % 3) * ROWF;
-      const int key = qkey<PXT>(px);
+    if (k <= TH + 3) {  // uniform
+      const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
+      floatx16 acc[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
-          const float bq[4] = {bv.x, bv.y, bv.z, bv.w};
-          float v[4];
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = valid ? (float)(T)(acc[t][4 * g + q] + bq[q]) : 0.f;
-          *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = make_float4(v[0], v[1], v[2], v[3]);
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int n = t * 32 + r, c = 2 * ks + hh;
+          const vec_t<T, 8> wf = *reinterpret_cast<const vec_t<T, 8>*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1))));
+          acc[t] = mfma32x32x16(wf, fq[S][ks], acc[t]);
         }
+      const int px = wave * 32 + r;
+      if (px < LT) {
+        float* slot = t1r + (k % 5) * ROWF;
+        const int key = qkey<PXT>(px);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
+            const float bq[4] = {bv.x, bv.y, bv.z, bv.w};
+            float v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = valid ? (float)(T)(acc[t][4 * g + q] + bq[q]) : 0.f;
+            *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+      }
     }
+    load_n1<T, KS>(rn, img, W, H, yy + U, gxm, lane_ok, hh, fq[S]);  // OOB past the image: zeros, no branch
   };
 
-  // dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row yd, from t1
-  // ring rows k0 .. k0 + 2; own_row: accumulate the depthwise weight / bias gradients of the tile's own pixels
-  auto dt2_px = [&](auto np_c, auto own_c, int dp0, int k0, int yd, const vec_t<T, 4>* dv, float* drow, bool own_row) {
+  // C: dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row i, from t1
+  // ring rows i .. i + 2; own_row: accumulate the depthwise weight / bias gradients of the tile's own pixels
+  auto dt2_px = [&](auto np_c, int dp0, int i, const vec_t<T, 4>* dv, T* drow, bool own_row) {
     constexpr int NP = decltype(np_c)::value;
-    constexpr bool OWN = decltype(own_c)::value;  // false: halo pixels (no weight-gradient work)
+    const int yd = y0 - 1 + i;
     f2v a2[NP][2];
     f2v xw[3][NP + 2][2];
 #pragma unroll
@@ -445,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     }
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
-      const float* row = t1r + ((k0 + dy) % 3) * ROWF;
+      const float* row = t1r + ((i + dy) % 5) * ROWF;
 #pragma unroll
       for (int c = 0; c < NP + 2; ++c) {
         const int px = dp0 + c;  // t1 ring pixel (image column x0 - 2 + px)
@@ -477,82 +484,92 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
         asm volatile("" : "+v"(pr));  // the fp32 product is what is rounded (the fused depthwise backward's convention)
         d2[e] = inside ? (T)pr : (T)0.f;
       }
-      const float4 dw4 = make_float4((float)d2[0], (float)d2[1], (float)d2[2], (float)d2[3]);
-      *reinterpret_cast<float4*>(drow + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4) = dw4;
-      if constexpr (OWN) {
-        const float own = own_row && gx >= x0 && gx < W ? 1.f : 0.f;  // multiply, not branch: no divergence
-        const f2v l0 = f2v{dw4.x, dw4.y} * own, l1 = f2v{dw4.z, dw4.w} * own;
+      const int hk = (dp >> 1) & 1;  // half swap: see the ring geometry above
+      *reinterpret_cast<vec_t<T, 4>*>(drow + dp * DP + (hk ^ hh) * 32 + 4 * (lane & 7)) = d2;
+      const float own = own_row && gx >= x0 && gx < W ? 1.f : 0.f;  // multiply, not branch: no divergence
+      const f2v l0 = f2v{(float)d2[0], (float)d2[1]} * own, l1 = f2v{(float)d2[2], (float)d2[3]} * own;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
-          aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
-        }
-        db[0] += l0;
-        db[1] += l1;
+      for (int t = 0; t < 9; ++t) {
+        aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
+        aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
       }
+      db[0] += l0;
+      db[1] += l1;
     }
   };
 
-  auto step = [&](auto j_c, int i) {
-    constexpr int J = decltype(j_c)::value;    // i = 3 m + J
-    constexpr int S = J % NR;                  // = i % 3: dt2 ring row and dh register slot of dt2 row i
-    constexpr int F = (J + 2) % NRF;           // = (i + 2) % NRF: n1 register slot of t1 ring row i + 2
-    const int yd = y0 - 1 + i;
-    __builtin_amdgcn_sched_barrier(0);  // no scheduling across steps (it hoists later steps' loads: register spills)
-    if (mfma_wave) mfma_row(IC<F>{}, i + 2);
-    lds_barrier();
-    float* drow = dt2r + S * ROWD;  // ring row i % 3 (NR = 3)
-    const bool own_row = i >= 1 && i <= TH && yd < H;
-    dt2_px(IC<PXT>{}, std::true_type{}, xl + 1, i, yd, dq[S], drow, own_row);
-    if (has_halo) dt2_px(IC<1>{}, std::true_type{}, dph, i, yd, &dqh[S], drow, false);  // own_row false: no dW
+  auto step = [&](auto j_c, int j) {
+    constexpr int J = decltype(j_c)::value;  // j = U m + J: the dh slot of dt2 row j
+    __builtin_amdgcn_sched_barrier(0);       // no scheduling across steps (it hoists later steps' loads: spills)
+    // A: t1 ring row j + 3 (register slot (j + 3) % U)
+    if (mfma_wave) mfma_row(IC<(J + 3) % U>{}, j + 3);
+    // B: dt1 of dt2-row o = j - 3 (image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1
+    {
+      const int o = j - 3, yo = y0 - 1 + o;
+      if (o >= 1 && o <= TH) {  // uniform
+        f2v acc[PXT][2];
 #pragma unroll
-    for (int j = 0; j < PXT; ++j) dq[S][j] = bload4<T>(rh, dh_off(yd + NR, x0 + xl + j, true));
-    dqh[S] = bload4<T>(rh, dh_off(yd + NR, x0 - 1 + dph, has_halo));
-    lds_barrier();
-    if (i >= 2) {
-      const int yo = yd - 1;
-      // dt1(p) = sum_t w[t] dt2(p - off_t): tap t = (dhh, dww) reads dt2 row yo - dhh (ring row i - 1 - dhh) at ring
-      // pixel xl + j + 1 - dww
-      f2v acc[PXT][2];
+        for (int jj = 0; jj < PXT; ++jj) acc[jj][0] = acc[jj][1] = f2v{0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < PXT; ++j) acc[j][0] = acc[j][1] = f2v{0.f, 0.f};
+        for (int dhh = -1; dhh <= 1; ++dhh) {
+          const T* dr = dt2r + ((o - dhh) & 3) * ROWD;  // tap (dhh, dww) reads dt2 row o - dhh at ring pixel p + 1 - dww
+          f2v gw[PXT + 2][2];
 #pragma unroll
-      for (int dhh = -1; dhh <= 1; ++dhh) {
-        const float* dr = dt2r + ((S + 2 - dhh) % 3) * ROWD;  // ring row (i - 1 - dhh) % 3
-        f2v gw[PXT + 2][2];
-#pragma unroll
-        for (int c = 0; c < PXT + 2; ++c) {
-          const int dp = xl + c;
-          const float4 v = *reinterpret_cast<const float4*>(dr + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4);
-          gw[c][0] = f2v{v.x, v.y};
-          gw[c][1] = f2v{v.z, v.w};
-        }
-#pragma unroll
-        for (int j = 0; j < PXT; ++j)
-#pragma unroll
-          for (int dww = -1; dww <= 1; ++dww) {
-            const int t = (dhh + 1) * 3 + (dww + 1);
-#pragma unroll
-            for (int e = 0; e < 2; ++e) acc[j][e] = __builtin_elementwise_fma(dw.w[t][e], gw[j + 1 - dww][e], acc[j][e]);
+          for (int c = 0; c < PXT + 2; ++c) {
+            const int dp = xl + c;
+            const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(dr + dp * DP + ((((dp >> 1) & 1) ^ hh) * 32) +
+                                                                        4 * (lane & 7));
+            gw[c][0] = f2v{(float)v[0], (float)v[1]};
+            gw[c][1] = f2v{(float)v[2], (float)v[3]};
           }
+#pragma unroll
+          for (int jj = 0; jj < PXT; ++jj)
+#pragma unroll
+            for (int dww = -1; dww <= 1; ++dww) {
+              const int t = (dhh + 1) * 3 + (dww + 1);
+#pragma unroll
+              for (int e = 0; e < 2; ++e)
+                acc[jj][e] = __builtin_elementwise_fma(dw.w[t][e], gw[jj + 1 - dww][e], acc[jj][e]);
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < PXT; ++jj) {
+          const int gx = x0 + xl + jj;
+          bstore4<T>(ro, yo < H && gx < W ? (int)((img + (long)yo * W + gx) * (4 * C)) + 2 * ch : OOB, f4of(acc[jj]));
+        }
+      } else {
+        // keep the VMEM stream uniform across steps (exact vmcnt accounting): dropped stores
+#pragma unroll
+        for (int jj = 0; jj < PXT; ++jj) bstore4<T>(ro, OOB, f4(0.f));
+      }
+    }
+    lds_barrier();
+    // C: dt2 row i = j
+    {
+      const int i = j, yd = y0 - 1 + i;
+      if (i <= TH + 1) {  // uniform
+        T* drow = dt2r + (i & 3) * ROWD;
+        const bool own_row = i >= 1 && i <= TH && yd < H;
+        dt2_px(IC<PXT>{}, xl + 1, i, dq[J], drow, own_row);
+        if (has_halo) dt2_px(IC<1>{}, dph, i, &dqh[J], drow, false);
       }
 #pragma unroll
-      for (int j = 0; j < PXT; ++j) {
-        const int gx = x0 + xl + j;
-        bstore4<T>(ro, yo < H && gx < W ? (int)((img + (long)yo * W + gx) * (4 * C)) + 2 * ch : OOB, f4of(acc[j]));
-      }
+      for (int jj = 0; jj < PXT; ++jj) dq[J][jj] = bload4<T>(rh, dh_off(yd + U, x0 + xl + jj, true));
+      dqh[J] = bload4<T>(rh, dh_off(yd + U, x0 - 1 + dph, has_halo));
     }
   };
 
-  if (mfma_wave) {
+  if (mfma_wave) {  // t1 ring rows 0 .. 2 (register slots 0 .. 2 % U)
     mfma_row(IC<0>{}, 0);
-    mfma_row(IC<1>{}, 1);
+    mfma_row(IC<1 % U>{}, 1);
+    mfma_row(IC<2 % U>{}, 2);
   }
+  static_assert(U == 2 || U == 3, "ring depth");
 #pragma unroll 1
-  for (int i = 0; i < TH + 2; i += 3) {
-    step(IC<0>{}, i);
-    step(IC<1>{}, i + 1);
-    step(IC<2>{}, i + 2);
+  for (int j = 0; j < NS; j += U) {
+    step(IC<0>{}, j);
+    step(IC<1>{}, j + 1);
+    if constexpr (U == 3) step(IC<2>{}, j + 2);
   }
   // ---- the tile's depthwise weight / bias gradients: 40 values per lane, summed over the lanes of one quad (lane bits
   // 3..4: a reduce-scatter, 40 -> 20 -> 10 values per lane), then over the 4 waves in order

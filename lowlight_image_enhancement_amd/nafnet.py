@@ -117,6 +117,7 @@ class NAFNet(nn.Module):
         # keeps t1 / t2 on chip (nbp_c1dw_fwd_tile), and the mirror backward that rebuilds them from n1
         # (nbp_c1dw_bwd_tile): the 2C-wide tape never reaches HBM
         self.fuse_c1dw_tile = True
+        self.c1dw_tile_channels = (32, 64)  # the levels (by channel count) that take it
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
@@ -396,7 +397,7 @@ class NAFNet(nn.Module):
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
-        tile = (self.fuse_c1dw_tile and dt != 0 and len(self._W) == 3
+        tile = (self.fuse_c1dw_tile and c in self.c1dw_tile_channels and dt != 0 and len(self._W) == 3
                 and query("c1dw_tile_supported", h, w, c, dt) == 1)
         c1dw = (not tile and self.fuse_c1dw and dt != 0 and len(self._W) == 3
                 and query("c1dw_supported", h, w, c, dt) == 1)

@@ -89,8 +89,8 @@ def main():
         print(f"B{B} {H}x{W} C{C} fp16 (M*C*2 = {mb:.1f} MB):", flush=True)
         for k, v in res.items():
             print(f"  {k:8s} {min(v):8.1f} us  (rounds: {', '.join(f'{x:.1f}' for x in v)})", flush=True)
-        print(f"  fwd new algorithmic bytes n1 + g = {2 * mb:.1f} MB -> {2 * mb / min(res['fwd_new']) * 1e-3:.2f} TB/s; "
-              f"bwd new dh + n1 + dt1 = {4 * mb:.1f} MB -> {4 * mb / min(res['bwd_new']) * 1e-3:.2f} TB/s", flush=True)
+        print(f"  fwd new algorithmic bytes n1 + g = {2 * mb:.1f} MB -> {2 * mb / min(res['fwd_new']):.2f} TB/s; "
+              f"bwd new dh + n1 + dt1 = {4 * mb:.1f} MB -> {4 * mb / min(res['bwd_new']):.2f} TB/s", flush=True)
 
 
 if __name__ == "__main__":
