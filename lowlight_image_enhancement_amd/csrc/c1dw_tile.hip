@@ -338,7 +338,6 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   constexpr int DP = 80;                 // T elements per dt2 ring pixel (64 + pad)
   constexpr int ROWD = LD * DP;          // T elements per dt2 ring row
   constexpr int U = C == 32 ? 3 : 2;     // register-ring slots (n1, dh) = the step loop's unroll
-  constexpr int NS = TH + 4;             // steps (the last dt1 row at j = TH + 3)
   constexpr int RPB = 256 / (C * 2);     // weight rows per 256-byte LDS bank row (the swizzle key's divisor)
   constexpr int NC = 2 * KS;             // 16-byte chunks per weight row
   __shared__ __attribute__((aligned(16))) float t1r[5 * ROWF];
@@ -440,9 +439,11 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
 
   // C: dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row i, from t1
   // ring rows i .. i + 2; own_row: accumulate the depthwise weight / bias gradients of the tile's own pixels
-  auto dt2_px = [&](auto np_c, int dp0, int i, const vec_t<T, 4>* dv, T* drow, bool own_row) {
+  auto dt2_px = [&](auto np_c, auto own_c, int dp0, int i, const vec_t<T, 4>* dv, T* drow, float own) {
     constexpr int NP = decltype(np_c)::value;
+    constexpr bool OWN = decltype(own_c)::value;
     const int yd = y0 - 1 + i;
+    const bool row_in = yd >= 0 && yd < H && i <= TH + 1;
     f2v a2[NP][2];
     f2v xw[3][NP + 2][2];
 #pragma unroll
@@ -470,7 +471,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       const int dp = dp0 + j, gx = x0 - 1 + dp;
-      const bool inside = yd >= 0 && yd < H && gx >= 0 && gx < W;
+      const bool inside = row_in && gx >= 0 && gx < W;
       const float4 tm = f4of(a2[j]);
       const float4 mine = make_float4((float)(T)tm.x, (float)(T)tm.y, (float)(T)tm.z, (float)(T)tm.w);  // t2 rounded
       const float4 other = swap32(mine, hh);  // the partner quad's rounded t2 (lane ^ 32)
@@ -486,91 +487,92 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       }
       const int hk = (dp >> 1) & 1;  // half swap: see the ring geometry above
       *reinterpret_cast<vec_t<T, 4>*>(drow + dp * DP + (hk ^ hh) * 32 + 4 * (lane & 7)) = d2;
-      const float own = own_row && gx >= x0 && gx < W ? 1.f : 0.f;  // multiply, not branch: no divergence
-      const f2v l0 = f2v{(float)d2[0], (float)d2[1]} * own, l1 = f2v{(float)d2[2], (float)d2[3]} * own;
+      if constexpr (OWN) {  // own (uniform 0 / 1): the dt2 row is one of the tile's; d2 is 0 outside the image
+        const f2v l0 = f2v{(float)d2[0], (float)d2[1]} * own, l1 = f2v{(float)d2[2], (float)d2[3]} * own;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
-        aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
+        for (int t = 0; t < 9; ++t) {
+          aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
+          aw[t][1] = __builtin_elementwise_fma(l1, xw[t / 3][j + t % 3][1], aw[t][1]);
+        }
+        db[0] += l0;
+        db[1] += l1;
       }
-      db[0] += l0;
-      db[1] += l1;
     }
   };
 
+  // step j: barrier(j); B(j + 1); C(j); A(j + 1).  Between two barriers the three phases touch disjoint ring slots (B:
+  // dt2 rows j - 3 .. j - 1, complete before barrier(j); C: t1 rows j .. j + 2, written by A(j - 1) before barrier(j),
+  // and dt2 row j into the slot of row j - 4, last read by B(j); A: t1 row j + 4 into the slot of row j - 1, last read
+  // by C(j - 1)), and B / C carry no branch, so the scheduler can overlap them; rows outside the tile are masked
+  // (dt2 zeroed, dt1 stores to an out-of-range offset)
   auto step = [&](auto j_c, int j) {
     constexpr int J = decltype(j_c)::value;  // j = U m + J: the dh slot of dt2 row j
     __builtin_amdgcn_sched_barrier(0);       // no scheduling across steps (it hoists later steps' loads: spills)
-    // A: t1 ring row j + 3 (register slot (j + 3) % U)
-    if (mfma_wave) mfma_row(IC<(J + 3) % U>{}, j + 3);
-    // B: dt1 of dt2-row o = j - 3 (image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1
+    lds_barrier();
+    // B: dt1 of dt2-row o = j - 2 (image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1
     {
-      const int o = j - 3, yo = y0 - 1 + o;
-      if (o >= 1 && o <= TH) {  // uniform
-        f2v acc[PXT][2];
+      const int o = j - 2, yo = y0 - 1 + o;
+      const bool orow = o >= 1 && o <= TH && yo < H;
+      f2v acc[PXT][2];
 #pragma unroll
-        for (int jj = 0; jj < PXT; ++jj) acc[jj][0] = acc[jj][1] = f2v{0.f, 0.f};
+      for (int jj = 0; jj < PXT; ++jj) acc[jj][0] = acc[jj][1] = f2v{0.f, 0.f};
 #pragma unroll
-        for (int dhh = -1; dhh <= 1; ++dhh) {
-          const T* dr = dt2r + ((o - dhh) & 3) * ROWD;  // tap (dhh, dww) reads dt2 row o - dhh at ring pixel p + 1 - dww
-          f2v gw[PXT + 2][2];
+      for (int dhh = -1; dhh <= 1; ++dhh) {
+        const T* dr = dt2r + ((o - dhh) & 3) * ROWD;  // tap (dhh, dww) reads dt2 row o - dhh at ring pixel p + 1 - dww
+        f2v gw[PXT + 2][2];
 #pragma unroll
-          for (int c = 0; c < PXT + 2; ++c) {
-            const int dp = xl + c;
-            const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(dr + dp * DP + ((((dp >> 1) & 1) ^ hh) * 32) +
-                                                                        4 * (lane & 7));
-            gw[c][0] = f2v{(float)v[0], (float)v[1]};
-            gw[c][1] = f2v{(float)v[2], (float)v[3]};
+        for (int c = 0; c < PXT + 2; ++c) {
+          const int dp = xl + c;
+          const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(dr + dp * DP + ((((dp >> 1) & 1) ^ hh) * 32) +
+                                                                      4 * (lane & 7));
+          gw[c][0] = f2v{(float)v[0], (float)v[1]};
+          gw[c][1] = f2v{(float)v[2], (float)v[3]};
+        }
+#pragma unroll
+        for (int jj = 0; jj < PXT; ++jj)
+#pragma unroll
+          for (int dww = -1; dww <= 1; ++dww) {
+            const int t = (dhh + 1) * 3 + (dww + 1);
+#pragma unroll
+            for (int e = 0; e < 2; ++e) acc[jj][e] = __builtin_elementwise_fma(dw.w[t][e], gw[jj + 1 - dww][e], acc[jj][e]);
           }
+      }
 #pragma unroll
-          for (int jj = 0; jj < PXT; ++jj)
-#pragma unroll
-            for (int dww = -1; dww <= 1; ++dww) {
-              const int t = (dhh + 1) * 3 + (dww + 1);
-#pragma unroll
-              for (int e = 0; e < 2; ++e)
-                acc[jj][e] = __builtin_elementwise_fma(dw.w[t][e], gw[jj + 1 - dww][e], acc[jj][e]);
-            }
-        }
-#pragma unroll
-        for (int jj = 0; jj < PXT; ++jj) {
-          const int gx = x0 + xl + jj;
-          bstore4<T>(ro, yo < H && gx < W ? (int)((img + (long)yo * W + gx) * (4 * C)) + 2 * ch : OOB, f4of(acc[jj]));
-        }
-      } else {
-        // keep the VMEM stream uniform across steps (exact vmcnt accounting): dropped stores
-#pragma unroll
-        for (int jj = 0; jj < PXT; ++jj) bstore4<T>(ro, OOB, f4(0.f));
+      for (int jj = 0; jj < PXT; ++jj) {
+        const int gx = x0 + xl + jj;
+        bstore4<T>(ro, orow && gx < W ? (int)((img + (long)yo * W + gx) * (4 * C)) + 2 * ch : OOB, f4of(acc[jj]));
       }
     }
-    lds_barrier();
     // C: dt2 row i = j
     {
       const int i = j, yd = y0 - 1 + i;
-      if (i <= TH + 1) {  // uniform
-        T* drow = dt2r + (i & 3) * ROWD;
-        const bool own_row = i >= 1 && i <= TH && yd < H;
-        dt2_px(IC<PXT>{}, xl + 1, i, dq[J], drow, own_row);
-        if (has_halo) dt2_px(IC<1>{}, dph, i, &dqh[J], drow, false);
-      }
+      T* drow = dt2r + (i & 3) * ROWD;
+      dt2_px(IC<PXT>{}, std::true_type{}, xl + 1, i, dq[J], drow, i >= 1 && i <= TH ? 1.f : 0.f);
+      if (has_halo) dt2_px(IC<1>{}, std::true_type{}, dph, i, &dqh[J], drow, 0.f);
 #pragma unroll
       for (int jj = 0; jj < PXT; ++jj) dq[J][jj] = bload4<T>(rh, dh_off(yd + U, x0 + xl + jj, true));
       dqh[J] = bload4<T>(rh, dh_off(yd + U, x0 - 1 + dph, has_halo));
     }
+    // A: t1 ring row j + 4 (register slot (j + 4) % U)
+    if (mfma_wave) mfma_row(IC<(J + 4) % U>{}, j + 4);
   };
 
-  if (mfma_wave) {  // t1 ring rows 0 .. 2 (register slots 0 .. 2 % U)
+  if (mfma_wave) {  // t1 ring rows 0 .. 3 (register slots k % U)
     mfma_row(IC<0>{}, 0);
     mfma_row(IC<1 % U>{}, 1);
     mfma_row(IC<2 % U>{}, 2);
+    mfma_row(IC<3 % U>{}, 3);
   }
   static_assert(U == 2 || U == 3, "ring depth");
+  constexpr int NS = TH + 3;  // steps j = 0 .. TH + 2: C(j) to dt2 row TH + 1, B(j + 1) to dt1 row TH
 #pragma unroll 1
-  for (int j = 0; j < NS; j += U) {
+  for (int j = 0; j < NS - NS % U; j += U) {
     step(IC<0>{}, j);
     step(IC<1>{}, j + 1);
     if constexpr (U == 3) step(IC<2>{}, j + 2);
   }
+  if constexpr (NS % U >= 1) step(IC<0>{}, NS - NS % U);
+  if constexpr (NS % U >= 2) step(IC<1>{}, NS - NS % U + 1);
   // ---- the tile's depthwise weight / bias gradients: 40 values per lane, summed over the lanes of one quad (lane bits
   // 3..4: a reduce-scatter, 40 -> 20 -> 10 values per lane), then over the 4 waves in order
   float v[40];

@@ -128,6 +128,7 @@ def test_tile_network_matches_stored_tape(dev, precision):
     torch.manual_seed(5)
     net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]).to(dev)
     net.precision = precision
+    net.c1dw_tile_channels = (32, 64)
     with torch.no_grad():
         net.flat.add_(torch.randn_like(net.flat) * 0.02)
     x = torch.rand(2, 3, 96, 80, device=dev)
