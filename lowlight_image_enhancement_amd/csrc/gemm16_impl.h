@@ -66,6 +66,31 @@ struct GemmPB {
   int tile_map;
 };
 
+// Timeline probe (scripts/gemm_timeline.py; built only into the probe library, scripts/build_probe.py, never into the
+// production .so): thread 0 of each gemm_glds_kernel workgroup records the 100 MHz global clock at 6 points of its life
+// (slot 0: the first instruction; 1: the kernel arguments in registers; 2: prologue DMAs issued; 3: K-tile 0 landed;
+// 4: last MFMA issued; 5: epilogue stores landed) plus HW_ID / XCC_ID (slots 6 / 7), 8 words per workgroup in grid
+// order
+#ifdef NBP_GEMM_PROBE
+constexpr int GEMM_PROBE_WGS = 16384;
+__device__ unsigned long long g_gemm_probe[GEMM_PROBE_WGS * 8];
+__device__ __forceinline__ void gemm_stamp_at(int i, unsigned long long t) {
+  if (threadIdx.x == 0) {
+    const unsigned w = blockIdx.x + gridDim.x * blockIdx.y;
+    if (w < GEMM_PROBE_WGS) {
+      g_gemm_probe[w * 8 + i] = t;
+      if (i == 0) {
+        g_gemm_probe[w * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        g_gemm_probe[w * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      }
+    }
+  }
+}
+#define GEMM_STAMP(i) gemm_stamp_at(i, __builtin_amdgcn_s_memrealtime())
+#else
+#define GEMM_STAMP(i) ((void)0)
+#endif
+
 __device__ __forceinline__ long s2d_off(int m, int k, int gh, int gw, int cs) {
   const int per = gh * gw;
   const int b = m / per, rem = m - b * per;
@@ -608,6 +633,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
   static_assert(NS >= 2 && NS <= 5, "ring depth");
   static_assert(SM_BYTES <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM_BYTES];
+#ifdef NBP_GEMM_PROBE
+  const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+  {
+    int mk = p.M + p.K;  // the kernel arguments in registers
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(mk)::"memory");
+    const unsigned long long t_args = __builtin_amdgcn_s_memrealtime() + (mk == -7 ? 1 : 0);
+    gemm_stamp_at(0, t_entry);
+    gemm_stamp_at(1, t_args);
+  }
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   // slot permutation key of row r
@@ -767,6 +802,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
+  GEMM_STAMP(2);
   for (int t = 0; t < nk; ++t) {
     // retire K-tile t (this wave's DMAs), leaving the later tiles of the ring in flight; the barrier then makes every
     // wave's part of tile t visible and frees the stage read at step t - 1 for tile t + NS - 1
@@ -777,11 +813,17 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (t == 0) GEMM_STAMP(3);
     if (t + NS - 1 < nk) issue(t + NS - 1);
     compute(t % NS);
   }
+  GEMM_STAMP(4);
   __syncthreads();  // the ring is drained (vmcnt(0) at the last step); every fragment read done before Cs aliases it
   gemm_epilogue<BM, BN, CMODE, TC, H, WN, WM, EPP, NPRE>(p, acc, smem, m0, n0, &lpre);
+#ifdef NBP_GEMM_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores landed
+  GEMM_STAMP(5);
+#endif
 }
 
 // ---------------------------------------------------------------- skinny GEMM (N, K <= 64), bf16 in / out
