@@ -1563,18 +1563,25 @@ void launch(const GemmPB& p, hipStream_t st) {
     if (ok) {
       // the ring depth the tile's LDS allows (stage = (BM + BN) x 128 B + scales; the fp32 C staging must fit too)
       constexpr int STB = (BM + BN) * 128 + (AMODE == AM_SCALE ? 256 : 0), CB = BM * (BN + 4) * 4;
+#ifdef NBP_GEMM_NS5  // probe builds only: a 5-deep ring where it fits
+      constexpr int NMAX = 5 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 5 :
+                           4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
+#else
       constexpr int NMAX = 4 * STB <= 160 * 1024 && CB <= 160 * 1024 ? 4 : (3 * STB <= 160 * 1024 ? 3 : 2);
+#endif
       const int nd = ns_env < 0 ? glds_auto_depth((long)grid.x * grid.y, STB, CB, NMAX) : (ns < NMAX ? ns : NMAX);
       if constexpr (BN >= 128 && CMODE != CM_LNBWD && CMODE != CM_CHANDOT) {
         // 2 x 4 waves of (BM / 2) x (BN / 4), two per SIMD (+2 % step over 2 x 2 waves)
         if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
         else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
-        else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+        else if (nd == 4 || NMAX < 5) gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
+        else gemm_glds_kernel<BM, BN, (NMAX >= 5 ? 5 : 2), AMODE, CMODE, TC, H, 4><<<grid, 512, 0, st>>>(p);
         return;
       }
       if (nd == 2) gemm_glds_kernel<BM, BN, 2, AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       else if (nd == 3) gemm_glds_kernel<BM, BN, (NMAX >= 3 ? 3 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
-      else gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      else if (nd == 4 || NMAX < 5) gemm_glds_kernel<BM, BN, (NMAX >= 4 ? 4 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
+      else gemm_glds_kernel<BM, BN, (NMAX >= 5 ? 5 : 2), AMODE, CMODE, TC, H><<<grid, 256, 0, st>>>(p);
       return;
     }
   }
@@ -1586,7 +1593,11 @@ void launch(const GemmPB& p, hipStream_t st) {
 
 // largest tile (no wider than N or taller than M, rounded up to 64) that still gives >= 512 blocks (2 per CU; with the
 // 8-wave DMA tiles: 1024 with the register-staged 4-wave kernel measured best); otherwise 64x64, the most blocks.
+#ifdef NBP_GEMM_MINBLK  // probe builds only (scripts/build_probe.py MINBLK=...)
+constexpr long GEMM_MINBLK = NBP_GEMM_MINBLK;
+#else
 constexpr long GEMM_MINBLK = 512;
+#endif
 
 // 256 x 256 tiles on 8 waves (2 x 4, 128 x 64 each; two-pass epilogue) for the 3x3 implicit-GEMM convs with N >= 256
 // while the grid still has >= 256 workgroups.  Measured (scripts/conv_micro.py, fp16, bs 8): +34-39 % on the 128^2 x

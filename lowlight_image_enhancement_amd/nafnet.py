@@ -117,10 +117,11 @@ class NAFNet(nn.Module):
         # keeps t1 / t2 on chip (nbp_c1dw_fwd_tile), and the mirror backward that rebuilds them from n1
         # (nbp_c1dw_bwd_tile): the 2C-wide tape never reaches HBM
         self.fuse_c1dw_tile = True
-        # the levels (by channel count) that take it: level 0 only.  The rebuild costs the backward ~1.3x the stored-tape
-        # kernel's VALU work (t1 epilogue + t2 recomputed), which the forward's saved tape traffic repays at level 0
-        # (eager 3.22 vs 3.36 ms for its 4 blocks) but not at level 1 (graph step -0.2 %)
-        self.c1dw_tile_channels = (32,)
+        # the levels (by channel count) that take it: none by default.  The rebuild costs the backward ~1.3x the
+        # stored-tape kernel's VALU work (t1 epilogue + t2 recomputed: 213 vs 147 us at level 0), which the forward's
+        # saved tape traffic (58 vs 107 us) only repays in the eager level time; the graph step measured 1306-1314
+        # img/s without it, 1303-1306 with it at levels 0 / 1
+        self.c1dw_tile_channels = ()
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
