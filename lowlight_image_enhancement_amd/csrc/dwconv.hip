@@ -7,14 +7,6 @@
 
 using namespace nbp;
 
-namespace nbp {  // dw_stream.hip: the row-streaming SCA + SimpleGate + depthwise backward (C % 16 == 0, 16-bit)
-bool dw_stream_ok(int B, int H, int W, int C, int dtype);
-long dw_stream_rows(int B, int H, int W, int C);
-int launch_dw_stream(const void* dh, const float* a, const float* ds, const void* t2, const void* t1, const float* wdw,
-                     void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C, int dtype,
-                     nbp_stream_t s);
-}  // namespace nbp
-
 namespace {
 
 struct Geo {
@@ -1176,10 +1168,7 @@ int nbp_sca_sg_bwd(const void* dh, const float* a, const float* ds, const void* 
 
 size_t nbp_dw_bwd_workspace_floats(int B, int H, int W, int C) {
   const size_t a = (size_t)B * nbp_dw_chunks(B, H, W, C, 1), t = (size_t)B * dw_tiles(H, W);
-  const size_t st = C % 16 == 0 ? (size_t)dw_stream_rows(B, H, W, C) : 0;
-  size_t m = a > t ? a : t;
-  m = m > st ? m : st;
-  return m * 2 * C * 10;
+  return (a > t ? a : t) * 2 * C * 10;
 }
 
 int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, float* dwdw, float* dbdw, float* ws,
@@ -1213,10 +1202,6 @@ int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const voi
   NBP_REQUIRE(dh && a && ds && t2 && t1 && wdw && dt1 && dwdw && dbdw && ws && B > 0 && H > 0 && W > 0,
               "nbp_sca_sg_dw_bwd: bad args");
   NBP_REQUIRE(dw_tiled_ok(C, dtype), "nbp_sca_sg_dw_bwd: C must be a multiple of %d", dtype != 0 ? 16 : 8);
-  // the row-streaming kernel where it applies; NBP_DW_STREAM=0 (read per call): the staged tiles (A/B, bitwise tests)
-  const char* e = getenv("NBP_DW_STREAM");
-  if (!(e && e[0] == '0') && dw_stream_ok(B, H, W, C, dtype))
-    return launch_dw_stream(dh, a, ds, t2, t1, wdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
   return launch_dw_tiled(nullptr, dh, a, ds, t2, t1, wdw, nullptr, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s);
 }
 

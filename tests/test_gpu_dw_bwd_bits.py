@@ -45,9 +45,7 @@ def _hashes(shape, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape,dtype", CASES, ids=[_key(s, d) for s, d in CASES])
-def test_dw_bwd_bits_unchanged(dev, shape, dtype, monkeypatch):
-    # the pins are the staged-tile kernel's (the row-streaming replacement is pinned against it in test_gpu_dw_stream.py)
-    monkeypatch.setenv("NBP_DW_STREAM", "0")
+def test_dw_bwd_bits_unchanged(dev, shape, dtype):
     gold = json.load(open(GOLD))
     assert _hashes(shape, dtype) == gold[_key(shape, dtype)]
 
