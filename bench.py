@@ -91,7 +91,8 @@ ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skin
 SINGLE_KERNEL = ("dw_bwd_32", "wgrad_group", "reduce", "c1dw_bwd_L0")
 UNIT_DEF = {
     "dw_bwd_32": "SURVEY §8(d)-style per pixel: dh C + t2 2C + t1 2C read, dt1 2C written = 7*C*s bytes per pixel "
-                 "(s = storage bytes), x B*H*W pixels of the launch (levels 0-3: the 32-wide tile kernel)",
+                 "(s = storage bytes), x B*H*W pixels of the launch (the 32-wide tile kernel at the levels that store "
+                 "the tape: 2-3 at cfg2; levels 0-1 rebuild it in c1dw_bwd_tile)",
     "wgrad_group": "per grouped launch: each queued problem's operands read once, M*(N+K)*s, + its fp32 dW (+db) "
                    "written once; the split-M fp32 slabs the launch writes instead are `slab_bytes_per_step`",
     "reduce": "per reduce_multi_kernel launch: the fp32 slabs read once + the reduced outputs written once",

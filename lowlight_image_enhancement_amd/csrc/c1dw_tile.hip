@@ -242,32 +242,31 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 // ---------------------------------------------------------------- backward
 // Geometry: a TH x TW (TW 32) tile of dt1 x one 32-gate-channel slice; t1 ring rows k = image row y0 - 2 + k (k 0 ..
 // TH + 3, pixels x0 - 2 .. x0 + TW + 1), dt2 rows i = image row y0 - 1 + i (i 0 .. TH + 1, pixels x0 - 1 .. x0 + TW).
-// One barrier per step j:
-//   A  (MFMA waves) t1 row k = j + 3 into t1 ring slot k % 5 (one step ahead of its first reader)
-//   B  dt1 of dt2-row o = j - 3 (1 <= o <= TH: image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1 (ring slots % 4),
-//      stored
-//   [barrier]
-//   C  dt2 row i = j (i <= TH + 1): t2 = depthwise(t1 rows i .. i + 2) rounded; dg = dh a + ds / HW; dt2 = (dg
-//      t2[partner], dg t2[gate]) rounded into dt2 ring slot i % 4; for the tile's own pixels dW2 += dt2 * window,
-//      db2 += dt2
-// Reads of a row happen only after the barrier that follows its write; a slot is rewritten only after the barrier
-// that follows its last read (5 t1 slots: rows j - 1 .. j + 2 may still be read by slower waves while row j + 3 is
-// written; 4 dt2 slots: rows o - 1 .. o + 1 = j - 4 .. j - 2 are read before the barrier, row j written after it).
-// t1 ring: fp32 (the rounded t1 widened once), quads keyed as the forward's.  dt2 ring: the rounded 16-bit dt2, 80
-// elements (160 B) per pixel, so the four pixels 2 apart that a 32-lane ds_read_b64 group spans start on banks 0 /
-// 16 / 32 / 48.  The conv1 weight slice and bias live in LDS; the n1 rows (MFMA waves) and the dh rows of the next
-// steps in register rings with static slots (the step loop unrolled by the ring depth U: 3 at C 32, 2 at C 64).
+// Step j: barrier(j), then
+//   B  dt1 of dt2-row o = j - 2 (1 <= o <= TH: image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1, stored
+//   C  dt2 row i = j: t2 = depthwise(t1 rows j .. j + 2) rounded; dg = dh a + ds / HW; dt2 = (dg t2[partner], ...)
+//      rounded into the dt2 ring; for the tile's own rows dW2 += dt2 * window, db2 += dt2
+//   A  (MFMA waves) t1 row j + 3
+// Between two barriers the phases touch disjoint slots of the two 4-slot rings: B reads dt2 rows j - 3 .. j - 1
+// (written by C before barrier(j)); C reads t1 rows j .. j + 2 (row j + 2 written by A before barrier(j)) and writes
+// dt2 row j into the slot of row j - 4 (last read by B before barrier(j)); A writes t1 row j + 3 into the slot of row
+// j - 1 (last read by C before barrier(j)).  B and C carry no branch: rows outside the tile are masked (dt2 zeroed,
+// dt1 stores to an out-of-range offset).
+// Both rings hold fp32 quads keyed as the forward's ring (rowring.h): the t1 ring the rounded t1 widened once, the dt2
+// ring the rounded dt2 widened once (no conversions in the dt1 taps).  The conv1 weight slice and bias live in LDS; the
+// n1 rows (MFMA waves) and the dh rows of the next steps in register rings with static slots (the step loop unrolled by
+// the ring depth U: 3 at C 32, 2 at C 64).
 template <typename T, int C>
 __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   constexpr int TH = CT_TH, TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int ROWF = LT * 64;          // floats per t1 ring row
-  constexpr int DP = 80;                 // T elements per dt2 ring pixel (64 + pad)
-  constexpr int ROWD = LD * DP;          // T elements per dt2 ring row
-  constexpr int U = C == 32 ? 3 : 2;     // register-ring slots (n1, dh) = the step loop's unroll
+  constexpr int ROWD = LD * 64;          // floats per dt2 ring row
+  constexpr int U = 2;                   // register-ring slots (n1, dh); the step loop is unrolled by 4 = the LDS
+                                         // rings' depth, so every ring and register slot is a compile-time index
   constexpr int RPB = 256 / (C * 2);     // weight rows per 256-byte LDS bank row (the swizzle key's divisor)
   constexpr int NC = 2 * KS;             // 16-byte chunks per weight row
-  __shared__ __attribute__((aligned(16))) float t1r[5 * ROWF];
-  __shared__ __attribute__((aligned(16))) T dt2r[4 * ROWD];
+  __shared__ __attribute__((aligned(16))) float t1r[4 * ROWF];
+  __shared__ __attribute__((aligned(16))) float dt2r[4 * ROWD];
   __shared__ __attribute__((aligned(16))) T w1s[64 * C];
   __shared__ __attribute__((aligned(16))) float b1s[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -325,11 +324,14 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   lds_barrier();  // weight slice and bias in LDS
 
   // A: t1 ring row k (image row y0 - 2 + k) from register slot S = k % U, which then takes row k + U
-  auto mfma_row = [&](auto slot_c, int k) {
-    constexpr int S = decltype(slot_c)::value;
+  auto mfma_row = [&](auto slot_c, auto ring_c, int k) {
+    constexpr int S = decltype(slot_c)::value;  // k % U
+    constexpr int R = decltype(ring_c)::value;  // k & 3
     const int yy = y0 - 2 + k;
     if (k <= TH + 3) {  // uniform
       const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
+      // the row inside the image and the tile's ring columns x0 - 2 .. x0 + TW + 1 too (uniform): no per-value select
+      const bool interior = yy >= 0 && yy < H && x0 >= 2 && x0 + TW + 2 <= W;
       floatx16 acc[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -345,19 +347,27 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
         }
       const int px = wave * 32 + r;
       if (px < LT) {
-        float* slot = t1r + (k % 5) * ROWF;
+        float* slot = t1r + R * ROWF;
         const int key = qkey<PXT>(px);
+        auto put = [&](auto masked_c) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+          for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
-            const float bq[4] = {bv.x, bv.y, bv.z, bv.w};
-            float v[4];
+            for (int g = 0; g < 4; ++g) {
+              const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
+              const float bq[4] = {bv.x, bv.y, bv.z, bv.w};
+              float v[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = valid ? (float)(T)(acc[t][4 * g + q] + bq[q]) : 0.f;
-            *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = make_float4(v[0], v[1], v[2], v[3]);
-          }
+              for (int q = 0; q < 4; ++q) {
+                v[q] = (float)(T)(acc[t][4 * g + q] + bq[q]);
+                if constexpr (decltype(masked_c)::value) v[q] = valid ? v[q] : 0.f;
+              }
+              *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) =
+                  make_float4(v[0], v[1], v[2], v[3]);
+            }
+        };
+        if (interior) put(std::false_type{});
+        else put(std::true_type{});
       }
     }
     load_n1<T, KS>(rn, img, W, H, yy + U, gxm, lane_ok, hh, fq[S]);  // OOB past the image: zeros, no branch
@@ -365,7 +375,8 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
 
   // C: dt2 of this lane's quad at NP adjacent dt2 ring pixels dp0 .. (image columns x0 - 1 + dp) of dt2 row i, from t1
   // ring rows i .. i + 2; own_row: accumulate the depthwise weight / bias gradients of the tile's own pixels
-  auto dt2_px = [&](auto np_c, auto own_c, int dp0, int i, const vec_t<T, 4>* dv, T* drow, float own) {
+  auto dt2_px = [&](auto np_c, auto own_c, auto ring_c, int dp0, int i, const vec_t<T, 4>* dv, float* drow, float own) {
+    constexpr int RI = decltype(ring_c)::value;  // i & 3
     constexpr int NP = decltype(np_c)::value;
     constexpr bool OWN = decltype(own_c)::value;
     const int yd = y0 - 1 + i;
@@ -379,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     }
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
-      const float* row = t1r + ((i + dy) % 5) * ROWF;
+      const float* row = t1r + ((RI + dy) & 3) * ROWF;
 #pragma unroll
       for (int c = 0; c < NP + 2; ++c) {
         const int px = dp0 + c;  // t1 ring pixel (image column x0 - 2 + px)
@@ -403,18 +414,17 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       const float4 other = swap32(mine, hh);  // the partner quad's rounded t2 (lane ^ 32)
       const float oth[4] = {other.x, other.y, other.z, other.w};
       const float av[4] = {ak.x, ak.y, ak.z, ak.w}, sv[4] = {sk.x, sk.y, sk.z, sk.w};
-      vec_t<T, 4> d2;
+      float d2[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float dg = fmaf((float)dv[j][e], av[e], sv[e]);
         float pr = dg * oth[e];
         asm volatile("" : "+v"(pr));  // the fp32 product is what is rounded (the fused depthwise backward's convention)
-        d2[e] = inside ? (T)pr : (T)0.f;
+        d2[e] = inside ? (float)(T)pr : 0.f;
       }
-      const int hk = (dp >> 1) & 1;  // half swap: see the ring geometry above
-      *reinterpret_cast<vec_t<T, 4>*>(drow + dp * DP + (hk ^ hh) * 32 + 4 * (lane & 7)) = d2;
+      *reinterpret_cast<float4*>(drow + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4) = make_float4(d2[0], d2[1], d2[2], d2[3]);
       if constexpr (OWN) {  // own (uniform 0 / 1): the dt2 row is one of the tile's; d2 is 0 outside the image
-        const f2v l0 = f2v{(float)d2[0], (float)d2[1]} * own, l1 = f2v{(float)d2[2], (float)d2[3]} * own;
+        const f2v l0 = f2v{d2[0], d2[1]} * own, l1 = f2v{d2[2], d2[3]} * own;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
           aw[t][0] = __builtin_elementwise_fma(l0, xw[t / 3][j + t % 3][0], aw[t][0]);
@@ -426,13 +436,9 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     }
   };
 
-  // step j: barrier(j); B(j + 1); C(j); A(j + 1).  Between two barriers the three phases touch disjoint ring slots (B:
-  // dt2 rows j - 3 .. j - 1, complete before barrier(j); C: t1 rows j .. j + 2, written by A(j - 1) before barrier(j),
-  // and dt2 row j into the slot of row j - 4, last read by B(j); A: t1 row j + 4 into the slot of row j - 1, last read
-  // by C(j - 1)), and B / C carry no branch, so the scheduler can overlap them; rows outside the tile are masked
-  // (dt2 zeroed, dt1 stores to an out-of-range offset)
+  // step j (see the geometry above): barrier(j); B: dt1 of dt2-row j - 2; C: dt2 row j; A: t1 row j + 3
   auto step = [&](auto j_c, int j) {
-    constexpr int J = decltype(j_c)::value;  // j = U m + J: the dh slot of dt2 row j
+    constexpr int J = decltype(j_c)::value;  // j = 4 m + J: ring slot of dt2 row j; dh register slot J % U
     __builtin_amdgcn_sched_barrier(0);       // no scheduling across steps (it hoists later steps' loads: spills)
     lds_barrier();
     // B: dt1 of dt2-row o = j - 2 (image row y0 - 1 + o) from dt2 rows o - 1 .. o + 1
@@ -444,15 +450,14 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       for (int jj = 0; jj < PXT; ++jj) acc[jj][0] = acc[jj][1] = f2v{0.f, 0.f};
 #pragma unroll
       for (int dhh = -1; dhh <= 1; ++dhh) {
-        const T* dr = dt2r + ((o - dhh) & 3) * ROWD;  // tap (dhh, dww) reads dt2 row o - dhh at ring pixel p + 1 - dww
+        const float* dr = dt2r + ((J + 2 - dhh) & 3) * ROWD;  // tap (dhh, dww): dt2 row o - dhh, ring pixel p + 1 - dww
         f2v gw[PXT + 2][2];
 #pragma unroll
         for (int c = 0; c < PXT + 2; ++c) {
           const int dp = xl + c;
-          const vec_t<T, 4> v = *reinterpret_cast<const vec_t<T, 4>*>(dr + dp * DP + ((((dp >> 1) & 1) ^ hh) * 32) +
-                                                                      4 * (lane & 7));
-          gw[c][0] = f2v{(float)v[0], (float)v[1]};
-          gw[c][1] = f2v{(float)v[2], (float)v[3]};
+          const float4 v = *reinterpret_cast<const float4*>(dr + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4);
+          gw[c][0] = f2v{v.x, v.y};
+          gw[c][1] = f2v{v.z, v.w};
         }
 #pragma unroll
         for (int jj = 0; jj < PXT; ++jj)
@@ -472,33 +477,34 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     // C: dt2 row i = j
     {
       const int i = j, yd = y0 - 1 + i;
-      T* drow = dt2r + (i & 3) * ROWD;
-      dt2_px(IC<PXT>{}, std::true_type{}, xl + 1, i, dq[J], drow, i >= 1 && i <= TH ? 1.f : 0.f);
-      if (has_halo) dt2_px(IC<1>{}, std::true_type{}, dph, i, &dqh[J], drow, 0.f);
+      float* drow = dt2r + J * ROWD;
+      dt2_px(IC<PXT>{}, std::true_type{}, IC<J>{}, xl + 1, i, dq[J % U], drow, i >= 1 && i <= TH ? 1.f : 0.f);
+      if (has_halo) dt2_px(IC<1>{}, std::true_type{}, IC<J>{}, dph, i, &dqh[J % U], drow, 0.f);  // (false: spills)
 #pragma unroll
-      for (int jj = 0; jj < PXT; ++jj) dq[J][jj] = bload4<T>(rh, dh_off(yd + U, x0 + xl + jj, true));
-      dqh[J] = bload4<T>(rh, dh_off(yd + U, x0 - 1 + dph, has_halo));
+      for (int jj = 0; jj < PXT; ++jj) dq[J % U][jj] = bload4<T>(rh, dh_off(yd + U, x0 + xl + jj, true));
+      dqh[J % U] = bload4<T>(rh, dh_off(yd + U, x0 - 1 + dph, has_halo));
     }
-    // A: t1 ring row j + 4 (register slot (j + 4) % U)
-    if (mfma_wave) mfma_row(IC<(J + 4) % U>{}, j + 4);
+    // A: t1 ring row j + 3 (register slot (j + 3) % U)
+    if (mfma_wave) mfma_row(IC<(J + 3) % U>{}, IC<(J + 3) & 3>{}, j + 3);
   };
 
-  if (mfma_wave) {  // t1 ring rows 0 .. 3 (register slots k % U)
-    mfma_row(IC<0>{}, 0);
-    mfma_row(IC<1 % U>{}, 1);
-    mfma_row(IC<2 % U>{}, 2);
-    mfma_row(IC<3 % U>{}, 3);
+  if (mfma_wave) {  // t1 ring rows 0 .. 2 (register slots k % U)
+    mfma_row(IC<0>{}, IC<0>{}, 0);
+    mfma_row(IC<1 % U>{}, IC<1>{}, 1);
+    mfma_row(IC<2 % U>{}, IC<2>{}, 2);
   }
-  static_assert(U == 2 || U == 3, "ring depth");
+  static_assert(U == 2, "register ring depth (divides the unroll of 4)");
   constexpr int NS = TH + 3;  // steps j = 0 .. TH + 2: C(j) to dt2 row TH + 1, B(j + 1) to dt1 row TH
 #pragma unroll 1
-  for (int j = 0; j < NS - NS % U; j += U) {
+  for (int j = 0; j < NS - NS % 4; j += 4) {
     step(IC<0>{}, j);
     step(IC<1>{}, j + 1);
-    if constexpr (U == 3) step(IC<2>{}, j + 2);
+    step(IC<2>{}, j + 2);
+    step(IC<3>{}, j + 3);
   }
-  if constexpr (NS % U >= 1) step(IC<0>{}, NS - NS % U);
-  if constexpr (NS % U >= 2) step(IC<1>{}, NS - NS % U + 1);
+  if constexpr (NS % 4 >= 1) step(IC<0>{}, NS - NS % 4);
+  if constexpr (NS % 4 >= 2) step(IC<1>{}, NS - NS % 4 + 1);
+  if constexpr (NS % 4 >= 3) step(IC<2>{}, NS - NS % 4 + 2);
   // ---- the tile's depthwise weight / bias gradients: 40 values per lane, summed over the lanes of one quad (lane bits
   // 3..4: a reduce-scatter, 40 -> 20 -> 10 values per lane), then over the 4 waves in order
   float v[40];

@@ -117,11 +117,11 @@ class NAFNet(nn.Module):
         # keeps t1 / t2 on chip (nbp_c1dw_fwd_tile), and the mirror backward that rebuilds them from n1
         # (nbp_c1dw_bwd_tile): the 2C-wide tape never reaches HBM
         self.fuse_c1dw_tile = True
-        # the levels (by channel count) that take it: none by default.  The rebuild costs the backward ~1.3x the
-        # stored-tape kernel's VALU work (t1 epilogue + t2 recomputed: 213 vs 147 us at level 0), which the forward's
-        # saved tape traffic (58 vs 107 us) only repays in the eager level time; the graph step measured 1306-1314
-        # img/s without it, 1303-1306 with it at levels 0 / 1
-        self.c1dw_tile_channels = ()
+        # the levels (by channel count) that take it: 0 and 1.  The rebuild costs the backward more VALU work than the
+        # stored-tape kernel (t1 epilogue + t2 recomputed: 172 vs 150 us at level 0, 102 vs 73 at level 1), which the
+        # forward's saved tape traffic repays (58 vs 109 us, 49 vs 57): graph step +1.1 % with both levels, +0.7 / +0.3 %
+        # with level 0 / 1 alone
+        self.c1dw_tile_channels = (32, 64)
         self._ln_carry = None
         # "fp32": fp32 operands everywhere (parity mode); "fp16" / "bf16": 16-bit activation storage and MFMA operands
         # with fp32 accumulation, statistics, parameters and gradients (fp16 = the reference's AMP autocast dtype,
