@@ -519,7 +519,9 @@ def main():
     # NBP_BENCH_REHEARSE=1 (one-GPU box only, never the measurement): every rank on cuda:0 over gloo, to exercise the
     # N > 1 path (graph segments + bucket all-reduces, barriers, max-over-ranks timing) where RCCL needs one GPU per rank
     rehearse = os.environ.get("NBP_BENCH_REHEARSE") == "1"
-    # device_count() does not initialise the GPU on this image: the parent of spawned ranks never touches it
+    # counting devices does not initialise the GPU on this image (its documented behaviour; the parent of spawned ranks
+    # makes no other GPU call and starts its ranks as child processes, no exec; success path recorded in
+    # profiles/r05_rehearsal/)
     how, world = plan_launch(args.gpus, os.environ, torch.cuda.device_count(), rehearse)
     if how == "spawn":
         sys.exit(spawn_ranks(world, sys.argv[1:]))

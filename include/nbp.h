@@ -315,7 +315,8 @@ int nbp_pix_loss_bwd(const float* a, const float* b, long n, int mode, float eps
  * clamp((1 - ssim) / 2, 0, 1) reduced by `reduction` 0 = 'mean' (loss[0]), 1 = 'sum' (loss[0]) or 2 = 'none' (lmap
  * [N][C][H][W]; loss may be null).  want_grad keeps the gradient coefficients in ws for nbp_ssim_loss_bwd, which writes
  * gx = d/dx: scaled by up[0] (mean / sum) or, with up_map (reduction 'none'), by the per-pixel upstream map.  The map
- * is symmetric in (x, y): d/dy is the same pair of calls with x and y swapped. */
+ * is symmetric in (x, y): d/dy is the same pair of calls with x and y swapped.  With want_grad = 1, loss and lmap may
+ * both be null: the call then only fills ws (the d/dy coefficients of that swapped call, no reduction, no map). */
 size_t nbp_ssim_workspace_floats(long n);
 int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W, int window, float max_val,
                       int clamp_in, int want_grad, int reduction, float* ws, float* loss, float* lmap, nbp_stream_t s);

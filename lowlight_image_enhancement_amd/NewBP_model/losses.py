@@ -81,7 +81,7 @@ _SSIM_REDUCTION = {"mean": 0, "sum": 1, "none": 2}
 class _SSIMLossFn(torch.autograd.Function):
     """kornia 0.6.12 ssim_loss: clamp((1 - ssim(x, y)) / 2, 0, 1) reduced by 'mean' / 'sum' / 'none' (the map).  The
     map is symmetric in (x, y), so d/dy is the kernel pair with the inputs swapped (a second forward, made only when
-    y needs a gradient)."""
+    y needs a gradient, that writes the coefficients only: no loss, no map)."""
 
     @staticmethod
     def forward(ctx, x, y, window, max_val, clamp_in, reduction):
@@ -99,9 +99,7 @@ class _SSIMLossFn(torch.autograd.Function):
         call("ssim_loss_fwd", x, y, N, C, H, W, window, float(max_val), clamp_in, int(want_x), red, wsx, loss, lmap)
         if want_y:
             wsy = torch.empty(query("ssim_workspace_floats", x.numel()), device=x.device)
-            tmp = torch.empty((), device=x.device) if red != 2 else torch.empty_like(x)
-            call("ssim_loss_fwd", y, x, N, C, H, W, window, float(max_val), clamp_in, 1, red, wsy,
-                 tmp if red != 2 else None, tmp if red == 2 else None)
+            call("ssim_loss_fwd", y, x, N, C, H, W, window, float(max_val), clamp_in, 1, red, wsy, None, None)
         ctx.save_for_backward(x, y, wsx, wsy)
         ctx.clamp_in, ctx.red = clamp_in, red
         return loss if red != 2 else lmap

@@ -355,12 +355,12 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
-              const float bq[4] = {bv.x, bv.y, bv.z, bv.w};
-              float v[4];
+              const f2v lo = round2<T>(f2v{acc[t][4 * g], acc[t][4 * g + 1]} + f2v{bv.x, bv.y});
+              const f2v hi = round2<T>(f2v{acc[t][4 * g + 2], acc[t][4 * g + 3]} + f2v{bv.z, bv.w});
+              float v[4] = {lo.x, lo.y, hi.x, hi.y};
+              if constexpr (decltype(masked_c)::value) {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                v[q] = (float)(T)(acc[t][4 * g + q] + bq[q]);
-                if constexpr (decltype(masked_c)::value) v[q] = valid ? v[q] : 0.f;
+                for (int q = 0; q < 4; ++q) v[q] = valid ? v[q] : 0.f;
               }
               *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) =
                   make_float4(v[0], v[1], v[2], v[3]);
@@ -409,19 +409,20 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     for (int j = 0; j < NP; ++j) {
       const int dp = dp0 + j, gx = x0 - 1 + dp;
       const bool inside = row_in && gx >= 0 && gx < W;
-      const float4 tm = f4of(a2[j]);
-      const float4 mine = make_float4((float)(T)tm.x, (float)(T)tm.y, (float)(T)tm.z, (float)(T)tm.w);  // t2 rounded
+      const f2v m0 = round2<T>(a2[j][0]), m1 = round2<T>(a2[j][1]);
+      const float4 mine = make_float4(m0.x, m0.y, m1.x, m1.y);  // t2 rounded
       const float4 other = swap32(mine, hh);  // the partner quad's rounded t2 (lane ^ 32)
       const float oth[4] = {other.x, other.y, other.z, other.w};
       const float av[4] = {ak.x, ak.y, ak.z, ak.w}, sv[4] = {sk.x, sk.y, sk.z, sk.w};
-      float d2[4];
+      float pr[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float dg = fmaf((float)dv[j][e], av[e], sv[e]);
-        float pr = dg * oth[e];
-        asm volatile("" : "+v"(pr));  // the fp32 product is what is rounded (the fused depthwise backward's convention)
-        d2[e] = inside ? (float)(T)pr : 0.f;
+        pr[e] = dg * oth[e];
+        asm volatile("" : "+v"(pr[e]));  // the fp32 product is what is rounded (the fused depthwise backward's convention)
       }
+      const f2v r0 = round2<T>(f2v{pr[0], pr[1]}), r1 = round2<T>(f2v{pr[2], pr[3]});
+      const float d2[4] = {inside ? r0.x : 0.f, inside ? r0.y : 0.f, inside ? r1.x : 0.f, inside ? r1.y : 0.f};
       *reinterpret_cast<float4*>(drow + (dp * 16 + (q16 ^ qkey<PXT>(dp))) * 4) = make_float4(d2[0], d2[1], d2[2], d2[3]);
       if constexpr (OWN) {  // own (uniform 0 / 1): the dt2 row is one of the tile's; d2 is 0 outside the image
         const f2v l0 = f2v{d2[0], d2[1]} * own, l1 = f2v{d2[2], d2[3]} * own;

@@ -461,7 +461,8 @@ size_t nbp_ssim_workspace_floats(long n) { return (size_t)5 * n + 4; }
 int nbp_ssim_loss_fwd(const float* x, const float* y, int N, int C, int H, int W, int window, float max_val,
                       int clamp_in, int want_grad, int reduction, float* ws, float* loss, float* lmap, nbp_stream_t s) {
   NBP_REQUIRE(x && y && ws && N > 0 && C > 0 && reduction >= 0 && reduction <= 2, "nbp_ssim_loss_fwd: bad args");
-  NBP_REQUIRE(reduction == 2 ? lmap != nullptr : loss != nullptr, "nbp_ssim_loss_fwd: output missing for the reduction");
+  NBP_REQUIRE((reduction == 2 ? lmap != nullptr : loss != nullptr) || (want_grad && !loss && !lmap),
+              "nbp_ssim_loss_fwd: output missing for the reduction");
   NBP_REQUIRE(window == 11, "nbp_ssim_loss_fwd: only the 11-tap window (SSIMLoss default) is implemented");
   NBP_REQUIRE(H > 5 && W > 5, "nbp_ssim_loss_fwd: reflect padding needs H, W > 5");
   NBP_REQUIRE((long)N * C <= 65535, "nbp_ssim_loss_fwd: N*C <= 65535 planes");

@@ -82,5 +82,13 @@ __device__ __forceinline__ float4 swap32(float4 v, bool upper) {
 template <int V>
 using IC = std::integral_constant<int, V>;
 
+// two fp32 values rounded to the storage type and widened back (v_cvt_pk_{f16,bf16}_f32: round to nearest even, the
+// scalar conversion's rounding, two values per instruction)
+template <typename T>
+__device__ __forceinline__ f2v round2(f2v v) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_convertvector(__builtin_convertvector(v, t2), f2v);
+}
+
 }  // namespace
 }  // namespace nbp
