@@ -140,16 +140,22 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
     if (px < LW) {
       float* slot = ring + (k & 3) * ROWF;
       const int key = qkey<PXT>(px);
+      // the row inside the image and the tile's ring columns x0 - 1 .. x0 + TW too (uniform): no per-value select
+      const bool interior = yy >= 0 && yy < H && x0 >= 1 && x0 + TW + 1 <= W;
+      auto put = [&](auto masked_c) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          vec_t<T, 4> o;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = (T)(acc[t][4 * g + q] + cw.bias[t][g][q]);
-          const float4 v = valid ? make_float4((float)o[0], (float)o[1], (float)o[2], (float)o[3]) : f4(0.f);
-          *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = v;
-        }
+          for (int g = 0; g < 4; ++g) {
+            const f2v lo = round2<T>(f2v{acc[t][4 * g], acc[t][4 * g + 1]} + f2v{cw.bias[t][g][0], cw.bias[t][g][1]});
+            const f2v hi = round2<T>(f2v{acc[t][4 * g + 2], acc[t][4 * g + 3]} + f2v{cw.bias[t][g][2], cw.bias[t][g][3]});
+            float4 v = make_float4(lo.x, lo.y, hi.x, hi.y);
+            if constexpr (decltype(masked_c)::value) v = valid ? v : f4(0.f);
+            *reinterpret_cast<float4*>(slot + (px * 16 + ((8 * t + 2 * g + hh) ^ key)) * 4) = v;
+          }
+      };
+      if (interior) put(std::false_type{});
+      else put(std::true_type{});
     }
     if constexpr (KEEP) {
 #pragma unroll
