@@ -443,6 +443,50 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     }
   };
 
+  // the halo dt2 pixel of waves 2 / 3 (ring pixel dph of dt2 row i): t2, the partner's t2, dt2 into the ring; no
+  // weight-gradient terms (it is not one of the tile's pixels)
+  auto halo_dt2 = [&](auto ring_c, int i, const vec_t<T, 4>& dv, float* drow) {
+    constexpr int RI = decltype(ring_c)::value;  // i & 3
+    const int yd = y0 - 1 + i, gx = x0 - 1 + dph;
+    const bool inside = yd >= 0 && yd < H && i <= TH + 1 && gx >= 0 && gx < W;
+    f2v a0 = f2v{dw.b.x, dw.b.y}, a1 = f2v{dw.b.z, dw.b.w};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float* row = t1r + ((RI + dy) & 3) * ROWF;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int px = dph + dx;
+        const float4 v = *reinterpret_cast<const float4*>(row + (px * 16 + (q16 ^ qkey<PXT>(px))) * 4);
+        a0 = __builtin_elementwise_fma(dw.w[dy * 3 + dx][0], f2v{v.x, v.y}, a0);
+        a1 = __builtin_elementwise_fma(dw.w[dy * 3 + dx][1], f2v{v.z, v.w}, a1);
+      }
+    }
+    const f2v m0 = round2<T>(a0), m1 = round2<T>(a1);
+    const float4 other = swap32(make_float4(m0.x, m0.y, m1.x, m1.y), hh);
+    const float oth[4] = {other.x, other.y, other.z, other.w};
+    const float av[4] = {ak.x, ak.y, ak.z, ak.w}, sv[4] = {sk.x, sk.y, sk.z, sk.w};
+    float pr[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      pr[e] = fmaf((float)dv[e], av[e], sv[e]) * oth[e];
+      asm volatile("" : "+v"(pr[e]));
+    }
+    const f2v r0 = round2<T>(f2v{pr[0], pr[1]}), r1 = round2<T>(f2v{pr[2], pr[3]});
+    *reinterpret_cast<float4*>(drow + (dph * 16 + (q16 ^ qkey<PXT>(dph))) * 4) =
+        inside ? make_float4(r0.x, r0.y, r1.x, r1.y) : f4(0.f);
+    // the weight-gradient partials pass through this branch untouched; naming them here (no instruction) keeps the
+    // register allocation of the unconditional path (without it the compiler spills 250+ VGPRs)
+#pragma unroll
+    for (int t = 0; t < 10; ++t)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        f2v v = t < 9 ? aw[t][e] : db[e];
+        asm volatile("" : "+v"(v));
+        if (t < 9) aw[t][e] = v;
+        else db[e] = v;
+      }
+  };
+
   // step j (see the geometry above): barrier(j); B: dt1 of dt2-row j - 2; C: dt2 row j; A: t1 row j + 3
   auto step = [&](auto j_c, int j) {
     constexpr int J = decltype(j_c)::value;  // j = 4 m + J: ring slot of dt2 row j; dh register slot J % U
@@ -486,7 +530,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       const int i = j, yd = y0 - 1 + i;
       float* drow = dt2r + J * ROWD;
       dt2_px(IC<PXT>{}, std::true_type{}, IC<J>{}, xl + 1, i, dq[J % U], drow, i >= 1 && i <= TH ? 1.f : 0.f);
-      if (has_halo) dt2_px(IC<1>{}, std::true_type{}, IC<J>{}, dph, i, &dqh[J % U], drow, 0.f);  // (false: spills)
+      if (has_halo) halo_dt2(IC<J>{}, i, dqh[J % U], drow);
 #pragma unroll
       for (int jj = 0; jj < PXT; ++jj) dq[J % U][jj] = bload4<T>(rh, dh_off(yd + U, x0 + xl + jj, true));
       dqh[J % U] = bload4<T>(rh, dh_off(yd + U, x0 - 1 + dph, has_halo));
