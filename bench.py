@@ -174,6 +174,12 @@ def cost_sg_rc_wg(a):  # cost_sg_rc + the folded weight gradients U = dout^T g, 
     return fl + 2.0 * M * N * N + 2.0 * M * 2 * N * K, by
 
 
+def cost_dgrad_ln_wg(a):  # cost_dgrad_ln + the folded conv1 weight gradient dW1 = dt1^T n1 (n1 rebuilt, not read)
+    fl, by = cost_dgrad_ln(a)
+    M, N, K = a[4], a[5], a[6]
+    return fl + 2.0 * M * N * K, by
+
+
 def cost_c1dw(a):  # (n1,w1,b1,wdw,bdw,t1,t2,g,pool,B,h,w,c,dt): n1 C in, t1 2C (+ t2 2C) + g C out, conv1 weight
     M, c = a[9] * a[10] * a[11], a[12]
     by = (M * c + 2 * M * c + (2 * M * c if a[6] is not None else 0) + M * c + 2 * c * c) * _e(a[13])
@@ -259,7 +265,8 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "gemm_f32": rec_plain("gemm_f32", cost_gemm_f32), "wgrad_f32": rec_wgrad, "wgrad_group": rec_wgroup,
            "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_dw_bwd,
            "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd), "gemm_ffn": rec_plain("gemm16", cost_ffn),
-           "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
+           "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg),
+           "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
            "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile), "c1dw_bwd_tile": rec_c1dw_bwd}
 
 
@@ -387,6 +394,8 @@ def make_trainer(dev, workload, precision, seed=0):
     tc = os.environ.get("NBP_C1DW_TILE_C")  # A/B experiments only: the levels (channel counts) on the tile path
     if tc is not None:
         net.c1dw_tile_channels = tuple(int(c) for c in tc.split(",") if c)
+    if os.environ.get("NBP_LN_WG") == "0":  # A/B only: the separate level-0 conv1 weight-gradient launch
+        net.ln_wg = False
     return NBPTrainer(net, psf_mode="rgb", psf_spec=spec, **wl["w"]), init_sd
 
 

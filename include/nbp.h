@@ -125,6 +125,16 @@ size_t nbp_dgrad_ln_workspace_floats(long M, int N);
 int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
                      const float* stats, const float* lnw, const void* dres, void* dx, float* dlnw, float* dlnb,
                      float* ws, size_t ws_floats, int dtype, nbp_stream_t s);
+/* nbp_dgrad_ln_bwd plus conv1's weight gradient from the same tiles (level 0: N = C = 32, K = 2C = 64; the separate
+ * nbp_wgrad_f32 launch and its re-read of dt / n1 disappear): dW = A^T n1 [K][N], db = colsum A [K], with n1 = lnw yhat
+ * + lnb rebuilt from x / stats exactly as nbp_ln_fwd_nhwc (and the nbp_gemm_res_ln / nbp_gemm_ffn epilogues) stored
+ * it.  Block partials in ws (nbp_dgrad_ln_bwd_wg_workspace_floats), reduced like nbp_wgrad_f32's slabs (deferred with
+ * the stage).  dx, dlnw, dlnb as nbp_dgrad_ln_bwd (dx bit for bit).  Reference: NAFNet_arch.py:60-64 (norm1 -> conv1),
+ * whose conv1 weight gradient torch autograd computes in a separate pass. */
+size_t nbp_dgrad_ln_bwd_wg_workspace_floats(long M, int N);
+int nbp_dgrad_ln_bwd_wg(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
+                        const float* stats, const float* lnw, const float* lnb, const void* dres, void* dx, float* dlnw,
+                        float* dlnb, float* dW, float* db, float* ws, size_t ws_floats, int dtype, nbp_stream_t s);
 /* NAFBlock conv3 / conv5 (N = C in {32, 64} on the skinny kernel with K <= 128, or 128 on 64 x 128 tiles; bf16) with
  * the next LayerNorm2d forward in the epilogue:
  * C = R + rscale * (A W^T + bias) (the block's y / out, NAFNet_arch.py:70-78) and nout / stats = LN(C) exactly as

@@ -891,8 +891,12 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   static_assert(!FFN || (NT == 1 && KS == 2), "FFN fusion: the level-0 block (N = K = 32)");
   constexpr bool RESLN = CMODE == CM_RESLN || FFN;
   constexpr bool RC = CMODE == CM_SGBWD_RC;
-  static_assert(!WGF || (RC && NT == 1 && KS == 2), "weight-gradient fold: level-0 conv5 dgrad (N = K = 32)");
-  constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : 8;  // bf16 row stride of the recomputed gate-input tile
+  constexpr bool WGR = WGF && RC;                 // conv5's U / V + conv4's dW / db (nbp_dgrad_sg_rc_wg)
+  constexpr bool WG1 = WGF && CMODE == CM_LNBWD;  // conv1's dW / db (nbp_dgrad_ln_bwd_wg)
+  static_assert(!WGF || (WGR && NT == 1 && KS == 2) || (WG1 && NT == 1 && KS == 4),
+                "weight-gradient folds: level-0 conv5 dgrad (N = K = 32), level-0 conv1 dgrad (N = 32, K = 64)");
+  // bf16 row stride of the recomputed gate-input tile (RC) / of the rebuilt n1 tile (WG1)
+  constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : (WG1 ? 32 : 8);
   __shared__ float stage[4][32 * LDT];
   __shared__ __attribute__((aligned(16))) H stage2[4][32 * LDT2];
   // WGF: the tile's dt (32 rows x 64, 192-byte rows: conflict-free ds_read_b64_tr_b16), later the block's reduction
@@ -964,6 +968,10 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   if (CMODE == CM_LNBWD) {  // rsc holds the LN weight of this lane's 8 columns
     const float4 s0 = ld4(p.lnw + ccol), s1 = ld4(p.lnw + ccol + 4);
     rsc[0] = s0.x; rsc[1] = s0.y; rsc[2] = s0.z; rsc[3] = s0.w; rsc[4] = s1.x; rsc[5] = s1.y; rsc[6] = s1.z; rsc[7] = s1.w;
+    if (WG1) {  // bia holds the LN bias (n1 = lnw yhat + lnb rebuilt for the conv1 weight gradient)
+      const float4 b0 = ld4(p.lnb_f + ccol), b1 = ld4(p.lnb_f + ccol + 4);
+      bia[0] = b0.x; bia[1] = b0.y; bia[2] = b0.z; bia[3] = b0.w; bia[4] = b1.x; bia[5] = b1.y; bia[6] = b1.z; bia[7] = b1.w;
+    }
   } else if (CMODE != CM_SGBWD && !RC) {
     if (p.bias) {
       const float4 b0 = ld4(p.bias + ccol), b1 = ld4(p.bias + ccol + 4);
@@ -1132,7 +1140,16 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
       for (int q = 0; q < NPL; ++q) {
         const int rr = lane / cpr + q * rstep;
         const long m = m0 + rr;
-        if (m >= M) break;
+        if (m >= M) {
+          if constexpr (WG1) {  // the fold's n1 tile: zero rows past M (their dt1 rows are zero, stale data could be NaN)
+            vec_t<H, 8> z;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) z[j] = (H)0.f;
+            *reinterpret_cast<vec_t<H, 8>*>(tileT + rr * LDT2 + ccol) = z;
+            continue;
+          }
+          break;
+        }
         const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
         const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
         const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
@@ -1148,6 +1165,12 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
           aw[j] = fmaf(v[j], yh[j], aw[j]);
           ab[j] += v[j];
         }
+        if constexpr (WG1) {  // n1 exactly as the forward LayerNorm stored it (nbp_ln_fwd_nhwc / the RESLN epilogue)
+          vec_t<H, 8> nn;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) nn[j] = (H)fmaf(rsc[j], yh[j], bia[j]);
+          *reinterpret_cast<vec_t<H, 8>*>(tileT + rr * LDT2 + ccol) = nn;
+        }
         sg = group_sum<G>(sg);
         sgy = group_sum<G>(sgy);
         const float mg = sg / (float)N, mgy = sgy / (float)N;
@@ -1160,7 +1183,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
     for (int rr = lane / cpr; !PRE && rr < 32; rr += rstep) {
       const long m = m0 + rr;
       if (m >= M) {
-        if constexpr (WGF) {  // the fold's dt tile: zero rows past M (their n2 rows are zero, stale data could be NaN)
+        if constexpr (WGR) {  // the fold's dt tile: zero rows past M (their n2 rows are zero, stale data could be NaN)
           vec_t<H, 8> z;
 #pragma unroll
           for (int j = 0; j < 8; ++j) z[j] = (H)0.f;
@@ -1182,7 +1205,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
           o[2 * j + 1] = (H)(d[j] * (float)tv[2 * j]);
         }
         *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
-        if constexpr (WGF) {
+        if constexpr (WGR) {
           *reinterpret_cast<vec_t<H, 8>*>(stage3[threadIdx.x >> 6] + rr * 96 + ccol) = o;
 #pragma unroll
           for (int j = 0; j < 8; ++j) ab[j] += (float)o[j];  // db2 partial of this lane's 8 columns
@@ -1265,7 +1288,41 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-    if constexpr (WGF) {
+    if constexpr (WG1) {
+      // stage dt1 (this GEMM's A) next to the rebuilt n1 tile, then accumulate dW1 += dt1^T n1 over the tile's 32 rows
+      // with transposed fragment reads (WGR's dW2 pattern; rows past M are zero in both tiles)
+      H* st = stage3[threadIdx.x >> 6];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        *reinterpret_cast<vec_t<H, 8>*>(st + r * 96 + ks * 16 + 8 * h) = a0[ks];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vsum[ks][e] += (float)a0[ks][e];  // db1 partial
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int grp = lane >> 4, gq = (lane & 15) >> 2, pp = lane & 3;
+      const int fcol = 16 * (grp & 1) + 4 * pp;
+#pragma unroll
+      for (int ks = 0; ks < 32; ks += 16) {
+        vec_t<H, 8> fa[2], fn;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int row = ks + 8 * h + 4 * tt + gq;
+          const vec_t<H, 4> a0v = ds_read_tr16<H>(st + row * 96 + fcol);
+          const vec_t<H, 4> a1v = ds_read_tr16<H>(st + row * 96 + 32 + fcol);
+          const vec_t<H, 4> nv = ds_read_tr16<H>(tileT + row * LDT2 + fcol);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            fa[0][4 * tt + e] = a0v[e];
+            fa[1][4 * tt + e] = a1v[e];
+            fn[4 * tt + e] = nv[e];
+          }
+        }
+        accw[0] = mfma32x32x16(fa[0], fn, accw[0]);
+        accw[1] = mfma32x32x16(fa[1], fn, accw[1]);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (WGR) {
       // stage dout (this GEMM's A) and n2 (A2) in the dead fp32 tile, g in the dead t tile (32-element rows), then
       // accumulate U += dout^T g and dW2 += dt^T n2 over the tile's 32 rows with transposed fragment reads
       H* sd = reinterpret_cast<H*>(tileS);
@@ -1318,7 +1375,47 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) c0[ks] = c1[ks];
   }
-  if constexpr (WGF) {
+  if constexpr (WG1) {
+    // block partials, waves combined in fixed order through stage3 (as fp32): [0, 2048) dW1 (row n = dt1 column,
+    // col k = n1 channel), [2048, 2112) db1
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) vsum[ks][e] += __shfl_xor(vsum[ks][e], o, 64);  // lanes sharing h
+    float* red = reinterpret_cast<float*>(&stage3[0][0]);
+    const int wv = threadIdx.x >> 6;
+    for (int w = 0; w < 4; ++w) {
+      __syncthreads();
+      if (wv == w) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int rr = 0; rr < 16; ++rr) {
+            const int n = i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * h, k = r;
+            float* d = red + n * 32 + k;
+            *d = (w == 0 ? 0.f : *d) + accw[i][rr];
+          }
+        if (r == 0)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float* d = red + 2048 + ks * 16 + 8 * h + e;
+              *d = (w == 0 ? 0.f : *d) + vsum[ks][e];
+            }
+      }
+    }
+    __syncthreads();
+    const long bb = blockIdx.x;
+    for (int i = threadIdx.x; i < 2112; i += blockDim.x) {
+      const float v = red[i];
+      if (i < 2048) p.slab_w2[bb * 2048 + i] = v;
+      else p.slab_b2[bb * 64 + i - 2048] = v;
+    }
+  }
+  if constexpr (WGR) {
     // block partials, waves combined in fixed order through stage3 (as fp32): [0, 2048) dW2 (row n = dt column, col k =
     // n2 channel), [2048, 3072) U, [3072, 3136) db2, [3136, 3168) V
 #pragma unroll

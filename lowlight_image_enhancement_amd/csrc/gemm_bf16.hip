@@ -97,6 +97,40 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
   return nbp_reduce_slab(slab_b, (int)nb, N, dlnb, s);
 }
 
+size_t nbp_dgrad_ln_bwd_wg_workspace_floats(long M, int N) {
+  return N == 32 ? (size_t)skinny_blocks(M) * (2 * N + 2048 + 64) : 0;
+}
+
+int nbp_dgrad_ln_bwd_wg(const void* A, long lda, const void* Wt, long ldb, int M, int N, int K, const void* x,
+                        const float* stats, const float* lnw, const float* lnb, const void* dres, void* dx, float* dlnw,
+                        float* dlnb, float* dW, float* db, float* ws, size_t ws_floats, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(A && Wt && x && stats && lnw && lnb && dres && dx && dlnw && dlnb && dW && db && ws && M > 0,
+              "nbp_dgrad_ln_bwd_wg: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_ln_bwd_wg: 16-bit storage (dtype 1 bf16 / 2 fp16)");
+  NBP_REQUIRE(N == 32 && K == 64 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_ln_bwd_wg: N = 32, K = 64 (N=%d K=%d)", N, K);
+  const long nb = skinny_blocks(M);
+  NBP_REQUIRE(ws_floats >= nbp_dgrad_ln_bwd_wg_workspace_floats(M, N), "nbp_dgrad_ln_bwd_wg: workspace too small");
+  float* slab_w = ws;
+  float* slab_b = slab_w + nb * N;
+  float* sw = slab_b + nb * N;
+  float* sb = sw + nb * 2048;
+  NBP_DISPATCH_H(dtype, {
+    SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, nullptr, 1, reinterpret_cast<const H*>(Wt), ldb,
+                 reinterpret_cast<H*>(dx), N, M, N, K, nullptr, reinterpret_cast<const H*>(x), nullptr, nullptr,
+                 reinterpret_cast<const float2*>(stats), lnw, reinterpret_cast<const H*>(dres), slab_w, slab_b};
+    p.lnb_f = lnb;
+    p.slab_w2 = sw;
+    p.slab_b2 = sb;
+    gemm_skinny_kernel<1, 4, AM_PLAIN, CM_LNBWD, H, true><<<dim3((unsigned)nb), 256, 0, S(s)>>>(p);
+  });
+  int rc = check_launch("dgrad_ln_bwd_wg");
+  if (rc) return rc;
+  if ((rc = nbp_reduce_slab(slab_w, (int)nb, N, dlnw, s))) return rc;
+  if ((rc = nbp_reduce_slab(slab_b, (int)nb, N, dlnb, s))) return rc;
+  if ((rc = nbp_reduce_slab(sw, (int)nb, 2L * N * N, dW, s))) return rc;
+  return nbp_reduce_slab(sb, (int)nb, 2L * N, db, s);
+}
+
 int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, int rows_per_img, const void* Bw,
                     long ldb, void* C, int M, int N, int K, const float* bias, const void* R, const float* rscale,
                     const float* lnw, const float* lnb, void* nout, float* stats, float eps, int dtype,

@@ -110,6 +110,9 @@ class NAFNet(nn.Module):
         # level 0 with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
         # (nbp_gemm_ffn, bitwise the two launches, +0.1 % step), g2 never stored
         self.fuse_ffn = True
+        # level 0: conv1's weight / bias gradients folded into the conv1 dgrad + norm1 backward pass (nbp_dgrad_ln_bwd_wg:
+        # n1 rebuilt from x and the LN statistics, dt1 already in registers; False: a separate nbp_wgrad_f32 launch)
+        self.ln_wg = True
         # the middle level (16 x 16 at C 512): conv1 -> depthwise -> SimpleGate -> pool as one whole-image launch
         # (nbp_c1_dw_sg_pool; t1 / t2 / g bitwise, the pool up to fp32 summation order)
         self.fuse_c1dw = True
@@ -746,6 +749,14 @@ class NAFNet(nn.Module):
             call("dw_bwd", dt2, *dw_args)
         # conv1 input gradient + norm1 backward + residual
         dx = E(M, c)
+        if fuse_ln and c == 32 and self.ln_wg:  # + conv1's dW / db from the same tiles (n1 rebuilt from x / stats)
+            n_ws = query("dgrad_ln_bwd_wg_workspace_floats", M, c)
+            call("dgrad_ln_bwd_wg", dt1, 2 * c, self._slice(Wt[2], pre + "conv1.weight"), 2 * c, M, c, 2 * c,
+                 S["x"].reshape(M, c), S["st1"], self._slice(P, pre + "norm1.weight"),
+                 self._slice(P, pre + "norm1.bias"), dy, dx, self._slice(dflat, pre + "norm1.weight"),
+                 self._slice(dflat, pre + "norm1.bias"), self._slice(dflat, pre + "conv1.weight"),
+                 self._slice(dflat, pre + "conv1.bias"), F(n_ws), n_ws, dt)
+            return dx.view(B, h, w, c)
         self._wgrad(dt1, 2 * c, AM_PLAIN, S["n1"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
         if fuse_ln:

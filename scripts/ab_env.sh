@@ -1,18 +1,13 @@
 #!/bin/bash
-# A/B bench runs under different environment settings: bash scripts/ab_env.sh "VAR=a" "VAR=b" ...
-# ("-" = defaults; "EAGER" or "EAGER:VAR=x" = the --eager launch mode).  Prints value / ms_per_step per arm into gpurun_out/ab.txt.
-set -uo pipefail
+# A/B of an executor switch in the quick bench: AB_VAR takes each of AB_VALS in turn (interleaved, REPS times), e.g.
+#   AB_VAR=NBP_LN_WG AB_VALS="1 0" scripts/ab_env.sh
+set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-: > gpurun_out/ab.txt
-for arm in "$@"; do
-  extra=""
-  envs="${arm#EAGER}"
-  envs="${envs#:}"
-  [ "$envs" = "-" ] && envs=""
-  [[ "$arm" == EAGER* ]] && extra="--eager"
-  env $envs timeout -k 10 300 python bench.py --steps 20 --warmup 3 --quick $extra > gpurun_out/ab_last.log 2>&1
-  rc=$?
-  if [ $rc -ne 0 ]; then echo "$arm rc=$rc" | tee -a gpurun_out/ab.txt; tail -5 gpurun_out/ab_last.log; exit $rc; fi
-  grep '^{' gpurun_out/ab_last.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$arm', d['value'], d['ms_per_step'])" | tee -a gpurun_out/ab.txt
+O=gpurun_out/${TAG:-ab}
+mkdir -p $O
+for rep in $(seq 1 ${REPS:-2}); do
+  for v in $AB_VALS; do
+    env "$AB_VAR=$v" timeout -k 10 300 python bench.py --quick --steps 20 --warmup 5 > $O/b_${rep}_$v.json 2> $O/b.err || { tail -30 $O/b.err; exit 1; }
+    python -c "import json; d=json.loads(open('$O/b_${rep}_$v.json').read().strip().splitlines()[-1]); print('$AB_VAR=$v', d['value'], d['ms_per_step'], {k: (v['fwd_ms'], v['bwd_ms']) for k, v in d['nafblock_roofline']['per_level_eager'].items() if 'C32' in k})"
+  done
 done
