@@ -428,6 +428,134 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
 
+// wgrad_bf16_kernel<.., RM = 64> (PLAIN / per-image scale X) with the split's 64-row stages streamed through a register
+// ring of D stages (stage i + D is fetched into stage i's registers once they are in LDS) and, with IL, the stages
+// assigned round-robin (split s takes stages s, s + S, s + 2S, ...: at any time the splits read one contiguous band of
+// rows instead of S regions a split apart).  D = 1 without IL is wgrad_bf16_kernel<.., 64>'s schedule (bitwise equal for
+// any D without IL; IL changes the rows of each split, so the fp32 summation order).
+template <int XMODE, typename H, int D, bool IL>
+__global__ __launch_bounds__(256) void wgrad_bf16_ring(WgradP p) {
+  constexpr int TNW = 64, LS = 96, RM = 64, NR = 2;
+  static_assert(XMODE == AM_PLAIN || XMODE == 3, "wgrad_bf16_ring: plain or per-image-scaled X");
+  __shared__ __attribute__((aligned(16))) H Gs[RM * LS];
+  __shared__ __attribute__((aligned(16))) H Xs[RM * LS];
+  const H* G = reinterpret_cast<const H*>(p.G);
+  const H* X = reinterpret_cast<const H*>(p.X);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int n0 = blockIdx.x * TNW, k0 = blockIdx.y * TNW, s = blockIdx.z, S_ = gridDim.z;
+  const int mb = IL ? s * RM : s * p.chunk;
+  const int me = IL ? p.M : min(p.M, mb + p.chunk);
+  const int sstride = IL ? S_ * RM : RM;  // rows between this split's consecutive stages
+  const int nst = mb < me ? (IL ? ((p.M + RM - 1) / RM - s + S_ - 1) / S_ : (me - mb + RM - 1) / RM) : 0;
+  const bool do_b = p.slab_b && blockIdx.y == 0;
+  floatx16 acc, tot;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = tot[r] = 0.f;
+  float bsum = 0.f;
+  int cur_img = mb / p.rows_per_img;
+  auto fold = [&](int im) {
+    const int kk = k0 + wk * 32 + (lane & 31);
+    const float sc = kk < p.K ? p.x_scale[(long)im * p.K + kk] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      tot[r] = fmaf(acc[r], sc, tot[r]);
+      acc[r] = 0.f;
+    }
+  };
+  const int lr = tid >> 3, lc = (tid & 7) * 8;
+  const bool gok = n0 + lc < p.N, xok = k0 + lc < p.K;
+  vec_t<H, 8> rg[D][NR], rx[D][NR];
+  auto load = [&](int m0, vec_t<H, 8>* g, vec_t<H, 8>* x) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int m = m0 + lr + 32 * i;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[i][j] = x[i][j] = (H)0.f;
+      if (m < me) {
+        if (gok) g[i] = *reinterpret_cast<const vec_t<H, 8>*>(G + (long)m * p.ldg + n0 + lc);
+        if (xok) x[i] = *reinterpret_cast<const vec_t<H, 8>*>(X + (long)m * p.ldx + k0 + lc);
+      }
+    }
+  };
+  const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
+  const int gcol = wn * 32 + 16 * (grp & 1) + 4 * pp;
+  const int xcol = wk * 32 + 16 * (grp & 1) + 4 * pp;
+  if (nst > 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (d < nst) load(mb + d * sstride, rg[d], rx[d]);
+    for (int i0 = 0; i0 < nst; i0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int i = i0 + d;
+        if (i < nst) {
+          const int ms = mb + i * sstride;
+          if constexpr (XMODE == 3) {
+            const int im = ms / p.rows_per_img;
+            if (im != cur_img) {
+              fold(cur_img);
+              cur_img = im;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            *reinterpret_cast<vec_t<H, 8>*>(Gs + (lr + 32 * r) * LS + lc) = rg[d][r];
+            *reinterpret_cast<vec_t<H, 8>*>(Xs + (lr + 32 * r) * LS + lc) = rx[d][r];
+          }
+          __syncthreads();
+          if (i + D < nst) load(ms + D * sstride, rg[d], rx[d]);
+#pragma unroll
+          for (int ks = 0; ks < RM; ks += 16) {
+            vec_t<H, 8> a, b;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const int row = ks + 8 * h + 4 * t + q;
+              const vec_t<H, 4> va = ds_read_tr16<H>(Gs + row * LS + gcol);
+              const vec_t<H, 4> vb = ds_read_tr16<H>(Xs + row * LS + xcol);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                a[4 * t + j] = va[j];
+                b[4 * t + j] = vb[j];
+              }
+            }
+            acc = mfma32x32x16(a, b, acc);
+          }
+          if (do_b && tid < TNW) {
+#pragma unroll 8
+            for (int r = 0; r < RM; ++r) bsum += (float)Gs[r * LS + tid];
+          }
+          __syncthreads();
+        }
+      }
+    }
+    if constexpr (XMODE == 3) fold(cur_img);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int n = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int k = k0 + wk * 32 + (lane & 31);
+    if (n < p.N && k < p.K) p.slab[((long)s * p.N + n) * p.K + k] = XMODE == 3 ? tot[r] : acc[r];
+  }
+  if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
+}
+
+template <typename H, int D, bool IL>
+void launch_ring(const WgradP& p, int x_mode, dim3 grid, hipStream_t st) {
+  if (x_mode == AM_PLAIN) wgrad_bf16_ring<AM_PLAIN, H, D, IL><<<grid, 256, 0, st>>>(p);
+  else wgrad_bf16_ring<3, H, D, IL><<<grid, 256, 0, st>>>(p);
+}
+
+// NBP_WGRAD_RING (A/B): the narrow weight gradient's register-ring depth (0: wgrad_bf16_kernel) plus 10 for the
+// round-robin stage assignment (e.g. 11: depth 1, interleaved)
+int wgrad_ring_mode() {
+  static const int d = [] {
+    const char* e = getenv("NBP_WGRAD_RING");
+    return e ? atoi(e) : 0;
+  }();
+  return d;
+}
+
 
 // bf16 weight gradient for the wide layers (N, K multiples of 128: NAFBlock 1x1 convs at C >= 128): a 128 x 128
 // output tile per workgroup, each wave a 64 x 64 quadrant (2 x 2 MFMA tiles of 32 x 32 x 16), 64-row stages
@@ -1550,6 +1678,16 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
       else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
+      else if (g_mode == AM_PLAIN && (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0)) &&
+               wgrad_ring_mode() > 0) {
+        const int rm = wgrad_ring_mode();
+        if (rm == 1) launch_ring<H, 1, false>(p, x_mode, grid, st);
+        else if (rm == 2) launch_ring<H, 2, false>(p, x_mode, grid, st);
+        else if (rm == 4) launch_ring<H, 4, false>(p, x_mode, grid, st);
+        else if (rm == 11) launch_ring<H, 1, true>(p, x_mode, grid, st);
+        else if (rm == 12) launch_ring<H, 2, true>(p, x_mode, grid, st);
+        else launch_ring<H, 4, true>(p, x_mode, grid, st);
+      }
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0)

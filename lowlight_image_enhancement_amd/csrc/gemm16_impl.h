@@ -1508,6 +1508,19 @@ long skinny_blocks(long M) {
   return blocks > cap ? cap : blocks;
 }
 
+// the weight-gradient fold kernels (WGF: 238-256 VGPRs, 2 waves per SIMD, so 2 blocks per CU resident): a grid of one
+// resident round (512) instead of two -- each wave walks twice the tiles with its prefetch overlapped, and the fold
+// slabs halve (A/B in the quick bench, fp16: 1350.2 / 1354.6 vs 1349.8 / 1347.8 img/s, eager level-0 backward 1.95 vs
+// 2.02 ms; profiles/r05_wgcap/).  NBP_SKINNY_WG_CAP overrides (A/B only).
+long skinny_wg_blocks(long M) {
+  static const long cap = [] {
+    const char* e = getenv("NBP_SKINNY_WG_CAP");
+    return e ? atol(e) : 512L;
+  }();
+  const long b = skinny_blocks(M);
+  return b > cap ? cap : b;
+}
+
 // K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads)
 template <int AMODE, int CMODE, typename H>
 void launch_skinny(const SkinnyP<H>& p, hipStream_t st) {

@@ -108,7 +108,7 @@ int nbp_dgrad_ln_bwd_wg(const void* A, long lda, const void* Wt, long ldb, int M
               "nbp_dgrad_ln_bwd_wg: bad args");
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_ln_bwd_wg: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   NBP_REQUIRE(N == 32 && K == 64 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_ln_bwd_wg: N = 32, K = 64 (N=%d K=%d)", N, K);
-  const long nb = skinny_blocks(M);
+  const long nb = skinny_wg_blocks(M);
   NBP_REQUIRE(ws_floats >= nbp_dgrad_ln_bwd_wg_workspace_floats(M, N), "nbp_dgrad_ln_bwd_wg: workspace too small");
   float* slab_w = ws;
   float* slab_b = slab_w + nb * N;
@@ -210,7 +210,7 @@ int nbp_dgrad_sg_rc_wg(const void* A, long lda, const void* Wt, long ldb, const 
               "nbp_dgrad_sg_rc_wg: bad args");
   NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_dgrad_sg_rc_wg: 16-bit storage (dtype 1 bf16 / 2 fp16)");
   NBP_REQUIRE(N == 32 && K == 32 && lda % 8 == 0 && ldb % 8 == 0, "nbp_dgrad_sg_rc_wg: N = K = 32 (N=%d K=%d)", N, K);
-  const long nb = skinny_blocks(M);
+  const long nb = skinny_wg_blocks(M);
   NBP_REQUIRE(ws_floats >= nbp_dgrad_sg_rc_wg_workspace_floats(M, N), "nbp_dgrad_sg_rc_wg: workspace too small");
   float* sw2 = ws;
   float* su = sw2 + nb * 2048;

@@ -1,0 +1,59 @@
+"""Narrow 16-bit weight gradients (nbp_wgrad_f32) on level-0/1 shapes, saved for a bitwise comparison between
+NBP_WGRAD_RING settings (the env is read once per process):
+  NBP_WGRAD_RING=0 python scripts/wgrad_ring_check.py a.pt && NBP_WGRAD_RING=4 python scripts/wgrad_ring_check.py b.pt
+  python scripts/wgrad_ring_check.py --compare a.pt b.pt
+Also times each shape (HIP events, 20 reps) so the A/B reads per kernel."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+# (M, N, K, x_mode, rows_per_img): level-1 conv1 / conv4 (128 x 64), U5 (64 x 64), level-0 / 1 U3 (per-image scale),
+# ragged M
+SHAPES = [(131072, 128, 64, 0, 0), (131072, 64, 64, 0, 0), (524288, 32, 32, 2, 65536), (131072, 64, 64, 2, 16384),
+          (5 * 64 + 7, 128, 64, 0, 0), (3 * 4096, 32, 32, 2, 4096)]
+
+
+def main():
+    if sys.argv[1] == "--compare":
+        a, b = torch.load(sys.argv[2]), torch.load(sys.argv[3])
+        ok = True
+        for k in a:
+            eq = torch.equal(a[k], b[k])
+            ok &= eq
+            print(k, "bitwise" if eq else f"DIFF max {(a[k] - b[k]).abs().max().item():.3e}")
+        sys.exit(0 if ok else 1)
+    from lowlight_image_enhancement_amd._lib import call, query
+    dev = torch.device("cuda:0")
+    out = {}
+    for M, N, K, xm, rows in SHAPES:
+        gen = torch.Generator(device=dev).manual_seed(M + N + K)
+        G = torch.randn(M, N, device=dev, generator=gen).to(torch.bfloat16)
+        X = torch.randn(M, K, device=dev, generator=gen).to(torch.bfloat16)
+        sc = torch.rand(max(M // max(rows, 1), 1) * K, device=dev, generator=gen) if xm == 2 else None
+        dW, db = torch.empty(N * K, device=dev), torch.empty(N, device=dev)
+        nw = query("wgrad_workspace_floats", M, N, K)
+        ws = torch.empty(nw, device=dev)
+        args = (G, N, 0, X, K, xm, sc, rows if xm == 2 else 1, M, N, K, 0, 0, 0, 0, dW, db, ws, nw, 1)
+        call("wgrad_f32", *args)
+        torch.cuda.synchronize()
+        ref = G.double().t() @ (X.double() * (sc.view(-1, K).repeat_interleave(rows, 0)[:M].double()
+                                              if sc is not None else 1.0))
+        err = (dW.view(N, K).double() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            call("wgrad_f32", *args)
+        e1.record()
+        torch.cuda.synchronize()
+        key = f"M{M}_N{N}_K{K}_x{xm}"
+        print(f"{key}: rel err vs f64 {err:.2e}, {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per call (+ slab reduce)")
+        assert err < 1e-4, key
+        out[key + "_dW"], out[key + "_db"] = dW.cpu(), db.cpu()
+    torch.save(out, sys.argv[1])
+
+
+if __name__ == "__main__":
+    main()
