@@ -428,134 +428,201 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
 
-// wgrad_bf16_kernel<.., RM = 64> (PLAIN / per-image scale X) with the split's 64-row stages streamed through a register
-// ring of D stages (stage i + D is fetched into stage i's registers once they are in LDS) and, with IL, the stages
-// assigned round-robin (split s takes stages s, s + S, s + 2S, ...: at any time the splits read one contiguous band of
-// rows instead of S regions a split apart).  D = 1 without IL is wgrad_bf16_kernel<.., 64>'s schedule (bitwise equal for
-// any D without IL; IL changes the rows of each split, so the fp32 summation order).
-template <int XMODE, typename H, int D, bool IL>
-__global__ __launch_bounds__(256) void wgrad_bf16_ring(WgradP p) {
-  constexpr int TNW = 64, LS = 96, RM = 64, NR = 2;
-  static_assert(XMODE == AM_PLAIN || XMODE == 3, "wgrad_bf16_ring: plain or per-image-scaled X");
-  __shared__ __attribute__((aligned(16))) H Gs[RM * LS];
-  __shared__ __attribute__((aligned(16))) H Xs[RM * LS];
+// Narrow 16-bit weight gradient with the whole N x K output in one workgroup (N in {32, 64, 128}, K in {32, 64}: the
+// level-0 / 1 NAFBlock 1x1 convs, plain or per-image-scaled X).  Against the 64 x 64 tiles above:
+//  * every operand row is read once (they read X once per 64-column n-tile: 1.33x the bytes at N = 128);
+//  * 1024 threads = 4 row groups of 4 waves, each group with its own LDS stage, taking the split's 64-row stages g,
+//    g + 4, ...; the groups' partials are combined in LDS in a fixed order, so a split (and its fp32 slab) covers 4x
+//    the rows at the same 16 waves per CU (one workgroup per CU);
+//  * below four 32 x 32 output tiles the waves sharing a tile split its 16-row k-steps instead of idling.
+// Fragments come transposed from 96-element LDS rows by ds_read_b64_tr_b16 as in wgrad_bf16_kernel.
+template <int XMODE, typename H, int NT, int KT>
+__global__ __launch_bounds__(1024) void wgrad_narrow_full(WgradP p) {
+  static_assert(XMODE == AM_PLAIN || XMODE == 3, "wgrad_narrow_full: plain or per-image-scaled X");
+  constexpr int N = 32 * NT, K = 32 * KT, RG = 4, RM = 64, LS = 96;
+  constexpr int NG = (N + 63) / 64;                          // 64-column G panels
+  constexpr int PANEL = RM * LS;                             // 16-bit elements per panel
+  constexpr int STAGE_BYTES = (NG + 1) * PANEL * (int)sizeof(H);
+  constexpr int T = NT * KT;                                 // 32 x 32 output tiles
+  constexpr int TW = T < 4 ? T : 4;                          // tiles a group's 4 waves work on at once
+  constexpr int TPW = T > 4 ? T / 4 : 1;                     // tiles per wave
+  constexpr int KSPLIT = 4 / TW;                             // waves sharing a tile (its k-steps split)
+  constexpr int RED_BYTES = (RG * 4 * TPW * 1024 + RG * N) * 4;
+  constexpr int SMEM = RG * STAGE_BYTES > RED_BYTES ? RG * STAGE_BYTES : RED_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, g = tid >> 8, gt = tid & 255, lane = tid & 63, w = gt >> 6;
+  H* Gs = reinterpret_cast<H*>(smem + g * STAGE_BYTES);
+  H* Xs = Gs + NG * PANEL;
   const H* G = reinterpret_cast<const H*>(p.G);
   const H* X = reinterpret_cast<const H*>(p.X);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave >> 1, wk = wave & 1;
-  const int n0 = blockIdx.x * TNW, k0 = blockIdx.y * TNW, s = blockIdx.z, S_ = gridDim.z;
-  const int mb = IL ? s * RM : s * p.chunk;
-  const int me = IL ? p.M : min(p.M, mb + p.chunk);
-  const int sstride = IL ? S_ * RM : RM;  // rows between this split's consecutive stages
-  const int nst = mb < me ? (IL ? ((p.M + RM - 1) / RM - s + S_ - 1) / S_ : (me - mb + RM - 1) / RM) : 0;
-  const bool do_b = p.slab_b && blockIdx.y == 0;
-  floatx16 acc, tot;
+  const int s = blockIdx.x;
+  const int mb = s * p.chunk, me = min(p.M, mb + p.chunk);
+  const bool do_b = p.slab_b != nullptr;
+  const int ksub = w / TW;
+  int tn[TPW], tk[TPW];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = tot[r] = 0.f;
+  for (int j = 0; j < TPW; ++j) {
+    const int t = T >= 4 ? w + 4 * j : w % TW;
+    tn[j] = t / KT;
+    tk[j] = t % KT;
+  }
+  floatx16 acc[TPW], tot[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = tot[j][r] = 0.f;
   float bsum = 0.f;
-  int cur_img = mb / p.rows_per_img;
-  auto fold = [&](int im) {
-    const int kk = k0 + wk * 32 + (lane & 31);
-    const float sc = kk < p.K ? p.x_scale[(long)im * p.K + kk] : 0.f;
+  int cur_img = -1;
+  auto fold = [&](int im) {  // XMODE 3: each image's partial scaled by its column factors
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      tot[r] = fmaf(acc[r], sc, tot[r]);
-      acc[r] = 0.f;
+    for (int j = 0; j < TPW; ++j) {
+      const float sc = p.x_scale[(long)im * K + tk[j] * 32 + (lane & 31)];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        tot[j][r] = fmaf(acc[j][r], sc, tot[j][r]);
+        acc[j][r] = 0.f;
+      }
     }
   };
-  const int lr = tid >> 3, lc = (tid & 7) * 8;
-  const bool gok = n0 + lc < p.N, xok = k0 + lc < p.K;
-  vec_t<H, 8> rg[D][NR], rx[D][NR];
-  auto load = [&](int m0, vec_t<H, 8>* g, vec_t<H, 8>* x) {
+  // loader: 8-element chunks, row-major over the stage (consecutive threads along a row, rows contiguous)
+  constexpr int GC = RM * N / 8 / 256, XC = RM * K / 8 / 256;
+  vec_t<H, 8> rg[GC], rx[XC];
+  auto load = [&](int m0) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int m = m0 + lr + 32 * i;
+    for (int i = 0; i < GC; ++i) {
+      const int c = gt + 256 * i, m = m0 + c / (N / 8), col = (c % (N / 8)) * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[i][j] = x[i][j] = (H)0.f;
-      if (m < me) {
-        if (gok) g[i] = *reinterpret_cast<const vec_t<H, 8>*>(G + (long)m * p.ldg + n0 + lc);
-        if (xok) x[i] = *reinterpret_cast<const vec_t<H, 8>*>(X + (long)m * p.ldx + k0 + lc);
-      }
+      for (int e = 0; e < 8; ++e) rg[i][e] = (H)0.f;
+      if (m < me) rg[i] = *reinterpret_cast<const vec_t<H, 8>*>(G + (long)m * p.ldg + col);
+    }
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const int c = gt + 256 * i, m = m0 + c / (K / 8), col = (c % (K / 8)) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rx[i][e] = (H)0.f;
+      if (m < me) rx[i] = *reinterpret_cast<const vec_t<H, 8>*>(X + (long)m * p.ldx + col);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < GC; ++i) {
+      const int c = gt + 256 * i, row = c / (N / 8), col = (c % (N / 8)) * 8;
+      *reinterpret_cast<vec_t<H, 8>*>(Gs + (col / 64) * PANEL + row * LS + col % 64) = rg[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const int c = gt + 256 * i, row = c / (K / 8), col = (c % (K / 8)) * 8;
+      *reinterpret_cast<vec_t<H, 8>*>(Xs + row * LS + col) = rx[i];
     }
   };
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
-  const int gcol = wn * 32 + 16 * (grp & 1) + 4 * pp;
-  const int xcol = wk * 32 + 16 * (grp & 1) + 4 * pp;
-  if (nst > 0) {
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-      if (d < nst) load(mb + d * sstride, rg[d], rx[d]);
-    for (int i0 = 0; i0 < nst; i0 += D) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int i = i0 + d;
-        if (i < nst) {
-          const int ms = mb + i * sstride;
-          if constexpr (XMODE == 3) {
-            const int im = ms / p.rows_per_img;
-            if (im != cur_img) {
-              fold(cur_img);
-              cur_img = im;
-            }
-          }
-#pragma unroll
-          for (int r = 0; r < NR; ++r) {
-            *reinterpret_cast<vec_t<H, 8>*>(Gs + (lr + 32 * r) * LS + lc) = rg[d][r];
-            *reinterpret_cast<vec_t<H, 8>*>(Xs + (lr + 32 * r) * LS + lc) = rx[d][r];
-          }
-          __syncthreads();
-          if (i + D < nst) load(ms + D * sstride, rg[d], rx[d]);
-#pragma unroll
-          for (int ks = 0; ks < RM; ks += 16) {
-            vec_t<H, 8> a, b;
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-              const int row = ks + 8 * h + 4 * t + q;
-              const vec_t<H, 4> va = ds_read_tr16<H>(Gs + row * LS + gcol);
-              const vec_t<H, 4> vb = ds_read_tr16<H>(Xs + row * LS + xcol);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                a[4 * t + j] = va[j];
-                b[4 * t + j] = vb[j];
-              }
-            }
-            acc = mfma32x32x16(a, b, acc);
-          }
-          if (do_b && tid < TNW) {
-#pragma unroll 8
-            for (int r = 0; r < RM; ++r) bsum += (float)Gs[r * LS + tid];
-          }
-          __syncthreads();
+  const int cofs = 16 * (grp & 1) + 4 * pp;
+  const int nst = mb < me ? (me - mb + RM - 1) / RM : 0;  // the split's stages; group g takes g, g + RG, ...
+  const int niter = (nst + RG - 1) / RG;                   // (block-uniform: every barrier is reached by all)
+  if (mb + g * RM < me) load(mb + g * RM);
+  for (int i = 0; i < niter; ++i) {
+    const int ms = mb + (i * RG + g) * RM;
+    const bool valid = ms < me;
+    if (valid) {
+      if constexpr (XMODE == 3) {
+        const int im = ms / p.rows_per_img;
+        if (im != cur_img) {
+          if (cur_img >= 0) fold(cur_img);
+          cur_img = im;
         }
       }
+      store();
     }
-    if constexpr (XMODE == 3) fold(cur_img);
-  }
+    __syncthreads();
+    if (ms + RG * RM < me) load(ms + RG * RM);
+    if (valid) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int n = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    const int k = k0 + wk * 32 + (lane & 31);
-    if (n < p.N && k < p.K) p.slab[((long)s * p.N + n) * p.K + k] = XMODE == 3 ? tot[r] : acc[r];
+      for (int kq = 0; kq < 4 / KSPLIT; ++kq) {
+        const int ks = (ksub + KSPLIT * kq) * 16;
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+          const H* gp = Gs + ((tn[j] * 32) / 64) * PANEL + (tn[j] * 32) % 64 + cofs;
+          const H* xp = Xs + tk[j] * 32 + cofs;
+          vec_t<H, 8> a, b;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int row = ks + 8 * h + 4 * t + q;
+            const vec_t<H, 4> va = ds_read_tr16<H>(gp + row * LS);
+            const vec_t<H, 4> vb = ds_read_tr16<H>(xp + row * LS);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              a[4 * t + e] = va[e];
+              b[4 * t + e] = vb[e];
+            }
+          }
+          acc[j] = mfma32x32x16(a, b, acc[j]);
+        }
+      }
+      if (do_b && gt < N) {
+        const H* col = Gs + (gt / 64) * PANEL + gt % 64;
+#pragma unroll 8
+        for (int r = 0; r < RM; ++r) bsum += (float)col[r * LS];
+      }
+    }
+    __syncthreads();
   }
-  if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
+  if constexpr (XMODE == 3) {
+    if (cur_img >= 0) fold(cur_img);
+  }
+  // partials through LDS (the stages are dead after the loop's last barrier), combined in a fixed order: row group,
+  // then the waves sharing a tile in k-step order
+  float* red = reinterpret_cast<float*>(smem);
+  float* redb = red + RG * 4 * TPW * 1024;
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int nl = (r & 3) + 8 * (r >> 2) + 4 * h, kl = lane & 31;
+      red[((g * 4 + w) * TPW + j) * 1024 + nl * 32 + kl] = XMODE == 3 ? tot[j][r] : acc[j][r];
+    }
+  if (do_b && gt < N) redb[g * N + gt] = bsum;
+  __syncthreads();
+  for (int e = tid; e < N * K; e += 1024) {
+    const int n = e / K, k = e % K, t = (n / 32) * KT + k / 32, off = (n % 32) * 32 + k % 32;
+    float v = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < RG; ++gg)
+#pragma unroll
+      for (int ku = 0; ku < KSPLIT; ++ku) {
+        const int wv = T >= 4 ? t % 4 : t + TW * ku, slot = T >= 4 ? t / 4 : 0;
+        v += red[((gg * 4 + wv) * TPW + slot) * 1024 + off];
+      }
+    p.slab[(long)s * N * K + e] = v;
+  }
+  if (do_b && tid < N) p.slab_b[(long)s * N + tid] = ((redb[tid] + redb[N + tid]) + redb[2 * N + tid]) + redb[3 * N + tid];
 }
 
-template <typename H, int D, bool IL>
-void launch_ring(const WgradP& p, int x_mode, dim3 grid, hipStream_t st) {
-  if (x_mode == AM_PLAIN) wgrad_bf16_ring<AM_PLAIN, H, D, IL><<<grid, 256, 0, st>>>(p);
-  else wgrad_bf16_ring<3, H, D, IL><<<grid, 256, 0, st>>>(p);
+// splits of the full-width narrow weight gradient: one workgroup (16 waves) per CU, >= 512 rows per split
+int wgrad_full_splits(int M) {
+  const int s = cdiv(M, 512);
+  return s < 1 ? 1 : (s > 256 ? 256 : s);
 }
 
-// NBP_WGRAD_RING (A/B): the narrow weight gradient's register-ring depth (0: wgrad_bf16_kernel) plus 10 for the
-// round-robin stage assignment (e.g. 11: depth 1, interleaved)
-int wgrad_ring_mode() {
-  static const int d = [] {
-    const char* e = getenv("NBP_WGRAD_RING");
-    return e ? atoi(e) : 0;
+// NBP_WGRAD_FULL=0: the 64 x 64-tile narrow weight gradient instead (A/B)
+bool wgrad_full_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NBP_WGRAD_FULL");
+    return !e || atoi(e) != 0;
   }();
-  return d;
+  return on;
 }
 
+template <typename H, int XM>
+void launch_wgrad_full(const WgradP& p, int S_, hipStream_t st) {
+  const int N = p.N, K = p.K;
+  if (N == 128 && K == 64) {
+    if constexpr (XM == AM_PLAIN) wgrad_narrow_full<XM, H, 4, 2><<<S_, 1024, 0, st>>>(p);  // (scaled: 12 VGPRs spill)
+  } else if (N == 128) wgrad_narrow_full<XM, H, 4, 1><<<S_, 1024, 0, st>>>(p);
+  else if (N == 64 && K == 64) wgrad_narrow_full<XM, H, 2, 2><<<S_, 1024, 0, st>>>(p);
+  else if (N == 64) wgrad_narrow_full<XM, H, 2, 1><<<S_, 1024, 0, st>>>(p);
+  else if (K == 64) wgrad_narrow_full<XM, H, 1, 2><<<S_, 1024, 0, st>>>(p);
+  else wgrad_narrow_full<XM, H, 1, 1><<<S_, 1024, 0, st>>>(p);
+}
 
 // bf16 weight gradient for the wide layers (N, K multiples of 128: NAFBlock 1x1 convs at C >= 128): a 128 x 128
 // output tile per workgroup, each wave a 64 x 64 quadrant (2 x 2 MFMA tiles of 32 x 32 x 16), 64-row stages
@@ -1463,7 +1530,7 @@ int conv_f32(const float* x, int B, int H, int W, int Cin, const float* w, int C
 extern "C" {
 
 size_t nbp_wgrad_workspace_floats(int M, int N, int K) {
-  const int S_ = wgrad_splits(M, N, K);
+  const int S_ = std::max(wgrad_splits(M, N, K), wgrad_full_splits(M));
   return (size_t)S_ * N * K + (size_t)S_ * N;
 }
 
@@ -1639,7 +1706,11 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
   NBP_REQUIRE(g_mode != AM_S2D || (N == 4 * cs_g && gh > 0 && gw > 0), "nbp_wgrad_f32: G s2d geometry");
   NBP_REQUIRE(x_mode != AM_S2D || (K == 4 * cs_x && gh > 0 && gw > 0), "nbp_wgrad_f32: X s2d geometry");
   NBP_REQUIRE(x_mode != AM_SCALE || (x_scale && rows_per_img > 0), "nbp_wgrad_f32: x_scale");
-  const int S_ = wgrad_splits(M, N, K);
+  // the full-width narrow kernel: level-0 / 1 shapes, 16-bit, plain G, plain or per-image-scaled X (64-row stages)
+  const bool full = dtype != 0 && wgrad_full_enabled() && g_mode == AM_PLAIN &&
+                    (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0 && N * K <= 4096)) &&
+                    (N == 32 || N == 64 || N == 128) && (K == 32 || K == 64) && ldg % 8 == 0 && ldx % 8 == 0;
+  const int S_ = full ? wgrad_full_splits(M) : wgrad_splits(M, N, K);
   NBP_REQUIRE(ws_floats >= (size_t)S_ * N * K + (size_t)S_ * N, "nbp_wgrad_f32: workspace too small");
   int chunk = cdiv(M, S_);
   chunk = cdiv(chunk, 64) * 64;
@@ -1668,6 +1739,11 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       if (x_mode != AM_SCALE) p.x_scale = nullptr;  // the group kernel selects the X mode by x_scale
       g_wqueue.push_back(p);
       g_stats_wgrad[0] = 1;
+    } else if (full) {
+      NBP_DISPATCH_H(dtype, {
+        if (x_mode == AM_PLAIN) launch_wgrad_full<H, AM_PLAIN>(p, S_, st);
+        else launch_wgrad_full<H, 3>(p, S_, st);
+      });
     } else NBP_DISPATCH_H(dtype, {
       const int ns = wgrad_glds_depth() % 10;  // (the loader-split variants are grouped-launch only)
       if (wide && ns == 4 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 4><<<wgrid, 256, 0, st>>>(p);
@@ -1678,16 +1754,6 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
       else if (wide && ns == 3) wgrad_bf16_wide_glds<AM_SCALE, H, 3><<<wgrid, 256, 0, st>>>(p);
       else if (wide && x_mode == AM_PLAIN) wgrad_bf16_wide<AM_PLAIN, H><<<wgrid, 256, 0, st>>>(p);
       else if (wide) wgrad_bf16_wide<AM_SCALE, H><<<wgrid, 256, 0, st>>>(p);
-      else if (g_mode == AM_PLAIN && (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0)) &&
-               wgrad_ring_mode() > 0) {
-        const int rm = wgrad_ring_mode();
-        if (rm == 1) launch_ring<H, 1, false>(p, x_mode, grid, st);
-        else if (rm == 2) launch_ring<H, 2, false>(p, x_mode, grid, st);
-        else if (rm == 4) launch_ring<H, 4, false>(p, x_mode, grid, st);
-        else if (rm == 11) launch_ring<H, 1, true>(p, x_mode, grid, st);
-        else if (rm == 12) launch_ring<H, 2, true>(p, x_mode, grid, st);
-        else launch_ring<H, 4, true>(p, x_mode, grid, st);
-      }
       else if (g_mode == AM_PLAIN && x_mode == AM_PLAIN)
         wgrad_bf16_kernel<AM_PLAIN, AM_PLAIN, H, 64><<<grid, 256, 0, st>>>(p);
       else if (g_mode == AM_PLAIN && x_mode == AM_SCALE && rows_per_img % 64 == 0)

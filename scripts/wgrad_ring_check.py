@@ -1,8 +1,8 @@
-"""Narrow 16-bit weight gradients (nbp_wgrad_f32) on level-0/1 shapes, saved for a bitwise comparison between
-NBP_WGRAD_RING settings (the env is read once per process):
-  NBP_WGRAD_RING=0 python scripts/wgrad_ring_check.py a.pt && NBP_WGRAD_RING=4 python scripts/wgrad_ring_check.py b.pt
-  python scripts/wgrad_ring_check.py --compare a.pt b.pt
-Also times each shape (HIP events, 20 reps) so the A/B reads per kernel."""
+"""Narrow 16-bit weight gradients (nbp_wgrad_f32) on level-0/1 shapes: float64 check, per-call time (HIP events, 20
+reps, slab reduction included) and the results saved for a bitwise comparison between two builds or env settings
+(an env switch is read once per process; round 5 used it for the register-ring variants, profiles/r05_wgrad_ring/):
+  NBP_LIB=a.so python scripts/wgrad_ring_check.py a.pt && NBP_LIB=b.so python scripts/wgrad_ring_check.py b.pt
+  python scripts/wgrad_ring_check.py --compare a.pt b.pt"""
 import os
 import sys
 
@@ -13,7 +13,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 # (M, N, K, x_mode, rows_per_img): level-1 conv1 / conv4 (128 x 64), U5 (64 x 64), level-0 / 1 U3 (per-image scale),
 # ragged M
 SHAPES = [(131072, 128, 64, 0, 0), (131072, 64, 64, 0, 0), (524288, 32, 32, 2, 65536), (131072, 64, 64, 2, 16384),
-          (5 * 64 + 7, 128, 64, 0, 0), (3 * 4096, 32, 32, 2, 4096)]
+          (5 * 64 + 7, 128, 64, 0, 0), (3 * 4096, 32, 32, 2, 4096), (524288, 64, 32, 0, 0), (131072, 32, 64, 0, 0),
+          (3 * 4096 + 640 + 5, 64, 32, 0, 0), (2 * 8192, 128, 32, 0, 0)]
 
 
 def main():
