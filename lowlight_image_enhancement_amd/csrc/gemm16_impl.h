@@ -833,6 +833,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
 // fragments while the current one is multiplied; a lane ends up owning one pixel's channels (4 consecutive per
 // register group), so the epilogue (bias, layer-scale residual, SimpleGate forward / backward) runs in registers and
 // stores 8 / 16-byte pieces that complete whole rows in L2.
+// The weight-gradient folds' LDS tiles (row-per-lane 16-byte stores, ds_read_b64_tr_b16 reads of 4 consecutive rows):
+// the 16-byte chunk index of a row XOR-swizzled by (row / 4) mod 4.  With 64-byte rows the plain layout puts the 16
+// lanes of a store on 4 chunk slots (4-way conflicts; 8-way for the 4-byte gate stores) -- measured 58 % of the
+// conv5-fold kernel's LDS-active cycles as bank conflicts; the 4 rows of a transposed read share row / 4, so they keep
+// one conflict-free 256-byte pattern.  (Not in the conv1 fold: its dt1 stage has 192-byte rows, and the extra address
+// registers spill its 256 VGPRs.)
+__device__ __forceinline__ int fswz(int row, int col) {
+  return (col & ~31) | ((((col >> 3) ^ (row >> 2)) & 3) << 3) | (col & 7);
+}
+
 template <typename H>
 struct SkinnyP {
   const H* A;
@@ -1331,15 +1341,16 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
       const H* st = stage3[threadIdx.x >> 6];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        *reinterpret_cast<vec_t<H, 8>*>(sd + r * 32 + ks * 16 + 8 * h) = a0[ks];
-        *reinterpret_cast<vec_t<H, 8>*>(sn + r * 32 + ks * 16 + 8 * h) = c0[ks];
+        *reinterpret_cast<vec_t<H, 8>*>(sd + r * 32 + fswz(r, ks * 16 + 8 * h)) = a0[ks];
+        *reinterpret_cast<vec_t<H, 8>*>(sn + r * 32 + fswz(r, ks * 16 + 8 * h)) = c0[ks];
 #pragma unroll
         for (int e = 0; e < 8; ++e) vsum[ks][e] += (float)a0[ks][e];  // V partial (rows past M are zero-filled)
       }
 #pragma unroll
       for (int t = 0; t < NT2; ++t)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<vec_t<H, 2>*>(sg + r * 32 + t * 16 + 4 * g + 2 * h) = g2h[t][g];
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<vec_t<H, 2>*>(sg + r * 32 + fswz(r, t * 16 + 4 * g + 2 * h)) = g2h[t][g];
       __builtin_amdgcn_wave_barrier();
       const int grp = lane >> 4, gq = (lane & 15) >> 2, pp = lane & 3;
       const int fcol = 16 * (grp & 1) + 4 * pp;
@@ -1351,9 +1362,9 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
           const int row = ks + 8 * h + 4 * tt + gq;
           const vec_t<H, 4> a0v = ds_read_tr16<H>(st + row * 96 + fcol);
           const vec_t<H, 4> a1v = ds_read_tr16<H>(st + row * 96 + 32 + fcol);
-          const vec_t<H, 4> nv = ds_read_tr16<H>(sn + row * 32 + fcol);
-          const vec_t<H, 4> uv = ds_read_tr16<H>(sd + row * 32 + fcol);
-          const vec_t<H, 4> gv = ds_read_tr16<H>(sg + row * 32 + fcol);
+          const vec_t<H, 4> nv = ds_read_tr16<H>(sn + row * 32 + fswz(row, fcol));
+          const vec_t<H, 4> uv = ds_read_tr16<H>(sd + row * 32 + fswz(row, fcol));
+          const vec_t<H, 4> gv = ds_read_tr16<H>(sg + row * 32 + fswz(row, fcol));
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             fa[0][4 * tt + e] = a0v[e];
