@@ -80,7 +80,7 @@ MFMA16_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA peak
 HBM_PEAK_GBPS = 8000.0
 ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
 ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
-                   "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel"], "wgrad_group": ["wgrad_bf16_wide_group"],
+                   "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel", "wgrad_narrow_full"], "wgrad_group": ["wgrad_bf16_wide_group"],
                    "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
                    "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32>"],
                    "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"],

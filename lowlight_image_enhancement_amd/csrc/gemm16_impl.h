@@ -1532,12 +1532,41 @@ long skinny_wg_blocks(long M) {
   return b > cap ? cap : b;
 }
 
-// K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads)
+// NBP_SKINNY_OCC=0: every skinny kernel on skinny_blocks' grid (A/B)
+bool skinny_occ_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NBP_SKINNY_OCC");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// the grid of one skinny instantiation: its tiles in workgroups of 4 waves, at most one resident round (occupancy x
+// CUs, from the HIP occupancy query: 2-4 workgroups per CU by its VGPRs) -- a second round re-pays the pipeline fill
+// that the grid-stride tile loop otherwise overlaps (the fold kernels: +0.3 % with 512 instead of 1024)
+template <int NT, int KS, int AMODE, int CMODE, typename H, bool WGF = false>
+long skinny_grid(long M) {
+  static const long cap = [] {
+    int occ = 0, dev = 0, ncu = 0;
+    if (!skinny_occ_enabled() || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gemm_skinny_kernel<NT, KS, AMODE, CMODE, H, WGF>, 256, 0) !=
+            hipSuccess || occ <= 0 || ncu <= 0)
+      return 1024L;
+    return (long)occ * ncu;
+  }();
+  const long b = skinny_blocks(M);
+  return b > cap ? cap : b;
+}
+
+// K <= 64 in 16-wide steps, or K <= 128 (KS = 8, the level-1 conv4 / conv1 dgrads); returns the grid (workgroups)
 template <int AMODE, int CMODE, typename H>
-void launch_skinny(const SkinnyP<H>& p, hipStream_t st) {
-  const dim3 g((unsigned)skinny_blocks(p.M));
+long launch_skinny(const SkinnyP<H>& p, hipStream_t st) {
+  long nb = 0;
   const int nt = (p.N + 31) / 32, ks = (p.K + 15) / 16;
-#define NBP_SKINNY(NT_, KS_) gemm_skinny_kernel<NT_, KS_, AMODE, CMODE, H><<<g, 256, 0, st>>>(p)
+#define NBP_SKINNY(NT_, KS_)                                          \
+  (nb = skinny_grid<NT_, KS_, AMODE, CMODE, H>(p.M),                  \
+   gemm_skinny_kernel<NT_, KS_, AMODE, CMODE, H><<<dim3((unsigned)nb), 256, 0, st>>>(p))
   if (nt == 1) {
     if (ks == 1) NBP_SKINNY(1, 1); else if (ks == 2) NBP_SKINNY(1, 2); else if (ks == 3) NBP_SKINNY(1, 3);
     else if (ks == 4) NBP_SKINNY(1, 4); else NBP_SKINNY(1, 8);
@@ -1546,6 +1575,7 @@ void launch_skinny(const SkinnyP<H>& p, hipStream_t st) {
     else if (ks == 4) NBP_SKINNY(2, 4); else NBP_SKINNY(2, 8);
   }
 #undef NBP_SKINNY
+  return nb;
 }
 
 // whether the skinny path serves this call (bf16 in / out, N and K <= 64, supported modes, aligned rows)

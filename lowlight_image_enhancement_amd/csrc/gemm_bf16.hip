@@ -79,15 +79,15 @@ int nbp_dgrad_ln_bwd(const void* A, long lda, const void* Wt, long ldb, int M, i
   } else {
     NBP_REQUIRE((N == 32 || N == 64) && K % 8 == 0 && K <= 128 && lda % 8 == 0 && ldb % 8 == 0,
                 "nbp_dgrad_ln_bwd: N must be 32, 64, 128, 256 or 512, K <= 128 (multiple of 8) (N=%d K=%d)", N, K);
-    nb = skinny_blocks(M);
-    NBP_REQUIRE(ws_floats >= (size_t)2 * nb * N, "nbp_dgrad_ln_bwd: workspace too small");
+    const long nbmax = skinny_blocks(M);  // the slab layout; the launch uses nb <= nbmax of them
+    NBP_REQUIRE(ws_floats >= (size_t)2 * nbmax * N, "nbp_dgrad_ln_bwd: workspace too small");
     slab_w = ws;
-    slab_b = ws + nb * N;
+    slab_b = ws + nbmax * N;
     NBP_DISPATCH_H(dtype, {
       SkinnyP<H> p{reinterpret_cast<const H*>(A), lda, nullptr, 1, reinterpret_cast<const H*>(Wt), ldb,
                    reinterpret_cast<H*>(dx), N, M, N, K, nullptr, reinterpret_cast<const H*>(x), nullptr, nullptr,
                    reinterpret_cast<const float2*>(stats), lnw, reinterpret_cast<const H*>(dres), slab_w, slab_b};
-      launch_skinny<AM_PLAIN, CM_LNBWD, H>(p, S(s));
+      nb = launch_skinny<AM_PLAIN, CM_LNBWD, H>(p, S(s));
     });
   }
   int rc = check_launch("dgrad_ln_bwd");
@@ -178,7 +178,8 @@ int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5
                  reinterpret_cast<H*>(out), C, M, C, C, b5, reinterpret_cast<const H*>(y), gamma, nullptr,
                  nullptr, lnw, nullptr, nullptr, nullptr, lnb, reinterpret_cast<H*>(nout),
                  reinterpret_cast<float2*>(stats), eps, nullptr, reinterpret_cast<const H*>(W4), b4};
-    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_FFN, H><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
+    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_FFN, H>
+        <<<dim3((unsigned)skinny_grid<1, 2, AM_PLAIN, CM_FFN, H>(M)), 256, 0, S(s)>>>(p);
   });
   return check_launch("gemm_ffn");
 }
@@ -194,7 +195,8 @@ int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const voi
                  reinterpret_cast<H*>(C), 2L * N, M, N, K, nullptr, nullptr, nullptr, nullptr,
                  nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
                  reinterpret_cast<const H*>(A2), reinterpret_cast<const H*>(W2), b2};
-    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC, H><<<dim3((unsigned)skinny_blocks(M)), 256, 0, S(s)>>>(p);
+    gemm_skinny_kernel<1, 2, AM_PLAIN, CM_SGBWD_RC, H>
+        <<<dim3((unsigned)skinny_grid<1, 2, AM_PLAIN, CM_SGBWD_RC, H>(M)), 256, 0, S(s)>>>(p);
   });
   return check_launch("dgrad_sg_rc");
 }

@@ -20,7 +20,7 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            # weight gradients launched at once (N or K <= 64) / the grouped wide launches of a U-Net level, and the
            # fp32 slab reductions (+ layer-scale post-ops) that fold their split-M partials: per KERNEL launch, the
            # unit bench.py's algorithmic bytes use for these classes
-           "wgrad_narrow": ("wgrad_bf16_kernel", "wgrad_f32_kernel"), "wgrad_group": ("wgrad_bf16_wide",),
+           "wgrad_narrow": ("wgrad_bf16_kernel", "wgrad_f32_kernel", "wgrad_narrow_full"), "wgrad_group": ("wgrad_bf16_wide",),
            "reduce": ("reduce_multi_kernel", "layer_scale_grad_kernel"),
            "dw_bwd": ("dw_bwd_tiled",), "dw_bwd_32": (re.compile(r"dw_bwd_tiledI\w+?Li32E"),),
            "dw_fwd": ("dw_sg_pool_tiled",), "c1dw": ("c1_dw_sg_pool_img",), "ln_fwd": ("ln_fwd_nhwc",),
