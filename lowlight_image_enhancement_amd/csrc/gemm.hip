@@ -428,21 +428,24 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgradP p) {
   if (do_b && tid < TNW && n0 + tid < p.N) p.slab_b[(long)s * p.N + n0 + tid] = bsum;
 }
 
-// Narrow 16-bit weight gradient with the whole N x K output in one workgroup (N in {32, 64, 128}, K in {32, 64}: the
-// level-0 / 1 NAFBlock 1x1 convs, plain or per-image-scaled X).  Against the 64 x 64 tiles above:
+// Narrow 16-bit weight gradient with the whole N x K output in one workgroup (N, K in {32, 64, 128}, at most 8 output
+// tiles of 32 x 32: the level-0 / 1 NAFBlock 1x1 convs with plain or per-image-scaled X, and the level-0 / 1 down /
+// up convs with the space-to-depth gather of X / G).  Against the 64 x 64 tiles above:
 //  * every operand row is read once (they read X once per 64-column n-tile: 1.33x the bytes at N = 128);
 //  * 1024 threads = 4 row groups of 4 waves, each group with its own LDS stage, taking the split's 64-row stages g,
 //    g + 4, ...; the groups' partials are combined in LDS in a fixed order, so a split (and its fp32 slab) covers 4x
 //    the rows at the same 16 waves per CU (one workgroup per CU);
 //  * below four 32 x 32 output tiles the waves sharing a tile split its 16-row k-steps instead of idling.
 // Fragments come transposed from 96-element LDS rows by ds_read_b64_tr_b16 as in wgrad_bf16_kernel.
-template <int XMODE, typename H, int NT, int KT>
+template <int GMODE, int XMODE, typename H, int NT, int KT>
 __global__ __launch_bounds__(1024) void wgrad_narrow_full(WgradP p) {
-  static_assert(XMODE == AM_PLAIN || XMODE == 3, "wgrad_narrow_full: plain or per-image-scaled X");
+  static_assert(XMODE == AM_PLAIN || XMODE == 3 || XMODE == AM_S2D, "wgrad_narrow_full: plain, scaled or S2D X");
+  static_assert(GMODE == AM_PLAIN || GMODE == AM_S2D, "wgrad_narrow_full: plain or S2D G");
+  static_assert(NT * KT <= 8, "wgrad_narrow_full: at most 8 output tiles");
   constexpr int N = 32 * NT, K = 32 * KT, RG = 4, RM = 64, LS = 96;
-  constexpr int NG = (N + 63) / 64;                          // 64-column G panels
+  constexpr int NG = (N + 63) / 64, NX = (K + 63) / 64;      // 64-column G / X panels
   constexpr int PANEL = RM * LS;                             // 16-bit elements per panel
-  constexpr int STAGE_BYTES = (NG + 1) * PANEL * (int)sizeof(H);
+  constexpr int STAGE_BYTES = (NG + NX) * PANEL * (int)sizeof(H);
   constexpr int T = NT * KT;                                 // 32 x 32 output tiles
   constexpr int TW = T < 4 ? T : 4;                          // tiles a group's 4 waves work on at once
   constexpr int TPW = T > 4 ? T / 4 : 1;                     // tiles per wave
@@ -493,14 +496,18 @@ __global__ __launch_bounds__(1024) void wgrad_narrow_full(WgradP p) {
       const int c = gt + 256 * i, m = m0 + c / (N / 8), col = (c % (N / 8)) * 8;
 #pragma unroll
       for (int e = 0; e < 8; ++e) rg[i][e] = (H)0.f;
-      if (m < me) rg[i] = *reinterpret_cast<const vec_t<H, 8>*>(G + (long)m * p.ldg + col);
+      if (m < me)
+        rg[i] = *reinterpret_cast<const vec_t<H, 8>*>(
+            G + (GMODE == AM_S2D ? s2d_off(m, col, p.gh, p.gw, p.cs_g) : (long)m * p.ldg + col));
     }
 #pragma unroll
     for (int i = 0; i < XC; ++i) {
       const int c = gt + 256 * i, m = m0 + c / (K / 8), col = (c % (K / 8)) * 8;
 #pragma unroll
       for (int e = 0; e < 8; ++e) rx[i][e] = (H)0.f;
-      if (m < me) rx[i] = *reinterpret_cast<const vec_t<H, 8>*>(X + (long)m * p.ldx + col);
+      if (m < me)
+        rx[i] = *reinterpret_cast<const vec_t<H, 8>*>(
+            X + (XMODE == AM_S2D ? s2d_off(m, col, p.gh, p.gw, p.cs_x) : (long)m * p.ldx + col));
     }
   };
   auto store = [&]() {
@@ -512,7 +519,7 @@ __global__ __launch_bounds__(1024) void wgrad_narrow_full(WgradP p) {
 #pragma unroll
     for (int i = 0; i < XC; ++i) {
       const int c = gt + 256 * i, row = c / (K / 8), col = (c % (K / 8)) * 8;
-      *reinterpret_cast<vec_t<H, 8>*>(Xs + row * LS + col) = rx[i];
+      *reinterpret_cast<vec_t<H, 8>*>(Xs + (col / 64) * PANEL + row * LS + col % 64) = rx[i];
     }
   };
   const int grp = lane >> 4, gi = lane & 15, q = gi >> 2, pp = gi & 3, h = lane >> 5;
@@ -542,7 +549,7 @@ __global__ __launch_bounds__(1024) void wgrad_narrow_full(WgradP p) {
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
           const H* gp = Gs + ((tn[j] * 32) / 64) * PANEL + (tn[j] * 32) % 64 + cofs;
-          const H* xp = Xs + tk[j] * 32 + cofs;
+          const H* xp = Xs + ((tk[j] * 32) / 64) * PANEL + (tk[j] * 32) % 64 + cofs;
           vec_t<H, 8> a, b;
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
@@ -616,12 +623,19 @@ template <typename H, int XM>
 void launch_wgrad_full(const WgradP& p, int S_, hipStream_t st) {
   const int N = p.N, K = p.K;
   if (N == 128 && K == 64) {
-    if constexpr (XM == AM_PLAIN) wgrad_narrow_full<XM, H, 4, 2><<<S_, 1024, 0, st>>>(p);  // (scaled: 12 VGPRs spill)
-  } else if (N == 128) wgrad_narrow_full<XM, H, 4, 1><<<S_, 1024, 0, st>>>(p);
-  else if (N == 64 && K == 64) wgrad_narrow_full<XM, H, 2, 2><<<S_, 1024, 0, st>>>(p);
-  else if (N == 64) wgrad_narrow_full<XM, H, 2, 1><<<S_, 1024, 0, st>>>(p);
-  else if (K == 64) wgrad_narrow_full<XM, H, 1, 2><<<S_, 1024, 0, st>>>(p);
-  else wgrad_narrow_full<XM, H, 1, 1><<<S_, 1024, 0, st>>>(p);
+    if constexpr (XM == AM_PLAIN) wgrad_narrow_full<AM_PLAIN, XM, H, 4, 2><<<S_, 1024, 0, st>>>(p);  // (scaled: spills)
+  } else if (N == 128) wgrad_narrow_full<AM_PLAIN, XM, H, 4, 1><<<S_, 1024, 0, st>>>(p);
+  else if (N == 64 && K == 64) wgrad_narrow_full<AM_PLAIN, XM, H, 2, 2><<<S_, 1024, 0, st>>>(p);
+  else if (N == 64) wgrad_narrow_full<AM_PLAIN, XM, H, 2, 1><<<S_, 1024, 0, st>>>(p);
+  else if (K == 64) wgrad_narrow_full<AM_PLAIN, XM, H, 1, 2><<<S_, 1024, 0, st>>>(p);
+  else wgrad_narrow_full<AM_PLAIN, XM, H, 1, 1><<<S_, 1024, 0, st>>>(p);
+}
+
+// the down conv (X gathered, N 64 x K 128) and up conv (G gathered, N 128 x K 64) gradients of levels 0 / 1
+template <typename H>
+void launch_wgrad_full_s2d(const WgradP& p, bool g_s2d, int S_, hipStream_t st) {
+  if (g_s2d) wgrad_narrow_full<AM_S2D, AM_PLAIN, H, 4, 2><<<S_, 1024, 0, st>>>(p);
+  else wgrad_narrow_full<AM_PLAIN, AM_S2D, H, 2, 4><<<S_, 1024, 0, st>>>(p);
 }
 
 // bf16 weight gradient for the wide layers (N, K multiples of 128: NAFBlock 1x1 convs at C >= 128): a 128 x 128
@@ -1710,7 +1724,11 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
   const bool full = dtype != 0 && wgrad_full_enabled() && g_mode == AM_PLAIN &&
                     (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0 && N * K <= 4096)) &&
                     (N == 32 || N == 64 || N == 128) && (K == 32 || K == 64) && ldg % 8 == 0 && ldx % 8 == 0;
-  const int S_ = full ? wgrad_full_splits(M) : wgrad_splits(M, N, K);
+  // ... and the level-0 / 1 down / up conv gradients (one side space-to-depth gathered, 8-channel chunks)
+  const bool full_s2d = dtype != 0 && wgrad_full_enabled() &&
+                        ((g_mode == AM_PLAIN && x_mode == AM_S2D && N == 64 && K == 128 && ldg % 8 == 0) ||
+                         (g_mode == AM_S2D && x_mode == AM_PLAIN && N == 128 && K == 64 && ldx % 8 == 0));
+  const int S_ = full || full_s2d ? wgrad_full_splits(M) : wgrad_splits(M, N, K);
   NBP_REQUIRE(ws_floats >= (size_t)S_ * N * K + (size_t)S_ * N, "nbp_wgrad_f32: workspace too small");
   int chunk = cdiv(M, S_);
   chunk = cdiv(chunk, 64) * 64;
@@ -1744,6 +1762,8 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
         if (x_mode == AM_PLAIN) launch_wgrad_full<H, AM_PLAIN>(p, S_, st);
         else launch_wgrad_full<H, 3>(p, S_, st);
       });
+    } else if (full_s2d) {
+      NBP_DISPATCH_H(dtype, launch_wgrad_full_s2d<H>(p, g_mode == AM_S2D, S_, st));
     } else NBP_DISPATCH_H(dtype, {
       const int ns = wgrad_glds_depth() % 10;  // (the loader-split variants are grouped-launch only)
       if (wide && ns == 4 && x_mode == AM_PLAIN) wgrad_bf16_wide_glds<AM_PLAIN, H, 4><<<wgrid, 256, 0, st>>>(p);

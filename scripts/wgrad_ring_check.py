@@ -53,6 +53,37 @@ def main():
         print(f"{key}: rel err vs f64 {err:.2e}, {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per call (+ slab reduce)")
         assert err < 1e-4, key
         out[key + "_dW"], out[key + "_db"] = dW.cpu(), db.cpu()
+    # space-to-depth gathers (the level-0 / 1 down conv: X gathered, N 64 x K 128; up conv: G gathered, N 128 x K 64)
+    for B, gh, gw, cs, side in ((2, 64, 64, 32, "x"), (2, 64, 64, 32, "g"), (1, 9, 7, 32, "x"), (1, 9, 7, 32, "g")):
+        M = B * gh * gw
+        gen = torch.Generator(device=dev).manual_seed(M + cs + (side == "g"))
+        fmap = torch.randn(B, 2 * gh, 2 * gw, cs, device=dev, generator=gen).to(torch.bfloat16)
+        flat = fmap.view(B, gh, 2, gw, 2, cs).permute(0, 1, 3, 2, 4, 5).reshape(M, 4 * cs)  # k = (kh*2 + kw)*cs + c
+        other = torch.randn(M, 2 * cs if side == "x" else 2 * cs, device=dev, generator=gen).to(torch.bfloat16)
+        if side == "x":  # G plain [M][N = 2cs], X gathered (K = 4cs)
+            N, K, G, X, gm, xm, csg, csx = 2 * cs, 4 * cs, other, fmap, 0, 1, 0, cs
+            ref = other.double().t() @ flat.double()
+        else:  # G gathered (N = 4cs), X plain [M][K = 2cs]
+            N, K, G, X, gm, xm, csg, csx = 4 * cs, 2 * cs, fmap, other, 1, 0, cs, 0
+            ref = flat.double().t() @ other.double()
+        dW, db = torch.empty(N * K, device=dev), torch.empty(N, device=dev)
+        nw = query("wgrad_workspace_floats", M, N, K)
+        args = (G, N, gm, X, K, xm, None, 1, M, N, K, gh, gw, csg, csx, dW, db, torch.empty(nw, device=dev), nw, 1)
+        call("wgrad_f32", *args)
+        torch.cuda.synchronize()
+        err = (dW.view(N, K).double() - ref).abs().max().item() / (ref.abs().max().item() + 1e-12)
+        bref = (other if side == "x" else flat).double().sum(0)
+        berr = (db.double() - bref).abs().max().item() / (bref.abs().max().item() + 1e-12)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            call("wgrad_f32", *args)
+        e1.record()
+        torch.cuda.synchronize()
+        key = f"s2d_{side}_M{M}_N{N}_K{K}"
+        print(f"{key}: rel err vs f64 {err:.2e} (db {berr:.2e}), {e0.elapsed_time(e1) / 20 * 1e3:.1f} us per call")
+        assert err < 1e-4 and berr < 1e-4, key
+        out[key + "_dW"], out[key + "_db"] = dW.cpu(), db.cpu()
     torch.save(out, sys.argv[1])
 
 
