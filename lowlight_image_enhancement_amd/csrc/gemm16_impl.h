@@ -837,8 +837,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_glds_kernel(GemmPB p) {
 // the 16-byte chunk index of a row XOR-swizzled by (row / 4) mod 4.  With 64-byte rows the plain layout puts the 16
 // lanes of a store on 4 chunk slots (4-way conflicts; 8-way for the 4-byte gate stores) -- measured 58 % of the
 // conv5-fold kernel's LDS-active cycles as bank conflicts; the 4 rows of a transposed read share row / 4, so they keep
-// one conflict-free 256-byte pattern.  (Not in the conv1 fold: its dt1 stage has 192-byte rows, and the extra address
-// registers spill its 256 VGPRs.)
+// one conflict-free 256-byte pattern.  (Not in the conv1 fold: at its 256 VGPRs even the one-XOR-per-side form spills
+// 2 in the fp16 build, measured -0.3 % against its 32 % conflicted LDS cycles; profiles/r05_swz1/.)
 __device__ __forceinline__ int fswz(int row, int col) {
   return (col & ~31) | ((((col >> 3) ^ (row >> 2)) & 3) << 3) | (col & 7);
 }
