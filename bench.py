@@ -174,12 +174,6 @@ def cost_sg_rc_wg(a):  # cost_sg_rc + the folded weight gradients U = dout^T g, 
     return fl + 2.0 * M * N * N + 2.0 * M * 2 * N * K, by
 
 
-def cost_res_ffn(a):  # (g,a,rows,W3,b3,x,beta,l2w,l2b,y,n2,st2,W4,b4,W5,b5,gamma,lw,lb,out,nout,st,M,C,eps,dt)
-    M, c = a[22], a[23]
-    by = (2 * M * c + 4 * M * c + (M * c if a[20] is not None else 0)) * 2 + 8 * M * (2 if a[20] is not None else 1)
-    return 2.0 * M * c * c + 2.0 * M * c * 2 * c + 2.0 * M * c * c, by
-
-
 def cost_dgrad_ln_wg(a):  # cost_dgrad_ln + the folded conv1 weight gradient dW1 = dt1^T n1 (n1 rebuilt, not read)
     fl, by = cost_dgrad_ln(a)
     M, N, K = a[4], a[5], a[6]
@@ -272,7 +266,7 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_dw_bwd,
            "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd), "gemm_ffn": rec_plain("gemm16", cost_ffn),
            "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg),
-           "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "gemm_res_ffn": rec_plain("gemm16", cost_res_ffn), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
+           "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
            "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile), "c1dw_bwd_tile": rec_c1dw_bwd}
 
 
@@ -402,8 +396,6 @@ def make_trainer(dev, workload, precision, seed=0):
         net.c1dw_tile_channels = tuple(int(c) for c in tc.split(",") if c)
     if os.environ.get("NBP_LN_WG") == "0":  # A/B only: the separate level-0 conv1 weight-gradient launch
         net.ln_wg = False
-    if os.environ.get("NBP_RESFFN") == "0":  # A/B only: level-0 conv3 and the FFN half as two launches
-        net.fuse_resffn = False
     return NBPTrainer(net, psf_mode="rgb", psf_spec=spec, **wl["w"]), init_sd
 
 

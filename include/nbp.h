@@ -151,16 +151,6 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
 int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5, const float* b5, const void* y,
                  const float* gamma, const float* lnw, const float* lnb, void* out, void* nout, float* stats, int M,
                  int C, float eps, int dtype, nbp_stream_t s);
-/* The level-0 NAFBlock's second half in one pass (NAFNet_arch.py:70-80; C = 32): nbp_gemm_res_ln's conv3 (A = g with
- * the per-image SCA column scale a, rows_per_img = H*W) -> y = x + beta (.) (g a W3^T + b3), n2 / st2 = norm2(y), then
- * nbp_gemm_ffn on that n2 tile (held on chip, not re-read) with the y rows kept in registers: out = y + gamma (.) (SG(n2
- * W4^T + b4) W5^T + b5) and, when nout is given, the next block's norm1 of out into nout / stats.  y, n2, st2, out, nout,
- * stats bit for bit the two launches'. */
-int nbp_gemm_res_ffn(const void* g, const float* a, int rows_per_img, const void* W3, const float* b3, const void* x,
-                     const float* beta, const float* ln2w, const float* ln2b, void* y, void* n2, float* st2,
-                     const void* W4, const float* b4, const void* W5, const float* b5, const float* gamma,
-                     const float* lnw, const float* lnb, void* out, void* nout, float* stats, int M, int C, float eps,
-                     int dtype, nbp_stream_t s);
 /* conv5 input gradient + SimpleGate backward with the gate input recomputed (bf16, N = K = C = 32: level 0, whose conv4
  * forward runs on the same skinny MFMA sequence): dg = A . Wt^T (the conv5 dgrad), t = A2 . W2^T + b2 rebuilt per tile (the conv4 forward: A2 = its input n2 [M][K],
  * W2 [2N][K] bf16 with SimpleGate pairs interleaved, b2 fp32), C[m][2c] = dg[c] t[2c+1], C[m][2c+1] = dg[c] t[2c]

@@ -26,7 +26,7 @@ namespace {
 // (acc = dg for column c; with R = t interleaved: C[2c] = dg * t[2c+1], C[2c+1] = dg * t[2c], row stride ldc).
 enum { AM_PLAIN = 0, AM_S2D = 1, AM_SCALE = 2, AM_IM2COL = 3, AM_CONV = 4 };
 enum { CM_PLAIN = 0, CM_D2S = 1, CM_RELU = 2, CM_MASK = 3, CM_SG = 4, CM_SGBWD = 5, CM_LNBWD = 6, CM_RESLN = 7,
-       CM_CHANDOT = 8, CM_SGBWD_RC = 9, CM_FFN = 10, CM_RESFFN = 11 };
+       CM_CHANDOT = 8, CM_SGBWD_RC = 9, CM_FFN = 10 };
 
 struct GemmPB {
   const void* A;
@@ -884,16 +884,6 @@ struct SkinnyP {
   float* slab_v;
   float* slab_w2;
   float* slab_b2;
-  // CM_RESFFN (the level-0 conv3 epilogue and the FFN half in one pass): W / bias / R / rscale / lnw / lnb_f / C /
-  // nout / stats_out are conv3 + norm2's (CM_RESLN), W2 / b2 conv4's (CM_FFN); conv5 and the next norm1:
-  const H* W3;          // conv5 weight [N][N]
-  const float* b3;      // conv5 bias
-  const float* rscale3; // gamma
-  H* C3;                // the block output
-  const float* lnw3;    // the next block's norm1 (with nout3 / stats_out3; null: none)
-  const float* lnb3;
-  H* nout3;
-  float2* stats_out3;
 };
 
 // CM_FFN (the level-0 NAFBlock FFN half, NAFNet_arch.py:74-80, N = K = 32): conv4 -> SimpleGate -> conv5 in one pass.
@@ -909,16 +899,14 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   constexpr int LDT = NT * 32 + 4;  // fp32 row stride of the wave's staging tile
   constexpr bool FFN = CMODE == CM_FFN;
   static_assert(!FFN || (NT == 1 && KS == 2), "FFN fusion: the level-0 block (N = K = 32)");
-  constexpr bool RF = CMODE == CM_RESFFN;
-  static_assert(!RF || (NT == 1 && KS == 2), "conv3 + FFN fusion: the level-0 block (N = K = 32)");
-  constexpr bool RESLN = CMODE == CM_RESLN || FFN || RF;
+  constexpr bool RESLN = CMODE == CM_RESLN || FFN;
   constexpr bool RC = CMODE == CM_SGBWD_RC;
   constexpr bool WGR = WGF && RC;                 // conv5's U / V + conv4's dW / db (nbp_dgrad_sg_rc_wg)
   constexpr bool WG1 = WGF && CMODE == CM_LNBWD;  // conv1's dW / db (nbp_dgrad_ln_bwd_wg)
   static_assert(!WGF || (WGR && NT == 1 && KS == 2) || (WG1 && NT == 1 && KS == 4),
                 "weight-gradient folds: level-0 conv5 dgrad (N = K = 32), level-0 conv1 dgrad (N = 32, K = 64)");
   // bf16 row stride of the recomputed gate-input tile (RC) / of the rebuilt n1 tile (WG1)
-  constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : (WG1 ? 32 : (RF ? 40 : 8));
+  constexpr int LDT2 = RC ? 2 * NT * 32 + 8 : (WG1 ? 32 : 8);
   __shared__ float stage[4][32 * LDT];
   __shared__ __attribute__((aligned(16))) H stage2[4][32 * LDT2];
   // WGF: the tile's dt (32 rows x 64, 192-byte rows: conflict-free ds_read_b64_tr_b16), later the block's reduction
@@ -928,15 +916,10 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
   H* tileT = stage2[threadIdx.x >> 6];
   const int M = p.M, N = p.N, K = p.K;
   // RC / FFN: the conv4 weight (2N rows, K = the conv4 input width = this GEMM's K) and bias in registers
-  constexpr int NT2 = RC || FFN || RF ? 2 * NT : 1;
+  constexpr int NT2 = RC || FFN ? 2 * NT : 1;
   vec_t<H, 8> w2[NT2][KS];
   float b2r[NT2][4][4];
-  vec_t<H, 8> w5[RF ? KS : 1];  // RF: conv5's weight (the B-operand of its MFMAs, as CM_FFN's w)
-  if constexpr (RF) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) w5[ks] = *reinterpret_cast<const vec_t<H, 8>*>(p.W3 + (long)r * N + ks * 16 + 8 * h);
-  }
-  if constexpr (RC || FFN || RF) {
+  if constexpr (RC || FFN) {
 #pragma unroll
     for (int t = 0; t < NT2; ++t) {
 #pragma unroll
@@ -1207,7 +1190,7 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
         *reinterpret_cast<vec_t<H, 8>*>(p.C + m * p.ldc + ccol) = o;
       }
     }
-    for (int rr = lane / cpr; !PRE && !RF && rr < 32; rr += rstep) {
+    for (int rr = lane / cpr; !PRE && rr < 32; rr += rstep) {
       const long m = m0 + rr;
       if (m >= M) {
         if constexpr (WGR) {  // the fold's dt tile: zero rows past M (their n2 rows are zero, stale data could be NaN)
@@ -1312,152 +1295,6 @@ void gemm_skinny_kernel(SkinnyP<H> p) {
           gv[j] = (H)pr;
         }
         *reinterpret_cast<vec_t<H, 4>*>(p.aux + m * (p.ldc / 2) + ccol / 2) = gv;
-      }
-    }
-    if constexpr (RF) {
-      // epilogue 1 (CM_RESLN's arithmetic): y = x + beta (conv3 + b3) stored, n2 = norm2(y) stored with its statistics
-      // and kept in the wave's LDS tile; y kept in registers for conv5's residual
-      constexpr int G = 4 * NT;
-      vec_t<H, 8> yk[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int rr = lane / cpr + q * rstep;
-        const long m = m0 + rr;
-        if (m < M) {
-          const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
-          const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
-          float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += bia[j];
-          const long off = m * p.ldc + ccol;
-          const vec_t<H, 8> rv = *reinterpret_cast<const vec_t<H, 8>*>(p.R + off);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (float)rv[j] + rsc[j] * v[j];
-          vec_t<H, 8> o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (H)v[j];
-          *reinterpret_cast<vec_t<H, 8>*>(p.C + off) = o;
-          yk[q] = o;
-          float xv[8], sm = 0.f, qs = 0.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            xv[j] = (float)o[j];
-            sm += xv[j];
-          }
-          sm = group_sum<G>(sm);
-          const float mu = sm / (float)N;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = xv[j] - mu;
-            qs = fmaf(d, d, qs);
-          }
-          qs = group_sum<G>(qs);
-          const float dd = sqrtf(qs / (float)N + p.eps), inv = 1.f / dd;
-          vec_t<H, 8> nn;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) nn[j] = (H)fmaf(aw[j], (xv[j] - mu) * inv, ab[j]);
-          *reinterpret_cast<vec_t<H, 8>*>(p.nout + m * N + ccol) = nn;
-          if (ccol == 0) p.stats_out[m] = make_float2(mu, dd);
-          *reinterpret_cast<vec_t<H, 8>*>(tileT + rr * LDT2 + ccol) = nn;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      // conv4 -> SimpleGate -> conv5 on the n2 tile: CM_FFN's sequence with the conv4 fragments read from LDS
-      vec_t<H, 8> af[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) af[ks] = *reinterpret_cast<const vec_t<H, 8>*>(tileT + r * LDT2 + ks * 16 + 8 * h);
-      vec_t<H, 2> gp[NT2][4];
-#pragma unroll
-      for (int t2 = 0; t2 < NT2; ++t2) {
-        floatx16 a2c;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) a2c[i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) a2c = mfma32x32x16(w2[t2][ks], af[ks], a2c);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float pr0 = (a2c[4 * g] + b2r[t2][g][0]) * (a2c[4 * g + 1] + b2r[t2][g][1]);
-          float pr1 = (a2c[4 * g + 2] + b2r[t2][g][2]) * (a2c[4 * g + 3] + b2r[t2][g][3]);
-          asm volatile("" : "+v"(pr0), "+v"(pr1));  // an fp32 product, then one rounding (as CM_FFN / CM_SG)
-          gp[t2][g][0] = (H)pr0;
-          gp[t2][g][1] = (H)pr1;
-        }
-      }
-      floatx16 acc5;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc5[i] = 0.f;
-#pragma unroll
-      for (int t2 = 0; t2 < NT2; ++t2) {
-        const vec_t<H, 2> s0 = h ? gp[t2][0] : gp[t2][2], s1 = h ? gp[t2][1] : gp[t2][3];
-        const vec_t<H, 2> r0 = __builtin_bit_cast(vec_t<H, 2>, __shfl_xor(__builtin_bit_cast(int, s0), 32, 64));
-        const vec_t<H, 2> r1 = __builtin_bit_cast(vec_t<H, 2>, __shfl_xor(__builtin_bit_cast(int, s1), 32, 64));
-        const vec_t<H, 2> q0 = h ? r0 : gp[t2][0], q1 = h ? gp[t2][2] : r0;
-        const vec_t<H, 2> q2 = h ? r1 : gp[t2][1], q3 = h ? gp[t2][3] : r1;
-        vec_t<H, 8> bg;
-        bg[0] = q0[0]; bg[1] = q0[1]; bg[2] = q1[0]; bg[3] = q1[1];
-        bg[4] = q2[0]; bg[5] = q2[1]; bg[6] = q3[0]; bg[7] = q3[1];
-        acc5 = mfma32x32x16(w5[t2], bg, acc5);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(tileS + r * LDT + 8 * g + 4 * h) =
-            make_float4(acc5[4 * g], acc5[4 * g + 1], acc5[4 * g + 2], acc5[4 * g + 3]);
-      __builtin_amdgcn_wave_barrier();
-      // epilogue 2 (CM_FFN's): out = y + gamma (conv5 + b5), the next block's norm1 when nout3 is given
-      float b5[8], gm[8], lw[8], lb[8];
-      {
-        const float4 x0 = ld4(p.b3 + ccol), x1 = ld4(p.b3 + ccol + 4), y0 = ld4(p.rscale3 + ccol),
-                     y1 = ld4(p.rscale3 + ccol + 4);
-        b5[0] = x0.x; b5[1] = x0.y; b5[2] = x0.z; b5[3] = x0.w; b5[4] = x1.x; b5[5] = x1.y; b5[6] = x1.z; b5[7] = x1.w;
-        gm[0] = y0.x; gm[1] = y0.y; gm[2] = y0.z; gm[3] = y0.w; gm[4] = y1.x; gm[5] = y1.y; gm[6] = y1.z; gm[7] = y1.w;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) lw[j] = lb[j] = 0.f;
-        if (p.nout3) {
-          const float4 w0 = ld4(p.lnw3 + ccol), w1 = ld4(p.lnw3 + ccol + 4), c0 = ld4(p.lnb3 + ccol),
-                       c1 = ld4(p.lnb3 + ccol + 4);
-          lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
-          lb[0] = c0.x; lb[1] = c0.y; lb[2] = c0.z; lb[3] = c0.w; lb[4] = c1.x; lb[5] = c1.y; lb[6] = c1.z; lb[7] = c1.w;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int rr = lane / cpr + q * rstep;
-        const long m = m0 + rr;
-        if (m < M) {
-          const float4 u0 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol);
-          const float4 u1 = *reinterpret_cast<const float4*>(tileS + rr * LDT + ccol + 4);
-          float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] += b5[j];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (float)yk[q][j] + gm[j] * v[j];
-          vec_t<H, 8> o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = (H)v[j];
-          *reinterpret_cast<vec_t<H, 8>*>(p.C3 + m * N + ccol) = o;
-          if (p.nout3) {
-            float xv[8], sm = 0.f, qs = 0.f;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              xv[j] = (float)o[j];
-              sm += xv[j];
-            }
-            sm = group_sum<G>(sm);
-            const float mu = sm / (float)N;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float d = xv[j] - mu;
-              qs = fmaf(d, d, qs);
-            }
-            qs = group_sum<G>(qs);
-            const float dd = sqrtf(qs / (float)N + p.eps), inv = 1.f / dd;
-            vec_t<H, 8> nn;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) nn[j] = (H)fmaf(lw[j], (xv[j] - mu) * inv, lb[j]);
-            *reinterpret_cast<vec_t<H, 8>*>(p.nout3 + m * N + ccol) = nn;
-            if (ccol == 0) p.stats_out3[m] = make_float2(mu, dd);
-          }
-        }
       }
     }
     __builtin_amdgcn_wave_barrier();

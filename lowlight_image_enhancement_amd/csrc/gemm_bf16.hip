@@ -184,35 +184,6 @@ int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5
   return check_launch("gemm_ffn");
 }
 
-int nbp_gemm_res_ffn(const void* g, const float* a, int rows_per_img, const void* W3, const float* b3, const void* x,
-                     const float* beta, const float* ln2w, const float* ln2b, void* y, void* n2, float* st2,
-                     const void* W4, const float* b4, const void* W5, const float* b5, const float* gamma,
-                     const float* lnw, const float* lnb, void* out, void* nout, float* stats, int M, int C, float eps,
-                     int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(g && a && rows_per_img > 0 && W3 && b3 && x && beta && ln2w && ln2b && y && n2 && st2 && W4 && b4 &&
-              W5 && b5 && gamma && out && M > 0, "nbp_gemm_res_ffn: bad args");
-  NBP_REQUIRE(!nout || (lnw && lnb && stats), "nbp_gemm_res_ffn: the next LayerNorm needs lnw, lnb, stats");
-  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_gemm_res_ffn: 16-bit storage (dtype 1 bf16 / 2 fp16)");
-  NBP_REQUIRE(C == 32, "nbp_gemm_res_ffn: the fused conv3 + FFN serves C = 32 (C=%d)", C);
-  NBP_DISPATCH_H(dtype, {
-    SkinnyP<H> p{reinterpret_cast<const H*>(g), C, a, rows_per_img, reinterpret_cast<const H*>(W3), C,
-                 reinterpret_cast<H*>(y), C, M, C, C, b3, reinterpret_cast<const H*>(x), beta, nullptr,
-                 nullptr, ln2w, nullptr, nullptr, nullptr, ln2b, reinterpret_cast<H*>(n2),
-                 reinterpret_cast<float2*>(st2), eps, nullptr, reinterpret_cast<const H*>(W4), b4};
-    p.W3 = reinterpret_cast<const H*>(W5);
-    p.b3 = b5;
-    p.rscale3 = gamma;
-    p.C3 = reinterpret_cast<H*>(out);
-    p.lnw3 = lnw;
-    p.lnb3 = lnb;
-    p.nout3 = reinterpret_cast<H*>(nout);
-    p.stats_out3 = reinterpret_cast<float2*>(stats);
-    gemm_skinny_kernel<1, 2, AM_SCALE, CM_RESFFN, H>
-        <<<dim3((unsigned)skinny_grid<1, 2, AM_SCALE, CM_RESFFN, H>(M)), 256, 0, S(s)>>>(p);
-  });
-  return check_launch("gemm_res_ffn");
-}
-
 int nbp_dgrad_sg_rc(const void* A, long lda, const void* Wt, long ldb, const void* A2, const void* W2, const float* b2,
                     void* C, int M, int N, int K, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(A && Wt && A2 && W2 && b2 && C && M > 0, "nbp_dgrad_sg_rc: bad args");

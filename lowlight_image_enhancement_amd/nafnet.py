@@ -110,8 +110,6 @@ class NAFNet(nn.Module):
         # level 0 with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
         # (nbp_gemm_ffn, bitwise the two launches, +0.1 % step), g2 never stored
         self.fuse_ffn = True
-        # ... and conv3's epilogue (y, norm2) in the same pass: n2 / y not re-read (nbp_gemm_res_ffn, bitwise)
-        self.fuse_resffn = False
         # level 0: conv1's weight / bias gradients folded into the conv1 dgrad + norm1 backward pass (nbp_dgrad_ln_bwd_wg:
         # n1 rebuilt from x and the LN statistics, dt1 already in registers; False: a separate nbp_wgrad_f32 launch)
         self.ln_wg = True
@@ -446,17 +444,7 @@ class NAFNet(nn.Module):
                  t2, g, pool, B, h, w, c, dt)
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"),
              mean, a, B, hw, c)
-        resffn = fuse_ln and ffn and self.fuse_resffn
-        if resffn:
-            lnw, lnb = ((self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"))
-                        if carry_next else (None, None))
-            call("gemm_res_ffn", g, a, hw, self._slice(self._W[1], pre + "conv3.weight"),
-                 self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
-                 self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), y, n2, st2,
-                 self._slice(self._W[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"),
-                 self._slice(self._W[1], pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
-                 self._slice(P, pre + "gamma"), lnw, lnb, out, nn1, nst1, M, c, LN_EPS, dt)
-        elif fuse_ln:
+        if fuse_ln:
             call("gemm_res_ln", g, c, AM_SCALE, a, hw, self._slice(self._W[1], pre + "conv3.weight"), c, y,
                  M, c, c, self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
                  self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS,
@@ -466,9 +454,7 @@ class NAFNet(nn.Module):
                      bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
             call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"),
                  n2, st2, M, c, LN_EPS, dt)
-        if resffn:
-            pass  # (the FFN half ran with conv3 above)
-        elif ffn:
+        if ffn:
             lnw, lnb = ((self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"))
                         if carry_next else (None, None))
             call("gemm_ffn", n2, self._slice(self._W[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"),
