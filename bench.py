@@ -82,22 +82,40 @@ ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
 ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
                    "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel", "wgrad_narrow_full"], "wgrad_group": ["wgrad_bf16_wide_group"],
                    "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
-                   "dw_bwd": ["dw_bwd_tiled"], "dw_bwd_32": ["dw_bwd_tiled<T, true, 32>"],
-                   "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"],
-                   "c1dw_tile_fwd": ["c1dw_fwd_tile"], "c1dw_tile_bwd": ["c1dw_bwd_tile"],
-                   "c1dw_bwd_L0": ["c1dw_bwd_tile<T, 32>"]}
-# classes that are ONE kernel (one template instance in the step): the headline `roofline` is the one of them with the
-# most time per step (the dominant kernel); the multi-kernel classes are reported beside it
-SINGLE_KERNEL = ("dw_bwd_32", "wgrad_group", "reduce", "c1dw_bwd_L0")
+                   "dw_bwd": ["dw_bwd_tiled"], "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"],
+                   "c1dw_tile_fwd": ["c1dw_fwd_tile"], "c1dw_tile_bwd": ["c1dw_bwd_tile"]}
+# ONE-kernel classes (one template instance each), timed per launch inside the library (nbp_launch_timing: events
+# around that launch alone on its stream) and keyed by the instance name the library records; the headline `roofline`
+# is the one with the most time per step (the dominant kernel).  Their rocprof names, as regexes over the mangled
+# names of kernel_stats.csv (exactly one instance per regex and dtype: tests/test_bench_launch.py checks the committed
+# record).
+INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_bwd_L1",
+             "dw_bwd_tiled<T,true,32>": "dw_bwd_32", "dw_bwd_tiled<T,true,16>": "dw_bwd_16",
+             "wgrad_bf16_wide_group<3,512,2>": "wgrad_group_512", "wgrad_bf16_wide_group<3,768,4>": "wgrad_group_768",
+             "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad"}
+SINGLE_KERNEL = tuple(INSTANCES.values())
+ROCPROF_KERNELS.update({
+    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32EE"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64EE"],
+    "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32EE"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16EE"],
+    "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
+    "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],
+    "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"]})
+# the Itanium mangling of the storage type in those names
+MANGLED_T = {"fp16": "DF16_", "bf16": "DF16b", "fp32": "f"}
 UNIT_DEF = {
     "dw_bwd_32": "SURVEY §8(d)-style per pixel: dh C + t2 2C + t1 2C read, dt1 2C written = 7*C*s bytes per pixel "
                  "(s = storage bytes), x B*H*W pixels of the launch (the 32-wide tile kernel at the levels that store "
                  "the tape: 2-3 at cfg2; levels 0-1 rebuild it in c1dw_bwd_tile)",
-    "wgrad_group": "per grouped launch: each queued problem's operands read once, M*(N+K)*s, + its fp32 dW (+db) "
-                   "written once; the split-M fp32 slabs the launch writes instead are `slab_bytes_per_step`",
-    "reduce": "per reduce_multi_kernel launch: the fp32 slabs read once + the reduced outputs written once",
+    "dw_bwd_16": "as dw_bwd_32 (7*C*s bytes per pixel), the 16-wide tile kernel (the 16 x 16 level)",
+    "wgrad_group_512": "per grouped launch of this instance (128-column tiles): each problem's operands read once, "
+                       "M*(N+K)*s, + its fp32 dW (+db) written once; the split-M fp32 slabs it writes instead are the "
+                       "wgrad_group class's `slab_bytes_per_step`",
+    "wgrad_group_768": "as wgrad_group_512, the 256-column-tile instance (the 16 x 16 level's plain problems, unsplit)",
+    "reduce_multi": "per reduce_multi_kernel launch: the fp32 slabs read once + the reduced outputs written once",
+    "layer_scale_grad": "per layer_scale_grad_kernel launch: U, V, W, b read, dW, db, dscale written (fp32)",
     "c1dw_bwd_L0": "per pixel: dh C + n1 C read, dt1 2C written = 4*C*s bytes (s = storage bytes; t1 / t2 rebuilt on "
-                   "chip, never read), x B*H*W pixels of the launch (level 0: C 32 at 256^2)",
+                   "chip, never read), x B*H*W pixels of the launch (level 0: C 32 at 256^2), + the conv1 weight",
+    "c1dw_bwd_L1": "as c1dw_bwd_L0 at level 1 (C 64 at 128^2)",
 }
 
 
@@ -197,12 +215,6 @@ def cost_c1dw_bwd_tile(a):  # (dh,a,ds,n1,w1,b1,wdw,bdw,dt1,dwdw,dbdw,ws,B,h,w,c
     return 2.0 * M * 2 * c * c + 3 * 2.0 * M * 2 * c * 9, (4 * M * c + 2 * c * c) * _e(a[16])
 
 
-def rec_c1dw_bwd(a):
-    fl, by = cost_c1dw_bwd_tile(a)
-    out = [("c1dw_tile_bwd", fl, by, 1, 0.0)]
-    if a[15] == 32:  # the level-0 instance c1dw_bwd_tile<T, 32>
-        out.append(("c1dw_bwd_L0", fl, by, 1, 0.0))
-    return out
 
 
 def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
@@ -246,14 +258,6 @@ def rec_flush(a):
     return [("reduce", 0.0, st[1] + st[2], int(st[3]), 0.0)]
 
 
-def rec_dw_bwd(a):
-    fl, by = cost_dw_bwd(a)
-    out = [("dw_bwd", fl, by, 1, 0.0)]
-    if a[12] >= 32:  # dw_bwd_tw(W): the 32-wide tile kernel dw_bwd_tiled<T, true, 32>
-        out.append(("dw_bwd_32", fl, by, 1, 0.0))
-    return out
-
-
 def _lib_stats(which):
     from lowlight_image_enhancement_amd import _lib
     return _lib.last_call_stats(which)
@@ -263,24 +267,29 @@ def _lib_stats(which):
 ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_plain("gemm16", cost_res_ln),
            "dgrad_ln_bwd": rec_plain("gemm16", cost_dgrad_ln), "dgrad_sg_rc": rec_plain("gemm16", cost_sg_rc),
            "gemm_f32": rec_plain("gemm_f32", cost_gemm_f32), "wgrad_f32": rec_wgrad, "wgrad_group": rec_wgroup,
-           "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_dw_bwd,
+           "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_plain("dw_bwd", cost_dw_bwd),
            "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd), "gemm_ffn": rec_plain("gemm16", cost_ffn),
            "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg),
            "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
-           "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile), "c1dw_bwd_tile": rec_c1dw_bwd}
+           "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile),
+           "c1dw_bwd_tile": rec_plain("c1dw_tile_bwd", cost_c1dw_bwd_tile)}
+
+
+def _pmc_newest_key(f):
+    """Record order under profiles/: round number first, a round's "final" record after its numbered ones (r04_final >
+    r04_v1)."""
+    import re
+    rel = os.path.relpath(f, os.path.join(ROOT, "profiles"))
+    nums = [int(t) for t in re.findall(r"\d+", rel)]
+    return (nums[:1], "final" in rel, nums)
 
 
 def _pmc_traffic(cls):
     """HBM bytes per launch of a kernel class from the newest committed PMC record (profiles/[*/]*pmc_traffic.json,
     scripts/pmc_pass.sh + scripts/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled)."""
     import glob
-    import re
-    def newest(f):  # round number first, a round's "final" record after its numbered ones (r04_final > r04_v1)
-        rel = os.path.relpath(f, os.path.join(ROOT, "profiles"))
-        nums = [int(t) for t in re.findall(r"\d+", rel)]
-        return (nums[:1], "final" in rel, nums)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))
-                   + glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc_traffic.json")), key=newest)
+                   + glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc_traffic.json")), key=_pmc_newest_key)
     if not files:
         return None, None
     rec = json.load(open(files[-1])).get("classes", {}).get(cls)
@@ -289,7 +298,7 @@ def _pmc_traffic(cls):
     return round(rec["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
-def _class_line(cls, v, steps, peak_tf):
+def _class_line(cls, v, steps, peak_tf, mt):
     """One kernel class of the profiled pass, per KERNEL launch (the unit of the PMC traffic record) and per step:
     launches, average launch, algorithmic bytes / FLOPs, the fraction of the HBM and MFMA roofs they reach, the PMC
     traffic and its ratio to the algorithmic bytes, and the fp32 split-M slab bytes the class writes (read back by
@@ -299,7 +308,7 @@ def _class_line(cls, v, steps, peak_tf):
     tfl = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     traffic, _ = _pmc_traffic(cls)
     alg = by / max(nl, 1)
-    line = {"rocprof_kernels": ROCPROF_KERNELS[cls], "ms_per_step": round(ms / steps, 3),
+    line = {"rocprof_kernels": [r.format(T=mt) for r in ROCPROF_KERNELS[cls]], "ms_per_step": round(ms / steps, 3),
             "launches_per_step": round(nl / steps, 2), "c_abi_calls_per_step": round(ncall / steps, 2),
             "avg_launch_us": round(ms * 1e3 / max(nl, 1), 2), "algorithmic_bytes_per_launch": round(alg),
             "algorithmic_bytes_per_step": round(by / steps), "algorithmic_flops_per_launch": round(fl / max(nl, 1)),
@@ -408,23 +417,32 @@ def batch(dev, B, img, rank):
 
 
 def raw_metric(tr, b, ratios):
-    """cfg5's linear-domain metric on the trainer's last output: phys_cons_raw(pred, short, psf, expo_ratio) with the
-    images' ratios cycling through `ratios`, fp16 inputs (the metric accumulates in fp32, phys_consistency.py:302-303),
-    mean and per-image values."""
+    """cfg5's linear-domain metric on the trainer's last output: phys_cons_raw(pred, short, psf, expo_ratio)
+    (metrics/phys_consistency.py:193-320: y_hat = psf * pred, times the ratio, against the observation, valid crop),
+    fp16 inputs (the metric accumulates in fp32, phys_consistency.py:302-303).  The observation is built from the bench
+    batch's ground truth with the SAME forward model and ratios (obs = ratio * psf(gt), reflect padding), so that
+    phys_cons_raw(gt, obs) is ~0 (`gt_mean`, the fp16 rounding of the inputs) and the value for the output measures its
+    distance from the physically consistent image; the training step itself runs on the bench's own synthetic pair."""
+    import torch.nn.functional as Fn
     from lowlight_image_enhancement_amd.metrics.phys_consistency import phys_cons_raw
     out = tr._graph_out if getattr(tr, "_graph", None) is not None else None
     if out is None:
         out = tr.net(b[0])
     B = out.shape[0]
     r = torch.tensor([ratios[i % len(ratios)] for i in range(B)], device=out.device)
-    pred, obs = out.detach().clamp_min(0).half(), b[2].half()
     k = tr.kernel  # [3, 1, 3, 3] depthwise crosstalk PSF -> the metric's [C_out, C_in, 3, 3] form (diagonal)
     psf = torch.zeros(k.shape[0], k.shape[0], k.shape[2], k.shape[3], device=k.device)
     for c in range(k.shape[0]):
         psf[c, c] = k[c, 0]
-    per = phys_cons_raw(pred, obs, psf, r, reduction="none")
+    gt = b[1].float()
+    kn = k / k.sum(dim=(2, 3), keepdim=True)  # the metric's normalize_psf (the trainer's kernel is normalised already)
+    obs = Fn.conv2d(Fn.pad(gt, (1, 1, 1, 1), mode="reflect"), kn, groups=k.shape[0]) * r.view(B, 1, 1, 1)
+    obs = obs.half()
+    per = phys_cons_raw(out.detach().clamp_min(0).half(), obs, psf, r, reduction="none")
+    per_gt = phys_cons_raw(gt.half(), obs, psf, r, reduction="none")
     return {"mean": round(float(per.mean()), 6), "per_image": [round(float(v), 6) for v in per.flatten()],
-            "expo_ratio": [float(v) for v in r.tolist()], "inputs": "fp16 (output clamp_min 0, short)"}
+            "gt_mean": round(float(per_gt.mean()), 6), "expo_ratio": [float(v) for v in r.tolist()],
+            "obs": "ratio * psf(gt) (reflect pad), fp16", "inputs": "fp16 (output clamp_min 0)"}
 
 
 def short_run(dev, workload, precision, steps=5, warmup=3):
@@ -585,6 +603,7 @@ def main():
 
     net._block_fwd, net._block_bwd = timed(orig_fwd, "fwd"), timed(orig_bwd, "bwd")
     step_events = []
+    _lib.launch_timing(True)  # the one-kernel classes: events around each of their launches inside the library
     tr.comm_probe = world > 1  # the eager steps' exposed all-reduce time (not NAFBlock time, not the rest either)
     for _ in range(args.steps):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -595,6 +614,12 @@ def main():
         step_events.append((e0, e1))
     torch.cuda.synchronize()
     _lib.PROFILE.clear()
+    inst = {}
+    for name, ms_, fl_, by_ in _lib.launch_timing_records():
+        if name in INSTANCES:
+            v = inst.setdefault(INSTANCES[name], [0.0, 0.0, 0.0, 0, 0, 0.0])
+            v[0] += ms_; v[1] += fl_; v[2] += by_; v[3] += 1; v[4] += 1  # noqa: E702
+    _lib.launch_timing(False)
     net._block_fwd, net._block_bwd = orig_fwd, orig_bwd
     eager_comm = tr.comm_stats() if world > 1 else None
     tr.comm_probe, tr.comm_events = False, []
@@ -647,7 +672,8 @@ def main():
         ms = sum(e0.elapsed_time(e1) for *_, e0, e1 in recs)
         classes[cls] = (ms, sum(r[0] for r in recs), sum(r[1] for r in recs), sum(r[2] for r in recs), len(recs),
                         sum(r[3] for r in recs))
-    # the dominant KERNEL: the single-kernel line with the most time per step
+    classes.update({k: tuple(v) for k, v in inst.items()})
+    # the dominant KERNEL: the one-instance line with the most time per step
     dom = max((k for k in classes if k in SINGLE_KERNEL), key=lambda k: classes[k][0])
     ms, fl, by, nl, _, _ = classes[dom]
     peak_tf = FP32_PEAK_TFLOPS if args.precision == "fp32" else MFMA16_PEAK_TFLOPS
@@ -661,7 +687,10 @@ def main():
         roof = {"bound": "mfma", "achieved": round(tflops, 3), "peak": peak_tf, "unit": "TFLOP/s",
                 "frac": round(tflops / peak_tf, 4)}
     traffic, tsrc = _pmc_traffic(dom)
-    roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel": dom, "rocprof_kernels": ROCPROF_KERNELS[dom],
+    roof.update({"traffic": traffic, "traffic_source": tsrc, "kernel": dom,
+                 "rocprof_kernels": [r.format(T=MANGLED_T[args.precision]) for r in ROCPROF_KERNELS[dom]],
+                 "timing": "HIP events around each launch of this instance inside the library (nbp_launch_timing), "
+                           "eager profiled steps",
                  "launches_per_step": round(nl / args.steps, 2), "ms_per_step": round(ms / args.steps, 3),
                  "avg_launch_us": round(ms * 1e3 / nl, 2), "algorithmic_bytes_per_launch": round(by / max(nl, 1)),
                  "algorithmic_bytes_per_step": round(by / args.steps),
@@ -669,7 +698,8 @@ def main():
                  "algorithmic_bytes_definition": UNIT_DEF[dom],
                  "algorithmic_flops_per_launch": round(fl / max(nl, 1)), "flop_intensity": round(fl / max(by, 1), 2),
                  "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_tf, 4),
-                 "classes": {k: _class_line(k, v, args.steps, peak_tf) for k, v in classes.items()}})
+                 "classes": {k: _class_line(k, v, args.steps, peak_tf, MANGLED_T[args.precision])
+                             for k, v in classes.items()}})
     blk_ms = sum(e0.elapsed_time(e1) for e0, e1, _, _ in blk_events) / args.steps
     eager_step_ms = sum(e0.elapsed_time(e1) for e0, e1 in step_events) / args.steps
     per_level = {}

@@ -204,6 +204,14 @@ int nbp_grad_reduce_flush(int stop, nbp_stream_t s);
  * FLOPs, operand bytes read once, fp32 dW / db bytes, fp32 slab bytes written at the group's M-splits, launches}.
  * Copies min(n, record length) values to out (the rest zero). */
 int nbp_last_call_stats(int which, double* out, int n);
+/* Per-launch timing of the entries that issue several kernel instances in one call (nbp_wgrad_group, the gradient-
+ * reduction flush): nbp_launch_timing(1) clears the record and brackets each such launch of this thread with HIP
+ * events (0: off, the default); nbp_launch_timing_get(i, name, cap, out) waits for record i and returns its kernel
+ * instance name and out = {milliseconds, algorithmic FLOPs, algorithmic bytes}.  Measurement plumbing of bench.py's
+ * per-instance roofline (the reference has no counterpart). */
+int nbp_launch_timing(int on);
+int nbp_launch_timing_count(void);
+int nbp_launch_timing_get(int i, char* name, int cap, double* out);
 int nbp_reduce_slab_batched(const float* slab, int batch, int S, long L, float scale, float* out, nbp_stream_t s);
 
 /* LayerNorm2d / LayerNormFunction (NAFNet_base/basicsr/models/archs/arch_util.py:264-300), NHWC, C any multiple of
@@ -247,8 +255,9 @@ int nbp_c1_dw_sg_pool(const void* n1, const void* w1, const float* b1, const flo
  * dt1 = dw3x3^T(dt2), dt2 = (dg t2[C:], dg t2[:C]), dg = dh a + ds / HW; dwdw / dbdw as nbp_sca_sg_dw_bwd (per-tile
  * slabs in ws, nbp_c1dw_bwd_workspace_floats, reduced with nbp_reduce_slab: deferred when deferral is on).  dt1 bitwise
  * equal to nbp_sca_sg_dw_bwd on the stored tape; dwdw / dbdw up to fp32 summation order.
- * nbp_c1dw_tile_supported(H, W, C, dtype) is 1 for the shapes served. */
-int nbp_c1dw_tile_supported(int H, int W, int C, int dtype);
+ * nbp_c1dw_tile_supported(B, H, W, C, dtype) is 1 for the shapes served (16-bit, C 32 / 64, and B*H*W*C*4 bytes within the
+ * kernels' 32-bit buffer offsets; larger levels take the stored-tape kernels). */
+int nbp_c1dw_tile_supported(int B, int H, int W, int C, int dtype);
 int nbp_c1dw_tile_rows(int H, int W, int C);
 int nbp_c1dw_fwd_tile(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
                       void* t2, void* g, float* pool_slab, int B, int H, int W, int C, int dtype, nbp_stream_t s);

@@ -156,6 +156,27 @@ def last_call_stats(which: int, n: int = 6) -> List[float]:
     return list(buf)
 
 
+def launch_timing(on: bool) -> None:
+    """nbp_launch_timing: bracket each launch of the multi-instance entries (grouped weight gradients, the gradient-
+    reduction flush) with HIP events (bench.py's per-instance roofline); switching clears the record."""
+    lib().dll.nbp_launch_timing(1 if on else 0)
+
+
+def launch_timing_records() -> List[Tuple[str, float, float, float]]:
+    """[(kernel instance, ms, algorithmic FLOPs, algorithmic bytes)] of the launches recorded since launch_timing(True)
+    (waits for each launch's end event)."""
+    L = lib().dll
+    out = []
+    name = ctypes.create_string_buffer(128)
+    buf = (ctypes.c_double * 3)()
+    for i in range(L.nbp_launch_timing_count()):
+        rc = L.nbp_launch_timing_get(i, ctypes.cast(name, ctypes.c_void_p), 128, ctypes.cast(buf, ctypes.c_void_p))
+        if rc != 0:
+            raise NBPError(f"nbp_launch_timing_get failed ({rc}): {L.nbp_last_error_string().decode()}")
+        out.append((name.value.decode(), buf[0], buf[1], buf[2]))
+    return out
+
+
 def require_cuda(*tensors):
     for t in tensors:
         if t is not None and (not t.is_cuda or t.dtype != torch.float32):

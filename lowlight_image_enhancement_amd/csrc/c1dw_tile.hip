@@ -604,10 +604,13 @@ int tile_w(int C) { return C == 32 ? 64 : 32; }
 
 extern "C" {
 
-int nbp_c1dw_tile_supported(int H, int W, int C, int dtype) {
+int nbp_c1dw_tile_supported(int B, int H, int W, int C, int dtype) {
   if (dtype != 1 && dtype != 2) return 0;
   if (C != 32 && C != 64) return 0;
-  return H > 0 && W > 0 ? 1 : 0;
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
+  // every buffer the kernels address (the largest: t1 / t2 / dt1, [M][2C] 16-bit = M * C * 4 bytes) by 32-bit buffer
+  // offsets, with OOB past its end: a masked access must fall outside the range (larger levels take the stored tape)
+  return (long)B * H * W * C * 4 <= (long)OOB ? 1 : 0;
 }
 
 int nbp_c1dw_tile_rows(int H, int W, int C) {
@@ -618,9 +621,9 @@ int nbp_c1dw_tile_rows(int H, int W, int C) {
 int nbp_c1dw_fwd_tile(const void* n1, const void* w1, const float* b1, const float* wdw, const float* bdw, void* t1,
                       void* t2, void* g, float* pool_slab, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(n1 && w1 && b1 && wdw && bdw && g && pool_slab && B > 0, "nbp_c1dw_fwd_tile: null pointer");
-  NBP_REQUIRE(nbp_c1dw_tile_supported(H, W, C, dtype), "nbp_c1dw_fwd_tile: unsupported shape (H %d W %d C %d dtype %d)",
-              H, W, C, dtype);
-  NBP_REQUIRE((long)B * H * W * C * 4 < (1L << 31), "nbp_c1dw_fwd_tile: B*H*W*2C*2 must be < 2^31 (buffer offsets)");
+  NBP_REQUIRE(nbp_c1dw_tile_supported(B, H, W, C, dtype),
+              "nbp_c1dw_fwd_tile: unsupported shape (B %d H %d W %d C %d dtype %d; B*H*W*2C*2 bytes must not exceed "
+              "the out-of-range buffer offset)", B, H, W, C, dtype);
   const int tw = tile_w(C);
   C1TileP p{};
   p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.t1 = t1; p.t2 = t2; p.g = g; p.pool = pool_slab;
@@ -650,9 +653,9 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
                       int W, int C, int dtype, nbp_stream_t s) {
   NBP_REQUIRE(dh && a && ds && n1 && w1 && b1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0,
               "nbp_c1dw_bwd_tile: null pointer");
-  NBP_REQUIRE(nbp_c1dw_tile_supported(H, W, C, dtype), "nbp_c1dw_bwd_tile: unsupported shape (H %d W %d C %d dtype %d)",
-              H, W, C, dtype);
-  NBP_REQUIRE((long)B * H * W * C * 4 < (1L << 31), "nbp_c1dw_bwd_tile: B*H*W*2C*2 must be < 2^31 (buffer offsets)");
+  NBP_REQUIRE(nbp_c1dw_tile_supported(B, H, W, C, dtype),
+              "nbp_c1dw_bwd_tile: unsupported shape (B %d H %d W %d C %d dtype %d; B*H*W*2C*2 bytes must not exceed "
+              "the out-of-range buffer offset)", B, H, W, C, dtype);
   C1TileP p{};
   p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.dh = dh; p.a = a; p.ds = ds; p.dt1 = dt1;
   p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, 32); p.tiles = cdiv(H, CT_TH) * p.tiles_x;
@@ -662,10 +665,16 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
   p.slab_b = ws + nrow * 2 * C * 9;
   const long nblk = nrow * (C / 32);
   NBP_REQUIRE(nblk < (1L << 31), "nbp_c1dw_bwd_tile: grid too large");
+  lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
     if (C == 32) c1dw_bwd_tile<H, 32><<<nblk, 256, 0, S(s)>>>(p);
     else c1dw_bwd_tile<H, 64><<<nblk, 256, 0, S(s)>>>(p);
   });
+  {  // per-launch record (nbp_launch_timing): dh C + n1 C in, dt1 2C out, the conv1 weight slice per slice
+    const double M = (double)B * H * W;
+    lt_end(S(s), C == 32 ? "c1dw_bwd_tile<T,32>" : "c1dw_bwd_tile<T,64>",
+           2.0 * M * 2 * C * C + 3 * 2.0 * M * 2 * C * 9, (4.0 * M * C + 2.0 * C * C) * 2);
+  }
   int rc = check_launch("c1dw_bwd_tile");
   if (rc) return rc;
   rc = nbp_reduce_slab(p.slab_w, (int)nrow, 2L * C * 9, dwdw, s);

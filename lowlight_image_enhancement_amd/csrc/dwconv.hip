@@ -1024,6 +1024,7 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   const long nblk = nrow * p.slices;
   NBP_REQUIRE(nblk < (1L << 31), "dw_bwd: grid too large");
   const bool fused = dh != nullptr;
+  lt_begin(S(s));
   NBP_DISPATCH_T(dtype, {
     constexpr int NQ = (64 / sizeof(T)) / 4;
     if (tw == 32) {
@@ -1034,6 +1035,12 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
       else dw_bwd_tiled<T, false, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
     }
   });
+  {  // per-launch record (nbp_launch_timing): fused: dh C + t2 2C + t1 2C in, dt1 2C out; else dt2 2C + t1 2C in, dt1 out
+    const double M = (double)B * H * W, es = dtype != 0 ? 2 : 4;
+    const char* nm = tw == 32 ? (fused ? "dw_bwd_tiled<T,true,32>" : "dw_bwd_tiled<T,false,32>")
+                              : (fused ? "dw_bwd_tiled<T,true,16>" : "dw_bwd_tiled<T,false,16>");
+    lt_end(S(s), nm, 2.0 * M * 2 * C * 18, (fused ? 7.0 : 6.0) * M * C * es);
+  }
   int rc = check_launch("dw_bwd_tiled");
   if (rc) return rc;
   rc = nbp_reduce_slab(p.slab_w, (int)nrow, 2L * C * 9, dwdw, s);

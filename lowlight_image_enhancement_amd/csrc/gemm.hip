@@ -1333,7 +1333,14 @@ void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vecto
       lblocks += d.N;
       rb.l[rb.nl++] = d;
     }
+    double by = 0;  // this launch's slabs read once + outputs written once
+    for (int k = 0; k < rb.n; ++k) by += (double)rb.d[k].S * rb.d[k].L * 4 + (double)rb.d[k].L * 4;
+    for (int k = 0; k < rb.nl; ++k)
+      by += (double)rb.l[k].SU * rb.l[k].N * rb.l[k].K * 4 + (double)rb.l[k].SV * rb.l[k].N * 4 +
+            (double)rb.l[k].N * (rb.l[k].K + 2) * 4;
+    lt_begin(st);
     reduce_multi_kernel<<<(unsigned)(blocks + lblocks), 256, 0, st>>>(rb);
+    lt_end(st, "reduce_multi_kernel", 0.0, by);
     g_stats_flush[3] += 1;
   }
 }
@@ -1388,7 +1395,11 @@ void launch_post(const std::vector<PDesc>& ops, hipStream_t st) {
       blocks += d.N;
       pb.d[pb.n++] = d;
     }
+    double by = 0;  // U, V, W, b, scale read; dW, db, dscale written
+    for (int k = 0; k < pb.n; ++k) by += (double)pb.d[k].N * (2.0 * pb.d[k].K + 4) * 4 + (double)pb.d[k].N * 2 * 4;
+    lt_begin(st);
     layer_scale_grad_kernel<<<blocks, 64, 0, st>>>(pb);
+    lt_end(st, "layer_scale_grad_kernel", 0.0, by);
   }
 }
 
@@ -1666,9 +1677,13 @@ void wgroup_launch_chunk(hipStream_t st, int ns, int q0, int q1) {
       WGroup g;
       g.n = 0;
       int blocks = 0;
+      double kfl = 0, kby = 0;  // this launch's algorithmic FLOPs / bytes (operands once, dW / db once)
       for (int q = q0; q < q1; ++q) {
         const WgradP& p = g_wqueue[q];
         if ((int)wide4(p) != kind) continue;
+        kfl += 2.0 * p.M * p.N * p.K;
+        kby += (double)p.M * (p.N + p.K) * (g_wqueue_dtype != 0 ? 2 : 4) + (double)p.N * p.K * 4 +
+               (p.slab_b ? (double)p.N * 4 : 0.0);
         g.p[g.n] = p;
         g.gx[g.n] = p.N / TNB;
         g.gy[g.n] = p.K / 128;
@@ -1679,6 +1694,9 @@ void wgroup_launch_chunk(hipStream_t st, int ns, int q0, int q1) {
       }
       if (!g.n) continue;
       g.start[g.n] = blocks;
+      const char* kname = kind ? "wgrad_bf16_wide_group<3,768,4>" : (ns == 44 || ns == 84) ? "wgrad_bf16_wide_group<4,512,2>"
+                          : (ns == 43 || ns == 83) ? "wgrad_bf16_wide_group<3,512,2>" : "wgrad_bf16_wide_group<256>";
+      lt_begin(st);
       NBP_DISPATCH_H(g_wqueue_dtype, {
         if (kind) {  // (a 4-deep ring of 48-KB stages would not fit in LDS)
           wgrad_bf16_wide_group<H, 3, 768, 4><<<blocks, 768, 0, st>>>(g);
@@ -1696,6 +1714,7 @@ void wgroup_launch_chunk(hipStream_t st, int ns, int q0, int q1) {
           wgrad_bf16_wide_group<H, 0><<<blocks, 256, 0, st>>>(g);
         }
       });
+      lt_end(st, kname, kfl, kby);
       g_stats_group[5] += 1;
     }
   }
@@ -1747,6 +1766,9 @@ int nbp_wgrad_f32(const void* G, long ldg, int g_mode, const void* X, long ldx, 
                 "nbp_wgrad_f32(16-bit): N, K and S2D channel counts must be multiples of 8");
     NBP_REQUIRE((g_mode == AM_S2D || ldg % 8 == 0) && (x_mode == AM_S2D || ldx % 8 == 0),
                 "nbp_wgrad_f32(16-bit): leading dimensions must be multiples of 8");
+    // every 16-bit kernel below reads G and X by 16-byte vectors from the base pointers (views at odd element offsets
+    // would be read from the wrong addresses)
+    NBP_REQUIRE((((uintptr_t)G | (uintptr_t)X) & 15) == 0, "nbp_wgrad_f32(16-bit): G and X must be 16-byte aligned");
     const bool wide = wide_wgrad(N, K) && g_mode == AM_PLAIN &&
                       (x_mode == AM_PLAIN || (x_mode == AM_SCALE && rows_per_img % 64 == 0));
     const dim3 wgrid(N / 128, K / 128, S_);

@@ -21,6 +21,9 @@ namespace nbp {
 // ---------------------------------------------------------------- error plumbing (host)
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// per-launch timing records (capi.hip, nbp_launch_timing): events around one kernel launch on stream st
+void lt_begin(hipStream_t st);
+void lt_end(hipStream_t st, const char* name, double flops, double bytes);
 // fp32 implicit-GEMM KH x KW / stride conv over NHWC maps (gemm.hip): mode 0 bias + ReLU, 1 bias, 2 ReLU-mask by R
 int conv_f32(const float* x, int B, int H, int W, int Cin, const float* w, int Cout, int KH, int KW, int stride, int pad,
              const float* bias, int mode, const float* R, float* y, hipStream_t st);

@@ -404,8 +404,7 @@ class NAFNet(nn.Module):
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
-        tile = (self.fuse_c1dw_tile and c in self.c1dw_tile_channels and dt != 0 and len(self._W) == 3
-                and query("c1dw_tile_supported", h, w, c, dt) == 1)
+        tile = len(self._W) == 3 and self.tile_level(B, h, w, c)
         c1dw = (not tile and self.fuse_c1dw and dt != 0 and len(self._W) == 3
                 and query("c1dw_supported", h, w, c, dt) == 1)
         chunks = (query("c1dw_tile_rows", h, w, c) if tile else
@@ -484,6 +483,15 @@ class NAFNet(nn.Module):
             tape.append(("block", pre, (B, h, w, c), dict(x=x, n1=n1, st1=st1, t1=t1, t2=t2, g=g, mean=mean, a=a, y=y,
                                                            n2=n2, st2=st2, t4=t4, g2=g2)))
         return self._ln_carry[0] if self._ln_carry is not None else out.view(B, h, w, c)
+
+    def tile_level(self, B: int, h: int, w: int, c: int) -> bool:
+        """Whether a block of this level takes the tile path (nbp_c1dw_fwd_tile / nbp_c1dw_bwd_tile: t1 / t2 rebuilt on
+        chip): 16-bit modes, the channel counts in c1dw_tile_channels, and a level small enough for the kernels' 32-bit
+        buffer offsets (nbp_c1dw_tile_supported depends on B: e.g. 16 images of 1024^2 at level 0 take the stored
+        tape)."""
+        dt = self.dt
+        return (self.fuse_c1dw_tile and c in self.c1dw_tile_channels and dt != 0
+                and query("c1dw_tile_supported", B, h, w, c, dt) == 1)
 
     def _down_fwd(self, P, i, x, B, h, w, c, tape):
         ho, wo = h // 2, w // 2

@@ -52,7 +52,8 @@ class NBPTrainer:
                  scheduler: Optional[TrueCosineAnnealingLR] = None, process_group=None, bucket_mb: float = 25.0,
                  w_deltaE: float = 0.0, w_perc: float = 0.0, w_lpips: float = 0.0, perceptual=None, lpips=None,
                  loss_scale: Optional[str] = "auto", init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
-                 backoff_factor: float = 0.5, growth_interval: int = 2000, lpips_net: str = "vgg"):
+                 backoff_factor: float = 0.5, growth_interval: int = 2000, lpips_net: str = "vgg",
+                 data_parallel: Optional[bool] = None):
         """Loss terms and weights as HybridLossPlus (losses.py:223-372): L1 (raw), Perc (VGG19), LPIPS (vgg), ΔE00,
         SSIM, Phys_srgb; a zero weight skips the term.  `perceptual` / `lpips`: PerceptualLoss / LPIPS modules
         (constructed with the synthetic offline weights when needed and not given; `lpips_net` picks the backbone of
@@ -108,7 +109,15 @@ class NBPTrainer:
         self.loss_buf = torch.zeros(6, device=dev)  # L1, SSIM, Phys, DeltaE, Perc, Total
         self.iter = 0  # iterations run (the scheduler's position; AdamW's own step count self.t excludes skips)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        have_pg = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if have_pg else 1
+        # the bucketed all-reduce path (per-stage hooks, asynchronous bucket all-reduces, graph segments cut at the
+        # buckets): on whenever world > 1; data_parallel=True forces it on a one-rank process group too (the RCCL
+        # rehearsal of the path on one GPU: a one-rank SUM all-reduce is the identity, so the step is bitwise the
+        # non-data-parallel one)
+        if data_parallel and not have_pg:
+            raise ValueError("data_parallel=True needs an initialised torch.distributed process group")
+        self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
         self.bucket_elems = int(bucket_mb * 1024 * 1024 / 4)
         self._handles: List = []
         self._cap: Optional[dict] = None  # segment capture state of the data-parallel graph step
@@ -120,7 +129,7 @@ class NBPTrainer:
         self.comm_buckets: List[tuple] = []
         self.comm_probe = False
         self.comm_events: List[tuple] = []
-        if self.world > 1:
+        if self.dp:
             dist.broadcast(net.flat.data, src=0, group=process_group)
 
     # ------------------------------------------------------------------ bucketed all-reduce during backward
@@ -224,11 +233,11 @@ class NBPTrainer:
             g = self.lpips.value_and_grad(out, gt, self.up[5:5 + B], self.lpips_buf, clamp=True,
                                           dt=self._trunk_dt(self.lpips))
             call("add", d_out, g, d_out, n, 0)
-        hook = self._on_stage if self.world > 1 else None
-        if self.world > 1 and self._cap is None:
+        hook = self._on_stage if self.dp else None
+        if self.dp and self._cap is None:
             self.comm_buckets = []
         net.exec_backward(tape, d_out, self.grad, need_dx=False, hook=hook)
-        if self.world > 1:
+        if self.dp:
             self._flush()
             if self._cap is None:
                 self._wait_buckets()
@@ -337,7 +346,7 @@ class NBPTrainer:
         ev = torch.cuda.Event()
         ev.record()
         self._lr_ev[slot] = ev
-        if self.world == 1:
+        if not self.dp:
             self._graph.replay()
             return self._graph_out
         self.comm_buckets = []
@@ -375,7 +384,7 @@ class NBPTrainer:
         torch.cuda.current_stream().wait_stream(side)
         for dst, src in zip(state, saved):
             dst.copy_(src)
-        if self.world == 1:
+        if not self.dp:
             self._graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._graph):
                 self._graph_out = self._graph_body()

@@ -22,10 +22,15 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            # unit bench.py's algorithmic bytes use for these classes
            "wgrad_narrow": ("wgrad_bf16_kernel", "wgrad_f32_kernel", "wgrad_narrow_full"), "wgrad_group": ("wgrad_bf16_wide",),
            "reduce": ("reduce_multi_kernel", "layer_scale_grad_kernel"),
-           "dw_bwd": ("dw_bwd_tiled",), "dw_bwd_32": (re.compile(r"dw_bwd_tiledI\w+?Li32E"),),
+           "dw_bwd": ("dw_bwd_tiled",), "dw_bwd_32": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi32EE"),),
            "dw_fwd": ("dw_sg_pool_tiled",), "c1dw": ("c1_dw_sg_pool_img",), "ln_fwd": ("ln_fwd_nhwc",),
            "c1dw_tile_fwd": ("c1dw_fwd_tile",), "c1dw_tile_bwd": ("c1dw_bwd_tile",),
-           "c1dw_bwd_L0": (re.compile(r"c1dw_bwd_tileI\w+?Li32E"),),
+           # bench.py's one-instance classes (INSTANCES / ROCPROF_KERNELS there)
+           "c1dw_bwd_L0": (re.compile(r"c1dw_bwd_tileI\w+?Li32EE"),), "c1dw_bwd_L1": (re.compile(r"c1dw_bwd_tileI\w+?Li64EE"),),
+           "dw_bwd_16": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi16EE"),),
+           "wgrad_group_512": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi512ELi2EE"),),
+           "wgrad_group_768": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi768ELi4EE"),),
+           "reduce_multi": ("reduce_multi_kernel",), "layer_scale_grad": ("layer_scale_grad_kernel",),
            "ln_bwd": ("ln_bwd_nhwc",),
            # VGG / AlexNet implicit-GEMM convs (cfg3's perceptual + LPIPS trunks): the tiled kernels with A mode 3 / 4
            "vgg_conv": (re.compile(r"gemm_(glds|bf16)_kernelILi\d+ELi\d+ELi\d+ELi[34]E"),),

@@ -316,6 +316,10 @@ def gen_nafblock(R):
     save("nafblock.npz", **out)
 
 
+CFG2 = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+CFG4 = dict(width=64, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
+
+
 def _net_case(R, name, cfg, seed, B, H, W, psf_mode, psf_spec, full=True, ratio=None):
     """NAFNet fwd+bwd under loss = L1(out, gt) + 0.1 * PhysSRGB(out.clamp01, short.clamp01, ratio)."""
     net = R.na.create_newbp_net(in_channels=3, **cfg)
@@ -365,16 +369,55 @@ def gen_nets(R):
          shapes=np.asarray([str(tuple(v.shape)) for v in net.state_dict().values()]))
 
 
-CFG2 = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
-CFG4 = dict(width=64, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
-
-
 def gen_cfg_nets(R):
     """BASELINE configs[1] model (w32 [2,2,4,8]/12/[2,2,2,2], rgb B2) at bs 2 x 256^2 and configs[3] model (w64, the
     per-GPU slice at 2 x 64^2): output, loss terms and per-tensor gradient sums / norms (the parameters come from the
     seeded recipe; full tensors would be 117 / 464 MB)."""
     _net_case(R, "nafnet_cfg2.npz", CFG2, 300, 2, 256, 256, "rgb", "B2", full=False)
     _net_case(R, "nafnet_w64.npz", CFG4, 301, 2, 64, 64, "rgb", "B2", full=False)
+
+
+def _autocast_grads(R, cfg, seed, B, H, W, scale=65536.0):
+    """The reference's fp32 and fp16-autocast backward of the _net_case loss (L1 + 0.1 * PhysSRGB) on the same weights
+    and batch: per-tensor cosine and relative-norm error of the fp16 gradients against the fp32 ones.  fp16 autocast as
+    the reference trains (image_restoration_model.py:255-310: autocast forward + loss, GradScaler-scaled backward,
+    unscaled gradients; init scale 2^16), here on the CPU."""
+    grads = {}
+    for amp in (False, True):
+        net = R.na.create_newbp_net(in_channels=3, **cfg)
+        st = recipe_state([(k, tuple(v.shape)) for k, v in net.state_dict().items()], seed=seed)
+        net.load_state_dict(st)
+        g = torch.Generator().manual_seed(seed + 1)
+        lq = torch.rand(B, 3, H, W, generator=g)
+        gt = torch.rand(B, 3, H, W, generator=g)
+        r = torch.ones(B, 1, 1, 1)
+        short = (lq * r).clamp(0, 1)
+        phys = R.lo.PhysicalConsistencyLossSRGB(R.na.create_crosstalk_psf("rgb", "B2"))
+        with torch.autocast("cpu", dtype=torch.float16, enabled=amp):
+            out = net(lq)
+            loss = F.l1_loss(out, gt) + 0.1 * phys(out.clamp(0, 1), short.clamp(0, 1), r)
+        (loss * (scale if amp else 1.0)).backward()
+        grads[amp] = {k: p.grad.double() / (scale if amp else 1.0) for k, p in net.named_parameters()}
+    keys = list(grads[False].keys())
+    cos, rel = [], []
+    for k in keys:
+        a, b = grads[True][k].flatten(), grads[False][k].flatten()
+        nb = b.norm().item()
+        cos.append((a @ b).item() / max(a.norm().item() * nb, 1e-300))
+        rel.append((a - b).norm().item() / max(nb, 1e-300))
+    return np.asarray(keys), np.asarray(cos), np.asarray(rel)
+
+
+def gen_fp16_grads(R):
+    """Calibration of the fp16 headline backward: the reference's OWN fp16-autocast gradients
+    against its fp32 gradients, per parameter tensor, at cfg2 (2 x 256^2, the nafnet_cfg2.npz weights and batch) and at
+    w64 (2 x 64^2, nafnet_w64.npz)."""
+    out = {}
+    for tag, cfg, seed, B, H, W in (("cfg2", CFG2, 300, 2, 256, 256), ("w64", CFG4, 301, 2, 64, 64)):
+        keys, cos, rel = _autocast_grads(R, cfg, seed, B, H, W)
+        out[tag + "_keys"], out[tag + "_cos"], out[tag + "_rel"] = keys, cos, rel
+        print(tag, "min cos", cos.min(), "max rel", rel.max(), "median rel", np.median(rel), flush=True)
+    save("fp16_grad_calib.npz", **out)
 
 
 def gen_widths(R):
@@ -500,7 +543,7 @@ def main():
     gens = dict(psf=gen_psf, phys_srgb=gen_phys_srgb, phys_raw_full=gen_phys_raw_full, phys_cons=gen_phys_cons, layernorm=gen_layernorm,
                 nafblock=gen_nafblock, nets=gen_nets, cfg_nets=gen_cfg_nets, widths=gen_widths, cfg5=gen_cfg5,
                 train_steps=gen_train_steps, color=gen_color, linear=gen_linear,
-                ssim_align=gen_ssim_align)
+                ssim_align=gen_ssim_align, fp16_grads=gen_fp16_grads)
     for name, fn in gens.items():
         if not args.only or name in args.only.split(","):
             fn(R)

@@ -84,3 +84,33 @@ def test_rehearsal_line_carries_the_comm_fields():
     assert c["allreduce_exposed_ms"] is not None and c["allreduce_exposed_ms"] >= 0
     assert c["allreduce_exposed_ms_eager"] is not None and c["probed_steps"] >= 1
     assert "exposed all-reduce" in line["nafblock_roofline"]["ms_method"]
+
+
+def _newest_kernel_stats():
+    import glob
+    fs = [f for f in glob.glob(os.path.join(ROOT, "profiles", "*", "kernel_stats.csv"))]
+    key = lambda f: bench._pmc_newest_key(f)  # noqa: E731
+    return sorted(fs, key=key)[-1] if fs else None
+
+
+def test_single_kernel_classes_name_one_rocprof_instance():
+    """every one-instance class of the bench (the candidates for the headline `roofline`) names
+    exactly one kernel instance per storage type in the newest committed rocprof summary (or none, if the record's
+    step never launched it), and the launch records the library writes map onto those classes."""
+    import csv
+    import re
+    path = _newest_kernel_stats()
+    assert path is not None
+    names = [r["Name"] for r in csv.DictReader(open(path))]
+    seen = 0
+    for cls in bench.SINGLE_KERNEL:
+        pats = [re.compile(p.format(T=bench.MANGLED_T["fp16"])) for p in bench.ROCPROF_KERNELS[cls]]
+        hits = [n for n in names if any(p.search(n) for p in pats)]
+        assert len(hits) <= 1, (cls, hits)
+        seen += len(hits)
+    assert seen >= 5, path
+    # the instance names the library records (nbp_launch_timing) are the keys of bench.INSTANCES
+    src = "".join(open(os.path.join(ROOT, "lowlight_image_enhancement_amd", "csrc", f)).read()
+                  for f in ("gemm.hip", "dwconv.hip", "c1dw_tile.hip"))
+    for inst in bench.INSTANCES:
+        assert f'"{inst}"' in src, inst

@@ -28,6 +28,26 @@ def test_error_reporting_without_gpu():
     assert b"nbp_gemm_f32" in L.nbp_last_error_string()
 
 
+def test_c1dw_tile_path_depends_on_the_batch():
+    """the tile kernels address [M][2C] 16-bit buffers by 32-bit offsets with an out-of-range sentinel; a
+    level whose buffers reach it must take the stored-tape path (host query, no kernel launch)."""
+    from lowlight_image_enhancement_amd._lib import query
+    from lowlight_image_enhancement_amd.nafnet import NAFNet
+    assert query("c1dw_tile_supported", 8, 1024, 1024, 32, 2) == 1  # 2^30 bytes
+    assert query("c1dw_tile_supported", 16, 1024, 1024, 32, 2) == 0  # 2^31 bytes: beyond the sentinel
+    assert query("c1dw_tile_supported", 15, 1024, 1024, 32, 1) == 1  # 0x78000000 bytes < 0x7fffff00
+    assert query("c1dw_tile_supported", 8, 1024, 1024, 64, 2) == 0
+    assert query("c1dw_tile_supported", 0, 256, 256, 32, 2) == 0
+    net = NAFNet(img_channel=3, width=32, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1])
+    net.precision = "fp16"
+    assert net.tile_level(16, 256, 256, 32) and net.tile_level(8, 512, 512, 64)
+    assert not net.tile_level(16, 1024, 1024, 32)  # BASELINE configs[4] on 2 GPUs: 16 x 1024^2 per GPU at level 0
+    assert net.tile_level(16, 512, 512, 64)
+    assert not net.tile_level(16, 64, 64, 128)
+    net.precision = "fp32"
+    assert not net.tile_level(2, 64, 64, 32)
+
+
 def test_host_psf_normalisation_bit_exact():
     from lowlight_image_enhancement_amd.NewBP_model.newbp_layer import build_psf_kernels, normalize_kernels
     g = golden("psf.npz")

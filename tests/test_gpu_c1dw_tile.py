@@ -44,7 +44,7 @@ def _two_launch_fwd(dev, dt, B, H, W, C, n1, w1, b1, wdw, bdw):
 @pytest.mark.parametrize("B,H,W,C", SHAPES)
 def test_fwd_tile_bitwise_equals_two_launches(dev, dt, B, H, W, C):
     from lowlight_image_enhancement_amd._lib import call, query
-    assert query("c1dw_tile_supported", H, W, C, dt) == 1
+    assert query("c1dw_tile_supported", B, H, W, C, dt) == 1
     Ht, M = DT[dt], B * H * W
     n1, w1, b1, wdw, bdw = _operands(dev, dt, B, H, W, C, B + H + W + C + dt)
     t1r, t2r, gr = _two_launch_fwd(dev, dt, B, H, W, C, n1, w1, b1, wdw, bdw)
@@ -112,26 +112,30 @@ def test_bwd_tile_dt1_bitwise_and_weight_grads(dev, dt, B, H, W, C):
 
 def test_tile_shapes_not_served(dev):
     from lowlight_image_enhancement_amd._lib import NBPError, call, query
-    assert query("c1dw_tile_supported", 64, 64, 128, 2) == 0
-    assert query("c1dw_tile_supported", 256, 256, 32, 0) == 0
-    assert query("c1dw_tile_supported", 256, 256, 48, 1) == 0
+    assert query("c1dw_tile_supported", 1, 64, 64, 128, 2) == 0
+    assert query("c1dw_tile_supported", 1, 256, 256, 32, 0) == 0
+    assert query("c1dw_tile_supported", 1, 256, 256, 48, 1) == 0
     z = torch.zeros(8, device=dev)
     with pytest.raises(NBPError, match="unsupported shape"):
         call("c1dw_fwd_tile", z, z, z, z, z, None, None, z, z, 1, 64, 64, 128, 2)
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-def test_tile_network_matches_stored_tape(dev, precision):
+@pytest.mark.parametrize("B,H,W", [(2, 96, 80), (1, 1024, 1024)], ids=["96x80", "cfg5_1024"])
+def test_tile_network_matches_stored_tape(dev, precision, B, H, W):
     """Width 32, two downs: levels 0 (C 32) and 1 (C 64) take the tile path.  Forward and parameter gradients against
-    the stored-tape path of the same network within the 16-bit rounding that the pool's summation order can move."""
+    the stored-tape path of the same network within the 16-bit rounding that the pool's summation order can move --
+    also at BASELINE configs[4]'s image size (1024^2: 1024 tiles per image at level 0, buffer offsets near 2^28 bytes;
+    ADVICE r5)."""
     from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
     torch.manual_seed(5)
     net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[1, 1], middle_blk_num=1, dec_blk_nums=[1, 1]).to(dev)
     net.precision = precision
     net.c1dw_tile_channels = (32, 64)
+    assert net.tile_level(B, H, W, 32) and net.tile_level(B, H // 2, W // 2, 64)
     with torch.no_grad():
         net.flat.add_(torch.randn_like(net.flat) * 0.02)
-    x = torch.rand(2, 3, 96, 80, device=dev)
+    x = torch.rand(B, 3, H, W, device=dev)
     res = []
     for fuse in (True, False):
         net.fuse_c1dw_tile = fuse

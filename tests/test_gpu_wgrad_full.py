@@ -68,3 +68,18 @@ def test_wgrad_full_space_to_depth(dev, B, gh, gw, side):
          torch.full((nw,), float("nan"), device=dev), nw, 1)
     torch.cuda.synchronize()
     _check(dW, db, ref, bref, M)
+
+
+def test_wgrad_16bit_rejects_misaligned_views(dev):
+    """the 16-bit weight-gradient kernels read G and X by 16-byte vectors from the base pointers; a view at
+    an odd element offset is refused loudly instead of being read from the wrong addresses."""
+    from lowlight_image_enhancement_amd._lib import NBPError, call, query
+    M, N, K = 4096, 32, 32
+    Gb = torch.zeros(M * N + 8, device=dev, dtype=torch.float16)
+    X = torch.zeros(M, K, device=dev, dtype=torch.float16)
+    dW, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+    n_ws = query("wgrad_workspace_floats", M, N, K)
+    ws = torch.empty(n_ws, device=dev)
+    call("wgrad_f32", Gb[:M * N].view(M, N), N, 0, X, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws, 2)
+    with pytest.raises(NBPError, match="16-byte aligned"):
+        call("wgrad_f32", Gb[1:1 + M * N].view(M, N), N, 0, X, K, 0, None, 1, M, N, K, 0, 0, 0, 0, dW, db, ws, n_ws, 2)
