@@ -95,7 +95,7 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
              "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad"}
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
-    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32EE"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64EE"],
+    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32E(Li\d+E)?E"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64E(Li\d+E)?E"],
     "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32EE"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16EE"],
     "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
     "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],

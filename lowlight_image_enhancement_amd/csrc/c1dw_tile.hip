@@ -262,9 +262,12 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 // ring the rounded dt2 widened once (no conversions in the dt1 taps).  The conv1 weight slice and bias live in LDS; the
 // n1 rows (MFMA waves) and the dh rows of the next steps in register rings with static slots (the step loop unrolled by
 // the ring depth U: 3 at C 32, 2 at C 64).
-template <typename T, int C>
+// BAL: the t1 rebuild spread over all four waves (wave w: pixel chunk w / 2, channel half w % 2 -- one 32 x 32 MFMA
+// chain and a 16-value epilogue each) instead of waves 0 / 1 doing both halves of one chunk each (two chains, 32
+// values) while waves 2 / 3 wait at the step's barrier
+template <typename T, int C, int TH, bool BAL>
 __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
-  constexpr int TH = CT_TH, TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
+  constexpr int TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int ROWF = LT * 64;          // floats per t1 ring row
   constexpr int ROWD = LD * 64;          // floats per dt2 ring row
   constexpr int U = 2;                   // register-ring slots (n1, dh); the step loop is unrolled by 4 = the LDS
@@ -293,10 +296,12 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     }
     if (tid < 64) b1s[tid] = p.b1[(tid < 32 ? 0 : C) + slice * 32 + (tid & 31)];
   }
-  // ---- MFMA lanes: waves 0 and 1, chunk = wave (t1 ring pixel wave * 32 + r = image column x0 - 2 + ...)
-  const bool mfma_wave = wave < 2;
-  const int gxm = x0 - 2 + wave * 32 + r;
-  const bool lane_ok = wave * 32 + r < LT;
+  // ---- MFMA lanes: waves 0 and 1, chunk = wave (t1 ring pixel wave * 32 + r = image column x0 - 2 + ...); BAL: every
+  // wave, chunk = wave / 2, channel half th = wave % 2
+  const bool mfma_wave = BAL || wave < 2;
+  const int chunk = BAL ? wave >> 1 : wave, th = wave & 1;
+  const int gxm = x0 - 2 + chunk * 32 + r;
+  const bool lane_ok = chunk * 32 + r < LT;
   vec_t<T, 8> fq[U][KS];  // n1 fragments of t1 ring row k in slot k % U
   if (mfma_wave)
 #pragma unroll
@@ -338,31 +343,33 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
       const bool valid = yy >= 0 && yy < H && lane_ok && gxm >= 0 && gxm < W;
       // the row inside the image and the tile's ring columns x0 - 2 .. x0 + TW + 1 too (uniform): no per-value select
       const bool interior = yy >= 0 && yy < H && x0 >= 2 && x0 + TW + 2 <= W;
-      floatx16 acc[2];
+      constexpr int NT = BAL ? 1 : 2;  // channel halves of this wave
+      floatx16 acc[NT];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int n = t * 32 + r, c = 2 * ks + hh;
+        for (int t = 0; t < NT; ++t) {
+          const int n = (BAL ? th : t) * 32 + r, c = 2 * ks + hh;
           const vec_t<T, 8> wf = *reinterpret_cast<const vec_t<T, 8>*>(w1s + n * C + 8 * (c ^ ((n / RPB) & (NC - 1))));
           acc[t] = mfma32x32x16(wf, fq[S][ks], acc[t]);
         }
-      const int px = wave * 32 + r;
+      const int px = chunk * 32 + r;
       if (px < LT) {
         float* slot = t1r + R * ROWF;
         const int key = qkey<PXT>(px);
         auto put = [&](auto masked_c) {
 #pragma unroll
-          for (int t = 0; t < 2; ++t)
+          for (int t0 = 0; t0 < NT; ++t0)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
+              const int t = BAL ? th : t0;
               const float4 bv = *reinterpret_cast<const float4*>(b1s + t * 32 + 8 * g + 4 * hh);
-              const f2v lo = round2<T>(f2v{acc[t][4 * g], acc[t][4 * g + 1]} + f2v{bv.x, bv.y});
-              const f2v hi = round2<T>(f2v{acc[t][4 * g + 2], acc[t][4 * g + 3]} + f2v{bv.z, bv.w});
+              const f2v lo = round2<T>(f2v{acc[t0][4 * g], acc[t0][4 * g + 1]} + f2v{bv.x, bv.y});
+              const f2v hi = round2<T>(f2v{acc[t0][4 * g + 2], acc[t0][4 * g + 3]} + f2v{bv.z, bv.w});
               float v[4] = {lo.x, lo.y, hi.x, hi.y};
               if constexpr (decltype(masked_c)::value) {
 #pragma unroll
@@ -600,6 +607,32 @@ using namespace nbp;
 
 namespace {
 int tile_w(int C) { return C == 32 ? 64 : 32; }
+// rows of a backward tile: 32 (the two-row halo of the rebuilt t1 and the one-row halo of the rebuilt t2 are then
+// 1.125 / 1.06 x the tile's rows instead of 1.25 / 1.125 at 16, and the per-tile weight-slice load and dW reduction
+// amortise over twice the pixels); NBP_C1DW_BWD_TH=16 / 32 (per C: "th32,th64") overrides for A/B runs
+// the balanced t1 rebuild (BAL) at C 32: 151.0 -> 148.7-149.4 us per level-0 launch (scripts/c1dw_tile_micro.py,
+// gpurun_out r6c); at C 64 its registers spill (256 VGPRs + 10) and it is slower (89.1 -> 93.3 us): off there.
+// NBP_C1DW_BWD_BAL=0 / 1 forces it off / on at both (A/B)
+bool bwd_bal(int C) {
+  static const int v = [] {
+    const char* e = getenv("NBP_C1DW_BWD_BAL");
+    return e ? atoi(e) : -1;
+  }();
+  return v < 0 ? C == 32 : v != 0;
+}
+int bwd_th(int C) {
+  static int th[2] = {0, 0};
+  if (!th[0]) {
+    th[0] = th[1] = 32;
+    if (const char* e = getenv("NBP_C1DW_BWD_TH")) {
+      int a = 0, b = 0;
+      const int n = sscanf(e, "%d,%d", &a, &b);
+      if (n >= 1 && (a == 16 || a == 32)) th[0] = th[1] = a;
+      if (n == 2 && (b == 16 || b == 32)) th[1] = b;
+    }
+  }
+  return th[C == 32 ? 0 : 1];
+}
 }  // namespace
 
 extern "C" {
@@ -645,7 +678,7 @@ int nbp_c1dw_fwd_tile(const void* n1, const void* w1, const float* b1, const flo
 }
 
 size_t nbp_c1dw_bwd_workspace_floats(int B, int H, int W, int C) {
-  return (size_t)B * cdiv(H, CT_TH) * cdiv(W, 32) * 2 * C * 10;
+  return (size_t)B * cdiv(H, bwd_th(C)) * cdiv(W, 32) * 2 * C * 10;
 }
 
 int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
@@ -658,7 +691,8 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
               "the out-of-range buffer offset)", B, H, W, C, dtype);
   C1TileP p{};
   p.n1 = n1; p.w1 = w1; p.b1 = b1; p.wdw = wdw; p.bdw = bdw; p.dh = dh; p.a = a; p.ds = ds; p.dt1 = dt1;
-  p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, 32); p.tiles = cdiv(H, CT_TH) * p.tiles_x;
+  const int th = bwd_th(C);
+  p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, 32); p.tiles = cdiv(H, th) * p.tiles_x;
   p.inv_hw = 1.f / (float)((long)H * W);
   const long nrow = (long)B * p.tiles;
   p.slab_w = ws;
@@ -667,8 +701,13 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
   NBP_REQUIRE(nblk < (1L << 31), "nbp_c1dw_bwd_tile: grid too large");
   lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
-    if (C == 32) c1dw_bwd_tile<H, 32><<<nblk, 256, 0, S(s)>>>(p);
-    else c1dw_bwd_tile<H, 64><<<nblk, 256, 0, S(s)>>>(p);
+    const bool bal = bwd_bal(C);
+    if (C == 32 && th == 32 && bal) c1dw_bwd_tile<H, 32, 32, true><<<nblk, 256, 0, S(s)>>>(p);
+    else if (C == 32 && th == 32) c1dw_bwd_tile<H, 32, 32, false><<<nblk, 256, 0, S(s)>>>(p);
+    else if (C == 32) c1dw_bwd_tile<H, 32, 16, false><<<nblk, 256, 0, S(s)>>>(p);
+    else if (th == 32 && bal) c1dw_bwd_tile<H, 64, 32, true><<<nblk, 256, 0, S(s)>>>(p);
+    else if (th == 32) c1dw_bwd_tile<H, 64, 32, false><<<nblk, 256, 0, S(s)>>>(p);
+    else c1dw_bwd_tile<H, 64, 16, false><<<nblk, 256, 0, S(s)>>>(p);
   });
   {  // per-launch record (nbp_launch_timing): dh C + n1 C in, dt1 2C out, the conv1 weight slice per slice
     const double M = (double)B * H * W;

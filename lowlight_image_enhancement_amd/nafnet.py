@@ -34,6 +34,12 @@ CM_SG, CM_SGBWD = 4, 5  # SimpleGate forward / backward fused into the GEMM epil
 CM_CHANDOT = 8  # dgrad with the SCA channel-dot partials in the epilogue (bf16 mode, C > 64)
 CM_PLAIN, CM_D2S = 0, 1
 LN_EPS = 1e-6
+# without a gradient-ready hook (one process: no bucketed all-reduce reads a stage's slice early) every deferred
+# gradient reduction of the backward runs in the backward's final flush instead of one flush launch per stage: 26
+# latency-bound reduce launches per step become a few full ones (+1.0 % at cfg2, fp16, in the quick bench: 1356 / 1358
+# vs 1342 / 1344 img/s, gpurun_out r6c; the round-1 measurement of the same change was neutral).  NBP_LATE_FLUSH=0:
+# per-stage flushes (A/B)
+_LATE_FLUSH = __import__("os").environ.get("NBP_LATE_FLUSH", "1") != "0"
 
 
 @dataclass
@@ -616,8 +622,10 @@ class NAFNet(nn.Module):
         return dx_img
 
     def _stage_done(self, name, hook):
-        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice (one flush
-        # at the end of a hook-less backward measured neutral)
+        # the stage's queued gradient reductions run before anyone (the DP all-reduce hook) reads its slice; without a
+        # hook they all wait for the backward's final flush (_LATE_FLUSH)
+        if hook is None and _LATE_FLUSH:
+            return
         call("grad_reduce_flush", 0)
         self._keep.clear()
         if hook is not None:

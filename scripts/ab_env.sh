@@ -1,14 +1,21 @@
 #!/bin/bash
-# A/B of an executor switch in the quick bench: AB_VAR takes each of AB_VALS in turn (interleaved, REPS times), e.g.
-#   AB_VAR=NBP_LN_WG AB_VALS="1 0" scripts/ab_env.sh
-set -euo pipefail
+# Interleaved A/B of environment settings on the quick bench (one gpurun session):
+#   bash scripts/ab_env.sh OUT "ENV_A" "ENV_B" [...]   (each ENV a space-separated list of VAR=value, "-" for none)
+set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/${TAG:-ab}
-mkdir -p $O
-for rep in $(seq 1 ${REPS:-2}); do
-  for v in $AB_VALS; do
-    t=$(basename "$v")  # (a path value, e.g. NBP_LIB=<an A/B build>)
-    env "$AB_VAR=$v" timeout -k 10 300 python bench.py --quick --steps 20 --warmup 5 > $O/b_${rep}_$t.json 2> $O/b.err || { tail -30 $O/b.err; exit 1; }
-    python -c "import json; d=json.loads(open('$O/b_${rep}_$t.json').read().strip().splitlines()[-1]); print('$AB_VAR=$t', d['value'], d['ms_per_step'], {k: (v['fwd_ms'], v['bwd_ms']) for k, v in d['nafblock_roofline']['per_level_eager'].items() if 'C32' in k})"
+export TMPDIR=/tmp
+OUT=$1
+shift
+mkdir -p gpurun_out/$OUT
+ROUNDS=${ROUNDS:-2}
+for r in $(seq $ROUNDS); do
+  i=0
+  for e in "$@"; do
+    i=$((i + 1))
+    envs=""
+    [ "$e" != "-" ] && envs="$e"
+    env $envs timeout -k 10 300 python bench.py --quick --steps ${STEPS:-20} --warmup 5 > gpurun_out/$OUT/ab_${i}_r$r.json 2> gpurun_out/$OUT/ab_${i}_r$r.err || exit $?
+    v=$(python -c "import json,sys;d=json.load(open('gpurun_out/$OUT/ab_${i}_r$r.json'));print(d['value'],d['ms_per_step'],d['roofline']['kernel'],d['roofline']['frac'])")
+    echo "round $r  [$e]  $v" | tee -a gpurun_out/$OUT/ab.txt
   done
 done

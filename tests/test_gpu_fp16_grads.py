@@ -13,7 +13,7 @@ reference's OWN fp16-autocast gradients (CPU, GradScaler init scale 2^16, unscal
 per-tensor cosine >= 0.9998 / 0.9995 and relative-norm error <= 2.0 % / 3.3 % (median 0.7 % / 1.5 %) at cfg2 / w64.
 This path stores every activation in fp16 between kernels (autocast keeps LayerNorm, SimpleGate, the SCA and the
 residual stream in fp32), so its rounding enters at more points: each tensor must reach cosine >= 0.99 and a relative
-error <= max(5 x the reference's autocast error for that tensor, 2 %)."""
+error <= max(3 x the reference's autocast error for that tensor, 2 %)."""
 import numpy as np
 import pytest
 import torch
@@ -25,7 +25,7 @@ T = torch.from_numpy
 
 CFG2 = dict(width=32, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
 CFG4 = dict(width=64, enc_blk_nums=[2, 2, 4, 8], middle_blk_num=12, dec_blk_nums=[2, 2, 2, 2])
-REL_FACTOR, REL_FLOOR, COS_MIN = 5.0, 0.02, 0.99
+REL_FACTOR, REL_FLOOR, COS_MIN = 3.0, 0.02, 0.99
 
 
 @pytest.mark.parametrize("tag,fixture,cfg", [("cfg2", "nafnet_cfg2.npz", CFG2), ("w64", "nafnet_w64.npz", CFG4)])
