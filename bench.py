@@ -92,14 +92,17 @@ ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skin
 INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_bwd_L1",
              "dw_bwd_tiled<T,true,32>": "dw_bwd_32", "dw_bwd_tiled<T,true,16>": "dw_bwd_16",
              "wgrad_bf16_wide_group<3,512,2>": "wgrad_group_512", "wgrad_bf16_wide_group<3,768,4>": "wgrad_group_768",
-             "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad"}
+             "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad",
+             "ffn_rows_fwd<512>": "ffn_rows_512", "ffn_rows_fwd<256>": "ffn_rows_256", "ffn_rows_fwd<128>": "ffn_rows_128"}
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
     "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32E(Li\d+E)?E"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64E(Li\d+E)?E"],
     "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32EE"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16EE"],
     "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
     "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],
-    "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"]})
+    "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"],
+    "ffn_rows_512": [r"ffn_rows_fwdI{T}Li512EE"], "ffn_rows_256": [r"ffn_rows_fwdI{T}Li256EE"],
+    "ffn_rows_128": [r"ffn_rows_fwdI{T}Li128EE"], "ffn_rows": ["ffn_rows_fwd"]})
 # the Itanium mangling of the storage type in those names
 MANGLED_T = {"fp16": "DF16_", "bf16": "DF16b", "fp32": "f"}
 UNIT_DEF = {
@@ -116,6 +119,9 @@ UNIT_DEF = {
     "c1dw_bwd_L0": "per pixel: dh C + n1 C read, dt1 2C written = 4*C*s bytes (s = storage bytes; t1 / t2 rebuilt on "
                    "chip, never read), x B*H*W pixels of the launch (level 0: C 32 at 256^2), + the conv1 weight",
     "c1dw_bwd_L1": "as c1dw_bwd_L0 at level 1 (C 64 at 128^2)",
+    "ffn_rows_512": "per pixel: g C + x C read, y + n2 + t4 (2C) + g2 + out (+ the next n1) written = 8-9 C s bytes, "
+                    "+ the three weights (4 C^2 s) once per launch (the middle level: C 512 at 16^2)",
+    "ffn_rows_256": "as ffn_rows_512 at C 256 (32^2)", "ffn_rows_128": "as ffn_rows_512 at C 128 (64^2)",
 }
 
 
@@ -217,6 +223,12 @@ def cost_c1dw_bwd_tile(a):  # (dh,a,ds,n1,w1,b1,wdw,bdw,dt1,dwdw,dbdw,ws,B,h,w,c
 
 
 
+def cost_ffn_rows(a):  # (g,a,hw,x,w3,b3,beta,lnw2,lnb2,w4,b4,w5,b5,gamma,lnw1,lnb1,y,n2,st2,t4,g2,out,nn1,nst1,M,C,eps,dt)
+    M, C = a[24], a[25]
+    nxt = a[14] is not None
+    return 8.0 * M * C * C, (M * C * (9 if nxt else 8) + 4 * C * C) * 2 + M * 8 * (2 if nxt else 1)
+
+
 def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
     M, N, K = a[11], a[12], a[13]
     return 2.0 * M * N * K, 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0))
@@ -272,7 +284,8 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg),
            "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
            "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile),
-           "c1dw_bwd_tile": rec_plain("c1dw_tile_bwd", cost_c1dw_bwd_tile)}
+           "c1dw_bwd_tile": rec_plain("c1dw_tile_bwd", cost_c1dw_bwd_tile),
+           "ffn_rows_fwd": rec_plain("ffn_rows", cost_ffn_rows)}
 
 
 def _pmc_newest_key(f):
@@ -405,6 +418,8 @@ def make_trainer(dev, workload, precision, seed=0):
         net.c1dw_tile_channels = tuple(int(c) for c in tc.split(",") if c)
     if os.environ.get("NBP_LN_WG") == "0":  # A/B only: the separate level-0 conv1 weight-gradient launch
         net.ln_wg = False
+    if os.environ.get("NBP_FFN_ROWS") == "0":  # A/B only: the deep-level FFN half as separate launches
+        net.fuse_ffn_rows = False
     return NBPTrainer(net, psf_mode="rgb", psf_spec=spec, **wl["w"]), init_sd
 
 

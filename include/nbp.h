@@ -151,6 +151,25 @@ int nbp_gemm_res_ln(const void* A, long lda, int a_mode, const float* a_scale, i
 int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5, const float* b5, const void* y,
                  const float* gamma, const float* lnw, const float* lnb, void* out, void* nout, float* stats, int M,
                  int C, float eps, int dtype, nbp_stream_t s);
+/* The deep-level NAFBlock FFN half in ONE row-stationary launch (NAFNet_arch.py:69-80 after the SCA; C 128 / 256 / 512,
+ * 16-bit): y = x + beta (.) ((g (.) a) W3^T + b3); n2 / st2 = LayerNorm2d(y) (norm2); t4 = n2 W4^T + b4 (SimpleGate pairs
+ * interleaved, 2C columns); g2 = t4[2c] t4[2c + 1]; out = y + gamma (.) (g2 W5^T + b5); with lnw1 / lnb1 also the next
+ * block's norm1 of out into nn1 / nst1.  a: [B][C] SCA scale (per image of rows_per_img rows); weights w3 / w4 / w5:
+ * 16-bit copies in fragment order (nbp_weights_frag).  Replaces nbp_gemm_bf16 / nbp_gemm_res_ln (conv3) + nbp_ln_fwd_nhwc + nbp_gemm_bf16 CM_SG
+ * (conv4) + nbp_gemm_res_ln / nbp_gemm_bf16 (conv5) + nbp_ln_fwd_nhwc, bitwise: every stored tensor equals theirs.
+ * Stats are (mu, den) float pairs.  nbp_ffn_rows_supported(M, C, rows_per_img, dtype): 1 for the shapes served
+ * (rows_per_img a multiple of 32). */
+int nbp_ffn_rows_supported(int M, int C, int rows_per_img, int dtype);
+/* The weights of nbp_ffn_rows_fwd in fragment order (per step, from the fp32 flat parameters): desc = [ndesc][3] int64
+ * {offset, rows N, cols K} (N a multiple of 32, K of 16); the 16-bit copy of matrix i goes to out at its own offset, as
+ * 1-KB blocks (32-row tile nt, 16-wide k-step ks) in (nt, ks) order, lane l's 16 bytes = row 32 nt + (l & 31), k 16 ks
+ * + 8 (l >> 5) .. + 7 (the 32 x 32 x 16 MFMA B operand; one contiguous load per wave). */
+int nbp_weights_frag(const float* flat, const long* desc, int ndesc, void* out, int dtype, nbp_stream_t s);
+int nbp_ffn_rows_fwd(const void* g, const float* a, int rows_per_img, const void* x, const void* w3, const float* b3,
+                     const float* beta, const float* lnw2, const float* lnb2, const void* w4, const float* b4,
+                     const void* w5, const float* b5, const float* gamma, const float* lnw1, const float* lnb1, void* y,
+                     void* n2, float* st2, void* t4, void* g2, void* out, void* nn1, float* nst1, int M, int C,
+                     float eps, int dtype, nbp_stream_t s);
 /* conv5 input gradient + SimpleGate backward with the gate input recomputed (bf16, N = K = C = 32: level 0, whose conv4
  * forward runs on the same skinny MFMA sequence): dg = A . Wt^T (the conv5 dgrad), t = A2 . W2^T + b2 rebuilt per tile (the conv4 forward: A2 = its input n2 [M][K],
  * W2 [2N][K] bf16 with SimpleGate pairs interleaved, b2 fp32), C[m][2c] = dg[c] t[2c+1], C[m][2c+1] = dg[c] t[2c]

@@ -1,0 +1,422 @@
+// The deep-level NAFBlock FFN half in ONE row-stationary launch (levels 2 / 3 / middle: C 128 / 256 / 512).
+//
+// NAFNet_arch.py:69-80 after the SCA: y = x + beta * conv3(g * a); n2 = norm2(y); t4 = conv4(n2); g2 = SimpleGate(t4);
+// out = y + gamma * conv5(g2) (+ the next block's norm1(out), arch_util.py:264-275).  Every step is pixel-local, so a
+// workgroup that owns 32 pixel rows can run the whole chain with no other workgroup: its A operand (32 rows x C, 16-bit)
+// stays in LDS from one GEMM to the next -- g * a, then n2, then g2 -- and the three weights stream through registers
+// from L2 (every workgroup reads the same 2-4 C^2 elements: conv3 C x C, conv4 2C x C, conv5 C x C), one 16-byte
+// B-operand fragment per lane per 32 x 32 x 16 MFMA, D k-steps in flight, no LDS and no barrier in the K loops.  The
+// two-launch form moved each activation through HBM between the GEMMs (and the C 512 level ran the LayerNorms as
+// launches of their own); here per pixel g, x in and y, n2, t4 (2C), g2, out (+ the next n1) out, each once.
+//
+// Bitwise contract (tests/test_gpu_ffn_rows.py pins it against the launches it replaces): per output element the MFMA
+// sequence of the tiled GEMM kernels (K ascending in steps of 16 on one accumulator: the A fragment of lane l is row l &
+// 31, k 16 s + 8 (l >> 5) .. + 7, as gemm_glds_kernel's); the SCA scale applied to the 16-bit A as (H)(g * a); the
+// epilogues of gemm_epilogue: v = acc + bias, y = fmaf(beta, v, x) and out = fmaf(gamma, v, y) rounded once, t4 = (H)v,
+// g2 = (H)(v[2c] v[2c + 1]) of the fp32 pair; the LayerNorms of CM_RESLN / ln_fwd_nhwc (8 consecutive channels per lane in
+// order, group butterflies over the C / 8 lanes of a row, mu = s / C, the centred sum of squares, sqrtf(q / C + eps),
+// fmaf(w, (x - mu) / den, b) rounded once).
+#include "nbp_common.h"
+
+namespace nbp {
+namespace {
+
+struct FfnRowsP {
+  const void* g;       // [M][C] SimpleGate output of the spatial branch
+  const float* a;      // [B][C] SCA scale (h = g * a is conv3's input)
+  const void* x;       // [M][C] block input (conv3's residual)
+  const void* w3;      // [C][C] 16-bit conv3 weight (forward copy, [out][in])
+  const float* b3;
+  const float* beta;
+  const float* lnw2;
+  const float* lnb2;
+  const void* w4;      // [2C][C] conv4 weight, SimpleGate pairs interleaved (rows 2c, 2c + 1)
+  const float* b4;
+  const void* w5;      // [C][C]
+  const float* b5;
+  const float* gamma;
+  const float* lnw1;   // the next block's norm1 (null: no next LayerNorm)
+  const float* lnb1;
+  void* y;             // [M][C] out
+  void* n2;            // [M][C] out
+  float2* st2;         // [M] out: (mu, den) of norm2
+  void* t4;            // [M][2C] out (interleaved pairs)
+  void* g2;            // [M][C] out
+  void* out;           // [M][C] out
+  void* nn1;           // [M][C] out (with lnw1)
+  float2* nst1;        // [M] out (with lnw1)
+  int M, rows_per_img;
+  float eps;
+};
+
+constexpr int FR_BM = 32;  // rows per workgroup (one MFMA row tile)
+constexpr int FR_D = 4;    // k-steps of B fragments in flight per wave
+
+template <int C>
+constexpr int fr_waves() { return C >= 256 ? 8 : 4; }
+
+// Weights in FRAGMENT order (nbp_weights_frag, per step): the 16-bit weight [N][K] as blocks of 1 KB, block (nt, ks) =
+// the B-operand fragments of rows 32 nt .. 32 nt + 31 at k-step ks, lane l's 16 bytes = row 32 nt + (l & 31), k 16 ks
+// + 8 (l >> 5) .. + 7 at byte 16 l.  A wave's fragment load is then one contiguous KB (row-major weights put each lane
+// on its own 32-byte row segment: measured 2x slower than the launches it replaces at C 512).
+
+// the B fragments of this wave's first D k-steps of C_out[32][N] = A[32][C] . W[N][C]^T (columns wave * N / NW ..):
+// issued ahead of the GEMM (before the previous phase's epilogue), so the K loop starts on landed data
+template <typename H, int C, int N>
+struct RowsB {
+  static constexpr int NW = fr_waves<C>(), TN = N / (32 * NW), KS = C / 16, D = FR_D;
+  vec_t<H, 8> q[D][TN];
+  const H* base;  // this lane's fragment of tile 0, k-step 0
+  __device__ __forceinline__ void prefetch(const H* __restrict__ W) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    base = W + ((long)(wave * (N / (32 * NW))) * KS * 64 + lane) * 8;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) q[d][j] = *reinterpret_cast<const vec_t<H, 8>*>(base + ((long)j * KS + d) * 512);
+  }
+};
+
+// this wave's 32-column tiles, fp32 accumulators; the fragments stream FR_D k-steps ahead
+template <typename H, int C, int N>
+__device__ __forceinline__ void rows_gemm(RowsB<H, C, N>& b, const H* As,
+                                          floatx16 (&acc)[N / (32 * fr_waves<C>())]) {
+  constexpr int TN = RowsB<H, C, N>::TN, KS = C / 16, D = FR_D;
+  static_assert(TN >= 1 && KS % D == 0 && KS >= D, "tile geometry");
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+  auto& bq = b.q;
+  const H* base = b.base;
+  const H* arow = As + r * C;
+  const int akey = r & 15;
+  // straight-line K loop (fully unrolled, one scheduling region per step): a rolled loop had its ring loads sunk to
+  // the top of the next iteration by the compiler, i.e. issued right before their use
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    __builtin_amdgcn_sched_barrier(0);
+    const vec_t<H, 8> af = *reinterpret_cast<const vec_t<H, 8>*>(arow + 8 * ((2 * s + h) ^ akey));
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[j] = mfma32x32x16(af, bq[s % D][j], acc[j]);
+    if (s + D < KS)  // (compile-time)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bq[s % D][j] = *reinterpret_cast<const vec_t<H, 8>*>(base + ((long)j * KS + s + D) * 512);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// this wave's accumulators of the columns [c0, c0 + C) into the fp32 staging rows (stride C + 4)
+template <int C, int N>
+__device__ __forceinline__ void stage_acc(const floatx16 (&acc)[N / (32 * fr_waves<C>())], float* Ss, int c0) {
+  constexpr int NW = fr_waves<C>(), TN = N / (32 * NW), SW = C + 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wave * (N / NW) + j * 32 + (lane & 31) - c0;
+    if (col < 0 || col >= C) continue;  // (wave-uniform: a wave's columns lie in one pass)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+      Ss[row * SW + col] = acc[j][e];
+    }
+  }
+}
+
+template <typename H>
+__device__ __forceinline__ void ld8h(const void* base, long off, float* v) {
+  const vec_t<H, 8> t = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(base) + off);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)t[j];
+}
+// 8 fp32 values rounded to H, each computed in fp32 first: the asm operand keeps the compiler from folding the
+// producing multiply / fma into the conversion (v_fma_mixlo_f16 rounds once; the tiled kernels round twice)
+template <typename H>
+__device__ __forceinline__ vec_t<H, 8> rnd8(const float* v) {
+  vec_t<H, 8> o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = v[j];
+    asm volatile("" : "+v"(t));
+    o[j] = (H)t;
+  }
+  return o;
+}
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const float4 a = ld4(p), b = ld4(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// the LayerNorm of one row's 8-channel chunk (the row's C / 8 chunks are C / 8 consecutive lanes): CM_RESLN /
+// ln_fwd_nhwc arithmetic, fp32 outputs (rounded by the caller), the statistics
+template <int C>
+__device__ __forceinline__ void ln_chunk(const float* xs, const float* w, const float* b, float eps, float* o,
+                                         float2& st) {
+  constexpr int G8 = C / 8;
+  float sm = 0.f, q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sm += xs[j];
+  sm = group_sum<G8>(sm);
+  const float mu = sm / (float)C;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float d = xs[j] - mu;
+    q = fmaf(d, d, q);
+  }
+  q = group_sum<G8>(q);
+  const float dd = sqrtf(q / (float)C + eps), inv = 1.f / dd;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    o[j] = fmaf(w[j], (xs[j] - mu) * inv, b[j]);
+    asm volatile("" : "+v"(o[j]));  // rounded to fp32 before the store conversion (no single-rounding fma_mix)
+  }
+  st = make_float2(mu, dd);
+}
+
+template <typename H, int C>
+__global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
+  constexpr int NW = fr_waves<C>(), NT = 64 * NW, BM = FR_BM;
+  constexpr int NCH = C / 8, SW = C + 4;
+  constexpr int NIT = BM * NCH / NT;  // row-pass chunks per thread
+  static_assert(NCH >= 16 && NIT * NT == BM * NCH, "row-pass geometry");
+  constexpr int AS = BM * C * 2, YS = BM * C * 2, SS = BM * SW * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[AS + YS + SS];
+  H* As = reinterpret_cast<H*>(smem);        // A operand rows, 16-byte chunk c of row r at slot c ^ (r & 15)
+  H* Ys = reinterpret_cast<H*>(smem + AS);   // y rows (conv5's residual), plain
+  float* Ss = reinterpret_cast<float*>(smem + AS + YS);  // fp32 accumulator staging
+  const int tid = threadIdx.x;
+  const int m0 = blockIdx.x * BM, M = p.M;
+  auto aslot = [&](int row, int c) { return As + row * C + 8 * (c ^ (row & 15)); };
+
+  // ---- the row-pass chunks of this thread (row, 8-channel chunk c): the residual x loaded under conv3's K loop
+  int prow[NIT], pc[NIT];
+  long poff[NIT];
+  bool pok[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * NT;
+    prow[it] = e / NCH;
+    pc[it] = e % NCH;
+    pok[it] = m0 + prow[it] < M;
+    poff[it] = (long)(pok[it] ? m0 + prow[it] : M - 1) * C + 8 * pc[it];  // clamped: no load behind a branch
+  }
+  // ---- A = (H)(g * a) of the workgroup's rows (one image: the launcher requires rows_per_img % 32 == 0)
+  {
+    const float* arow = p.a + (long)(m0 / p.rows_per_img) * C;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      float gv[8], sv[8], pr[8];
+      ld8h<H>(p.g, poff[it], gv);
+      ld8(arow + 8 * pc[it], sv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pr[j] = pok[it] ? gv[j] * sv[j] : 0.f;
+      *reinterpret_cast<vec_t<H, 8>*>(aslot(prow[it], pc[it])) = rnd8<H>(pr);
+    }
+  }
+  vec_t<H, 8> xres[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) xres[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.x) + poff[it]);
+  RowsB<H, C, C> b3;
+  b3.prefetch(reinterpret_cast<const H*>(p.w3));
+  __syncthreads();
+
+  // ---- conv3 + bias + beta residual -> y; norm2 -> n2 (the next A operand), stats
+  RowsB<H, C, 2 * C> b4;
+  {
+    floatx16 acc[C / (32 * NW)];
+    rows_gemm<H, C, C>(b3, As, acc);
+    b4.prefetch(reinterpret_cast<const H*>(p.w4));  // conv4's first k-steps under this epilogue
+    stage_acc<C, C>(acc, Ss, 0);
+  }
+  __syncthreads();  // every wave is done with As (conv3's A) and has staged its columns
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = prow[it], c8 = 8 * pc[it];
+    float v[8], bb[8], sc[8], xv[8], yv[8];
+    ld8(Ss + row * SW + c8, v);
+    ld8(p.b3 + c8, bb);
+    ld8(p.beta + c8, sc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xv[j] = (float)xres[it][j];
+      v[j] += bb[j];
+      yv[j] = fmaf(sc[j], v[j], xv[j]);
+    }
+    const vec_t<H, 8> yh = rnd8<H>(yv);
+    *reinterpret_cast<vec_t<H, 8>*>(Ys + row * C + c8) = yh;
+    float xs[8], w[8], b[8], o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xs[j] = (float)yh[j];
+    ld8(p.lnw2 + c8, w);
+    ld8(p.lnb2 + c8, b);
+    float2 st;
+    ln_chunk<C>(xs, w, b, p.eps, o, st);
+    const vec_t<H, 8> nh = rnd8<H>(o);
+    *reinterpret_cast<vec_t<H, 8>*>(aslot(row, pc[it])) = nh;
+    if (pok[it]) {
+      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.y) + poff[it]) = yh;
+      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.n2) + poff[it]) = nh;
+      if (c8 == 0) p.st2[m0 + row] = st;
+    }
+  }
+  __syncthreads();
+
+  // ---- conv4 + bias -> t4 (interleaved pairs); g2 = t4[2c] t4[2c + 1] (the next A operand); two passes of C columns
+  RowsB<H, C, C> b5;
+  {
+    floatx16 acc[2 * C / (32 * NW)];
+    rows_gemm<H, C, 2 * C>(b4, As, acc);
+    b5.prefetch(reinterpret_cast<const H*>(p.w5));  // conv5's first k-steps under this epilogue
+    __syncthreads();  // every wave is done with As (n2): the gates overwrite it
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (pass) __syncthreads();  // pass 0's staging rows are consumed
+      stage_acc<C, 2 * C>(acc, Ss, pass * C);
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int row = prow[it], c8 = 8 * pc[it], gcol = pass * C + c8;  // t4 columns gcol .. gcol + 7
+        float v[8], bb[8];
+        ld8(Ss + row * SW + c8, v);
+        ld8(p.b4 + gcol, bb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += bb[j];
+        float gv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          gv[j] = v[2 * j] * v[2 * j + 1];
+          asm volatile("" : "+v"(gv[j]));  // the fp32 product is what is rounded (the SimpleGate convention)
+        }
+        vec_t<H, 4> gh;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) gh[j] = (H)gv[j];
+        // gate channels gcol / 2 .. + 3: half of the 16-byte chunk gcol / 16 of the A row
+        *reinterpret_cast<vec_t<H, 4>*>(aslot(row, gcol / 16) + (gcol / 2) % 8) = gh;
+        if (pok[it]) {
+          const long r = m0 + row;
+          *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.t4) + r * 2 * C + gcol) = rnd8<H>(v);
+          *reinterpret_cast<vec_t<H, 4>*>(reinterpret_cast<H*>(p.g2) + r * C + gcol / 2) = gh;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- conv5 + bias + gamma residual -> out (+ the next block's norm1)
+  {
+    floatx16 acc[C / (32 * NW)];
+    rows_gemm<H, C, C>(b5, As, acc);
+    stage_acc<C, C>(acc, Ss, 0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = prow[it], c8 = 8 * pc[it];
+    float v[8], bb[8], sc[8], ov[8];
+    ld8(Ss + row * SW + c8, v);
+    ld8(p.b5 + c8, bb);
+    ld8(p.gamma + c8, sc);
+    const vec_t<H, 8> yh = *reinterpret_cast<const vec_t<H, 8>*>(Ys + row * C + c8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] += bb[j];
+      ov[j] = fmaf(sc[j], v[j], (float)yh[j]);
+    }
+    const vec_t<H, 8> oh = rnd8<H>(ov);
+    if (pok[it]) *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.out) + poff[it]) = oh;
+    if (p.lnw1) {  // (uniform)
+      float xs[8], w[8], b[8], o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xs[j] = (float)oh[j];
+      ld8(p.lnw1 + c8, w);
+      ld8(p.lnb1 + c8, b);
+      float2 st;
+      ln_chunk<C>(xs, w, b, p.eps, o, st);
+      if (pok[it]) {
+        *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.nn1) + poff[it]) = rnd8<H>(o);
+        if (c8 == 0) p.nst1[m0 + row] = st;
+      }
+    }
+  }
+}
+
+// fp32 flat parameters -> 16-bit fragment-ordered copies of the listed [rows][cols] matrices (desc rows {offset, rows,
+// cols}; output at the same offsets): one thread per 16-byte output chunk, in output order
+template <typename H>
+__global__ __launch_bounds__(256) void weights_frag_kernel(const float* __restrict__ src, const long* __restrict__ desc,
+                                                           H* __restrict__ dst) {
+  const long off = desc[blockIdx.y * 3], N = desc[blockIdx.y * 3 + 1], K = desc[blockIdx.y * 3 + 2];
+  const long nchunk = N * K / 8;
+  for (long c = blockIdx.x * 256L + threadIdx.x; c < nchunk; c += gridDim.x * 256L) {
+    const long blk = c / 64;
+    const int lane = (int)(c % 64);
+    const long KS = K / 16;
+    const long nt = blk / KS, ks = blk % KS;
+    const long n = nt * 32 + (lane & 31), k = ks * 16 + 8 * (lane >> 5);
+    const float4 a = ld4(src + off + n * K + k), b = ld4(src + off + n * K + k + 4);
+    vec_t<H, 8> o;
+    o[0] = (H)a.x; o[1] = (H)a.y; o[2] = (H)a.z; o[3] = (H)a.w; o[4] = (H)b.x; o[5] = (H)b.y; o[6] = (H)b.z; o[7] = (H)b.w;
+    *reinterpret_cast<vec_t<H, 8>*>(dst + off + c * 8) = o;
+  }
+}
+
+}  // namespace
+}  // namespace nbp
+
+using namespace nbp;
+
+extern "C" {
+
+int nbp_weights_frag(const float* flat, const long* desc, int ndesc, void* out, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(flat && desc && out && ndesc > 0 && ndesc <= 65535, "nbp_weights_frag: bad args");
+  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_weights_frag: dtype 1 (bf16) or 2 (fp16)");
+  NBP_REQUIRE((((uintptr_t)flat | (uintptr_t)out) & 15) == 0, "nbp_weights_frag: flat / out must be 16-byte aligned");
+  NBP_DISPATCH_H(dtype, { weights_frag_kernel<H><<<dim3(64, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<H*>(out)); });
+  return check_launch("weights_frag");
+}
+
+int nbp_ffn_rows_supported(int M, int C, int rows_per_img, int dtype) {
+  if (dtype != 1 && dtype != 2) return 0;
+  if (C != 128 && C != 256 && C != 512) return 0;
+  return M > 0 && rows_per_img > 0 && rows_per_img % FR_BM == 0 && M % rows_per_img == 0 ? 1 : 0;
+}
+
+int nbp_ffn_rows_fwd(const void* g, const float* a, int rows_per_img, const void* x, const void* w3, const float* b3,
+                     const float* beta, const float* lnw2, const float* lnb2, const void* w4, const float* b4,
+                     const void* w5, const float* b5, const float* gamma, const float* lnw1, const float* lnb1, void* y,
+                     void* n2, float* st2, void* t4, void* g2, void* out, void* nn1, float* nst1, int M, int C,
+                     float eps, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(g && a && x && w3 && b3 && beta && lnw2 && lnb2 && w4 && b4 && w5 && b5 && gamma && y && n2 && st2 && t4 &&
+                  g2 && out,
+              "nbp_ffn_rows_fwd: null pointer");
+  NBP_REQUIRE(nbp_ffn_rows_supported(M, C, rows_per_img, dtype),
+              "nbp_ffn_rows_fwd: unsupported shape (M %d C %d rows_per_img %d dtype %d)", M, C, rows_per_img, dtype);
+  NBP_REQUIRE((lnw1 == nullptr) == (lnb1 == nullptr) && (lnw1 == nullptr) == (nn1 == nullptr) &&
+                  (lnw1 == nullptr) == (nst1 == nullptr),
+              "nbp_ffn_rows_fwd: the next LayerNorm's weight, bias, output and statistics come together");
+  const uintptr_t al = (uintptr_t)g | (uintptr_t)x | (uintptr_t)w3 | (uintptr_t)w4 | (uintptr_t)w5 | (uintptr_t)y |
+                       (uintptr_t)n2 | (uintptr_t)t4 | (uintptr_t)g2 | (uintptr_t)out | (uintptr_t)(nn1 ? nn1 : out) |
+                       (uintptr_t)a | (uintptr_t)b3 | (uintptr_t)beta | (uintptr_t)lnw2 | (uintptr_t)lnb2 |
+                       (uintptr_t)b4 | (uintptr_t)b5 | (uintptr_t)gamma | (uintptr_t)(lnw1 ? lnw1 : b5) |
+                       (uintptr_t)(lnb1 ? lnb1 : b5);
+  NBP_REQUIRE((al & 15) == 0, "nbp_ffn_rows_fwd: operands must be 16-byte aligned");
+  NBP_REQUIRE(((uintptr_t)st2 & 7) == 0 && ((uintptr_t)nst1 & 7) == 0, "nbp_ffn_rows_fwd: statistics 8-byte aligned");
+  FfnRowsP p{g, a, x, w3, b3, beta, lnw2, lnb2, w4, b4, w5, b5, gamma, lnw1, lnb1, y, n2,
+             reinterpret_cast<float2*>(st2), t4, g2, out, nn1, reinterpret_cast<float2*>(nst1), M, rows_per_img, eps};
+  const int grid = cdiv(M, FR_BM);
+  lt_begin(S(s));
+  NBP_DISPATCH_H(dtype, {
+    if (C == 128) ffn_rows_fwd<H, 128><<<grid, 64 * fr_waves<128>(), 0, S(s)>>>(p);
+    else if (C == 256) ffn_rows_fwd<H, 256><<<grid, 64 * fr_waves<256>(), 0, S(s)>>>(p);
+    else ffn_rows_fwd<H, 512><<<grid, 64 * fr_waves<512>(), 0, S(s)>>>(p);
+  });
+  {  // per-launch record (nbp_launch_timing): g, x in; y, n2, t4 (2C), g2, out (+ n1) out; the weights once
+    const double Md = M, Cd = C;
+    lt_end(S(s), C == 512 ? "ffn_rows_fwd<512>" : C == 256 ? "ffn_rows_fwd<256>" : "ffn_rows_fwd<128>",
+           8.0 * Md * Cd * Cd, (Md * Cd * (lnw1 ? 9 : 8) + 4 * Cd * Cd) * 2 + Md * 8 * (lnw1 ? 2 : 1));
+  }
+  return check_launch("ffn_rows_fwd");
+}
+
+}  // extern "C"

@@ -323,9 +323,15 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
         for (int j = 0; j < 8; ++j) v[j] = rv[j] > 0.f ? v[j] : 0.f;
       }
       if (CMODE == CM_SG) {
+        // an fp32 product, then one rounding to the storage type -- the SimpleGate convention of every other kernel
+        // (left implicit, the fp16 build formed two of a chunk's four gates with v_fma_mixlo_f16, a single rounding of
+        // the exact product, and the other two with v_pk_mul_f32 + v_cvt_pk_f16_f32)
         float g[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) g[j] = v[2 * j] * v[2 * j + 1];
+        for (int j = 0; j < 4; ++j) {
+          g[j] = v[2 * j] * v[2 * j + 1];
+          asm volatile("" : "+v"(g[j]));
+        }
         // 4 gate values (8 bytes of bf16 / 16 of fp32) at row grow, column gcol / 2 of the [M][N/2] map
         if constexpr (sizeof(TC) == 4) {
           st4(reinterpret_cast<float*>(p.pre) + (long)grow * (p.ldc / 2) + gcol / 2, make_float4(g[0], g[1], g[2], g[3]));
@@ -388,7 +394,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
         if (CMODE == CM_MASK) x = ldf<TC>(p.R, off) > 0.f ? x : 0.f;
         if (CMODE == CM_SG) {
           v[j] = x;
-          if (j & 1) stf<TC>(p.pre, (long)grow * (p.ldc / 2) + col / 2, v[j - 1] * x);
+          if (j & 1) {
+            float gq = v[j - 1] * x;
+            asm volatile("" : "+v"(gq));  // (as the vector path: an fp32 product, then one rounding)
+            stf<TC>(p.pre, (long)grow * (p.ldc / 2) + col / 2, gq);
+          }
         } else if (p.pre) {
           stf<TC>(p.pre, off, x);
         }

@@ -116,6 +116,9 @@ class NAFNet(nn.Module):
         # level 0 with that rebuild: conv4 -> SimpleGate -> conv5 (+ residual + next LayerNorm) as one pass
         # (nbp_gemm_ffn, bitwise the two launches, +0.1 % step), g2 never stored
         self.fuse_ffn = True
+        # levels with C in {128, 256, 512} (16-bit): conv3 -> norm2 -> conv4 -> SimpleGate -> conv5 (-> the next norm1)
+        # in one row-stationary launch (nbp_ffn_rows_fwd; bitwise the launches it replaces)
+        self.fuse_ffn_rows = True
         # level 0: conv1's weight / bias gradients folded into the conv1 dgrad + norm1 backward pass (nbp_dgrad_ln_bwd_wg:
         # n1 rebuilt from x and the LN statistics, dt1 already in registers; False: a separate nbp_wgrad_f32 launch)
         self.ln_wg = True
@@ -151,6 +154,14 @@ class NAFNet(nn.Module):
                                         for k, e in self.entries.items() if self._is_gemm_weight(k)],
                                        dtype=torch.int64).reshape(-1, 4)
         self._tdesc = None
+        # the weights nbp_ffn_rows_fwd reads (conv3 / conv4 / conv5 of the levels with C in {128, 256, 512}), {offset,
+        # rows, cols}
+        self._fdesc_cpu = torch.tensor([[e.offset, e.ref_shape[0], e.numel // e.ref_shape[0]]
+                                        for k, e in self.entries.items()
+                                        if k.endswith(("conv3.weight", "conv4.weight", "conv5.weight"))
+                                        and e.numel // e.ref_shape[0] in (128, 256, 512)],
+                                       dtype=torch.int64).reshape(-1, 3)
+        self._fdesc = None
 
     # ------------------------------------------------------------------ layout
     def _build_layout(self):
@@ -221,13 +232,19 @@ class NAFNet(nn.Module):
             k.startswith(("downs.", "ups.")) and k.endswith("weight"))
 
     def _prep_weights(self, P: torch.Tensor):
-        """16-bit copy of the flat parameters + transposed copies of the GEMM weights (for the dgrads)."""
+        """16-bit copy of the flat parameters + transposed copies of the GEMM weights (for the dgrads) + fragment-ordered
+        copies of the deep levels' conv3 / conv4 / conv5 weights (nbp_ffn_rows_fwd; None when no level takes it)."""
         if self._tdesc is None or self._tdesc.device != P.device:
             self._tdesc = self._tdesc_cpu.to(P.device)
+            self._fdesc = self._fdesc_cpu.to(P.device) if self._fdesc_cpu.shape[0] else None
         wb = torch.empty(self.numel, dtype=self.adt, device=P.device)
         wt = torch.empty(self.numel, dtype=self.adt, device=P.device)
         call("weights_bf16", P, self.numel, wb, self._tdesc, self._tdesc.shape[0], wt, self.dt)
-        return wb, wt
+        wf = None
+        if self.fuse_ffn_rows and self._fdesc is not None:
+            wf = torch.empty(self.numel, dtype=self.adt, device=P.device)
+            call("weights_frag", P, self._fdesc, self._fdesc.shape[0], wf, self.dt)
+        return wb, wt, wf
 
     @property
     def adt(self) -> torch.dtype:
@@ -406,12 +423,12 @@ class NAFNet(nn.Module):
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: torch.empty(*s, device=dev)  # noqa: E731  (fp32 statistics)
         dt = self.dt
-        fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) == 3 and c in (32, 64, 128, 256)
+        fuse_ln = self.fuse_ln_fwd and dt != 0 and len(self._W) >= 3 and c in (32, 64, 128, 256)
         carry, self._ln_carry = self._ln_carry, None
         have_n1 = carry is not None and carry[0] is x
         n1, st1 = (carry[1], carry[2]) if have_n1 else (E(M, c), F(M, 2))
-        tile = len(self._W) == 3 and self.tile_level(B, h, w, c)
-        c1dw = (not tile and self.fuse_c1dw and dt != 0 and len(self._W) == 3
+        tile = len(self._W) >= 3 and self.tile_level(B, h, w, c)
+        c1dw = (not tile and self.fuse_c1dw and dt != 0 and len(self._W) >= 3
                 and query("c1dw_supported", h, w, c, dt) == 1)
         chunks = (query("c1dw_tile_rows", h, w, c) if tile else
                   (1 if c1dw else query("dw_fwd_slab_rows", B, h, w, c, dt)))
@@ -423,14 +440,18 @@ class NAFNet(nn.Module):
         y, n2, st2 = E(M, c), E(M, c), F(M, 2)
         # t4 channel pairs interleaved (conv4 rows stored so); at C = 32 it is dropped when the backward rebuilds
         # it (sg_rc) or there is no backward
-        drop_t4 = dt != 0 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) == 3))
+        drop_t4 = dt != 0 and c == 32 and (tape is None or (self.sg_rc and self.fold_ls and len(self._W) >= 3))
         # the fused FFN half (g2 never stored) wherever the backward rebuilds g2 too (nbp_dgrad_sg_rc_wg)
-        ffn = drop_t4 and self.fuse_ffn and len(self._W) == 3 and (tape is None or self.sg_rc_wg)
+        ffn = drop_t4 and self.fuse_ffn and len(self._W) >= 3 and (tape is None or self.sg_rc_wg)
         t4, g2 = (None if drop_t4 else E(M, 2 * c)), (None if ffn else E(M, c))
         out = E(M, c)
-        carry_next = fuse_ln and next_pre is not None
-        nn1, nst1 = (E(M, c), F(M, 2)) if carry_next else (None, None)
         hw = h * w
+        # deep levels (C 128 / 256 / 512): conv3 -> norm2 -> conv4 -> SimpleGate -> conv5 (-> the next norm1) as ONE
+        # row-stationary launch (nbp_ffn_rows_fwd, bitwise the launches it replaces)
+        rows_ffn = (self.fuse_ffn_rows and dt != 0 and len(self._W) >= 4 and self._W[3] is not None and t4 is not None
+                    and g2 is not None and query("ffn_rows_supported", M, c, hw, dt) == 1)
+        carry_next = (fuse_ln or rows_ffn) and next_pre is not None
+        nn1, nst1 = (E(M, c), F(M, 2)) if carry_next else (None, None)
         if not have_n1:
             call("ln_fwd_nhwc", x, self._slice(P, pre + "norm1.weight"), self._slice(P, pre + "norm1.bias"),
                  n1, st1, M, c, LN_EPS, dt)
@@ -449,7 +470,16 @@ class NAFNet(nn.Module):
                  t2, g, pool, B, h, w, c, dt)
         call("sca_fwd", pool, chunks, self._slice(P, pre + "sca.1.weight"), self._slice(P, pre + "sca.1.bias"),
              mean, a, B, hw, c)
-        if fuse_ln:
+        if rows_ffn:
+            lnw, lnb = ((self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"))
+                        if carry_next else (None, None))
+            call("ffn_rows_fwd", g, a, hw, x, self._slice(self._W[3], pre + "conv3.weight"),
+                 self._slice(P, pre + "conv3.bias"), self._slice(P, pre + "beta"), self._slice(P, pre + "norm2.weight"),
+                 self._slice(P, pre + "norm2.bias"), self._slice(self._W[3], pre + "conv4.weight"),
+                 self._slice(P, pre + "conv4.bias"), self._slice(self._W[3], pre + "conv5.weight"),
+                 self._slice(P, pre + "conv5.bias"), self._slice(P, pre + "gamma"), lnw, lnb, y, n2, st2, t4, g2, out,
+                 nn1, nst1, M, c, LN_EPS, dt)
+        elif fuse_ln:
             call("gemm_res_ln", g, c, AM_SCALE, a, hw, self._slice(self._W[1], pre + "conv3.weight"), c, y,
                  M, c, c, self._slice(P, pre + "conv3.bias"), x, self._slice(P, pre + "beta"),
                  self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"), n2, st2, LN_EPS,
@@ -459,7 +489,9 @@ class NAFNet(nn.Module):
                      bias=self._slice(P, pre + "conv3.bias"), R=x, rscale=self._slice(P, pre + "beta"))
             call("ln_fwd_nhwc", y, self._slice(P, pre + "norm2.weight"), self._slice(P, pre + "norm2.bias"),
                  n2, st2, M, c, LN_EPS, dt)
-        if ffn:
+        if rows_ffn:
+            pass
+        elif ffn:
             lnw, lnb = ((self._slice(P, next_pre + "norm1.weight"), self._slice(P, next_pre + "norm1.bias"))
                         if carry_next else (None, None))
             call("gemm_ffn", n2, self._slice(self._W[1], pre + "conv4.weight"), self._slice(P, pre + "conv4.bias"),
@@ -472,7 +504,7 @@ class NAFNet(nn.Module):
             self._mm(self._W, n2, c, AM_PLAIN, None, 1, pre + "conv4.weight", t4, 2 * c, CM_PLAIN, M, 2 * c,
                      c, bias=self._slice(P, pre + "conv4.bias"))
             call("sg_fwd", t4, g2, M, c, 1, dt)
-        if ffn:
+        if ffn or rows_ffn:
             pass
         elif carry_next:
             call("gemm_res_ln", g2, c, AM_PLAIN, None, 1, self._slice(self._W[1], pre + "conv5.weight"), c,
@@ -664,7 +696,7 @@ class NAFNet(nn.Module):
         # (gamma as the A-operand column scale); U5 = dout^T g2, V5 = colsum dout feed dW5 = gamma (.) U5,
         # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
         dt4 = E(M, 2 * c)
-        folded = len(Wt) == 3 and self.fold_ls  # gamma / beta already in the transposed bf16 weights
+        folded = len(Wt) >= 3 and self.fold_ls  # gamma / beta already in the transposed bf16 weights
         U5, V5 = F(c * c), F(c)
         wg_folded = False
         if dt != 0:  # SimpleGate backward in the dgrad epilogue: dg2 never materialises

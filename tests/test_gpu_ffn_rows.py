@@ -1,0 +1,164 @@
+"""The deep-level FFN half in one row-stationary launch (nbp_ffn_rows_fwd; NAFNet_arch.py:69-80 after the SCA, with the
+next block's norm1, arch_util.py:264-275): every tensor it stores -- y, n2 and its statistics, t4, g2, out and the next
+block's n1 and statistics -- bitwise equal to the launches it replaces (conv3 with the SCA scale + residual and norm2,
+conv4 with the SimpleGate epilogue, conv5 + residual (+ norm1)), at C 128 / 256 / 512 in both 16-bit types and images
+of 256 / 1024 / 4096 rows; and a network whose levels 2 / 3 / middle take it trains
+bitwise like the unfused network."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DT = {1: torch.bfloat16, 2: torch.float16}
+AM_SCALE, AM_PLAIN, CM_PLAIN, CM_SG = 2, 0, 0, 4
+EPS = 1e-6
+
+
+def _bits(t):
+    return t.view(torch.int16) if t.dtype in (torch.float16, torch.bfloat16) else t.view(torch.int32)
+
+
+def _operands(dev, dt, B, hw, C, seed):
+    Ht = DT[dt]
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    M = B * hw
+    R = lambda *s: torch.randn(*s, device=dev, generator=gen)  # noqa: E731
+    ops = dict(
+        g=R(M, C).to(Ht), a=torch.rand(B, C, device=dev, generator=gen) + 0.5, x=(R(M, C) * 2 + 0.3).to(Ht),
+        w3=(R(C, C) / C ** 0.5).to(Ht), b3=R(C) * 0.1, beta=R(C) * 0.3, lnw2=1 + 0.1 * R(C), lnb2=0.1 * R(C),
+        w4=(R(2 * C, C) / C ** 0.5).to(Ht), b4=R(2 * C) * 0.1, w5=(R(C, C) / C ** 0.5).to(Ht), b5=R(C) * 0.1,
+        gamma=R(C) * 0.3, lnw1=1 + 0.1 * R(C), lnb1=0.1 * R(C))
+    return ops
+
+
+def to_frag(W):
+    """[N][K] -> fragment order (include/nbp.h nbp_weights_frag): 1-KB blocks (32-row tile, 16-wide k-step), lane l =
+    row (l & 31), k half (l >> 5)"""
+    N, K = W.shape
+    return W.reshape(N // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4).contiguous().reshape(-1)
+
+
+def _fused(dev, dt, M, C, hw, o, nxt, got):
+    from lowlight_image_enhancement_amd._lib import call
+    if "f3" not in o:
+        o["f3"], o["f4"], o["f5"] = to_frag(o["w3"]), to_frag(o["w4"]), to_frag(o["w5"])
+    call("ffn_rows_fwd", o["g"], o["a"], hw, o["x"], o["f3"], o["b3"], o["beta"], o["lnw2"], o["lnb2"],
+         o["f4"], o["b4"], o["f5"], o["b5"], o["gamma"], o["lnw1"] if nxt else None,
+         o["lnb1"] if nxt else None, got["y"], got["n2"], got["st2"], got["t4"], got["g2"], got["out"], got["nn1"],
+         got["nst1"], M, C, EPS, dt)
+
+
+def _reference(dev, dt, M, C, hw, o, nxt):
+    """the launches the executor issued before (nafnet.py _block_fwd: conv3 / norm2, conv4 CM_SG, conv5 / norm1)"""
+    from lowlight_image_enhancement_amd._lib import call
+    Ht = DT[dt]
+    E = lambda n: torch.empty(M, n, device=dev, dtype=Ht)  # noqa: E731
+    y, n2, g2, out = E(C), E(C), E(C), E(C)
+    t4 = E(2 * C)
+    st2 = torch.empty(M, 2, device=dev)
+    nn1, nst1 = (E(C), torch.empty(M, 2, device=dev)) if nxt else (None, None)
+    if C in (128, 256):
+        call("gemm_res_ln", o["g"], C, AM_SCALE, o["a"], hw, o["w3"], C, y, M, C, C, o["b3"], o["x"], o["beta"],
+             o["lnw2"], o["lnb2"], n2, st2, EPS, dt)
+    else:
+        call("gemm_bf16", o["g"], C, AM_SCALE, o["a"], hw, dt, o["w3"], C, y, C, CM_PLAIN, dt, M, C, C, 0, 0, 0,
+             o["b3"], o["x"], o["beta"], None)
+        call("ln_fwd_nhwc", y, o["lnw2"], o["lnb2"], n2, st2, M, C, EPS, dt)
+    call("gemm_bf16", n2, C, AM_PLAIN, None, 1, dt, o["w4"], C, t4, 2 * C, CM_SG, dt, M, 2 * C, C, 0, 0, 0, o["b4"], None,
+         None, g2)
+    if nxt and C in (128, 256):
+        call("gemm_res_ln", g2, C, AM_PLAIN, None, 1, o["w5"], C, out, M, C, C, o["b5"], y, o["gamma"], o["lnw1"],
+             o["lnb1"], nn1, nst1, EPS, dt)
+    else:
+        call("gemm_bf16", g2, C, AM_PLAIN, None, 1, dt, o["w5"], C, out, C, CM_PLAIN, dt, M, C, C, 0, 0, 0, o["b5"], y,
+             o["gamma"], None)
+        if nxt:
+            call("ln_fwd_nhwc", out, o["lnw1"], o["lnb1"], nn1, nst1, M, C, EPS, dt)
+    return dict(y=y, n2=n2, st2=st2, t4=t4, g2=g2, out=out, nn1=nn1, nst1=nst1)
+
+
+CASES = [(128, 2, 4096, True), (128, 1, 1024, False), (256, 2, 1024, True), (256, 3, 256, True), (256, 1, 4096, False),
+         (512, 16, 256, False), (512, 2, 256, True), (512, 1, 1024, True)]
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("C,B,hw,nxt", CASES)
+def test_ffn_rows_bitwise_equals_the_launches(dev, dt, C, B, hw, nxt):
+    from lowlight_image_enhancement_amd._lib import call, query
+    M = B * hw
+    assert query("ffn_rows_supported", M, C, hw, dt) == 1
+    o = _operands(dev, dt, B, hw, C, C + B + hw + dt)
+    ref = _reference(dev, dt, M, C, hw, o, nxt)
+    Ht = DT[dt]
+    # outputs pre-filled with NaN: every element must be written
+    nan = lambda *s, dtype=Ht: torch.full(s, float("nan"), device=dev, dtype=dtype)  # noqa: E731
+    got = dict(y=nan(M, C), n2=nan(M, C), st2=nan(M, 2, dtype=torch.float32), t4=nan(M, 2 * C), g2=nan(M, C),
+               out=nan(M, C), nn1=nan(M, C) if nxt else None,
+               nst1=nan(M, 2, dtype=torch.float32) if nxt else None)
+    _fused(dev, dt, M, C, hw, o, nxt, got)
+    torch.cuda.synchronize()
+    for k, v in ref.items():
+        if v is None:
+            continue
+        assert torch.equal(_bits(got[k]), _bits(v)), (k, (got[k].float() - v.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+def test_weights_frag_layout(dev, dt):
+    """nbp_weights_frag: the 16-bit fragment-ordered copies at their flat offsets, bitwise the torch permutation of the
+    rounded rows (the rest of the buffer untouched)."""
+    from lowlight_image_enhancement_amd._lib import call
+    gen = torch.Generator(device=dev).manual_seed(3)
+    shapes = [(256, 128), (512, 256), (1024, 512), (512, 512)]
+    offs, o = [], 8
+    for n, k in shapes:
+        offs.append(o)
+        o += n * k + 8
+    flat = torch.randn(o, device=dev, generator=gen)
+    desc = torch.tensor([[of, n, k] for of, (n, k) in zip(offs, shapes)], dtype=torch.int64, device=dev)
+    out = torch.full((o,), 7.0, device=dev, dtype=DT[dt])
+    call("weights_frag", flat, desc, len(shapes), out, dt)
+    torch.cuda.synchronize()
+    for of, (n, k) in zip(offs, shapes):
+        ref = to_frag(flat[of:of + n * k].view(n, k).to(DT[dt]))
+        assert torch.equal(_bits(out[of:of + n * k]), _bits(ref))
+        assert (out[of - 8:of].float() == 7.0).all()
+
+
+def test_ffn_rows_refusals(dev):
+    """Shapes not served: C outside {128, 256, 512}, the fp32 mode, images whose row count is not a multiple of 32 (the
+    executor keeps the launches there); a call with such a shape fails loudly."""
+    from lowlight_image_enhancement_amd._lib import NBPError, call, query
+    assert query("ffn_rows_supported", 4096, 512, 256, 2) == 1
+    assert query("ffn_rows_supported", 4096, 64, 256, 2) == 0
+    assert query("ffn_rows_supported", 48 * 5, 256, 48, 2) == 0
+    assert query("ffn_rows_supported", 4096, 256, 256, 0) == 0
+    z = torch.zeros(64, device=dev)
+    with pytest.raises(NBPError, match="unsupported shape"):
+        call("ffn_rows_fwd", z, z, 48, z, z, z, z, z, z, z, z, z, z, z, None, None, z, z, z, z, z, z, None, None, 48,
+             256, EPS, 2)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_ffn_rows_network_bitwise(dev, precision):
+    """Width 32, four downs at 128^2: levels 2 (32^2, C 128), 3 (16^2, C 256) and the middle (8^2 = 64 rows, C 512) take
+    the fused launch; outputs and every parameter gradient bitwise those of the unfused network."""
+    from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
+    torch.manual_seed(9)
+    net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[1, 1, 2, 2], middle_blk_num=2,
+                           dec_blk_nums=[1, 1, 1, 1]).to(dev)
+    net.precision = precision
+    with torch.no_grad():
+        net.flat.add_(torch.randn_like(net.flat) * 0.02)
+    x = torch.rand(2, 3, 128, 128, device=dev)
+    res = []
+    for fuse in (True, False):
+        net.fuse_ffn_rows = fuse
+        net.flat.grad = None
+        out = net(x)
+        out.square().mean().backward()
+        res.append((out.detach().clone(), net.flat.grad.clone()))
+    net.fuse_ffn_rows = True
+    (o1, g1), (o0, g0) = res
+    assert torch.equal(o1, o0)
+    assert torch.equal(g1, g0)
