@@ -93,7 +93,9 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
              "dw_bwd_tiled<T,true,32>": "dw_bwd_32", "dw_bwd_tiled<T,true,16>": "dw_bwd_16",
              "wgrad_bf16_wide_group<3,512,2>": "wgrad_group_512", "wgrad_bf16_wide_group<3,768,4>": "wgrad_group_768",
              "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad",
-             "ffn_rows_fwd<512>": "ffn_rows_512", "ffn_rows_fwd<256>": "ffn_rows_256", "ffn_rows_fwd<128>": "ffn_rows_128"}
+             "ffn_rows_fwd<512>": "ffn_rows_512", "ffn_rows_fwd<256>": "ffn_rows_256", "ffn_rows_fwd<128>": "ffn_rows_128",
+             "ffn_rows_bwd<512>": "ffn_rows_bwd_512", "ffn_rows_bwd<256>": "ffn_rows_bwd_256",
+             "ffn_rows_bwd<128>": "ffn_rows_bwd_128"}
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
     "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32E(Li\d+E)?E"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64E(Li\d+E)?E"],
@@ -102,7 +104,9 @@ ROCPROF_KERNELS.update({
     "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],
     "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"],
     "ffn_rows_512": [r"ffn_rows_fwdI{T}Li512EE"], "ffn_rows_256": [r"ffn_rows_fwdI{T}Li256EE"],
-    "ffn_rows_128": [r"ffn_rows_fwdI{T}Li128EE"], "ffn_rows": ["ffn_rows_fwd"]})
+    "ffn_rows_128": [r"ffn_rows_fwdI{T}Li128EE"], "ffn_rows": ["ffn_rows_fwd", "ffn_rows_bwd"],
+    "ffn_rows_bwd_512": [r"ffn_rows_bwdI{T}Li512EE"], "ffn_rows_bwd_256": [r"ffn_rows_bwdI{T}Li256EE"],
+    "ffn_rows_bwd_128": [r"ffn_rows_bwdI{T}Li128EE"]})
 # the Itanium mangling of the storage type in those names
 MANGLED_T = {"fp16": "DF16_", "bf16": "DF16b", "fp32": "f"}
 UNIT_DEF = {
@@ -122,6 +126,9 @@ UNIT_DEF = {
     "ffn_rows_512": "per pixel: g C + x C read, y + n2 + t4 (2C) + g2 + out (+ the next n1) written = 8-9 C s bytes, "
                     "+ the three weights (4 C^2 s) once per launch (the middle level: C 512 at 16^2)",
     "ffn_rows_256": "as ffn_rows_512 at C 256 (32^2)", "ffn_rows_128": "as ffn_rows_512 at C 128 (64^2)",
+    "ffn_rows_bwd_512": "per pixel: dout C + t4 2C + y C + g C read, dt4 2C + dy C + dh C written = 9 C s bytes, + the "
+                        "three weights (4 C^2 s) once per launch and the per-32-row partial sums (the middle level)",
+    "ffn_rows_bwd_256": "as ffn_rows_bwd_512 at C 256 (32^2)", "ffn_rows_bwd_128": "as ffn_rows_bwd_512 at C 128 (64^2)",
 }
 
 
@@ -229,6 +236,11 @@ def cost_ffn_rows(a):  # (g,a,hw,x,w3,b3,beta,lnw2,lnb2,w4,b4,w5,b5,gamma,lnw1,l
     return 8.0 * M * C * C, (M * C * (9 if nxt else 8) + 4 * C * C) * 2 + M * 8 * (2 if nxt else 1)
 
 
+def cost_ffn_rows_bwd(a):  # (dout,t4,y,st2,lnw2,g,w5t,w4t,w3t,dt4,dy,dh,sw,sb,da,M,C,hw,dt)
+    M, C = a[15], a[16]
+    return 8.0 * M * C * C, (M * C * 9 + 4 * C * C) * 2 + M * 8 + 3 * (M // 32) * C * 4
+
+
 def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)
     M, N, K = a[11], a[12], a[13]
     return 2.0 * M * N * K, 4 * (M * K + N * K + M * N + (M * N if a[18] is not None else 0))
@@ -285,7 +297,7 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
            "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile),
            "c1dw_bwd_tile": rec_plain("c1dw_tile_bwd", cost_c1dw_bwd_tile),
-           "ffn_rows_fwd": rec_plain("ffn_rows", cost_ffn_rows)}
+           "ffn_rows_fwd": rec_plain("ffn_rows", cost_ffn_rows), "ffn_rows_bwd": rec_plain("ffn_rows", cost_ffn_rows_bwd)}
 
 
 def _pmc_newest_key(f):

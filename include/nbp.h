@@ -155,16 +155,27 @@ int nbp_gemm_ffn(const void* n2, const void* W4, const float* b4, const void* W5
  * 16-bit): y = x + beta (.) ((g (.) a) W3^T + b3); n2 / st2 = LayerNorm2d(y) (norm2); t4 = n2 W4^T + b4 (SimpleGate pairs
  * interleaved, 2C columns); g2 = t4[2c] t4[2c + 1]; out = y + gamma (.) (g2 W5^T + b5); with lnw1 / lnb1 also the next
  * block's norm1 of out into nn1 / nst1.  a: [B][C] SCA scale (per image of rows_per_img rows); weights w3 / w4 / w5:
- * 16-bit copies in fragment order (nbp_weights_frag).  Replaces nbp_gemm_bf16 / nbp_gemm_res_ln (conv3) + nbp_ln_fwd_nhwc + nbp_gemm_bf16 CM_SG
+ * 16-bit copies in fragment order (nbp_frag16).  Replaces nbp_gemm_bf16 / nbp_gemm_res_ln (conv3) + nbp_ln_fwd_nhwc + nbp_gemm_bf16 CM_SG
  * (conv4) + nbp_gemm_res_ln / nbp_gemm_bf16 (conv5) + nbp_ln_fwd_nhwc, bitwise: every stored tensor equals theirs.
  * Stats are (mu, den) float pairs.  nbp_ffn_rows_supported(M, C, rows_per_img, dtype): 1 for the shapes served
  * (rows_per_img a multiple of 32). */
 int nbp_ffn_rows_supported(int M, int C, int rows_per_img, int dtype);
-/* The weights of nbp_ffn_rows_fwd in fragment order (per step, from the fp32 flat parameters): desc = [ndesc][3] int64
- * {offset, rows N, cols K} (N a multiple of 32, K of 16); the 16-bit copy of matrix i goes to out at its own offset, as
- * 1-KB blocks (32-row tile nt, 16-wide k-step ks) in (nt, ks) order, lane l's 16 bytes = row 32 nt + (l & 31), k 16 ks
- * + 8 (l >> 5) .. + 7 (the 32 x 32 x 16 MFMA B operand; one contiguous load per wave). */
-int nbp_weights_frag(const float* flat, const long* desc, int ndesc, void* out, int dtype, nbp_stream_t s);
+/* 16-bit matrices [N][K] at their flat offsets (desc = [ndesc][3] int64 {offset, N, K}; N a multiple of 32, K of 16)
+ * copied into fragment order at the same offsets of out: 1-KB blocks (32-row tile nt, 16-wide k-step ks) in (nt, ks)
+ * order, lane l's 16 bytes = row 32 nt + (l & 31), k 16 ks + 8 (l >> 5) .. + 7 (the 32 x 32 x 16 MFMA B operand of
+ * nbp_ffn_rows_fwd / nbp_ffn_rows_bwd; one contiguous load per wave).  A permutation: values bitwise the source's. */
+int nbp_frag16(const void* src, const long* desc, int ndesc, void* out, nbp_stream_t s);
+/* The backward of nbp_ffn_rows_fwd's chain in ONE row-stationary launch (levels C 128 / 256 / 512, 16-bit): dg2 = dout
+ * W5'^T, dt4 = SimpleGate backward on the stored t4, dn2 = dt4 W4^T, dy = LayerNorm2d backward (norm2: y, st2, lnw2) +
+ * dout, dh = dy W3'^T, where W5' / W3' are the layer-scale-folded transposed weights of the tiled dgrads (gamma / beta
+ * (.) W)^T and all three weights are fragment-ordered (nbp_frag16 of the transposed 16-bit copies); plus, per 32-row
+ * block b, slab_w[b] = sum dn2 * yhat, slab_b[b] = sum dn2 (norm2's weight / bias gradient partials) and da[b] = sum dh
+ * (.) g (the SCA channel-dot partials, [B][rows_per_img / 32][C]).  Replaces nbp_gemm_bf16 CM_SGBWD + nbp_dgrad_ln_bwd
+ * (or nbp_gemm_bf16 + nbp_ln_bwd_nhwc at C 512) + nbp_gemm_bf16 CM_CHANDOT: dt4 / dy / dh bitwise theirs, the partial
+ * sums up to fp32 summation order.  Shapes as nbp_ffn_rows_supported. */
+int nbp_ffn_rows_bwd(const void* dout, const void* t4, const void* y, const float* st2, const float* lnw2, const void* g,
+                     const void* w5t, const void* w4t, const void* w3t, void* dt4, void* dy, void* dh, float* slab_w,
+                     float* slab_b, float* da, int M, int C, int rows_per_img, int dtype, nbp_stream_t s);
 int nbp_ffn_rows_fwd(const void* g, const float* a, int rows_per_img, const void* x, const void* w3, const float* b3,
                      const float* beta, const float* lnw2, const float* lnb2, const void* w4, const float* b4,
                      const void* w5, const float* b5, const float* gamma, const float* lnw1, const float* lnb1, void* y,

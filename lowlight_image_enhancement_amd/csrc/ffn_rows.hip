@@ -55,21 +55,21 @@ constexpr int FR_D = 4;    // k-steps of B fragments in flight per wave
 template <int C>
 constexpr int fr_waves() { return C >= 256 ? 8 : 4; }
 
-// Weights in FRAGMENT order (nbp_weights_frag, per step): the 16-bit weight [N][K] as blocks of 1 KB, block (nt, ks) =
-// the B-operand fragments of rows 32 nt .. 32 nt + 31 at k-step ks, lane l's 16 bytes = row 32 nt + (l & 31), k 16 ks
-// + 8 (l >> 5) .. + 7 at byte 16 l.  A wave's fragment load is then one contiguous KB (row-major weights put each lane
-// on its own 32-byte row segment: measured 2x slower than the launches it replaces at C 512).
+// Weights in FRAGMENT order (nbp_frag16, per step): a 16-bit B operand [N][K] as blocks of 1 KB, block (nt, ks) = the
+// fragments of rows 32 nt .. 32 nt + 31 at k-step ks, lane l's 16 bytes = row 32 nt + (l & 31), k 16 ks + 8 (l >> 5)
+// .. + 7 at byte 16 l.  A wave's fragment load is one contiguous KB (row-major weights put each lane on its own
+// 32-byte row segment: measured 2x slower than the launches the forward kernel replaces at C 512).
 
-// the B fragments of this wave's first D k-steps of C_out[32][N] = A[32][C] . W[N][C]^T (columns wave * N / NW ..):
-// issued ahead of the GEMM (before the previous phase's epilogue), so the K loop starts on landed data
-template <typename H, int C, int N>
+// the B fragments of this wave's first D k-steps of C_out[32][N] = A[32][K] . B[N][K]^T (this wave's columns: wave *
+// N / NW ..), issued ahead of the GEMM (under the previous phase's epilogue): the K loop starts on landed data
+template <typename H, int NW, int K, int N>
 struct RowsB {
-  static constexpr int NW = fr_waves<C>(), TN = N / (32 * NW), KS = C / 16, D = FR_D;
+  static constexpr int TN = N / (32 * NW), KS = K / 16, D = FR_D;
   vec_t<H, 8> q[D][TN];
   const H* base;  // this lane's fragment of tile 0, k-step 0
   __device__ __forceinline__ void prefetch(const H* __restrict__ W) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    base = W + ((long)(wave * (N / (32 * NW))) * KS * 64 + lane) * 8;
+    base = W + ((long)(wave * TN) * KS * 64 + lane) * 8;
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
@@ -77,12 +77,12 @@ struct RowsB {
   }
 };
 
-// this wave's 32-column tiles, fp32 accumulators; the fragments stream FR_D k-steps ahead
-template <typename H, int C, int N>
-__device__ __forceinline__ void rows_gemm(RowsB<H, C, N>& b, const H* As,
-                                          floatx16 (&acc)[N / (32 * fr_waves<C>())]) {
-  constexpr int TN = RowsB<H, C, N>::TN, KS = C / 16, D = FR_D;
-  static_assert(TN >= 1 && KS % D == 0 && KS >= D, "tile geometry");
+// this wave's 32-column tiles of C_out = A . B^T, fp32 accumulators (K ascending in steps of 16 on one accumulator);
+// A: [32][K] 16-bit in LDS, 16-byte chunk c of row r at slot c ^ (r & 15); the fragments stream FR_D k-steps ahead
+template <typename H, int NW, int K, int N>
+__device__ __forceinline__ void rows_gemm(RowsB<H, NW, K, N>& b, const H* As, floatx16 (&acc)[N / (32 * NW)]) {
+  constexpr int TN = N / (32 * NW), KS = K / 16, D = FR_D;
+  static_assert(TN >= 1 && KS % D == 0 && KS >= D && K / 8 >= 16, "tile geometry");
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int j = 0; j < TN; ++j)
@@ -90,7 +90,7 @@ __device__ __forceinline__ void rows_gemm(RowsB<H, C, N>& b, const H* As,
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
   auto& bq = b.q;
   const H* base = b.base;
-  const H* arow = As + r * C;
+  const H* arow = As + r * K;
   const int akey = r & 15;
   // straight-line K loop (fully unrolled, one scheduling region per step): a rolled loop had its ring loads sunk to
   // the top of the next iteration by the compiler, i.e. issued right before their use
@@ -107,15 +107,15 @@ __device__ __forceinline__ void rows_gemm(RowsB<H, C, N>& b, const H* As,
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// this wave's accumulators of the columns [c0, c0 + C) into the fp32 staging rows (stride C + 4)
-template <int C, int N>
-__device__ __forceinline__ void stage_acc(const floatx16 (&acc)[N / (32 * fr_waves<C>())], float* Ss, int c0) {
-  constexpr int NW = fr_waves<C>(), TN = N / (32 * NW), SW = C + 4;
+// this wave's accumulators of the columns [c0, c0 + PC) into the fp32 staging rows (stride SW floats)
+template <int NW, int N, int PC, int SW>
+__device__ __forceinline__ void stage_acc(const floatx16 (&acc)[N / (32 * NW)], float* Ss, int c0) {
+  constexpr int TN = N / (32 * NW);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = wave * (N / NW) + j * 32 + (lane & 31) - c0;
-    if (col < 0 || col >= C) continue;  // (wave-uniform: a wave's columns lie in one pass)
+    const int col = (wave * TN + j) * 32 + (lane & 31) - c0;
+    if (col < 0 || col >= PC) continue;  // (wave-uniform: a wave's columns lie in one pass)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
@@ -217,17 +217,17 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   vec_t<H, 8> xres[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) xres[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.x) + poff[it]);
-  RowsB<H, C, C> b3;
+  RowsB<H, NW, C, C> b3;
   b3.prefetch(reinterpret_cast<const H*>(p.w3));
   __syncthreads();
 
   // ---- conv3 + bias + beta residual -> y; norm2 -> n2 (the next A operand), stats
-  RowsB<H, C, 2 * C> b4;
+  RowsB<H, NW, C, 2 * C> b4;
   {
     floatx16 acc[C / (32 * NW)];
-    rows_gemm<H, C, C>(b3, As, acc);
+    rows_gemm<H, NW, C, C>(b3, As, acc);
     b4.prefetch(reinterpret_cast<const H*>(p.w4));  // conv4's first k-steps under this epilogue
-    stage_acc<C, C>(acc, Ss, 0);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0);
   }
   __syncthreads();  // every wave is done with As (conv3's A) and has staged its columns
 #pragma unroll
@@ -263,16 +263,16 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   __syncthreads();
 
   // ---- conv4 + bias -> t4 (interleaved pairs); g2 = t4[2c] t4[2c + 1] (the next A operand); two passes of C columns
-  RowsB<H, C, C> b5;
+  RowsB<H, NW, C, C> b5;
   {
     floatx16 acc[2 * C / (32 * NW)];
-    rows_gemm<H, C, 2 * C>(b4, As, acc);
+    rows_gemm<H, NW, C, 2 * C>(b4, As, acc);
     b5.prefetch(reinterpret_cast<const H*>(p.w5));  // conv5's first k-steps under this epilogue
     __syncthreads();  // every wave is done with As (n2): the gates overwrite it
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       if (pass) __syncthreads();  // pass 0's staging rows are consumed
-      stage_acc<C, 2 * C>(acc, Ss, pass * C);
+      stage_acc<NW, 2 * C, C, SW>(acc, Ss, pass * C);
       __syncthreads();
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
@@ -306,8 +306,8 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   // ---- conv5 + bias + gamma residual -> out (+ the next block's norm1)
   {
     floatx16 acc[C / (32 * NW)];
-    rows_gemm<H, C, C>(b5, As, acc);
-    stage_acc<C, C>(acc, Ss, 0);
+    rows_gemm<H, NW, C, C>(b5, As, acc);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0);
   }
   __syncthreads();
 #pragma unroll
@@ -341,24 +341,227 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   }
 }
 
-// fp32 flat parameters -> 16-bit fragment-ordered copies of the listed [rows][cols] matrices (desc rows {offset, rows,
-// cols}; output at the same offsets): one thread per 16-byte output chunk, in output order
-template <typename H>
-__global__ __launch_bounds__(256) void weights_frag_kernel(const float* __restrict__ src, const long* __restrict__ desc,
-                                                           H* __restrict__ dst) {
+// 16-bit [N][K] matrices (desc rows {offset, N, K}) -> fragment order at the same offsets: one thread per 16-byte
+// output chunk, in output order (a permutation: the values are bitwise the source's)
+__global__ __launch_bounds__(256) void frag16_kernel(const uint16_t* __restrict__ src, const long* __restrict__ desc,
+                                                     uint16_t* __restrict__ dst) {
   const long off = desc[blockIdx.y * 3], N = desc[blockIdx.y * 3 + 1], K = desc[blockIdx.y * 3 + 2];
-  const long nchunk = N * K / 8;
+  const long nchunk = N * K / 8, KS = K / 16;
   for (long c = blockIdx.x * 256L + threadIdx.x; c < nchunk; c += gridDim.x * 256L) {
     const long blk = c / 64;
     const int lane = (int)(c % 64);
-    const long KS = K / 16;
-    const long nt = blk / KS, ks = blk % KS;
-    const long n = nt * 32 + (lane & 31), k = ks * 16 + 8 * (lane >> 5);
-    const float4 a = ld4(src + off + n * K + k), b = ld4(src + off + n * K + k + 4);
-    vec_t<H, 8> o;
-    o[0] = (H)a.x; o[1] = (H)a.y; o[2] = (H)a.z; o[3] = (H)a.w; o[4] = (H)b.x; o[5] = (H)b.y; o[6] = (H)b.z; o[7] = (H)b.w;
-    *reinterpret_cast<vec_t<H, 8>*>(dst + off + c * 8) = o;
+    const long n = (blk / KS) * 32 + (lane & 31), k = (blk % KS) * 16 + 8 * (lane >> 5);
+    *reinterpret_cast<uint4*>(dst + off + c * 8) = *reinterpret_cast<const uint4*>(src + off + n * K + k);
   }
+}
+
+// ---------------------------------------------------------------- backward
+// The mirror chain (NAFNet_arch.py:69-80 backward, the layer scales folded into the transposed weights as the tiled
+// dgrads take them): dg2 = dout W5'^T (W5' = (gamma (.) W5)^T); dt4 = SimpleGate backward (dt4[2c] = dg2[c] t4[2c + 1],
+// dt4[2c + 1] = dg2[c] t4[2c]); dn2 = dt4 W4^T...; dy = norm2 backward(dn2) + dout (arch_util.py:277-289); dh = dy W3'^T
+// (W3' = (beta (.) W3)^T), with the SCA channel-dot partials sum_rows dh (.) g and the norm2 weight / bias partials of
+// the workgroup's rows.  A operands in LDS: dout (then dy, in place), dt4; fp32 staging without padding (160 KB at C
+// 512).  dt4 / dy / dh bitwise the launches it replaces (nbp_gemm_bf16 CM_SGBWD; nbp_dgrad_ln_bwd at C 128 / 256, or
+// nbp_gemm_bf16 + nbp_ln_bwd_nhwc on the rounded dn2 at C 512; nbp_gemm_bf16 CM_CHANDOT); the partial sums are per
+// 32-row block in an order of their own.
+struct FfnRowsBwdP {
+  const void* dout;    // [M][C]
+  const void* t4;      // [M][2C] (forward tape, pairs interleaved)
+  const void* y;       // [M][C] norm2 input
+  const float2* st2;   // [M] (mu, den)
+  const float* lnw2;
+  const void* g;       // [M][C] SimpleGate output of the spatial branch (the SCA channel dot)
+  const void* w5;      // fragment-ordered 16-bit (gamma (.) W5)^T   [C][C]
+  const void* w4;      // fragment-ordered 16-bit W4^T               [C][2C]
+  const void* w3;      // fragment-ordered 16-bit (beta (.) W3)^T    [C][C]
+  void* dt4;           // [M][2C] out
+  void* dy;            // [M][C] out
+  void* dh;            // [M][C] out
+  float* slab_w;       // [M / 32][C] out: sum over the block's rows of dn2 * yhat
+  float* slab_b;       // [M / 32][C] out: sum of dn2
+  float* da;           // [M / 32][C] out: sum of dh * g (image-major row blocks: [B][HW / 32][C])
+  int M;
+};
+
+// the partials of one 8-column chunk of every row-pass thread, summed over the threads that share the chunk (lanes
+// C / 8 apart, then the waves in order) into out[c] (Red: LDS scratch of NW x C floats)
+template <int C, int NW>
+__device__ __forceinline__ void chunk_partials_out(float (&v)[8], float* red, float* out) {
+  constexpr int NCH = C / 8;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int o = NCH; o < 64; o <<= 1) v[j] += __shfl_xor(v[j], o, 64);
+  if (lane < NCH)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wave * C + lane * 8 + j] = v[j];
+  __syncthreads();
+  for (int c = tid; c < C; c += 64 * NW) {
+    float t = red[c];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += red[w * C + c];
+    out[c] = t;
+  }
+  __syncthreads();
+}
+
+template <typename H, int C>
+__global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p) {
+  constexpr int NW = fr_waves<C>(), NT = 64 * NW, BM = FR_BM;
+  constexpr int NCH = C / 8, SW = C;
+  constexpr int NIT = BM * NCH / NT;
+  static_assert(NCH >= 16 && NIT * NT == BM * NCH, "row-pass geometry");
+  constexpr int A1 = BM * C * 2, A2 = BM * 2 * C * 2, SS = BM * SW * 4;
+  static_assert(A1 + A2 + SS <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[A1 + A2 + SS];
+  H* Ad = reinterpret_cast<H*>(smem);             // dout rows, then dy (in place)
+  H* At = reinterpret_cast<H*>(smem + A1);        // dt4 rows (2C)
+  float* Ss = reinterpret_cast<float*>(smem + A1 + A2);
+  const int tid = threadIdx.x;
+  const int m0 = blockIdx.x * BM, M = p.M;
+  const long blk = blockIdx.x;
+  auto slot = [&](H* base, int K, int row, int c) { return base + row * K + 8 * (c ^ (row & 15)); };
+
+  int prow[NIT], pc[NIT];
+  long poff[NIT];
+  bool pok[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int e = tid + it * NT;
+    prow[it] = e / NCH;
+    pc[it] = e % NCH;
+    pok[it] = m0 + prow[it] < M;
+    poff[it] = (long)(pok[it] ? m0 + prow[it] : M - 1) * C + 8 * pc[it];
+  }
+  // ---- dout rows -> LDS; the SimpleGate inputs of the first epilogue loaded under the first K loop
+  vec_t<H, 8> tq[NIT][2];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    vec_t<H, 8> d = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.dout) + poff[it]);
+    if (!pok[it]) d = vec_t<H, 8>{};
+    *reinterpret_cast<vec_t<H, 8>*>(slot(Ad, C, prow[it], pc[it])) = d;
+    const H* t4 = reinterpret_cast<const H*>(p.t4) + 2 * poff[it];
+    tq[it][0] = *reinterpret_cast<const vec_t<H, 8>*>(t4);
+    tq[it][1] = *reinterpret_cast<const vec_t<H, 8>*>(t4 + 8);
+  }
+  RowsB<H, NW, C, C> b5;
+  b5.prefetch(reinterpret_cast<const H*>(p.w5));
+  __syncthreads();
+
+  // ---- dg2 = dout W5'^T; dt4 (SimpleGate backward) -> memory and the next A operand
+  RowsB<H, NW, 2 * C, C> b4;
+  {
+    floatx16 acc[C / (32 * NW)];
+    rows_gemm<H, NW, C, C>(b5, Ad, acc);
+    b4.prefetch(reinterpret_cast<const H*>(p.w4));
+    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+  }
+  __syncthreads();
+  vec_t<H, 8> yq[NIT];
+  float2 stq[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = prow[it], c8 = 8 * pc[it];
+    float v[8], o[16];
+    ld8(Ss + row * SW + c8, v);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // dt4[2c] = dg[c] t4[2c + 1], dt4[2c + 1] = dg[c] t4[2c]: fp32 products, one rounding
+        o[8 * h + 2 * j] = v[4 * h + j] * (float)tq[it][h][2 * j + 1];
+        o[8 * h + 2 * j + 1] = v[4 * h + j] * (float)tq[it][h][2 * j];
+      }
+    const vec_t<H, 8> lo = rnd8<H>(o), hi = rnd8<H>(o + 8);
+    *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, row, 2 * pc[it])) = lo;
+    *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, row, 2 * pc[it] + 1)) = hi;
+    if (pok[it]) {
+      H* d = reinterpret_cast<H*>(p.dt4) + 2 * poff[it];
+      *reinterpret_cast<vec_t<H, 8>*>(d) = lo;
+      *reinterpret_cast<vec_t<H, 8>*>(d + 8) = hi;
+    }
+    yq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.y) + poff[it]);  // for the LN backward
+    stq[it] = p.st2[pok[it] ? m0 + row : M - 1];
+  }
+  __syncthreads();
+
+  // ---- dn2 = dt4 W4^T; dy = norm2 backward + dout -> memory and the next A operand (in place of dout)
+  RowsB<H, NW, C, C> b3;
+  {
+    floatx16 acc[C / (32 * NW)];
+    rows_gemm<H, NW, 2 * C, C>(b4, At, acc);
+    b3.prefetch(reinterpret_cast<const H*>(p.w3));
+    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+  }
+  __syncthreads();
+  float aw[8], ab[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) aw[j] = ab[j] = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = prow[it], c8 = 8 * pc[it];
+    float d[8], w[8], rr[8], yh[8];
+    ld8(Ss + row * SW + c8, d);
+    if constexpr (C == 512) {  // the two-launch form at this level stores dn2 in the storage type first
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = (float)(H)d[j];
+    }
+    ld8(p.lnw2 + c8, w);
+    const vec_t<H, 8> dres = *reinterpret_cast<const vec_t<H, 8>*>(slot(Ad, C, row, pc[it]));
+    const float2 st = pok[it] ? stq[it] : make_float2(0.f, 1.f);
+    const float rinv = 1.f / st.y;
+    float sg = 0.f, sgy = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!pok[it]) d[j] = 0.f;
+      yh[j] = pok[it] ? ((float)yq[it][j] - st.x) * rinv : 0.f;
+      rr[j] = (float)dres[j];
+      sg = fmaf(d[j], w[j], sg);
+      sgy = fmaf(d[j] * w[j], yh[j], sgy);
+      aw[j] = fmaf(d[j], yh[j], aw[j]);
+      ab[j] += d[j];
+    }
+    sg = group_sum<NCH>(sg);
+    sgy = group_sum<NCH>(sgy);
+    const float mg = sg / (float)C, mgy = sgy / (float)C;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(rinv, fmaf(-yh[j], mgy, d[j] * w[j]) - mg, rr[j]);
+    const vec_t<H, 8> dyh = rnd8<H>(o);
+    *reinterpret_cast<vec_t<H, 8>*>(slot(Ad, C, row, pc[it])) = dyh;
+    if (pok[it]) *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.dy) + poff[it]) = dyh;
+  }
+  __syncthreads();  // dy complete in LDS; the staging rows are free: the norm2 partials through them
+  chunk_partials_out<C, NW>(aw, Ss, p.slab_w + blk * C);
+  chunk_partials_out<C, NW>(ab, Ss, p.slab_b + blk * C);
+  vec_t<H, 8> gq[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) gq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.g) + poff[it]);
+
+  // ---- dh = dy W3'^T -> memory; the SCA channel-dot partials sum_rows dh g
+  {
+    floatx16 acc[C / (32 * NW)];
+    rows_gemm<H, NW, C, C>(b3, Ad, acc);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+  }
+  __syncthreads();
+  float cd[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cd[j] = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = prow[it], c8 = 8 * pc[it];
+    float v[8];
+    ld8(Ss + row * SW + c8, v);
+    const vec_t<H, 8> dhh = rnd8<H>(v);
+    if (pok[it]) {
+      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.dh) + poff[it]) = dhh;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cd[j] = fmaf((float)dhh[j], (float)gq[it][j], cd[j]);
+    }
+  }
+  __syncthreads();  // the staging rows are read: the channel-dot partials through them
+  chunk_partials_out<C, NW>(cd, Ss, p.da + blk * C);
 }
 
 }  // namespace
@@ -368,12 +571,12 @@ using namespace nbp;
 
 extern "C" {
 
-int nbp_weights_frag(const float* flat, const long* desc, int ndesc, void* out, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(flat && desc && out && ndesc > 0 && ndesc <= 65535, "nbp_weights_frag: bad args");
-  NBP_REQUIRE(dtype == 1 || dtype == 2, "nbp_weights_frag: dtype 1 (bf16) or 2 (fp16)");
-  NBP_REQUIRE((((uintptr_t)flat | (uintptr_t)out) & 15) == 0, "nbp_weights_frag: flat / out must be 16-byte aligned");
-  NBP_DISPATCH_H(dtype, { weights_frag_kernel<H><<<dim3(64, ndesc), 256, 0, S(s)>>>(flat, desc, reinterpret_cast<H*>(out)); });
-  return check_launch("weights_frag");
+int nbp_frag16(const void* src, const long* desc, int ndesc, void* out, nbp_stream_t s) {
+  NBP_REQUIRE(src && desc && out && ndesc > 0 && ndesc <= 65535, "nbp_frag16: bad args");
+  NBP_REQUIRE((((uintptr_t)src | (uintptr_t)out) & 15) == 0, "nbp_frag16: src / out must be 16-byte aligned");
+  frag16_kernel<<<dim3(64, ndesc), 256, 0, S(s)>>>(reinterpret_cast<const uint16_t*>(src), desc,
+                                                   reinterpret_cast<uint16_t*>(out));
+  return check_launch("frag16");
 }
 
 int nbp_ffn_rows_supported(int M, int C, int rows_per_img, int dtype) {
@@ -417,6 +620,38 @@ int nbp_ffn_rows_fwd(const void* g, const float* a, int rows_per_img, const void
            8.0 * Md * Cd * Cd, (Md * Cd * (lnw1 ? 9 : 8) + 4 * Cd * Cd) * 2 + Md * 8 * (lnw1 ? 2 : 1));
   }
   return check_launch("ffn_rows_fwd");
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int nbp_ffn_rows_bwd(const void* dout, const void* t4, const void* y, const float* st2, const float* lnw2, const void* g,
+                     const void* w5t, const void* w4t, const void* w3t, void* dt4, void* dy, void* dh, float* slab_w,
+                     float* slab_b, float* da, int M, int C, int rows_per_img, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dout && t4 && y && st2 && lnw2 && g && w5t && w4t && w3t && dt4 && dy && dh && slab_w && slab_b && da,
+              "nbp_ffn_rows_bwd: null pointer");
+  NBP_REQUIRE(nbp_ffn_rows_supported(M, C, rows_per_img, dtype),
+              "nbp_ffn_rows_bwd: unsupported shape (M %d C %d rows_per_img %d dtype %d)", M, C, rows_per_img, dtype);
+  const uintptr_t al = (uintptr_t)dout | (uintptr_t)t4 | (uintptr_t)y | (uintptr_t)lnw2 | (uintptr_t)g | (uintptr_t)w5t |
+                       (uintptr_t)w4t | (uintptr_t)w3t | (uintptr_t)dt4 | (uintptr_t)dy | (uintptr_t)dh |
+                       (uintptr_t)slab_w | (uintptr_t)slab_b | (uintptr_t)da;
+  NBP_REQUIRE((al & 15) == 0 && ((uintptr_t)st2 & 7) == 0, "nbp_ffn_rows_bwd: operands must be 16-byte aligned");
+  FfnRowsBwdP p{dout, t4, y, reinterpret_cast<const float2*>(st2), lnw2, g, w5t, w4t, w3t, dt4, dy, dh, slab_w, slab_b,
+                da, M};
+  const int grid = cdiv(M, FR_BM);
+  lt_begin(S(s));
+  NBP_DISPATCH_H(dtype, {
+    if (C == 128) ffn_rows_bwd<H, 128><<<grid, 64 * fr_waves<128>(), 0, S(s)>>>(p);
+    else if (C == 256) ffn_rows_bwd<H, 256><<<grid, 64 * fr_waves<256>(), 0, S(s)>>>(p);
+    else ffn_rows_bwd<H, 512><<<grid, 64 * fr_waves<512>(), 0, S(s)>>>(p);
+  });
+  {  // per-launch record: dout, t4 (2C), y, g in; dt4 (2C), dy, dh out; the three weights once
+    const double Md = M, Cd = C;
+    lt_end(S(s), C == 512 ? "ffn_rows_bwd<512>" : C == 256 ? "ffn_rows_bwd<256>" : "ffn_rows_bwd<128>",
+           8.0 * Md * Cd * Cd, (Md * Cd * 9 + 4 * Cd * Cd) * 2 + Md * 8 + 3.0 * (Md / FR_BM) * Cd * 4);
+  }
+  return check_launch("ffn_rows_bwd");
 }
 
 }  // extern "C"

@@ -251,12 +251,13 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       const float4 w0 = ld4(p.lnw + gcol), w1 = ld4(p.lnw + gcol + 4);
       const float lw[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float yh[8], sg = 0.f, sgy = 0.f;
+      // the arithmetic of ln_bwd_nhwc (and of nbp_ffn_rows_bwd), contractions spelt out: the same dx bits whichever
+      // kernel runs the LayerNorm backward
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         yh[j] = (xv[j] - st.x) * inv;
-        const float gg = v[j] * lw[j];
-        sg += gg;
-        sgy = fmaf(gg, yh[j], sgy);
+        sg = fmaf(v[j], lw[j], sg);
+        sgy = fmaf(v[j] * lw[j], yh[j], sgy);
         cd[j] = fmaf(v[j], yh[j], cd[j]);  // dlnw partial
         cb[j] += v[j];                      // dlnb partial
       }
@@ -265,7 +266,10 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
       const float mg = sg / (float)N, mgy = sgy / (float)N;
       float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[j] * lw[j] - yh[j] * mgy - mg) * inv + rv[j];
+      for (int j = 0; j < 8; ++j) {
+        o[j] = fmaf(inv, fmaf(-yh[j], mgy, v[j] * lw[j]) - mg, rv[j]);
+        asm volatile("" : "+v"(o[j]));  // rounded to fp32, then to the storage type
+      }
       st8f<TC>(p.C, off, o);
       continue;
     }
@@ -290,19 +294,22 @@ __device__ __forceinline__ void gemm_epilogue(const GemmPB& p, floatx16 (&acc)[B
         ld8f<TC>(p.R, off, ta);
         ld8f<TC>(p.R, off + 8, tb);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 4; ++j) {  // fp32 products, then one rounding each (the SimpleGate convention)
           oa[2 * j] = v[j] * ta[2 * j + 1];
           oa[2 * j + 1] = v[j] * ta[2 * j];
           ob[2 * j] = v[4 + j] * tb[2 * j + 1];
           ob[2 * j + 1] = v[4 + j] * tb[2 * j];
+          asm volatile("" : "+v"(oa[2 * j]), "+v"(oa[2 * j + 1]), "+v"(ob[2 * j]), "+v"(ob[2 * j + 1]));
         }
         st8f<TC>(p.C, off, oa);
         st8f<TC>(p.C, off + 8, ob);
       } else {
         for (int j = 0; j < 8 && gcol + j < N; ++j) {
           const float t0 = ldf<TC>(p.R, off + 2 * j), t1 = ldf<TC>(p.R, off + 2 * j + 1);
-          stf<TC>(p.C, off + 2 * j, v[j] * t1);
-          stf<TC>(p.C, off + 2 * j + 1, v[j] * t0);
+          float q0 = v[j] * t1, q1 = v[j] * t0;
+          asm volatile("" : "+v"(q0), "+v"(q1));
+          stf<TC>(p.C, off + 2 * j, q0);
+          stf<TC>(p.C, off + 2 * j + 1, q1);
         }
       }
       continue;

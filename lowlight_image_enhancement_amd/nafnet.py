@@ -237,14 +237,17 @@ class NAFNet(nn.Module):
         if self._tdesc is None or self._tdesc.device != P.device:
             self._tdesc = self._tdesc_cpu.to(P.device)
             self._fdesc = self._fdesc_cpu.to(P.device) if self._fdesc_cpu.shape[0] else None
+            self._fdesc_t = self._fdesc_cpu[:, [0, 2, 1]].contiguous().to(P.device)  # the transposed copies: [in][out]
         wb = torch.empty(self.numel, dtype=self.adt, device=P.device)
         wt = torch.empty(self.numel, dtype=self.adt, device=P.device)
         call("weights_bf16", P, self.numel, wb, self._tdesc, self._tdesc.shape[0], wt, self.dt)
-        wf = None
-        if self.fuse_ffn_rows and self._fdesc is not None:
+        wf = wtf = None
+        if self.fuse_ffn_rows and self._fdesc is not None:  # fragment-ordered copies (nbp_frag16): forward, transposed
             wf = torch.empty(self.numel, dtype=self.adt, device=P.device)
-            call("weights_frag", P, self._fdesc, self._fdesc.shape[0], wf, self.dt)
-        return wb, wt, wf
+            call("frag16", wb, self._fdesc, self._fdesc.shape[0], wf)
+            wtf = torch.empty(self.numel, dtype=self.adt, device=P.device)
+            call("frag16", wt, self._fdesc_t, self._fdesc_t.shape[0], wtf)
+        return wb, wt, wf, wtf
 
     @property
     def adt(self) -> torch.dtype:
@@ -683,15 +686,14 @@ class NAFNet(nn.Module):
     def _reduce(self, slab, S, L, out):
         call("reduce_slab", slab, S, L, out)
 
-    def _block_bwd(self, P, Wt, dflat, pre, geo, S, dout):
-        B, h, w, c = geo
+    def _ffn_bwd_launches(self, P, Wt, dflat, pre, B, h, w, c, S, dout):
+        """The FFN half's backward as separate launches; returns (dy, dh, SCA channel-dot slab, its chunks per image)."""
         M = B * h * w
         HW = h * w
         dev = dout.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
         dt = self.dt
-        dout = dout.reshape(M, c)
         # out = y + gamma * conv5(g2): no stored pre-activation, no scaled-gradient pass.  dg2 = (gamma (.) dout) W5
         # (gamma as the A-operand column scale); U5 = dout^T g2, V5 = colsum dout feed dW5 = gamma (.) U5,
         # db5 = gamma (.) V5, dgamma = rowsum(W5 (.) U5) + b5 (.) V5 (nbp_layer_scale_grad, after the reductions).
@@ -773,6 +775,59 @@ class NAFNet(nn.Module):
             chunks = query("dw_chunks", B, h, w, c, 0)
             da_slab = F(B * chunks * c)
             call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
+        return dy, dh, da_slab, chunks
+
+    def _ffn_bwd_rows(self, P, Wt, dflat, pre, B, h, w, c, S, dout):
+        """The FFN half's backward in one row-stationary launch (nbp_ffn_rows_bwd: dt4, dy, dh bitwise the launches; the
+        norm2 weight / bias and SCA channel-dot partials per 32-row block), then the weight gradients it feeds queued
+        as in _ffn_bwd_launches."""
+        M = B * h * w
+        HW = h * w
+        dev = dout.device
+        E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
+        F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
+        dt = self.dt
+        nb = M // 32
+        dt4, dy, dh = E(M, 2 * c), E(M, c), E(M, c)
+        sw, sb, da_slab = F(nb * c), F(nb * c), F(nb * c)
+        call("ffn_rows_bwd", dout, S["t4"], S["y"].reshape(M, c), S["st2"], self._slice(P, pre + "norm2.weight"),
+             S["g"], self._slice(Wt[4], pre + "conv5.weight"), self._slice(Wt[4], pre + "conv4.weight"),
+             self._slice(Wt[4], pre + "conv3.weight"), dt4, dy, dh, sw, sb, da_slab, M, c, HW, dt)
+        U5, V5 = F(c * c), F(c)
+        self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
+        call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
+             self._slice(P, pre + "gamma"), self._slice(dflat, pre + "conv5.weight"),
+             self._slice(dflat, pre + "conv5.bias"), self._slice(dflat, pre + "gamma"), c, c)
+        self._wgrad(dt4, 2 * c, AM_PLAIN, S["n2"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
+                    self._slice(dflat, pre + "conv4.weight"), self._slice(dflat, pre + "conv4.bias"))
+        self._reduce(sw, nb, c, self._slice(dflat, pre + "norm2.weight"))
+        self._reduce(sb, nb, c, self._slice(dflat, pre + "norm2.bias"))
+        U3, V3 = F(c * c), F(c)
+        self._wgrad(dy, c, AM_PLAIN, S["g"], c, AM_SCALE, S["a"], HW, M, c, c, 0, 0, 0, 0, U3, V3)
+        call("layer_scale_grad", U3, V3, self._slice(P, pre + "conv3.weight"), self._slice(P, pre + "conv3.bias"),
+             self._slice(P, pre + "beta"), self._slice(dflat, pre + "conv3.weight"),
+             self._slice(dflat, pre + "conv3.bias"), self._slice(dflat, pre + "beta"), c, c)
+        return dy, dh, da_slab, HW // 32
+
+    def _block_bwd(self, P, Wt, dflat, pre, geo, S, dout):
+        B, h, w, c = geo
+        M = B * h * w
+        HW = h * w
+        dev = dout.device
+        E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
+        F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
+        dt = self.dt
+        dout = dout.reshape(M, c)
+        # the FFN half's backward: conv5 dgrad + SimpleGate backward, conv4 dgrad + norm2 backward, conv3 dgrad (+ the SCA
+        # channel-dot partials) and the weight gradients they feed
+        rows = (self.fuse_ffn_rows and dt != 0 and len(Wt) >= 5 and Wt[4] is not None and self.fold_ls
+                and S["t4"] is not None and S["g2"] is not None and query("ffn_rows_supported", M, c, HW, dt) == 1)
+        if rows:
+            dy, dh, da_slab, chunks = self._ffn_bwd_rows(P, Wt, dflat, pre, B, h, w, c, S, dout)
+        else:
+            dy, dh, da_slab, chunks = self._ffn_bwd_launches(P, Wt, dflat, pre, B, h, w, c, S, dout)
+        # LN backward in the conv1 dgrad's epilogue below (dn1 never stored) at these widths
+        fuse_ln = dt != 0 and c in (32, 64, 128, 256)
         # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch
         ds = F(B, c)
         call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,

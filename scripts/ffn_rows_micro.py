@@ -39,5 +39,43 @@ def main():
                   f"({mb:.1f} MB algorithmic -> {mb / min(res['new']):.2f} TB/s)", flush=True)
 
 
+
+
+def main_bwd(iters=20):
+    """the backward chain (nbp_ffn_rows_bwd) against its launches at the same shapes"""
+    from test_gpu_ffn_rows import _bwd_reference, to_frag, DT
+    dev = torch.device("cuda:0")
+    dt = 2
+    Ht = DT[dt]
+    for C, hw in ((128, 4096), (256, 1024), (512, 256)):
+        B = 16
+        M = B * hw
+        g = torch.Generator(device=dev).manual_seed(2)
+        R = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+        y = R(M, C).to(Ht)
+        o = dict(dout=R(M, C).to(Ht), t4=R(M, 2 * C).to(Ht), y=y, st2=torch.rand(M, 2, device=dev) + 0.5,
+                 lnw2=1 + 0.1 * R(C), g=R(M, C).to(Ht), w5t=(R(C, C) / C ** 0.5).to(Ht),
+                 w4t=(R(C, 2 * C) / C ** 0.5).to(Ht), w3t=(R(C, C) / C ** 0.5).to(Ht))
+        f5, f4, f3 = to_frag(o["w5t"]), to_frag(o["w4t"]), to_frag(o["w3t"])
+        nb = M // 32
+        outs = [torch.empty(M, n, device=dev, dtype=Ht) for n in (2 * C, C, C)]
+        slabs = [torch.empty(nb * C, device=dev) for _ in range(3)]
+
+        def old():
+            _bwd_reference(dev, dt, M, C, hw, o)
+
+        def new():
+            call("ffn_rows_bwd", o["dout"], o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], f5, f4, f3, *outs, *slabs, M,
+                 C, hw, dt)
+        res = {"old": [], "new": []}
+        for _ in range(3):
+            res["old"].append(graph_time(old, iters))
+            res["new"].append(graph_time(new, iters))
+        mb = (M * C * 9 + 4 * C * C) * 2 / 1e6
+        print(f"bwd C{C} {hw} px/img B{B}: launches {min(res['old']):.1f} us, fused {min(res['new']):.1f} us "
+              f"({mb:.1f} MB algorithmic -> {mb / min(res['new']):.2f} TB/s)", flush=True)
+
+
 if __name__ == "__main__":
     main()
+    main_bwd()

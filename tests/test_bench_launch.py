@@ -111,6 +111,6 @@ def test_single_kernel_classes_name_one_rocprof_instance():
     assert seen >= 5, path
     # the instance names the library records (nbp_launch_timing) are the keys of bench.INSTANCES
     src = "".join(open(os.path.join(ROOT, "lowlight_image_enhancement_amd", "csrc", f)).read()
-                  for f in ("gemm.hip", "dwconv.hip", "c1dw_tile.hip"))
+                  for f in ("gemm.hip", "dwconv.hip", "c1dw_tile.hip", "ffn_rows.hip"))
     for inst in bench.INSTANCES:
         assert f'"{inst}"' in src, inst

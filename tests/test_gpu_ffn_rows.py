@@ -2,8 +2,8 @@
 next block's norm1, arch_util.py:264-275): every tensor it stores -- y, n2 and its statistics, t4, g2, out and the next
 block's n1 and statistics -- bitwise equal to the launches it replaces (conv3 with the SCA scale + residual and norm2,
 conv4 with the SimpleGate epilogue, conv5 + residual (+ norm1)), at C 128 / 256 / 512 in both 16-bit types and images
-of 256 / 1024 / 4096 rows; and a network whose levels 2 / 3 / middle take it trains
-bitwise like the unfused network."""
+of 256 / 1024 / 4096 rows; and the backward chain (nbp_ffn_rows_bwd) likewise for
+dt4 / dy / dh; a network whose levels 2 / 3 / middle take both trains like the unfused network."""
 import pytest
 import torch
 
@@ -104,24 +104,23 @@ def test_ffn_rows_bitwise_equals_the_launches(dev, dt, C, B, hw, nxt):
 
 
 @pytest.mark.parametrize("dt", [1, 2])
-def test_weights_frag_layout(dev, dt):
-    """nbp_weights_frag: the 16-bit fragment-ordered copies at their flat offsets, bitwise the torch permutation of the
-    rounded rows (the rest of the buffer untouched)."""
+def test_frag16_layout(dev, dt):
+    """nbp_frag16: fragment-ordered copies of 16-bit matrices at their flat offsets, bitwise the torch permutation (the
+    rest of the buffer untouched)."""
     from lowlight_image_enhancement_amd._lib import call
     gen = torch.Generator(device=dev).manual_seed(3)
-    shapes = [(256, 128), (512, 256), (1024, 512), (512, 512)]
+    shapes = [(256, 128), (512, 256), (1024, 512), (512, 512), (256, 512)]
     offs, o = [], 8
     for n, k in shapes:
         offs.append(o)
         o += n * k + 8
-    flat = torch.randn(o, device=dev, generator=gen)
+    src = torch.randn(o, device=dev, generator=gen).to(DT[dt])
     desc = torch.tensor([[of, n, k] for of, (n, k) in zip(offs, shapes)], dtype=torch.int64, device=dev)
     out = torch.full((o,), 7.0, device=dev, dtype=DT[dt])
-    call("weights_frag", flat, desc, len(shapes), out, dt)
+    call("frag16", src, desc, len(shapes), out)
     torch.cuda.synchronize()
     for of, (n, k) in zip(offs, shapes):
-        ref = to_frag(flat[of:of + n * k].view(n, k).to(DT[dt]))
-        assert torch.equal(_bits(out[of:of + n * k]), _bits(ref))
+        assert torch.equal(_bits(out[of:of + n * k]), _bits(to_frag(src[of:of + n * k].view(n, k))))
         assert (out[of - 8:of].float() == 7.0).all()
 
 
@@ -139,10 +138,80 @@ def test_ffn_rows_refusals(dev):
              256, EPS, 2)
 
 
+def _bwd_reference(dev, dt, M, C, hw, o):
+    """the launches the executor issued before (nafnet.py _ffn_bwd_launches): conv5 dgrad CM_SGBWD, conv4 dgrad + norm2
+    backward (nbp_dgrad_ln_bwd at C 128 / 256; nbp_gemm_bf16 + nbp_ln_bwd_nhwc at C 512), conv3 dgrad CM_CHANDOT"""
+    from lowlight_image_enhancement_amd._lib import call, query
+    Ht = DT[dt]
+    E = lambda n: torch.empty(M, n, device=dev, dtype=Ht)  # noqa: E731
+    dt4, dy, dh = E(2 * C), E(C), E(C)
+    dlnw, dlnb = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    call("gemm_bf16", o["dout"], C, AM_PLAIN, None, 1, dt, o["w5t"], C, dt4, 2 * C, CM_SGBWD, dt, M, C, C, 0, 0, 0, None,
+         o["t4"], None, None)
+    if C in (128, 256):
+        n_ws = query("dgrad_ln_workspace_floats", M, C)
+        ws = torch.empty(n_ws, device=dev)
+        call("dgrad_ln_bwd", dt4, 2 * C, o["w4t"], 2 * C, M, C, 2 * C, o["y"], o["st2"], o["lnw2"], o["dout"], dy, dlnw,
+             dlnb, ws, n_ws, dt)
+    else:
+        dn2 = E(C)
+        call("gemm_bf16", dt4, 2 * C, AM_PLAIN, None, 1, dt, o["w4t"], 2 * C, dn2, C, CM_PLAIN, dt, M, C, 2 * C, 0, 0, 0,
+             None, None, None, None)
+        lg = query("ln_nhwc_grid", M, C, dt)
+        sw, sb = torch.empty(lg * C, device=dev), torch.empty(lg * C, device=dev)
+        call("ln_bwd_nhwc", dn2, o["y"], o["st2"], o["lnw2"], o["dout"], dy, sw, sb, M, C, dt)
+        call("reduce_slab", sw, lg, C, dlnw)
+        call("reduce_slab", sb, lg, C, dlnb)
+    B = M // hw
+    da = torch.empty(B * (hw // 64) * C, device=dev)
+    call("gemm_bf16", dy, C, AM_PLAIN, None, hw, dt, o["w3t"], C, dh, C, CM_CHANDOT, dt, M, C, C, 0, 0, 0, None, o["g"],
+         None, da)
+    return dict(dt4=dt4, dy=dy, dh=dh, dlnw=dlnw, dlnb=dlnb, da=da.view(B, hw // 64, C).sum(1))
+
+
+CM_SGBWD, CM_CHANDOT = 5, 8
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("C,B,hw", [(128, 2, 4096), (128, 1, 1024), (256, 2, 1024), (256, 3, 256), (512, 16, 256),
+                                    (512, 1, 1024)])
+def test_ffn_rows_bwd_bitwise_equals_the_launches(dev, dt, C, B, hw):
+    """nbp_ffn_rows_bwd: dt4, dy, dh bitwise the launches it replaces; the norm2 weight / bias gradients and the SCA
+    channel dot (its per-32-row partials summed per image) within fp32 summation order of theirs."""
+    from lowlight_image_enhancement_amd._lib import call
+    Ht = DT[dt]
+    M = B * hw
+    gen = torch.Generator(device=dev).manual_seed(C + B + hw + 7 * dt)
+    R = lambda *s: torch.randn(*s, device=dev, generator=gen)  # noqa: E731
+    y = (R(M, C) * 1.5 + 0.2).to(Ht)
+    yd = y.double()
+    mu = yd.mean(1, keepdim=True)
+    den = ((yd - mu) ** 2).mean(1, keepdim=True).add(1e-6).sqrt()
+    o = dict(dout=R(M, C).to(Ht), t4=R(M, 2 * C).to(Ht), y=y, st2=torch.cat([mu, den], 1).float().contiguous(),
+             lnw2=1 + 0.1 * R(C), g=R(M, C).to(Ht), w5t=(R(C, C) / C ** 0.5).to(Ht), w4t=(R(C, 2 * C) / C ** 0.5).to(Ht),
+             w3t=(R(C, C) / C ** 0.5).to(Ht))
+    ref = _bwd_reference(dev, dt, M, C, hw, o)
+    nan = lambda *s: torch.full(s, float("nan"), device=dev, dtype=Ht)  # noqa: E731
+    nb = M // 32
+    got = dict(dt4=nan(M, 2 * C), dy=nan(M, C), dh=nan(M, C))
+    sw, sb, da = (torch.full((nb * C,), float("nan"), device=dev) for _ in range(3))
+    call("ffn_rows_bwd", o["dout"], o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], to_frag(o["w5t"]), to_frag(o["w4t"]),
+         to_frag(o["w3t"]), got["dt4"], got["dy"], got["dh"], sw, sb, da, M, C, hw, dt)
+    torch.cuda.synchronize()
+    for k in ("dt4", "dy", "dh"):
+        assert torch.equal(_bits(got[k]), _bits(ref[k])), (k, (got[k].float() - ref[k].float()).abs().max().item())
+    for k, v in (("dlnw", sw.view(nb, C).sum(0)), ("dlnb", sb.view(nb, C).sum(0)),
+                 ("da", da.view(B, hw // 32, C).sum(1))):
+        r = ref[k]
+        assert (v - r).abs().max().item() <= 2e-5 * r.abs().max().item() + 1e-6, k
+
+
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-def test_ffn_rows_network_bitwise(dev, precision):
+def test_ffn_rows_network(dev, precision):
     """Width 32, four downs at 128^2: levels 2 (32^2, C 128), 3 (16^2, C 256) and the middle (8^2 = 64 rows, C 512) take
-    the fused launch; outputs and every parameter gradient bitwise those of the unfused network."""
+    the fused launches (forward and backward): the output bitwise that of the unfused network; every parameter gradient
+    within the 16-bit rounding that the partial sums' fp32 order can move (the SCA gradient enters the depthwise
+    backward's 16-bit dt2)."""
     from lowlight_image_enhancement_amd.NewBP_model.newbp_net_arch import create_newbp_net
     torch.manual_seed(9)
     net = create_newbp_net(in_channels=3, width=32, enc_blk_nums=[1, 1, 2, 2], middle_blk_num=2,
@@ -161,4 +230,4 @@ def test_ffn_rows_network_bitwise(dev, precision):
     net.fuse_ffn_rows = True
     (o1, g1), (o0, g0) = res
     assert torch.equal(o1, o0)
-    assert torch.equal(g1, g0)
+    assert (g1 - g0).norm().item() <= 2e-3 * g0.norm().item()
