@@ -47,6 +47,7 @@ struct FfnRowsP {
   float2* nst1;        // [M] out (with lnw1)
   int M, rows_per_img;
   float eps;
+  int rot;             // column-group rotation (colgroup)
 };
 
 constexpr int FR_BM = 32;  // rows per workgroup (one MFMA row tile)
@@ -62,14 +63,24 @@ constexpr int fr_waves() { return C >= 256 ? 8 : 4; }
 
 // the B fragments of this wave's first D k-steps of C_out[32][N] = A[32][K] . B[N][K]^T (this wave's columns: wave *
 // N / NW ..), issued ahead of the GEMM (under the previous phase's epilogue): the K loop starts on landed data
+// The column group of a wave: the wave index, rotated (rot != 0) by the workgroup's index among the workgroups that
+// share its XCD under round-robin placement (blocks b, b + 8, ...; speed only): the 16-32 workgroups of an XCD then pull
+// eight different weight regions into its L2 at once instead of all waiting on the same lines (the weights of a block
+// come from HBM / the Infinity Cache once per step)
+template <int NW>
+__device__ __forceinline__ int colgroup(int rot) {
+  const int wave = threadIdx.x >> 6;
+  return rot ? (wave + (int)(blockIdx.x >> 3)) % NW : wave;
+}
+
 template <typename H, int NW, int K, int N>
 struct RowsB {
   static constexpr int TN = N / (32 * NW), KS = K / 16, D = FR_D;
   vec_t<H, 8> q[D][TN];
   const H* base;  // this lane's fragment of tile 0, k-step 0
-  __device__ __forceinline__ void prefetch(const H* __restrict__ W) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    base = W + ((long)(wave * TN) * KS * 64 + lane) * 8;
+  __device__ __forceinline__ void prefetch(const H* __restrict__ W, int rot) {
+    const int lane = threadIdx.x & 63, cg = colgroup<NW>(rot);
+    base = W + ((long)(cg * TN) * KS * 64 + lane) * 8;
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
@@ -109,12 +120,12 @@ __device__ __forceinline__ void rows_gemm(RowsB<H, NW, K, N>& b, const H* As, fl
 
 // this wave's accumulators of the columns [c0, c0 + PC) into the fp32 staging rows (stride SW floats)
 template <int NW, int N, int PC, int SW>
-__device__ __forceinline__ void stage_acc(const floatx16 (&acc)[N / (32 * NW)], float* Ss, int c0) {
+__device__ __forceinline__ void stage_acc(const floatx16 (&acc)[N / (32 * NW)], float* Ss, int c0, int rot) {
   constexpr int TN = N / (32 * NW);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, cg = colgroup<NW>(rot);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = (wave * TN + j) * 32 + (lane & 31) - c0;
+    const int col = (cg * TN + j) * 32 + (lane & 31) - c0;
     if (col < 0 || col >= PC) continue;  // (wave-uniform: a wave's columns lie in one pass)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -218,7 +229,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
 #pragma unroll
   for (int it = 0; it < NIT; ++it) xres[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.x) + poff[it]);
   RowsB<H, NW, C, C> b3;
-  b3.prefetch(reinterpret_cast<const H*>(p.w3));
+  b3.prefetch(reinterpret_cast<const H*>(p.w3), p.rot);
   __syncthreads();
 
   // ---- conv3 + bias + beta residual -> y; norm2 -> n2 (the next A operand), stats
@@ -226,8 +237,8 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   {
     floatx16 acc[C / (32 * NW)];
     rows_gemm<H, NW, C, C>(b3, As, acc);
-    b4.prefetch(reinterpret_cast<const H*>(p.w4));  // conv4's first k-steps under this epilogue
-    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+    b4.prefetch(reinterpret_cast<const H*>(p.w4), p.rot);  // conv4's first k-steps under this epilogue
+    stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();  // every wave is done with As (conv3's A) and has staged its columns
 #pragma unroll
@@ -267,12 +278,12 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   {
     floatx16 acc[2 * C / (32 * NW)];
     rows_gemm<H, NW, C, 2 * C>(b4, As, acc);
-    b5.prefetch(reinterpret_cast<const H*>(p.w5));  // conv5's first k-steps under this epilogue
+    b5.prefetch(reinterpret_cast<const H*>(p.w5), p.rot);  // conv5's first k-steps under this epilogue
     __syncthreads();  // every wave is done with As (n2): the gates overwrite it
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
       if (pass) __syncthreads();  // pass 0's staging rows are consumed
-      stage_acc<NW, 2 * C, C, SW>(acc, Ss, pass * C);
+      stage_acc<NW, 2 * C, C, SW>(acc, Ss, pass * C, p.rot);
       __syncthreads();
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
@@ -307,7 +318,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   {
     floatx16 acc[C / (32 * NW)];
     rows_gemm<H, NW, C, C>(b5, As, acc);
-    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();
 #pragma unroll
@@ -381,6 +392,7 @@ struct FfnRowsBwdP {
   float* slab_b;       // [M / 32][C] out: sum of dn2
   float* da;           // [M / 32][C] out: sum of dh * g (image-major row blocks: [B][HW / 32][C])
   int M;
+  int rot;             // column-group rotation (colgroup)
 };
 
 // the partials of one 8-column chunk of every row-pass thread, summed over the threads that share the chunk (lanes
@@ -446,7 +458,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     tq[it][1] = *reinterpret_cast<const vec_t<H, 8>*>(t4 + 8);
   }
   RowsB<H, NW, C, C> b5;
-  b5.prefetch(reinterpret_cast<const H*>(p.w5));
+  b5.prefetch(reinterpret_cast<const H*>(p.w5), p.rot);
   __syncthreads();
 
   // ---- dg2 = dout W5'^T; dt4 (SimpleGate backward) -> memory and the next A operand
@@ -454,8 +466,8 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   {
     floatx16 acc[C / (32 * NW)];
     rows_gemm<H, NW, C, C>(b5, Ad, acc);
-    b4.prefetch(reinterpret_cast<const H*>(p.w4));
-    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+    b4.prefetch(reinterpret_cast<const H*>(p.w4), p.rot);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();
   vec_t<H, 8> yq[NIT];
@@ -490,8 +502,8 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   {
     floatx16 acc[C / (32 * NW)];
     rows_gemm<H, NW, 2 * C, C>(b4, At, acc);
-    b3.prefetch(reinterpret_cast<const H*>(p.w3));
-    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+    b3.prefetch(reinterpret_cast<const H*>(p.w3), p.rot);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();
   float aw[8], ab[8];
@@ -542,7 +554,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   {
     floatx16 acc[C / (32 * NW)];
     rows_gemm<H, NW, C, C>(b3, Ad, acc);
-    stage_acc<NW, C, C, SW>(acc, Ss, 0);
+    stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();
   float cd[8];
@@ -568,6 +580,17 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
 }  // namespace nbp
 
 using namespace nbp;
+
+namespace {
+// NBP_FFN_ROT=0: no column-group rotation (A/B)
+int ffn_rot() {
+  static const int v = [] {
+    const char* e = getenv("NBP_FFN_ROT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+}  // namespace
 
 extern "C" {
 
@@ -606,7 +629,8 @@ int nbp_ffn_rows_fwd(const void* g, const float* a, int rows_per_img, const void
   NBP_REQUIRE((al & 15) == 0, "nbp_ffn_rows_fwd: operands must be 16-byte aligned");
   NBP_REQUIRE(((uintptr_t)st2 & 7) == 0 && ((uintptr_t)nst1 & 7) == 0, "nbp_ffn_rows_fwd: statistics 8-byte aligned");
   FfnRowsP p{g, a, x, w3, b3, beta, lnw2, lnb2, w4, b4, w5, b5, gamma, lnw1, lnb1, y, n2,
-             reinterpret_cast<float2*>(st2), t4, g2, out, nn1, reinterpret_cast<float2*>(nst1), M, rows_per_img, eps};
+             reinterpret_cast<float2*>(st2), t4, g2, out, nn1, reinterpret_cast<float2*>(nst1), M, rows_per_img, eps,
+             ffn_rot()};
   const int grid = cdiv(M, FR_BM);
   lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
@@ -638,7 +662,7 @@ int nbp_ffn_rows_bwd(const void* dout, const void* t4, const void* y, const floa
                        (uintptr_t)slab_w | (uintptr_t)slab_b | (uintptr_t)da;
   NBP_REQUIRE((al & 15) == 0 && ((uintptr_t)st2 & 7) == 0, "nbp_ffn_rows_bwd: operands must be 16-byte aligned");
   FfnRowsBwdP p{dout, t4, y, reinterpret_cast<const float2*>(st2), lnw2, g, w5t, w4t, w3t, dt4, dy, dh, slab_w, slab_b,
-                da, M};
+                da, M, ffn_rot()};
   const int grid = cdiv(M, FR_BM);
   lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
