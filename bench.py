@@ -95,7 +95,8 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
              "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad",
              "ffn_rows_fwd<512>": "ffn_rows_512", "ffn_rows_fwd<256>": "ffn_rows_256", "ffn_rows_fwd<128>": "ffn_rows_128",
              "ffn_rows_bwd<512>": "ffn_rows_bwd_512", "ffn_rows_bwd<256>": "ffn_rows_bwd_256",
-             "ffn_rows_bwd<128>": "ffn_rows_bwd_128"}
+             "ffn_rows_bwd<128>": "ffn_rows_bwd_128", "ffn_rows_bwd<512,pre>": "ffn_rows_bwd_pre_512",
+             "ffn_rows_bwd<256,pre>": "ffn_rows_bwd_pre_256", "ffn_rows_bwd<128,pre>": "ffn_rows_bwd_pre_128"}
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
     "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32E(Li\d+E)?E"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64E(Li\d+E)?E"],
@@ -105,8 +106,9 @@ ROCPROF_KERNELS.update({
     "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"],
     "ffn_rows_512": [r"ffn_rows_fwdI{T}Li512EE"], "ffn_rows_256": [r"ffn_rows_fwdI{T}Li256EE"],
     "ffn_rows_128": [r"ffn_rows_fwdI{T}Li128EE"], "ffn_rows": ["ffn_rows_fwd", "ffn_rows_bwd"],
-    "ffn_rows_bwd_512": [r"ffn_rows_bwdI{T}Li512EE"], "ffn_rows_bwd_256": [r"ffn_rows_bwdI{T}Li256EE"],
-    "ffn_rows_bwd_128": [r"ffn_rows_bwdI{T}Li128EE"]})
+    "ffn_rows_bwd_512": [r"ffn_rows_bwdI{T}Li512ELb0EE"], "ffn_rows_bwd_256": [r"ffn_rows_bwdI{T}Li256ELb0EE"],
+    "ffn_rows_bwd_128": [r"ffn_rows_bwdI{T}Li128ELb0EE"], "ffn_rows_bwd_pre_512": [r"ffn_rows_bwdI{T}Li512ELb1EE"],
+    "ffn_rows_bwd_pre_256": [r"ffn_rows_bwdI{T}Li256ELb1EE"], "ffn_rows_bwd_pre_128": [r"ffn_rows_bwdI{T}Li128ELb1EE"]})
 # the Itanium mangling of the storage type in those names
 MANGLED_T = {"fp16": "DF16_", "bf16": "DF16b", "fp32": "f"}
 UNIT_DEF = {
@@ -129,6 +131,11 @@ UNIT_DEF = {
     "ffn_rows_bwd_512": "per pixel: dout C + t4 2C + y C + g C read, dt4 2C + dy C + dh C written = 9 C s bytes, + the "
                         "three weights (4 C^2 s) once per launch and the per-32-row partial sums (the middle level)",
     "ffn_rows_bwd_256": "as ffn_rows_bwd_512 at C 256 (32^2)", "ffn_rows_bwd_128": "as ffn_rows_bwd_512 at C 128 (64^2)",
+    "ffn_rows_bwd_pre_512": "as ffn_rows_bwd_512 (dout made in-kernel, not read), + the following block's conv1 input "
+                            "gradient: dt1 2C + x C + dres C read, dx C written = 14 C s bytes per pixel, + four "
+                            "weights (6 C^2 s) once per launch",
+    "ffn_rows_bwd_pre_256": "as ffn_rows_bwd_pre_512 at C 256 (32^2)",
+    "ffn_rows_bwd_pre_128": "as ffn_rows_bwd_pre_512 at C 128 (64^2)",
 }
 
 
@@ -236,9 +243,11 @@ def cost_ffn_rows(a):  # (g,a,hw,x,w3,b3,beta,lnw2,lnb2,w4,b4,w5,b5,gamma,lnw1,l
     return 8.0 * M * C * C, (M * C * (9 if nxt else 8) + 4 * C * C) * 2 + M * 8 * (2 if nxt else 1)
 
 
-def cost_ffn_rows_bwd(a):  # (dout,t4,y,st2,lnw2,g,w5t,w4t,w3t,dt4,dy,dh,sw,sb,da,M,C,hw,dt)
-    M, C = a[15], a[16]
-    return 8.0 * M * C * C, (M * C * 9 + 4 * C * C) * 2 + M * 8 + 3 * (M // 32) * C * 4
+def cost_ffn_rows_bwd(a):  # (dout,t4,y,st2,lnw2,g,w5t,w4t,w3t,dt4,dy,dh,sw,sb,da,dt1,w1t,x1,st1,lnw1,dres1,dx1,sw1,sb1,M,C,hw,dt)
+    M, C = a[24], a[25]
+    pre = a[15] is not None  # + the following block's conv1 input gradient / norm1 backward
+    return (8.0 + 4.0 * pre) * M * C * C, ((M * C * (14 if pre else 9) + (6 if pre else 4) * C * C) * 2
+                                           + M * 8 * (2 if pre else 1) + (5 if pre else 3) * (M // 32) * C * 4)
 
 
 def cost_gemm_f32(a):  # (A,lda,amode,ascale,rows,B,ldb,bnk,C,ldc,cmode,M,N,K,gh,gw,cs,bias,R,rscale,pre)

@@ -172,10 +172,16 @@ int nbp_frag16(const void* src, const long* desc, int ndesc, void* out, nbp_stre
  * block b, slab_w[b] = sum dn2 * yhat, slab_b[b] = sum dn2 (norm2's weight / bias gradient partials) and da[b] = sum dh
  * (.) g (the SCA channel-dot partials, [B][rows_per_img / 32][C]).  Replaces nbp_gemm_bf16 CM_SGBWD + nbp_dgrad_ln_bwd
  * (or nbp_gemm_bf16 + nbp_ln_bwd_nhwc at C 512) + nbp_gemm_bf16 CM_CHANDOT: dt4 / dy / dh bitwise theirs, the partial
- * sums up to fp32 summation order.  Shapes as nbp_ffn_rows_supported. */
+ * sums up to fp32 summation order.  With dt1 (dout null): first the FOLLOWING block's conv1 input gradient + norm1 backward
+ * (the executor's pending one; both blocks of one level, NAFNet_arch.py:60-63 backward): dx1 = LayerNorm2d backward(dt1
+ * W1^T; x1, st1, lnw1) + dres1 (that block's dy), stored and taken as this block's dout, with norm1's partials per 32-row
+ * block in slab_w1 / slab_b1 (w1t: fragment-ordered W1^T [C][2C]; dx1 bitwise nbp_dgrad_ln_bwd / nbp_gemm_bf16 +
+ * nbp_ln_bwd_nhwc).  Shapes as nbp_ffn_rows_supported. */
 int nbp_ffn_rows_bwd(const void* dout, const void* t4, const void* y, const float* st2, const float* lnw2, const void* g,
                      const void* w5t, const void* w4t, const void* w3t, void* dt4, void* dy, void* dh, float* slab_w,
-                     float* slab_b, float* da, int M, int C, int rows_per_img, int dtype, nbp_stream_t s);
+                     float* slab_b, float* da, const void* dt1, const void* w1t, const void* x1, const float* st1,
+                     const float* lnw1, const void* dres1, void* dx1, float* slab_w1, float* slab_b1, int M, int C,
+                     int rows_per_img, int dtype, nbp_stream_t s);
 int nbp_ffn_rows_fwd(const void* g, const float* a, int rows_per_img, const void* x, const void* w3, const float* b3,
                      const float* beta, const float* lnw2, const float* lnb2, const void* w4, const float* b4,
                      const void* w5, const float* b5, const float* gamma, const float* lnw1, const float* lnb1, void* y,

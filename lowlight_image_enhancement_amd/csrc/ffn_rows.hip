@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void frag16_kernel(const uint16_t* __restrict_
 // nbp_gemm_bf16 + nbp_ln_bwd_nhwc on the rounded dn2 at C 512; nbp_gemm_bf16 CM_CHANDOT); the partial sums are per
 // 32-row block in an order of their own.
 struct FfnRowsBwdP {
-  const void* dout;    // [M][C]
+  const void* dout;    // [M][C] (null with PRE: produced in-kernel as dx1)
   const void* t4;      // [M][2C] (forward tape, pairs interleaved)
   const void* y;       // [M][C] norm2 input
   const float2* st2;   // [M] (mu, den)
@@ -391,6 +391,16 @@ struct FfnRowsBwdP {
   float* slab_w;       // [M / 32][C] out: sum over the block's rows of dn2 * yhat
   float* slab_b;       // [M / 32][C] out: sum of dn2
   float* da;           // [M / 32][C] out: sum of dh * g (image-major row blocks: [B][HW / 32][C])
+  // PRE: the FOLLOWING block's (in forward order) conv1 input gradient + norm1 backward first, its dx = this block's dout
+  const void* dt1;     // [M][2C] that block's conv1 output gradient
+  const void* w1;      // fragment-ordered 16-bit W1^T [C][2C]
+  const void* x1;      // [M][C] that block's input (norm1's input)
+  const float2* st1;   // [M]
+  const float* lnw1;
+  const void* dres1;   // [M][C] that block's dy (the residual branch)
+  void* dx1;           // [M][C] out (= dout)
+  float* slab_w1;      // [M / 32][C] out: norm1's partials
+  float* slab_b1;
   int M;
   int rot;             // column-group rotation (colgroup)
 };
@@ -418,7 +428,53 @@ __device__ __forceinline__ void chunk_partials_out(float (&v)[8], float* red, fl
   __syncthreads();
 }
 
-template <typename H, int C>
+// The LayerNorm2d backward of the staged fp32 input gradients dn (rows of the row pass), ln_bwd_nhwc's arithmetic with
+// its contractions spelt out (as the CM_LNBWD epilogue): dx = (dn w - yhat mean(dn w yhat) - mean(dn w)) / den + dres,
+// rounded once; dx into the A buffer (slot of each chunk) and memory; the weight / bias partials into aw / ab.  RND: dn
+// rounded to the storage type first (the two-launch form at C 512 stores it).
+template <typename H, int C, int NIT, bool RND, typename Slot>
+__device__ __forceinline__ void ln_bwd_rows(const float* Ss, const float* lnw, const vec_t<H, 8> (&xq)[NIT],
+                                            const float2 (&stq)[NIT], const vec_t<H, 8> (&rq)[NIT], const int* prow,
+                                            const int* pc, const bool* pok, const long* poff, Slot slot, void* gout,
+                                            float (&aw)[8], float (&ab)[8]) {
+  constexpr int NCH = C / 8, SW = C;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) aw[j] = ab[j] = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = prow[it], c8 = 8 * pc[it];
+    float d[8], w[8], yh[8];
+    ld8(Ss + row * SW + c8, d);
+    if constexpr (RND) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = (float)(H)d[j];
+    }
+    ld8(lnw + c8, w);
+    const float2 st = pok[it] ? stq[it] : make_float2(0.f, 1.f);
+    const float rinv = 1.f / st.y;
+    float sg = 0.f, sgy = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!pok[it]) d[j] = 0.f;
+      yh[j] = pok[it] ? ((float)xq[it][j] - st.x) * rinv : 0.f;
+      sg = fmaf(d[j], w[j], sg);
+      sgy = fmaf(d[j] * w[j], yh[j], sgy);
+      aw[j] = fmaf(d[j], yh[j], aw[j]);
+      ab[j] += d[j];
+    }
+    sg = group_sum<NCH>(sg);
+    sgy = group_sum<NCH>(sgy);
+    const float mg = sg / (float)C, mgy = sgy / (float)C;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(rinv, fmaf(-yh[j], mgy, d[j] * w[j]) - mg, (float)rq[it][j]);
+    const vec_t<H, 8> oh = rnd8<H>(o);
+    *reinterpret_cast<vec_t<H, 8>*>(slot(row, pc[it])) = oh;
+    if (pok[it]) *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(gout) + poff[it]) = oh;
+  }
+}
+
+template <typename H, int C, bool PRE>
 __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p) {
   constexpr int NW = fr_waves<C>(), NT = 64 * NW, BM = FR_BM;
   constexpr int NCH = C / 8, SW = C;
@@ -427,13 +483,14 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   constexpr int A1 = BM * C * 2, A2 = BM * 2 * C * 2, SS = BM * SW * 4;
   static_assert(A1 + A2 + SS <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) unsigned char smem[A1 + A2 + SS];
-  H* Ad = reinterpret_cast<H*>(smem);             // dout rows, then dy (in place)
-  H* At = reinterpret_cast<H*>(smem + A1);        // dt4 rows (2C)
+  H* Ad = reinterpret_cast<H*>(smem);             // dout rows (read, or made here with PRE), then dy (in place)
+  H* At = reinterpret_cast<H*>(smem + A1);        // (PRE: dt1 rows), dt4 rows (2C)
   float* Ss = reinterpret_cast<float*>(smem + A1 + A2);
   const int tid = threadIdx.x;
   const int m0 = blockIdx.x * BM, M = p.M;
   const long blk = blockIdx.x;
   auto slot = [&](H* base, int K, int row, int c) { return base + row * K + 8 * (c ^ (row & 15)); };
+  auto dslot = [&](int row, int c) { return slot(Ad, C, row, c); };
 
   int prow[NIT], pc[NIT];
   long poff[NIT];
@@ -446,13 +503,50 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     pok[it] = m0 + prow[it] < M;
     poff[it] = (long)(pok[it] ? m0 + prow[it] : M - 1) * C + 8 * pc[it];
   }
-  // ---- dout rows -> LDS; the SimpleGate inputs of the first epilogue loaded under the first K loop
+  if constexpr (PRE) {
+    // ---- the following block's dx = norm1 backward(dt1 W1^T) + its dy: this block's dout, made in LDS
+    RowsB<H, NW, 2 * C, C> b1;
+    b1.prefetch(reinterpret_cast<const H*>(p.w1), p.rot);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {  // dt1 rows (2C: chunks 2c, 2c + 1 of the thread's chunk c)
+      const H* d1 = reinterpret_cast<const H*>(p.dt1) + 2 * poff[it];
+      vec_t<H, 8> lo = *reinterpret_cast<const vec_t<H, 8>*>(d1), hi = *reinterpret_cast<const vec_t<H, 8>*>(d1 + 8);
+      if (!pok[it]) lo = hi = vec_t<H, 8>{};
+      *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, prow[it], 2 * pc[it])) = lo;
+      *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, prow[it], 2 * pc[it] + 1)) = hi;
+    }
+    __syncthreads();
+    {
+      floatx16 acc[C / (32 * NW)];
+      int off = 0;  // opaque: the conv4 K loop below reads the same rows, and its A addresses, shared, spill at C 512
+      asm volatile("" : "+s"(off));
+      rows_gemm<H, NW, 2 * C, C>(b1, At + off, acc);
+      stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
+    }
+    vec_t<H, 8> xq[NIT], rq[NIT];  // the norm1 operands after the K loop (live across it they spill at C 512)
+    float2 stq[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      xq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.x1) + poff[it]);
+      rq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.dres1) + poff[it]);
+      stq[it] = p.st1[pok[it] ? m0 + prow[it] : M - 1];
+    }
+    __syncthreads();
+    float aw[8], ab[8];
+    ln_bwd_rows<H, C, NIT, C == 512>(Ss, p.lnw1, xq, stq, rq, prow, pc, pok, poff, dslot, p.dx1, aw, ab);
+    __syncthreads();
+    chunk_partials_out<C, NW>(aw, Ss, p.slab_w1 + blk * C);
+    chunk_partials_out<C, NW>(ab, Ss, p.slab_b1 + blk * C);
+  }
+  // ---- dout rows -> LDS (PRE: made above); the SimpleGate inputs of the first epilogue loaded under the first K loop
   vec_t<H, 8> tq[NIT][2];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    vec_t<H, 8> d = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.dout) + poff[it]);
-    if (!pok[it]) d = vec_t<H, 8>{};
-    *reinterpret_cast<vec_t<H, 8>*>(slot(Ad, C, prow[it], pc[it])) = d;
+    if constexpr (!PRE) {
+      vec_t<H, 8> d = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.dout) + poff[it]);
+      if (!pok[it]) d = vec_t<H, 8>{};
+      *reinterpret_cast<vec_t<H, 8>*>(dslot(prow[it], pc[it])) = d;
+    }
     const H* t4 = reinterpret_cast<const H*>(p.t4) + 2 * poff[it];
     tq[it][0] = *reinterpret_cast<const vec_t<H, 8>*>(t4);
     tq[it][1] = *reinterpret_cast<const vec_t<H, 8>*>(t4 + 8);
@@ -470,7 +564,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();
-  vec_t<H, 8> yq[NIT];
+  vec_t<H, 8> yq[NIT], rq2[NIT];
   float2 stq[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -494,6 +588,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     }
     yq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.y) + poff[it]);  // for the LN backward
     stq[it] = p.st2[pok[it] ? m0 + row : M - 1];
+    rq2[it] = *reinterpret_cast<const vec_t<H, 8>*>(dslot(row, pc[it]));  // dout: the residual branch
   }
   __syncthreads();
 
@@ -507,42 +602,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   }
   __syncthreads();
   float aw[8], ab[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) aw[j] = ab[j] = 0.f;
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int row = prow[it], c8 = 8 * pc[it];
-    float d[8], w[8], rr[8], yh[8];
-    ld8(Ss + row * SW + c8, d);
-    if constexpr (C == 512) {  // the two-launch form at this level stores dn2 in the storage type first
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = (float)(H)d[j];
-    }
-    ld8(p.lnw2 + c8, w);
-    const vec_t<H, 8> dres = *reinterpret_cast<const vec_t<H, 8>*>(slot(Ad, C, row, pc[it]));
-    const float2 st = pok[it] ? stq[it] : make_float2(0.f, 1.f);
-    const float rinv = 1.f / st.y;
-    float sg = 0.f, sgy = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (!pok[it]) d[j] = 0.f;
-      yh[j] = pok[it] ? ((float)yq[it][j] - st.x) * rinv : 0.f;
-      rr[j] = (float)dres[j];
-      sg = fmaf(d[j], w[j], sg);
-      sgy = fmaf(d[j] * w[j], yh[j], sgy);
-      aw[j] = fmaf(d[j], yh[j], aw[j]);
-      ab[j] += d[j];
-    }
-    sg = group_sum<NCH>(sg);
-    sgy = group_sum<NCH>(sgy);
-    const float mg = sg / (float)C, mgy = sgy / (float)C;
-    float o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = fmaf(rinv, fmaf(-yh[j], mgy, d[j] * w[j]) - mg, rr[j]);
-    const vec_t<H, 8> dyh = rnd8<H>(o);
-    *reinterpret_cast<vec_t<H, 8>*>(slot(Ad, C, row, pc[it])) = dyh;
-    if (pok[it]) *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.dy) + poff[it]) = dyh;
-  }
+  ln_bwd_rows<H, C, NIT, C == 512>(Ss, p.lnw2, yq, stq, rq2, prow, pc, pok, poff, dslot, p.dy, aw, ab);
   __syncthreads();  // dy complete in LDS; the staging rows are free: the norm2 partials through them
   chunk_partials_out<C, NW>(aw, Ss, p.slab_w + blk * C);
   chunk_partials_out<C, NW>(ab, Ss, p.slab_b + blk * C);
@@ -553,7 +613,9 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   // ---- dh = dy W3'^T -> memory; the SCA channel-dot partials sum_rows dh g
   {
     floatx16 acc[C / (32 * NW)];
-    rows_gemm<H, NW, C, C>(b3, Ad, acc);
+    int off = 0;  // opaque: the A addresses of the conv5 K loop (same rows) are not kept live to here
+    asm volatile("" : "+s"(off));
+    rows_gemm<H, NW, C, C>(b3, Ad + off, acc);
     stage_acc<NW, C, C, SW>(acc, Ss, 0, p.rot);
   }
   __syncthreads();
@@ -652,28 +714,45 @@ extern "C" {
 
 int nbp_ffn_rows_bwd(const void* dout, const void* t4, const void* y, const float* st2, const float* lnw2, const void* g,
                      const void* w5t, const void* w4t, const void* w3t, void* dt4, void* dy, void* dh, float* slab_w,
-                     float* slab_b, float* da, int M, int C, int rows_per_img, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(dout && t4 && y && st2 && lnw2 && g && w5t && w4t && w3t && dt4 && dy && dh && slab_w && slab_b && da,
+                     float* slab_b, float* da, const void* dt1, const void* w1t, const void* x1, const float* st1,
+                     const float* lnw1, const void* dres1, void* dx1, float* slab_w1, float* slab_b1, int M, int C,
+                     int rows_per_img, int dtype, nbp_stream_t s) {
+  const bool pre = dt1 != nullptr;
+  NBP_REQUIRE(t4 && y && st2 && lnw2 && g && w5t && w4t && w3t && dt4 && dy && dh && slab_w && slab_b && da &&
+                  (pre ? (w1t && x1 && st1 && lnw1 && dres1 && dx1 && slab_w1 && slab_b1) : dout != nullptr),
               "nbp_ffn_rows_bwd: null pointer");
   NBP_REQUIRE(nbp_ffn_rows_supported(M, C, rows_per_img, dtype),
               "nbp_ffn_rows_bwd: unsupported shape (M %d C %d rows_per_img %d dtype %d)", M, C, rows_per_img, dtype);
-  const uintptr_t al = (uintptr_t)dout | (uintptr_t)t4 | (uintptr_t)y | (uintptr_t)lnw2 | (uintptr_t)g | (uintptr_t)w5t |
-                       (uintptr_t)w4t | (uintptr_t)w3t | (uintptr_t)dt4 | (uintptr_t)dy | (uintptr_t)dh |
-                       (uintptr_t)slab_w | (uintptr_t)slab_b | (uintptr_t)da;
-  NBP_REQUIRE((al & 15) == 0 && ((uintptr_t)st2 & 7) == 0, "nbp_ffn_rows_bwd: operands must be 16-byte aligned");
+  uintptr_t al = (uintptr_t)t4 | (uintptr_t)y | (uintptr_t)lnw2 | (uintptr_t)g | (uintptr_t)w5t | (uintptr_t)w4t |
+                 (uintptr_t)w3t | (uintptr_t)dt4 | (uintptr_t)dy | (uintptr_t)dh | (uintptr_t)slab_w | (uintptr_t)slab_b |
+                 (uintptr_t)da;
+  al |= pre ? (uintptr_t)dt1 | (uintptr_t)w1t | (uintptr_t)x1 | (uintptr_t)lnw1 | (uintptr_t)dres1 | (uintptr_t)dx1 |
+                  (uintptr_t)slab_w1 | (uintptr_t)slab_b1
+            : (uintptr_t)dout;
+  NBP_REQUIRE((al & 15) == 0 && ((uintptr_t)st2 & 7) == 0 && ((uintptr_t)st1 & 7) == 0,
+              "nbp_ffn_rows_bwd: operands must be 16-byte aligned");
   FfnRowsBwdP p{dout, t4, y, reinterpret_cast<const float2*>(st2), lnw2, g, w5t, w4t, w3t, dt4, dy, dh, slab_w, slab_b,
-                da, M, ffn_rot()};
+                da, dt1, w1t, x1, reinterpret_cast<const float2*>(st1), lnw1, dres1, dx1, slab_w1, slab_b1, M, ffn_rot()};
   const int grid = cdiv(M, FR_BM);
   lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
-    if (C == 128) ffn_rows_bwd<H, 128><<<grid, 64 * fr_waves<128>(), 0, S(s)>>>(p);
-    else if (C == 256) ffn_rows_bwd<H, 256><<<grid, 64 * fr_waves<256>(), 0, S(s)>>>(p);
-    else ffn_rows_bwd<H, 512><<<grid, 64 * fr_waves<512>(), 0, S(s)>>>(p);
+    if (C == 128 && pre) ffn_rows_bwd<H, 128, true><<<grid, 64 * fr_waves<128>(), 0, S(s)>>>(p);
+    else if (C == 128) ffn_rows_bwd<H, 128, false><<<grid, 64 * fr_waves<128>(), 0, S(s)>>>(p);
+    else if (C == 256 && pre) ffn_rows_bwd<H, 256, true><<<grid, 64 * fr_waves<256>(), 0, S(s)>>>(p);
+    else if (C == 256) ffn_rows_bwd<H, 256, false><<<grid, 64 * fr_waves<256>(), 0, S(s)>>>(p);
+    else if (pre) ffn_rows_bwd<H, 512, true><<<grid, 64 * fr_waves<512>(), 0, S(s)>>>(p);
+    else ffn_rows_bwd<H, 512, false><<<grid, 64 * fr_waves<512>(), 0, S(s)>>>(p);
   });
-  {  // per-launch record: dout, t4 (2C), y, g in; dt4 (2C), dy, dh out; the three weights once
+  {  // per-launch record: dout, t4 (2C), y, g in; dt4 (2C), dy, dh out; the three weights once (PRE: + dt1 2C, x, dy
+     // in, dx out, W1)
     const double Md = M, Cd = C;
-    lt_end(S(s), C == 512 ? "ffn_rows_bwd<512>" : C == 256 ? "ffn_rows_bwd<256>" : "ffn_rows_bwd<128>",
-           8.0 * Md * Cd * Cd, (Md * Cd * 9 + 4 * Cd * Cd) * 2 + Md * 8 + 3.0 * (Md / FR_BM) * Cd * 4);
+    const char* nm = C == 512 ? (pre ? "ffn_rows_bwd<512,pre>" : "ffn_rows_bwd<512>")
+                     : C == 256 ? (pre ? "ffn_rows_bwd<256,pre>" : "ffn_rows_bwd<256>")
+                                : (pre ? "ffn_rows_bwd<128,pre>" : "ffn_rows_bwd<128>");
+    const double fl = 8.0 * Md * Cd * Cd + (pre ? 4.0 * Md * Cd * Cd : 0.0);
+    const double by = (Md * Cd * (pre ? 14 : 9) + (pre ? 6 : 4) * Cd * Cd) * 2 + Md * 8 * (pre ? 2 : 1) +
+                      (pre ? 5.0 : 3.0) * (Md / FR_BM) * Cd * 4;
+    lt_end(S(s), nm, fl, by);
   }
   return check_launch("ffn_rows_bwd");
 }

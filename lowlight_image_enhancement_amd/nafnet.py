@@ -119,6 +119,9 @@ class NAFNet(nn.Module):
         # levels with C in {128, 256, 512} (16-bit): conv3 -> norm2 -> conv4 -> SimpleGate -> conv5 (-> the next norm1)
         # in one row-stationary launch (nbp_ffn_rows_fwd; bitwise the launches it replaces)
         self.fuse_ffn_rows = True
+        # backward at those levels: a block's conv1 input gradient + norm1 backward deferred into the preceding block's
+        # row-stationary launch (nbp_ffn_rows_bwd with dt1: its dx made in LDS as that block's dout; NBP_FFN_PRE=0 off)
+        self.ffn_rows_pre = __import__("os").environ.get("NBP_FFN_PRE", "1") != "0"
         # level 0: conv1's weight / bias gradients folded into the conv1 dgrad + norm1 backward pass (nbp_dgrad_ln_bwd_wg:
         # n1 rebuilt from x and the LN statistics, dt1 already in registers; False: a separate nbp_wgrad_f32 launch)
         self.ln_wg = True
@@ -154,11 +157,11 @@ class NAFNet(nn.Module):
                                         for k, e in self.entries.items() if self._is_gemm_weight(k)],
                                        dtype=torch.int64).reshape(-1, 4)
         self._tdesc = None
-        # the weights nbp_ffn_rows_fwd reads (conv3 / conv4 / conv5 of the levels with C in {128, 256, 512}), {offset,
-        # rows, cols}
+        # the weights nbp_ffn_rows_fwd / _bwd read (conv3 / conv4 / conv5, and conv1 for the backward's deferred input
+        # gradient, of the levels with C in {128, 256, 512}), {offset, rows, cols}
         self._fdesc_cpu = torch.tensor([[e.offset, e.ref_shape[0], e.numel // e.ref_shape[0]]
                                         for k, e in self.entries.items()
-                                        if k.endswith(("conv3.weight", "conv4.weight", "conv5.weight"))
+                                        if k.endswith(("conv1.weight", "conv3.weight", "conv4.weight", "conv5.weight"))
                                         and e.numel // e.ref_shape[0] in (128, 256, 512)],
                                        dtype=torch.int64).reshape(-1, 3)
         self._fdesc = None
@@ -590,10 +593,12 @@ class NAFNet(nn.Module):
         dx_img = None
         level: Optional[List[str]] = None  # stages of the current grouped level, completed when it closes
         level_c = 0
-        for rec in reversed(tape):
+        pend = None  # a block's deferred conv1 input gradient + norm1 backward (taken by the preceding block)
+        recs = [r for r in reversed(tape) if r[0] != "weights"]
+        for idx, rec in enumerate(recs):
             kind = rec[0]
-            if kind == "weights":
-                continue
+            if pend is not None and kind != "block":  # not expected (deferral looks ahead to a block): resolve it
+                dfeat, pend = self._conv1_bwd(P, Wt, dflat, **pend), None
             grouped = kind == "block" and self._level_grouped(rec[2][3])
             if level is not None and not (grouped and rec[2][3] == level_c):
                 self._close_level(level, hook)
@@ -612,7 +617,12 @@ class NAFNet(nn.Module):
                 self._stage_done("ending", hook)
             elif kind == "block":
                 pre, geo, S = rec[1], rec[2], rec[3]
-                dfeat = self._block_bwd(P, Wt, dflat, pre, geo, S, dfeat)
+                # defer into the preceding block of the same (grouped) level when that one takes the row-stationary
+                # backward: the norm1 gradients of this block then land before the level closes
+                nxt = recs[idx + 1] if idx + 1 < len(recs) else None
+                defer = (self.ffn_rows_pre and level is not None and nxt is not None and nxt[0] == "block"
+                         and tuple(nxt[2]) == tuple(geo) and self._rows_ok(Wt, nxt[3], geo))
+                dfeat, pend = self._block_bwd(P, Wt, dflat, pre, geo, S, dfeat, pend, defer)
                 if level is not None:
                     level.append(pre[:-1])
                 else:
@@ -777,22 +787,42 @@ class NAFNet(nn.Module):
             call("img_chan_dot", dh, S["g"], da_slab, B, h, w, c, dt)
         return dy, dh, da_slab, chunks
 
-    def _ffn_bwd_rows(self, P, Wt, dflat, pre, B, h, w, c, S, dout):
+    def _rows_ok(self, Wt, S, geo) -> bool:
+        """Whether a block's FFN backward takes the row-stationary launch (nbp_ffn_rows_bwd)."""
+        B, h, w, c = geo
+        return (self.fuse_ffn_rows and self.dt != 0 and len(Wt) >= 5 and Wt[4] is not None and self.fold_ls
+                and S["t4"] is not None and S["g2"] is not None
+                and query("ffn_rows_supported", B * h * w, c, h * w, self.dt) == 1)
+
+    def _ffn_bwd_rows(self, P, Wt, dflat, pre, B, h, w, c, S, dout, pend=None):
         """The FFN half's backward in one row-stationary launch (nbp_ffn_rows_bwd: dt4, dy, dh bitwise the launches; the
         norm2 weight / bias and SCA channel-dot partials per 32-row block), then the weight gradients it feeds queued
-        as in _ffn_bwd_launches."""
+        as in _ffn_bwd_launches.  With pend (the following block's deferred conv1 input gradient, dout None) the launch
+        first makes that block's dx = this block's dout (bitwise _conv1_bwd), its norm1 partials reduced here.  Returns
+        (dy, dh, SCA slab, chunks per image, dout)."""
         M = B * h * w
         HW = h * w
-        dev = dout.device
+        dev = (dout if dout is not None else pend["dt1"]).device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
         dt = self.dt
         nb = M // 32
         dt4, dy, dh = E(M, 2 * c), E(M, c), E(M, c)
         sw, sb, da_slab = F(nb * c), F(nb * c), F(nb * c)
-        call("ffn_rows_bwd", dout, S["t4"], S["y"].reshape(M, c), S["st2"], self._slice(P, pre + "norm2.weight"),
-             S["g"], self._slice(Wt[4], pre + "conv5.weight"), self._slice(Wt[4], pre + "conv4.weight"),
-             self._slice(Wt[4], pre + "conv3.weight"), dt4, dy, dh, sw, sb, da_slab, M, c, HW, dt)
+        pre_args = (None,) * 9
+        if pend is not None:
+            q = pend["pre"]
+            dout = E(M, c)
+            sw1, sb1 = F(nb * c), F(nb * c)
+            pre_args = (pend["dt1"], self._slice(Wt[4], q + "conv1.weight"), pend["x"], pend["st1"],
+                        self._slice(P, q + "norm1.weight"), pend["dy"], dout, sw1, sb1)
+        call("ffn_rows_bwd", None if pend is not None else dout, S["t4"], S["y"].reshape(M, c), S["st2"],
+             self._slice(P, pre + "norm2.weight"), S["g"], self._slice(Wt[4], pre + "conv5.weight"),
+             self._slice(Wt[4], pre + "conv4.weight"), self._slice(Wt[4], pre + "conv3.weight"), dt4, dy, dh, sw, sb,
+             da_slab, *pre_args, M, c, HW, dt)
+        if pend is not None:
+            self._reduce(sw1, nb, c, self._slice(dflat, pend["pre"] + "norm1.weight"))
+            self._reduce(sb1, nb, c, self._slice(dflat, pend["pre"] + "norm1.bias"))
         U5, V5 = F(c * c), F(c)
         self._wgrad(dout, c, AM_PLAIN, S["g2"], c, AM_PLAIN, None, 1, M, c, c, 0, 0, 0, 0, U5, V5)
         call("layer_scale_grad", U5, V5, self._slice(P, pre + "conv5.weight"), self._slice(P, pre + "conv5.bias"),
@@ -807,27 +837,30 @@ class NAFNet(nn.Module):
         call("layer_scale_grad", U3, V3, self._slice(P, pre + "conv3.weight"), self._slice(P, pre + "conv3.bias"),
              self._slice(P, pre + "beta"), self._slice(dflat, pre + "conv3.weight"),
              self._slice(dflat, pre + "conv3.bias"), self._slice(dflat, pre + "beta"), c, c)
-        return dy, dh, da_slab, HW // 32
+        return dy, dh, da_slab, HW // 32, dout
 
-    def _block_bwd(self, P, Wt, dflat, pre, geo, S, dout):
+    def _block_bwd(self, P, Wt, dflat, pre, geo, S, dout, pend=None, defer=False):
+        """One block's backward.  dout None: the following block's conv1 input gradient is pending (pend) and made by
+        this block's row-stationary launch.  defer: this block's own conv1 input gradient + norm1 backward is left
+        pending for the preceding block.  Returns (dx or None, pending or None)."""
         B, h, w, c = geo
         M = B * h * w
         HW = h * w
+        dt = self.dt
+        # the FFN half's backward: conv5 dgrad + SimpleGate backward, conv4 dgrad + norm2 backward, conv3 dgrad (+ the SCA
+        # channel-dot partials) and the weight gradients they feed
+        rows = self._rows_ok(Wt, S, geo)
+        if pend is not None and not rows:  # not expected (the walker's look-ahead uses the same test): resolve it here
+            dout, pend = self._conv1_bwd(P, Wt, dflat, **pend), None
+        if rows:
+            dy, dh, da_slab, chunks, dout = self._ffn_bwd_rows(P, Wt, dflat, pre, B, h, w, c, S,
+                                                               None if pend is not None else dout.reshape(M, c), pend)
+        else:
+            dout = dout.reshape(M, c)
+            dy, dh, da_slab, chunks = self._ffn_bwd_launches(P, Wt, dflat, pre, B, h, w, c, S, dout)
         dev = dout.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
-        dt = self.dt
-        dout = dout.reshape(M, c)
-        # the FFN half's backward: conv5 dgrad + SimpleGate backward, conv4 dgrad + norm2 backward, conv3 dgrad (+ the SCA
-        # channel-dot partials) and the weight gradients they feed
-        rows = (self.fuse_ffn_rows and dt != 0 and len(Wt) >= 5 and Wt[4] is not None and self.fold_ls
-                and S["t4"] is not None and S["g2"] is not None and query("ffn_rows_supported", M, c, HW, dt) == 1)
-        if rows:
-            dy, dh, da_slab, chunks = self._ffn_bwd_rows(P, Wt, dflat, pre, B, h, w, c, S, dout)
-        else:
-            dy, dh, da_slab, chunks = self._ffn_bwd_launches(P, Wt, dflat, pre, B, h, w, c, S, dout)
-        # LN backward in the conv1 dgrad's epilogue below (dn1 never stored) at these widths
-        fuse_ln = dt != 0 and c in (32, 64, 128, 256)
         # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch
         ds = F(B, c)
         call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,
@@ -851,28 +884,38 @@ class NAFNet(nn.Module):
             call("sca_sg_bwd", dh, S["a"], ds, S["t2"], dt2, M, c, HW, dt)
             call("dw_bwd", dt2, *dw_args)
         # conv1 input gradient + norm1 backward + residual
-        dx = E(M, c)
-        if fuse_ln and c == 32 and self.ln_wg:  # + conv1's dW / db from the same tiles (n1 rebuilt from x / stats)
+        if dt != 0 and c == 32 and self.ln_wg:  # + conv1's dW / db from the same tiles (n1 rebuilt from x / stats)
+            dx = E(M, c)
             n_ws = query("dgrad_ln_bwd_wg_workspace_floats", M, c)
             call("dgrad_ln_bwd_wg", dt1, 2 * c, self._slice(Wt[2], pre + "conv1.weight"), 2 * c, M, c, 2 * c,
                  S["x"].reshape(M, c), S["st1"], self._slice(P, pre + "norm1.weight"),
                  self._slice(P, pre + "norm1.bias"), dy, dx, self._slice(dflat, pre + "norm1.weight"),
                  self._slice(dflat, pre + "norm1.bias"), self._slice(dflat, pre + "conv1.weight"),
                  self._slice(dflat, pre + "conv1.bias"), F(n_ws), n_ws, dt)
-            return dx.view(B, h, w, c)
+            return dx.view(B, h, w, c), None
         self._wgrad(dt1, 2 * c, AM_PLAIN, S["n1"], c, AM_PLAIN, None, 1, M, 2 * c, c, 0, 0, 0, 0,
                     self._slice(dflat, pre + "conv1.weight"), self._slice(dflat, pre + "conv1.bias"))
-        if fuse_ln:
-            self._dgrad_ln(Wt, dflat, P, pre, "conv1.weight", "norm1", dt1, S["x"].reshape(M, c), S["st1"], dy, dx,
-                           M, c)
+        pend = dict(pre=pre, geo=geo, dt1=dt1, x=S["x"].reshape(M, c), st1=S["st1"], dy=dy)
+        if defer:
+            return None, pend
+        return self._conv1_bwd(P, Wt, dflat, **pend), None
+
+    def _conv1_bwd(self, P, Wt, dflat, pre, geo, dt1, x, st1, dy):
+        """conv1 input gradient + norm1 backward + the residual dy: a block's dx."""
+        B, h, w, c = geo
+        M = B * h * w
+        dt = self.dt
+        dx = torch.empty(M, c, device=dt1.device, dtype=self.adt)
+        # LN backward in the conv1 dgrad's epilogue (dn1 never stored) at these widths
+        if dt != 0 and c in (32, 64, 128, 256):
+            self._dgrad_ln(Wt, dflat, P, pre, "conv1.weight", "norm1", dt1, x, st1, dy, dx, M, c)
         else:
-            dn1 = E(M, c)
+            dn1 = torch.empty(M, c, device=dt1.device, dtype=self.adt)
             self._mm(Wt, dt1, 2 * c, AM_PLAIN, None, 1, pre + "conv1.weight", dn1, c, CM_PLAIN, M, c, 2 * c,
                      dgrad=True)
             lg = query("ln_nhwc_grid", M, c, dt)
-            sw, sb = F(lg * c), F(lg * c)
-            call("ln_bwd_nhwc", dn1, S["x"].reshape(M, c), S["st1"], self._slice(P, pre + "norm1.weight"), dy, dx,
-                 sw, sb, M, c, dt)
+            sw, sb = self._ws(lg * c, dt1.device), self._ws(lg * c, dt1.device)
+            call("ln_bwd_nhwc", dn1, x, st1, self._slice(P, pre + "norm1.weight"), dy, dx, sw, sb, M, c, dt)
             self._reduce(sw, lg, c, self._slice(dflat, pre + "norm1.weight"))
             self._reduce(sb, lg, c, self._slice(dflat, pre + "norm1.bias"))
         return dx.view(B, h, w, c)

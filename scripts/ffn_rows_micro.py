@@ -43,7 +43,7 @@ def main():
 
 def main_bwd(iters=20):
     """the backward chain (nbp_ffn_rows_bwd) against its launches at the same shapes"""
-    from test_gpu_ffn_rows import _bwd_reference, to_frag, DT
+    from test_gpu_ffn_rows import _bwd_reference, _dgrad_ln_reference, to_frag, DT
     dev = torch.device("cuda:0")
     dt = 2
     Ht = DT[dt]
@@ -61,19 +61,35 @@ def main_bwd(iters=20):
         outs = [torch.empty(M, n, device=dev, dtype=Ht) for n in (2 * C, C, C)]
         slabs = [torch.empty(nb * C, device=dev) for _ in range(3)]
 
+        # the pending conv1 input gradient of the following block (nbp_ffn_rows_bwd with dt1)
+        q = dict(dt1=R(M, 2 * C).to(Ht), w1t=(R(C, 2 * C) / C ** 0.5).to(Ht), x1=R(M, C).to(Ht),
+                 st1=torch.rand(M, 2, device=dev) + 0.5, lnw1=1 + 0.1 * R(C), dres1=R(M, C).to(Ht))
+        f1 = to_frag(q["w1t"])
+        dx1 = torch.empty(M, C, device=dev, dtype=Ht)
+        slabs1 = [torch.empty(nb * C, device=dev) for _ in range(2)]
+
         def old():
             _bwd_reference(dev, dt, M, C, hw, o)
 
         def new():
-            call("ffn_rows_bwd", o["dout"], o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], f5, f4, f3, *outs, *slabs, M,
-                 C, hw, dt)
-        res = {"old": [], "new": []}
+            call("ffn_rows_bwd", o["dout"], o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], f5, f4, f3, *outs, *slabs,
+                 *(None,) * 9, M, C, hw, dt)
+
+        def old_pre():
+            _dgrad_ln_reference(dev, dt, M, C, q["dt1"], q["w1t"], q["x1"], q["st1"], q["lnw1"], q["dres1"])
+            new()
+
+        def new_pre():
+            call("ffn_rows_bwd", None, o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], f5, f4, f3, *outs, *slabs,
+                 q["dt1"], f1, q["x1"], q["st1"], q["lnw1"], q["dres1"], dx1, *slabs1, M, C, hw, dt)
+        res = {"old": [], "new": [], "old_pre": [], "new_pre": []}
         for _ in range(3):
-            res["old"].append(graph_time(old, iters))
-            res["new"].append(graph_time(new, iters))
+            for k, f in (("old", old), ("new", new), ("old_pre", old_pre), ("new_pre", new_pre)):
+                res[k].append(graph_time(f, iters))
         mb = (M * C * 9 + 4 * C * C) * 2 / 1e6
         print(f"bwd C{C} {hw} px/img B{B}: launches {min(res['old']):.1f} us, fused {min(res['new']):.1f} us "
-              f"({mb:.1f} MB algorithmic -> {mb / min(res['new']):.2f} TB/s)", flush=True)
+              f"({mb:.1f} MB algorithmic -> {mb / min(res['new']):.2f} TB/s); + conv1 dgrad/norm1: launches + fused "
+              f"{min(res['old_pre']):.1f} us, one launch {min(res['new_pre']):.1f} us", flush=True)
 
 
 if __name__ == "__main__":

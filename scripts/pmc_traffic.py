@@ -32,8 +32,14 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            "wgrad_group_512": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi512ELi2EE"),),
            "wgrad_group_768": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi768ELi4EE"),),
            "reduce_multi": ("reduce_multi_kernel",), "layer_scale_grad": ("layer_scale_grad_kernel",),
-           "ffn_rows": ("ffn_rows_fwd", "ffn_rows_bwd"), "ffn_rows_bwd_512": (re.compile(r"ffn_rows_bwdI\w+?Li512EE"),),
-           "ffn_rows_bwd_256": (re.compile(r"ffn_rows_bwdI\w+?Li256EE"),), "ffn_rows_bwd_128": (re.compile(r"ffn_rows_bwdI\w+?Li128EE"),), "ffn_rows_512": (re.compile(r"ffn_rows_fwdI\w+?Li512EE"),),
+           "ffn_rows": ("ffn_rows_fwd", "ffn_rows_bwd"),
+           "ffn_rows_bwd_512": (re.compile(r"ffn_rows_bwdI\w+?Li512ELb0EE"),),
+           "ffn_rows_bwd_256": (re.compile(r"ffn_rows_bwdI\w+?Li256ELb0EE"),),
+           "ffn_rows_bwd_128": (re.compile(r"ffn_rows_bwdI\w+?Li128ELb0EE"),),
+           "ffn_rows_bwd_pre_512": (re.compile(r"ffn_rows_bwdI\w+?Li512ELb1EE"),),
+           "ffn_rows_bwd_pre_256": (re.compile(r"ffn_rows_bwdI\w+?Li256ELb1EE"),),
+           "ffn_rows_bwd_pre_128": (re.compile(r"ffn_rows_bwdI\w+?Li128ELb1EE"),),
+           "ffn_rows_512": (re.compile(r"ffn_rows_fwdI\w+?Li512EE"),),
            "ffn_rows_256": (re.compile(r"ffn_rows_fwdI\w+?Li256EE"),), "ffn_rows_128": (re.compile(r"ffn_rows_fwdI\w+?Li128EE"),),
            "ln_bwd": ("ln_bwd_nhwc",),
            # VGG / AlexNet implicit-GEMM convs (cfg3's perceptual + LPIPS trunks): the tiled kernels with A mode 3 / 4

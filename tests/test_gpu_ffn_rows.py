@@ -144,24 +144,10 @@ def _bwd_reference(dev, dt, M, C, hw, o):
     from lowlight_image_enhancement_amd._lib import call, query
     Ht = DT[dt]
     E = lambda n: torch.empty(M, n, device=dev, dtype=Ht)  # noqa: E731
-    dt4, dy, dh = E(2 * C), E(C), E(C)
-    dlnw, dlnb = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dt4, dh = E(2 * C), E(C)
     call("gemm_bf16", o["dout"], C, AM_PLAIN, None, 1, dt, o["w5t"], C, dt4, 2 * C, CM_SGBWD, dt, M, C, C, 0, 0, 0, None,
          o["t4"], None, None)
-    if C in (128, 256):
-        n_ws = query("dgrad_ln_workspace_floats", M, C)
-        ws = torch.empty(n_ws, device=dev)
-        call("dgrad_ln_bwd", dt4, 2 * C, o["w4t"], 2 * C, M, C, 2 * C, o["y"], o["st2"], o["lnw2"], o["dout"], dy, dlnw,
-             dlnb, ws, n_ws, dt)
-    else:
-        dn2 = E(C)
-        call("gemm_bf16", dt4, 2 * C, AM_PLAIN, None, 1, dt, o["w4t"], 2 * C, dn2, C, CM_PLAIN, dt, M, C, 2 * C, 0, 0, 0,
-             None, None, None, None)
-        lg = query("ln_nhwc_grid", M, C, dt)
-        sw, sb = torch.empty(lg * C, device=dev), torch.empty(lg * C, device=dev)
-        call("ln_bwd_nhwc", dn2, o["y"], o["st2"], o["lnw2"], o["dout"], dy, sw, sb, M, C, dt)
-        call("reduce_slab", sw, lg, C, dlnw)
-        call("reduce_slab", sb, lg, C, dlnb)
+    dy, dlnw, dlnb = _dgrad_ln_reference(dev, dt, M, C, dt4, o["w4t"], o["y"], o["st2"], o["lnw2"], o["dout"])
     B = M // hw
     da = torch.empty(B * (hw // 64) * C, device=dev)
     call("gemm_bf16", dy, C, AM_PLAIN, None, hw, dt, o["w3t"], C, dh, C, CM_CHANDOT, dt, M, C, C, 0, 0, 0, None, o["g"],
@@ -169,35 +155,79 @@ def _bwd_reference(dev, dt, M, C, hw, o):
     return dict(dt4=dt4, dy=dy, dh=dh, dlnw=dlnw, dlnb=dlnb, da=da.view(B, hw // 64, C).sum(1))
 
 
+def _dgrad_ln_reference(dev, dt, M, C, d, wt, x, st, lnw, dres):
+    """the (K = 2C) input gradient + LayerNorm2d backward + residual as the executor launches it (nafnet.py
+    _conv1_bwd / _ffn_bwd_launches): nbp_dgrad_ln_bwd at C 128 / 256, nbp_gemm_bf16 + nbp_ln_bwd_nhwc at C 512.
+    Returns (dx, d weight, d bias)."""
+    from lowlight_image_enhancement_amd._lib import call, query
+    out = torch.empty(M, C, device=dev, dtype=DT[dt])
+    dlnw, dlnb = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    if C in (128, 256):
+        n_ws = query("dgrad_ln_workspace_floats", M, C)
+        ws = torch.empty(n_ws, device=dev)
+        call("dgrad_ln_bwd", d, 2 * C, wt, 2 * C, M, C, 2 * C, x, st, lnw, dres, out, dlnw, dlnb, ws, n_ws, dt)
+    else:
+        dn = torch.empty(M, C, device=dev, dtype=DT[dt])
+        call("gemm_bf16", d, 2 * C, AM_PLAIN, None, 1, dt, wt, 2 * C, dn, C, CM_PLAIN, dt, M, C, 2 * C, 0, 0, 0,
+             None, None, None, None)
+        lg = query("ln_nhwc_grid", M, C, dt)
+        sw, sb = torch.empty(lg * C, device=dev), torch.empty(lg * C, device=dev)
+        call("ln_bwd_nhwc", dn, x, st, lnw, dres, out, sw, sb, M, C, dt)
+        call("reduce_slab", sw, lg, C, dlnw)
+        call("reduce_slab", sb, lg, C, dlnb)
+    return out, dlnw, dlnb
+
+
+def _ln_input(R, M, C, Ht):
+    x = (R(M, C) * 1.5 + 0.2).to(Ht)
+    xd = x.double()
+    mu = xd.mean(1, keepdim=True)
+    den = ((xd - mu) ** 2).mean(1, keepdim=True).add(1e-6).sqrt()
+    return x, torch.cat([mu, den], 1).float().contiguous()
+
+
 CM_SGBWD, CM_CHANDOT = 5, 8
 
 
+@pytest.mark.parametrize("pre", [False, True])
 @pytest.mark.parametrize("dt", [1, 2])
 @pytest.mark.parametrize("C,B,hw", [(128, 2, 4096), (128, 1, 1024), (256, 2, 1024), (256, 3, 256), (512, 16, 256),
                                     (512, 1, 1024)])
-def test_ffn_rows_bwd_bitwise_equals_the_launches(dev, dt, C, B, hw):
+def test_ffn_rows_bwd_bitwise_equals_the_launches(dev, dt, C, B, hw, pre):
     """nbp_ffn_rows_bwd: dt4, dy, dh bitwise the launches it replaces; the norm2 weight / bias gradients and the SCA
-    channel dot (its per-32-row partials summed per image) within fp32 summation order of theirs."""
+    channel dot (its per-32-row partials summed per image) within fp32 summation order of theirs.  pre: dout is made
+    in the launch as the following block's dx (its conv1 input gradient + norm1 backward + residual), bitwise
+    _dgrad_ln_reference, norm1's weight / bias gradients within fp32 summation order."""
     from lowlight_image_enhancement_amd._lib import call
     Ht = DT[dt]
     M = B * hw
     gen = torch.Generator(device=dev).manual_seed(C + B + hw + 7 * dt)
     R = lambda *s: torch.randn(*s, device=dev, generator=gen)  # noqa: E731
-    y = (R(M, C) * 1.5 + 0.2).to(Ht)
-    yd = y.double()
-    mu = yd.mean(1, keepdim=True)
-    den = ((yd - mu) ** 2).mean(1, keepdim=True).add(1e-6).sqrt()
-    o = dict(dout=R(M, C).to(Ht), t4=R(M, 2 * C).to(Ht), y=y, st2=torch.cat([mu, den], 1).float().contiguous(),
-             lnw2=1 + 0.1 * R(C), g=R(M, C).to(Ht), w5t=(R(C, C) / C ** 0.5).to(Ht), w4t=(R(C, 2 * C) / C ** 0.5).to(Ht),
-             w3t=(R(C, C) / C ** 0.5).to(Ht))
-    ref = _bwd_reference(dev, dt, M, C, hw, o)
+    y, st2 = _ln_input(R, M, C, Ht)
+    o = dict(dout=R(M, C).to(Ht), t4=R(M, 2 * C).to(Ht), y=y, st2=st2, lnw2=1 + 0.1 * R(C), g=R(M, C).to(Ht),
+             w5t=(R(C, C) / C ** 0.5).to(Ht), w4t=(R(C, 2 * C) / C ** 0.5).to(Ht), w3t=(R(C, C) / C ** 0.5).to(Ht))
     nan = lambda *s: torch.full(s, float("nan"), device=dev, dtype=Ht)  # noqa: E731
     nb = M // 32
+    pre_args, ref1 = (None,) * 9, None
+    if pre:
+        x1, st1 = _ln_input(R, M, C, Ht)
+        q = dict(dt1=R(M, 2 * C).to(Ht), w1t=(R(C, 2 * C) / C ** 0.5).to(Ht), x1=x1, st1=st1, lnw1=1 + 0.1 * R(C),
+                 dres1=R(M, C).to(Ht))
+        ref1 = _dgrad_ln_reference(dev, dt, M, C, q["dt1"], q["w1t"], x1, st1, q["lnw1"], q["dres1"])
+        o["dout"] = ref1[0]
+        dx1 = nan(M, C)
+        sw1, sb1 = (torch.full((nb * C,), float("nan"), device=dev) for _ in range(2))
+        pre_args = (q["dt1"], to_frag(q["w1t"]), x1, st1, q["lnw1"], q["dres1"], dx1, sw1, sb1)
+    ref = _bwd_reference(dev, dt, M, C, hw, o)
     got = dict(dt4=nan(M, 2 * C), dy=nan(M, C), dh=nan(M, C))
     sw, sb, da = (torch.full((nb * C,), float("nan"), device=dev) for _ in range(3))
-    call("ffn_rows_bwd", o["dout"], o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], to_frag(o["w5t"]), to_frag(o["w4t"]),
-         to_frag(o["w3t"]), got["dt4"], got["dy"], got["dh"], sw, sb, da, M, C, hw, dt)
+    call("ffn_rows_bwd", None if pre else o["dout"], o["t4"], o["y"], o["st2"], o["lnw2"], o["g"], to_frag(o["w5t"]),
+         to_frag(o["w4t"]), to_frag(o["w3t"]), got["dt4"], got["dy"], got["dh"], sw, sb, da, *pre_args, M, C, hw, dt)
     torch.cuda.synchronize()
+    if pre:
+        assert torch.equal(_bits(dx1), _bits(ref1[0])), (dx1.float() - ref1[0].float()).abs().max().item()
+        for v, r in ((sw1.view(nb, C).sum(0), ref1[1]), (sb1.view(nb, C).sum(0), ref1[2])):
+            assert (v - r).abs().max().item() <= 2e-5 * r.abs().max().item() + 1e-6
     for k in ("dt4", "dy", "dh"):
         assert torch.equal(_bits(got[k]), _bits(ref[k])), (k, (got[k].float() - ref[k].float()).abs().max().item())
     for k, v in (("dlnw", sw.view(nb, C).sum(0)), ("dlnb", sb.view(nb, C).sum(0)),
