@@ -70,7 +70,36 @@ constexpr int fr_waves() { return C >= 256 ? 8 : 4; }
 template <int NW>
 __device__ __forceinline__ int colgroup(int rot) {
   const int wave = threadIdx.x >> 6;
-  return rot ? (wave + (int)(blockIdx.x >> 3)) % NW : wave;
+  return (rot & 1) ? (wave + (int)(blockIdx.x >> 3)) % NW : wave;
+}
+
+// activation rows in / out of HBM: read and written once per launch; with rot & 2 through the non-temporal policy, so
+// that they do not evict the weights every workgroup of the XCD streams from its L2 (speed only)
+// The launch's weights pulled into the L2 of every XCD at once (rot & 4; speed only): workgroup j of an XCD (blocks b,
+// b + 8, ...: j = b / 8 of n = grid / 8) issues 1-KB wave-instructions of LDS-DMA over its 1 / n share of each matrix,
+// into a scratch KB per wave that nothing reads (the fp32 staging rows, first written after a __syncthreads, whose
+// vmcnt(0) has drained these).  The weights come from HBM once per step (the Infinity Cache has been overrun by then):
+// streamed by the K loops alone, each XCD's workgroups wait on the same few misses in lockstep
+template <int NW>
+__device__ __forceinline__ void l2_pull(const void* w, long bytes, float* scratch) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long n = (gridDim.x + 7) >> 3, j = blockIdx.x >> 3, nq = bytes >> 10;
+  unsigned char* dst = reinterpret_cast<unsigned char*>(scratch) + wave * 1024;
+  for (long q = j * NW + wave; q < nq; q += n * NW)
+    glds16(reinterpret_cast<const unsigned char*>(w) + (q << 10) + lane * 16, dst);
+}
+
+// (off counts elements of E, the base's own type: a T of several E starts at base + off)
+template <typename T, typename E>
+__device__ __forceinline__ T gload(const E* base, long off, int rot) {
+  const T* q = reinterpret_cast<const T*>(base + off);
+  return (rot & 2) ? __builtin_nontemporal_load(q) : *q;
+}
+template <typename T, typename E>
+__device__ __forceinline__ void gstore(E* base, long off, T v, int rot) {
+  T* q = reinterpret_cast<T*>(base + off);
+  if (rot & 2) __builtin_nontemporal_store(v, q);
+  else *q = v;
 }
 
 template <typename H, int NW, int K, int N>
@@ -136,8 +165,8 @@ __device__ __forceinline__ void stage_acc(const floatx16 (&acc)[N / (32 * NW)], 
 }
 
 template <typename H>
-__device__ __forceinline__ void ld8h(const void* base, long off, float* v) {
-  const vec_t<H, 8> t = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(base) + off);
+__device__ __forceinline__ void ld8h(const void* base, long off, float* v, int rot) {
+  const vec_t<H, 8> t = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(base) + off, 0, rot);
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (float)t[j];
 }
@@ -198,6 +227,11 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   float* Ss = reinterpret_cast<float*>(smem + AS + YS);  // fp32 accumulator staging
   const int tid = threadIdx.x;
   const int m0 = blockIdx.x * BM, M = p.M;
+  if (p.rot & 4) {
+    l2_pull<NW>(p.w3, (long)C * C * 2, Ss);
+    l2_pull<NW>(p.w4, (long)2 * C * C * 2, Ss);
+    l2_pull<NW>(p.w5, (long)C * C * 2, Ss);
+  }
   auto aslot = [&](int row, int c) { return As + row * C + 8 * (c ^ (row & 15)); };
 
   // ---- the row-pass chunks of this thread (row, 8-channel chunk c): the residual x loaded under conv3's K loop
@@ -218,7 +252,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       float gv[8], sv[8], pr[8];
-      ld8h<H>(p.g, poff[it], gv);
+      ld8h<H>(p.g, poff[it], gv, p.rot);
       ld8(arow + 8 * pc[it], sv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) pr[j] = pok[it] ? gv[j] * sv[j] : 0.f;
@@ -227,7 +261,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
   }
   vec_t<H, 8> xres[NIT];
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) xres[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.x) + poff[it]);
+  for (int it = 0; it < NIT; ++it) xres[it] = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(p.x), poff[it], p.rot);
   RowsB<H, NW, C, C> b3;
   b3.prefetch(reinterpret_cast<const H*>(p.w3), p.rot);
   __syncthreads();
@@ -266,8 +300,8 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
     const vec_t<H, 8> nh = rnd8<H>(o);
     *reinterpret_cast<vec_t<H, 8>*>(aslot(row, pc[it])) = nh;
     if (pok[it]) {
-      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.y) + poff[it]) = yh;
-      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.n2) + poff[it]) = nh;
+      gstore(reinterpret_cast<H*>(p.y), poff[it], yh, p.rot);
+      gstore(reinterpret_cast<H*>(p.n2), poff[it], nh, p.rot);
       if (c8 == 0) p.st2[m0 + row] = st;
     }
   }
@@ -306,8 +340,8 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
         *reinterpret_cast<vec_t<H, 4>*>(aslot(row, gcol / 16) + (gcol / 2) % 8) = gh;
         if (pok[it]) {
           const long r = m0 + row;
-          *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.t4) + r * 2 * C + gcol) = rnd8<H>(v);
-          *reinterpret_cast<vec_t<H, 4>*>(reinterpret_cast<H*>(p.g2) + r * C + gcol / 2) = gh;
+          gstore(reinterpret_cast<H*>(p.t4), r * 2 * C + gcol, rnd8<H>(v), p.rot);
+          gstore(reinterpret_cast<H*>(p.g2), r * C + gcol / 2, gh, p.rot);
         }
       }
     }
@@ -335,7 +369,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
       ov[j] = fmaf(sc[j], v[j], (float)yh[j]);
     }
     const vec_t<H, 8> oh = rnd8<H>(ov);
-    if (pok[it]) *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.out) + poff[it]) = oh;
+    if (pok[it]) gstore(reinterpret_cast<H*>(p.out), poff[it], oh, p.rot);
     if (p.lnw1) {  // (uniform)
       float xs[8], w[8], b[8], o[8];
 #pragma unroll
@@ -345,7 +379,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_fwd(FfnRowsP p) {
       float2 st;
       ln_chunk<C>(xs, w, b, p.eps, o, st);
       if (pok[it]) {
-        *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.nn1) + poff[it]) = rnd8<H>(o);
+        gstore(reinterpret_cast<H*>(p.nn1), poff[it], rnd8<H>(o), p.rot);
         if (c8 == 0) p.nst1[m0 + row] = st;
       }
     }
@@ -436,7 +470,7 @@ template <typename H, int C, int NIT, bool RND, typename Slot>
 __device__ __forceinline__ void ln_bwd_rows(const float* Ss, const float* lnw, const vec_t<H, 8> (&xq)[NIT],
                                             const float2 (&stq)[NIT], const vec_t<H, 8> (&rq)[NIT], const int* prow,
                                             const int* pc, const bool* pok, const long* poff, Slot slot, void* gout,
-                                            float (&aw)[8], float (&ab)[8]) {
+                                            float (&aw)[8], float (&ab)[8], int rot) {
   constexpr int NCH = C / 8, SW = C;
 #pragma unroll
   for (int j = 0; j < 8; ++j) aw[j] = ab[j] = 0.f;
@@ -470,7 +504,7 @@ __device__ __forceinline__ void ln_bwd_rows(const float* Ss, const float* lnw, c
     for (int j = 0; j < 8; ++j) o[j] = fmaf(rinv, fmaf(-yh[j], mgy, d[j] * w[j]) - mg, (float)rq[it][j]);
     const vec_t<H, 8> oh = rnd8<H>(o);
     *reinterpret_cast<vec_t<H, 8>*>(slot(row, pc[it])) = oh;
-    if (pok[it]) *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(gout) + poff[it]) = oh;
+    if (pok[it]) gstore(reinterpret_cast<H*>(gout), poff[it], oh, rot);
   }
 }
 
@@ -488,6 +522,12 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   float* Ss = reinterpret_cast<float*>(smem + A1 + A2);
   const int tid = threadIdx.x;
   const int m0 = blockIdx.x * BM, M = p.M;
+  if (p.rot & 4) {
+    if constexpr (PRE) l2_pull<NW>(p.w1, (long)2 * C * C * 2, Ss);
+    l2_pull<NW>(p.w5, (long)C * C * 2, Ss);
+    l2_pull<NW>(p.w4, (long)2 * C * C * 2, Ss);
+    l2_pull<NW>(p.w3, (long)C * C * 2, Ss);
+  }
   const long blk = blockIdx.x;
   auto slot = [&](H* base, int K, int row, int c) { return base + row * K + 8 * (c ^ (row & 15)); };
   auto dslot = [&](int row, int c) { return slot(Ad, C, row, c); };
@@ -510,7 +550,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {  // dt1 rows (2C: chunks 2c, 2c + 1 of the thread's chunk c)
       const H* d1 = reinterpret_cast<const H*>(p.dt1) + 2 * poff[it];
-      vec_t<H, 8> lo = *reinterpret_cast<const vec_t<H, 8>*>(d1), hi = *reinterpret_cast<const vec_t<H, 8>*>(d1 + 8);
+      vec_t<H, 8> lo = gload<vec_t<H, 8>>(d1, 0, p.rot), hi = gload<vec_t<H, 8>>(d1, 8, p.rot);
       if (!pok[it]) lo = hi = vec_t<H, 8>{};
       *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, prow[it], 2 * pc[it])) = lo;
       *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, prow[it], 2 * pc[it] + 1)) = hi;
@@ -527,13 +567,13 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     float2 stq[NIT];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      xq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.x1) + poff[it]);
-      rq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.dres1) + poff[it]);
+      xq[it] = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(p.x1), poff[it], p.rot);
+      rq[it] = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(p.dres1), poff[it], p.rot);
       stq[it] = p.st1[pok[it] ? m0 + prow[it] : M - 1];
     }
     __syncthreads();
     float aw[8], ab[8];
-    ln_bwd_rows<H, C, NIT, C == 512>(Ss, p.lnw1, xq, stq, rq, prow, pc, pok, poff, dslot, p.dx1, aw, ab);
+    ln_bwd_rows<H, C, NIT, C == 512>(Ss, p.lnw1, xq, stq, rq, prow, pc, pok, poff, dslot, p.dx1, aw, ab, p.rot);
     __syncthreads();
     chunk_partials_out<C, NW>(aw, Ss, p.slab_w1 + blk * C);
     chunk_partials_out<C, NW>(ab, Ss, p.slab_b1 + blk * C);
@@ -543,13 +583,13 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     if constexpr (!PRE) {
-      vec_t<H, 8> d = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.dout) + poff[it]);
+      vec_t<H, 8> d = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(p.dout), poff[it], p.rot);
       if (!pok[it]) d = vec_t<H, 8>{};
       *reinterpret_cast<vec_t<H, 8>*>(dslot(prow[it], pc[it])) = d;
     }
     const H* t4 = reinterpret_cast<const H*>(p.t4) + 2 * poff[it];
-    tq[it][0] = *reinterpret_cast<const vec_t<H, 8>*>(t4);
-    tq[it][1] = *reinterpret_cast<const vec_t<H, 8>*>(t4 + 8);
+    tq[it][0] = gload<vec_t<H, 8>>(t4, 0, p.rot);
+    tq[it][1] = gload<vec_t<H, 8>>(t4, 8, p.rot);
   }
   RowsB<H, NW, C, C> b5;
   b5.prefetch(reinterpret_cast<const H*>(p.w5), p.rot);
@@ -583,10 +623,10 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     *reinterpret_cast<vec_t<H, 8>*>(slot(At, 2 * C, row, 2 * pc[it] + 1)) = hi;
     if (pok[it]) {
       H* d = reinterpret_cast<H*>(p.dt4) + 2 * poff[it];
-      *reinterpret_cast<vec_t<H, 8>*>(d) = lo;
-      *reinterpret_cast<vec_t<H, 8>*>(d + 8) = hi;
+      gstore(d, 0, lo, p.rot);
+      gstore(d, 8, hi, p.rot);
     }
-    yq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.y) + poff[it]);  // for the LN backward
+    yq[it] = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(p.y), poff[it], p.rot);  // for the LN backward
     stq[it] = p.st2[pok[it] ? m0 + row : M - 1];
     rq2[it] = *reinterpret_cast<const vec_t<H, 8>*>(dslot(row, pc[it]));  // dout: the residual branch
   }
@@ -602,13 +642,13 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
   }
   __syncthreads();
   float aw[8], ab[8];
-  ln_bwd_rows<H, C, NIT, C == 512>(Ss, p.lnw2, yq, stq, rq2, prow, pc, pok, poff, dslot, p.dy, aw, ab);
+  ln_bwd_rows<H, C, NIT, C == 512>(Ss, p.lnw2, yq, stq, rq2, prow, pc, pok, poff, dslot, p.dy, aw, ab, p.rot);
   __syncthreads();  // dy complete in LDS; the staging rows are free: the norm2 partials through them
   chunk_partials_out<C, NW>(aw, Ss, p.slab_w + blk * C);
   chunk_partials_out<C, NW>(ab, Ss, p.slab_b + blk * C);
   vec_t<H, 8> gq[NIT];
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) gq[it] = *reinterpret_cast<const vec_t<H, 8>*>(reinterpret_cast<const H*>(p.g) + poff[it]);
+  for (int it = 0; it < NIT; ++it) gq[it] = gload<vec_t<H, 8>>(reinterpret_cast<const H*>(p.g), poff[it], p.rot);
 
   // ---- dh = dy W3'^T -> memory; the SCA channel-dot partials sum_rows dh g
   {
@@ -629,7 +669,7 @@ __global__ __launch_bounds__(64 * fr_waves<C>()) void ffn_rows_bwd(FfnRowsBwdP p
     ld8(Ss + row * SW + c8, v);
     const vec_t<H, 8> dhh = rnd8<H>(v);
     if (pok[it]) {
-      *reinterpret_cast<vec_t<H, 8>*>(reinterpret_cast<H*>(p.dh) + poff[it]) = dhh;
+      gstore(reinterpret_cast<H*>(p.dh), poff[it], dhh, p.rot);
 #pragma unroll
       for (int j = 0; j < 8; ++j) cd[j] = fmaf((float)dhh[j], (float)gq[it][j], cd[j]);
     }
@@ -645,10 +685,15 @@ using namespace nbp;
 
 namespace {
 // NBP_FFN_ROT=0: no column-group rotation (A/B)
+// bit 0: column-group rotation (NBP_FFN_ROT, default on); bit 1: non-temporal rows (NBP_FFN_NT, measured neutral);
+// bit 2: the weights pulled into L2 at launch start (NBP_FFN_PF, default on: middle-level forward over 12 distinct
+// weight / activation sets 46.5 -> 37.4 us per launch, step +3.2 %, gpurun_out r6q)
 int ffn_rot() {
   static const int v = [] {
     const char* e = getenv("NBP_FFN_ROT");
-    return e ? atoi(e) : 1;
+    const char* n = getenv("NBP_FFN_NT");
+    const char* f = getenv("NBP_FFN_PF");
+    return ((e ? atoi(e) : 1) & 1) | ((n ? atoi(n) : 0) ? 2 : 0) | ((f ? atoi(f) : 1) ? 4 : 0);
   }();
   return v;
 }
