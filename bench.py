@@ -99,7 +99,7 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
              "ffn_rows_bwd<256,pre>": "ffn_rows_bwd_pre_256", "ffn_rows_bwd<128,pre>": "ffn_rows_bwd_pre_128"}
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
-    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32E(Li\d+E)?E"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64E(Li\d+E)?E"],
+    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32ELi\d+ELb[01]EE"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64ELi\d+ELb[01]EE"],
     "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32EE"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16EE"],
     "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
     "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],

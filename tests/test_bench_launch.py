@@ -102,11 +102,21 @@ def test_single_kernel_classes_name_one_rocprof_instance():
     path = _newest_kernel_stats()
     assert path is not None
     names = [r["Name"] for r in csv.DictReader(open(path))]
+    # the record's own bench line: a class it saw launched must name exactly one instance (a template parameter added
+    # to a kernel changes its mangled name: a stale regex would otherwise match nothing, silently)
+    bj = os.path.join(os.path.dirname(path), "bench.json")
+    launched = set()
+    if os.path.exists(bj):
+        import json
+        classes = json.load(open(bj))["roofline"].get("classes", {})
+        launched = {c for c, v in classes.items() if (v.get("launches_per_step") or 0) > 0}
     seen = 0
     for cls in bench.SINGLE_KERNEL:
         pats = [re.compile(p.format(T=bench.MANGLED_T["fp16"])) for p in bench.ROCPROF_KERNELS[cls]]
         hits = [n for n in names if any(p.search(n) for p in pats)]
         assert len(hits) <= 1, (cls, hits)
+        if cls in launched:
+            assert len(hits) == 1, (cls, "launched in the record's bench line but no rocprof instance matches")
         seen += len(hits)
     assert seen >= 5, path
     # the instance names the library records (nbp_launch_timing) are the keys of bench.INSTANCES
