@@ -609,7 +609,9 @@ namespace {
 int tile_w(int C) { return C == 32 ? 64 : 32; }
 // rows of a backward tile: 32 (the two-row halo of the rebuilt t1 and the one-row halo of the rebuilt t2 are then
 // 1.125 / 1.06 x the tile's rows instead of 1.25 / 1.125 at 16, and the per-tile weight-slice load and dW reduction
-// amortise over twice the pixels); NBP_C1DW_BWD_TH=16 / 32 (per C: "th32,th64") overrides for A/B runs
+// amortise over twice the pixels); NBP_C1DW_BWD_TH=16 / 32 (per C: "th32,th64") overrides for A/B runs; 64 at level 0
+// (512 workgroups: one resident round) measured 148.3 -> 141.1 us per launch in scripts/c1dw_tile_micro.py but
+// neutral-to-negative in the step (1476.8 / 1470.7 vs 1479.3 / 1474.1 img/s, gpurun_out r6v): not the default
 // the balanced t1 rebuild (BAL) at C 32: 151.0 -> 148.7-149.4 us per level-0 launch (scripts/c1dw_tile_micro.py,
 // gpurun_out r6c); at C 64 its registers spill (256 VGPRs + 10) and it is slower (89.1 -> 93.3 us): off there.
 // NBP_C1DW_BWD_BAL=0 / 1 forces it off / on at both (A/B)
@@ -627,7 +629,8 @@ int bwd_th(int C) {
     if (const char* e = getenv("NBP_C1DW_BWD_TH")) {
       int a = 0, b = 0;
       const int n = sscanf(e, "%d,%d", &a, &b);
-      if (n >= 1 && (a == 16 || a == 32)) th[0] = th[1] = a;
+      if (n >= 1 && (a == 16 || a == 32 || a == 64)) th[0] = a;  // 64: level 0 (C 32) only
+      if (n >= 1 && (a == 16 || a == 32)) th[1] = a;
       if (n == 2 && (b == 16 || b == 32)) th[1] = b;
     }
   }
@@ -702,7 +705,9 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
   lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
     const bool bal = bwd_bal(C);
-    if (C == 32 && th == 32 && bal) c1dw_bwd_tile<H, 32, 32, true><<<nblk, 256, 0, S(s)>>>(p);
+    if (C == 32 && th == 64 && bal) c1dw_bwd_tile<H, 32, 64, true><<<nblk, 256, 0, S(s)>>>(p);
+    else if (C == 32 && th == 64) c1dw_bwd_tile<H, 32, 64, false><<<nblk, 256, 0, S(s)>>>(p);
+    else if (C == 32 && th == 32 && bal) c1dw_bwd_tile<H, 32, 32, true><<<nblk, 256, 0, S(s)>>>(p);
     else if (C == 32 && th == 32) c1dw_bwd_tile<H, 32, 32, false><<<nblk, 256, 0, S(s)>>>(p);
     else if (C == 32) c1dw_bwd_tile<H, 32, 16, false><<<nblk, 256, 0, S(s)>>>(p);
     else if (th == 32 && bal) c1dw_bwd_tile<H, 64, 32, true><<<nblk, 256, 0, S(s)>>>(p);
