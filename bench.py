@@ -91,6 +91,7 @@ ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skin
 # record).
 INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_bwd_L1",
              "dw_bwd_tiled<T,true,32>": "dw_bwd_32", "dw_bwd_tiled<T,true,16>": "dw_bwd_16",
+             "dw_bwd_tiled<T,true,32,sca>": "dw_bwd_sca_32", "dw_bwd_tiled<T,true,16,sca>": "dw_bwd_sca_16",
              "wgrad_bf16_wide_group<3,512,2>": "wgrad_group_512", "wgrad_bf16_wide_group<3,768,4>": "wgrad_group_768",
              "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad",
              "ffn_rows_fwd<512>": "ffn_rows_512", "ffn_rows_fwd<256>": "ffn_rows_256", "ffn_rows_fwd<128>": "ffn_rows_128",
@@ -100,7 +101,8 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
     "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32ELi\d+ELb[01]EE"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64ELi\d+ELb[01]EE"],
-    "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32EE"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16EE"],
+    "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32E(Lb0E)?E"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16E(Lb0E)?E"],
+    "dw_bwd_sca_32": [r"dw_bwd_tiledI{T}Lb1ELi32ELb1EE"], "dw_bwd_sca_16": [r"dw_bwd_tiledI{T}Lb1ELi16ELb1EE"],
     "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
     "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],
     "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"],
@@ -116,6 +118,9 @@ UNIT_DEF = {
                  "(s = storage bytes), x B*H*W pixels of the launch (the 32-wide tile kernel at the levels that store "
                  "the tape: 2-3 at cfg2; levels 0-1 rebuild it in c1dw_bwd_tile)",
     "dw_bwd_16": "as dw_bwd_32 (7*C*s bytes per pixel), the 16-wide tile kernel (the 16 x 16 level)",
+    "dw_bwd_sca_32": "as dw_bwd_32, + the SCA backward folded in: the channel-dot slab (B x chunks x C) and W_sca "
+                     "(C^2) read, dW_sca (C^2) written, fp32",
+    "dw_bwd_sca_16": "as dw_bwd_sca_32, the 16-wide tile kernel (the 16 x 16 level)",
     "wgrad_group_512": "per grouped launch of this instance (128-column tiles): each problem's operands read once, "
                        "M*(N+K)*s, + its fp32 dW (+db) written once; the split-M fp32 slabs it writes instead are the "
                        "wgrad_group class's `slab_bytes_per_step`",
@@ -193,6 +198,13 @@ def cost_wgrad(a):  # (G,ldg,gm,X,ldx,xm,xs,rows,M,N,K,gh,gw,csg,csx,dW,db,ws,n_
 def cost_dw_bwd(a):  # (dh,a,ds,t2,t1,wdw,dt1,dwdw,dbdw,ws,B,h,w,c,dt): dh C + t2 2C + t1 2C in, dt1 2C out
     M, c = a[10] * a[11] * a[12], a[13]
     return 2.0 * M * 2 * c * 18, 7 * M * c * _e(a[14])
+
+
+def cost_sca_dw_bwd(a):  # (dh,a,da_slab,chunks,wsca,mean,dwsca,dbsca,t2,t1,wdw,dt1,dwdw,dbdw,ws,B,h,w,c,dt): as
+    # cost_dw_bwd + the SCA backward: the channel-dot slab and W_sca read, dW_sca written (fp32)
+    B, c = a[15], a[18]
+    M = B * a[16] * a[17]
+    return (2.0 * M * 2 * c * 18 + 4.0 * B * c * c, 7 * M * c * _e(a[19]) + 4 * (B * a[3] * c + 2 * c * c))
 
 
 def cost_dw_fwd(a):  # (t1,w,b,t2,g,pool,B,h,w,c,dt): t1 2C in, t2 2C + g C out
@@ -301,6 +313,7 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "dgrad_ln_bwd": rec_plain("gemm16", cost_dgrad_ln), "dgrad_sg_rc": rec_plain("gemm16", cost_sg_rc),
            "gemm_f32": rec_plain("gemm_f32", cost_gemm_f32), "wgrad_f32": rec_wgrad, "wgrad_group": rec_wgroup,
            "grad_reduce_flush": rec_flush, "sca_sg_dw_bwd": rec_plain("dw_bwd", cost_dw_bwd),
+           "sca_dw_bwd": rec_plain("dw_bwd", cost_sca_dw_bwd),
            "dw_sg_pool_fwd": rec_plain("dw_fwd", cost_dw_fwd), "gemm_ffn": rec_plain("gemm16", cost_ffn),
            "dgrad_sg_rc_wg": rec_plain("gemm16", cost_sg_rc_wg),
            "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),

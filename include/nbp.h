@@ -331,6 +331,15 @@ int nbp_dw_bwd(const void* dt2, const void* t1, const float* wdw, void* dt1, flo
 int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const void* t2, const void* t1, const float* wdw,
                       void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H, int W, int C, int dtype,
                       nbp_stream_t s);
+/* The SCA backward (nbp_sca_bwd_fused) folded into nbp_sca_sg_dw_bwd: each workgroup reduces its image's channel-dot
+ * partials (da_slab [B][chunks][C]) and forms ds of its own gate channels (ds[b][i] = sum_o W_sca[o][i] da[b][o]) before
+ * the fused depthwise backward; rows o of dwsca / dbsca (= sum_b da[b][o] mean[b][:] / da[b][o]) are spread over the
+ * workgroups.  16-bit, C a multiple of 16, C <= 1024, B <= 256.  Replaces, for the levels with the stored tape, the
+ * reference's SCA backward (NAFNet_arch.py:39-41, 67) and the two launches; ds / dW / db equal theirs up to fp32
+ * summation order. */
+int nbp_sca_dw_bwd(const void* dh, const float* a, const float* da_slab, int chunks, const float* wsca, const float* mean,
+                   float* dwsca, float* dbsca, const void* t2, const void* t1, const float* wdw, void* dt1, float* dwdw,
+                   float* dbdw, float* ws, int B, int H, int W, int C, int dtype, nbp_stream_t s);
 
 /* SimpleGate on the FFN half (NAFNet_arch.py:75): g = t[:C]*t[C:], and its backward. */
 /* layout 0: t = [t_a | t_b] halves; layout 1: pairs (a_c, b_c) interleaved (the internal conv4 channel order). */

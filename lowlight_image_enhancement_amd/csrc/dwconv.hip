@@ -554,7 +554,122 @@ struct DwTileP {
   float* slab_b;    // [rows][2C]
   int B, H, W, C, tiles_x, tiles, slices;
   float inv_hw;
+  // SCA: the SCA backward folded in (nbp_sca_dw_bwd): ds of the workgroup's gate channels from the channel-dot slab,
+  // and rows of the SCA weight / bias gradients
+  const float* da_slab;  // [B][chunks][C]
+  const float* wsca;     // [C][C]
+  const float* mean;     // [B][C]
+  float* dwsca;          // [C][C] out
+  float* dbsca;          // [C] out
+  int chunks;
 };
+
+// SCA backward pieces (NAFNet_arch.py:39-41, 67; the arithmetic of sca_bwd_fused, fixed orders of their own):
+// da[b][o] = sum over the image's chunks of the slab, ds[b][i] = sum_o W[o][i] da[b][o], dW[o][i] = sum_b da[b][o]
+// mean[b][i], db[o] = sum_b da[b][o].  Every piece is laid out for loads in flight (a dependent chain of L2 round trips
+// per workgroup cost more than the launch it replaces): the chunk sums split over thread groups with 8 independent
+// loads per step, the GEMV over float4 W quads with a thread's loads issued together.
+
+// sum of n values v[k0], v[k0 + step], ... (k < n) of a strided array, 8 loads in flight, fixed order
+__device__ __forceinline__ float strided_sum(const float* __restrict__ v, long stride, int k0, int step, int n) {
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = k0;
+  for (; k + 7 * step < n; k += 8 * step) {
+    float t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = v[(long)(k + q * step) * stride];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] += t[q];
+  }
+  for (int q = 0; k < n; k += step, ++q) a[q] += v[(long)k * stride];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+// ds of the HS gate channels cbase .. of image b into sds.  Scratch: part (max(NT, C) floats), sdb (C), red (NT * 4)
+template <int NT, int HS>
+__device__ void sca_ds_slice(const DwTileP& p, int b, int cbase, float* part, float* sdb, float* red, float* sds) {
+  const int tid = threadIdx.x, C = p.C, chunks = p.chunks;
+  // da[b][o]: thread (o0 = tid % OW, kg = tid / OW) sums chunks kg, kg + KG, ... of o = o0, o0 + OW, ...
+  const int OW = C < NT ? C : NT, KG = NT / OW;
+  const float* sl = p.da_slab + (long)b * chunks * C;
+  const int o0 = tid % OW, kg = tid / OW;
+  if (kg < KG)
+    for (int o = o0; o < C; o += OW) part[kg * C + o] = strided_sum(sl + o, C, kg, KG, chunks);
+  __syncthreads();
+  for (int o = tid; o < C; o += NT) {
+    float t = 0.f;
+    for (int g = 0; g < KG; ++g) t += part[g * C + o];
+    sdb[o] = t;
+  }
+  __syncthreads();
+  // ds: thread (quad qd of the HS channels, o group og) over o = og, og + NG, ...: float4 W loads, 8 at once
+  constexpr int NQ4 = HS / 4, NG = NT / NQ4;
+  static_assert(HS % 4 == 0 && NT % NQ4 == 0, "SCA GEMV geometry");
+  const int qd = tid % NQ4, og = tid / NQ4;
+  const float* wq = p.wsca + cbase + 4 * qd;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int o = og; o < C; o += 8 * NG) {
+    float4 w[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = o + q * NG < C ? ld4(wq + (long)(o + q * NG) * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float d = o + q * NG < C ? sdb[o + q * NG] : 0.f;
+      acc.x = fmaf(w[q].x, d, acc.x);
+      acc.y = fmaf(w[q].y, d, acc.y);
+      acc.z = fmaf(w[q].z, d, acc.z);
+      acc.w = fmaf(w[q].w, d, acc.w);
+    }
+  }
+  reinterpret_cast<float4*>(red)[og * NQ4 + qd] = acc;
+  __syncthreads();
+  if (tid < HS) {
+    float v = 0.f;
+    for (int g = 0; g < NG; ++g) v += red[g * HS + tid];
+    sds[tid] = v;
+  }
+  __syncthreads();
+}
+// the SCA weight / bias gradient rows o = blockIdx.x, + gridDim.x, ...  Scratch: part (max(NT, B) <= SCA_DW_BMAX floats:
+// KG * B <= NT when B < NT, else B), sdo (B)
+template <int NT>
+__device__ void sca_dw_rows(const DwTileP& p, float* part, float* sdo) {
+  const int tid = threadIdx.x, C = p.C, B = p.B, chunks = p.chunks;
+  const int BW = B < NT ? B : NT, KG = NT / BW;  // thread (image bb0 = tid % BW, chunk group kg = tid / BW)
+  const int bb0 = tid % BW, kg = tid / BW;
+  for (int o = blockIdx.x; o < C; o += gridDim.x) {
+    __syncthreads();  // scratch free
+    if (kg < KG)
+      for (int bb = bb0; bb < B; bb += BW)
+        part[kg * B + bb] = strided_sum(p.da_slab + (long)bb * chunks * C + o, C, kg, KG, chunks);
+    __syncthreads();
+    for (int bb = tid; bb < B; bb += NT) {
+      float t = 0.f;
+      for (int g = 0; g < KG; ++g) t += part[g * B + bb];
+      sdo[bb] = t;
+    }
+    __syncthreads();
+    for (int i = tid; i < C; i += NT) {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (8 mean loads in flight; fixed-order combine)
+      int bb = 0;
+      for (; bb + 7 < B; bb += 8) {
+        float m[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) m[q] = p.mean[(long)(bb + q) * C + i];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = fmaf(sdo[bb + q], m[q], a[q]);
+      }
+      for (int q = 0; bb < B; ++bb, ++q) a[q] = fmaf(sdo[bb], p.mean[(long)bb * C + i], a[q]);
+      p.dwsca[(long)o * C + i] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    }
+    if (tid == 0) {
+      float t = 0.f;
+      for (int bb = 0; bb < B; ++bb) t += sdo[bb];
+      p.dbsca[o] = t;
+    }
+  }
+}
+constexpr int SCA_DW_BMAX = 256;  // images (the dW rows' da staging)
 
 constexpr int DWT_TH = 16;
 inline int dw_bwd_tw(int W) { return W >= 32 ? 32 : 16; }
@@ -595,8 +710,9 @@ __device__ __forceinline__ void unpack16(uint4 r, float* f) {
 
 // (A variant that recomputed t2 from t1 in LDS instead of reading it, so that the forward need not store it, measured
 // neutral to slower and was removed in round 4.)
-template <typename T, bool FUSED, int DWT_TW>
+template <typename T, bool FUSED, int DWT_TW, bool SCA = false>
 __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
+  static_assert(!SCA || FUSED, "the SCA fold feeds the fused loader");
   constexpr int E = 16 / sizeof(T);      // elements per 16-byte chunk
   constexpr int CSL = 64 / sizeof(T);    // conv channels per slice
   constexpr int HS = CSL / 2;            // gate channels per slice
@@ -684,6 +800,12 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
       }
     }
   }
+  // SCA scratch in the dt2 tile (written only below, after the ds values are in registers; and free again after the
+  // final reduction): no LDS of its own, the resident workgroups per CU unchanged
+  float* sca_s = reinterpret_cast<float*>(sg);  // part [1024] | sdb [1024] | red [4 NT] | sds [HS]
+  static_assert(!SCA || (2048 + 4 * NT + HS) * 4 <= LH * LW * CSL * (int)sizeof(T), "SCA scratch");
+  static_assert(!SCA || (NT <= SCA_DW_BMAX && 2 * SCA_DW_BMAX * 4 <= LH * LW * CSL * (int)sizeof(T)), "SCA scratch");
+  if constexpr (SCA) sca_ds_slice<NT, HS>(p, b, cbase, sca_s, sca_s + 1024, sca_s + 2048, sca_s + 2048 + 4 * NT);
   if (FUSED) {
     // NT is even, so this thread's chunk k = tid & 1 (and its E channels) is the same in every pass: a and ds / HW once
     static_assert(NT % 2 == 0, "chunk parity per thread");
@@ -693,9 +815,11 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         ak[j] = p.a[(long)b * C + c + j];
-        sk[j] = p.ds[(long)b * C + c + j] * p.inv_hw;
+        if constexpr (SCA) sk[j] = sca_s[2048 + 4 * NT + (tid & 1) * E + j] * p.inv_hw;
+        else sk[j] = p.ds[(long)b * C + c + j] * p.inv_hw;
       }
     }
+    if constexpr (SCA) __syncthreads();  // every thread holds its ds before the tile overwrites the scratch
 #pragma unroll
     for (int it = 0; it < N2; ++it) {
       const int i = tid + it * NT;
@@ -832,6 +956,7 @@ __global__ __launch_bounds__(256) void dw_bwd_tiled(DwTileP p) {
     if (t < 9) p.slab_w[(row * C2 + ch) * 9 + t] = s;
     else p.slab_b[row * C2 + ch] = s;
   }
+  if constexpr (SCA) sca_dw_rows<NT>(p, sca_s, sca_s + SCA_DW_BMAX);  // (its first barrier: the reduction is done)
 }
 
 // ---------------------------------------------------------------- LDS-tiled depthwise 3x3 + SimpleGate + pool partials
@@ -1012,12 +1137,16 @@ Geo make_geo(int B, int H, int W, int C, int Q, int block, long cap_blocks) {
 
 int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float* ds, const void* t2, const void* t1,
                     const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
-                    int W, int C, int dtype, nbp_stream_t s) {
+                    int W, int C, int dtype, nbp_stream_t s, const DwTileP* sca = nullptr) {
   NBP_REQUIRE((long)W * 2 * C < (1L << 24), "depthwise backward: W * 2C must be < 2^24 (24-bit tile offsets)");
   const int hs = dtype != 0 ? 16 : 8;
   const int tw = dw_bwd_tw(W);
   DwTileP p{dt2, dh, a, ds, t2, t1, wdw, bdw, dt1, nullptr, nullptr, B, H, W, C, cdiv(W, tw), dw_tiles(H, W),
             C / hs, 1.f / (float)(H * W)};
+  if (sca) {
+    p.da_slab = sca->da_slab; p.wsca = sca->wsca; p.mean = sca->mean; p.dwsca = sca->dwsca; p.dbsca = sca->dbsca;
+    p.chunks = sca->chunks;
+  }
   const long nrow = (long)B * p.tiles;
   p.slab_w = ws;
   p.slab_b = ws + nrow * 2 * C * 9;
@@ -1028,17 +1157,19 @@ int launch_dw_tiled(const void* dt2, const void* dh, const float* a, const float
   NBP_DISPATCH_T(dtype, {
     constexpr int NQ = (64 / sizeof(T)) / 4;
     if (tw == 32) {
-      if (fused) dw_bwd_tiled<T, true, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      if (sca) dw_bwd_tiled<T, true, 32, true><<<nblk, NQ * 32, 0, S(s)>>>(p);
+      else if (fused) dw_bwd_tiled<T, true, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
       else dw_bwd_tiled<T, false, 32><<<nblk, NQ * 32, 0, S(s)>>>(p);
     } else {
-      if (fused) dw_bwd_tiled<T, true, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      if (sca) dw_bwd_tiled<T, true, 16, true><<<nblk, NQ * 16, 0, S(s)>>>(p);
+      else if (fused) dw_bwd_tiled<T, true, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
       else dw_bwd_tiled<T, false, 16><<<nblk, NQ * 16, 0, S(s)>>>(p);
     }
   });
   {  // per-launch record (nbp_launch_timing): fused: dh C + t2 2C + t1 2C in, dt1 2C out; else dt2 2C + t1 2C in, dt1 out
     const double M = (double)B * H * W, es = dtype != 0 ? 2 : 4;
-    const char* nm = tw == 32 ? (fused ? "dw_bwd_tiled<T,true,32>" : "dw_bwd_tiled<T,false,32>")
-                              : (fused ? "dw_bwd_tiled<T,true,16>" : "dw_bwd_tiled<T,false,16>");
+    const char* nm = tw == 32 ? (sca ? "dw_bwd_tiled<T,true,32,sca>" : fused ? "dw_bwd_tiled<T,true,32>" : "dw_bwd_tiled<T,false,32>")
+                              : (sca ? "dw_bwd_tiled<T,true,16,sca>" : fused ? "dw_bwd_tiled<T,true,16>" : "dw_bwd_tiled<T,false,16>");
     lt_end(S(s), nm, 2.0 * M * 2 * C * 18, (fused ? 7.0 : 6.0) * M * C * es);
   }
   int rc = check_launch("dw_bwd_tiled");
@@ -1213,6 +1344,20 @@ int nbp_sca_sg_dw_bwd(const void* dh, const float* a, const float* ds, const voi
 }
 
 int nbp_dw_tiled(int C, int dtype) { return dw_tiled_ok(C, dtype) ? 1 : 0; }
+
+// The SCA backward folded into the fused depthwise backward: nbp_sca_bwd_fused + nbp_sca_sg_dw_bwd in one launch.
+int nbp_sca_dw_bwd(const void* dh, const float* a, const float* da_slab, int chunks, const float* wsca, const float* mean,
+                   float* dwsca, float* dbsca, const void* t2, const void* t1, const float* wdw, void* dt1, float* dwdw,
+                   float* dbdw, float* ws, int B, int H, int W, int C, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(dh && a && da_slab && wsca && mean && dwsca && dbsca && t2 && t1 && wdw && dt1 && dwdw && dbdw && ws &&
+                  B > 0 && H > 0 && W > 0 && chunks > 0,
+              "nbp_sca_dw_bwd: bad args");
+  NBP_REQUIRE(dw_tiled_ok(C, dtype) && dtype != 0, "nbp_sca_dw_bwd: 16-bit, C a multiple of 16");
+  NBP_REQUIRE(C <= 1024 && B <= SCA_DW_BMAX, "nbp_sca_dw_bwd: C <= 1024, B <= %d", SCA_DW_BMAX);
+  DwTileP q{};
+  q.da_slab = da_slab; q.wsca = wsca; q.mean = mean; q.dwsca = dwsca; q.dbsca = dbsca; q.chunks = chunks;
+  return launch_dw_tiled(nullptr, dh, a, nullptr, t2, t1, wdw, nullptr, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s, &q);
+}
 
 
 }  // extern "C"

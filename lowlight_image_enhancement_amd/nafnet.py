@@ -122,6 +122,9 @@ class NAFNet(nn.Module):
         # backward at those levels: a block's conv1 input gradient + norm1 backward deferred into the preceding block's
         # row-stationary launch (nbp_ffn_rows_bwd with dt1: its dx made in LDS as that block's dout; NBP_FFN_PRE=0 off)
         self.ffn_rows_pre = __import__("os").environ.get("NBP_FFN_PRE", "1") != "0"
+        # levels with the stored tape: the SCA backward (ds, the SCA weight gradients) inside the fused depthwise
+        # backward (nbp_sca_dw_bwd) instead of its own launch before it (NBP_SCA_FOLD=0: two launches)
+        self.sca_fold = __import__("os").environ.get("NBP_SCA_FOLD", "1") != "0"
         # level 0: conv1's weight / bias gradients folded into the conv1 dgrad + norm1 backward pass (nbp_dgrad_ln_bwd_wg:
         # n1 rebuilt from x and the LN statistics, dt1 already in registers; False: a separate nbp_wgrad_f32 launch)
         self.ln_wg = True
@@ -861,10 +864,13 @@ class NAFNet(nn.Module):
         dev = dout.device
         E = lambda *s: torch.empty(*s, device=dev, dtype=self.adt)  # noqa: E731
         F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
-        # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch
-        ds = F(B, c)
-        call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,
-             self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
+        # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch (or inside the
+        # depthwise backward below)
+        sca_fold = (self.sca_fold and dt != 0 and S["t1"] is not None and c % 16 == 0 and c <= 1024 and B <= 256)
+        if not sca_fold:
+            ds = F(B, c)
+            call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,
+                 self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), B, c)
         # SimpleGate + depthwise conv2 (fused when the channel slicing allows: dt2 stays in LDS)
         dt1 = E(M, 2 * c)
         if S["t1"] is None:  # levels 0 / 1 tile path: t1 / t2 rebuilt from n1 on chip (nbp_c1dw_bwd_tile)
@@ -877,7 +883,10 @@ class NAFNet(nn.Module):
             ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
             dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
                        self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        if S["t1"] is not None and c % (16 if dt != 0 else 8) == 0:
+        if sca_fold:
+            call("sca_dw_bwd", dh, S["a"], da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"],
+                 self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), S["t2"], *dw_args)
+        elif S["t1"] is not None and c % (16 if dt != 0 else 8) == 0:
             call("sca_sg_dw_bwd", dh, S["a"], ds, S["t2"], *dw_args)
         elif S["t1"] is not None:
             dt2 = E(M, 2 * c)
