@@ -90,6 +90,7 @@ ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skin
 # names of kernel_stats.csv (exactly one instance per regex and dtype: tests/test_bench_launch.py checks the committed
 # record).
 INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_bwd_L1",
+             "c1dw_bwd_tile<T,32,sca>": "c1dw_bwd_sca_L0", "c1dw_bwd_tile<T,64,sca>": "c1dw_bwd_sca_L1",
              "dw_bwd_tiled<T,true,32>": "dw_bwd_32", "dw_bwd_tiled<T,true,16>": "dw_bwd_16",
              "dw_bwd_tiled<T,true,32,sca>": "dw_bwd_sca_32", "dw_bwd_tiled<T,true,16,sca>": "dw_bwd_sca_16",
              "wgrad_bf16_wide_group<3,512,2>": "wgrad_group_512", "wgrad_bf16_wide_group<3,768,4>": "wgrad_group_768",
@@ -100,7 +101,10 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
              "ffn_rows_bwd<256,pre>": "ffn_rows_bwd_pre_256", "ffn_rows_bwd<128,pre>": "ffn_rows_bwd_pre_128"}
 SINGLE_KERNEL = tuple(INSTANCES.values())
 ROCPROF_KERNELS.update({
-    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32ELi\d+ELb[01]EE"], "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64ELi\d+ELb[01]EE"],
+    "c1dw_bwd_L0": [r"c1dw_bwd_tileI{T}Li32ELi\d+ELb[01]E(Lb0E)?E"],
+    "c1dw_bwd_L1": [r"c1dw_bwd_tileI{T}Li64ELi\d+ELb[01]E(Lb0E)?E"],
+    "c1dw_bwd_sca_L0": [r"c1dw_bwd_tileI{T}Li32ELi\d+ELb[01]ELb1EE"],
+    "c1dw_bwd_sca_L1": [r"c1dw_bwd_tileI{T}Li64ELi\d+ELb[01]ELb1EE"],
     "dw_bwd_32": [r"dw_bwd_tiledI{T}Lb1ELi32E(Lb0E)?E"], "dw_bwd_16": [r"dw_bwd_tiledI{T}Lb1ELi16E(Lb0E)?E"],
     "dw_bwd_sca_32": [r"dw_bwd_tiledI{T}Lb1ELi32ELb1EE"], "dw_bwd_sca_16": [r"dw_bwd_tiledI{T}Lb1ELi16ELb1EE"],
     "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
@@ -130,6 +134,9 @@ UNIT_DEF = {
     "c1dw_bwd_L0": "per pixel: dh C + n1 C read, dt1 2C written = 4*C*s bytes (s = storage bytes; t1 / t2 rebuilt on "
                    "chip, never read), x B*H*W pixels of the launch (level 0: C 32 at 256^2), + the conv1 weight",
     "c1dw_bwd_L1": "as c1dw_bwd_L0 at level 1 (C 64 at 128^2)",
+    "c1dw_bwd_sca_L0": "as c1dw_bwd_L0, + the SCA backward folded in: the channel-dot slab (B x chunks x C) and W_sca "
+                       "(C^2) read, dW_sca (C^2) written, fp32",
+    "c1dw_bwd_sca_L1": "as c1dw_bwd_sca_L0 at level 1 (C 64 at 128^2)",
     "ffn_rows_512": "per pixel: g C + x C read, y + n2 + t4 (2C) + g2 + out (+ the next n1) written = 8-9 C s bytes, "
                     "+ the three weights (4 C^2 s) once per launch (the middle level: C 512 at 16^2)",
     "ffn_rows_256": "as ffn_rows_512 at C 256 (32^2)", "ffn_rows_128": "as ffn_rows_512 at C 128 (64^2)",
@@ -242,6 +249,14 @@ def cost_c1dw_fwd_tile(a):  # (n1,w1,b1,wdw,bdw,t1,t2,g,pool,B,h,w,c,dt): n1 C i
     return 2.0 * M * 2 * c * c + 2.0 * M * 2 * c * 9, by
 
 
+def cost_sca_c1dw_bwd_tile(a):  # (dh,a,da_slab,chunks,wsca,mean,dwsca,dbsca,n1,w1,b1,wdw,bdw,dt1,dwdw,dbdw,ws,B,h,w,c,
+    # dt): cost_c1dw_bwd_tile + the folded SCA backward (the channel-dot slab and W_sca read, dW_sca written, fp32)
+    B, c = a[17], a[20]
+    M = B * a[18] * a[19]
+    return (2.0 * M * 2 * c * c + 3 * 2.0 * M * 2 * c * 9 + 4.0 * B * c * c,
+            (4 * M * c + 2 * c * c) * _e(a[21]) + 4 * (B * a[3] * c + 2 * c * c))
+
+
 def cost_c1dw_bwd_tile(a):  # (dh,a,ds,n1,w1,b1,wdw,bdw,dt1,dwdw,dbdw,ws,B,h,w,c,dt): dh C + n1 C in, dt1 2C out
     M, c = a[12] * a[13] * a[14], a[15]
     return 2.0 * M * 2 * c * c + 3 * 2.0 * M * 2 * c * 9, (4 * M * c + 2 * c * c) * _e(a[16])
@@ -319,6 +334,7 @@ ENTRIES = {"gemm_bf16": rec_plain("gemm16", cost_gemm16), "gemm_res_ln": rec_pla
            "dgrad_ln_bwd_wg": rec_plain("gemm16", cost_dgrad_ln_wg), "c1_dw_sg_pool": rec_plain("c1dw", cost_c1dw),
            "c1dw_fwd_tile": rec_plain("c1dw_tile_fwd", cost_c1dw_fwd_tile),
            "c1dw_bwd_tile": rec_plain("c1dw_tile_bwd", cost_c1dw_bwd_tile),
+           "sca_c1dw_bwd_tile": rec_plain("c1dw_tile_bwd", cost_sca_c1dw_bwd_tile),
            "ffn_rows_fwd": rec_plain("ffn_rows", cost_ffn_rows), "ffn_rows_bwd": rec_plain("ffn_rows", cost_ffn_rows_bwd)}
 
 

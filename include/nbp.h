@@ -301,6 +301,13 @@ size_t nbp_c1dw_bwd_workspace_floats(int B, int H, int W, int C);
 int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
                       const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
                       int W, int C, int dtype, nbp_stream_t s);
+/* nbp_c1dw_bwd_tile with the SCA backward (nbp_sca_bwd_fused) folded in, as nbp_sca_dw_bwd does for the stored-tape
+ * levels: ds of each workgroup's 32 gate channels from the channel-dot partials (da_slab [B][chunks][C]) first, rows of
+ * dwsca / dbsca spread over the workgroups.  B <= 256; the default tile variant (NBP_C1DW_BWD_TH / _BAL unset). */
+int nbp_sca_c1dw_bwd_tile(const void* dh, const float* a, const float* da_slab, int chunks, const float* wsca,
+                          const float* mean, float* dwsca, float* dbsca, const void* n1, const void* w1, const float* b1,
+                          const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B,
+                          int H, int W, int C, int dtype, nbp_stream_t s);
 /* SCA 1x1 conv on the pooled vector (:39-41): mean[B][C], a[B][C] = W mean + b. */
 int nbp_sca_fwd(const float* pool_slab, int chunks, const float* wsca, const float* bsca, float* mean, float* a, int B,
                 int HW, int C, nbp_stream_t s);

@@ -22,6 +22,7 @@
 // rounded t2 with dg rounded once, dt1 taps 0..8 from zero.  The pool and the depthwise weight gradients are per-tile
 // partial sums in an order of their own (equal to the two-launch values up to fp32 summation order).
 #include "rowring.h"
+#include "sca_bwd.h"
 
 namespace nbp {
 namespace {
@@ -48,6 +49,13 @@ struct C1TileP {
   float* slab_b;      // [B * tiles][2C]    out: per-tile depthwise bias-gradient partials
   int B, H, W, tiles_x, tiles;
   float inv_hw;
+  // backward with the SCA backward folded in (nbp_sca_c1dw_bwd_tile; ds above unused)
+  const float* da_slab;  // [B][chunks][C]
+  const float* wsca;     // [C][C]
+  const float* mean;     // [B][C]
+  float* dwsca;          // [C][C] out
+  float* dbsca;          // [C] out
+  int chunks;
 };
 
 // the slice's conv1 weight rows (A operand: n = t * 32 + r, t 0 gate rows slice * 32 + r, 1 partner rows C + ...) in
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_fwd_tile(C1TileP p) {
 // BAL: the t1 rebuild spread over all four waves (wave w: pixel chunk w / 2, channel half w % 2 -- one 32 x 32 MFMA
 // chain and a 16-value epilogue each) instead of waves 0 / 1 doing both halves of one chunk each (two chains, 32
 // values) while waves 2 / 3 wait at the step's barrier
-template <typename T, int C, int TH, bool BAL>
+template <typename T, int C, int TH, bool BAL, bool SCA = false>
 __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   constexpr int TW = 32, PXT = 2, LT = TW + 4, LD = TW + 2, KS = C / 16, NSL = C / 32;
   constexpr int ROWF = LT * 64;          // floats per t1 ring row
@@ -285,6 +293,11 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   const int H = p.H, W = p.W;
   const long img = (long)b * H * W, M = (long)p.B * H * W;
   const __amdgpu_buffer_rsrc_t rn = rsrc(p.n1, M * C * 2), rh = rsrc(p.dh, M * C * 2), ro = rsrc(p.dt1, M * C * 4);
+  // ---- SCA: ds of the slice's 32 gate channels from the channel-dot partials (sca_bwd.h), first, while nothing else
+  // is live; scratch in the dt2 ring (first written after step 0's barrier): part | da | GEMV partials | ds
+  [[maybe_unused]] const ScaBwdP sq{p.da_slab, p.wsca, p.mean, p.dwsca, p.dbsca, p.chunks, p.B, C};
+  static_assert(!SCA || 3072 + 32 <= 4 * ROWD, "SCA scratch");
+  if constexpr (SCA) sca_ds_slice<256, 32>(sq, b, slice * 32, dt2r, dt2r + 1024, dt2r + 2048, dt2r + 3072);
   // ---- the slice's conv1 weight rows (n = t * 32 + rr) and bias into LDS; chunk c of row n at c ^ key(n)
   {
     const T* w1 = reinterpret_cast<const T*>(p.w1);
@@ -317,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
   DwQuad dw;
   dw.load(p.wdw, p.bdw, ch);
   const float4 ak = ld4(p.a + (long)b * C + gch);
-  const float4 sk = ld4(p.ds + (long)b * C + gch) * f4(p.inv_hw);
+  const float4 sk = (SCA ? ld4(dt2r + 3072 + 4 * (lane & 7)) : ld4(p.ds + (long)b * C + gch)) * f4(p.inv_hw);
   auto dh_off = [&](int yy, int gx, bool lane_has) {
     return lane_has && yy >= 0 && yy < H && gx >= 0 && gx < W ? (int)((img + (long)yy * W + gx) * (2 * C)) + 2 * gch : OOB;
   };
@@ -598,6 +611,7 @@ __global__ __launch_bounds__(256, 2) void c1dw_bwd_tile(C1TileP p) {
     if (e < 36) p.slab_w[(row * 2 * C + c4 + (e & 3)) * 9 + (e >> 2)] = s;
     else p.slab_b[row * 2 * C + c4 + (e - 36)] = s;
   }
+  if constexpr (SCA) sca_dw_rows<256>(sq, dt2r, dt2r + SCA_DW_BMAX);  // (the dt2 ring is dead; its first barrier)
 }
 
 }  // namespace
@@ -684,10 +698,13 @@ size_t nbp_c1dw_bwd_workspace_floats(int B, int H, int W, int C) {
   return (size_t)B * cdiv(H, bwd_th(C)) * cdiv(W, 32) * 2 * C * 10;
 }
 
-int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
-                      const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
-                      int W, int C, int dtype, nbp_stream_t s) {
-  NBP_REQUIRE(dh && a && ds && n1 && w1 && b1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0,
+}  // extern "C"
+
+namespace {
+int c1dw_bwd_launch(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
+                    const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
+                    int W, int C, int dtype, nbp_stream_t s, const ScaBwdP* sca) {
+  NBP_REQUIRE(dh && a && (ds || sca) && n1 && w1 && b1 && wdw && bdw && dt1 && dwdw && dbdw && ws && B > 0,
               "nbp_c1dw_bwd_tile: null pointer");
   NBP_REQUIRE(nbp_c1dw_tile_supported(B, H, W, C, dtype),
               "nbp_c1dw_bwd_tile: unsupported shape (B %d H %d W %d C %d dtype %d; B*H*W*2C*2 bytes must not exceed "
@@ -697,15 +714,24 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
   const int th = bwd_th(C);
   p.B = B; p.H = H; p.W = W; p.tiles_x = cdiv(W, 32); p.tiles = cdiv(H, th) * p.tiles_x;
   p.inv_hw = 1.f / (float)((long)H * W);
+  if (sca) {
+    p.da_slab = sca->da_slab; p.wsca = sca->wsca; p.mean = sca->mean; p.dwsca = sca->dwsca; p.dbsca = sca->dbsca;
+    p.chunks = sca->chunks;
+  }
   const long nrow = (long)B * p.tiles;
   p.slab_w = ws;
   p.slab_b = ws + nrow * 2 * C * 9;
   const long nblk = nrow * (C / 32);
   NBP_REQUIRE(nblk < (1L << 31), "nbp_c1dw_bwd_tile: grid too large");
+  const bool bal = bwd_bal(C);
+  // the SCA fold is instantiated for the default variants (TH 32; the balanced rebuild at C 32 only)
+  NBP_REQUIRE(!sca || (th == 32 && bal == (C == 32)),
+              "nbp_sca_c1dw_bwd_tile: the SCA fold needs the default tile variant (NBP_C1DW_BWD_TH / _BAL unset)");
   lt_begin(S(s));
   NBP_DISPATCH_H(dtype, {
-    const bool bal = bwd_bal(C);
-    if (C == 32 && th == 64 && bal) c1dw_bwd_tile<H, 32, 64, true><<<nblk, 256, 0, S(s)>>>(p);
+    if (sca && C == 32) c1dw_bwd_tile<H, 32, 32, true, true><<<nblk, 256, 0, S(s)>>>(p);
+    else if (sca) c1dw_bwd_tile<H, 64, 32, false, true><<<nblk, 256, 0, S(s)>>>(p);
+    else if (C == 32 && th == 64 && bal) c1dw_bwd_tile<H, 32, 64, true><<<nblk, 256, 0, S(s)>>>(p);
     else if (C == 32 && th == 64) c1dw_bwd_tile<H, 32, 64, false><<<nblk, 256, 0, S(s)>>>(p);
     else if (C == 32 && th == 32 && bal) c1dw_bwd_tile<H, 32, 32, true><<<nblk, 256, 0, S(s)>>>(p);
     else if (C == 32 && th == 32) c1dw_bwd_tile<H, 32, 32, false><<<nblk, 256, 0, S(s)>>>(p);
@@ -714,16 +740,39 @@ int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const voi
     else if (th == 32) c1dw_bwd_tile<H, 64, 32, false><<<nblk, 256, 0, S(s)>>>(p);
     else c1dw_bwd_tile<H, 64, 16, false><<<nblk, 256, 0, S(s)>>>(p);
   });
-  {  // per-launch record (nbp_launch_timing): dh C + n1 C in, dt1 2C out, the conv1 weight slice per slice
+  {  // per-launch record (nbp_launch_timing): dh C + n1 C in, dt1 2C out, the conv1 weight slice per slice (+ SCA:
+     // the channel-dot slab and W_sca read, dW_sca written)
     const double M = (double)B * H * W;
-    lt_end(S(s), C == 32 ? "c1dw_bwd_tile<T,32>" : "c1dw_bwd_tile<T,64>",
-           2.0 * M * 2 * C * C + 3 * 2.0 * M * 2 * C * 9, (4.0 * M * C + 2.0 * C * C) * 2);
+    const char* nm = sca ? (C == 32 ? "c1dw_bwd_tile<T,32,sca>" : "c1dw_bwd_tile<T,64,sca>")
+                         : (C == 32 ? "c1dw_bwd_tile<T,32>" : "c1dw_bwd_tile<T,64>");
+    const double sb = sca ? 4.0 * ((double)B * sca->chunks * C + 2.0 * C * C) : 0.0;
+    lt_end(S(s), nm, 2.0 * M * 2 * C * C + 3 * 2.0 * M * 2 * C * 9 + (sca ? 4.0 * B * C * C : 0.0),
+           (4.0 * M * C + 2.0 * C * C) * 2 + sb);
   }
   int rc = check_launch("c1dw_bwd_tile");
   if (rc) return rc;
   rc = nbp_reduce_slab(p.slab_w, (int)nrow, 2L * C * 9, dwdw, s);
   if (rc) return rc;
   return nbp_reduce_slab(p.slab_b, (int)nrow, 2L * C, dbdw, s);
+}
+}  // namespace
+
+extern "C" {
+
+int nbp_c1dw_bwd_tile(const void* dh, const float* a, const float* ds, const void* n1, const void* w1, const float* b1,
+                      const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B, int H,
+                      int W, int C, int dtype, nbp_stream_t s) {
+  return c1dw_bwd_launch(dh, a, ds, n1, w1, b1, wdw, bdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s, nullptr);
+}
+
+int nbp_sca_c1dw_bwd_tile(const void* dh, const float* a, const float* da_slab, int chunks, const float* wsca,
+                          const float* mean, float* dwsca, float* dbsca, const void* n1, const void* w1, const float* b1,
+                          const float* wdw, const float* bdw, void* dt1, float* dwdw, float* dbdw, float* ws, int B,
+                          int H, int W, int C, int dtype, nbp_stream_t s) {
+  NBP_REQUIRE(da_slab && wsca && mean && dwsca && dbsca && chunks > 0, "nbp_sca_c1dw_bwd_tile: null pointer");
+  NBP_REQUIRE(B <= SCA_DW_BMAX, "nbp_sca_c1dw_bwd_tile: B <= %d", SCA_DW_BMAX);
+  const ScaBwdP q{da_slab, wsca, mean, dwsca, dbsca, chunks, B, C};
+  return c1dw_bwd_launch(dh, a, nullptr, n1, w1, b1, wdw, bdw, dt1, dwdw, dbdw, ws, B, H, W, C, dtype, s, &q);
 }
 
 }  // extern "C"

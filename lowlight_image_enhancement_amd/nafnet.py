@@ -866,7 +866,10 @@ class NAFNet(nn.Module):
         F = lambda *s: self._ws(math.prod(s), dev)  # noqa: E731  (slabs live until the stage's flush)
         # ds = da . W_sca and the SCA weight gradients dW = da^T mean, db = colsum(da) in one launch (or inside the
         # depthwise backward below)
-        sca_fold = (self.sca_fold and dt != 0 and S["t1"] is not None and c % 16 == 0 and c <= 1024 and B <= 256)
+        env = __import__("os").environ
+        sca_fold = self.sca_fold and dt != 0 and c <= 1024 and B <= 256 and (
+            (S["t1"] is not None and c % 16 == 0)  # nbp_sca_dw_bwd
+            or (S["t1"] is None and not env.get("NBP_C1DW_BWD_TH") and not env.get("NBP_C1DW_BWD_BAL")))  # the tile
         if not sca_fold:
             ds = F(B, c)
             call("sca_bwd_fused", da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"], ds,
@@ -875,15 +878,19 @@ class NAFNet(nn.Module):
         dt1 = E(M, 2 * c)
         if S["t1"] is None:  # levels 0 / 1 tile path: t1 / t2 rebuilt from n1 on chip (nbp_c1dw_bwd_tile)
             ws = F(query("c1dw_bwd_workspace_floats", B, h, w, c))
-            call("c1dw_bwd_tile", dh, S["a"], ds, S["n1"], self._slice(Wt[1], pre + "conv1.weight"),
-                 self._slice(P, pre + "conv1.bias"), self._slice(P, pre + "conv2.weight"),
-                 self._slice(P, pre + "conv2.bias"), dt1, self._slice(dflat, pre + "conv2.weight"),
-                 self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
+            tail = (S["n1"], self._slice(Wt[1], pre + "conv1.weight"), self._slice(P, pre + "conv1.bias"),
+                    self._slice(P, pre + "conv2.weight"), self._slice(P, pre + "conv2.bias"), dt1,
+                    self._slice(dflat, pre + "conv2.weight"), self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
+            if sca_fold:
+                call("sca_c1dw_bwd_tile", dh, S["a"], da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"],
+                     self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), *tail)
+            else:
+                call("c1dw_bwd_tile", dh, S["a"], ds, *tail)
         else:
             ws = F(query("dw_bwd_workspace_floats", B, h, w, c))
             dw_args = (S["t1"], self._slice(P, pre + "conv2.weight"), dt1, self._slice(dflat, pre + "conv2.weight"),
                        self._slice(dflat, pre + "conv2.bias"), ws, B, h, w, c, dt)
-        if sca_fold:
+        if sca_fold and S["t1"] is not None:
             call("sca_dw_bwd", dh, S["a"], da_slab, chunks, self._slice(P, pre + "sca.1.weight"), S["mean"],
                  self._slice(dflat, pre + "sca.1.weight"), self._slice(dflat, pre + "sca.1.bias"), S["t2"], *dw_args)
         elif S["t1"] is not None and c % (16 if dt != 0 else 8) == 0:

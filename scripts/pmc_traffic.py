@@ -28,8 +28,10 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            "dw_fwd": ("dw_sg_pool_tiled",), "c1dw": ("c1_dw_sg_pool_img",), "ln_fwd": ("ln_fwd_nhwc",),
            "c1dw_tile_fwd": ("c1dw_fwd_tile",), "c1dw_tile_bwd": ("c1dw_bwd_tile",),
            # bench.py's one-instance classes (INSTANCES / ROCPROF_KERNELS there)
-           "c1dw_bwd_L0": (re.compile(r"c1dw_bwd_tileI\w+?Li32ELi\d+ELb[01]EE"),),
-           "c1dw_bwd_L1": (re.compile(r"c1dw_bwd_tileI\w+?Li64ELi\d+ELb[01]EE"),),
+           "c1dw_bwd_L0": (re.compile(r"c1dw_bwd_tileI\w+?Li32ELi\d+ELb[01]E(Lb0E)?E"),),
+           "c1dw_bwd_L1": (re.compile(r"c1dw_bwd_tileI\w+?Li64ELi\d+ELb[01]E(Lb0E)?E"),),
+           "c1dw_bwd_sca_L0": (re.compile(r"c1dw_bwd_tileI\w+?Li32ELi\d+ELb[01]ELb1EE"),),
+           "c1dw_bwd_sca_L1": (re.compile(r"c1dw_bwd_tileI\w+?Li64ELi\d+ELb[01]ELb1EE"),),
            "dw_bwd_16": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi16E(Lb0E)?E"),),
            "wgrad_group_512": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi512ELi2EE"),),
            "wgrad_group_768": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi768ELi4EE"),),

@@ -83,3 +83,36 @@ def test_sca_fold_random_within_rounding(dev, dt, B, H, W, C):
     for k in ("dwdw", "dbdw"):
         r = ref[k]
         assert (got[k] - r).abs().max().item() <= 1e-2 * r.abs().max().item(), k
+
+
+def _run_tile(dev, dt, B, H, W, C, o, chunks, fold):
+    from lowlight_image_enhancement_amd._lib import call, query
+    M = B * H * W
+    dt1 = torch.full((M, 2 * C), float("nan"), device=dev, dtype=DT[dt])
+    dwdw, dbdw = torch.zeros(2 * C * 9, device=dev), torch.zeros(2 * C, device=dev)
+    dws, dbs = torch.full((C * C,), float("nan"), device=dev), torch.full((C,), float("nan"), device=dev)
+    ws = torch.empty(query("c1dw_bwd_workspace_floats", B, H, W, C), device=dev)
+    tail = (o["n1"], o["w1"], o["b1"], o["wdw"], o["bdw"], dt1, dwdw, dbdw, ws, B, H, W, C, dt)
+    if fold:
+        call("sca_c1dw_bwd_tile", o["dh"], o["a"], o["da"], chunks, o["wsca"], o["mean"], dws, dbs, *tail)
+    else:
+        ds = torch.empty(B, C, device=dev)
+        call("sca_bwd_fused", o["da"], chunks, o["wsca"], o["mean"], ds, dws, dbs, B, C)
+        call("c1dw_bwd_tile", o["dh"], o["a"], ds, *tail)
+    torch.cuda.synchronize()
+    return dict(dt1=dt1, dwdw=dwdw, dbdw=dbdw, dws=dws, dbs=dbs)
+
+
+@pytest.mark.parametrize("dt", [1, 2])
+@pytest.mark.parametrize("B,H,W,C", [(2, 64, 64, 32), (3, 40, 72, 32), (2, 64, 64, 64), (16, 32, 32, 64)])
+def test_sca_fold_tile_exact_bitwise(dev, dt, B, H, W, C):
+    """the same fold in the level-0 / 1 tile backward (nbp_sca_c1dw_bwd_tile vs nbp_sca_bwd_fused +
+    nbp_c1dw_bwd_tile): exact dyadic SCA inputs, everything bitwise"""
+    o, chunks = _case(dev, dt, B, H, W, C, True, 5 + C + H)
+    g = torch.Generator(device=dev).manual_seed(77 + C)
+    R = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
+    o.update(n1=R(B * H * W, C).to(DT[dt]), w1=(R(2 * C, C) / C ** 0.5).to(DT[dt]), b1=R(2 * C) * 0.1,
+             bdw=R(2 * C) * 0.1)
+    got, ref = _run_tile(dev, dt, B, H, W, C, o, chunks, True), _run_tile(dev, dt, B, H, W, C, o, chunks, False)
+    for k in ("dt1", "dws", "dbs", "dwdw", "dbdw"):
+        assert torch.equal(_bits(got[k]), _bits(ref[k])), k
