@@ -100,18 +100,28 @@ __device__ void sca_dw_rows(const ScaBwdP& p, float* part, float* sdo) {
       sdo[bb] = t;
     }
     __syncthreads();
-    for (int i = tid; i < C; i += NT) {
-      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (8 mean loads in flight; fixed-order combine)
-      int bb = 0;
-      for (; bb + 7 < B; bb += 8) {
-        float m[8];
+    // 4 columns per thread at once, 16 images each: 64 mean loads in flight (a column at a time left 2 x 4 dependent
+    // round trips at the end of every workgroup); the sum over b ascending
+    for (int i0 = tid; i0 < C; i0 += 4 * NT) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int b0 = 0; b0 < B; b0 += 16) {
+        float m[4][16];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) m[q] = p.mean[(long)(bb + q) * C + i];
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) a[q] = fmaf(sdo[bb + q], m[q], a[q]);
+          for (int q = 0; q < 16; ++q) {
+            const int i = i0 + u * NT;
+            m[u][q] = i < C && b0 + q < B ? p.mean[(long)(b0 + q) * C + i] : 0.f;
+          }
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          if (b0 + q < B)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = fmaf(sdo[b0 + q], m[u][q], acc[u]);
       }
-      for (int q = 0; bb < B; ++bb, ++q) a[q] = fmaf(sdo[bb], p.mean[(long)bb * C + i], a[q]);
-      p.dwsca[(long)o * C + i] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + u * NT < C) p.dwsca[(long)o * C + i0 + u * NT] = acc[u];
     }
     if (tid == 0) {
       float t = 0.f;
