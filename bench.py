@@ -81,7 +81,7 @@ HBM_PEAK_GBPS = 8000.0
 ESIZE = {"fp32": 4, "bf16": 2, "fp16": 2}
 ROCPROF_KERNELS = {"gemm16": ["gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kernel"], "gemm_f32": ["gemm_f32_kernel"],
                    "wgrad_narrow": ["wgrad_bf16_kernel", "wgrad_f32_kernel", "wgrad_narrow_full"], "wgrad_group": ["wgrad_bf16_wide_group"],
-                   "reduce": ["reduce_multi_kernel", "layer_scale_grad_kernel"],
+                   "reduce": ["reduce_multi_kernel", "reduce_table_kernel", "layer_scale_grad_kernel"],
                    "dw_bwd": ["dw_bwd_tiled"], "dw_fwd": ["dw_sg_pool_tiled"], "c1dw": ["c1_dw_sg_pool_img"],
                    "c1dw_tile_fwd": ["c1dw_fwd_tile"], "c1dw_tile_bwd": ["c1dw_bwd_tile"]}
 # ONE-kernel classes (one template instance each), timed per launch inside the library (nbp_launch_timing: events
@@ -94,7 +94,8 @@ INSTANCES = {"c1dw_bwd_tile<T,32>": "c1dw_bwd_L0", "c1dw_bwd_tile<T,64>": "c1dw_
              "dw_bwd_tiled<T,true,32>": "dw_bwd_32", "dw_bwd_tiled<T,true,16>": "dw_bwd_16",
              "dw_bwd_tiled<T,true,32,sca>": "dw_bwd_sca_32", "dw_bwd_tiled<T,true,16,sca>": "dw_bwd_sca_16",
              "wgrad_bf16_wide_group<3,512,2>": "wgrad_group_512", "wgrad_bf16_wide_group<3,768,4>": "wgrad_group_768",
-             "reduce_multi_kernel": "reduce_multi", "layer_scale_grad_kernel": "layer_scale_grad",
+             "reduce_multi_kernel": "reduce_multi", "reduce_table_kernel": "reduce_table",
+             "layer_scale_grad_kernel": "layer_scale_grad",
              "ffn_rows_fwd<512>": "ffn_rows_512", "ffn_rows_fwd<256>": "ffn_rows_256", "ffn_rows_fwd<128>": "ffn_rows_128",
              "ffn_rows_bwd<512>": "ffn_rows_bwd_512", "ffn_rows_bwd<256>": "ffn_rows_bwd_256",
              "ffn_rows_bwd<128>": "ffn_rows_bwd_128", "ffn_rows_bwd<512,pre>": "ffn_rows_bwd_pre_512",
@@ -109,7 +110,8 @@ ROCPROF_KERNELS.update({
     "dw_bwd_sca_32": [r"dw_bwd_tiledI{T}Lb1ELi32ELb1EE"], "dw_bwd_sca_16": [r"dw_bwd_tiledI{T}Lb1ELi16ELb1EE"],
     "wgrad_group_512": [r"wgrad_bf16_wide_groupI{T}Li3ELi512ELi2EE"],
     "wgrad_group_768": [r"wgrad_bf16_wide_groupI{T}Li3ELi768ELi4EE"],
-    "reduce_multi": [r"reduce_multi_kernel"], "layer_scale_grad": [r"layer_scale_grad_kernel"],
+    "reduce_multi": [r"reduce_multi_kernel"], "reduce_table": [r"reduce_table_kernel"],
+    "layer_scale_grad": [r"layer_scale_grad_kernel"],
     "ffn_rows_512": [r"ffn_rows_fwdI{T}Li512EE"], "ffn_rows_256": [r"ffn_rows_fwdI{T}Li256EE"],
     "ffn_rows_128": [r"ffn_rows_fwdI{T}Li128EE"], "ffn_rows": ["ffn_rows_fwd", "ffn_rows_bwd"],
     "ffn_rows_bwd_512": [r"ffn_rows_bwdI{T}Li512ELb0EE"], "ffn_rows_bwd_256": [r"ffn_rows_bwdI{T}Li256ELb0EE"],
@@ -130,6 +132,8 @@ UNIT_DEF = {
                        "wgrad_group class's `slab_bytes_per_step`",
     "wgrad_group_768": "as wgrad_group_512, the 256-column-tile instance (the 16 x 16 level's plain problems, unsplit)",
     "reduce_multi": "per reduce_multi_kernel launch: the fp32 slabs read once + the reduced outputs written once",
+    "reduce_table": "per reduce_table_kernel launch (a whole flush from the device descriptor table): the fp32 slabs "
+                    "read once + the reduced outputs written once",
     "layer_scale_grad": "per layer_scale_grad_kernel launch: U, V, W, b read, dW, db, dscale written (fp32)",
     "c1dw_bwd_L0": "per pixel: dh C + n1 C read, dt1 2C written = 4*C*s bytes (s = storage bytes; t1 / t2 rebuilt on "
                    "chip, never read), x B*H*W pixels of the launch (level 0: C 32 at 256^2), + the conv1 weight",

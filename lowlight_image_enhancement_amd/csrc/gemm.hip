@@ -1213,10 +1213,7 @@ RDesc make_rdesc(const float* slab, int S, long L, float* out) {
 }
 long rdesc_blocks(const RDesc& d) { return cdiv(d.L, (long)(256 / d.ty) * d.vec); }
 
-__device__ void layer_scale_row(const RBatch& rb, int lb, float* red) {
-  int j = 0;
-  while (j + 1 < rb.nl && rb.l[j + 1].blk0 <= lb) ++j;
-  const LDesc& d = rb.l[j];
+__device__ void layer_scale_row_d(const LDesc& d, int lb, float* red) {
   const int row = lb - d.blk0, K = d.K, N = d.N;
   int txq = 1;
   while (txq * 4 < K) txq <<= 1;  // column lanes (4 columns each), a power of two <= 256 (K <= 1024)
@@ -1254,6 +1251,14 @@ __device__ void layer_scale_row(const RBatch& rb, int lb, float* red) {
   }
 }
 
+__device__ void layer_scale_row(const RBatch& rb, int lb, float* red) {
+  int j = 0;
+  while (j + 1 < rb.nl && rb.l[j + 1].blk0 <= lb) ++j;
+  layer_scale_row_d(rb.l[j], lb, red);
+}
+
+__device__ void reduce_desc_block(const RDesc& d, int bid, float* red);
+
 __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
   __shared__ float red[256 * 4];
   const int bid = blockIdx.x;
@@ -1263,7 +1268,44 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(RBatch rb) {
   }
   int k = 0;
   while (k + 1 < rb.n && rb.d[k + 1].blk0 <= bid) ++k;
-  const RDesc& d = rb.d[k];
+  reduce_desc_block(rb.d[k], bid, red);
+}
+
+// one flush as ONE launch: the descriptors in a device table (written by reduce_desc_write from by-value batches, so
+// a captured graph replays them), each block's found by binary search on blk0; the same per-descriptor code
+__global__ __launch_bounds__(256) void reduce_table_kernel(const RDesc* __restrict__ dd, int n, const LDesc* __restrict__ dl,
+                                                           int nl, int lblk0) {
+  __shared__ float red[256 * 4];
+  const int bid = blockIdx.x;
+  if (bid >= lblk0) {
+    const int lb = bid - lblk0;
+    int lo = 0, hi = nl - 1;  // the last descriptor with blk0 <= lb
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (dl[mid].blk0 <= lb) lo = mid;
+      else hi = mid - 1;
+    }
+    const LDesc d = dl[lo];
+    layer_scale_row_d(d, lb, red);
+    return;
+  }
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (dd[mid].blk0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const RDesc d = dd[lo];
+  reduce_desc_block(d, bid, red);
+}
+
+__global__ __launch_bounds__(64) void reduce_desc_write(RBatch rb, RDesc* __restrict__ dd, LDesc* __restrict__ dl) {
+  const int t = threadIdx.x;
+  if (t < rb.n) dd[t] = rb.d[t];
+  if (t < rb.nl) dl[t] = rb.l[t];
+}
+
+__device__ void reduce_desc_block(const RDesc& d, int bid, float* red) {
   const int TY = d.ty, TXQ = 256 / TY, VEC = d.vec;
   const int tx = threadIdx.x % TXQ, ty = threadIdx.x / TXQ;
   const long col = ((long)(bid - d.blk0) * TXQ + tx) * VEC;
@@ -1295,6 +1337,33 @@ thread_local double g_stats_wgrad[4];
 // [4] = fp32 slab bytes written at the group's M-splits, [5] = kernel launches
 thread_local double g_stats_group[6];
 
+// the flush's device descriptor table, per device: grown outside graph capture only, never freed (a captured graph
+// keeps addressing the table it was captured with); NBP_REDUCE_TABLE=0: the batched launches
+bool reduce_table(hipStream_t st, int nd, int nl, RDesc** dd, LDesc** dl) {
+  static const bool on = [] {
+    const char* e = getenv("NBP_REDUCE_TABLE");
+    return !e || atoi(e) != 0;
+  }();
+  struct Tab { void* p = nullptr; int cd = 0, cl = 0; };
+  static Tab tabs[64];
+  int dev = 0;
+  if (!on || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  Tab& t = tabs[dev];
+  if (t.cd < nd || t.cl < nl) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+    const int cd = nd > 4096 ? nd : 4096, cl = nl > 512 ? nl : 512;
+    void* q = nullptr;
+    if (hipMalloc(&q, (size_t)cd * sizeof(RDesc) + (size_t)cl * sizeof(LDesc)) != hipSuccess) return false;
+    t.p = q;  // (the previous table stays allocated)
+    t.cd = cd;
+    t.cl = cl;
+  }
+  *dd = reinterpret_cast<RDesc*>(t.p);
+  *dl = reinterpret_cast<LDesc*>(reinterpret_cast<char*>(t.p) + (size_t)t.cd * sizeof(RDesc));
+  return true;
+}
+
 void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vector<LDesc>& ls = {}) {
   static const bool log = getenv("NBP_REDUCE_LOG") != nullptr;  // diagnostic: the flush's descriptors to stderr
   if (log) {
@@ -1313,6 +1382,42 @@ void launch_multi(const std::vector<RDesc>& ds, hipStream_t st, const std::vecto
     g_stats_flush[0] += (double)(ds.size() + ls.size());
     g_stats_flush[1] += rd;
     g_stats_flush[2] += wr;
+  }
+  RDesc* dd = nullptr;
+  LDesc* dl = nullptr;
+  if ((ds.size() > (size_t)RB_MAX || ls.size() > (size_t)LB_MAX) &&
+      reduce_table(st, (int)ds.size(), (int)ls.size(), &dd, &dl)) {
+    // one launch: the descriptors written in by-value batches, blk0 over the whole flush
+    long blocks = 0;
+    int lblocks = 0;
+    double by = 0;
+    size_t i = 0, j = 0;
+    while (i < ds.size() || j < ls.size()) {
+      RBatch rb;
+      rb.n = rb.nl = 0;
+      const size_t i0 = i, j0 = j;
+      for (; i < ds.size() && rb.n < RB_MAX; ++i) {
+        RDesc d = ds[i];
+        d.blk0 = (int)blocks;
+        blocks += rdesc_blocks(d);
+        by += (double)d.S * d.L * 4 + (double)d.L * 4;
+        rb.d[rb.n++] = d;
+      }
+      for (; j < ls.size() && rb.nl < LB_MAX; ++j) {
+        LDesc d = ls[j];
+        d.blk0 = lblocks;
+        lblocks += d.N;
+        by += (double)d.SU * d.N * d.K * 4 + (double)d.SV * d.N * 4 + (double)d.N * (d.K + 2) * 4;
+        rb.l[rb.nl++] = d;
+      }
+      reduce_desc_write<<<1, 64, 0, st>>>(rb, dd + i0, dl + j0);
+    }
+    lt_begin(st);
+    reduce_table_kernel<<<(unsigned)(blocks + lblocks), 256, 0, st>>>(dd, (int)ds.size(), dl, (int)ls.size(),
+                                                                       (int)blocks);
+    lt_end(st, "reduce_table_kernel", 0.0, by);
+    g_stats_flush[3] += 1;
+    return;
   }
   size_t i = 0, j = 0;
   while (i < ds.size() || j < ls.size()) {

@@ -21,7 +21,7 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            # fp32 slab reductions (+ layer-scale post-ops) that fold their split-M partials: per KERNEL launch, the
            # unit bench.py's algorithmic bytes use for these classes
            "wgrad_narrow": ("wgrad_bf16_kernel", "wgrad_f32_kernel", "wgrad_narrow_full"), "wgrad_group": ("wgrad_bf16_wide",),
-           "reduce": ("reduce_multi_kernel", "layer_scale_grad_kernel"),
+           "reduce": ("reduce_multi_kernel", "reduce_table_kernel", "layer_scale_grad_kernel"),
            "dw_bwd": ("dw_bwd_tiled",), "dw_bwd_32": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi32E(Lb0E)?E"),),
            "dw_bwd_sca_32": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi32ELb1EE"),),
            "dw_bwd_sca_16": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi16ELb1EE"),),
@@ -35,7 +35,8 @@ CLASSES = {"gemm16": ("gemm_glds_kernel", "gemm_bf16_kernel", "gemm_skinny_kerne
            "dw_bwd_16": (re.compile(r"dw_bwd_tiledI\w+?Lb1ELi16E(Lb0E)?E"),),
            "wgrad_group_512": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi512ELi2EE"),),
            "wgrad_group_768": (re.compile(r"wgrad_bf16_wide_groupI\w+?Li3ELi768ELi4EE"),),
-           "reduce_multi": ("reduce_multi_kernel",), "layer_scale_grad": ("layer_scale_grad_kernel",),
+           "reduce_multi": ("reduce_multi_kernel",), "reduce_table": ("reduce_table_kernel",),
+           "layer_scale_grad": ("layer_scale_grad_kernel",),
            "ffn_rows": ("ffn_rows_fwd", "ffn_rows_bwd"),
            "ffn_rows_bwd_512": (re.compile(r"ffn_rows_bwdI\w+?Li512ELb0EE"),),
            "ffn_rows_bwd_256": (re.compile(r"ffn_rows_bwdI\w+?Li256ELb0EE"),),
